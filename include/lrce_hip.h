@@ -1,0 +1,188 @@
+/* lrce_hip.h — C ABI of the MI355X (gfx950) LRCE hot-path library (liblrce_hip.so).
+ *
+ * Plain pointers and sizes only: every tensor argument is a device pointer owned by the caller
+ * (PyTorch's caching allocator in the Python host layer), outputs are written in place, nothing
+ * is freed, and every entry point enqueues on the HIP stream passed as `stream` (hipStream_t,
+ * NULL = default stream) and returns immediately.  Return value 0 = success; otherwise a
+ * LRCE_E_* code, with a message available from lrce_last_error() (thread-local).
+ *
+ * dtypes: "bf16" = bfloat16 stored as uint16_t, "f32" = IEEE float.  All matrices are row-major
+ * with explicit leading dimensions (in elements).
+ *
+ * The reference (Sejong-VLI/VQA-LRCE-KBS-2023) is pure PyTorch and has no native boundary; each
+ * entry point below replaces the ATen kernels the reference's modules launch at the cited
+ * file:line (paths relative to the reference root).  SURVEY.md §2.1 lists them.
+ */
+#ifndef LRCE_HIP_H
+#define LRCE_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  LRCE_OK = 0,
+  LRCE_E_ARG = 1,     /* bad shape / pointer / flag combination */
+  LRCE_E_LAUNCH = 2,  /* hipGetLastError after launch */
+  LRCE_E_UNSUPPORTED = 3
+};
+
+/* ---------------------------------------------------------------- GEMM (MFMA bf16 -> f32 acc)
+ * C[b][m][n] (+)= epilogue( alpha * sum_k A(m,k) * B(n,k) )
+ *   A(m,k) = a_kmajor ? A[m*lda + k] : A[k*lda + m]      (a_f32: A is f32, rounded to bf16 on load)
+ *   B(n,k) = b_kmajor ? B[n*ldb + k] : B[k*ldb + n]      (bf16)
+ *   a_map (optional int32): gathers A rows — replaces m (a_kmajor) or k (!a_kmajor) by a_map[.]
+ *   c_map (optional int32): scatters output rows — row m is written to c_map[m] (also the row of
+ *                           the RESID / DGELU aux read).
+ * Replaces: nn.Linear forward/backward (addmm/mm) at video_swin_ori.py:46-57,150,152,318;
+ * fusionv3.py:154,160; the decoder/BERT linears; conv3d patch-embed as a K=96 GEMM (:458).
+ */
+enum {
+  LRCE_EPI_BIAS = 1,      /* + bias[n] (f32) */
+  LRCE_EPI_GELU = 2,      /* y = gelu_erf(y); with AUX_OUT the pre-activation is stored (bf16) */
+  LRCE_EPI_DGELU = 4,     /* y *= gelu_erf'(aux[row][n])  (aux bf16 pre-activation) */
+  LRCE_EPI_RESID = 8,     /* y += aux[row][n]  (aux f32) */
+  LRCE_EPI_OUT_F32 = 16,  /* C is f32 (else bf16) */
+  LRCE_EPI_ATOMIC = 32,   /* f32 atomicAdd into C (split-K / gradient accumulation) */
+  LRCE_EPI_ACCUM = 64,    /* C(f32) += y, non-atomic */
+  LRCE_EPI_AUX_OUT = 128, /* store pre-activation (bf16) into aux_out */
+  LRCE_EPI_OUT_BOTH = 256 /* also write a bf16 copy of y into aux_out (f32 C + bf16 shadow) */
+};
+
+typedef struct LrceGemmDesc {
+  const void* a;
+  const void* b;
+  void* c;
+  int64_t lda, ldb, ldc;
+  int64_t stride_a, stride_b, stride_c; /* batch strides (elements) */
+  int32_t m, n, k, batch;
+  int32_t a_kmajor, b_kmajor, a_f32;
+  int32_t flags;      /* LRCE_EPI_* */
+  int32_t split_k;    /* >1 requires LRCE_EPI_ATOMIC */
+  const float* bias;
+  const void* aux;
+  int64_t ld_aux;
+  void* aux_out;
+  int64_t ld_aux_out;
+  const int32_t* a_map;
+  const int32_t* c_map;
+  float alpha;
+  int32_t scale_cols; /* columns [0, scale_cols) are multiplied by scale_val after the bias */
+  float scale_val;
+  /* DropPath (video_swin_ori.py:243,299): per-sample branch scale.  Epilogue: y *= row_scale[m /
+   * rows_per_scale] before the RESID add.  A loader (f32 A only): every A element of logical row r
+   * (m if a_kmajor else k, before a_map) is multiplied by a_row_scale[r / a_rows_per_scale]. */
+  const float* row_scale;
+  int32_t rows_per_scale;
+  const float* a_row_scale;
+  int32_t a_rows_per_scale;
+} LrceGemmDesc;
+
+int lrce_gemm(const LrceGemmDesc* desc, void* stream);
+
+/* ---------------------------------------------------------------- LayerNorm
+ * Row r of the (rows x cols) LN input is the concatenation of nseg segments of cols/nseg
+ * channels, segment s read from source row in_map[r*nseg+s] of x (identity if in_map == NULL;
+ * a negative index reads zeros = padding).  Output row r goes to out_map[r] (identity if NULL).
+ * Saves per-row mean and rstd (f32) for the backward.
+ * Replaces: nn.LayerNorm at video_swin_ori.py:252,285,339,476-480,684; PatchMerging gather
+ * (:333-337, nseg=4); window_partition + torch.roll (:60-72,262) via in_map; embedding.py:22,62;
+ * fusionv3.py:48; BERT LayerNorms. */
+int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_map, int nseg,
+                       const float* w, const float* b, float eps,
+                       void* y, int y_f32, const int32_t* out_map,
+                       float* mean, float* rstd, int rows, int cols, void* stream);
+
+/* dy row r (read from dy_map[r] if given), x/mean/rstd as in forward.  dx for segment s is written
+ * to row in_map[r*nseg+s] of dx (f32): dx = LN_bwd + (dres ? dres[same row] : 0).  dw/db (f32,
+ * may be NULL) are accumulated with atomics. */
+int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map,
+                       const void* x, int x_f32, const int32_t* in_map, int nseg,
+                       const float* mean, const float* rstd, const float* w,
+                       float* dx, const float* dres, float* dw, float* db,
+                       int rows, int cols, void* stream);
+
+/* ---------------------------------------------------------------- Swin 3D window attention
+ * Replaces WindowAttention3D.forward video_swin_ori.py:164-186 (QK^T, relative-position bias,
+ * shift mask, softmax, PV) for windows of n <= 160 tokens and head_dim 32.
+ * qkv: bf16 [n_win*n][3C] window-ordered rows (q columns pre-scaled by head_dim^-0.5*log2(e)),
+ * out: bf16 [n_win*n][C], lse: f32 [n_win][nH][160] (log2 domain).
+ * bias tiles are built once per layer by lrce_wattn_bias_build from the f32 table
+ * (relative_position_bias_table) and the int64 relative_position_index (ld = index_ld), with the
+ * shift mask of each window pattern given as per-token region ids region[n_pat][n] (-100 between
+ * different regions, video_swin_ori.py:346-359); win_pat[w] selects the pattern of window w. */
+int64_t lrce_wattn_bias_elems(int n_pat, int nH);
+int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
+                          const int32_t* region, int n_pat, float* bias_fwd, float* bias_bwd, void* stream);
+int lrce_wattn_fwd(const uint16_t* qkv, const float* bias_fwd, const int32_t* win_pat,
+                   uint16_t* out, float* lse, int n_win, int n, int nH, void* stream);
+/* dqkv: bf16 [n_win*n][3C] (d/dq, d/dk, d/dv w.r.t. the UNSCALED q).  ds_scratch: bf16,
+ * lrce_wattn_ds_elems(n_win, nH) elements; table_grad (f32 [table_rows][nH]) is accumulated. */
+int64_t lrce_wattn_ds_elems(int n_win, int nH);
+int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                   const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv, uint16_t* ds_scratch,
+                   int n_win, int n, int nH, void* stream);
+int lrce_wattn_dbias(const uint16_t* ds_scratch, int n_win, int n, int nH, const int64_t* index, int index_ld,
+                     float* table_grad, void* stream);
+
+/* ---------------------------------------------------------------- small multi-head attention
+ * Generic masked SDPA for BERT self-attention (text.py:12-17, L<=64) and the fusion decoder's
+ * cross-attention (fusionv3.py:44-49 via nn.MultiheadAttention, Lq=1, Lk=183/191).
+ * q: [B][Lq] rows of ld_q, head h at column h*d; k,v likewise; key_mask: int32 [B][Lk] (1 keep, 0
+ * masked, NULL = all keep).  out bf16 [B][Lq][ld_o], lse f32 [B][H][Lq]. scale applied to q.k. */
+int lrce_mha_fwd(const uint16_t* q, int64_t ld_q, const uint16_t* k, const uint16_t* v, int64_t ld_kv,
+                 int64_t stride_kv_b, const int32_t* key_mask, uint16_t* out, int64_t ld_o, float* lse,
+                 int B, int H, int Lq, int Lk, int d, float scale, void* stream);
+int lrce_mha_bwd(const uint16_t* q, int64_t ld_q, const uint16_t* k, const uint16_t* v, int64_t ld_kv,
+                 int64_t stride_kv_b, const int32_t* key_mask, const uint16_t* out, int64_t ld_o,
+                 const uint16_t* dout, const float* lse, float* dq, int64_t ld_dq, float* dk, float* dv,
+                 int64_t ld_dkv, int64_t stride_dkv_b, int B, int H, int Lq, int Lk, int d, float scale,
+                 void* stream);
+
+/* ---------------------------------------------------------------- elementwise / data movement */
+/* Normalize (video.py:35) + zero-pad T to a multiple of 2 (video_swin_ori.py:472-473) + im2col of
+ * the (2,4,4) patches: clips f32 [B][S][T][3][H][W] -> patches bf16 [(B*S)*D'*H'*W'][96], rows
+ * ordered (b, s, d, h, w) (all B*S clips form one Swin batch, video.py:33-42), cols (c, kt, kh, kw). */
+int lrce_patch_im2col(const float* clips, uint16_t* patches, int B, int S, int T, int H, int W, void* stream);
+/* column sums: out[n] (+)= sum_m x[m][n] (x f32 or bf16, optional row map): bias gradients */
+int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, int m, int n, float* out, void* stream);
+/* f32 -> bf16 cast (n elements) */
+int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
+/* y = x * keep / (1-p) with keep ~ Bernoulli(1-p) from a counter hash (seed, offset); p=0 copies.
+ * Optional bf16 copy.  In place allowed. */
+int lrce_dropout(const float* x, float* y, uint16_t* y_bf16, int64_t n, float p, uint64_t seed, void* stream);
+int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t seed, void* stream);
+
+/* Fused optimizer step over the flat parameter buffer (agent_base.py:27-44,103-108).  Every tensor
+ * starts at a multiple of 1024 elements; chunk_tensor[c] is the tensor id of 1024-element chunk c.
+ * lrce_l2norm_multi: sumsq[t] = ||p_t||^2 (zeroed here).  lrce_adamw_step: torch.optim.AdamW update
+ * (decoupled weight decay, bias corrections bc1 = 1-beta1^t, bc2 = 1-beta2^t) on the gradient
+ * grad_scale * g + reg * p / ||p|| (the L2-regulariser term), tensor_lr[t] per tensor; also writes
+ * the bf16 shadow copy of p (p_bf16, optional) used by the next forward. */
+int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks, float* sumsq, int n_tensors, void* stream);
+int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
+                    const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
+                    float weight_decay, float grad_scale, float reg, float bc1, float bc2, void* stream);
+
+/* BERT embeddings before their LayerNorm (HF BertEmbeddings): out[r] = word[ids[r]] + pos[r % L] +
+ * type[types[r]] (f32 tables, int64 ids), and the scatter-add backward into the three tables. */
+int lrce_bert_embed_fwd(const int64_t* ids, const int64_t* types, const float* word, const float* pos, const float* typ,
+                        float* out, int rows, int L, int C, void* stream);
+int lrce_bert_embed_bwd(const float* dout, const int64_t* ids, const int64_t* types, float* dword, float* dpos, float* dtyp,
+                        int rows, int L, int C, void* stream);
+/* LRCE positional embeddings before their LayerNorm (embedding.py:47-63, 17-23). */
+int lrce_video_posembed_fwd(const float* x, const float* cls, const float* pos, const float* len, const float* clip, float* out,
+                            int B, int S, int Tg, int P, int C, void* stream);
+int lrce_video_posembed_bwd(const float* dout, float* dx, float* dcls, float* dpos, float* dlen, float* dclip, int B, int S,
+                            int Tg, int P, int C, void* stream);
+int lrce_text_posembed_fwd(const float* x, const float* cls, const float* pos, float* out, int B, int L, int C, void* stream);
+int lrce_text_posembed_bwd(const float* dout, float* dx, float* dcls, float* dpos, int B, int L, int C, void* stream);
+
+int lrce_version(void);
+const char* lrce_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,261 @@
+"""Op-level parity of the HIP kernels (through the C ABI) against plain PyTorch fp32 references of
+the same math.  GPU only."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import lrce_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.manual_seed(0)
+
+
+def K():
+    from lrce import kernels
+    return kernels
+
+
+def rel(a, b):
+    a = a.float(); b = b.float()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 384, 128), (300, 200, 96), (1000, 768, 1024), (17, 72, 200)])
+@pytest.mark.parametrize("a_km,b_km,a_f32", [(1, 1, 0), (1, 0, 0), (0, 0, 0), (1, 1, 1), (0, 0, 1), (0, 1, 0)])
+def test_gemm_layouts(M, N, Kd, a_km, b_km, a_f32):
+    k = K()
+    A = torch.randn(M, Kd, device=dev)
+    B = torch.randn(N, Kd, device=dev)
+    if not a_km and M % 8:
+        pytest.skip("M-major A needs M % 8 == 0")
+    if not b_km and N % 8:
+        pytest.skip("N-major B needs N % 8 == 0")
+    Ab = A if a_f32 else bf(A)
+    ref = bf(A).float() @ bf(B).float().t()
+    a_store = Ab.contiguous() if a_km else Ab.t().contiguous()
+    b_store = bf(B).contiguous() if b_km else bf(B).t().contiguous()
+    C = torch.empty(M, N, device=dev, dtype=torch.float32)
+    k.gemm(a_store, b_store, C, M, N, Kd, a_kmajor=bool(a_km), b_kmajor=bool(b_km), flags=16)
+    torch.cuda.synchronize()
+    assert rel(C, ref) < 2e-3
+
+
+def test_gemm_epilogues_and_maps():
+    k = K()
+    M, N, Kd = 520, 256, 160
+    x = torch.randn(M, Kd, device=dev)
+    w = torch.randn(N, Kd, device=dev) / math.sqrt(Kd)
+    b = torch.randn(N, device=dev)
+    xb, wb = bf(x), bf(w)
+    # GELU + pre-activation store
+    pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    y = k.linear(xb, wb, b, gelu=True, pre_out=pre)
+    ref_pre = xb.float() @ wb.float().t() + b
+    assert rel(pre, ref_pre) < 1e-2
+    assert rel(y, F.gelu(ref_pre)) < 1e-2
+    # residual with scatter map + gather map + column scale + row scale
+    perm = torch.randperm(M, device=dev).int()
+    gat = torch.randperm(M, device=dev).int()
+    resid = torch.randn(M, N, device=dev)
+    rs = torch.rand(4, device=dev) + 0.5
+    out = torch.empty(M, N, device=dev)
+    k.linear(xb, wb, b, out=out, resid=resid, c_map=perm, a_map=gat, scale_cols=64, scale_val=0.5,
+             row_scale=rs, rows_per_scale=130)
+    acc = xb.float()[gat.long()] @ wb.float().t() + b
+    acc[:, :64] *= 0.5
+    acc = acc * rs[torch.arange(M, device=dev) // 130][:, None]
+    ref = resid.clone()
+    ref[perm.long()] += acc
+    assert rel(out, ref) < 1e-2
+    # dX with dgelu and f32 dy with row scale
+    dy = torch.randn(M, N, device=dev)
+    dx = k.linear_dx(dy, wb, dgelu_pre=None, a_row_scale=rs, a_rows_per_scale=130)
+    ref_dx = (bf(dy * rs[torch.arange(M, device=dev) // 130][:, None]).float()) @ wb.float()
+    assert rel(dx, ref_dx) < 1e-2
+    dz = torch.randn(M, Kd, device=dev)
+    dpre = k.linear_dx(bf(dz), bf(w.t().contiguous()), out_f32=False, dgelu_pre=pre)
+    pre_r = pre.float().requires_grad_(True)
+    F.gelu(pre_r).sum().backward()
+    ref_dpre = (bf(dz).float() @ bf(w.t().contiguous()).float()) * pre_r.grad
+    assert rel(dpre, ref_dpre) < 2e-2
+    # dW with split-K atomics and gathered rows of dy
+    dw = torch.zeros(N, Kd, device=dev)
+    k.linear_dw(dy, xb, dw, a_map=gat)
+    ref_dw = bf(dy[gat.long()]).float().t() @ xb.float()
+    assert rel(dw, ref_dw) < 1e-2
+    # colsum
+    cs = torch.zeros(N, device=dev)
+    k.colsum(dy, cs, row_map=gat)
+    assert rel(cs, dy.sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("C,nseg,x_f32", [(128, 1, True), (768, 1, False), (2048, 4, True), (1024, 1, True)])
+def test_layernorm_fwd_bwd(C, nseg, x_f32):
+    k = K()
+    R = 333
+    seg = C // nseg
+    src = torch.randn(R * nseg, seg, device=dev) * 2 + 0.5
+    if not x_f32:
+        src = bf(src)
+    in_map = torch.randperm(R * nseg, device=dev).int()
+    w = torch.randn(C, device=dev) * 0.2 + 1
+    b = torch.randn(C, device=dev) * 0.1
+    y, mean, rstd = k.layernorm(src, w, b, 1e-5, in_map=in_map, nseg=nseg, rows=R, cols=C, out_f32=True)
+    xr = src.float()[in_map.long()].view(R, C).clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (C,), wr, br, 1e-5)
+    assert rel(y, yr) < 1e-4
+    dy = torch.randn(R, C, device=dev)
+    yr.backward(dy)
+    dx = torch.zeros(R * nseg, seg, device=dev)
+    dres = torch.randn(R * nseg, seg, device=dev)
+    dw = torch.zeros(C, device=dev)
+    db = torch.zeros(C, device=dev)
+    k.layernorm_bwd(dy, src, mean, rstd, w, dx, in_map=in_map, nseg=nseg, dres=dres, dw=dw, db=db, rows=R, cols=C)
+    ref_dx = dres.clone()
+    ref_dx[in_map.long()] += xr.grad.view(R * nseg, seg)
+    assert rel(dx, ref_dx) < 1e-4
+    assert rel(dw, wr.grad) < 1e-4
+    assert rel(db, br.grad) < 1e-4
+
+
+def _wattn_reference(qkv, table, index, region, win_pat, nH, n, c):
+    """fp32 reference of video_swin_ori.py:164-186 on the same stored (pre-scaled) q."""
+    nw = qkv.shape[0] // n
+    C = qkv.shape[1] // 3
+    hd = C // nH
+    x = qkv.float().view(nw, n, 3, nH, hd).permute(2, 0, 3, 1, 4)
+    q = (x[0] / c).requires_grad_(True)
+    kk = x[1].clone().requires_grad_(True)
+    v = x[2].clone().requires_grad_(True)
+    tab = table.clone().requires_grad_(True)
+    bias = tab[index[:n, :n].reshape(-1)].view(n, n, nH).permute(2, 0, 1)
+    mask = (region[win_pat.long()][:, :, None] != region[win_pat.long()][:, None, :]).float() * -100.0
+    s = (q * hd ** -0.5) @ kk.transpose(-1, -2) + bias[None] + mask[:, None]
+    o = s.softmax(-1) @ v
+    return o.transpose(1, 2).reshape(nw * n, C), (q, kk, v, tab)
+
+
+@pytest.mark.parametrize("nH,n_win", [(4, 9), (16, 5), (32, 2)])
+def test_window_attention_fwd_bwd(nH, n_win):
+    k = K()
+    n, hd = 147, 32
+    C = nH * hd
+    c = hd ** -0.5 * math.log2(math.e)
+    qkv = torch.randn(n_win * n, 3 * C, device=dev)
+    qkv[:, :C] *= c
+    qkv = bf(qkv)
+    table = torch.randn(2535, nH, device=dev)
+    index = O.relative_position_index((8, 7, 7)).to(dev)
+    n_pat = 3
+    region = torch.zeros(n_pat, n, dtype=torch.int32, device=dev)
+    region[1, 60:] = 1
+    region[2] = torch.randint(0, 3, (n,), device=dev).int()
+    win_pat = torch.randint(0, n_pat, (n_win,), device=dev).int()
+    bf_ = torch.empty(k.wattn_bias_elems(n_pat, nH), device=dev)
+    bb_ = torch.empty_like(bf_)
+    k.wattn_bias_build(table, index, n, nH, region, n_pat, bf_, bb_)
+    out = torch.empty(n_win * n, C, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(n_win, nH, 160, device=dev)
+    k.wattn_fwd(qkv, bf_, win_pat, out, lse, n_win, n, nH)
+    ref, (q, kk, v, tab) = _wattn_reference(qkv, table, index, region, win_pat, nH, n, c)
+    assert rel(out, ref) < 1e-2
+    dout = bf(torch.randn(n_win * n, C, device=dev))
+    ref.backward(dout.float())
+    dqkv = torch.empty(n_win * n, 3 * C, device=dev, dtype=torch.bfloat16)
+    ds = torch.empty(k.wattn_ds_elems(n_win, nH), device=dev, dtype=torch.bfloat16)
+    k.wattn_bwd(qkv, out, dout, lse, bb_, win_pat, dqkv, ds, n_win, n, nH)
+    tg = torch.zeros(2535, nH, device=dev)
+    k.wattn_dbias(ds, n_win, n, nH, index, tg)
+    d = dqkv.float().view(n_win, n, 3, nH, hd).permute(2, 0, 3, 1, 4)
+    assert rel(d[0], q.grad) < 2e-2
+    assert rel(d[1], kk.grad) < 2e-2
+    assert rel(d[2], v.grad) < 2e-2
+    assert rel(tg, tab.grad) < 2e-2
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,masked", [(3, 12, 32, 32, True), (4, 12, 1, 183, False), (2, 12, 40, 40, True)])
+def test_mha_fwd_bwd(B, H, Lq, Lk, masked):
+    k = K()
+    d = 64
+    q = bf(torch.randn(B, Lq, H * d, device=dev))
+    kv = bf(torch.randn(B, Lk, 2 * H * d, device=dev))
+    kmask = torch.ones(B, Lk, dtype=torch.int32, device=dev)
+    if masked:
+        kmask[0, 20:] = 0
+        kmask[-1, 5:] = 0
+    out = torch.empty(B, Lq, H * d, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, Lq, device=dev)
+    scale = 1 / 8
+    k.mha_fwd(q, H * d, kv, kv[..., H * d:], 2 * H * d, Lk * 2 * H * d, kmask, out, H * d, lse, B, H, Lq, Lk, d, scale)
+    qr = q.float().view(B, Lq, H, d).transpose(1, 2).requires_grad_(True)
+    kr = kv[..., :H * d].float().reshape(B, Lk, H, d).transpose(1, 2).contiguous().requires_grad_(True)
+    vr = kv[..., H * d:].float().reshape(B, Lk, H, d).transpose(1, 2).contiguous().requires_grad_(True)
+    s = (qr @ kr.transpose(-1, -2)) * scale + (1 - kmask.float())[:, None, None, :] * -1e30
+    o = (s.softmax(-1) @ vr).transpose(1, 2).reshape(B, Lq, H * d)
+    assert rel(out, o) < 1e-2
+    dout = bf(torch.randn(B, Lq, H * d, device=dev))
+    o.backward(dout.float())
+    dq = torch.empty(B, Lq, H * d, device=dev)
+    dkv = torch.empty(B, Lk, 2 * H * d, device=dev)
+    k.mha_bwd(q, H * d, kv, kv[..., H * d:], 2 * H * d, Lk * 2 * H * d, kmask, out, H * d, dout, lse, dq, H * d,
+              dkv, dkv[..., H * d:], 2 * H * d, Lk * 2 * H * d, B, H, Lq, Lk, d, scale)
+    assert rel(dq, qr.grad.transpose(1, 2).reshape(B, Lq, H * d)) < 1e-2
+    assert rel(dkv[..., :H * d], kr.grad.transpose(1, 2).reshape(B, Lk, H * d)) < 1e-2
+    assert rel(dkv[..., H * d:], vr.grad.transpose(1, 2).reshape(B, Lk, H * d)) < 1e-2
+
+
+def test_patch_im2col_matches_conv():
+    k = K()
+    B, S, T, H, W = 2, 3, 5, 32, 48
+    clips = torch.rand(B, S, T, 3, H, W, device=dev)
+    Dp = (T + 1) // 2
+    patches = torch.empty(B * S * Dp * (H // 4) * (W // 4), 96, device=dev, dtype=torch.bfloat16)
+    k.patch_im2col(clips, patches)
+    wconv = torch.randn(128, 3, 2, 4, 4, device=dev)
+    x = O.normalize_clip(clips.cpu()).to(dev).flatten(0, 1).transpose(1, 2)
+    x = F.pad(x, (0, 0, 0, 0, 0, T % 2))
+    ref = F.conv3d(x, wconv, stride=(2, 4, 4)).permute(0, 2, 3, 4, 1).reshape(-1, 128)
+    got = patches.float() @ wconv.view(128, 96).t()
+    assert rel(got, ref) < 1e-2
+
+
+def test_adamw_matches_torch():
+    k = K()
+    n = 3 * 1024
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    chunk_tensor = torch.tensor([0, 1, 1], dtype=torch.int32, device=dev)
+    lrs = torch.tensor([1e-3, 5e-4], device=dev)
+    sumsq = torch.empty(2, device=dev)
+    pref = [p[:1024].clone().requires_grad_(True), p[1024:].clone().requires_grad_(True)]
+    opt = torch.optim.AdamW([{"params": [pref[0]], "lr": 1e-3}, {"params": [pref[1]], "lr": 5e-4}], betas=(0.9, 0.999))
+    reg = 0.001
+    for step in range(1, 4):
+        k.l2norm_multi(p, chunk_tensor, 3, sumsq, 2)
+        pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
+        k.adamw_step(p, g, m, v, chunk_tensor, lrs, sumsq, pb, 3, 0.9, 0.999, 1e-8, 0.01, 1.0, reg,
+                     1 - 0.9 ** step, 1 - 0.999 ** step)
+        opt.zero_grad()
+        loss = (pref[0] * g[:1024]).sum() + (pref[1] * g[1024:]).sum() + reg * (pref[0].norm() + pref[1].norm())
+        loss.backward()
+        opt.step()
+    torch.cuda.synchronize()
+    assert rel(p, torch.cat([pref[0].detach(), pref[1].detach()])) < 1e-5

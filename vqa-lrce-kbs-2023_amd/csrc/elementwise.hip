@@ -1,0 +1,281 @@
+// Memory-bound helpers on the LRCE path: patch im2col (+ImageNet normalise +T padding), bias
+// column sums, casts, dropout, and the embedding sums of BERT / LRCE positional embeddings.
+// All vectorised 16 B per lane where the layout allows; HBM-bound by construction.
+#include "common.h"
+#include "lrce_capi.h"
+
+namespace {
+
+// ---------------------------------------------------------------- patch im2col
+// clips f32 [B][S][T][3][H][W] -> patches bf16 [(b*S + s)*Dp*Hp*Wp + (d*Hp + h)*Wp + w][96],
+// column = c*32 + kt*16 + kh*4 + kw (conv3d weight [128][3][2][4][4] flattened).
+// Normalize (video.py:35) precedes the T padding (video_swin_ori.py:472-473): padded frames are 0.
+__global__ void im2col_kernel(const float* __restrict__ clips, bf16* __restrict__ out, int B, int S, int T, int H, int W) {
+  const int Dp = (T + 1) / 2, Hp = H / 4, Wp = W / 4;
+  const long long tok = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long long ntok = (long long)S * B * Dp * Hp * Wp;
+  if (tok >= ntok) return;
+  const int lane = threadIdx.x & 63;
+  // lane < 24: one (c, kt, kh) row of 4 kw values
+  if (lane >= 24) return;
+  long long t = tok;
+  const int w = t % Wp; t /= Wp;
+  const int h = t % Hp; t /= Hp;
+  const int d = t % Dp; t /= Dp;
+  const int s = t % S;
+  const int b = t / S;
+  const int c = lane >> 3, kt = (lane >> 2) & 1, kh = lane & 3;
+  const int frame = 2 * d + kt;
+  const float mean = c == 0 ? 0.485f : (c == 1 ? 0.456f : 0.406f);
+  const float istd = c == 0 ? 1.0f / 0.229f : (c == 1 ? 1.0f / 0.224f : 1.0f / 0.225f);
+  bf16x4 o;
+  if (frame < T) {
+    const float* src = clips + ((((long long)b * S + s) * T + frame) * 3 + c) * H * W + (long long)(4 * h + kh) * W + 4 * w;
+    const float4 v = *reinterpret_cast<const float4*>(src);
+    o[0] = f2bf((v.x - mean) * istd); o[1] = f2bf((v.y - mean) * istd);
+    o[2] = f2bf((v.z - mean) * istd); o[3] = f2bf((v.w - mean) * istd);
+  } else {
+    o[0] = o[1] = o[2] = o[3] = f2bf(0.f);
+  }
+  *reinterpret_cast<bf16x4*>(out + tok * 96 + lane * 4) = o;
+}
+
+// ---------------------------------------------------------------- column sums
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ x, const int* __restrict__ map, long long ld, int m, int n, float* __restrict__ out) {
+  // block: 256 threads = 64 columns x 4 row-groups; grid.x over column blocks, grid.y over row chunks
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int rows_per = (m + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows_per, r1 = min(m, r0 + rows_per);
+  float s = 0.f;
+  if (col < n)
+    for (int r = r0 + rg; r < r1; r += 4) {
+      const long long rr = map ? (long long)map[r] : (long long)r;
+      s += (float)x[rr * ld + col];
+    }
+  __shared__ float red[4][64];
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && col < n) atomicAdd(out + col, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+__global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    const float4 v = *reinterpret_cast<const float4*>(x + i);
+    bf16x4 o;
+    o[0] = f2bf(v.x); o[1] = f2bf(v.y); o[2] = f2bf(v.z); o[3] = f2bf(v.w);
+    *reinterpret_cast<bf16x4*>(y + i) = o;
+  } else {
+    for (long long j = i; j < n; ++j) y[j] = f2bf(x[j]);
+  }
+}
+
+__global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, bf16* __restrict__ yb, long long n, float p,
+                               uint64_t seed) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = x[i];
+  if (p > 0.f) v = (lrce_uniform(seed, i) >= p) ? v / (1.0f - p) : 0.f;
+  y[i] = v;
+  if (yb) yb[i] = f2bf(v);
+}
+
+__global__ void dropout_bwd_kernel(const float* __restrict__ dy, float* __restrict__ dx, long long n, float p, uint64_t seed) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = dy[i];
+  if (p > 0.f) v = (lrce_uniform(seed, i) >= p) ? v / (1.0f - p) : 0.f;
+  dx[i] = v;
+}
+
+// ---------------------------------------------------------------- embeddings
+// BERT: out[r][c] = word[ids[r]][c] + pos[r % L][c] + type[types[r]][c]
+__global__ void bert_embed_kernel(const long long* __restrict__ ids, const long long* __restrict__ types, const float* __restrict__ word,
+                                  const float* __restrict__ pos, const float* __restrict__ typ, float* __restrict__ out, int rows, int L,
+                                  int C) {
+  const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e >= (long long)rows * C) return;
+  const int r = e / C, c = e % C;
+  const float4 a = *reinterpret_cast<const float4*>(word + ids[r] * C + c);
+  const float4 b = *reinterpret_cast<const float4*>(pos + (long long)(r % L) * C + c);
+  const float4 t = *reinterpret_cast<const float4*>(typ + types[r] * C + c);
+  *reinterpret_cast<float4*>(out + e) = make_float4(a.x + b.x + t.x, a.y + b.y + t.y, a.z + b.z + t.z, a.w + b.w + t.w);
+}
+__global__ void bert_embed_bwd_kernel(const float* __restrict__ d, const long long* __restrict__ ids, const long long* __restrict__ types,
+                                      float* __restrict__ dword, float* __restrict__ dpos, float* __restrict__ dtyp, int rows, int L, int C) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)rows * C) return;
+  const int r = e / C, c = e % C;
+  const float g = d[e];
+  atomicAdd(dword + ids[r] * C + c, g);
+  atomicAdd(dpos + (long long)(r % L) * C + c, g);
+  atomicAdd(dtyp + types[r] * C + c, g);
+}
+
+// LRCE VideoPosEmbed (embedding.py:47-63) before its LayerNorm:
+// out[b,s,t,p,c] = (p == 0 ? cls[c] : x[b,s,t,p-1,c]) + pos[p,c] + len[t,c] + clip[s,c]
+__global__ void video_pos_kernel(const float* __restrict__ x, const float* __restrict__ cls, const float* __restrict__ pos,
+                                 const float* __restrict__ len, const float* __restrict__ clip, float* __restrict__ out, int B, int S,
+                                 int Tg, int P, int C) {
+  const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long long total = (long long)B * S * Tg * (P + 1) * C;
+  if (e >= total) return;
+  long long t = e / C;
+  const int c = e % C;
+  const int p = t % (P + 1); t /= (P + 1);
+  const int tg = t % Tg; t /= Tg;
+  const int s = t % S;
+  const long long bst = t * Tg + tg;  // (b*S + s)*Tg + tg
+  float4 v = p == 0 ? *reinterpret_cast<const float4*>(cls + c)
+                    : *reinterpret_cast<const float4*>(x + (bst * P + (p - 1)) * C + c);
+  const float4 a = *reinterpret_cast<const float4*>(pos + (long long)p * C + c);
+  const float4 l = *reinterpret_cast<const float4*>(len + (long long)tg * C + c);
+  const float4 k = *reinterpret_cast<const float4*>(clip + (long long)s * C + c);
+  *reinterpret_cast<float4*>(out + e) = make_float4(v.x + a.x + l.x + k.x, v.y + a.y + l.y + k.y, v.z + a.z + l.z + k.z, v.w + a.w + l.w + k.w);
+}
+__global__ void video_pos_bwd_kernel(const float* __restrict__ d, float* __restrict__ dx, float* __restrict__ dcls, float* __restrict__ dpos,
+                                     float* __restrict__ dlen, float* __restrict__ dclip, int B, int S, int Tg, int P, int C) {
+  // one thread per (p, c): loop over (b, s, t); len/clip/cls through atomics of per-thread sums
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (c >= C) return;
+  float sp = 0.f;
+  for (int s = 0; s < S; ++s) {
+    float ss = 0.f;
+    for (int tg = 0; tg < Tg; ++tg) {
+      float st = 0.f;
+      for (int b = 0; b < B; ++b) {
+        const long long bst = ((long long)b * S + s) * Tg + tg;
+        const float g = d[(bst * (P + 1) + p) * C + c];
+        st += g;
+        if (p > 0) dx[(bst * P + (p - 1)) * C + c] = g;
+      }
+      ss += st;
+      atomicAdd(dlen + (long long)tg * C + c, st);
+    }
+    sp += ss;
+    atomicAdd(dclip + (long long)s * C + c, ss);
+  }
+  dpos[(long long)p * C + c] += sp;
+  if (p == 0) dcls[c] += sp;
+}
+
+// TextPosEmbed (embedding.py:17-23): out[b,l,c] = (l == 0 ? cls[c] : x[b,l-1,c]) + pos[l,c]
+__global__ void text_pos_kernel(const float* __restrict__ x, const float* __restrict__ cls, const float* __restrict__ pos,
+                                float* __restrict__ out, int B, int L, int C) {
+  const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e >= (long long)B * (L + 1) * C) return;
+  const long long r = e / C;
+  const int c = e % C, l = r % (L + 1), b = r / (L + 1);
+  float4 v = l == 0 ? *reinterpret_cast<const float4*>(cls + c) : *reinterpret_cast<const float4*>(x + ((long long)b * L + l - 1) * C + c);
+  const float4 a = *reinterpret_cast<const float4*>(pos + (long long)l * C + c);
+  *reinterpret_cast<float4*>(out + e) = make_float4(v.x + a.x, v.y + a.y, v.z + a.z, v.w + a.w);
+}
+__global__ void text_pos_bwd_kernel(const float* __restrict__ d, float* __restrict__ dx, float* __restrict__ dcls, float* __restrict__ dpos,
+                                    int B, int L, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = blockIdx.y;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float g = d[((long long)b * (L + 1) + l) * C + c];
+    s += g;
+    if (l > 0) dx[((long long)b * L + l - 1) * C + c] = g;
+  }
+  dpos[(long long)l * C + c] += s;
+  if (l == 0) dcls[c] += s;
+}
+
+}  // namespace
+
+extern "C" int lrce_patch_im2col(const float* clips, uint16_t* patches, int B, int S, int T, int H, int W, void* stream) {
+  if (!clips || !patches) return lrce_fail(LRCE_E_ARG, "patch_im2col: null pointer");
+  if (H % 4 || W % 4 || T < 1) return lrce_fail(LRCE_E_ARG, "patch_im2col: H,W must be multiples of 4");
+  const long long ntok = (long long)S * B * ((T + 1) / 2) * (H / 4) * (W / 4);
+  im2col_kernel<<<(ntok + 3) / 4, 256, 0, static_cast<hipStream_t>(stream)>>>(clips, reinterpret_cast<bf16*>(patches), B, S, T, H, W);
+  return lrce_check_launch("patch_im2col");
+}
+
+extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, int m, int n, float* out, void* stream) {
+  if (!x || !out) return lrce_fail(LRCE_E_ARG, "colsum: null pointer");
+  if (m <= 0 || n <= 0) return LRCE_OK;
+  int chunks = (m + 255) / 256;
+  if (chunks > 256) chunks = 256;
+  dim3 grid((n + 63) / 64, chunks);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (x_f32) colsum_kernel<float><<<grid, 256, 0, s>>>(static_cast<const float*>(x), row_map, ld, m, n, out);
+  else colsum_kernel<bf16><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), row_map, ld, m, n, out);
+  return lrce_check_launch("colsum");
+}
+
+extern "C" int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream) {
+  if (!x || !y) return lrce_fail(LRCE_E_ARG, "cast_bf16: null pointer");
+  if (n <= 0) return LRCE_OK;
+  const long long thr = (n + 3) / 4;
+  cast_kernel<<<(thr + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(x, reinterpret_cast<bf16*>(y), n);
+  return lrce_check_launch("cast_bf16");
+}
+
+extern "C" int lrce_dropout(const float* x, float* y, uint16_t* y_bf16, int64_t n, float p, uint64_t seed, void* stream) {
+  if (!x || !y) return lrce_fail(LRCE_E_ARG, "dropout: null pointer");
+  if (n <= 0) return LRCE_OK;
+  dropout_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(x, y, reinterpret_cast<bf16*>(y_bf16), n, p, seed);
+  return lrce_check_launch("dropout");
+}
+
+extern "C" int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t seed, void* stream) {
+  if (!dy || !dx) return lrce_fail(LRCE_E_ARG, "dropout_bwd: null pointer");
+  if (n <= 0) return LRCE_OK;
+  dropout_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(dy, dx, n, p, seed);
+  return lrce_check_launch("dropout_bwd");
+}
+
+extern "C" int lrce_bert_embed_fwd(const int64_t* ids, const int64_t* types, const float* word, const float* pos, const float* typ,
+                                   float* out, int rows, int L, int C, void* stream) {
+  if (!ids || !types || !word || !pos || !typ || !out || C % 4) return lrce_fail(LRCE_E_ARG, "bert_embed_fwd: bad args");
+  const long long thr = (long long)rows * C / 4;
+  bert_embed_kernel<<<(thr + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(
+      reinterpret_cast<const long long*>(ids), reinterpret_cast<const long long*>(types), word, pos, typ, out, rows, L, C);
+  return lrce_check_launch("bert_embed_fwd");
+}
+
+extern "C" int lrce_bert_embed_bwd(const float* dout, const int64_t* ids, const int64_t* types, float* dword, float* dpos, float* dtyp,
+                                   int rows, int L, int C, void* stream) {
+  if (!dout || !ids || !types || !dword || !dpos || !dtyp) return lrce_fail(LRCE_E_ARG, "bert_embed_bwd: null pointer");
+  const long long n = (long long)rows * C;
+  bert_embed_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(
+      dout, reinterpret_cast<const long long*>(ids), reinterpret_cast<const long long*>(types), dword, dpos, dtyp, rows, L, C);
+  return lrce_check_launch("bert_embed_bwd");
+}
+
+extern "C" int lrce_video_posembed_fwd(const float* x, const float* cls, const float* pos, const float* len, const float* clip, float* out,
+                                       int B, int S, int Tg, int P, int C, void* stream) {
+  if (!x || !cls || !pos || !len || !clip || !out || C % 4) return lrce_fail(LRCE_E_ARG, "video_posembed_fwd: bad args");
+  const long long thr = (long long)B * S * Tg * (P + 1) * C / 4;
+  video_pos_kernel<<<(thr + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(x, cls, pos, len, clip, out, B, S, Tg, P, C);
+  return lrce_check_launch("video_posembed_fwd");
+}
+
+extern "C" int lrce_video_posembed_bwd(const float* dout, float* dx, float* dcls, float* dpos, float* dlen, float* dclip, int B, int S,
+                                       int Tg, int P, int C, void* stream) {
+  if (!dout || !dx || !dcls || !dpos || !dlen || !dclip) return lrce_fail(LRCE_E_ARG, "video_posembed_bwd: null pointer");
+  dim3 grid((C + 255) / 256, P + 1);
+  video_pos_bwd_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(dout, dx, dcls, dpos, dlen, dclip, B, S, Tg, P, C);
+  return lrce_check_launch("video_posembed_bwd");
+}
+
+extern "C" int lrce_text_posembed_fwd(const float* x, const float* cls, const float* pos, float* out, int B, int L, int C, void* stream) {
+  if (!x || !cls || !pos || !out || C % 4) return lrce_fail(LRCE_E_ARG, "text_posembed_fwd: bad args");
+  const long long thr = (long long)B * (L + 1) * C / 4;
+  text_pos_kernel<<<(thr + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(x, cls, pos, out, B, L, C);
+  return lrce_check_launch("text_posembed_fwd");
+}
+
+extern "C" int lrce_text_posembed_bwd(const float* dout, float* dx, float* dcls, float* dpos, int B, int L, int C, void* stream) {
+  if (!dout || !dx || !dcls || !dpos) return lrce_fail(LRCE_E_ARG, "text_posembed_bwd: null pointer");
+  dim3 grid((C + 255) / 256, L + 1);
+  text_pos_bwd_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(dout, dx, dcls, dpos, B, L, C);
+  return lrce_check_launch("text_posembed_bwd");
+}

@@ -1,0 +1,80 @@
+// Fused optimizer step over the flat parameter buffer: the caller side of the LRCE training step
+// (AdamW with 3 learning-rate groups, agent_base.py:27-44, plus the L2-norm regulariser
+// reg * sum_t ||p_t||_2, agent_base.py:103-108, whose gradient reg * p_t / ||p_t|| is folded in
+// here instead of being back-propagated through 783 norm kernels).  Parameters are laid out so
+// that every tensor starts at a multiple of 1024 elements; chunk c (1024 elements) belongs to one
+// tensor (chunk_tensor[c]).  One pass reads p, g, m, v and writes p, m, v and the bf16 shadow
+// copy the forward kernels consume: 4+4+4+4 + 4+4+4+2 = 30 B per parameter, HBM-bound.
+#include "common.h"
+#include "lrce_capi.h"
+
+namespace {
+
+__global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ p, const int* __restrict__ chunk_tensor, int n_chunks,
+                                                    float* __restrict__ sumsq) {
+  const int c = blockIdx.x;
+  if (c >= n_chunks) return;
+  const float4 v = reinterpret_cast<const float4*>(p + (long long)c * 1024)[threadIdx.x];
+  float s = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  s = wave_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(sumsq + chunk_tensor[c], red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                                    float* __restrict__ v, const int* __restrict__ chunk_tensor,
+                                                    const float* __restrict__ tensor_lr, const float* __restrict__ sumsq,
+                                                    bf16* __restrict__ pb, int n_chunks, float b1, float b2, float eps, float wd,
+                                                    float gscale, float reg, float bc1, float bc2) {
+  const int c = blockIdx.x;
+  if (c >= n_chunks) return;
+  const int t = chunk_tensor[c];
+  const float lr = tensor_lr[t];
+  const float ss = sumsq ? sumsq[t] : 0.f;
+  const float rc = (reg != 0.f && ss > 0.f) ? reg * rsqrtf(ss) : 0.f;
+  const long long i = (long long)c * 1024 + threadIdx.x * 4;
+  float4 pp = *reinterpret_cast<float4*>(p + i);
+  const float4 gg = *reinterpret_cast<const float4*>(g + i);
+  float4 mm = *reinterpret_cast<float4*>(m + i);
+  float4 vv = *reinterpret_cast<float4*>(v + i);
+  const float step = lr / bc1, isb2 = rsqrtf(bc2), decay = 1.0f - lr * wd;
+  float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+  bf16x4 ob;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float gr = ga[j] * gscale + rc * pa[j];
+    ma[j] = b1 * ma[j] + (1.0f - b1) * gr;
+    va[j] = b2 * va[j] + (1.0f - b2) * gr * gr;
+    const float np = pa[j] * decay - step * ma[j] / (sqrtf(va[j]) * isb2 + eps);
+    pa[j] = np;
+    ob[j] = f2bf(np);
+  }
+  *reinterpret_cast<float4*>(p + i) = pp;
+  *reinterpret_cast<float4*>(m + i) = mm;
+  *reinterpret_cast<float4*>(v + i) = vv;
+  if (pb) *reinterpret_cast<bf16x4*>(pb + i) = ob;
+}
+
+}  // namespace
+
+extern "C" int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks, float* sumsq, int n_tensors,
+                                 void* stream) {
+  if (!p || !chunk_tensor || !sumsq) return lrce_fail(LRCE_E_ARG, "l2norm_multi: null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipMemsetAsync(sumsq, 0, sizeof(float) * n_tensors, s);
+  if (n_chunks > 0) sumsq_kernel<<<n_chunks, 256, 0, s>>>(p, chunk_tensor, n_chunks, sumsq);
+  return lrce_check_launch("l2norm_multi");
+}
+
+extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
+                               const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
+                               float weight_decay, float grad_scale, float reg, float bc1, float bc2, void* stream) {
+  if (!p || !g || !m || !v || !chunk_tensor || !tensor_lr) return lrce_fail(LRCE_E_ARG, "adamw_step: null pointer");
+  if (n_chunks > 0)
+    adamw_kernel<<<n_chunks, 256, 0, static_cast<hipStream_t>(stream)>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq,
+                                                                         reinterpret_cast<bf16*>(p_bf16), n_chunks, beta1, beta2, eps,
+                                                                         weight_decay, grad_scale, reg, bc1, bc2);
+  return lrce_check_launch("adamw_step");
+}

@@ -1,0 +1,431 @@
+// Fused 3D shifted-window attention for Video Swin (WindowAttention3D.forward,
+// video_swin_ori.py:158-189) on gfx950.
+//
+// One wave owns one (window, head) problem: n <= 160 tokens (147 = 3x7x7 padded to 5 tiles of
+// 32), head_dim 32.  All products use v_mfma_f32_32x32x16_bf16.
+//
+// Forward computes S^T = K Q^T so each lane owns one query column and 80 key rows: the softmax
+// row reductions are in-lane plus one cross-half exchange, and the probabilities are already the
+// B operand of O^T = V^T P^T (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's
+// operand").  The relative-position bias, the shift mask (-100) and the key padding (-1e30) are
+// pre-combined per (mask pattern, head), pre-multiplied by log2(e) and stored in the exact
+// per-lane accumulator order, so the MFMA chain starts from the bias: no VALU for scale/bias/mask.
+// q is pre-scaled by head_dim^-0.5 * log2(e) in the QKV GEMM epilogue, so p = exp2(s - max).
+//
+// Backward recomputes S = Q K^T (rows = queries) tile by tile, and produces dV = P^T dO and
+// dK = dS^T Q with P / dS straight from registers as A operands, dQ = dS K through a 2 KB LDS
+// transpose of dS; dQ accumulates across key tiles in registers.  dS (bf16) is also written in
+// per-lane tile order for the bias-table gradient (lrce_wattn_dbias sums it over windows).
+#include "common.h"
+#include "lrce_capi.h"
+
+namespace {
+
+constexpr int TQ = 32;        // tile edge
+constexpr int NTILE = 5;      // 160 / 32
+constexpr int NPAD = 160;
+constexpr int HD = 32;        // head dim
+constexpr int TILE_ELEMS = 64 * 16;
+constexpr int PH_ELEMS = NTILE * NTILE * TILE_ELEMS;  // per (pattern, head)
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float NEG_BIG = -1.0e30f;
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// row index (inside a 32x32 C tile) held in register `reg` by lane half `h`
+__device__ __forceinline__ int crow(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+__device__ __forceinline__ bf16x8 ld_row16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// transposed read of an LDS image [rows][32] bf16 (64-B rows): returns 8 elements
+// element j = img[r_base + 8*(j>>2) + 4*hh + (j&3)][c = 16*((lane>>4)&1) + (lane&15)],
+// i.e. the operand fragment whose k index follows the permuted accumulator order.
+__device__ __forceinline__ bf16x8 tr_read_perm(const bf16* img, int r_base, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int hh = g >> 1, cb = 16 * (g & 1);
+  bf16x8 out;
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    const int row = r_base + 8 * h2 + 4 * hh + q;
+    const LRCE_LDS s16x4* src = (const LRCE_LDS s16x4*)(img + row * 32 + cb + 4 * p);
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<LRCE_LDS s16x4*>(src));
+    bf16x4 b = *reinterpret_cast<bf16x4*>(&v);
+    out[4 * h2 + 0] = b[0]; out[4 * h2 + 1] = b[1]; out[4 * h2 + 2] = b[2]; out[4 * h2 + 3] = b[3];
+  }
+  return out;
+}
+// same, natural k order: element j = img[r_base + 8*hh + 4*(j>>2) + (j&3)][c]
+__device__ __forceinline__ bf16x8 tr_read_nat(const bf16* img, int r_base, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int hh = g >> 1, cb = 16 * (g & 1);
+  bf16x8 out;
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    const int row = r_base + 8 * hh + 4 * h2 + q;
+    const LRCE_LDS s16x4* src = (const LRCE_LDS s16x4*)(img + row * 32 + cb + 4 * p);
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<LRCE_LDS s16x4*>(src));
+    bf16x4 b = *reinterpret_cast<bf16x4*>(&v);
+    out[4 * h2 + 0] = b[0]; out[4 * h2 + 1] = b[1]; out[4 * h2 + 2] = b[2]; out[4 * h2 + 3] = b[3];
+  }
+  return out;
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& a, int s) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(a[8 * s + j]);
+  return o;
+}
+
+// stage rows [0,160) x 32 cols of a head slice into an LDS image (zero rows >= n)
+__device__ __forceinline__ void stage_img(bf16* img, const bf16* src, long long ld, int n, int lane) {
+#pragma unroll
+  for (int t = 0; t < 10; ++t) {
+    const int c = lane + 64 * t;
+    const int row = c >> 2, part = c & 3;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < n) v = *reinterpret_cast<const uint4*>(src + row * ld + part * 8);
+    *reinterpret_cast<uint4*>(img + row * 32 + part * 8) = v;
+  }
+}
+
+// ------------------------------------------------------------------------------ bias tiles
+__global__ void bias_build_kernel(const float* table, const int64_t* index, int ld, int n, int nH,
+                                  const int* region, int n_pat, float* bf, float* bb) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)n_pat * nH * PH_ELEMS;
+  if (e >= total) return;
+  const int reg = e & 15, lane = (e >> 4) & 63;
+  const int tile = (e / TILE_ELEMS) % (NTILE * NTILE);
+  const int ph = e / PH_ELEMS;
+  const int h = ph % nH, pat = ph / nH;
+  const int qt = tile / NTILE, kt = tile % NTILE;
+  const int* rg = region ? region + pat * n : nullptr;
+  auto val = [&](int i, int j) -> float {
+    if (j >= n) return NEG_BIG;
+    if (i >= n) return 0.f;
+    float v = table[index[(long long)i * ld + j] * nH + h];
+    if (rg && rg[i] != rg[j]) v += -100.0f;
+    return v * LOG2E;
+  };
+  const int hh = lane >> 5, col = lane & 31;
+  // forward: S^T tile (rows = keys, cols = queries)
+  bf[e] = val(qt * TQ + col, kt * TQ + crow(reg, hh));
+  // backward: S tile (rows = queries, cols = keys)
+  bb[e] = val(qt * TQ + crow(reg, hh), kt * TQ + col);
+}
+
+// ------------------------------------------------------------------------------ forward
+__global__ void __launch_bounds__(256, 2) wattn_fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ biasf,
+                                                           const int* __restrict__ win_pat, bf16* __restrict__ out,
+                                                           float* __restrict__ lse, int n_win, int n, int nH) {
+  __shared__ __attribute__((aligned(16))) bf16 vimg_all[4][NPAD * HD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int w = blockIdx.x * 4 + wave, h = blockIdx.y;
+  if (w >= n_win) return;
+  const int C = nH * HD;
+  const long long ld = 3LL * C;
+  const bf16* base = qkv + (long long)w * n * ld;
+  bf16* vimg = vimg_all[wave];
+  stage_img(vimg, base + 2 * C + h * HD, ld, n, lane);
+
+  const int hh = lane >> 5, r32 = lane & 31;
+  bf16x8 kf[NTILE][2];
+#pragma unroll
+  for (int kt = 0; kt < NTILE; ++kt) {
+    const int key = kt * TQ + r32;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 v = {};
+      if (key < n) v = ld_row16(base + key * ld + C + h * HD + 16 * s + 8 * hh);
+      kf[kt][s] = v;
+    }
+  }
+  wave_lds_fence();
+  const int pat = win_pat ? win_pat[w] : 0;
+  const float* bp = biasf + (long long)(pat * nH + h) * PH_ELEMS + lane * 16;
+
+  for (int qt = 0; qt < NTILE; ++qt) {
+    if (qt * TQ >= n) break;
+    const int qi = qt * TQ + r32;
+    bf16x8 qf[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 v = {};
+      if (qi < n) v = ld_row16(base + qi * ld + h * HD + 16 * s + 8 * hh);
+      qf[s] = v;
+    }
+    f32x16 acc[NTILE];
+#pragma unroll
+    for (int kt = 0; kt < NTILE; ++kt) {
+      const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + kt) * TILE_ELEMS);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 b = src[u];
+        acc[kt][4 * u] = b.x; acc[kt][4 * u + 1] = b.y; acc[kt][4 * u + 2] = b.z; acc[kt][4 * u + 3] = b.w;
+      }
+      acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][0], qf[0], acc[kt], 0, 0, 0);
+      acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][1], qf[1], acc[kt], 0, 0, 0);
+    }
+    float m = NEG_BIG;
+#pragma unroll
+    for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[kt][r]);
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(acc[kt][r] - m);
+        acc[kt][r] = p;
+        sum += p;
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    f32x16 o = {};
+#pragma unroll
+    for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 a = tr_read_perm(vimg, kt * TQ + 16 * s, lane);
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pack8(acc[kt], s), o, 0, 0, 0);
+      }
+    if (qi < n) {
+      const float inv = 1.0f / sum;
+      bf16* dst = out + ((long long)w * n + qi) * C + h * HD + 4 * hh;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        bf16x4 v;
+        v[0] = f2bf(o[4 * rr] * inv); v[1] = f2bf(o[4 * rr + 1] * inv);
+        v[2] = f2bf(o[4 * rr + 2] * inv); v[3] = f2bf(o[4 * rr + 3] * inv);
+        *reinterpret_cast<bf16x4*>(dst + 8 * rr) = v;
+      }
+      if (hh == 0) lse[((long long)w * nH + h) * NPAD + qi] = m + __log2f(sum);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+struct BwdLds {
+  bf16 q[NPAD * HD];
+  bf16 k[NPAD * HD];
+  bf16 dout[NPAD * HD];
+  bf16 t[TQ * TQ];
+  float lse[NPAD];
+  float delta[NPAD];
+};
+
+__global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
+                                                           const bf16* __restrict__ dout, const float* __restrict__ lse_g,
+                                                           const float* __restrict__ biasb, const int* __restrict__ win_pat,
+                                                           bf16* __restrict__ dqkv, bf16* __restrict__ ds_out,
+                                                           int n_win, int n, int nH, float scale) {
+  __shared__ __attribute__((aligned(16))) BwdLds L_all[2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int w = blockIdx.x * 2 + wave, h = blockIdx.y;
+  if (w >= n_win) return;
+  BwdLds& L = L_all[wave];
+  const int C = nH * HD;
+  const long long ld = 3LL * C;
+  const bf16* base = qkv + (long long)w * n * ld;
+  const bf16* obase = outp + (long long)w * n * C + h * HD;
+  const bf16* dobase = dout + (long long)w * n * C + h * HD;
+  stage_img(L.q, base + h * HD, ld, n, lane);
+  stage_img(L.k, base + C + h * HD, ld, n, lane);
+  stage_img(L.dout, dobase, C, n, lane);
+  const float* lsep = lse_g + ((long long)w * nH + h) * NPAD;
+  for (int qi = lane; qi < NPAD; qi += 64) {
+    float d = 0.f, l = 0.f;
+    if (qi < n) {
+#pragma unroll
+      for (int part = 0; part < 4; ++part) {
+        const bf16x8 a = ld_row16(obase + qi * C + part * 8);
+        const bf16x8 b = ld_row16(dobase + qi * C + part * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
+      }
+      l = lsep[qi];
+    }
+    L.delta[qi] = d;
+    L.lse[qi] = l;
+  }
+  wave_lds_fence();
+
+  const int hh = lane >> 5, r32 = lane & 31;
+  const int pat = win_pat ? win_pat[w] : 0;
+  const float* bp = biasb + (long long)(pat * nH + h) * PH_ELEMS + lane * 16;
+  bf16* dsp = ds_out + ((long long)w * nH + h) * PH_ELEMS + lane * 16;
+  const float kscale = 1.0f / LOG2E;
+  const int nqt = (n + TQ - 1) / TQ;
+
+  f32x16 dq[NTILE];
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t) dq[t] = f32x16{};
+
+#pragma unroll
+  for (int kt = 0; kt < NTILE; ++kt) {
+    if (kt < nqt) {
+      const int key = kt * TQ + r32;
+      bf16x8 kf[2], vf[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 a = {}, b = {};
+        if (key < n) {
+          a = ld_row16(base + key * ld + C + h * HD + 16 * s + 8 * hh);
+          b = ld_row16(base + key * ld + 2 * C + h * HD + 16 * s + 8 * hh);
+        }
+        kf[s] = a;
+        vf[s] = b;
+      }
+      f32x16 dv = {}, dk = {};
+#pragma unroll
+      for (int qt = 0; qt < NTILE; ++qt) {
+        if (qt < nqt) {
+          // S tile: rows = queries, cols = keys
+          f32x16 sacc;
+          const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + kt) * TILE_ELEMS);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float4 b = src[u];
+            sacc[4 * u] = b.x; sacc[4 * u + 1] = b.y; sacc[4 * u + 2] = b.z; sacc[4 * u + 3] = b.w;
+          }
+          bf16x8 qa[2], da[2];
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            qa[s] = *reinterpret_cast<const bf16x8*>(L.q + (qt * TQ + r32) * HD + 16 * s + 8 * hh);
+            da[s] = *reinterpret_cast<const bf16x8*>(L.dout + (qt * TQ + r32) * HD + 16 * s + 8 * hh);
+          }
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[0], kf[0], sacc, 0, 0, 0);
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[1], kf[1], sacc, 0, 0, 0);
+          f32x16 dp = {};
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[0], vf[0], dp, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[1], vf[1], dp, 0, 0, 0);
+          // P and dS (natural-log scale)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int qi = qt * TQ + crow(r, hh);
+            const float p = exp2f(sacc[r] - L.lse[qi]);
+            sacc[r] = p;
+            dp[r] = p * (dp[r] - L.delta[qi]);
+          }
+          // dV += P^T dO ; dK += dS^T Q~
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pack8(sacc, s), tr_read_perm(L.dout, qt * TQ + 16 * s, lane), dv, 0, 0, 0);
+            dk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pack8(dp, s), tr_read_perm(L.q, qt * TQ + 16 * s, lane), dk, 0, 0, 0);
+          }
+          // dS -> global scratch (bias gradient) and LDS transpose image T[key][query]
+          {
+            bf16x8 lo = pack8(dp, 0), hi = pack8(dp, 1);
+            bf16* o = dsp + (qt * NTILE + kt) * TILE_ELEMS;
+            *reinterpret_cast<bf16x8*>(o) = lo;
+            *reinterpret_cast<bf16x8*>(o + 8) = hi;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              bf16x4 v;
+              v[0] = f2bf(dp[4 * rr]); v[1] = f2bf(dp[4 * rr + 1]); v[2] = f2bf(dp[4 * rr + 2]); v[3] = f2bf(dp[4 * rr + 3]);
+              *reinterpret_cast<bf16x4*>(L.t + r32 * TQ + 8 * rr + 4 * hh) = v;
+            }
+          }
+          wave_lds_fence();
+          // dQ[qt] += dS K : A = dS rows (from T, transposed read), B = K rows (transposed read)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 a = tr_read_nat(L.t, 16 * s, lane);
+            const bf16x8 b = tr_read_nat(L.k, kt * TQ + 16 * s, lane);
+            dq[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, dq[qt], 0, 0, 0);
+          }
+          wave_lds_fence();
+        }
+      }
+      // write dK, dV rows (keys) of this tile: rows = crow(r,hh), col = d = r32
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kk = kt * TQ + crow(r, hh);
+        if (kk < n) {
+          bf16* row = dqkv + ((long long)w * n + kk) * ld + h * HD + r32;
+          row[C] = f2bf(dk[r] * kscale);
+          row[2 * C] = f2bf(dv[r]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < NTILE; ++qt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = qt * TQ + crow(r, hh);
+      if (qi < n) dqkv[((long long)w * n + qi) * ld + h * HD + r32] = f2bf(dq[qt][r] * scale);
+    }
+  }
+}
+
+// sum dS over windows (per head, per padded (q,k)) and scatter-add into the bias table gradient
+__global__ void dbias_kernel(const bf16* __restrict__ ds, int n_win, int n, int nH, const int64_t* __restrict__ index,
+                             int ld, float* __restrict__ tgrad) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)nH * PH_ELEMS) return;
+  const int h = e / PH_ELEMS, el = e % PH_ELEMS;
+  const int reg = el & 15, lane = (el >> 4) & 63, tile = el / TILE_ELEMS;
+  const int qt = tile / NTILE, kt = tile % NTILE;
+  const int qi = qt * TQ + crow(reg, lane >> 5), kj = kt * TQ + (lane & 31);
+  if (qi >= n || kj >= n) return;
+  float s = 0.f;
+  const bf16* p = ds + (long long)h * PH_ELEMS + el;
+  const long long stride = (long long)nH * PH_ELEMS;
+  for (int w = 0; w < n_win; ++w) s += bf2f(p[w * stride]);
+  atomicAdd(tgrad + index[(long long)qi * ld + kj] * nH + h, s);
+}
+
+}  // namespace
+
+extern "C" int64_t lrce_wattn_bias_elems(int n_pat, int nH) { return (int64_t)n_pat * nH * PH_ELEMS; }
+extern "C" int64_t lrce_wattn_ds_elems(int n_win, int nH) { return (int64_t)n_win * nH * PH_ELEMS; }
+
+extern "C" int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
+                                     const int32_t* region, int n_pat, float* bias_fwd, float* bias_bwd, void* stream) {
+  if (!table || !index || !bias_fwd || !bias_bwd) return lrce_fail(LRCE_E_ARG, "wattn_bias_build: null pointer");
+  if (n <= 0 || n > NPAD || n_pat < 1 || nH < 1) return lrce_fail(LRCE_E_ARG, "wattn_bias_build: n=%d", n);
+  const long long total = (long long)n_pat * nH * PH_ELEMS;
+  bias_build_kernel<<<(total + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(table, index, index_ld, n, nH, region,
+                                                                                    n_pat, bias_fwd, bias_bwd);
+  return lrce_check_launch("wattn_bias_build");
+}
+
+extern "C" int lrce_wattn_fwd(const uint16_t* qkv, const float* bias_fwd, const int32_t* win_pat, uint16_t* out, float* lse,
+                              int n_win, int n, int nH, void* stream) {
+  if (!qkv || !bias_fwd || !out || !lse) return lrce_fail(LRCE_E_ARG, "wattn_fwd: null pointer");
+  if (n <= 4 * TQ || n > NPAD) return lrce_fail(LRCE_E_ARG, "wattn_fwd: n=%d outside (128,160]", n);
+  if (n_win <= 0) return LRCE_OK;
+  dim3 grid((n_win + 3) / 4, nH);
+  wattn_fwd_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const bf16*>(qkv), bias_fwd, win_pat,
+                                                                      reinterpret_cast<bf16*>(out), lse, n_win, n, nH);
+  return lrce_check_launch("wattn_fwd");
+}
+
+extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                              const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv, uint16_t* ds_scratch, int n_win,
+                              int n, int nH, void* stream) {
+  if (!qkv || !out || !dout || !lse || !bias_bwd || !dqkv || !ds_scratch) return lrce_fail(LRCE_E_ARG, "wattn_bwd: null pointer");
+  if (n <= 4 * TQ || n > NPAD) return lrce_fail(LRCE_E_ARG, "wattn_bwd: n=%d outside (128,160]", n);
+  if (n_win <= 0) return LRCE_OK;
+  dim3 grid((n_win + 1) / 2, nH);
+  const float scale = 1.0f / sqrtf((float)HD);
+  wattn_bwd_kernel<<<grid, 128, 0, static_cast<hipStream_t>(stream)>>>(
+      reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const bf16*>(out), reinterpret_cast<const bf16*>(dout), lse, bias_bwd,
+      win_pat, reinterpret_cast<bf16*>(dqkv), reinterpret_cast<bf16*>(ds_scratch), n_win, n, nH, scale);
+  return lrce_check_launch("wattn_bwd");
+}
+
+extern "C" int lrce_wattn_dbias(const uint16_t* ds_scratch, int n_win, int n, int nH, const int64_t* index, int index_ld,
+                                float* table_grad, void* stream) {
+  if (!ds_scratch || !index || !table_grad) return lrce_fail(LRCE_E_ARG, "wattn_dbias: null pointer");
+  const long long total = (long long)nH * PH_ELEMS;
+  dbias_kernel<<<(total + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const bf16*>(ds_scratch), n_win,
+                                                                                   n, nH, index, index_ld, table_grad);
+  return lrce_check_launch("wattn_dbias");
+}

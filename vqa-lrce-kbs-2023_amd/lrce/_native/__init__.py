@@ -1,0 +1,116 @@
+"""ctypes binding of liblrce_hip.so (C ABI declared in include/lrce_hip.h).
+
+The product path calls ONLY these functions for compute; there is no eager/PyTorch fallback.  If
+the library (or a GPU) is missing every entry point raises immediately.  Tensors are passed as
+raw device pointers; the stream is torch's current HIP stream for the tensor's device.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblrce_hip.so")
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"liblrce_hip.so not built ({LIB_PATH}); run `python __graft_entry__.py` / make -C csrc")
+        _lib = ctypes.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+def loaded():
+    return _lib is not None
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("a", ctypes.c_void_p), ("b", ctypes.c_void_p), ("c", ctypes.c_void_p),
+        ("lda", ctypes.c_int64), ("ldb", ctypes.c_int64), ("ldc", ctypes.c_int64),
+        ("stride_a", ctypes.c_int64), ("stride_b", ctypes.c_int64), ("stride_c", ctypes.c_int64),
+        ("m", ctypes.c_int32), ("n", ctypes.c_int32), ("k", ctypes.c_int32), ("batch", ctypes.c_int32),
+        ("a_kmajor", ctypes.c_int32), ("b_kmajor", ctypes.c_int32), ("a_f32", ctypes.c_int32),
+        ("flags", ctypes.c_int32), ("split_k", ctypes.c_int32),
+        ("bias", ctypes.c_void_p), ("aux", ctypes.c_void_p), ("ld_aux", ctypes.c_int64),
+        ("aux_out", ctypes.c_void_p), ("ld_aux_out", ctypes.c_int64),
+        ("a_map", ctypes.c_void_p), ("c_map", ctypes.c_void_p),
+        ("alpha", ctypes.c_float), ("scale_cols", ctypes.c_int32), ("scale_val", ctypes.c_float),
+        ("row_scale", ctypes.c_void_p), ("rows_per_scale", ctypes.c_int32),
+        ("a_row_scale", ctypes.c_void_p), ("a_rows_per_scale", ctypes.c_int32),
+    ]
+
+
+EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = 1, 2, 4, 8
+EPI_OUT_F32, EPI_ATOMIC, EPI_ACCUM, EPI_AUX_OUT, EPI_OUT_BOTH = 16, 32, 64, 128, 256
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+_U64 = ctypes.c_uint64
+
+_SIGS = {
+    "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
+    "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _I, _I, _P],
+    "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
+    "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _P, _P],
+    "lrce_wattn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lrce_wattn_dbias": [_P, _I, _I, _I, _P, _I, _P, _P],
+    "lrce_mha_fwd": [_P, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _I, _I, _I, _I, _I, _F, _P],
+    "lrce_mha_bwd": [_P, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I64,
+                     _I, _I, _I, _I, _I, _F, _P],
+    "lrce_patch_im2col": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _P],
+    "lrce_cast_bf16": [_P, _P, _I64, _P],
+    "lrce_dropout": [_P, _P, _P, _I64, _F, _U64, _P],
+    "lrce_dropout_bwd": [_P, _P, _I64, _F, _U64, _P],
+    "lrce_bert_embed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lrce_bert_embed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lrce_video_posembed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lrce_video_posembed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lrce_text_posembed_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
+    "lrce_text_posembed_bwd": [_P, _P, _P, _P, _I, _I, _I, _P],
+    "lrce_l2norm_multi": [_P, _P, _I, _P, _I, _P],
+    "lrce_adamw_step": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _F, _P],
+    "lrce_version": [],
+    "lrce_last_error": [],
+}
+_RET = {"lrce_last_error": ctypes.c_char_p, "lrce_wattn_bias_elems": _I64, "lrce_wattn_ds_elems": _I64}
+_SIGS["lrce_wattn_bias_elems"] = [_I, _I]
+_SIGS["lrce_wattn_ds_elems"] = [_I, _I]
+
+
+def _declare(L):
+    for name, args in _SIGS.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = _RET.get(name, ctypes.c_int)
+
+
+def exported_symbols():
+    return sorted(_SIGS)
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise NativeError(f"{name} failed ({rc}): {lib().lrce_last_error().decode()}")

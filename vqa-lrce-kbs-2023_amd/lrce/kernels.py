@@ -1,0 +1,244 @@
+"""Tensor-level wrappers over the C ABI (lrce._native).  Every function here launches hand-written
+gfx950 kernels from liblrce_hip.so on the current HIP stream; none computes with PyTorch.
+
+Conventions: activations are 2-D row-major [rows, features]; weights are nn.Linear layout
+[out, in]; "bf16" tensors are torch.bfloat16; gradients of parameters are f32 and accumulated.
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _native as N
+from ._native import ptr, stream_of, call
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+NUM_CU = 256
+
+
+def _chk(t, dtype=None, name="tensor"):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise N.NativeError(f"{name} must be a HIP device tensor (no CPU fallback on the product path)")
+    if dtype is not None and t.dtype != dtype:
+        raise N.NativeError(f"{name}: expected {dtype}, got {t.dtype}")
+
+
+def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, flags=0, bias=None,
+         aux=None, ld_aux=0, aux_out=None, ld_aux_out=0, a_map=None, c_map=None, alpha=1.0, split_k=1,
+         scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, a_row_scale=None, a_rows_per_scale=1,
+         batch=1, stride_a=0, stride_b=0, stride_c=0):
+    """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc."""
+    _chk(a, None, "A"); _chk(b, BF16, "B"); _chk(c, None, "C")
+    a_f32 = a.dtype == F32
+    if not a_f32 and a.dtype != BF16:
+        raise N.NativeError("gemm: A must be bf16 or f32")
+    if lda is None:
+        lda = k if a_kmajor else m
+    if ldb is None:
+        ldb = k if b_kmajor else n
+    if ldc is None:
+        ldc = n
+    d = N.GemmDesc()
+    d.a, d.b, d.c = ptr(a), ptr(b), ptr(c)
+    d.lda, d.ldb, d.ldc = lda, ldb, ldc
+    d.stride_a, d.stride_b, d.stride_c = stride_a, stride_b, stride_c
+    d.m, d.n, d.k, d.batch = m, n, k, batch
+    d.a_kmajor, d.b_kmajor, d.a_f32 = int(a_kmajor), int(b_kmajor), int(a_f32)
+    d.flags, d.split_k = flags, split_k
+    d.bias, d.aux, d.ld_aux = ptr(bias), ptr(aux), ld_aux
+    d.aux_out, d.ld_aux_out = ptr(aux_out), ld_aux_out
+    d.a_map, d.c_map = ptr(a_map), ptr(c_map)
+    d.alpha, d.scale_cols, d.scale_val = alpha, scale_cols, scale_val
+    d.row_scale, d.rows_per_scale = ptr(row_scale), rows_per_scale
+    d.a_row_scale, d.a_rows_per_scale = ptr(a_row_scale), a_rows_per_scale
+    call("lrce_gemm", ctypes.byref(d), stream_of(c))
+
+
+def _split_for(m_out, n_out, k_red):
+    tiles = math.ceil(m_out / 128) * math.ceil(n_out / 128)
+    want = max(1, (2 * NUM_CU * 2) // tiles)
+    return int(max(1, min(want, k_red // 512)))
+
+
+def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None, resid=None, c_map=None,
+           a_map=None, rows=None, scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, bf16_shadow=None):
+    """y = x W^T (+b) [gelu] [*row_scale] [+resid]; x [M,K] bf16/f32, W [N,K] bf16."""
+    M = rows if rows is not None else x.shape[0]
+    K = x.shape[-1]
+    Nn = w.shape[0]
+    flags = 0
+    if bias is not None:
+        flags |= N.EPI_BIAS
+    if gelu:
+        flags |= N.EPI_GELU
+        if pre_out is not None:
+            flags |= N.EPI_AUX_OUT
+    if resid is not None:
+        flags |= N.EPI_RESID
+    if out is None:
+        out = torch.empty((M if c_map is None else resid.shape[0] if resid is not None else M, Nn),
+                          dtype=F32 if out_f32 else BF16, device=x.device)
+    if out.dtype == F32:
+        flags |= N.EPI_OUT_F32
+        if bf16_shadow is not None:
+            flags |= N.EPI_OUT_BOTH
+    aux = resid
+    aux_out = pre_out if gelu else bf16_shadow
+    gemm(x, w, out, M, Nn, K, flags=flags, bias=bias, aux=aux, ld_aux=Nn, aux_out=aux_out, ld_aux_out=Nn,
+         a_map=a_map, c_map=c_map, scale_cols=scale_cols, scale_val=scale_val, row_scale=row_scale,
+         rows_per_scale=rows_per_scale)
+    return out
+
+
+def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows=None, a_row_scale=None,
+              a_rows_per_scale=1, accumulate=False):
+    """dX = dY W ; dY [M,N] (bf16/f32), W [N,K] bf16 -> [M,K]; optional *gelu'(pre)."""
+    M = rows if rows is not None else dy.shape[0]
+    Nn, K = w.shape
+    flags = 0
+    if dgelu_pre is not None:
+        flags |= N.EPI_DGELU
+    if out is None:
+        out = torch.empty((M, K), dtype=F32 if out_f32 else BF16, device=dy.device)
+    if out.dtype == F32:
+        flags |= N.EPI_ACCUM if accumulate else N.EPI_OUT_F32
+    gemm(dy, w, out, M, K, Nn, a_kmajor=True, b_kmajor=False, lda=dy.shape[-1], ldb=K, flags=flags,
+         aux=dgelu_pre, ld_aux=K, a_map=a_map, a_row_scale=a_row_scale, a_rows_per_scale=a_rows_per_scale)
+    return out
+
+
+def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_scale=1):
+    """dW[N,K] += dY^T X ; dY [M,N] (bf16/f32, rows optionally gathered by a_map), X [M,K] bf16."""
+    M = rows if rows is not None else x.shape[0]
+    Nn = dw.shape[0]
+    K = dw.shape[1]
+    split = _split_for(Nn, K, M)
+    gemm(dy, x, dw, Nn, K, M, a_kmajor=False, b_kmajor=False, lda=dy.shape[-1], ldb=x.shape[-1], ldc=K,
+         flags=N.EPI_ATOMIC, a_map=a_map, split_k=split, a_row_scale=a_row_scale, a_rows_per_scale=a_rows_per_scale)
+
+
+def colsum(x, out, *, row_map=None, rows=None):
+    M = rows if rows is not None else x.shape[0]
+    call("lrce_colsum", ptr(x), int(x.dtype == F32), ptr(row_map), x.shape[-1], M, x.shape[-1], ptr(out), stream_of(out))
+
+
+def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out_map=None, rows=None, cols=None,
+              stats=True, out_rows=None):
+    R = rows if rows is not None else x.shape[0]
+    Cc = cols if cols is not None else x.shape[-1] * nseg
+    if out is None:
+        out = torch.empty((out_rows or R, Cc), dtype=F32 if out_f32 else BF16, device=x.device)
+    mean = torch.empty(R, dtype=F32, device=x.device) if stats else None
+    rstd = torch.empty(R, dtype=F32, device=x.device) if stats else None
+    call("lrce_layernorm_fwd", ptr(x), int(x.dtype == F32), ptr(in_map), nseg, ptr(w), ptr(b), eps, ptr(out),
+         int(out.dtype == F32), ptr(out_map), ptr(mean), ptr(rstd), R, Cc, stream_of(out))
+    return out, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1, dres=None, dw=None, db=None,
+                  rows=None, cols=None):
+    R = rows if rows is not None else mean.shape[0]
+    Cc = cols if cols is not None else w.shape[0]
+    call("lrce_layernorm_bwd", ptr(dy), int(dy.dtype == F32), ptr(dy_map), ptr(x), int(x.dtype == F32), ptr(in_map),
+         nseg, ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dres), ptr(dw), ptr(db), R, Cc, stream_of(dx))
+    return dx
+
+
+def wattn_bias_elems(n_pat, nH):
+    return N.lib().lrce_wattn_bias_elems(n_pat, nH)
+
+
+def wattn_bias_build(table, index, n, nH, region, n_pat, bias_fwd, bias_bwd):
+    call("lrce_wattn_bias_build", ptr(table), ptr(index), index.shape[-1], n, nH, ptr(region), n_pat,
+         ptr(bias_fwd), ptr(bias_bwd), stream_of(bias_fwd))
+
+
+def wattn_fwd(qkv, bias_fwd, win_pat, out, lse, n_win, n, nH):
+    call("lrce_wattn_fwd", ptr(qkv), ptr(bias_fwd), ptr(win_pat), ptr(out), ptr(lse), n_win, n, nH, stream_of(out))
+
+
+def wattn_bwd(qkv, out, dout, lse, bias_bwd, win_pat, dqkv, ds, n_win, n, nH):
+    call("lrce_wattn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(bias_bwd), ptr(win_pat), ptr(dqkv), ptr(ds),
+         n_win, n, nH, stream_of(dqkv))
+
+
+def wattn_ds_elems(n_win, nH):
+    return N.lib().lrce_wattn_ds_elems(n_win, nH)
+
+
+def wattn_dbias(ds, n_win, n, nH, index, table_grad):
+    call("lrce_wattn_dbias", ptr(ds), n_win, n, nH, ptr(index), index.shape[-1], ptr(table_grad), stream_of(table_grad))
+
+
+def mha_fwd(q, ld_q, k, v, ld_kv, stride_kv_b, key_mask, out, ld_o, lse, B, H, Lq, Lk, d, scale):
+    call("lrce_mha_fwd", ptr(q), ld_q, ptr(k), ptr(v), ld_kv, stride_kv_b, ptr(key_mask), ptr(out), ld_o, ptr(lse),
+         B, H, Lq, Lk, d, scale, stream_of(out))
+
+
+def mha_bwd(q, ld_q, k, v, ld_kv, stride_kv_b, key_mask, out, ld_o, dout, lse, dq, ld_dq, dk, dv, ld_dkv,
+            stride_dkv_b, B, H, Lq, Lk, d, scale):
+    call("lrce_mha_bwd", ptr(q), ld_q, ptr(k), ptr(v), ld_kv, stride_kv_b, ptr(key_mask), ptr(out), ld_o, ptr(dout),
+         ptr(lse), ptr(dq), ld_dq, ptr(dk), ptr(dv), ld_dkv, stride_dkv_b, B, H, Lq, Lk, d, scale, stream_of(dq))
+
+
+def patch_im2col(clips, patches):
+    B, S, T, C, H, W = clips.shape
+    call("lrce_patch_im2col", ptr(clips), ptr(patches), B, S, T, H, W, stream_of(patches))
+
+
+def cast_bf16(x, y):
+    call("lrce_cast_bf16", ptr(x), ptr(y), x.numel(), stream_of(y))
+
+
+def dropout(x, p, seed, out=None, out_bf16=None):
+    if out is None:
+        out = torch.empty_like(x)
+    call("lrce_dropout", ptr(x), ptr(out), ptr(out_bf16), x.numel(), float(p), seed & (2 ** 64 - 1), stream_of(out))
+    return out
+
+
+def dropout_bwd(dy, p, seed, out=None):
+    if out is None:
+        out = torch.empty_like(dy)
+    call("lrce_dropout_bwd", ptr(dy), ptr(out), dy.numel(), float(p), seed & (2 ** 64 - 1), stream_of(out))
+    return out
+
+
+def bert_embed_fwd(ids, types, word, pos, typ, out, rows, L, C):
+    call("lrce_bert_embed_fwd", ptr(ids), ptr(types), ptr(word), ptr(pos), ptr(typ), ptr(out), rows, L, C, stream_of(out))
+
+
+def bert_embed_bwd(dout, ids, types, dword, dpos, dtyp, rows, L, C):
+    call("lrce_bert_embed_bwd", ptr(dout), ptr(ids), ptr(types), ptr(dword), ptr(dpos), ptr(dtyp), rows, L, C,
+         stream_of(dout))
+
+
+def video_posembed_fwd(x, cls, pos, len_, clip, out, B, S, Tg, P, C):
+    call("lrce_video_posembed_fwd", ptr(x), ptr(cls), ptr(pos), ptr(len_), ptr(clip), ptr(out), B, S, Tg, P, C,
+         stream_of(out))
+
+
+def video_posembed_bwd(dout, dx, dcls, dpos, dlen, dclip, B, S, Tg, P, C):
+    call("lrce_video_posembed_bwd", ptr(dout), ptr(dx), ptr(dcls), ptr(dpos), ptr(dlen), ptr(dclip), B, S, Tg, P, C,
+         stream_of(dout))
+
+
+def text_posembed_fwd(x, cls, pos, out, B, L, C):
+    call("lrce_text_posembed_fwd", ptr(x), ptr(cls), ptr(pos), ptr(out), B, L, C, stream_of(out))
+
+
+def text_posembed_bwd(dout, dx, dcls, dpos, B, L, C):
+    call("lrce_text_posembed_bwd", ptr(dout), ptr(dx), ptr(dcls), ptr(dpos), B, L, C, stream_of(dout))
+
+
+def l2norm_multi(p, chunk_tensor, n_chunks, sumsq, n_tensors):
+    call("lrce_l2norm_multi", ptr(p), ptr(chunk_tensor), n_chunks, ptr(sumsq), n_tensors, stream_of(p))
+
+
+def adamw_step(p, g, m, v, chunk_tensor, tensor_lr, sumsq, p_bf16, n_chunks, beta1, beta2, eps, wd, grad_scale, reg,
+               bc1, bc2):
+    call("lrce_adamw_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(chunk_tensor), ptr(tensor_lr), ptr(sumsq), ptr(p_bf16),
+         n_chunks, beta1, beta2, eps, wd, grad_scale, reg, bc1, bc2, stream_of(p))
