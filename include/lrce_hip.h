@@ -141,12 +141,17 @@ int lrce_mha_bwd(const uint16_t* q, int64_t ld_q, const uint16_t* k, const uint1
                  void* stream);
 
 /* ---------------------------------------------------------------- elementwise / data movement */
-/* Normalize (video.py:35) + zero-pad T to a multiple of 2 (video_swin_ori.py:472-473) + im2col of
- * the (2,4,4) patches: clips f32 [B][S][T][3][H][W] -> patches bf16 [(B*S)*D'*H'*W'][96], rows
- * ordered (b, s, d, h, w) (all B*S clips form one Swin batch, video.py:33-42), cols (c, kt, kh, kw). */
-int lrce_patch_im2col(const float* clips, uint16_t* patches, int B, int S, int T, int H, int W, void* stream);
-/* column sums: out[n] (+)= sum_m x[m][n] (x f32 or bf16, optional row map): bias gradients */
-int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, int m, int n, float* out, void* stream);
+/* Patch-embed input stage: [ImageNet Normalize (video.py:35)] + zero-pad T to a multiple of 2
+ * (video_swin_ori.py:472-473) + im2col of the non-overlapping (2,4,4) patches of conv3d (:458,475).
+ * Clip n, frame t, channel c lives at clips[n*s_clip + t*s_t + c*s_c] (rows of W floats, H rows):
+ * (B,S,T,3,H,W) clips -> s_clip=T*3*H*W, s_t=3*H*W, s_c=H*W; (B,3,T,H,W) -> 3*T*H*W, H*W, T*H*W.
+ * patches: bf16 [n_clips*D'*H'*W'][96], rows (n, d, h, w), cols (c, kt, kh, kw). */
+int lrce_patch_im2col(const float* clips, int n_clips, int T, int H, int W, int64_t s_clip, int64_t s_t, int64_t s_c,
+                      int normalize, uint16_t* patches, void* stream);
+/* column sums: out[n] += sum_m x[row_map[m]][n] * row_scale[m / rows_per_scale] (x f32 or bf16; map and
+ * scale optional): bias gradients (nn.Linear bias, incl. DropPath-scaled branches) */
+int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, int m, int n, const float* row_scale,
+                int rows_per_scale, float* out, void* stream);
 /* f32 -> bf16 cast (n elements) */
 int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
 /* y = x * keep / (1-p) with keep ~ Bernoulli(1-p) from a counter hash (seed, offset); p=0 copies.

@@ -227,6 +227,9 @@ def test_patch_im2col_matches_conv():
     Dp = (T + 1) // 2
     patches = torch.empty(B * S * Dp * (H // 4) * (W // 4), 96, device=dev, dtype=torch.bfloat16)
     k.patch_im2col(clips, patches)
+    p2 = torch.empty_like(patches)
+    k.patch_im2col(O.normalize_clip(clips.cpu()).to(dev).flatten(0, 1).transpose(1, 2).contiguous(), p2, layout='BCTHW', normalize=False)
+    assert rel(p2, patches) < 1e-2
     wconv = torch.randn(128, 3, 2, 4, 4, device=dev)
     x = O.normalize_clip(clips.cpu()).to(dev).flatten(0, 1).transpose(1, 2)
     x = F.pad(x, (0, 0, 0, 0, 0, T % 2))

@@ -7,30 +7,33 @@
 namespace {
 
 // ---------------------------------------------------------------- patch im2col
-// clips f32 [B][S][T][3][H][W] -> patches bf16 [(b*S + s)*Dp*Hp*Wp + (d*Hp + h)*Wp + w][96],
-// column = c*32 + kt*16 + kh*4 + kw (conv3d weight [128][3][2][4][4] flattened).
-// Normalize (video.py:35) precedes the T padding (video_swin_ori.py:472-473): padded frames are 0.
-__global__ void im2col_kernel(const float* __restrict__ clips, bf16* __restrict__ out, int B, int S, int T, int H, int W) {
+// clip n, frame t, channel c at clips[n*s_clip + t*s_t + c*s_c + y*W + x] (f32) ->
+// patches bf16 [(n*Dp + d)*Hp*Wp + h*Wp + w][96], column = c*32 + kt*16 + kh*4 + kw (the conv3d
+// weight [128][3][2][4][4] flattened).  Normalize (video.py:35, if `normalize`) precedes the zero
+// padding of T to a multiple of 2 (video_swin_ori.py:472-473): padded frames are exactly 0.
+__global__ void im2col_kernel(const float* __restrict__ clips, bf16* __restrict__ out, int n_clips, int T, int H, int W,
+                              long long s_clip, long long s_t, long long s_c, int normalize) {
   const int Dp = (T + 1) / 2, Hp = H / 4, Wp = W / 4;
   const long long tok = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const long long ntok = (long long)S * B * Dp * Hp * Wp;
+  const long long ntok = (long long)n_clips * Dp * Hp * Wp;
   if (tok >= ntok) return;
   const int lane = threadIdx.x & 63;
-  // lane < 24: one (c, kt, kh) row of 4 kw values
-  if (lane >= 24) return;
+  if (lane >= 24) return;  // lane = (c, kt, kh): one row of 4 kw values
   long long t = tok;
   const int w = t % Wp; t /= Wp;
   const int h = t % Hp; t /= Hp;
-  const int d = t % Dp; t /= Dp;
-  const int s = t % S;
-  const int b = t / S;
+  const int d = t % Dp;
+  const long long n = t / Dp;
   const int c = lane >> 3, kt = (lane >> 2) & 1, kh = lane & 3;
   const int frame = 2 * d + kt;
-  const float mean = c == 0 ? 0.485f : (c == 1 ? 0.456f : 0.406f);
-  const float istd = c == 0 ? 1.0f / 0.229f : (c == 1 ? 1.0f / 0.224f : 1.0f / 0.225f);
+  float mean = 0.f, istd = 1.f;
+  if (normalize) {
+    mean = c == 0 ? 0.485f : (c == 1 ? 0.456f : 0.406f);
+    istd = c == 0 ? 1.0f / 0.229f : (c == 1 ? 1.0f / 0.224f : 1.0f / 0.225f);
+  }
   bf16x4 o;
   if (frame < T) {
-    const float* src = clips + ((((long long)b * S + s) * T + frame) * 3 + c) * H * W + (long long)(4 * h + kh) * W + 4 * w;
+    const float* src = clips + n * s_clip + frame * s_t + c * s_c + (long long)(4 * h + kh) * W + 4 * w;
     const float4 v = *reinterpret_cast<const float4*>(src);
     o[0] = f2bf((v.x - mean) * istd); o[1] = f2bf((v.y - mean) * istd);
     o[2] = f2bf((v.z - mean) * istd); o[3] = f2bf((v.w - mean) * istd);
@@ -42,7 +45,8 @@ __global__ void im2col_kernel(const float* __restrict__ clips, bf16* __restrict_
 
 // ---------------------------------------------------------------- column sums
 template <typename T>
-__global__ void colsum_kernel(const T* __restrict__ x, const int* __restrict__ map, long long ld, int m, int n, float* __restrict__ out) {
+__global__ void colsum_kernel(const T* __restrict__ x, const int* __restrict__ map, long long ld, int m, int n,
+                              const float* __restrict__ rsc, int rps, float* __restrict__ out) {
   // block: 256 threads = 64 columns x 4 row-groups; grid.x over column blocks, grid.y over row chunks
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rg = threadIdx.x >> 6;
@@ -52,7 +56,8 @@ __global__ void colsum_kernel(const T* __restrict__ x, const int* __restrict__ m
   if (col < n)
     for (int r = r0 + rg; r < r1; r += 4) {
       const long long rr = map ? (long long)map[r] : (long long)r;
-      s += (float)x[rr * ld + col];
+      const float f = rsc ? rsc[r / rps] : 1.0f;
+      s += (float)x[rr * ld + col] * f;
     }
   __shared__ float red[4][64];
   red[rg][threadIdx.x & 63] = s;
@@ -190,23 +195,27 @@ __global__ void text_pos_bwd_kernel(const float* __restrict__ d, float* __restri
 
 }  // namespace
 
-extern "C" int lrce_patch_im2col(const float* clips, uint16_t* patches, int B, int S, int T, int H, int W, void* stream) {
+extern "C" int lrce_patch_im2col(const float* clips, int n_clips, int T, int H, int W, int64_t s_clip, int64_t s_t,
+                                 int64_t s_c, int normalize, uint16_t* patches, void* stream) {
   if (!clips || !patches) return lrce_fail(LRCE_E_ARG, "patch_im2col: null pointer");
-  if (H % 4 || W % 4 || T < 1) return lrce_fail(LRCE_E_ARG, "patch_im2col: H,W must be multiples of 4");
-  const long long ntok = (long long)S * B * ((T + 1) / 2) * (H / 4) * (W / 4);
-  im2col_kernel<<<(ntok + 3) / 4, 256, 0, static_cast<hipStream_t>(stream)>>>(clips, reinterpret_cast<bf16*>(patches), B, S, T, H, W);
+  if (H % 4 || W % 4 || T < 1 || n_clips < 1) return lrce_fail(LRCE_E_ARG, "patch_im2col: H,W must be multiples of 4");
+  const long long ntok = (long long)n_clips * ((T + 1) / 2) * (H / 4) * (W / 4);
+  im2col_kernel<<<(ntok + 3) / 4, 256, 0, static_cast<hipStream_t>(stream)>>>(clips, reinterpret_cast<bf16*>(patches), n_clips, T,
+                                                                            H, W, s_clip, s_t, s_c, normalize);
   return lrce_check_launch("patch_im2col");
 }
 
-extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, int m, int n, float* out, void* stream) {
+extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, int m, int n, const float* row_scale,
+                           int rows_per_scale, float* out, void* stream) {
+  if (rows_per_scale < 1) rows_per_scale = 1;
   if (!x || !out) return lrce_fail(LRCE_E_ARG, "colsum: null pointer");
   if (m <= 0 || n <= 0) return LRCE_OK;
   int chunks = (m + 255) / 256;
   if (chunks > 256) chunks = 256;
   dim3 grid((n + 63) / 64, chunks);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (x_f32) colsum_kernel<float><<<grid, 256, 0, s>>>(static_cast<const float*>(x), row_map, ld, m, n, out);
-  else colsum_kernel<bf16><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), row_map, ld, m, n, out);
+  if (x_f32) colsum_kernel<float><<<grid, 256, 0, s>>>(static_cast<const float*>(x), row_map, ld, m, n, row_scale, rows_per_scale, out);
+  else colsum_kernel<bf16><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), row_map, ld, m, n, row_scale, rows_per_scale, out);
   return lrce_check_launch("colsum");
 }
 

@@ -70,8 +70,8 @@ _SIGS = {
     "lrce_mha_fwd": [_P, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _I, _I, _I, _I, _I, _F, _P],
     "lrce_mha_bwd": [_P, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I64,
                      _I, _I, _I, _I, _I, _F, _P],
-    "lrce_patch_im2col": [_P, _P, _I, _I, _I, _I, _I, _P],
-    "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _P],
+    "lrce_patch_im2col": [_P, _I, _I, _I, _I, _I64, _I64, _I64, _I, _P, _P],
+    "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _I, _P, _P],
     "lrce_cast_bf16": [_P, _P, _I64, _P],
     "lrce_dropout": [_P, _P, _P, _I64, _F, _U64, _P],
     "lrce_dropout_bwd": [_P, _P, _I64, _F, _U64, _P],

@@ -1,0 +1,454 @@
+"""Video Swin Transformer 3D (Swin-B, patch 2x4x4, window 8x7x7) on the gfx950 kernels.
+
+Re-designed from lrce/feature_extractor/video_swin_ori.py of the reference (a port of the official
+Video-Swin-Transformer): same module tree and state-dict keys (`patch_embed.proj/norm`,
+`layers.i.blocks.j.{norm1,attn.{relative_position_bias_table,relative_position_index,qkv,proj},
+norm2,mlp.{fc1,fc2}}`, `layers.i.downsample.{norm,reduction}`, `norm`), same math, different
+execution:
+
+* activations are token-major 2-D tensors, residual stream in f32, GEMM operands in bf16;
+* torch.roll + window_partition / window_reverse (video_swin_ori.py:60-88,262,276) are index maps
+  (`win2sp`) fused into the LN1 gather and the proj-GEMM scatter epilogue — no copies;
+* the relative-position bias + shift mask (:171-179, 346-359) are pre-combined per mask pattern
+  into accumulator-order tiles that the fused window-attention kernel starts its MFMA chain from;
+* one autograd Function per block (forward 6 launches, backward 15) with gradients accumulated
+  straight into the flat parameter store (lrce/flat.py).
+"""
+import math
+from functools import lru_cache
+
+import torch
+import torch.nn as nn
+
+from .. import kernels as K
+from ..runtime import ensure
+
+LOG2E = 1.4426950408889634
+
+
+def get_window_size(x_size, window_size, shift_size=None):
+    """video_swin_ori.py:91-104: a dim no larger than the window uses the whole dim, zero shift."""
+    ws = list(window_size)
+    ss = list(shift_size) if shift_size is not None else None
+    for i in range(len(x_size)):
+        if x_size[i] <= window_size[i]:
+            ws[i] = x_size[i]
+            if ss is not None:
+                ss[i] = 0
+    return tuple(ws) if ss is None else (tuple(ws), tuple(ss))
+
+
+def relative_position_index(window):
+    """Pairwise index into the (2Wd-1)(2Wh-1)(2Ww-1) bias table (video_swin_ori.py:133-148)."""
+    wd, wh, ww = window
+    g = torch.stack(torch.meshgrid(torch.arange(wd), torch.arange(wh), torch.arange(ww), indexing="ij")).flatten(1)
+    rel = (g[:, :, None] - g[:, None, :]).permute(1, 2, 0) + torch.tensor([wd - 1, wh - 1, ww - 1])
+    return rel[..., 0] * ((2 * wh - 1) * (2 * ww - 1)) + rel[..., 1] * (2 * ww - 1) + rel[..., 2]
+
+
+# ----------------------------------------------------------------------------------- geometry
+class StageGeometry:
+    """Index maps for one stage at a given input size (cached per device)."""
+
+    def __init__(self, nc, D, H, W, window, device):
+        half = tuple(i // 2 for i in window)
+        ws, ss = get_window_size((D, H, W), window, half)
+        if D % ws[0] or H % ws[1] or W % ws[2]:
+            raise ValueError(f"Swin stage {D}x{H}x{W} needs window padding (unsupported; 224x224x(5|16) inputs never do)")
+        self.nc, self.D, self.H, self.W = nc, D, H, W
+        self.ws, self.ss = ws, ss
+        self.n = ws[0] * ws[1] * ws[2]
+        self.nW = (D // ws[0]) * (H // ws[1]) * (W // ws[2])
+        self.n_win = nc * self.nW
+        self.M = nc * D * H * W
+        self.rows_per_clip = D * H * W
+        self.win2sp = self._win_map((0, 0, 0), device)
+        self.shifted = any(s > 0 for s in ss)
+        if self.shifted:
+            self.win2sp_shift = self._win_map(ss, device)
+            self.region, self.win_pat, self.n_pat = self._mask_patterns(device)
+        self.merge_map = self._merge_map(device) if (H % 2 == 0 and W % 2 == 0) else None
+
+    def _win_map(self, shift, device):
+        D, H, W = self.D, self.H, self.W
+        wd, wh, ww = self.ws
+        ar = lambda n: torch.arange(n, device=device)
+        b, iwd, iwh, iww, td, th, tw = torch.meshgrid(ar(self.nc), ar(D // wd), ar(H // wh), ar(W // ww), ar(wd), ar(wh),
+                                                      ar(ww), indexing="ij")
+        d = (iwd * wd + td + shift[0]) % D
+        h = (iwh * wh + th + shift[1]) % H
+        w = (iww * ww + tw + shift[2]) % W
+        return (((b * D + d) * H + h) * W + w).reshape(-1).to(torch.int32).contiguous()
+
+    def _mask_patterns(self, device):
+        """Region labels of compute_mask (video_swin_ori.py:346-359) over the rolled volume, as
+        per-window region-id rows, de-duplicated into patterns (windows away from the rolled
+        border all share the all-zero pattern)."""
+        D, H, W = self.D, self.H, self.W
+        ws, ss = self.ws, self.ss
+        lab = torch.zeros(D, H, W, dtype=torch.int32)
+        cnt = 0
+        for sd in (slice(-ws[0]), slice(-ws[0], -ss[0]), slice(-ss[0], None)):
+            for sh in (slice(-ws[1]), slice(-ws[1], -ss[1]), slice(-ss[1], None)):
+                for sw in (slice(-ws[2]), slice(-ws[2], -ss[2]), slice(-ss[2], None)):
+                    lab[sd, sh, sw] = cnt
+                    cnt += 1
+        wd, wh, ww = ws
+        win = lab.view(D // wd, wd, H // wh, wh, W // ww, ww).permute(0, 2, 4, 1, 3, 5).reshape(-1, self.n)
+        patterns, inv = torch.unique(win, dim=0, return_inverse=True)
+        win_pat = inv.to(torch.int32).repeat(self.nc)
+        return patterns.to(torch.int32).contiguous().to(device), win_pat.contiguous().to(device), patterns.shape[0]
+
+    def _merge_map(self, device):
+        """PatchMerging concat order x0..x3 = (h,w) offsets (0,0),(1,0),(0,1),(1,1) (:333-337)."""
+        nc, D, H, W = self.nc, self.D, self.H, self.W
+        ar = lambda n: torch.arange(n, device=device)
+        b, d, i, j, s = torch.meshgrid(ar(nc), ar(D), ar(H // 2), ar(W // 2), ar(4), indexing="ij")
+        dh = torch.tensor([0, 1, 0, 1], device=device)[s]
+        dw = torch.tensor([0, 0, 1, 1], device=device)[s]
+        return (((b * D + d) * H + 2 * i + dh) * W + 2 * j + dw).reshape(-1).to(torch.int32).contiguous()
+
+
+_GEO_CACHE = {}
+
+
+def stage_geometry(nc, D, H, W, window, device):
+    key = (nc, D, H, W, tuple(window), str(device))
+    g = _GEO_CACHE.get(key)
+    if g is None:
+        if len(_GEO_CACHE) > 64:
+            _GEO_CACHE.clear()
+        g = _GEO_CACHE[key] = StageGeometry(nc, D, H, W, window, device)
+    return g
+
+
+def _g(flat, p):
+    return flat.g32(p) if p.requires_grad else None
+
+
+# ----------------------------------------------------------------------------------- modules
+class Mlp(nn.Module):
+    def __init__(self, in_features, hidden_features):
+        super().__init__()
+        self.fc1 = nn.Linear(in_features, hidden_features)
+        self.act = nn.GELU()
+        self.fc2 = nn.Linear(hidden_features, in_features)
+
+
+class WindowAttention3D(nn.Module):
+    def __init__(self, dim, window_size, num_heads):
+        super().__init__()
+        self.dim, self.window_size, self.num_heads = dim, window_size, num_heads
+        wd, wh, ww = window_size
+        self.relative_position_bias_table = nn.Parameter(torch.zeros((2 * wd - 1) * (2 * wh - 1) * (2 * ww - 1), num_heads))
+        nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
+        self.register_buffer("relative_position_index", relative_position_index(window_size))
+        self.qkv = nn.Linear(dim, 3 * dim)
+        self.proj = nn.Linear(dim, dim)
+
+
+class SwinTransformerBlock3D(nn.Module):
+    def __init__(self, dim, num_heads, window_size, shift_size, drop_path=0.0):
+        super().__init__()
+        self.dim, self.num_heads, self.window_size, self.shift_size = dim, num_heads, window_size, shift_size
+        self.drop_path = drop_path
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn = WindowAttention3D(dim, window_size, num_heads)
+        self.norm2 = nn.LayerNorm(dim)
+        self.mlp = Mlp(dim, 4 * dim)
+
+    def tensors(self):
+        return [p for p in self.parameters()]
+
+
+class PatchMerging(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        self.reduction = nn.Linear(4 * dim, 2 * dim, bias=False)
+        self.norm = nn.LayerNorm(4 * dim)
+
+
+class BasicLayer(nn.Module):
+    def __init__(self, dim, depth, num_heads, window_size, drop_path, downsample):
+        super().__init__()
+        self.window_size = window_size
+        self.shift_size = tuple(i // 2 for i in window_size)
+        self.blocks = nn.ModuleList([
+            SwinTransformerBlock3D(dim, num_heads, window_size, (0, 0, 0) if i % 2 == 0 else self.shift_size,
+                                   drop_path[i]) for i in range(depth)])
+        self.downsample = PatchMerging(dim) if downsample else None
+
+
+class PatchEmbed3D(nn.Module):
+    def __init__(self, patch_size=(2, 4, 4), in_chans=3, embed_dim=128):
+        super().__init__()
+        self.patch_size, self.embed_dim = patch_size, embed_dim
+        self.proj = nn.Conv3d(in_chans, embed_dim, kernel_size=patch_size, stride=patch_size)
+        self.norm = nn.LayerNorm(embed_dim)
+
+
+# ----------------------------------------------------------------------------------- autograd
+class _PatchEmbedFn(torch.autograd.Function):
+    """im2col(+normalize, +T pad) -> K=96 GEMM (+bias) -> LN(128); video_swin_ori.py:464-482."""
+
+    @staticmethod
+    def forward(ctx, clips, pe, flat, layout, normalize, *params):
+        if layout == "BSTCHW":
+            B, S, T, _, H, W = clips.shape
+            nc = B * S
+        else:
+            B, _, T, H, W = clips.shape
+            nc = B
+        clips = clips.contiguous()
+        Dp, Hp, Wp = (T + 1) // 2, H // 4, W // 4
+        M = nc * Dp * Hp * Wp
+        patches = torch.empty(M, 96, dtype=torch.bfloat16, device=clips.device)
+        K.patch_im2col(clips, patches, layout=layout, normalize=normalize)
+        w16 = flat.w16(pe.proj.weight).view(pe.embed_dim, 96)
+        y = K.linear(patches, w16, pe.proj.bias, out_f32=True)
+        x, mean, rstd = K.layernorm(y, pe.norm.weight, pe.norm.bias, 1e-5, out_f32=True)
+        ctx.pe, ctx.flat = pe, flat
+        ctx.patches, ctx.y, ctx.mean, ctx.rstd = patches, y, mean, rstd
+        ctx.shape = (nc, Dp, Hp, Wp)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        pe, flat = ctx.pe, ctx.flat
+        dy = torch.empty_like(ctx.y)
+        K.layernorm_bwd(dx.contiguous(), ctx.y, ctx.mean, ctx.rstd, pe.norm.weight, dy,
+                        dw=_g(flat, pe.norm.weight), db=_g(flat, pe.norm.bias))
+        gw = _g(flat, pe.proj.weight)
+        if gw is not None:
+            K.linear_dw(dy, ctx.patches, gw.view(pe.embed_dim, 96))
+        gb = _g(flat, pe.proj.bias)
+        if gb is not None:
+            K.colsum(dy, gb)
+        return (None,) * (5 + len(list(pe.parameters())))
+
+
+def _drop_path_scale(rate, nc, device, training):
+    if not training or rate <= 0.0:
+        return None
+    keep = 1.0 - rate
+    return torch.floor(keep + torch.rand(nc, device=device)) / keep
+
+
+class _SwinBlockFn(torch.autograd.Function):
+    """One SwinTransformerBlock3D (video_swin_ori.py:248-306) forward / backward."""
+
+    @staticmethod
+    def forward(ctx, x, blk, geo, flat, dp1, dp2, *params):
+        C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
+        at = blk.attn
+        shifted = geo.shifted and any(s > 0 for s in blk.shift_size)
+        wmap = geo.win2sp_shift if shifted else geo.win2sp
+        region, win_pat, n_pat = (geo.region, geo.win_pat, geo.n_pat) if shifted else (None, None, 1)
+        dev = x.device
+        bias_f = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev)
+        bias_b = torch.empty_like(bias_f)
+        K.wattn_bias_build(at.relative_position_bias_table, at.relative_position_index, n, nH, region, n_pat,
+                           bias_f, bias_b)
+        xw, m1, r1 = K.layernorm(x, blk.norm1.weight, blk.norm1.bias, 1e-5, in_map=wmap, rows=M)
+        c = (C // nH) ** -0.5 * LOG2E
+        qkv = K.linear(xw, flat.w16(at.qkv.weight), at.qkv.bias, scale_cols=C, scale_val=c)
+        o = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+        lse = torch.empty(geo.n_win, nH, 160, device=dev)
+        K.wattn_fwd(qkv, bias_f, win_pat, o, lse, geo.n_win, n, nH)
+        x_mid = torch.empty(M, C, device=dev)
+        K.linear(o, flat.w16(at.proj.weight), at.proj.bias, out=x_mid, resid=x, c_map=wmap, row_scale=dp1,
+                 rows_per_scale=geo.rows_per_clip)
+        h2, m2, r2 = K.layernorm(x_mid, blk.norm2.weight, blk.norm2.bias, 1e-5)
+        pre = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=dev)
+        g = K.linear(h2, flat.w16(blk.mlp.fc1.weight), blk.mlp.fc1.bias, gelu=True, pre_out=pre)
+        out = torch.empty(M, C, device=dev)
+        K.linear(g, flat.w16(blk.mlp.fc2.weight), blk.mlp.fc2.bias, out=out, resid=x_mid, row_scale=dp2,
+                 rows_per_scale=geo.rows_per_clip)
+        if any(t.requires_grad for t in (x,) + params):
+            ctx.save = (x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_b)
+            ctx.blk, ctx.geo, ctx.flat, ctx.dp1, ctx.dp2 = blk, geo, flat, dp1, dp2
+            ctx.wmap, ctx.win_pat = wmap, win_pat
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_b = ctx.save
+        blk, geo, flat, dp1, dp2, wmap = ctx.blk, ctx.geo, ctx.flat, ctx.dp1, ctx.dp2, ctx.wmap
+        at = blk.attn
+        C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
+        rpc = geo.rows_per_clip
+        dout = dout.contiguous()
+        # MLP branch: y = x_mid + s2 * fc2(gelu(fc1(LN2(x_mid))))
+        gw = _g(flat, blk.mlp.fc2.weight)
+        if gw is not None:
+            K.linear_dw(dout, g, gw, a_row_scale=dp2, a_rows_per_scale=rpc)
+        gb = _g(flat, blk.mlp.fc2.bias)
+        if gb is not None:
+            K.colsum(dout, gb, row_scale=dp2, rows_per_scale=rpc)
+        dpre = K.linear_dx(dout, flat.w16(blk.mlp.fc2.weight), out_f32=False, dgelu_pre=pre, a_row_scale=dp2,
+                           a_rows_per_scale=rpc)
+        del g, pre
+        gw = _g(flat, blk.mlp.fc1.weight)
+        if gw is not None:
+            K.linear_dw(dpre, h2, gw)
+        gb = _g(flat, blk.mlp.fc1.bias)
+        if gb is not None:
+            K.colsum(dpre, gb)
+        dh2 = K.linear_dx(dpre, flat.w16(blk.mlp.fc1.weight))
+        del dpre, h2
+        dx_mid = torch.empty_like(x_mid)
+        K.layernorm_bwd(dh2, x_mid, m2, r2, blk.norm2.weight, dx_mid, dres=dout,
+                        dw=_g(flat, blk.norm2.weight), db=_g(flat, blk.norm2.bias))
+        del dh2
+        # attention branch: x_mid = x + s1 * unwindow(proj(attn(qkv(LN1(window(x))))))
+        gw = _g(flat, at.proj.weight)
+        if gw is not None:
+            K.linear_dw(dx_mid, o, gw, a_map=wmap, a_row_scale=dp1, a_rows_per_scale=rpc)
+        gb = _g(flat, at.proj.bias)
+        if gb is not None:
+            K.colsum(dx_mid, gb, row_scale=dp1, rows_per_scale=rpc)
+        do = K.linear_dx(dx_mid, flat.w16(at.proj.weight), out_f32=False, a_map=wmap, rows=M, a_row_scale=dp1,
+                         a_rows_per_scale=rpc)
+        dqkv = torch.empty_like(qkv)
+        ds = torch.empty(K.wattn_ds_elems(geo.n_win, nH), dtype=torch.bfloat16, device=dout.device)
+        K.wattn_bwd(qkv, o, do, lse, bias_b, ctx.win_pat, dqkv, ds, geo.n_win, n, nH)
+        del do, o
+        gt = _g(flat, at.relative_position_bias_table)
+        if gt is not None:
+            K.wattn_dbias(ds, geo.n_win, n, nH, at.relative_position_index, gt)
+        del ds
+        gw = _g(flat, at.qkv.weight)
+        if gw is not None:
+            K.linear_dw(dqkv, xw, gw)
+        gb = _g(flat, at.qkv.bias)
+        if gb is not None:
+            K.colsum(dqkv, gb)
+        dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight))
+        del dqkv, qkv, xw
+        dx = torch.empty_like(x)
+        K.layernorm_bwd(dxw, x, m1, r1, blk.norm1.weight, dx, in_map=wmap, dres=dx_mid,
+                        dw=_g(flat, blk.norm1.weight), db=_g(flat, blk.norm1.bias))
+        ctx.save = None
+        return (dx, None, None, None, None, None) + (None,) * len(ctx.needs_input_grad[6:])
+
+
+class _PatchMergeFn(torch.autograd.Function):
+    """PatchMerging (video_swin_ori.py:321-342): 2x2 gather + LN(4C) fused, then the 4C->2C GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, pm, geo, flat, *params):
+        C = pm.dim
+        Mo = geo.M // 4
+        xl, mean, rstd = K.layernorm(x, pm.norm.weight, pm.norm.bias, 1e-5, in_map=geo.merge_map, nseg=4, rows=Mo,
+                                     cols=4 * C)
+        y = K.linear(xl, flat.w16(pm.reduction.weight), out_f32=True)
+        ctx.save = (x, xl, mean, rstd)
+        ctx.pm, ctx.geo, ctx.flat = pm, geo, flat
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, xl, mean, rstd = ctx.save
+        pm, geo, flat = ctx.pm, ctx.geo, ctx.flat
+        dy = dy.contiguous()
+        gw = _g(flat, pm.reduction.weight)
+        if gw is not None:
+            K.linear_dw(dy, xl, gw)
+        dxl = K.linear_dx(dy, flat.w16(pm.reduction.weight))
+        dx = torch.empty_like(x)
+        K.layernorm_bwd(dxl, x, mean, rstd, pm.norm.weight, dx, in_map=geo.merge_map, nseg=4, rows=geo.M // 4,
+                        cols=4 * pm.dim, dw=_g(flat, pm.norm.weight), db=_g(flat, pm.norm.bias))
+        ctx.save = None
+        return (dx, None, None, None) + (None,) * len(ctx.needs_input_grad[4:])
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ln, flat, eps, *params):
+        y, mean, rstd = K.layernorm(x, ln.weight, ln.bias, eps, out_f32=True)
+        ctx.save = (x, mean, rstd)
+        ctx.ln, ctx.flat = ln, flat
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd = ctx.save
+        dx = torch.empty_like(x)
+        K.layernorm_bwd(dy.contiguous(), x, mean, rstd, ctx.ln.weight, dx, dw=_g(ctx.flat, ctx.ln.weight),
+                        db=_g(ctx.flat, ctx.ln.bias))
+        return (dx, None, None, None) + (None,) * len(ctx.needs_input_grad[4:])
+
+
+# ----------------------------------------------------------------------------------- backbone
+class SwinTransformer3D(nn.Module):
+    """Swin3D backbone; parameter tree of video_swin_ori.py:485-571 (frozen_stages=-1, patch_norm)."""
+
+    def __init__(self, patch_size=(2, 4, 4), in_chans=3, embed_dim=128, depths=(2, 2, 18, 2), num_heads=(4, 8, 16, 32),
+                 window_size=(8, 7, 7), drop_path_rate=0.2, patch_norm=True, **unused):
+        super().__init__()
+        if not patch_norm:
+            raise ValueError("patch_norm=False is not used by the LRCE extractor")
+        self.embed_dim, self.window_size, self.patch_size = embed_dim, tuple(window_size), tuple(patch_size)
+        self.depths, self.num_heads = tuple(depths), tuple(num_heads)
+        self.patch_embed = PatchEmbed3D(patch_size, in_chans, embed_dim)
+        self.pos_drop = nn.Dropout(0.0)
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, sum(depths))]
+        self.layers = nn.ModuleList()
+        for i, (dep, nh) in enumerate(zip(depths, num_heads)):
+            self.layers.append(BasicLayer(embed_dim * 2 ** i, dep, nh, self.window_size,
+                                          dpr[sum(depths[:i]):sum(depths[:i + 1])], i < len(depths) - 1))
+        self.num_features = embed_dim * 2 ** (len(depths) - 1)
+        self.norm = nn.LayerNorm(self.num_features)
+
+    def forward_tokens(self, clips, layout="BSTCHW", normalize=True):
+        """clips (B,S,T,3,H,W) f32 in [0,1] (normalised in-kernel) or (B,3,T,H,W) already normalised.
+        Returns (features f32 [n_clips*D'*H'*W', C_out], (n_clips, D', H', W'))."""
+        flat = ensure(self)
+        dev = clips.device
+        x = _PatchEmbedFn.apply(clips, self.patch_embed, flat, layout, normalize, *self.patch_embed.parameters())
+        if layout == "BSTCHW":
+            B, S, T, _, H, W = clips.shape
+            nc = B * S
+        else:
+            B, _, T, H, W = clips.shape
+            nc = B
+        D, H, W = (T + 1) // 2, H // 4, W // 4
+        for layer in self.layers:
+            geo = stage_geometry(nc, D, H, W, self.window_size, dev)
+            for blk in layer.blocks:
+                dp1 = _drop_path_scale(blk.drop_path, nc, dev, self.training)
+                dp2 = _drop_path_scale(blk.drop_path, nc, dev, self.training)
+                x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, *blk.parameters())
+            if layer.downsample is not None:
+                x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())
+                H, W = H // 2, W // 2
+        x = _LayerNormFn.apply(x, self.norm, flat, 1e-5, *self.norm.parameters())
+        return x, (nc, D, H, W)
+
+    def forward_stage(self, i, x_cl, depth=None):
+        """Run stage i (its first `depth` blocks, all by default, then PatchMerging) on channels-last
+        x_cl (nc, D, H, W, C) f32; returns the next stage's channels-last input.  (Test /
+        introspection entry: per-stage parity fixtures.)"""
+        flat = ensure(self)
+        nc, D, H, W, C = x_cl.shape
+        geo = stage_geometry(nc, D, H, W, self.window_size, x_cl.device)
+        x = x_cl.reshape(-1, C).contiguous()
+        layer = self.layers[i]
+        for blk in list(layer.blocks)[:depth]:
+            dp1 = _drop_path_scale(blk.drop_path, nc, x.device, self.training)
+            dp2 = _drop_path_scale(blk.drop_path, nc, x.device, self.training)
+            x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, *blk.parameters())
+        if layer.downsample is not None:
+            x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())
+            H, W = H // 2, W // 2
+        return x.view(nc, D, H, W, -1)
+
+    def forward(self, x):
+        """Reference signature (video_swin_ori.py:674-687): x (B,3,T,H,W) normalised -> (B,C,D',H',W')."""
+        feats, (nc, D, H, W) = self.forward_tokens(x.contiguous(), layout="BCTHW", normalize=False)
+        return feats.view(nc, D, H, W, -1).permute(0, 4, 1, 2, 3)
+
+    def train(self, mode=True):
+        # the reference's override returns None (video_swin_ori.py:689-692); keep nn.Module semantics
+        return super().train(mode)

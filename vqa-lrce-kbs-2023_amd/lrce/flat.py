@@ -1,0 +1,93 @@
+"""Flat parameter storage for a module on one HIP device.
+
+All parameters live as views of ONE f32 master buffer; a bf16 shadow of the same layout feeds the
+MFMA kernels; gradients are views of ONE f32 buffer that the backward kernels accumulate into
+directly (atomics / fused epilogues), so there is no per-parameter autograd accumulation pass.
+Every tensor starts on a 1024-element boundary, so 1024-element chunks map to exactly one tensor:
+this is what lets the fused L2-norm + AdamW kernels (csrc/optim.hip) and the gradient all-reduce
+buckets work on plain contiguous ranges.  Parameter names/shapes are untouched, so state_dict()
+keeps the reference key schema.
+"""
+import torch
+
+from . import kernels as K
+
+ALIGN = 1024
+
+
+class FlatParams:
+    def __init__(self, module, device):
+        self.device = torch.device(device)
+        self.params = [p for p in module.parameters()]
+        self.names = {id(p): n for n, p in module.named_parameters()}
+        offs, o = [], 0
+        for p in self.params:
+            offs.append(o)
+            o += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.total = o
+        self.offsets = offs
+        self.f32 = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.bf16 = torch.empty(self.total, dtype=torch.bfloat16, device=self.device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self._index = {}
+        for i, (p, off) in enumerate(zip(self.params, offs)):
+            n = p.numel()
+            self.f32[off:off + n].copy_(p.detach().reshape(-1))
+            p.data = self.f32[off:off + n].view(p.shape)
+            self._index[id(p)] = i
+        chunk_tensor = torch.empty(self.total // ALIGN, dtype=torch.int32)
+        for i, (p, off) in enumerate(zip(self.params, offs)):
+            n = (p.numel() + ALIGN - 1) // ALIGN
+            chunk_tensor[off // ALIGN: off // ALIGN + n] = i
+        self.chunk_tensor = chunk_tensor.to(self.device)
+        self.n_chunks = self.total // ALIGN
+        self._bf16_version = -1
+        self.attach_grads(zero=True)
+
+    # ------------------------------------------------------------------ views
+    def _slice(self, buf, p):
+        i = self._index[id(p)]
+        off = self.offsets[i]
+        return buf[off:off + p.numel()].view(p.shape)
+
+    def w16(self, p):
+        return self._slice(self.bf16, p)
+
+    def g32(self, p):
+        """f32 gradient accumulator of p (None if p is frozen)."""
+        if not p.requires_grad:
+            return None
+        return self._slice(self.grad, p)
+
+    def range_of(self, p):
+        i = self._index[id(p)]
+        return self.offsets[i], self.offsets[i] + (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+
+    def owns(self, p):
+        return id(p) in self._index
+
+    # ------------------------------------------------------------------ sync
+    def refresh_bf16(self):
+        """Re-cast the bf16 shadow if the masters changed (optimizer step, load_state_dict, ...).
+        Views share the base's version counter, so one check covers every parameter."""
+        v = self.f32._version
+        if v != self._bf16_version:
+            K.cast_bf16(self.f32, self.bf16)
+            self._bf16_version = self.f32._version
+
+    def mark_bf16_fresh(self):
+        self._bf16_version = self.f32._version
+
+    def attach_grads(self, zero=False):
+        """Make every p.grad the flat view (torch's zero_grad(set_to_none=True) drops them)."""
+        need = zero
+        for p in (self.params[0], self.params[-1]):  # zero_grad() touches all or none
+            if not p.requires_grad:
+                continue
+            g = p.grad
+            if g is None or g.data_ptr() != self._slice(self.grad, p).data_ptr():
+                need = True
+        if need:
+            self.grad.zero_()
+            for p in self.params:
+                p.grad = self._slice(self.grad, p) if p.requires_grad else None

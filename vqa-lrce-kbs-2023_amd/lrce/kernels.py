@@ -120,9 +120,10 @@ def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_
          flags=N.EPI_ATOMIC, a_map=a_map, split_k=split, a_row_scale=a_row_scale, a_rows_per_scale=a_rows_per_scale)
 
 
-def colsum(x, out, *, row_map=None, rows=None):
+def colsum(x, out, *, row_map=None, rows=None, row_scale=None, rows_per_scale=1):
     M = rows if rows is not None else x.shape[0]
-    call("lrce_colsum", ptr(x), int(x.dtype == F32), ptr(row_map), x.shape[-1], M, x.shape[-1], ptr(out), stream_of(out))
+    call("lrce_colsum", ptr(x), int(x.dtype == F32), ptr(row_map), x.shape[-1], M, x.shape[-1], ptr(row_scale),
+         rows_per_scale, ptr(out), stream_of(out))
 
 
 def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out_map=None, rows=None, cols=None,
@@ -184,9 +185,16 @@ def mha_bwd(q, ld_q, k, v, ld_kv, stride_kv_b, key_mask, out, ld_o, dout, lse, d
          ptr(lse), ptr(dq), ld_dq, ptr(dk), ptr(dv), ld_dkv, stride_dkv_b, B, H, Lq, Lk, d, scale, stream_of(dq))
 
 
-def patch_im2col(clips, patches):
-    B, S, T, C, H, W = clips.shape
-    call("lrce_patch_im2col", ptr(clips), ptr(patches), B, S, T, H, W, stream_of(patches))
+def patch_im2col(clips, patches, *, layout="BSTCHW", normalize=True):
+    """clips f32 (B,S,T,3,H,W) [layout BSTCHW] or (B,3,T,H,W) [layout BCTHW] -> patches bf16 [tokens, 96]."""
+    if layout == "BSTCHW":
+        B, S, T, C, H, W = clips.shape
+        n, s_clip, s_t, s_c = B * S, T * C * H * W, C * H * W, H * W
+    else:
+        B, C, T, H, W = clips.shape
+        n, s_clip, s_t, s_c = B, C * T * H * W, H * W, T * H * W
+    call("lrce_patch_im2col", ptr(clips), n, T, H, W, s_clip, s_t, s_c, int(normalize), ptr(patches),
+         stream_of(patches))
 
 
 def cast_bf16(x, y):
