@@ -31,7 +31,7 @@ enum {
 /* ---------------------------------------------------------------- GEMM (MFMA bf16 -> f32 acc)
  * C[b][m][n] (+)= epilogue( alpha * sum_k A(m,k) * B(n,k) )
  *   A(m,k) = a_kmajor ? A[m*lda + k] : A[k*lda + m]      (a_f32: A is f32, rounded to bf16 on load)
- *   B(n,k) = b_kmajor ? B[n*ldb + k] : B[k*ldb + n]      (bf16)
+ *   B(n,k) = b_kmajor ? B[n*ldb + k] : B[k*ldb + n]      (bf16, or f32 with b_f32)
  *   a_map (optional int32): gathers A rows — replaces m (a_kmajor) or k (!a_kmajor) by a_map[.]
  *   c_map (optional int32): scatters output rows — row m is written to c_map[m] (also the row of
  *                           the RESID / DGELU aux read).
@@ -77,6 +77,9 @@ typedef struct LrceGemmDesc {
   int32_t rows_per_scale;
   const float* a_row_scale;
   int32_t a_rows_per_scale;
+  /* b_f32 = 1: B is f32 (then A must be f32): exact-f32 MFMA path (v_mfma_f32_16x16x4_f32) for the
+   * small-M recurrent-decoder linears that read the f32 master weights directly. */
+  int32_t b_f32;
 } LrceGemmDesc;
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);
@@ -85,13 +88,14 @@ int lrce_gemm(const LrceGemmDesc* desc, void* stream);
  * Row r of the (rows x cols) LN input is the concatenation of nseg segments of cols/nseg
  * channels, segment s read from source row in_map[r*nseg+s] of x (identity if in_map == NULL;
  * a negative index reads zeros = padding).  Output row r goes to out_map[r] (identity if NULL).
- * Saves per-row mean and rstd (f32) for the backward.
+ * Saves per-row mean and rstd (f32) for the backward.  y_bf16_copy (optional): a bf16 copy of y (f32 y
+ * for the residual stream + bf16 operand for the next GEMM / weight gradient, one pass).
  * Replaces: nn.LayerNorm at video_swin_ori.py:252,285,339,476-480,684; PatchMerging gather
  * (:333-337, nseg=4); window_partition + torch.roll (:60-72,262) via in_map; embedding.py:22,62;
  * fusionv3.py:48; BERT LayerNorms. */
 int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_map, int nseg,
                        const float* w, const float* b, float eps,
-                       void* y, int y_f32, const int32_t* out_map,
+                       void* y, int y_f32, uint16_t* y_bf16_copy, const int32_t* out_map,
                        float* mean, float* rstd, int rows, int cols, void* stream);
 
 /* dy row r (read from dy_map[r] if given), x/mean/rstd as in forward.  dx for segment s is written
@@ -127,18 +131,50 @@ int lrce_wattn_dbias(const uint16_t* ds_scratch, int n_win, int n, int nH, const
                      float* table_grad, void* stream);
 
 /* ---------------------------------------------------------------- small multi-head attention
- * Generic masked SDPA for BERT self-attention (text.py:12-17, L<=64) and the fusion decoder's
- * cross-attention (fusionv3.py:44-49 via nn.MultiheadAttention, Lq=1, Lk=183/191).
- * q: [B][Lq] rows of ld_q, head h at column h*d; k,v likewise; key_mask: int32 [B][Lk] (1 keep, 0
- * masked, NULL = all keep).  out bf16 [B][Lq][ld_o], lse f32 [B][H][Lq]. scale applied to q.k. */
-int lrce_mha_fwd(const uint16_t* q, int64_t ld_q, const uint16_t* k, const uint16_t* v, int64_t ld_kv,
-                 int64_t stride_kv_b, const int32_t* key_mask, uint16_t* out, int64_t ld_o, float* lse,
-                 int B, int H, int Lq, int Lk, int d, float scale, void* stream);
-int lrce_mha_bwd(const uint16_t* q, int64_t ld_q, const uint16_t* k, const uint16_t* v, int64_t ld_kv,
-                 int64_t stride_kv_b, const int32_t* key_mask, const uint16_t* out, int64_t ld_o,
-                 const uint16_t* dout, const float* lse, float* dq, int64_t ld_dq, float* dk, float* dv,
-                 int64_t ld_dkv, int64_t stride_dkv_b, int B, int H, int Lq, int Lk, int d, float scale,
-                 void* stream);
+ * Masked SDPA, head_dim 64, for BERT self-attention (text.py:12-17 -> HF BertSelfAttention, L<=64)
+ * and the LRCE decoder cross-attention (fusionv3.py:44-49 -> nn.MultiheadAttention, Lq=1).
+ * Query row (b, i) at q[(b*Lq + i)*ld_q + h*64].  Keys j < lk1 come from segment 1: row
+ * k1[(b/kv1_bdiv)*stride_kv1_b + j*ld_kv1 + h*64]; keys lk1 <= j < lk1+lk2 from segment 2 likewise
+ * (e.g. [video tokens of the step ; question tokens] without materialising the concatenation;
+ * kv1_bdiv = 5 shares one video memory across the 5 MC choices).  key_mask int32 [B][lk1+lk2]
+ * (1 keep / 0 masked, NULL = keep all) = HF's additive -inf padding mask.  drop_p > 0: dropout on
+ * the attention probabilities (train mode), mask = hash(seed, ((b*H+h)*Lq+i)*Lk+j) >= drop_p.
+ * out bf16 [B*Lq][ld_o], lse f32 [B][H][Lq] (natural log).  Backward: dq f32 written; dk1,dv1,dk2,dv2
+ * f32 ACCUMULATED (atomics; caller zeroes), laid out like k1,v1,k2,v2 with their own ld/stride. */
+typedef struct LrceMhaDesc {
+  const uint16_t* q;
+  int64_t ld_q;
+  const uint16_t* k1;
+  const uint16_t* v1;
+  int64_t ld_kv1, stride_kv1_b;
+  int32_t kv1_bdiv, lk1;
+  const uint16_t* k2;
+  const uint16_t* v2;
+  int64_t ld_kv2, stride_kv2_b;
+  int32_t kv2_bdiv, lk2;
+  const int32_t* key_mask;
+  uint16_t* out;
+  int64_t ld_o;
+  float* lse;
+  int32_t B, H, Lq, d;
+  float scale;
+  float drop_p;
+  uint64_t seed;
+  int32_t f32_io;   /* 1: q, out, dout are f32 (decoder query path); K/V stay bf16 */
+  /* backward only */
+  const uint16_t* dout;
+  float* dq;
+  int64_t ld_dq;
+  float* dk1;
+  float* dv1;
+  int64_t ld_dkv1, stride_dkv1_b;
+  float* dk2;
+  float* dv2;
+  int64_t ld_dkv2, stride_dkv2_b;
+} LrceMhaDesc;
+
+int lrce_mha_fwd(const LrceMhaDesc* desc, void* stream);
+int lrce_mha_bwd(const LrceMhaDesc* desc, void* stream);
 
 /* ---------------------------------------------------------------- elementwise / data movement */
 /* Patch-embed input stage: [ImageNet Normalize (video.py:35)] + zero-pad T to a multiple of 2
@@ -154,10 +190,13 @@ int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, in
                 int rows_per_scale, float* out, void* stream);
 /* f32 -> bf16 cast (n elements) */
 int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
-/* y = x * keep / (1-p) with keep ~ Bernoulli(1-p) from a counter hash (seed, offset); p=0 copies.
- * Optional bf16 copy.  In place allowed. */
-int lrce_dropout(const float* x, float* y, uint16_t* y_bf16, int64_t n, float p, uint64_t seed, void* stream);
-int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t seed, void* stream);
+/* Dropout (nn.Dropout / F.dropout semantics, train mode): y = (res ? res : 0) + x * keep / (1-p),
+ * keep = hash(seed, i / group) >= p (group > 1 drops whole groups, e.g. per attention head);
+ * p = 0 copies.  Optional bf16 copy of y.  In place allowed.  Backward: dx = dy * keep / (1-p)
+ * (the residual's gradient is dy itself). */
+int lrce_dropout(const float* x, const float* res, float* y, uint16_t* y_bf16, int64_t n, float p, uint64_t seed,
+                 int64_t group, void* stream);
+int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t seed, int64_t group, void* stream);
 
 /* Fused optimizer step over the flat parameter buffer (agent_base.py:27-44,103-108).  Every tensor
  * starts at a multiple of 1024 elements; chunk_tensor[c] is the tensor id of 1024-element chunk c.
@@ -175,7 +214,7 @@ int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t*
 int lrce_bert_embed_fwd(const int64_t* ids, const int64_t* types, const float* word, const float* pos, const float* typ,
                         float* out, int rows, int L, int C, void* stream);
 int lrce_bert_embed_bwd(const float* dout, const int64_t* ids, const int64_t* types, float* dword, float* dpos, float* dtyp,
-                        int rows, int L, int C, void* stream);
+                        int rows, int L, int C, int64_t pad_id, void* stream); /* pad_id: word row without grad (-1 none) */
 /* LRCE positional embeddings before their LayerNorm (embedding.py:47-63, 17-23). */
 int lrce_video_posembed_fwd(const float* x, const float* cls, const float* pos, const float* len, const float* clip, float* out,
                             int B, int S, int Tg, int P, int C, void* stream);

@@ -203,8 +203,9 @@ def bert(ids, mask, types, sd, p="text_extractor.bert.", n_layers=12, n_heads=12
     reference but unused (text.py:12-17), so it is not restated."""
     B, L = ids.shape
     e = p + "embeddings."
-    x = sd[e + "word_embeddings.weight"][ids] + sd[e + "position_embeddings.weight"][:L].unsqueeze(0) \
-        + sd[e + "token_type_embeddings.weight"][types]
+    # word embeddings are nn.Embedding(vocab, 768, padding_idx=pad_token_id=0): row 0 gets no gradient
+    x = F.embedding(ids, sd[e + "word_embeddings.weight"], padding_idx=0) \
+        + sd[e + "position_embeddings.weight"][:L].unsqueeze(0) + sd[e + "token_type_embeddings.weight"][types]
     x = _ln(x, sd, e + "LayerNorm.", LN_EPS_BERT)
     add = (1.0 - mask.to(x.dtype))[:, None, None, :] * torch.finfo(x.dtype).min
     hd = x.shape[-1] // n_heads

@@ -171,8 +171,22 @@ def bert_fixture(seed):
                         y=y.numpy(), ids2=ids2.numpy(), mask2=mask2.numpy(), types2=types2.numpy(), y2=y2.numpy())
 
 
+def schema_fixture():
+    """State-dict key schema (name -> shape, dtype) of the reference E2E models: the drop-in contract
+    for checkpoints."""
+    import json
+    out = {}
+    for name, ts in (("msvd-qa-oe", (3,)), ("tgif-transition", (3,)), ("tgif-count", (3,)), ("msrvtt-qa-oe", (1, 2, 3))):
+        m = build_e2e(CONFIGS[name], ts)
+        out[f"{name}_ts{''.join(map(str, ts))}"] = {k: [list(v.shape), str(v.dtype)] for k, v in m.state_dict().items()}
+    with open(os.path.join(HERE, "state_dict_schema.json"), "w") as f:
+        json.dump(out, f, sort_keys=True)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ops", "e2e"]
+    which = sys.argv[1:] or ["ops", "e2e", "schema"]
+    if "schema" in which:
+        schema_fixture()
     if "ops" in which:
         patch_embed_fixture(11)
         swin_stage_fixture("stage1_28", 0, 128, 4, 28, True, 12)

@@ -1,0 +1,51 @@
+"""CPU tests of the product's host layer: state-dict schema parity with the reference (golden
+fixture generated from the reference itself), constructor / argument surfaces."""
+import json
+import os
+
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+CASES = {
+    "msvd-qa-oe_ts3": ("oe", 1000, 32, [3]),
+    "tgif-transition_ts3": ("mc", 1, 40, [3]),
+    "tgif-count_ts3": ("count", 1, 30, [3]),
+    "msrvtt-qa-oe_ts123": ("oe", 1500, 37, [1, 2, 3]),
+}
+
+
+@pytest.fixture(scope="module")
+def schema():
+    with open(os.path.join(GOLDEN, "state_dict_schema.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_state_dict_schema_matches_reference(schema, case):
+    from lrce.models import e2e
+    task, ncls, L, ts = CASES[case]
+    cls = {"oe": e2e.E2EOpenEnded, "mc": e2e.E2EMultipleChoice, "count": e2e.E2ECount}[task]
+    m = cls(768, ncls, 0.1, (7, 7), 1024, 5, ts, L)
+    ours = {k: [list(v.shape), str(v.dtype)] for k, v in m.state_dict().items()}
+    ref = schema[case]
+    assert sorted(ours) == sorted(ref)
+    bad = [k for k in ref if ours[k] != ref[k]]
+    assert not bad, bad[:5]
+
+
+def test_reference_checkpoint_extras_are_tolerated():
+    """transformers 4.20 checkpoints carry bert.embeddings.position_ids (persistent buffer then)."""
+    from lrce.models import e2e
+    m = e2e.E2EOpenEnded(768, 1000, 0.1, (7, 7), 1024, 5, [3], 32)
+    sd = m.state_dict()
+    sd["text_extractor.bert.embeddings.position_ids"] = torch.arange(512).view(1, -1)
+    m.load_state_dict(sd, strict=True)
+
+
+def test_param_count_matches_survey():
+    from lrce.models import e2e
+    m = e2e.E2EOpenEnded(768, 1000, 0.1, (7, 7), 1024, 5, [3], 32)
+    n = sum(p.numel() for p in m.parameters())
+    assert abs(n / 1e6 - 312.2) < 0.1

@@ -54,6 +54,27 @@ def test_gemm_layouts(M, N, Kd, a_km, b_km, a_f32):
     assert rel(C, ref) < 2e-3
 
 
+@pytest.mark.parametrize("M,N,Kd", [(10, 768, 768), (50, 3072, 768), (45, 768, 3072), (128, 200, 96)])
+@pytest.mark.parametrize("a_km,b_km", [(1, 1), (1, 0), (0, 0)])
+def test_gemm_exact_f32_path(M, N, Kd, a_km, b_km):
+    """B f32 selects the exact-f32 MFMA path (decoder query side): fp32-level agreement."""
+    k = K()
+    if not a_km and M % 4:
+        pytest.skip("M-major A needs M % 4 == 0")
+    A = torch.randn(M, Kd, device=dev)
+    B = torch.randn(N, Kd, device=dev)
+    ref = (A.double() @ B.double().t()).float()
+    C = torch.empty(M, N, device=dev)
+    bias = torch.randn(N, device=dev)
+    a_store = A.contiguous() if a_km else A.t().contiguous()
+    b_store = B.contiguous() if b_km else B.t().contiguous()
+    k.gemm(a_store, b_store, C, M, N, Kd, a_kmajor=bool(a_km), b_kmajor=bool(b_km), flags=16 | 1, bias=bias)
+    assert rel(C, ref + bias) < 1e-5
+    C2 = torch.zeros(M, N, device=dev)
+    k.gemm(a_store, b_store, C2, M, N, Kd, a_kmajor=bool(a_km), b_kmajor=bool(b_km), flags=32 | 1, bias=bias, split_k=3)
+    assert rel(C2, ref + bias) < 1e-5
+
+
 def test_gemm_epilogues_and_maps():
     k = K()
     M, N, Kd = 520, 256, 160
@@ -189,12 +210,18 @@ def test_window_attention_fwd_bwd(nH, n_win):
     assert rel(tg, tab.grad) < 2e-2
 
 
-@pytest.mark.parametrize("B,H,Lq,Lk,masked", [(3, 12, 32, 32, True), (4, 12, 1, 183, False), (2, 12, 40, 40, True)])
-def test_mha_fwd_bwd(B, H, Lq, Lk, masked):
+@pytest.mark.parametrize("B,H,Lq,Lk,masked,split,bdiv,drop", [
+    (3, 12, 32, 32, True, 0, 1, 0.0), (4, 12, 1, 183, False, 150, 1, 0.0), (2, 12, 40, 40, True, 0, 1, 0.0),
+    (10, 12, 1, 191, False, 150, 5, 0.0), (3, 12, 32, 32, True, 0, 1, 0.3), (5, 12, 1, 183, False, 150, 5, 0.5)])
+def test_mha_fwd_bwd(B, H, Lq, Lk, masked, split, bdiv, drop):
+    """Two key segments (video memory shared by `bdiv` rows + text memory), padding mask, dropout."""
     k = K()
     d = 64
+    lk1 = split if split else Lk
+    lk2 = Lk - lk1
     q = bf(torch.randn(B, Lq, H * d, device=dev))
-    kv = bf(torch.randn(B, Lk, 2 * H * d, device=dev))
+    kv1 = bf(torch.randn(B // bdiv, lk1, 2 * H * d, device=dev))
+    kv2 = bf(torch.randn(B, max(lk2, 1), 2 * H * d, device=dev))
     kmask = torch.ones(B, Lk, dtype=torch.int32, device=dev)
     if masked:
         kmask[0, 20:] = 0
@@ -202,22 +229,68 @@ def test_mha_fwd_bwd(B, H, Lq, Lk, masked):
     out = torch.empty(B, Lq, H * d, device=dev, dtype=torch.bfloat16)
     lse = torch.empty(B, H, Lq, device=dev)
     scale = 1 / 8
-    k.mha_fwd(q, H * d, kv, kv[..., H * d:], 2 * H * d, Lk * 2 * H * d, kmask, out, H * d, lse, B, H, Lq, Lk, d, scale)
+    desc = k.mha_desc(q, Lq, k1=kv1, v1=kv1[..., H * d:], lk1=lk1, ld_kv1=2 * H * d, stride_kv1_b=lk1 * 2 * H * d,
+                      kv1_bdiv=bdiv, k2=kv2 if lk2 else None, v2=kv2[..., H * d:] if lk2 else None, lk2=lk2,
+                      ld_kv2=2 * H * d, stride_kv2_b=max(lk2, 1) * 2 * H * d, key_mask=kmask, out=out, lse=lse, B=B, H=H,
+                      scale=scale, drop_p=drop, seed=1234)
+    k.mha_fwd(desc, out)
+    kvf = torch.cat([kv1.float().repeat_interleave(bdiv, 0), kv2.float()[:, :lk2]], 1)
     qr = q.float().view(B, Lq, H, d).transpose(1, 2).requires_grad_(True)
-    kr = kv[..., :H * d].float().reshape(B, Lk, H, d).transpose(1, 2).contiguous().requires_grad_(True)
-    vr = kv[..., H * d:].float().reshape(B, Lk, H, d).transpose(1, 2).contiguous().requires_grad_(True)
+    kr = kvf[..., :H * d].reshape(B, Lk, H, d).transpose(1, 2).contiguous().requires_grad_(True)
+    vr = kvf[..., H * d:].reshape(B, Lk, H, d).transpose(1, 2).contiguous().requires_grad_(True)
     s = (qr @ kr.transpose(-1, -2)) * scale + (1 - kmask.float())[:, None, None, :] * -1e30
-    o = (s.softmax(-1) @ vr).transpose(1, 2).reshape(B, Lq, H * d)
+    P = s.softmax(-1)
+    if drop > 0:
+        # reproduce the kernel's counter-hash mask on the host: exact recomputation of lrce_uniform
+        idx = torch.arange(B * H * Lq * Lk, dtype=torch.int64).view(B, H, Lq, Lk)
+        keep = (_hash_uniform(1234, idx) >= drop).to(dev).float() / (1 - drop)
+        P = P * keep
+    o = (P @ vr).transpose(1, 2).reshape(B, Lq, H * d)
     assert rel(out, o) < 1e-2
     dout = bf(torch.randn(B, Lq, H * d, device=dev))
     o.backward(dout.float())
     dq = torch.empty(B, Lq, H * d, device=dev)
-    dkv = torch.empty(B, Lk, 2 * H * d, device=dev)
-    k.mha_bwd(q, H * d, kv, kv[..., H * d:], 2 * H * d, Lk * 2 * H * d, kmask, out, H * d, dout, lse, dq, H * d,
-              dkv, dkv[..., H * d:], 2 * H * d, Lk * 2 * H * d, B, H, Lq, Lk, d, scale)
+    dkv1 = torch.zeros(B // bdiv, lk1, 2 * H * d, device=dev)
+    dkv2 = torch.zeros(B, max(lk2, 1), 2 * H * d, device=dev)
+    k.mha_bwd(desc, dout=dout, dq=dq, dk1=dkv1, dv1=dkv1[..., H * d:], ld_dkv1=2 * H * d, stride_dkv1_b=lk1 * 2 * H * d,
+              dk2=dkv2 if lk2 else None, dv2=dkv2[..., H * d:] if lk2 else None, ld_dkv2=2 * H * d,
+              stride_dkv2_b=max(lk2, 1) * 2 * H * d)
     assert rel(dq, qr.grad.transpose(1, 2).reshape(B, Lq, H * d)) < 1e-2
-    assert rel(dkv[..., :H * d], kr.grad.transpose(1, 2).reshape(B, Lk, H * d)) < 1e-2
-    assert rel(dkv[..., H * d:], vr.grad.transpose(1, 2).reshape(B, Lk, H * d)) < 1e-2
+    gk = kr.grad.transpose(1, 2).reshape(B, Lk, H * d)
+    gv = vr.grad.transpose(1, 2).reshape(B, Lk, H * d)
+    gk1 = gk[:, :lk1].reshape(B // bdiv, bdiv, lk1, H * d).sum(1)
+    gv1 = gv[:, :lk1].reshape(B // bdiv, bdiv, lk1, H * d).sum(1)
+    assert rel(dkv1[..., :H * d], gk1) < 1e-2
+    assert rel(dkv1[..., H * d:], gv1) < 1e-2
+    if lk2:
+        assert rel(dkv2[:, :lk2, :H * d], gk[:, lk1:]) < 1e-2
+        assert rel(dkv2[:, :lk2, H * d:], gv[:, lk1:]) < 1e-2
+
+
+def _hash_uniform(seed, idx):
+    """Host restatement of lrce_uniform (csrc/common.h): 64-bit mix hash of seed*phi + idx -> [0,1)."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        v = np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + idx.numpy().astype(np.uint64)
+        v ^= v >> np.uint64(33)
+        v *= np.uint64(0xff51afd7ed558ccd)
+        v ^= v >> np.uint64(33)
+        v *= np.uint64(0xc4ceb9fe1a85ec53)
+        v ^= v >> np.uint64(33)
+    u32 = (v & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    return torch.from_numpy((u32 >> 8).astype(np.float32) * np.float32(1.0 / 16777216.0))
+
+
+def test_dropout_residual_and_groups():
+    k = K()
+    x = torch.randn(4096, device=dev)
+    r = torch.randn(4096, device=dev)
+    y = k.dropout(x, 0.25, 77, res=r, group=64)
+    keep = (_hash_uniform(77, torch.arange(4096) // 64) >= 0.25).to(dev).float()
+    assert rel(y, r + x * keep / 0.75) < 1e-6
+    dx = k.dropout_bwd(x, 0.25, 77, group=64)
+    assert rel(dx, x * keep / 0.75) < 1e-6
+    assert 0.6 < keep.mean().item() < 0.9
 
 
 def test_patch_im2col_matches_conv():

@@ -77,21 +77,23 @@ __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, l
   }
 }
 
-__global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, bf16* __restrict__ yb, long long n, float p,
-                               uint64_t seed) {
+__global__ void dropout_kernel(const float* __restrict__ x, const float* __restrict__ res, float* __restrict__ y,
+                               bf16* __restrict__ yb, long long n, float p, uint64_t seed, long long group) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float v = x[i];
-  if (p > 0.f) v = (lrce_uniform(seed, i) >= p) ? v / (1.0f - p) : 0.f;
+  if (p > 0.f) v = (lrce_uniform(seed, i / group) >= p) ? v / (1.0f - p) : 0.f;
+  if (res) v += res[i];
   y[i] = v;
   if (yb) yb[i] = f2bf(v);
 }
 
-__global__ void dropout_bwd_kernel(const float* __restrict__ dy, float* __restrict__ dx, long long n, float p, uint64_t seed) {
+__global__ void dropout_bwd_kernel(const float* __restrict__ dy, float* __restrict__ dx, long long n, float p, uint64_t seed,
+                                   long long group) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float v = dy[i];
-  if (p > 0.f) v = (lrce_uniform(seed, i) >= p) ? v / (1.0f - p) : 0.f;
+  if (p > 0.f) v = (lrce_uniform(seed, i / group) >= p) ? v / (1.0f - p) : 0.f;
   dx[i] = v;
 }
 
@@ -109,12 +111,13 @@ __global__ void bert_embed_kernel(const long long* __restrict__ ids, const long 
   *reinterpret_cast<float4*>(out + e) = make_float4(a.x + b.x + t.x, a.y + b.y + t.y, a.z + b.z + t.z, a.w + b.w + t.w);
 }
 __global__ void bert_embed_bwd_kernel(const float* __restrict__ d, const long long* __restrict__ ids, const long long* __restrict__ types,
-                                      float* __restrict__ dword, float* __restrict__ dpos, float* __restrict__ dtyp, int rows, int L, int C) {
+                                      float* __restrict__ dword, float* __restrict__ dpos, float* __restrict__ dtyp, int rows, int L, int C,
+                                      long long pad_id) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long long)rows * C) return;
   const int r = e / C, c = e % C;
   const float g = d[e];
-  atomicAdd(dword + ids[r] * C + c, g);
+  if (ids[r] != pad_id) atomicAdd(dword + ids[r] * C + c, g);  // nn.Embedding(padding_idx): no grad
   atomicAdd(dpos + (long long)(r % L) * C + c, g);
   atomicAdd(dtyp + types[r] * C + c, g);
 }
@@ -227,17 +230,21 @@ extern "C" int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stre
   return lrce_check_launch("cast_bf16");
 }
 
-extern "C" int lrce_dropout(const float* x, float* y, uint16_t* y_bf16, int64_t n, float p, uint64_t seed, void* stream) {
+extern "C" int lrce_dropout(const float* x, const float* res, float* y, uint16_t* y_bf16, int64_t n, float p, uint64_t seed,
+                            int64_t group, void* stream) {
   if (!x || !y) return lrce_fail(LRCE_E_ARG, "dropout: null pointer");
   if (n <= 0) return LRCE_OK;
-  dropout_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(x, y, reinterpret_cast<bf16*>(y_bf16), n, p, seed);
+  if (group < 1) group = 1;
+  dropout_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(x, res, y, reinterpret_cast<bf16*>(y_bf16), n, p,
+                                                                               seed, group);
   return lrce_check_launch("dropout");
 }
 
-extern "C" int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t seed, void* stream) {
+extern "C" int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t seed, int64_t group, void* stream) {
   if (!dy || !dx) return lrce_fail(LRCE_E_ARG, "dropout_bwd: null pointer");
   if (n <= 0) return LRCE_OK;
-  dropout_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(dy, dx, n, p, seed);
+  if (group < 1) group = 1;
+  dropout_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(dy, dx, n, p, seed, group);
   return lrce_check_launch("dropout_bwd");
 }
 
@@ -251,11 +258,11 @@ extern "C" int lrce_bert_embed_fwd(const int64_t* ids, const int64_t* types, con
 }
 
 extern "C" int lrce_bert_embed_bwd(const float* dout, const int64_t* ids, const int64_t* types, float* dword, float* dpos, float* dtyp,
-                                   int rows, int L, int C, void* stream) {
+                                   int rows, int L, int C, int64_t pad_id, void* stream) {
   if (!dout || !ids || !types || !dword || !dpos || !dtyp) return lrce_fail(LRCE_E_ARG, "bert_embed_bwd: null pointer");
   const long long n = (long long)rows * C;
   bert_embed_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(
-      dout, reinterpret_cast<const long long*>(ids), reinterpret_cast<const long long*>(types), dword, dpos, dtyp, rows, L, C);
+      dout, reinterpret_cast<const long long*>(ids), reinterpret_cast<const long long*>(types), dword, dpos, dtyp, rows, L, C, pad_id);
   return lrce_check_launch("bert_embed_bwd");
 }
 

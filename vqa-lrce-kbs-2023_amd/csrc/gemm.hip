@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + wn * 64 + j * 16 + (lane & 15);
     if (n >= p.n) continue;
-    float bias = (fl & LRCE_EPI_BIAS) ? p.bias[n] : 0.f;
+    float bias = ((fl & LRCE_EPI_BIAS) && sk == 0) ? p.bias[n] : 0.f;
     const float csc = (n < p.scale_cols) ? p.scale_val : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
         }
         if (fl & LRCE_EPI_DGELU) v *= gelu_grad_f(bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]));
         if (p.row_scale) v *= p.row_scale[m / p.rows_per_scale];
-        if (fl & LRCE_EPI_RESID) v += static_cast<const float*>(p.aux)[row * p.ld_aux + n];
+        if ((fl & LRCE_EPI_RESID) && sk == 0) v += static_cast<const float*>(p.aux)[row * p.ld_aux + n];
         if (fl & LRCE_EPI_ATOMIC) {
           atomicAdd(reinterpret_cast<float*>(cbase) + row * p.ldc + n, v);
         } else if (fl & LRCE_EPI_ACCUM) {
@@ -241,9 +241,15 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
 
 }  // namespace
 
+int lrce_gemm_f32(const LrceGemmDesc* d, void* stream);
+
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
   if (!d || !d->a || !d->b || !d->c) return lrce_fail(LRCE_E_ARG, "gemm: null pointer");
   if (d->m <= 0 || d->n <= 0 || d->k <= 0 || d->batch <= 0) return lrce_fail(LRCE_E_ARG, "gemm: empty shape");
+  if ((d->flags & (LRCE_EPI_DGELU | LRCE_EPI_RESID)) && !d->aux) return lrce_fail(LRCE_E_ARG, "gemm: aux missing");
+  if ((d->flags & (LRCE_EPI_AUX_OUT | LRCE_EPI_OUT_BOTH)) && !d->aux_out) return lrce_fail(LRCE_E_ARG, "gemm: aux_out missing");
+  if ((d->flags & LRCE_EPI_BIAS) && !d->bias) return lrce_fail(LRCE_E_ARG, "gemm: bias missing");
+  if (d->b_f32) return lrce_gemm_f32(d, stream);
   // vector loads need the contiguous dim of every operand to be a multiple of 8 elements
   if (d->a_kmajor ? (d->k % 8) : (d->m % 8)) return lrce_fail(LRCE_E_ARG, "gemm: A contiguous dim %% 8 != 0");
   if (d->b_kmajor ? (d->k % 8) : (d->n % 8)) return lrce_fail(LRCE_E_ARG, "gemm: B contiguous dim %% 8 != 0");

@@ -43,7 +43,7 @@ __device__ __forceinline__ long long src_off(const int* in_map, int nseg, int se
 
 template <typename TX, typename TY>
 __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, int nseg, const float* w, const float* b,
-                                              float eps, TY* y, const int* out_map, float* mean_o, float* rstd_o,
+                                              float eps, TY* y, bf16* y2, const int* out_map, float* mean_o, float* rstd_o,
                                               int rows, int cols) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -85,6 +85,7 @@ __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, in
       o.z = (v[t].z - mean) * rstd * ww.z + bb.z;
       o.w = (v[t].w - mean) * rstd * ww.w + bb.w;
       st4<TY>(y + orow * cols + 4 * c, o);
+      if (y2) st4<bf16>(y2 + orow * cols + 4 * c, o);
     }
   }
   if (lane == 0) {
@@ -172,8 +173,8 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
 }  // namespace
 
 extern "C" int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_map, int nseg, const float* w,
-                                  const float* b, float eps, void* y, int y_f32, const int32_t* out_map, float* mean,
-                                  float* rstd, int rows, int cols, void* stream) {
+                                  const float* b, float eps, void* y, int y_f32, uint16_t* y2, const int32_t* out_map,
+                                  float* mean, float* rstd, int rows, int cols, void* stream) {
   if (!x || !y || !w || !b) return lrce_fail(LRCE_E_ARG, "layernorm_fwd: null pointer");
   if (nseg < 1) nseg = 1;
   if (cols % 4 || (cols / nseg) % 4 || cols % nseg || cols > 64 * 4 * MAXC)
@@ -181,7 +182,7 @@ extern "C" int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_ma
   if (rows <= 0) return LRCE_OK;
   dim3 grid((rows + 3) / 4);
   hipStream_t s = static_cast<hipStream_t>(stream);
-#define LNF(TX, TY) ln_fwd<TX, TY><<<grid, 256, 0, s>>>(static_cast<const TX*>(x), in_map, nseg, w, b, eps, static_cast<TY*>(y), out_map, mean, rstd, rows, cols)
+#define LNF(TX, TY) ln_fwd<TX, TY><<<grid, 256, 0, s>>>(static_cast<const TX*>(x), in_map, nseg, w, b, eps, static_cast<TY*>(y), reinterpret_cast<bf16*>(y2), out_map, mean, rstd, rows, cols)
   if (x_f32 && y_f32) LNF(float, float);
   else if (x_f32) LNF(float, bf16);
   else if (y_f32) LNF(bf16, float);

@@ -1,10 +1,14 @@
-// Small masked multi-head attention, head_dim 64: BERT self-attention (L = 30..40, 12 heads;
-// HF BertSelfAttention as called from text.py:12-17) and the LRCE decoder cross-attention
-// (one summary-token query against 183/191 memory keys; nn.MultiheadAttention inside
-// nn.TransformerDecoderLayer, fusionv3.py:8-17,44-49).  These problems are tiny (<= 192 keys,
-// <= 64 queries per (batch, head)) and latency-bound, so one workgroup owns a (batch, head),
-// keeps K/V in LDS and computes in f32 on the VALU: the GEMM-shaped projections around it run
-// on MFMA in lrce_gemm.
+// Small masked multi-head attention, head_dim 64:
+//  * BERT self-attention (L = 30..40 tokens, 12 heads; HF BertSelfAttention via text.py:12-17);
+//  * the LRCE decoder cross-attention: one summary-token query against the step's memory
+//    [video clip tokens (150) ; question tokens (L+1)] (nn.MultiheadAttention inside
+//    nn.TransformerDecoderLayer, fusionv3.py:8-17,44-49).
+// The keys come from up to two segments so the memory is never concatenated in HBM: the text
+// segment's K/V are projected ONCE and reused by every recurrent step, and the video segment can be
+// shared by `bdiv` consecutive batch rows (the 5 answer choices of the MC head, fusionv3.py:259).
+// Attention-probability dropout (train mode) is applied in-kernel from a counter hash, identically
+// in the backward.  Problems are tiny and latency-bound: one workgroup per (batch row, head), K/V in
+// LDS, f32 VALU math; the projections around it run on MFMA in lrce_gemm.
 #include "common.h"
 #include "lrce_capi.h"
 
@@ -13,27 +17,41 @@ namespace {
 constexpr int D = 64;
 constexpr int MAXK = 192;
 
-__global__ void __launch_bounds__(256) mha_fwd_kernel(const bf16* __restrict__ q, long long ldq, const bf16* __restrict__ k,
-                                                      const bf16* __restrict__ v, long long ldkv, long long skv,
-                                                      const int* __restrict__ kmask, bf16* __restrict__ out, long long ldo,
-                                                      float* __restrict__ lse, int B, int H, int Lq, int Lk, float scale) {
+struct MhaP {
+  LrceMhaDesc d;
+};
+
+__device__ __forceinline__ const bf16* key_row(const LrceMhaDesc& d, const uint16_t* p1, const uint16_t* p2, int b, int j, int h) {
+  if (j < d.lk1) return reinterpret_cast<const bf16*>(p1) + (long long)(b / d.kv1_bdiv) * d.stride_kv1_b + (long long)j * d.ld_kv1 + h * D;
+  return reinterpret_cast<const bf16*>(p2) + (long long)(b / d.kv2_bdiv) * d.stride_kv2_b + (long long)(j - d.lk1) * d.ld_kv2 + h * D;
+}
+
+__device__ __forceinline__ float ld_io(const LrceMhaDesc& d, const void* p, long long i) {
+  return d.f32_io ? static_cast<const float*>(p)[i] : bf2f(static_cast<const bf16*>(p)[i]);
+}
+
+__device__ __forceinline__ float drop_factor(const LrceMhaDesc& d, int b, int h, int i, int j, int Lk) {
+  if (d.drop_p <= 0.f) return 1.f;
+  const uint64_t idx = (((uint64_t)b * d.H + h) * d.Lq + i) * (uint64_t)Lk + j;
+  return lrce_uniform(d.seed, idx) >= d.drop_p ? 1.0f / (1.0f - d.drop_p) : 0.f;
+}
+
+__global__ void __launch_bounds__(256) mha_fwd_kernel(MhaP P) {
+  const LrceMhaDesc& d = P.d;
   __shared__ float ks[MAXK][D + 1];
   __shared__ float vs[MAXK][D];
   __shared__ float ps[4][MAXK];
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int b = blockIdx.x / d.H, h = blockIdx.x % d.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bf16* kb = k + b * skv + h * D;
-  const bf16* vb = v + b * skv + h * D;
+  const int Lk = d.lk1 + d.lk2;
   for (int e = threadIdx.x; e < Lk * D; e += 256) {
     const int j = e / D, dd = e % D;
-    ks[j][dd] = bf2f(kb[j * ldkv + dd]);
-    vs[j][dd] = bf2f(vb[j * ldkv + dd]);
+    ks[j][dd] = bf2f(key_row(d, d.k1, d.k2, b, j, h)[dd]);
+    vs[j][dd] = bf2f(key_row(d, d.v1, d.v2, b, j, h)[dd]);
   }
   __syncthreads();
-  for (int i = wave; i < Lq; i += 4) {
-    const bf16* qr = q + ((long long)b * Lq + i) * ldq + h * D;
-    const float qd = bf2f(qr[lane]) * scale;
-    // scores: each lane accumulates q . k_j for keys j = lane + 64t; q broadcast through shuffles
+  for (int i = wave; i < d.Lq; i += 4) {
+    const float qd = ld_io(d, d.q, ((long long)b * d.Lq + i) * d.ld_q + h * D + lane) * d.scale;
     float sc[MAXK / 64];
 #pragma unroll
     for (int t = 0; t < MAXK / 64; ++t) sc[t] = 0.f;
@@ -45,13 +63,13 @@ __global__ void __launch_bounds__(256) mha_fwd_kernel(const bf16* __restrict__ q
         if (j < Lk) sc[t] += qv * ks[j][dd];
       }
     }
-    // masked / padded keys: excluded explicitly (no infinities: -1e30 sentinel, keep flags)
+    // masked / padded keys are excluded explicitly (no infinities: hipcc may assume finite math)
     float m = -1.0e30f;
     bool keep[MAXK / 64];
 #pragma unroll
     for (int t = 0; t < MAXK / 64; ++t) {
       const int j = lane + 64 * t;
-      keep[t] = j < Lk && (!kmask || kmask[(long long)b * Lk + j] != 0);
+      keep[t] = j < Lk && (!d.key_mask || d.key_mask[(long long)b * Lk + j] != 0);
       if (keep[t]) m = fmaxf(m, sc[t]);
     }
     m = wave_max(m);
@@ -60,7 +78,7 @@ __global__ void __launch_bounds__(256) mha_fwd_kernel(const bf16* __restrict__ q
     for (int t = 0; t < MAXK / 64; ++t) {
       const int j = lane + 64 * t;
       const float p = keep[t] ? __expf(sc[t] - m) : 0.f;
-      if (j < Lk) ps[wave][j] = p;
+      if (j < Lk) ps[wave][j] = p * drop_factor(d, b, h, i, j, Lk);
       s += p;
     }
     s = wave_sum(s);
@@ -68,50 +86,46 @@ __global__ void __launch_bounds__(256) mha_fwd_kernel(const bf16* __restrict__ q
     __builtin_amdgcn_wave_barrier();
     float o = 0.f;
     for (int j = 0; j < Lk; ++j) o += ps[wave][j] * vs[j][lane];
-    out[((long long)b * Lq + i) * ldo + h * D + lane] = f2bf(o / s);
-    if (lane == 0) lse[((long long)b * H + h) * Lq + i] = m + __logf(s);
+    const long long oi = ((long long)b * d.Lq + i) * d.ld_o + h * D + lane;
+    if (d.f32_io) reinterpret_cast<float*>(d.out)[oi] = o / s;
+    else reinterpret_cast<bf16*>(d.out)[oi] = f2bf(o / s);
+    if (lane == 0) d.lse[((long long)b * d.H + h) * d.Lq + i] = m + __logf(s);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
 }
 
-__global__ void __launch_bounds__(256) mha_bwd_kernel(const bf16* __restrict__ q, long long ldq, const bf16* __restrict__ k,
-                                                      const bf16* __restrict__ v, long long ldkv, long long skv,
-                                                      const int* __restrict__ kmask, const bf16* __restrict__ outp, long long ldo,
-                                                      const bf16* __restrict__ dout, const float* __restrict__ lse,
-                                                      float* __restrict__ dq, long long lddq, float* __restrict__ dk,
-                                                      float* __restrict__ dv, long long lddkv, long long sdkv, int B, int H, int Lq,
-                                                      int Lk, float scale) {
+__global__ void __launch_bounds__(256) mha_bwd_kernel(MhaP P) {
+  const LrceMhaDesc& d = P.d;
   __shared__ bf16 ks[MAXK][D + 2];
   __shared__ bf16 vs[MAXK][D + 2];
   __shared__ float dks[MAXK][D];
   __shared__ float dvs[MAXK][D];
   __shared__ float ps[4][MAXK];
   __shared__ float dss[4][MAXK];
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int b = blockIdx.x / d.H, h = blockIdx.x % d.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bf16* kb = k + b * skv + h * D;
-  const bf16* vb = v + b * skv + h * D;
+  const int Lk = d.lk1 + d.lk2;
   for (int e = threadIdx.x; e < Lk * D; e += 256) {
     const int j = e / D, dd = e % D;
-    ks[j][dd] = kb[j * ldkv + dd];
-    vs[j][dd] = vb[j * ldkv + dd];
+    ks[j][dd] = key_row(d, d.k1, d.k2, b, j, h)[dd];
+    vs[j][dd] = key_row(d, d.v1, d.v2, b, j, h)[dd];
     dks[j][dd] = 0.f;
     dvs[j][dd] = 0.f;
   }
   __syncthreads();
-  for (int i = wave; i < Lq; i += 4) {
-    const long long row = (long long)b * Lq + i;
-    const float qd = bf2f(q[row * ldq + h * D + lane]);
-    const float dod = bf2f(dout[row * ldo + h * D + lane]);
-    const float od = bf2f(outp[row * ldo + h * D + lane]);
+  for (int i = wave; i < d.Lq; i += 4) {
+    const long long row = (long long)b * d.Lq + i;
+    const float qd = ld_io(d, d.q, row * d.ld_q + h * D + lane);
+    const float dod = ld_io(d, d.dout, row * d.ld_o + h * D + lane);
+    const float od = ld_io(d, d.out, row * d.ld_o + h * D + lane);
     const float delta = wave_sum(dod * od);
-    const float l = lse[((long long)b * H + h) * Lq + i];
+    const float l = d.lse[((long long)b * d.H + h) * d.Lq + i];
     float sc[MAXK / 64], dp[MAXK / 64];
 #pragma unroll
     for (int t = 0; t < MAXK / 64; ++t) { sc[t] = 0.f; dp[t] = 0.f; }
     for (int dd = 0; dd < D; ++dd) {
-      const float qv = __shfl(qd, dd, 64) * scale;
+      const float qv = __shfl(qd, dd, 64) * d.scale;
       const float gv = __shfl(dod, dd, 64);
 #pragma unroll
       for (int t = 0; t < MAXK / 64; ++t) {
@@ -123,10 +137,11 @@ __global__ void __launch_bounds__(256) mha_bwd_kernel(const bf16* __restrict__ q
     for (int t = 0; t < MAXK / 64; ++t) {
       const int j = lane + 64 * t;
       if (j < Lk) {
-        const bool keep = !kmask || kmask[(long long)b * Lk + j] != 0;
+        const bool keep = !d.key_mask || d.key_mask[(long long)b * Lk + j] != 0;
         const float p = keep ? __expf(sc[t] - l) : 0.f;
-        ps[wave][j] = p;
-        dss[wave][j] = p * (dp[t] - delta);
+        const float f = drop_factor(d, b, h, i, j, Lk);
+        ps[wave][j] = p * f;                 // dV uses the dropped probabilities
+        dss[wave][j] = p * (f * dp[t] - delta);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -135,43 +150,52 @@ __global__ void __launch_bounds__(256) mha_bwd_kernel(const bf16* __restrict__ q
     for (int j = 0; j < Lk; ++j) {
       const float ds = dss[wave][j];
       g += ds * bf2f(ks[j][lane]);
-      atomicAdd(&dks[j][lane], ds * qd * scale);
+      atomicAdd(&dks[j][lane], ds * qd * d.scale);
       atomicAdd(&dvs[j][lane], ps[wave][j] * dod);
     }
-    dq[row * lddq + h * D + lane] = g * scale;
+    d.dq[row * d.ld_dq + h * D + lane] = g * d.scale;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
   for (int e = threadIdx.x; e < Lk * D; e += 256) {
     const int j = e / D, dd = e % D;
-    dk[b * sdkv + j * lddkv + h * D + dd] = dks[j][dd];
-    dv[b * sdkv + j * lddkv + h * D + dd] = dvs[j][dd];
+    if (j < d.lk1) {
+      const long long o = (long long)(b / d.kv1_bdiv) * d.stride_dkv1_b + (long long)j * d.ld_dkv1 + h * D + dd;
+      atomicAdd(d.dk1 + o, dks[j][dd]);
+      atomicAdd(d.dv1 + o, dvs[j][dd]);
+    } else {
+      const long long o = (long long)(b / d.kv2_bdiv) * d.stride_dkv2_b + (long long)(j - d.lk1) * d.ld_dkv2 + h * D + dd;
+      atomicAdd(d.dk2 + o, dks[j][dd]);
+      atomicAdd(d.dv2 + o, dvs[j][dd]);
+    }
   }
+}
+
+int check(const LrceMhaDesc* d, bool bwd) {
+  if (!d || !d->q || !d->k1 || !d->v1 || !d->out || !d->lse) return lrce_fail(LRCE_E_ARG, "mha: null pointer");
+  if (d->d != D) return lrce_fail(LRCE_E_ARG, "mha: head dim %d unsupported (64)", d->d);
+  if (d->lk2 > 0 && (!d->k2 || !d->v2)) return lrce_fail(LRCE_E_ARG, "mha: second key segment missing");
+  const int Lk = d->lk1 + d->lk2;
+  if (d->lk1 < 1 || Lk > MAXK || d->Lq < 1 || d->B < 1 || d->H < 1) return lrce_fail(LRCE_E_ARG, "mha: Lk=%d unsupported", Lk);
+  if (d->kv1_bdiv < 1 || (d->lk2 > 0 && d->kv2_bdiv < 1)) return lrce_fail(LRCE_E_ARG, "mha: bdiv < 1");
+  if (bwd && (!d->dout || !d->dq || !d->dk1 || !d->dv1 || (d->lk2 > 0 && (!d->dk2 || !d->dv2))))
+    return lrce_fail(LRCE_E_ARG, "mha_bwd: null gradient pointer");
+  return LRCE_OK;
 }
 
 }  // namespace
 
-extern "C" int lrce_mha_fwd(const uint16_t* q, int64_t ld_q, const uint16_t* k, const uint16_t* v, int64_t ld_kv,
-                            int64_t stride_kv_b, const int32_t* key_mask, uint16_t* out, int64_t ld_o, float* lse, int B, int H,
-                            int Lq, int Lk, int d, float scale, void* stream) {
-  if (!q || !k || !v || !out || !lse) return lrce_fail(LRCE_E_ARG, "mha_fwd: null pointer");
-  if (d != D || Lk < 1 || Lk > MAXK || Lq < 1) return lrce_fail(LRCE_E_ARG, "mha_fwd: d=%d Lk=%d unsupported", d, Lk);
-  mha_fwd_kernel<<<B * H, 256, 0, static_cast<hipStream_t>(stream)>>>(
-      reinterpret_cast<const bf16*>(q), ld_q, reinterpret_cast<const bf16*>(k), reinterpret_cast<const bf16*>(v), ld_kv,
-      stride_kv_b, key_mask, reinterpret_cast<bf16*>(out), ld_o, lse, B, H, Lq, Lk, scale);
+extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
+  if (int rc = check(d, false)) return rc;
+  MhaP p{*d};
+  mha_fwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
   return lrce_check_launch("mha_fwd");
 }
 
-extern "C" int lrce_mha_bwd(const uint16_t* q, int64_t ld_q, const uint16_t* k, const uint16_t* v, int64_t ld_kv,
-                            int64_t stride_kv_b, const int32_t* key_mask, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                            const float* lse, float* dq, int64_t ld_dq, float* dk, float* dv, int64_t ld_dkv,
-                            int64_t stride_dkv_b, int B, int H, int Lq, int Lk, int d, float scale, void* stream) {
-  if (!q || !k || !v || !out || !dout || !lse || !dq || !dk || !dv) return lrce_fail(LRCE_E_ARG, "mha_bwd: null pointer");
-  if (d != D || Lk < 1 || Lk > MAXK || Lq < 1) return lrce_fail(LRCE_E_ARG, "mha_bwd: d=%d Lk=%d unsupported", d, Lk);
-  mha_bwd_kernel<<<B * H, 256, 0, static_cast<hipStream_t>(stream)>>>(
-      reinterpret_cast<const bf16*>(q), ld_q, reinterpret_cast<const bf16*>(k), reinterpret_cast<const bf16*>(v), ld_kv,
-      stride_kv_b, key_mask, reinterpret_cast<const bf16*>(out), ld_o, reinterpret_cast<const bf16*>(dout), lse, dq, ld_dq, dk, dv,
-      ld_dkv, stride_dkv_b, B, H, Lq, Lk, scale);
+extern "C" int lrce_mha_bwd(const LrceMhaDesc* d, void* stream) {
+  if (int rc = check(d, true)) return rc;
+  MhaP p{*d};
+  mha_bwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
   return lrce_check_launch("mha_bwd");
 }

@@ -47,6 +47,23 @@ class GemmDesc(ctypes.Structure):
         ("alpha", ctypes.c_float), ("scale_cols", ctypes.c_int32), ("scale_val", ctypes.c_float),
         ("row_scale", ctypes.c_void_p), ("rows_per_scale", ctypes.c_int32),
         ("a_row_scale", ctypes.c_void_p), ("a_rows_per_scale", ctypes.c_int32),
+        ("b_f32", ctypes.c_int32),
+    ]
+
+
+class MhaDesc(ctypes.Structure):
+    _fields_ = [
+        ("q", ctypes.c_void_p), ("ld_q", ctypes.c_int64),
+        ("k1", ctypes.c_void_p), ("v1", ctypes.c_void_p), ("ld_kv1", ctypes.c_int64), ("stride_kv1_b", ctypes.c_int64),
+        ("kv1_bdiv", ctypes.c_int32), ("lk1", ctypes.c_int32),
+        ("k2", ctypes.c_void_p), ("v2", ctypes.c_void_p), ("ld_kv2", ctypes.c_int64), ("stride_kv2_b", ctypes.c_int64),
+        ("kv2_bdiv", ctypes.c_int32), ("lk2", ctypes.c_int32),
+        ("key_mask", ctypes.c_void_p), ("out", ctypes.c_void_p), ("ld_o", ctypes.c_int64), ("lse", ctypes.c_void_p),
+        ("B", ctypes.c_int32), ("H", ctypes.c_int32), ("Lq", ctypes.c_int32), ("d", ctypes.c_int32),
+        ("scale", ctypes.c_float), ("drop_p", ctypes.c_float), ("seed", ctypes.c_uint64), ("f32_io", ctypes.c_int32),
+        ("dout", ctypes.c_void_p), ("dq", ctypes.c_void_p), ("ld_dq", ctypes.c_int64),
+        ("dk1", ctypes.c_void_p), ("dv1", ctypes.c_void_p), ("ld_dkv1", ctypes.c_int64), ("stride_dkv1_b", ctypes.c_int64),
+        ("dk2", ctypes.c_void_p), ("dv2", ctypes.c_void_p), ("ld_dkv2", ctypes.c_int64), ("stride_dkv2_b", ctypes.c_int64),
     ]
 
 
@@ -61,22 +78,21 @@ _U64 = ctypes.c_uint64
 
 _SIGS = {
     "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
-    "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _I, _I, _P],
+    "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _P],
     "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
     "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _P, _P],
     "lrce_wattn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_dbias": [_P, _I, _I, _I, _P, _I, _P, _P],
-    "lrce_mha_fwd": [_P, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _I, _I, _I, _I, _I, _F, _P],
-    "lrce_mha_bwd": [_P, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I64,
-                     _I, _I, _I, _I, _I, _F, _P],
+    "lrce_mha_fwd": [ctypes.POINTER(MhaDesc), _P],
+    "lrce_mha_bwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_patch_im2col": [_P, _I, _I, _I, _I, _I64, _I64, _I64, _I, _P, _P],
     "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _I, _P, _P],
     "lrce_cast_bf16": [_P, _P, _I64, _P],
-    "lrce_dropout": [_P, _P, _P, _I64, _F, _U64, _P],
-    "lrce_dropout_bwd": [_P, _P, _I64, _F, _U64, _P],
+    "lrce_dropout": [_P, _P, _P, _P, _I64, _F, _U64, _I64, _P],
+    "lrce_dropout_bwd": [_P, _P, _I64, _F, _U64, _I64, _P],
     "lrce_bert_embed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
-    "lrce_bert_embed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lrce_bert_embed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I64, _P],
     "lrce_video_posembed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lrce_video_posembed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lrce_text_posembed_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],

@@ -1,0 +1,230 @@
+"""TextExtractor (reference lrce/feature_extractor/text.py:5-17) = BERT-base-uncased encoder on the
+gfx950 kernels.
+
+The reference wraps HF `BertModel.from_pretrained('bert-base-uncased')` (transformers 4.20.1) and
+returns `last_hidden_state`.  This module re-implements that encoder (published algorithm: word +
+position + token-type embeddings -> LN(1e-12) -> 12 post-norm layers of masked 12-head attention
+and a GELU(erf) FFN; dropout 0.1 on embeddings, attention probabilities and both residual
+branches in train mode) with the SAME parameter names (`bert.embeddings.*`, `bert.encoder.layer.i.*`,
+`bert.pooler.dense`), so HF checkpoints load unchanged (`bert.embeddings.position_ids`, a persistent
+buffer in 4.20, is accepted and ignored).  The pooler is kept for the schema but, as in the
+reference (its output is never used by the loss), not computed.  No network fetch: weights come
+from a checkpoint or the caller.
+"""
+import torch
+import torch.nn as nn
+
+from .. import kernels as K
+from ..runtime import ensure
+
+HIDDEN, HEADS, INTER, VOCAB, MAXPOS, TYPES, EPS = 768, 12, 3072, 30522, 512, 2, 1e-12
+
+
+def _g(flat, p):
+    return flat.g32(p) if p.requires_grad else None
+
+
+class BertEmbeddings(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(VOCAB, HIDDEN, padding_idx=0)
+        self.position_embeddings = nn.Embedding(MAXPOS, HIDDEN)
+        self.token_type_embeddings = nn.Embedding(TYPES, HIDDEN)
+        self.LayerNorm = nn.LayerNorm(HIDDEN, eps=EPS)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        state_dict.pop(prefix + "position_ids", None)
+        state_dict.pop(prefix + "token_type_ids", None)
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
+
+class BertSelfAttention(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.query = nn.Linear(HIDDEN, HIDDEN)
+        self.key = nn.Linear(HIDDEN, HIDDEN)
+        self.value = nn.Linear(HIDDEN, HIDDEN)
+
+
+class _DenseLN(nn.Module):
+    def __init__(self, fan_in):
+        super().__init__()
+        self.dense = nn.Linear(fan_in, HIDDEN)
+        self.LayerNorm = nn.LayerNorm(HIDDEN, eps=EPS)
+
+
+class BertAttention(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.self = BertSelfAttention()
+        self.output = _DenseLN(HIDDEN)
+
+
+class BertIntermediate(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.dense = nn.Linear(HIDDEN, INTER)
+
+
+class BertLayer(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.attention = BertAttention()
+        self.intermediate = BertIntermediate()
+        self.output = _DenseLN(INTER)
+
+
+class BertEncoder(nn.Module):
+    def __init__(self, n_layers=12):
+        super().__init__()
+        self.layer = nn.ModuleList([BertLayer() for _ in range(n_layers)])
+
+
+class BertPooler(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.dense = nn.Linear(HIDDEN, HIDDEN)
+
+
+# ----------------------------------------------------------------------------------- autograd
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, types, emb, flat, p, seed, *params):
+        B, L = ids.shape
+        rows = B * L
+        dev = ids.device
+        s = torch.empty(rows, HIDDEN, device=dev)
+        K.bert_embed_fwd(ids, types, emb.word_embeddings.weight, emb.position_embeddings.weight,
+                         emb.token_type_embeddings.weight, s, rows, L, HIDDEN)
+        x, mean, rstd = K.layernorm(s, emb.LayerNorm.weight, emb.LayerNorm.bias, EPS, out_f32=True)
+        y = K.dropout(x, p, seed) if p > 0 else x
+        ctx.save = (ids, types, s, mean, rstd)
+        ctx.emb, ctx.flat, ctx.p, ctx.seed, ctx.L = emb, flat, p, seed, L
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ids, types, s, mean, rstd = ctx.save
+        emb, flat = ctx.emb, ctx.flat
+        dy = dy.contiguous()
+        dx = K.dropout_bwd(dy, ctx.p, ctx.seed) if ctx.p > 0 else dy
+        ds = torch.empty_like(s)
+        K.layernorm_bwd(dx, s, mean, rstd, emb.LayerNorm.weight, ds, dw=_g(flat, emb.LayerNorm.weight),
+                        db=_g(flat, emb.LayerNorm.bias))
+        gw, gp, gt = (_g(flat, emb.word_embeddings.weight), _g(flat, emb.position_embeddings.weight),
+                      _g(flat, emb.token_type_embeddings.weight))
+        if gw is not None and gp is not None and gt is not None:
+            K.bert_embed_bwd(ds, ids, types, gw, gp, gt, s.shape[0], ctx.L, HIDDEN)
+        ctx.save = None
+        return (None,) * (6 + len(ctx.needs_input_grad[6:]))
+
+
+class _LayerFn(torch.autograd.Function):
+    """One post-norm BERT layer (HF BertLayer): x -> LN(x + drop(attn_out)) -> LN(. + drop(FFN))."""
+
+    @staticmethod
+    def forward(ctx, x, mask, layer, flat, p, seed, B, L, *params):
+        dev = x.device
+        rows = B * L
+        sa, ao, it, oo = layer.attention.self, layer.attention.output, layer.intermediate, layer.output
+        xb = torch.empty(rows, HIDDEN, dtype=torch.bfloat16, device=dev)
+        K.cast_bf16(x, xb)
+        q = K.linear(xb, flat.w16(sa.query.weight), sa.query.bias)
+        k = K.linear(xb, flat.w16(sa.key.weight), sa.key.bias)
+        v = K.linear(xb, flat.w16(sa.value.weight), sa.value.bias)
+        ctxt = torch.empty(rows, HIDDEN, dtype=torch.bfloat16, device=dev)
+        lse = torch.empty(B, HEADS, L, device=dev)
+        desc = K.mha_desc(q, L, k1=k, v1=v, lk1=L, ld_kv1=HIDDEN, stride_kv1_b=L * HIDDEN, key_mask=mask, out=ctxt,
+                          lse=lse, B=B, H=HEADS, scale=0.125, drop_p=p, seed=seed)
+        K.mha_fwd(desc, ctxt)
+        a = K.linear(ctxt, flat.w16(ao.dense.weight), ao.dense.bias, out_f32=True)
+        a2 = K.dropout(a, p, seed + 1, res=x)
+        h1b = torch.empty(rows, HIDDEN, dtype=torch.bfloat16, device=dev)
+        h1, m1, r1 = K.layernorm(a2, ao.LayerNorm.weight, ao.LayerNorm.bias, EPS, out_f32=True, bf16_copy=h1b)
+        pre = torch.empty(rows, INTER, dtype=torch.bfloat16, device=dev)
+        g = K.linear(h1b, flat.w16(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre)
+        o = K.linear(g, flat.w16(oo.dense.weight), oo.dense.bias, out_f32=True)
+        o2 = K.dropout(o, p, seed + 2, res=h1)
+        out, m2, r2 = K.layernorm(o2, oo.LayerNorm.weight, oo.LayerNorm.bias, EPS, out_f32=True)
+        ctx.save = (xb, q, k, v, mask, ctxt, lse, a2, m1, r1, h1b, pre, g, o2, m2, r2)
+        ctx.desc = desc
+        ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L = layer, flat, p, seed, B, L
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xb, q, k, v, mask, ctxt, lse, a2, m1, r1, h1b, pre, g, o2, m2, r2 = ctx.save
+        layer, flat, p, seed, B, L = ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L
+        sa, ao, it, oo = layer.attention.self, layer.attention.output, layer.intermediate, layer.output
+        dout = dout.contiguous()
+        do2 = torch.empty_like(o2)
+        K.layernorm_bwd(dout, o2, m2, r2, oo.LayerNorm.weight, do2, dw=_g(flat, oo.LayerNorm.weight),
+                        db=_g(flat, oo.LayerNorm.bias))
+        do = K.dropout_bwd(do2, p, seed + 2) if p > 0 else do2
+        _wgrad(flat, oo.dense, do, g)
+        dh1 = K.linear_dx(do, flat.w16(oo.dense.weight), out_f32=True, dgelu_pre=pre)   # d(pre) in f32
+        _wgrad(flat, it.dense, dh1, h1b)
+        dh1x = K.linear_dx(dh1, flat.w16(it.dense.weight), resid=do2)
+        da2 = torch.empty_like(a2)
+        K.layernorm_bwd(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, dw=_g(flat, ao.LayerNorm.weight),
+                        db=_g(flat, ao.LayerNorm.bias))
+        da = K.dropout_bwd(da2, p, seed + 1) if p > 0 else da2
+        _wgrad(flat, ao.dense, da, ctxt)
+        dctx = K.linear_dx(da, flat.w16(ao.dense.weight), out_f32=False)
+        rows = B * L
+        dq = torch.empty(rows, HIDDEN, device=dout.device)
+        dk = torch.zeros(rows, HIDDEN, device=dout.device)
+        dv = torch.zeros(rows, HIDDEN, device=dout.device)
+        K.mha_bwd(ctx.desc, dout=dctx, dq=dq, dk1=dk, dv1=dv, ld_dkv1=HIDDEN, stride_dkv1_b=L * HIDDEN)
+        for lin, dg in ((sa.query, dq), (sa.key, dk), (sa.value, dv)):
+            _wgrad(flat, lin, dg, xb)
+        dx = K.linear_dx(dq, flat.w16(sa.query.weight), resid=da2)
+        K.linear_dx(dk, flat.w16(sa.key.weight), out=dx, accumulate=True)
+        K.linear_dx(dv, flat.w16(sa.value.weight), out=dx, accumulate=True)
+        ctx.save = ctx.desc = None
+        return (dx,) + (None,) * (7 + len(ctx.needs_input_grad[8:]))
+
+
+def _wgrad(flat, lin, dy, x16):
+    gw = _g(flat, lin.weight)
+    if gw is not None:
+        K.linear_dw(dy, x16, gw)
+    if lin.bias is not None:
+        gb = _g(flat, lin.bias)
+        if gb is not None:
+            K.colsum(dy, gb)
+
+
+class BertModel(nn.Module):
+    def __init__(self, n_layers=12, hidden_dropout=0.1, attention_dropout=0.1):
+        super().__init__()
+        self.embeddings = BertEmbeddings()
+        self.encoder = BertEncoder(n_layers)
+        self.pooler = BertPooler()
+        self.hidden_dropout, self.attention_dropout = hidden_dropout, attention_dropout
+        if hidden_dropout != attention_dropout:
+            raise ValueError("bert-base uses one dropout rate (0.1) for hidden states and attention probs")
+
+    def forward(self, input_ids, attention_mask=None, token_type_ids=None):
+        flat = ensure(self)
+        B, L = input_ids.shape
+        dev = input_ids.device
+        ids = input_ids.contiguous().to(torch.int64)
+        types = (token_type_ids if token_type_ids is not None else torch.zeros_like(ids)).contiguous().to(torch.int64)
+        mask = (attention_mask if attention_mask is not None else torch.ones_like(ids)).to(torch.int32).contiguous()
+        p = self.hidden_dropout if self.training else 0.0
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+        anchor = [t for t in self.embeddings.parameters()]
+        x = _EmbedFn.apply(ids, types, self.embeddings, flat, p, seed, *anchor)
+        for i, layer in enumerate(self.encoder.layer):
+            x = _LayerFn.apply(x, mask, layer, flat, p, seed + 16 * (i + 1), B, L, *layer.parameters())
+        return x.view(B, L, HIDDEN)
+
+
+class TextExtractor(nn.Module):
+    def __init__(self, bert=None):
+        super().__init__()
+        self.bert = bert if bert is not None else BertModel()
+
+    def forward(self, input_ids, attention_mask, token_type_ids):
+        return self.bert(input_ids, attention_mask, token_type_ids)

@@ -31,10 +31,11 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
          scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, a_row_scale=None, a_rows_per_scale=1,
          batch=1, stride_a=0, stride_b=0, stride_c=0):
     """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc."""
-    _chk(a, None, "A"); _chk(b, BF16, "B"); _chk(c, None, "C")
+    _chk(a, None, "A"); _chk(b, None, "B"); _chk(c, None, "C")
     a_f32 = a.dtype == F32
-    if not a_f32 and a.dtype != BF16:
-        raise N.NativeError("gemm: A must be bf16 or f32")
+    b_f32 = b.dtype == F32
+    if (not a_f32 and a.dtype != BF16) or (not b_f32 and b.dtype != BF16):
+        raise N.NativeError("gemm: operands must be bf16 or f32")
     if lda is None:
         lda = k if a_kmajor else m
     if ldb is None:
@@ -54,6 +55,7 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.alpha, d.scale_cols, d.scale_val = alpha, scale_cols, scale_val
     d.row_scale, d.rows_per_scale = ptr(row_scale), rows_per_scale
     d.a_row_scale, d.a_rows_per_scale = ptr(a_row_scale), a_rows_per_scale
+    d.b_f32 = int(b_f32)
     call("lrce_gemm", ctypes.byref(d), stream_of(c))
 
 
@@ -94,19 +96,23 @@ def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None
 
 
 def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows=None, a_row_scale=None,
-              a_rows_per_scale=1, accumulate=False):
-    """dX = dY W ; dY [M,N] (bf16/f32), W [N,K] bf16 -> [M,K]; optional *gelu'(pre)."""
+              a_rows_per_scale=1, accumulate=False, resid=None):
+    """dX = dY W (+ resid) ; dY [M,N] (bf16/f32), W [N,K] bf16 -> [M,K]; optional *gelu'(pre)."""
     M = rows if rows is not None else dy.shape[0]
     Nn, K = w.shape
     flags = 0
     if dgelu_pre is not None:
         flags |= N.EPI_DGELU
+    if resid is not None:
+        assert dgelu_pre is None
+        flags |= N.EPI_RESID
     if out is None:
         out = torch.empty((M, K), dtype=F32 if out_f32 else BF16, device=dy.device)
     if out.dtype == F32:
         flags |= N.EPI_ACCUM if accumulate else N.EPI_OUT_F32
     gemm(dy, w, out, M, K, Nn, a_kmajor=True, b_kmajor=False, lda=dy.shape[-1], ldb=K, flags=flags,
-         aux=dgelu_pre, ld_aux=K, a_map=a_map, a_row_scale=a_row_scale, a_rows_per_scale=a_rows_per_scale)
+         aux=dgelu_pre if dgelu_pre is not None else resid, ld_aux=K, a_map=a_map, a_row_scale=a_row_scale,
+         a_rows_per_scale=a_rows_per_scale)
     return out
 
 
@@ -127,7 +133,7 @@ def colsum(x, out, *, row_map=None, rows=None, row_scale=None, rows_per_scale=1)
 
 
 def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out_map=None, rows=None, cols=None,
-              stats=True, out_rows=None):
+              stats=True, out_rows=None, bf16_copy=None):
     R = rows if rows is not None else x.shape[0]
     Cc = cols if cols is not None else x.shape[-1] * nseg
     if out is None:
@@ -135,7 +141,7 @@ def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out
     mean = torch.empty(R, dtype=F32, device=x.device) if stats else None
     rstd = torch.empty(R, dtype=F32, device=x.device) if stats else None
     call("lrce_layernorm_fwd", ptr(x), int(x.dtype == F32), ptr(in_map), nseg, ptr(w), ptr(b), eps, ptr(out),
-         int(out.dtype == F32), ptr(out_map), ptr(mean), ptr(rstd), R, Cc, stream_of(out))
+         int(out.dtype == F32), ptr(bf16_copy), ptr(out_map), ptr(mean), ptr(rstd), R, Cc, stream_of(out))
     return out, mean, rstd
 
 
@@ -174,15 +180,33 @@ def wattn_dbias(ds, n_win, n, nH, index, table_grad):
     call("lrce_wattn_dbias", ptr(ds), n_win, n, nH, ptr(index), index.shape[-1], ptr(table_grad), stream_of(table_grad))
 
 
-def mha_fwd(q, ld_q, k, v, ld_kv, stride_kv_b, key_mask, out, ld_o, lse, B, H, Lq, Lk, d, scale):
-    call("lrce_mha_fwd", ptr(q), ld_q, ptr(k), ptr(v), ld_kv, stride_kv_b, ptr(key_mask), ptr(out), ld_o, ptr(lse),
-         B, H, Lq, Lk, d, scale, stream_of(out))
+def mha_desc(q, Lq, *, k1, v1, lk1, ld_kv1, stride_kv1_b, kv1_bdiv=1, k2=None, v2=None, lk2=0, ld_kv2=0,
+             stride_kv2_b=0, kv2_bdiv=1, key_mask=None, out, lse, B, H, scale, ld_q=None, ld_o=None, drop_p=0.0,
+             seed=0, d=64):
+    m = N.MhaDesc()
+    m.q, m.ld_q = ptr(q), ld_q if ld_q is not None else H * d
+    m.k1, m.v1, m.ld_kv1, m.stride_kv1_b, m.kv1_bdiv, m.lk1 = ptr(k1), ptr(v1), ld_kv1, stride_kv1_b, kv1_bdiv, lk1
+    m.k2, m.v2, m.ld_kv2, m.stride_kv2_b, m.kv2_bdiv, m.lk2 = ptr(k2), ptr(v2), ld_kv2, stride_kv2_b, kv2_bdiv, lk2
+    m.key_mask, m.out, m.ld_o, m.lse = ptr(key_mask), ptr(out), ld_o if ld_o is not None else H * d, ptr(lse)
+    m.B, m.H, m.Lq, m.d, m.scale = B, H, Lq, d, scale
+    m.drop_p, m.seed = float(drop_p), seed & (2 ** 64 - 1)
+    m.f32_io = int(q.dtype == F32)
+    if (out.dtype == F32) != (q.dtype == F32):
+        raise N.NativeError("mha: q and out must share dtype (bf16, or f32 for the decoder path)")
+    return m
 
 
-def mha_bwd(q, ld_q, k, v, ld_kv, stride_kv_b, key_mask, out, ld_o, dout, lse, dq, ld_dq, dk, dv, ld_dkv,
-            stride_dkv_b, B, H, Lq, Lk, d, scale):
-    call("lrce_mha_bwd", ptr(q), ld_q, ptr(k), ptr(v), ld_kv, stride_kv_b, ptr(key_mask), ptr(out), ld_o, ptr(dout),
-         ptr(lse), ptr(dq), ld_dq, ptr(dk), ptr(dv), ld_dkv, stride_dkv_b, B, H, Lq, Lk, d, scale, stream_of(dq))
+def mha_fwd(desc, stream_tensor):
+    call("lrce_mha_fwd", ctypes.byref(desc), stream_of(stream_tensor))
+
+
+def mha_bwd(desc, *, dout, dq, dk1, dv1, ld_dkv1, stride_dkv1_b, dk2=None, dv2=None, ld_dkv2=0, stride_dkv2_b=0,
+            ld_dq=None):
+    desc.dout, desc.dq = ptr(dout), ptr(dq)
+    desc.ld_dq = ld_dq if ld_dq is not None else desc.H * desc.d
+    desc.dk1, desc.dv1, desc.ld_dkv1, desc.stride_dkv1_b = ptr(dk1), ptr(dv1), ld_dkv1, stride_dkv1_b
+    desc.dk2, desc.dv2, desc.ld_dkv2, desc.stride_dkv2_b = ptr(dk2), ptr(dv2), ld_dkv2, stride_dkv2_b
+    call("lrce_mha_bwd", ctypes.byref(desc), stream_of(dq))
 
 
 def patch_im2col(clips, patches, *, layout="BSTCHW", normalize=True):
@@ -201,17 +225,19 @@ def cast_bf16(x, y):
     call("lrce_cast_bf16", ptr(x), ptr(y), x.numel(), stream_of(y))
 
 
-def dropout(x, p, seed, out=None, out_bf16=None):
+def dropout(x, p, seed, out=None, out_bf16=None, res=None, group=1):
+    """y = res + dropout(x) (train-mode nn.Dropout semantics, counter-hash mask)."""
     if out is None:
         out = torch.empty_like(x)
-    call("lrce_dropout", ptr(x), ptr(out), ptr(out_bf16), x.numel(), float(p), seed & (2 ** 64 - 1), stream_of(out))
+    call("lrce_dropout", ptr(x), ptr(res), ptr(out), ptr(out_bf16), x.numel(), float(p), seed & (2 ** 64 - 1), group,
+         stream_of(out))
     return out
 
 
-def dropout_bwd(dy, p, seed, out=None):
+def dropout_bwd(dy, p, seed, out=None, group=1):
     if out is None:
         out = torch.empty_like(dy)
-    call("lrce_dropout_bwd", ptr(dy), ptr(out), dy.numel(), float(p), seed & (2 ** 64 - 1), stream_of(out))
+    call("lrce_dropout_bwd", ptr(dy), ptr(out), dy.numel(), float(p), seed & (2 ** 64 - 1), group, stream_of(out))
     return out
 
 
@@ -219,8 +245,8 @@ def bert_embed_fwd(ids, types, word, pos, typ, out, rows, L, C):
     call("lrce_bert_embed_fwd", ptr(ids), ptr(types), ptr(word), ptr(pos), ptr(typ), ptr(out), rows, L, C, stream_of(out))
 
 
-def bert_embed_bwd(dout, ids, types, dword, dpos, dtyp, rows, L, C):
-    call("lrce_bert_embed_bwd", ptr(dout), ptr(ids), ptr(types), ptr(dword), ptr(dpos), ptr(dtyp), rows, L, C,
+def bert_embed_bwd(dout, ids, types, dword, dpos, dtyp, rows, L, C, pad_id=0):
+    call("lrce_bert_embed_bwd", ptr(dout), ptr(ids), ptr(types), ptr(dword), ptr(dpos), ptr(dtyp), rows, L, C, pad_id,
          stream_of(dout))
 
 

@@ -1,0 +1,71 @@
+"""End-to-end LRCE models (reference lrce/models/e2e.py) on the gfx950 path.
+
+Same classes, constructor signatures (positional as train_ddp.py:89-98, keyword as eval.py:66-74),
+attributes (`text_extractor`, `video_extractor`, `fusion_model`) and forward contract:
+    forward(video_clips (B,S,T,3,H,W) f32, texts (B,L)|(B,5,L) int64, texts_attention_mask,
+            texts_type_ids) -> (B,num_classes) | (B,5) | (B,)
+The reference asserts the Kinetics-600 Swin checkpoint exists (e2e.py:11) and downloads BERT by
+name (text.py:9); this build loads the checkpoint when present and otherwise keeps its own
+initialisation (synthetic benchmarking / tests), and never touches the network.
+"""
+from typing import Iterable, List
+
+import torch
+import torch.nn as nn
+
+from ..feature_extractor.text import TextExtractor
+from ..feature_extractor.video import VideoExtractor, SWIN_B_CKPT
+from ..runtime import prepare
+from .fusionv3 import LRCEOpenEnded, LRCEMultipleChoice, LRCECount
+
+
+class E2EBase(nn.Module):
+    def __init__(self, swin_ckpt=SWIN_B_CKPT) -> None:
+        super().__init__()
+        self.text_extractor = TextExtractor()
+        self.video_extractor = VideoExtractor(swin_ckpt)
+
+    def extract_text_features(self, texts, attention_mask, texts_type_ids):
+        return self.text_extractor(texts, attention_mask, texts_type_ids)
+
+    def extract_video_features(self, video_clips):
+        return self.video_extractor(video_clips)
+
+    def forward(self, video_clips, texts, texts_attention_mask, texts_type_ids):
+        prepare(self)
+        video_features = self.extract_video_features(video_clips)
+        texts_features = self.extract_text_features(texts, texts_attention_mask, texts_type_ids)
+        return self.fusion_model(video_features, texts_features, texts_attention_mask)
+
+
+class E2EOpenEnded(E2EBase):
+    def __init__(self, feature_dim: int, num_classes: int, drop_out_rate: float = 0.1,
+                 video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
+                 temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 30) -> None:
+        super().__init__()
+        self.fusion_model = LRCEOpenEnded(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
+                                          frame_sample_size, temporal_scale, text_seq_len)
+
+
+class E2EMultipleChoice(E2EBase):
+    def __init__(self, feature_dim: int, num_classes: int, drop_out_rate: float = 0.1,
+                 video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
+                 temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 40) -> None:
+        super().__init__()
+        self.fusion_model = LRCEMultipleChoice(feature_dim, num_classes, drop_out_rate, video_feature_res,
+                                               video_feature_dim, frame_sample_size, temporal_scale, text_seq_len)
+
+    def extract_text_features(self, texts, attention_mask, texts_type_ids):
+        """e2e.py:77-81: the 5 question+answer sequences go through BERT as B*5 rows."""
+        batch_size, total_choice, seq_len = texts.shape
+        out = self.text_extractor(texts.flatten(0, 1), attention_mask.flatten(0, 1), texts_type_ids.flatten(0, 1))
+        return out.view(batch_size, total_choice, seq_len, -1)
+
+
+class E2ECount(E2EBase):
+    def __init__(self, feature_dim: int, num_classes: int = 1, drop_out_rate: float = 0.1,
+                 video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
+                 temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 30) -> None:
+        super().__init__()
+        self.fusion_model = LRCECount(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
+                                      frame_sample_size, temporal_scale, text_seq_len)

@@ -1,0 +1,364 @@
+"""LRCE fusion (reference lrce/models/fusionv3.py) on the gfx950 kernels.
+
+FusionTransformer (fusionv3.py:5-51): a learned summary token is refined recurrently, one clip at a
+time: s <- Dropout(LN(s + Decoder12(s, [video_clip_i ; question]))).  The decoder is
+nn.TransformerDecoder(12 x TransformerDecoderLayer(768, 12 heads, FFN 3072, GELU, post-norm,
+eps 1e-12, dropout p)); parameter names are kept (`transformer.layers.k.self_attn.in_proj_weight`,
+`multihead_attn.*`, `linear1/2`, `norm1..3`, `fusion_layer_norm`, `summarization_token`).
+
+Execution re-design (same math):
+* the memory never depends on the summary token, so its K/V projections are computed up front with
+  one MFMA GEMM per layer over ALL clips (and the question tokens ONCE for every step, instead of
+  once per step); the MC head shares the video K/V across the 5 choices (fusionv3.py:259);
+* self-attention over a single query token is softmax over one key == 1, so it is exactly
+  out_proj(v_proj(s)) (+ the attention-weight dropout, one mask per head);
+* the whole S x 12 recurrence is ONE autograd node: dK/dV accumulate in f32 across steps inside its
+  backward and the projection weight gradients are taken once per layer.
+`texts_attention_mask` is accepted and ignored exactly like the reference (no key-padding mask).
+"""
+from typing import Iterable, List
+
+import torch
+import torch.nn as nn
+
+from .. import kernels as K
+from ..runtime import ensure
+from .embedding import TextPosEmbed, VideoPosEmbed, VideoEmbedFn, TextEmbedFn, init_weight
+
+EPS = 1e-12
+E = 768
+NHEAD = 12
+FF = 3072
+
+
+def _g(flat, p):
+    return flat.g32(p) if p.requires_grad else None
+
+
+def _rows(t, a, b):
+    return t[a:b] if t is not None else None
+
+
+def _wgrad(flat, w, b, dy, x16, rows=None):
+    """dW (+)= dy^T x16 (rows [a,b) of a stacked weight if given), db (+)= colsum(dy)."""
+    gw = _g(flat, w)
+    if gw is not None:
+        if rows is not None:
+            gw = gw[rows[0]:rows[1]]
+        n = gw.shape[0]
+        if n % 8:
+            dyp = torch.nn.functional.pad(dy, (0, 8 - n % 8))
+            tmp = torch.zeros(dyp.shape[1], gw.shape[1], device=dy.device)
+            K.linear_dw(dyp, x16, tmp)
+            gw.add_(tmp[:n])
+        else:
+            K.linear_dw(dy, x16, gw)
+    if b is not None:
+        gb = _g(flat, b)
+        if gb is not None:
+            if rows is not None:
+                gb = gb[rows[0]:rows[1]]
+            K.colsum(dy, gb)
+
+
+class MultiheadAttentionParams(nn.Module):
+    """Parameter container with nn.MultiheadAttention's names (in_proj_weight/bias, out_proj)."""
+
+    def __init__(self, embed_dim, num_heads):
+        super().__init__()
+        self.embed_dim, self.num_heads = embed_dim, num_heads
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * embed_dim, embed_dim))
+        self.in_proj_bias = nn.Parameter(torch.zeros(3 * embed_dim))
+        self.out_proj = nn.Linear(embed_dim, embed_dim)
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        nn.init.zeros_(self.out_proj.bias)
+
+
+class TransformerDecoderLayer(nn.Module):
+    def __init__(self, d_model=E, nhead=NHEAD, dim_feedforward=FF, dropout=0.1):
+        super().__init__()
+        self.self_attn = MultiheadAttentionParams(d_model, nhead)
+        self.multihead_attn = MultiheadAttentionParams(d_model, nhead)
+        self.linear1 = nn.Linear(d_model, dim_feedforward)
+        self.linear2 = nn.Linear(dim_feedforward, d_model)
+        self.norm1 = nn.LayerNorm(d_model, eps=EPS)
+        self.norm2 = nn.LayerNorm(d_model, eps=EPS)
+        self.norm3 = nn.LayerNorm(d_model, eps=EPS)
+        self.dropout_p = dropout
+
+
+class TransformerDecoder(nn.Module):
+    def __init__(self, num_layers, dropout):
+        super().__init__()
+        self.layers = nn.ModuleList([TransformerDecoderLayer(dropout=dropout) for _ in range(num_layers)])
+        self.num_layers = num_layers
+
+
+# ----------------------------------------------------------------------------------- decoder
+class _Step:
+    """Saved activations of one (step, layer)."""
+    __slots__ = ("x0", "sad", "x1p", "m1", "r1", "x1", "q", "ctx", "lse", "desc", "x2p", "m2", "r2", "x2", "pre",
+                 "gd", "x3p", "m3", "r3")
+
+
+def _layer_fwd(lay, flat, x0, kvv, kvt, step, S, Lt, nmc, p, seed, save):
+    """One TransformerDecoderLayer (post-norm) on the summary-token rows x0 (Bq, E) f32.
+    Query-side linears run on the exact-f32 MFMA path with the f32 master weights (M = Bq is tiny,
+    the recurrence is precision-critical); only the memory K/V (big-M GEMMs) are bf16."""
+    sa, ca = lay.self_attn, lay.multihead_attn
+    # self-attention over one token: out_proj(dropout_head(v_proj(x)))
+    sad = K.linear(x0, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out_f32=True)
+    K.dropout(sad, p, seed, out=sad, group=E // NHEAD)
+    sao = K.linear(sad, sa.out_proj.weight, sa.out_proj.bias, out_f32=True)
+    x1p = K.dropout(sao, p, seed + 1, res=x0)
+    x1, m1, r1 = K.layernorm(x1p, lay.norm1.weight, lay.norm1.bias, EPS, out_f32=True)
+    # cross-attention to [video tokens of this step ; question tokens]
+    q = K.linear(x1, ca.in_proj_weight[:E], ca.in_proj_bias[:E], out_f32=True)
+    Bq = x0.shape[0]
+    ctx = torch.empty(Bq, E, device=x0.device)
+    lse = torch.empty(Bq, NHEAD, 1, device=x0.device)
+    lv = 150
+    kv1 = kvv[step * lv * 2 * E:]
+    desc = K.mha_desc(q, 1, k1=kv1, v1=kv1[E:], lk1=lv, ld_kv1=2 * E, stride_kv1_b=S * lv * 2 * E, kv1_bdiv=nmc,
+                      k2=kvt, v2=kvt[E:], lk2=Lt, ld_kv2=2 * E, stride_kv2_b=Lt * 2 * E, kv2_bdiv=1, out=ctx, lse=lse,
+                      B=Bq, H=NHEAD, scale=(E // NHEAD) ** -0.5, drop_p=p, seed=seed + 2)
+    K.mha_fwd(desc, ctx)
+    cao = K.linear(ctx, ca.out_proj.weight, ca.out_proj.bias, out_f32=True)
+    x2p = K.dropout(cao, p, seed + 3, res=x1)
+    x2, m2, r2 = K.layernorm(x2p, lay.norm2.weight, lay.norm2.bias, EPS, out_f32=True)
+    # FFN: linear2(dropout(gelu(linear1(x))))
+    pre = torch.empty(Bq, FF, dtype=torch.bfloat16, device=x0.device)
+    gd = K.linear(x2, lay.linear1.weight, lay.linear1.bias, gelu=True, pre_out=pre, out_f32=True)
+    K.dropout(gd, p, seed + 4, out=gd)
+    f = K.linear(gd, lay.linear2.weight, lay.linear2.bias, out_f32=True)
+    x3p = K.dropout(f, p, seed + 5, res=x2)
+    x3, m3, r3 = K.layernorm(x3p, lay.norm3.weight, lay.norm3.bias, EPS, out_f32=True)
+    if save is not None:
+        st = _Step()
+        st.x0, st.sad, st.x1p, st.m1, st.r1, st.x1, st.q, st.ctx, st.lse, st.desc = \
+            x0, sad, x1p, m1, r1, x1, q, ctx, lse, desc
+        st.x2p, st.m2, st.r2, st.x2, st.pre, st.gd, st.x3p, st.m3, st.r3 = x2p, m2, r2, x2, pre, gd, x3p, m3, r3
+        save.append(st)
+    return x3
+
+
+def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed):
+    """Backward of _layer_fwd; accumulates into the layer's dK/dV buffers, returns d(x0)."""
+    sa, ca = lay.self_attn, lay.multihead_attn
+    Bq = dx3.shape[0]
+    dx3p = torch.empty_like(st.x3p)
+    K.layernorm_bwd(dx3, st.x3p, st.m3, st.r3, lay.norm3.weight, dx3p, dw=_g(flat, lay.norm3.weight),
+                    db=_g(flat, lay.norm3.bias))
+    df = K.dropout_bwd(dx3p, p, seed + 5) if p > 0 else dx3p
+    _wgrad(flat, lay.linear2.weight, lay.linear2.bias, df, st.gd)
+    dgp = K.linear_dx(df, lay.linear2.weight, dgelu_pre=st.pre)
+    if p > 0:
+        K.dropout_bwd(dgp, p, seed + 4, out=dgp)
+    _wgrad(flat, lay.linear1.weight, lay.linear1.bias, dgp, st.x2)
+    dx2 = K.linear_dx(dgp, lay.linear1.weight, resid=dx3p)
+    dx2p = torch.empty_like(st.x2p)
+    K.layernorm_bwd(dx2, st.x2p, st.m2, st.r2, lay.norm2.weight, dx2p, dw=_g(flat, lay.norm2.weight),
+                    db=_g(flat, lay.norm2.bias))
+    dcao = K.dropout_bwd(dx2p, p, seed + 3) if p > 0 else dx2p
+    _wgrad(flat, ca.out_proj.weight, ca.out_proj.bias, dcao, st.ctx)
+    dctx = K.linear_dx(dcao, ca.out_proj.weight)
+    dq = torch.empty(Bq, E, device=dx3.device)
+    K.mha_bwd(st.desc, dout=dctx, dq=dq, dk1=dkvv_step, dv1=dkvv_step[E:], ld_dkv1=2 * E,
+              stride_dkv1_b=S * 150 * 2 * E, dk2=dkvt, dv2=dkvt[E:], ld_dkv2=2 * E, stride_dkv2_b=Lt * 2 * E)
+    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dq, st.x1, rows=(0, E))
+    dx1 = K.linear_dx(dq, ca.in_proj_weight[:E], resid=dx2p)
+    dx1p = torch.empty_like(st.x1p)
+    K.layernorm_bwd(dx1, st.x1p, st.m1, st.r1, lay.norm1.weight, dx1p, dw=_g(flat, lay.norm1.weight),
+                    db=_g(flat, lay.norm1.bias))
+    dsao = K.dropout_bwd(dx1p, p, seed + 1) if p > 0 else dx1p
+    _wgrad(flat, sa.out_proj.weight, sa.out_proj.bias, dsao, st.sad)
+    dsav = K.linear_dx(dsao, sa.out_proj.weight)
+    if p > 0:
+        K.dropout_bwd(dsav, p, seed, out=dsav, group=E // NHEAD)
+    _wgrad(flat, sa.in_proj_weight, sa.in_proj_bias, dsav, st.x0, rows=(2 * E, 3 * E))
+    return K.linear_dx(dsav, sa.in_proj_weight[2 * E:], resid=dx1p)
+
+
+class _RecurrentDecoderFn(torch.autograd.Function):
+    """FusionTransformer.forward (fusionv3.py:27-51) as one autograd node."""
+
+    @staticmethod
+    def forward(ctx, v, v16, t, t16, ft, flat, p, seed, B, S, nmc, *params):
+        dev = v.device
+        layers = ft.transformer.layers
+        Lt = t.shape[1]
+        Bq = t.shape[0]
+        rows_v = B * S * 150
+        v16 = v16.view(rows_v, E)
+        t16 = t16.view(Bq * Lt, E)
+        kvv, kvt = [], []
+        for lay in layers:
+            ca = lay.multihead_attn
+            w = flat.w16(ca.in_proj_weight)[E:]
+            kvv.append(K.linear(v16, w, ca.in_proj_bias[E:]))
+            kvt.append(K.linear(t16, w, ca.in_proj_bias[E:]))
+        s = ft.summarization_token.detach().reshape(1, E).expand(Bq, E).contiguous()
+        saves = []
+        fused = []
+        for i in range(S):
+            x = s
+            step_saves = []
+            for l, lay in enumerate(layers):
+                x = _layer_fwd(lay, flat, x, kvv[l].view(-1), kvt[l].view(-1), i, S, Lt, nmc, p,
+                               seed + 64 * (i * len(layers) + l), step_saves)
+            tsum = K.dropout(x, 0.0, 0, res=s)
+            u, mu, ru = K.layernorm(tsum, ft.fusion_layer_norm.weight, ft.fusion_layer_norm.bias, EPS, out_f32=True)
+            s = K.dropout(u, p, seed + 7 + 64 * 1000 * (i + 1))
+            saves.append(step_saves)
+            fused.append((tsum, mu, ru))
+        ctx.save = (kvv, kvt, saves, fused, v16, t16)
+        ctx.ft, ctx.flat, ctx.p, ctx.seed, ctx.dims = ft, flat, p, seed, (B, S, nmc, Bq, Lt)
+        return s
+
+    @staticmethod
+    def backward(ctx, ds):
+        kvv, kvt, saves, fused, v16, t16 = ctx.save
+        ft, flat, p, seed = ctx.ft, ctx.flat, ctx.p, ctx.seed
+        B, S, nmc, Bq, Lt = ctx.dims
+        layers = ft.transformer.layers
+        dev = ds.device
+        dkvv = [torch.zeros(B * S * 150, 2 * E, device=dev) for _ in layers]
+        dkvt = [torch.zeros(Bq * Lt, 2 * E, device=dev) for _ in layers]
+        ds = ds.contiguous()
+        for i in reversed(range(S)):
+            tsum, mu, ru = fused[i]
+            du = K.dropout_bwd(ds, p, seed + 7 + 64 * 1000 * (i + 1)) if p > 0 else ds
+            dt = torch.empty_like(tsum)
+            K.layernorm_bwd(du, tsum, mu, ru, ft.fusion_layer_norm.weight, dt, dw=_g(flat, ft.fusion_layer_norm.weight),
+                            db=_g(flat, ft.fusion_layer_norm.bias))
+            dx = dt
+            for l in reversed(range(len(layers))):
+                dx = _layer_bwd(layers[l], flat, saves[i][l], dx, dkvv[l].view(-1)[i * 150 * 2 * E:],
+                                dkvt[l].view(-1), S, Lt, p, seed + 64 * (i * len(layers) + l))
+            ds = K.dropout(dx, 0.0, 0, res=dt)   # s fed both the residual and the decoder
+            saves[i] = None
+        gt = _g(flat, ft.summarization_token)
+        if gt is not None:
+            K.colsum(ds, gt.view(E))
+        dv = torch.zeros(B * S * 150, E, device=dev)
+        dtt = torch.zeros(Bq * Lt, E, device=dev)
+        for l, lay in enumerate(layers):
+            ca = lay.multihead_attn
+            _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dkvv[l], v16, rows=(E, 3 * E))
+            _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dkvt[l], t16, rows=(E, 3 * E))
+            w = flat.w16(ca.in_proj_weight)[E:]
+            K.linear_dx(dkvv[l], w, out=dv, accumulate=True)
+            K.linear_dx(dkvt[l], w, out=dtt, accumulate=True)
+        ctx.save = None
+        return (dv.view(B, S, 150, E), None, dtt.view(Bq, Lt, E)) + (None,) * (8 + len(ctx.needs_input_grad[11:]))
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T + b (final_fc, fusionv3.py:160,195) on the exact-f32 MFMA path (M = B rows)."""
+
+    @staticmethod
+    def forward(ctx, x, lin, flat, *params):
+        x = x.contiguous()
+        y = K.linear(x, lin.weight, lin.bias, out_f32=True)
+        ctx.x, ctx.lin, ctx.flat = x, lin, flat
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        lin, flat = ctx.lin, ctx.flat
+        _wgrad(flat, lin.weight, lin.bias, dy, ctx.x)
+        w = lin.weight.detach()
+        n = w.shape[0]
+        if n % 8:  # single-output heads (MC / Count): pad the reduction dim to the vector width
+            dy = torch.nn.functional.pad(dy, (0, 8 - n % 8))
+            w = torch.nn.functional.pad(w, (0, 0, 0, 8 - n % 8))
+        dx = K.linear_dx(dy, w)
+        ctx.x = None
+        return (dx, None, None) + (None,) * len(ctx.needs_input_grad[3:])
+
+
+class FusionTransformer(nn.Module):
+    def __init__(self, feature_dim: int = 768, drop_out_rate: float = 0.1) -> None:
+        super().__init__()
+        if feature_dim != E:
+            raise ValueError("the LRCE decoder is 768-wide (12 heads x 64)")
+        self.transformer = TransformerDecoder(12, drop_out_rate)
+        self.fusion_layer_norm = nn.LayerNorm(feature_dim, eps=EPS)
+        self.dropout = nn.Dropout(drop_out_rate)
+        self.summarization_token = init_weight((1, 1, feature_dim))
+        self.drop_out_rate = drop_out_rate
+
+    def run(self, v, v16, t, t16, B, nmc):
+        """v (B,S,150,E) f32 + bf16 copy, t (B*nmc, L+1, E) f32 + bf16 copy -> (B*nmc, E)."""
+        flat = ensure(self)
+        S = v.shape[1]
+        p = self.drop_out_rate if self.training else 0.0
+        seed = int(torch.randint(0, 2 ** 40, (1,)).item())
+        return _RecurrentDecoderFn.apply(v, v16, t, t16, self, flat, p, seed, B, S, nmc, *self.parameters())
+
+
+class LRCEOpenEnded(nn.Module):
+    def __init__(self, feature_dim: int, num_classes: int, drop_out_rate: float = 0.1,
+                 video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
+                 temporal_scale: List[int] = [1, 2, 3], question_seq_len: int = 30) -> None:
+        super().__init__()
+        self.feature_dim, self.video_feature_dim = feature_dim, video_feature_dim
+        self.video_pos_embed = VideoPosEmbed(feature_dim, video_feature_res, frame_sample_size, clip_size=sum(temporal_scale))
+        self.question_pos_embed = TextPosEmbed(question_seq_len, feature_dim)
+        if video_feature_dim != feature_dim:
+            self.projection_layer = nn.Linear(video_feature_dim, feature_dim)
+        self.video_dropout = nn.Dropout(drop_out_rate)
+        self.question_dropout = nn.Dropout(drop_out_rate)
+        self.fusion_transformer = FusionTransformer(feature_dim, drop_out_rate=drop_out_rate)
+        self.final_fc = nn.Linear(feature_dim, num_classes)
+        self.drop_out_rate = drop_out_rate
+
+    def _embed(self, video_features, text_features):
+        flat = ensure(self)
+        p = self.drop_out_rate if self.training else 0.0
+        seed = int(torch.randint(0, 2 ** 40, (1,)).item())
+        proj = getattr(self, "projection_layer", None)
+        vpe, qpe = self.video_pos_embed, self.question_pos_embed
+        vparams = list(vpe.parameters()) + (list(proj.parameters()) if proj is not None else [])
+        v, v16 = VideoEmbedFn.apply(video_features.contiguous().float(), proj, vpe, flat, p, seed, *vparams)
+        t, t16 = TextEmbedFn.apply(text_features.contiguous().float(), qpe, flat, p, seed + 1, *qpe.parameters())
+        return flat, v, v16, t, t16
+
+    def _head(self, flat, summarized):
+        return _LinearFn.apply(summarized, self.final_fc, flat, *self.final_fc.parameters())
+
+    def forward(self, video_features, text_features, texts_attention_mask):
+        """fusionv3.py:168-198.  video (B,S,Tg,49,Dv), text (B,L,E) -> logits (B, num_classes)."""
+        batch = video_features.shape[0]
+        flat, v, v16, t, t16 = self._embed(video_features, text_features)
+        s = self.fusion_transformer.run(v, v16, t, t16, batch, 1)
+        return self._head(flat, s).view(batch, -1)
+
+
+class LRCEMultipleChoice(LRCEOpenEnded):
+    def __init__(self, feature_dim, num_classes, drop_out_rate=0.1, video_feature_res=(7, 7), video_feature_dim=768,
+                 frame_sample_size=5, temporal_scale=[1, 2, 3], qa_seq_len=40):
+        super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
+                         frame_sample_size, temporal_scale, qa_seq_len)
+
+    def forward(self, video_features, text_features, texts_attention_mask):
+        """fusionv3.py:230-265.  text (B,5,L,E): each choice is a separate decoder row sharing the
+        video memory (expand + flatten, choice-minor) -> logits (B, 5)."""
+        batch, total_mc = text_features.shape[:2]
+        flat, v, v16, t, t16 = self._embed(video_features, text_features.flatten(0, 1))
+        s = self.fusion_transformer.run(v, v16, t, t16, batch, total_mc)
+        return self._head(flat, s).view(batch, total_mc)
+
+
+class LRCECount(LRCEOpenEnded):
+    def __init__(self, feature_dim, num_classes=1, drop_out_rate=0.1, video_feature_res=(7, 7), video_feature_dim=768,
+                 frame_sample_size=5, temporal_scale=[1, 2, 3], question_seq_len=30):
+        super().__init__(feature_dim, 1, drop_out_rate, video_feature_res, video_feature_dim, frame_sample_size,
+                         temporal_scale, question_seq_len)
+
+    def forward(self, video_features, text_features, texts_attention_mask):
+        """fusionv3.py:360-369: single-neuron regression head + ReLU."""
+        batch = video_features.shape[0]
+        out = super().forward(video_features, text_features, texts_attention_mask)
+        return torch.relu(out.view(batch))
