@@ -1,0 +1,214 @@
+#!/usr/bin/env python
+"""bench.py — LRCE training-step throughput on MI355X (QA-samples/s, fwd+bwd).
+
+One step = the reference's train_ddp.py step (agent_oe.py:19-48) on a synthetic MSVD-QA batch:
+E2EOpenEnded forward (Video Swin-B 3D on 3 clips x 5 frames x 224^2 -> BERT-base on a 20-token
+question padded to 32 -> 3-step x 12-layer recurrent LRCE decoder -> 1000-way head), cross-entropy,
+backward, gradient all-reduce (N>1, RCCL buckets overlapped with backward), and the fused AdamW step
+with the L2 regulariser (reg 0.001) over all 312 M parameters.  Train mode: dropout 0.5 in the fusion
+model (train_ddp default drop-out-rate), BERT dropout 0.1, Swin DropPath 0.2.  Inputs resident in
+HBM before the timed region.  bf16 MFMA compute with f32 master weights / residual stream.
+
+    python bench.py [--gpus N --steps K --warmup W]
+N>1: launched by torch.distributed.run (one process per GPU, RCCL); each rank runs bs=10 (weak
+scaling); rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "vqa-lrce-kbs-2023_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0      # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+METRIC = "QA-samples/sec (fwd+bwd) at bs=10\u00d716f\u00d7224\u00b2, 1/2/4/8 MI355X; Swin-attn MFMA%"  # BASELINE.json
+STEP_GFLOP_PER_SAMPLE = 933.3       # fwd+bwd, msvd-qa-oe, temporal scale 3 (flop_counter)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch-size", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-batch", type=int, default=3)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def build(batch, device, seed=0):
+    from lrce.models.e2e import E2EOpenEnded
+    from lrce.optim import FusedAdamW
+    from lrce.runtime import prepare
+    torch.manual_seed(seed)
+    # msvd-qa-oe config (configs/msvd-qa-oe.json): feature 768, 1000 answers, text_seq_len 32,
+    # video_feature_dim 1024; train_ddp defaults: drop-out-rate 0.5, temporal-scale [3]
+    model = E2EOpenEnded(768, 1000, 0.5, (7, 7), 1024, 5, [3], 32).to(device).train()
+    prepare(model)
+    reducer = None
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        from lrce.distributed import attach
+        reducer = attach(model, bucket_mb=64)
+    lr = 5e-6  # args.py default --lr, expanded to 3 groups (args.py:110-111)
+    opt = FusedAdamW(model, [{"params": model.fusion_model.parameters(), "lr": lr},
+                             {"params": model.text_extractor.parameters(), "lr": lr},
+                             {"params": model.video_extractor.parameters(), "lr": lr}],
+                     lr=lr, betas=(0.9, 0.999), reg_strength=0.001)
+    g = torch.Generator(device="cpu").manual_seed(1000 + (dist.get_rank() if dist.is_initialized() else 0))
+    clips = torch.rand(batch, 3, 5, 3, 224, 224, generator=g).to(device)   # 16-frame clip -> 3 x 5 frames
+    ids = torch.zeros(batch, 32, dtype=torch.int64)
+    ids[:, 0], ids[:, 19] = 101, 102
+    ids[:, 1:19] = torch.randint(1000, 30522, (batch, 18), generator=g)     # 20-token question
+    mask = (ids != 0).long()
+    types = torch.zeros_like(ids)
+    labels = torch.randint(0, 1000, (batch,), generator=g)
+    return model, opt, reducer, (clips, ids.to(device), mask.to(device), types.to(device), labels.to(device))
+
+
+def train_step(model, opt, reducer, batch):
+    clips, ids, mask, types, labels = batch
+    out = model(clips, ids, mask, types)
+    loss = F.cross_entropy(out, labels, ignore_index=-100)
+    loss.backward()
+    scale = reducer.finish() if reducer is not None else 1.0
+    opt.step(grad_scale=scale)
+    opt.zero_grad()
+    return loss
+
+
+def cpu_baseline(batch, threads):
+    """CPU leg: the oracle (oracle/lrce_oracle.py, the fp32 PyTorch restatement of the reference
+    pinned by tests/golden) running the same training step — forward, CE + L2 loss, backward,
+    AdamW — on a bounded sample (`batch` QA-samples, no dropout).  Checker/baseline only."""
+    from oracle import lrce_oracle as O
+    from lrce.models.e2e import E2EOpenEnded
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    tmpl = E2EOpenEnded(768, 1000, 0.5, (7, 7), 1024, 5, [3], 32)
+    sd = {k: (v.detach().clone().requires_grad_(True) if v.is_floating_point() else v)
+          for k, v in tmpl.state_dict().items()}
+    del tmpl
+    params = [v for v in sd.values() if v.requires_grad]
+    g = torch.Generator().manual_seed(7)
+    clips = torch.rand(batch, 3, 5, 3, 224, 224, generator=g)
+    ids = torch.zeros(batch, 32, dtype=torch.int64)
+    ids[:, 0], ids[:, 19] = 101, 102
+    ids[:, 1:19] = torch.randint(1000, 30522, (batch, 18), generator=g)
+    mask, types = (ids != 0).long(), torch.zeros_like(ids)
+    labels = torch.randint(0, 1000, (batch,), generator=g)
+    opt = torch.optim.AdamW(params, lr=5e-6, weight_decay=0.01)
+    t0 = time.perf_counter()
+    out = O.e2e_forward(sd, clips, ids, mask, types, "oe")
+    loss = F.cross_entropy(out, labels) + 0.001 * O.l2_reg(params)
+    loss.backward()
+    opt.step()
+    dt = time.perf_counter() - t0
+    return batch / dt, dt
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    from lrce import kernels as K
+    from lrce import _native
+    _native.lib()
+    log(f"rank {rank}/{world}: building model (bs={args.batch_size})")
+    model, opt, reducer, batch = build(args.batch_size, device)
+    for i in range(args.warmup):
+        train_step(model, opt, reducer, batch)
+        torch.cuda.synchronize()
+        log(f"warmup {i + 1}/{args.warmup}")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer = K.KernelTimer("wattn_fwd", "wattn_bwd", "gemm", "gemm_f32")
+    t0 = time.perf_counter()
+    with timer:
+        for i in range(args.steps):
+            loss = train_step(model, opt, reducer, batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_v = float(loss.item())
+    samples = world * args.batch_size * args.steps
+    value = samples / elapsed
+    ms = 1000.0 * elapsed / args.steps
+    log(f"loss {loss_v:.4f}  {value:.2f} samples/s  {ms:.1f} ms/step")
+
+    out = {"metric": METRIC,
+           "value": round(value, 3), "unit": "QA-samples/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights, U[0,1) clips, 20-token questions)",
+           "config": {"workload": "msvd-qa-oe train_ddp step: Swin-B 3D + BERT-base + LRCE-12 decoder, temporal-scale 3",
+                      "global_batch": samples // args.steps, "per_gpu_batch": args.batch_size, "frames": 16,
+                      "resolution": 224, "question_tokens": 20, "text_seq_len": 32,
+                      "parallelism": f"dp{world}"},
+           "loss": round(loss_v, 4),
+           "model_tflops": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0, 2),
+           "model_mfu": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0 / (MFMA_BF16_PEAK_TFLOPS * world), 4)}
+    out["roofline"] = _roofline(timer)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline (oracle, fp32) ...")
+        try:
+            v, dt = cpu_baseline(args.cpu_baseline_batch, args.cpu_threads)
+            out["cpu_baseline"] = {"value": round(v, 4), "unit": "QA-samples/s", "cores": args.cpu_threads, "kind": "port",
+                                   "sample": f"1 full training step (fwd+bwd+AdamW, fp32) of the CPU oracle at batch "
+                                             f"{args.cpu_baseline_batch}, {dt:.1f} s"}
+        except Exception as e:  # the baseline must not hide the GPU number
+            out["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _roofline(timer):
+    """Roofline of the Swin window-attention forward kernel (the kernel the north star names):
+    algorithmic flops per launch = 4 * n^2 * d per (window, head), n = 147 tokens (8x7x7 window clamped to
+    the 3x7x7 token grid of a 5-frame clip),
+    d = 32, x windows x heads of the stage; duration = HIP events recorded around
+    every launch on its stream during the timed steps.  Bound: MFMA (dense bf16 peak)."""
+    n, mean_ms, tflops, _ = timer.summary("wattn_fwd")
+    if not n:
+        return None
+    roof = {"kernel": "lrce_wattn_fwd", "bound": "mfma", "achieved": round(tflops, 2),
+            "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+            "traffic": None, "launches": n, "mean_launch_ms": round(mean_ms, 4)}
+    extra = {}
+    for name in ("wattn_bwd", "gemm", "gemm_f32"):
+        if name in timer.names:
+            c, m, t, _ = timer.summary(name)
+            if c:
+                extra[name] = {"launches": c, "mean_launch_ms": round(m, 4), "achieved_tflops": round(t, 2),
+                               "frac": round(t / MFMA_BF16_PEAK_TFLOPS, 4)}
+    roof["others"] = extra
+    return roof
+
+
+if __name__ == "__main__":
+    main()

@@ -136,7 +136,7 @@ def _e2e(name, ts=(3,)):
 def test_e2e_logits_match_reference_golden(name, batch):
     g = load_golden(f"e2e_{name}_b{batch}.npz")
     ts = tuple(int(x) for x in g["temporal_scale"])
-    m, _, task = _e2e(name, ts)
+    m, filled, task = _e2e(name, ts)
     clips = W.synthetic_clips(batch, sum(ts), seed=int(g["seed"]))
     np.testing.assert_allclose(csum(clips), g["clips_csum"], rtol=1e-9)
     with torch.no_grad():
@@ -152,7 +152,6 @@ def test_e2e_logits_match_reference_golden(name, batch):
     if task == "oe":
         assert err < 1e-2
     else:
-        _, filled, _ = _e2e(name, ts)
         ids, mask, types = (torch.from_numpy(g[k]) for k in ("ids", "mask", "types"))
         with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
             yb = O.e2e_forward(oracle_sd(filled), clips, ids, mask, types, task)

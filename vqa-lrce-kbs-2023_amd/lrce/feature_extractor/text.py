@@ -116,6 +116,7 @@ class _EmbedFn(torch.autograd.Function):
         if gw is not None and gp is not None and gt is not None:
             K.bert_embed_bwd(ds, ids, types, gw, gp, gt, s.shape[0], ctx.L, HIDDEN)
         ctx.save = None
+        flat.notify(emb.parameters())
         return (None,) * (6 + len(ctx.needs_input_grad[6:]))
 
 
@@ -182,6 +183,7 @@ class _LayerFn(torch.autograd.Function):
         K.linear_dx(dk, flat.w16(sa.key.weight), out=dx, accumulate=True)
         K.linear_dx(dv, flat.w16(sa.value.weight), out=dx, accumulate=True)
         ctx.save = ctx.desc = None
+        flat.notify(layer.parameters())
         return (dx,) + (None,) * (7 + len(ctx.needs_input_grad[8:]))
 
 

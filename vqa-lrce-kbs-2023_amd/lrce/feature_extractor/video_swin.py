@@ -225,6 +225,7 @@ class _PatchEmbedFn(torch.autograd.Function):
         gb = _g(flat, pe.proj.bias)
         if gb is not None:
             K.colsum(dy, gb)
+        flat.notify(pe.parameters())
         return (None,) * (5 + len(list(pe.parameters())))
 
 
@@ -330,6 +331,7 @@ class _SwinBlockFn(torch.autograd.Function):
         K.layernorm_bwd(dxw, x, m1, r1, blk.norm1.weight, dx, in_map=wmap, dres=dx_mid,
                         dw=_g(flat, blk.norm1.weight), db=_g(flat, blk.norm1.bias))
         ctx.save = None
+        flat.notify(blk.parameters())
         return (dx, None, None, None, None, None) + (None,) * len(ctx.needs_input_grad[6:])
 
 
@@ -360,6 +362,7 @@ class _PatchMergeFn(torch.autograd.Function):
         K.layernorm_bwd(dxl, x, mean, rstd, pm.norm.weight, dx, in_map=geo.merge_map, nseg=4, rows=geo.M // 4,
                         cols=4 * pm.dim, dw=_g(flat, pm.norm.weight), db=_g(flat, pm.norm.bias))
         ctx.save = None
+        flat.notify(pm.parameters())
         return (dx, None, None, None) + (None,) * len(ctx.needs_input_grad[4:])
 
 
@@ -377,6 +380,7 @@ class _LayerNormFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         K.layernorm_bwd(dy.contiguous(), x, mean, rstd, ctx.ln.weight, dx, dw=_g(ctx.flat, ctx.ln.weight),
                         db=_g(ctx.flat, ctx.ln.bias))
+        ctx.flat.notify(ctx.ln.parameters())
         return (dx, None, None, None) + (None,) * len(ctx.needs_input_grad[4:])
 
 

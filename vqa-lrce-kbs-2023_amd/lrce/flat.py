@@ -16,9 +16,14 @@ ALIGN = 1024
 
 
 class FlatParams:
-    def __init__(self, module, device):
+    def __init__(self, module, device, order=None):
         self.device = torch.device(device)
         self.params = [p for p in module.parameters()]
+        if order is not None:  # layout order (e.g. reverse forward order for gradient buckets)
+            ids = {id(p) for p in self.params}
+            assert len(order) == len(self.params) and {id(p) for p in order} == ids, "order must permute parameters"
+            self.params = list(order)
+        self.reducer = None
         self.names = {id(p): n for n, p in module.named_parameters()}
         offs, o = [], 0
         for p in self.params:
@@ -43,6 +48,11 @@ class FlatParams:
         self.n_chunks = self.total // ALIGN
         self._bf16_version = -1
         self.attach_grads(zero=True)
+
+    def notify(self, params):
+        """Called by native autograd Functions when their parameters' gradients are final."""
+        if self.reducer is not None:
+            self.reducer.notify(params)
 
     # ------------------------------------------------------------------ views
     def _slice(self, buf, p):

@@ -17,6 +17,62 @@ F32 = torch.float32
 NUM_CU = 256
 
 
+class KernelTimer:
+    """Brackets selected launches with HIP events on the launch stream (bench.py roofline):
+    `with KernelTimer("wattn_fwd") as kt: ...` then kt.mean_ms(), kt.calls, kt.flops."""
+    active = None
+
+    def __init__(self, *names):
+        self.names = set(names)
+        self.events = {n: [] for n in names}
+        self.flops = {n: 0.0 for n in names}
+        self.bytes = {n: 0.0 for n in names}
+
+    def __enter__(self):
+        KernelTimer.active = self
+        return self
+
+    def __exit__(self, *a):
+        KernelTimer.active = None
+
+    def wrap(self, name, stream_tensor, fn, flops=0.0, nbytes=0.0):
+        if name not in self.names:
+            return fn()
+        s = torch.cuda.current_stream(stream_tensor.device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        r = fn()
+        e1.record(s)
+        self.events[name].append((e0, e1))
+        self.flops[name] += flops
+        self.bytes[name] += nbytes
+        return r
+
+    def calls(self, name):
+        return len(self.events[name])
+
+    def total_ms(self, name):
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.events[name])
+
+    def mean_ms(self, name):
+        return self.total_ms(name) / max(1, self.calls(name))
+
+    def summary(self, name):
+        """(calls, mean ms per launch, algorithmic TFLOP/s, algorithmic GB/s) for one kernel family."""
+        n, t = self.calls(name), self.total_ms(name)
+        if n == 0 or t <= 0:
+            return n, None, None, None
+        return n, t / n, self.flops[name] / t / 1e9, self.bytes[name] / t / 1e6
+
+
+def _timed(name, stream_tensor, fn, flops=0.0, nbytes=0.0):
+    kt = KernelTimer.active
+    if kt is None:
+        return fn()
+    return kt.wrap(name, stream_tensor, fn, flops, nbytes)
+
+
 def _chk(t, dtype=None, name="tensor"):
     if t is None:
         return
@@ -56,7 +112,8 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.row_scale, d.rows_per_scale = ptr(row_scale), rows_per_scale
     d.a_row_scale, d.a_rows_per_scale = ptr(a_row_scale), a_rows_per_scale
     d.b_f32 = int(b_f32)
-    call("lrce_gemm", ctypes.byref(d), stream_of(c))
+    _timed("gemm_f32" if b_f32 else "gemm", c, lambda: call("lrce_gemm", ctypes.byref(d), stream_of(c)),
+           flops=2.0 * m * n * k * batch)
 
 
 def _split_for(m_out, n_out, k_red):
@@ -164,12 +221,17 @@ def wattn_bias_build(table, index, n, nH, region, n_pat, bias_fwd, bias_bwd):
 
 
 def wattn_fwd(qkv, bias_fwd, win_pat, out, lse, n_win, n, nH):
-    call("lrce_wattn_fwd", ptr(qkv), ptr(bias_fwd), ptr(win_pat), ptr(out), ptr(lse), n_win, n, nH, stream_of(out))
+    # algorithmic work: QK^T + PV = 4 n^2 d per (window, head), d = 32
+    _timed("wattn_fwd", out, lambda: call("lrce_wattn_fwd", ptr(qkv), ptr(bias_fwd), ptr(win_pat), ptr(out), ptr(lse),
+                                           n_win, n, nH, stream_of(out)),
+           flops=4.0 * n * n * 32 * n_win * nH)
 
 
 def wattn_bwd(qkv, out, dout, lse, bias_bwd, win_pat, dqkv, ds, n_win, n, nH):
-    call("lrce_wattn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(bias_bwd), ptr(win_pat), ptr(dqkv), ptr(ds),
-         n_win, n, nH, stream_of(dqkv))
+    # algorithmic work: dV, dP, dQ, dK = 8 n^2 d per (window, head)
+    _timed("wattn_bwd", dqkv, lambda: call("lrce_wattn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(bias_bwd),
+                                            ptr(win_pat), ptr(dqkv), ptr(ds), n_win, n, nH, stream_of(dqkv)),
+           flops=8.0 * n * n * 32 * n_win * nH)
 
 
 def wattn_ds_elems(n_win, nH):

@@ -28,6 +28,16 @@ class E2EBase(nn.Module):
     def extract_text_features(self, texts, attention_mask, texts_type_ids):
         return self.text_extractor(texts, attention_mask, texts_type_ids)
 
+    def lrce_param_order(self):
+        """Flat-store layout = reverse forward order (fusion, BERT top-down, Swin top-down), so the
+        gradient buckets complete in sequence during backward; the unused BERT pooler goes last."""
+        fusion = list(self.fusion_model.parameters())[::-1]
+        bert = self.text_extractor.bert
+        pool = {id(p) for p in bert.pooler.parameters()}
+        text = [p for p in self.text_extractor.parameters() if id(p) not in pool][::-1]
+        video = list(self.video_extractor.parameters())[::-1]
+        return fusion + text + video + list(bert.pooler.parameters())
+
     def extract_video_features(self, video_clips):
         return self.video_extractor(video_clips)
 

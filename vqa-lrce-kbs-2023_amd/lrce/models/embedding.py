@@ -99,6 +99,7 @@ class VideoEmbedFn(torch.autograd.Function):
         else:
             dvf = dy
         ctx.save = None
+        flat.notify(list(pe.parameters()) + (list(proj.parameters()) if proj is not None else []))
         return (dvf.view(B, S, Tg, P, Cin),) + (None,) * (5 + len(ctx.needs_input_grad[6:]))
 
 
@@ -134,4 +135,5 @@ class TextEmbedFn(torch.autograd.Function):
         tmp = [g if g is not None else torch.zeros(t.shape, device=dz.device) for g, t in zip(gs, (pe.emb_cls, pe.emb_pos))]
         K.text_posembed_bwd(dz, dx, tmp[0], tmp[1], B, L, C)
         ctx.save = None
+        flat.notify(pe.parameters())
         return (dx.view(B, L, C),) + (None,) * (4 + len(ctx.needs_input_grad[5:]))

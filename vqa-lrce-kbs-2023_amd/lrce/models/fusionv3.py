@@ -250,6 +250,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             K.linear_dx(dkvv[l], w, out=dv, accumulate=True)
             K.linear_dx(dkvt[l], w, out=dtt, accumulate=True)
         ctx.save = None
+        flat.notify(ft.parameters())
         return (dv.view(B, S, 150, E), None, dtt.view(Bq, Lt, E)) + (None,) * (8 + len(ctx.needs_input_grad[11:]))
 
 
@@ -275,6 +276,7 @@ class _LinearFn(torch.autograd.Function):
             w = torch.nn.functional.pad(w, (0, 0, 0, 8 - n % 8))
         dx = K.linear_dx(dy, w)
         ctx.x = None
+        flat.notify(lin.parameters())
         return (dx, None, None) + (None,) * len(ctx.needs_input_grad[3:])
 
 

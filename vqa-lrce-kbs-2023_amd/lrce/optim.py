@@ -1,0 +1,75 @@
+"""Fused AdamW over the flat parameter store (reference agent_base.py:27-44 + the L2 regulariser of
+agent_base.py:103-108 / agent_oe.py:36).
+
+The reference builds torch.optim.AdamW with three parameter groups (fusion, text, video; lr may be
+given per group, args.py:110-111) and adds reg_strength * sum_t ||p_t||_2 to the loss, so every
+step back-propagates 783 norm kernels.  Here the regulariser's gradient reg * p_t / ||p_t|| is
+added inside the update kernel (csrc/optim.hip) from one multi-tensor norm pass: the optimizer step
+is two launches for all 312 M parameters, and it also refreshes the bf16 shadow the forward reads.
+Semantics = torch.optim.AdamW (decoupled weight decay 0.01 default, bias-corrected moments).
+"""
+import math
+
+import torch
+
+from . import kernels as K
+from .runtime import flat_of, ensure
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, model, groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, reg_strength=0.0):
+        """groups: list of iterables of parameters (e.g. [fusion.parameters(), text..., video...]) or of
+        dicts {'params': ..., 'lr': ...}; every parameter must belong to `model`'s flat store."""
+        flat = flat_of(model) or ensure(model)
+        pg = []
+        for g in groups:
+            if isinstance(g, dict):
+                pg.append({"params": list(g["params"]), "lr": g.get("lr", lr)})
+            else:
+                pg.append({"params": list(g), "lr": lr})
+        super().__init__(pg, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.flat = flat
+        self.reg_strength = float(reg_strength)
+        dev = flat.device
+        self.exp_avg = torch.zeros_like(flat.f32)
+        self.exp_avg_sq = torch.zeros_like(flat.f32)
+        self.sumsq = torch.zeros(len(flat.params), device=dev)
+        self._index = {id(p): i for i, p in enumerate(flat.params)}
+        self.tensor_lr = torch.zeros(len(flat.params), device=dev)
+        self._lr_cache = None
+        self.step_count = 0
+        self.last_l2 = None
+
+    def _sync_lrs(self):
+        key = tuple(g["lr"] for g in self.param_groups)
+        if key == self._lr_cache:
+            return
+        lrs = torch.zeros(len(self.flat.params))
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.requires_grad:
+                    lrs[self._index[id(p)]] = g["lr"]
+        self.tensor_lr.copy_(lrs, non_blocking=True)
+        self._lr_cache = key
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale=1.0):
+        loss = closure() if closure is not None else None
+        flat = self.flat
+        self._sync_lrs()
+        self.step_count += 1
+        b1, b2 = self.defaults["betas"]
+        t = self.step_count
+        K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params))
+        K.adamw_step(flat.f32, flat.grad, self.exp_avg, self.exp_avg_sq, flat.chunk_tensor, self.tensor_lr, self.sumsq,
+                     flat.bf16, flat.n_chunks, b1, b2, self.defaults["eps"], self.defaults["weight_decay"],
+                     float(grad_scale), self.reg_strength, 1.0 - b1 ** t, 1.0 - b2 ** t)
+        flat.mark_bf16_fresh()
+        return loss
+
+    def l2_term(self):
+        """sum_t ||p_t||_2 of the parameters before the last step (device scalar; no sync)."""
+        return self.sumsq.sqrt().sum()
+
+    def zero_grad(self, set_to_none=False):
+        self.flat.grad.zero_()

@@ -28,7 +28,8 @@ def bind(root, device=None):
     for name, b in root.named_buffers():
         if b.device != device:
             raise RuntimeError(f"buffer {name} not on {device}: call model.to(device) first")
-    flat = FlatParams(root, device)
+    order = root.lrce_param_order() if hasattr(root, "lrce_param_order") else None
+    flat = FlatParams(root, device, order)
     _set_flat(root, flat)
     object.__setattr__(root, "_lrce_root", True)
     return flat
