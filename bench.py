@@ -47,6 +47,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-batch", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--mode", choices=["graph", "eager"], default="graph",
+                    help="graph: the step replayed from a HIP graph (N>1: graph(fwd+bwd) -> RCCL bucket "
+                         "all-reduce -> graph(optimizer)); eager: launched from Python, all-reduce overlapped "
+                         "with backward")
+    ap.add_argument("--roofline-steps", type=int, default=2)
     return ap.parse_args()
 
 
@@ -88,6 +93,39 @@ def train_step(model, opt, reducer, batch):
     opt.step(grad_scale=scale)
     opt.zero_grad()
     return loss
+
+
+def make_step(model, opt, reducer, batch, mode, world):
+    from lrce.graph import CapturedStep
+    if mode == "eager":
+        return lambda: train_step(model, opt, reducer, batch)
+    if reducer is None:
+        def whole():
+            opt.zero_grad()
+            clips, ids, mask, types, labels = batch
+            loss = F.cross_entropy(model(clips, ids, mask, types), labels, ignore_index=-100)
+            loss.backward()
+            opt.step()
+            return loss
+        return CapturedStep(whole).replay
+    flat = reducer.flat
+    flat.reducer = None
+
+    def fwd_bwd():
+        opt.zero_grad()
+        clips, ids, mask, types, labels = batch
+        loss = F.cross_entropy(model(clips, ids, mask, types), labels, ignore_index=-100)
+        loss.backward()
+        return loss
+    g1 = CapturedStep(fwd_bwd)
+    g2 = CapturedStep(lambda: opt.step(grad_scale=1.0 / world) or opt.step_t, warmup=1)
+
+    def step():
+        loss = g1.replay()
+        reducer.reduce_all()
+        g2.replay()
+        return loss
+    return step
 
 
 def cpu_baseline(batch, threads):
@@ -134,18 +172,24 @@ def main():
     _native.lib()
     log(f"rank {rank}/{world}: building model (bs={args.batch_size})")
     model, opt, reducer, batch = build(args.batch_size, device)
+    try:
+        step = make_step(model, opt, reducer, batch, args.mode, world)
+    except Exception as e:  # capture failure must not hide the measurement: fall back loudly
+        log(f"graph capture failed ({e!r}); timing eager steps")
+        args.mode = "eager"
+        if reducer is not None:
+            reducer.flat.reducer = reducer
+        step = make_step(model, opt, reducer, batch, "eager", world)
     for i in range(args.warmup):
-        train_step(model, opt, reducer, batch)
+        step()
         torch.cuda.synchronize()
         log(f"warmup {i + 1}/{args.warmup}")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timer = K.KernelTimer("wattn_fwd", "wattn_bwd", "gemm", "gemm_f32")
     t0 = time.perf_counter()
-    with timer:
-        for i in range(args.steps):
-            loss = train_step(model, opt, reducer, batch)
+    for i in range(args.steps):
+        loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -158,7 +202,16 @@ def main():
     samples = world * args.batch_size * args.steps
     value = samples / elapsed
     ms = 1000.0 * elapsed / args.steps
-    log(f"loss {loss_v:.4f}  {value:.2f} samples/s  {ms:.1f} ms/step")
+    log(f"loss {loss_v:.4f}  {value:.2f} samples/s  {ms:.1f} ms/step ({args.mode})")
+    # per-kernel roofline: HIP events around every launch of the timed kernels, on their launch
+    # stream, over eager steps of the same workload (a graph replay hides individual launches)
+    timer = K.KernelTimer("wattn_fwd", "wattn_bwd", "gemm", "gemm_f32")
+    if reducer is not None:
+        reducer.flat.reducer = reducer
+    with timer:
+        for i in range(args.roofline_steps):
+            train_step(model, opt, reducer, batch)
+    torch.cuda.synchronize()
 
     out = {"metric": METRIC,
            "value": round(value, 3), "unit": "QA-samples/s", "n_gpus": world, "steps": args.steps,
@@ -167,7 +220,7 @@ def main():
            "config": {"workload": "msvd-qa-oe train_ddp step: Swin-B 3D + BERT-base + LRCE-12 decoder, temporal-scale 3",
                       "global_batch": samples // args.steps, "per_gpu_batch": args.batch_size, "frames": 16,
                       "resolution": 224, "question_tokens": 20, "text_seq_len": 32,
-                      "parallelism": f"dp{world}"},
+                      "parallelism": f"dp{world}", "launch": args.mode},
            "loss": round(loss_v, 4),
            "model_tflops": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0, 2),
            "model_mfu": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0 / (MFMA_BF16_PEAK_TFLOPS * world), 4)}

@@ -197,6 +197,11 @@ int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
 int lrce_dropout(const float* x, const float* res, float* y, uint16_t* y_bf16, int64_t n, float p, uint64_t seed,
                  int64_t group, void* stream);
 int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t seed, int64_t group, void* stream);
+/* Device-side RNG offset for graph replay: every hash-based mask (lrce_dropout*, lrce_mha_* dropout)
+ * uses seed + *offset when a device pointer is registered (NULL = 0, the default).  A captured
+ * HIP graph bakes the host seeds; advancing *offset (one device add per training step) gives each
+ * replay fresh masks while forward and backward of one step still agree. */
+int lrce_set_rng_offset(const uint64_t* offset);
 
 /* Fused optimizer step over the flat parameter buffer (agent_base.py:27-44,103-108).  Every tensor
  * starts at a multiple of 1024 elements; chunk_tensor[c] is the tensor id of 1024-element chunk c.
@@ -207,7 +212,8 @@ int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t se
 int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks, float* sumsq, int n_tensors, void* stream);
 int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
                     const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
-                    float weight_decay, float grad_scale, float reg, float bc1, float bc2, void* stream);
+                    float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
+                    void* stream); /* step: optional device step count t; when set, bc1/bc2 are computed from it */
 
 /* BERT embeddings before their LayerNorm (HF BertEmbeddings): out[r] = word[ids[r]] + pos[r % L] +
  * type[types[r]] (f32 tables, int64 ids), and the scatter-add backward into the three tables. */

@@ -75,6 +75,45 @@ def test_gemm_exact_f32_path(M, N, Kd, a_km, b_km):
     assert rel(C2, ref + bias) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,R", [(768, 3072, 10), (3072, 768, 50), (768, 768, 64)])
+def test_gemm_f32_outer_accumulate(M, N, R):
+    """dW (+)= dY^T X with a skinny reduction (decoder weight gradients): outer-product kernel."""
+    k = K()
+    dy = torch.randn(R, M, device=dev)
+    x = torch.randn(R, N, device=dev)
+    dw0 = torch.randn(M, N, device=dev)
+    dw = dw0.clone()
+    k.linear_dw(dy, x, dw)
+    ref = dw0.double() + dy.double().t() @ x.double()
+    assert rel(dw, ref.float()) < 1e-5
+
+
+@pytest.mark.parametrize("M", [1, 10, 50])
+def test_gemm_f32_skinny_epilogues(M):
+    """Decoder query-side linears: GELU + bf16 pre-activation, residual, dGELU on the skinny path."""
+    k = K()
+    E, FF = 768, 3072
+    x = torch.randn(M, E, device=dev)
+    w1 = torch.randn(FF, E, device=dev) / math.sqrt(E)
+    b1 = torch.randn(FF, device=dev)
+    pre = torch.empty(M, FF, device=dev, dtype=torch.bfloat16)
+    g = k.linear(x, w1, b1, gelu=True, pre_out=pre, out_f32=True)
+    ref_pre = x.double() @ w1.double().t() + b1.double()
+    assert rel(pre, ref_pre.float()) < 8e-3
+    assert rel(g, F.gelu(ref_pre).float()) < 1e-5
+    res = torch.randn(M, E, device=dev)
+    w2 = torch.randn(E, FF, device=dev) / math.sqrt(FF)
+    y = k.linear(g, w2, None, resid=res, out_f32=True)
+    assert rel(y, (g.double() @ w2.double().t() + res.double()).float()) < 1e-5
+    dy = torch.randn(M, E, device=dev)
+    dgp = k.linear_dx(dy, w2, dgelu_pre=pre)
+    pr = pre.double().requires_grad_(True)
+    F.gelu(pr).sum().backward()
+    assert rel(dgp, ((dy.double() @ w2.double()) * pr.grad).float()) < 1e-5
+    dx = k.linear_dx(dgp, w1, resid=res)
+    assert rel(dx, (dgp.double() @ w1.double() + res.double()).float()) < 1e-5
+
+
 def test_gemm_epilogues_and_maps():
     k = K()
     M, N, Kd = 520, 256, 160
@@ -214,6 +253,7 @@ def test_window_attention_fwd_bwd(nH, n_win):
     (3, 12, 32, 32, True, 0, 1, 0.0), (4, 12, 1, 183, False, 150, 1, 0.0), (2, 12, 40, 40, True, 0, 1, 0.0),
     (10, 12, 1, 191, False, 150, 5, 0.0), (3, 12, 32, 32, True, 0, 1, 0.3), (5, 12, 1, 183, False, 150, 5, 0.5)])
 def test_mha_fwd_bwd(B, H, Lq, Lk, masked, split, bdiv, drop):
+    K().rng_offset(dev).zero_()   # host reference masks assume offset 0
     """Two key segments (video memory shared by `bdiv` rows + text memory), padding mask, dropout."""
     k = K()
     d = 64
@@ -282,6 +322,7 @@ def _hash_uniform(seed, idx):
 
 
 def test_dropout_residual_and_groups():
+    K().rng_offset(dev).zero_()
     k = K()
     x = torch.randn(4096, device=dev)
     r = torch.randn(4096, device=dev)
@@ -335,3 +376,20 @@ def test_adamw_matches_torch():
         opt.step()
     torch.cuda.synchronize()
     assert rel(p, torch.cat([pref[0].detach(), pref[1].detach()])) < 1e-5
+
+
+def test_rng_offset_changes_masks_and_backward_agrees():
+    """The device RNG offset (graph replay) moves every mask; dropout backward uses the same mask as
+    its forward at the same offset."""
+    k = K()
+    off = k.rng_offset(dev)
+    off.zero_()
+    x = torch.randn(1 << 16, device=dev)
+    y0 = k.dropout(x, 0.5, 9)
+    k.rng_advance(dev)
+    y1 = k.dropout(x, 0.5, 9)
+    assert not torch.equal(y0 != 0, y1 != 0)
+    dx = k.dropout_bwd(torch.ones_like(x), 0.5, 9)
+    assert torch.equal(dx != 0, y1 != 0)
+    off.zero_()
+    assert torch.equal(k.dropout(x, 0.5, 9), y0)

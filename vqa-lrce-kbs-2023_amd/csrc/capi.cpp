@@ -22,3 +22,10 @@ int lrce_check_launch(const char* what) {
 
 extern "C" int lrce_version(void) { return 1; }
 extern "C" const char* lrce_last_error(void) { return g_err; }
+
+static const uint64_t* g_rng_offset = nullptr;
+extern "C" int lrce_set_rng_offset(const uint64_t* offset) {
+  g_rng_offset = offset;
+  return LRCE_OK;
+}
+const uint64_t* lrce_rng_offset() { return g_rng_offset; }

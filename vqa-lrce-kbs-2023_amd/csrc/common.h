@@ -52,3 +52,4 @@ __device__ __forceinline__ uint32_t lrce_hash(uint64_t x) {
 __device__ __forceinline__ float lrce_uniform(uint64_t seed, uint64_t idx) {
   return (lrce_hash(seed * 0x9E3779B97F4A7C15ULL + idx) >> 8) * (1.0f / 16777216.0f);
 }
+__device__ __forceinline__ uint64_t lrce_seed(uint64_t seed, const uint64_t* off) { return off ? seed + *off : seed; }

@@ -78,22 +78,23 @@ __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, l
 }
 
 __global__ void dropout_kernel(const float* __restrict__ x, const float* __restrict__ res, float* __restrict__ y,
-                               bf16* __restrict__ yb, long long n, float p, uint64_t seed, long long group) {
+                               bf16* __restrict__ yb, long long n, float p, uint64_t seed, long long group,
+                               const uint64_t* __restrict__ off) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float v = x[i];
-  if (p > 0.f) v = (lrce_uniform(seed, i / group) >= p) ? v / (1.0f - p) : 0.f;
+  if (p > 0.f) v = (lrce_uniform(lrce_seed(seed, off), i / group) >= p) ? v / (1.0f - p) : 0.f;
   if (res) v += res[i];
   y[i] = v;
   if (yb) yb[i] = f2bf(v);
 }
 
 __global__ void dropout_bwd_kernel(const float* __restrict__ dy, float* __restrict__ dx, long long n, float p, uint64_t seed,
-                                   long long group) {
+                                   long long group, const uint64_t* __restrict__ off) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float v = dy[i];
-  if (p > 0.f) v = (lrce_uniform(seed, i / group) >= p) ? v / (1.0f - p) : 0.f;
+  if (p > 0.f) v = (lrce_uniform(lrce_seed(seed, off), i / group) >= p) ? v / (1.0f - p) : 0.f;
   dx[i] = v;
 }
 
@@ -236,7 +237,7 @@ extern "C" int lrce_dropout(const float* x, const float* res, float* y, uint16_t
   if (n <= 0) return LRCE_OK;
   if (group < 1) group = 1;
   dropout_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(x, res, y, reinterpret_cast<bf16*>(y_bf16), n, p,
-                                                                               seed, group);
+                                                                               seed, group, lrce_rng_offset());
   return lrce_check_launch("dropout");
 }
 
@@ -244,7 +245,7 @@ extern "C" int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, 
   if (!dy || !dx) return lrce_fail(LRCE_E_ARG, "dropout_bwd: null pointer");
   if (n <= 0) return LRCE_OK;
   if (group < 1) group = 1;
-  dropout_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(dy, dx, n, p, seed, group);
+  dropout_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(dy, dx, n, p, seed, group, lrce_rng_offset());
   return lrce_check_launch("dropout_bwd");
 }
 

@@ -10,6 +10,13 @@
 // read with ds_read_b128; M/N-major tiles live as [k][128] with 8-B units XOR-swizzled by a 3-bit
 // function of k and are read with ds_read_b64_tr_b16 (hardware transpose), so no operand is
 // ever transposed through HBM.
+// Epilogue: each wave stages its 64x64 fp32 tile through LDS (two padded 32-row halves) and applies
+// bias / GELU / dGELU / row scale / residual / output conversion on 8 consecutive columns per lane,
+// so every global access of the epilogue is a 16-B vector (scalar fallback for ragged / unaligned
+// edges).  All operand loads are unconditional (out-of-range lanes read a clamped in-bounds address
+// and are zeroed by a select), which keeps the global loads of a K-tile batched.
+#include <type_traits>
+
 #include "common.h"
 #include "lrce_capi.h"
 
@@ -39,6 +46,7 @@ struct GemmP {
   const float* a_row_scale;
   int a_rows_per_scale;
   int tiles_m, tiles_n;
+  int vec;  // 1: c/aux/aux_out/bias rows are 16-B aligned and n % 8 == 0 (vector epilogue)
 };
 
 // ---- LDS addressing --------------------------------------------------------------------------
@@ -64,37 +72,32 @@ __device__ __forceinline__ void load_tile(Stage& st, const void* base, long long
     if (KMAJ) { r = c >> 3; kk = (c & 7) << 3; }
     else { kk = c >> 4; r = (c & 15) << 3; }
     const int gr = row0 + r, gk = k0 + kk;
-    uint4 val = make_uint4(0, 0, 0, 0);
-    bool ok = KMAJ ? (gr < rows_total && gk < kdim) : (gk < kdim && gr < rows_total);
-    if (ok) {
-      long long off;
-      if (KMAJ) {
-        const long long rr = map ? (long long)map[gr] : (long long)gr;
-        off = rr * ld + gk;
-      } else {
-        const long long kr = map ? (long long)map[gk] : (long long)gk;
-        off = kr * ld + gr;
-      }
-      if (F32) {
-        const float4* p = reinterpret_cast<const float4*>(static_cast<const float*>(base) + off);
-        float4 x0 = p[0], x1 = p[1];
-        if (rsc) {
-          if (KMAJ) {
-            const float f = rsc[gr / rps];
-            x0.x *= f; x0.y *= f; x0.z *= f; x0.w *= f; x1.x *= f; x1.y *= f; x1.z *= f; x1.w *= f;
-          } else {
-            const float f = rsc[gk / rps];
-            x0.x *= f; x0.y *= f; x0.z *= f; x0.w *= f; x1.x *= f; x1.y *= f; x1.z *= f; x1.w *= f;
-          }
-        }
-        bf16x8 t;
-        t[0] = f2bf(x0.x); t[1] = f2bf(x0.y); t[2] = f2bf(x0.z); t[3] = f2bf(x0.w);
-        t[4] = f2bf(x1.x); t[5] = f2bf(x1.y); t[6] = f2bf(x1.z); t[7] = f2bf(x1.w);
-        val = *reinterpret_cast<uint4*>(&t);
-      } else {
-        val = *reinterpret_cast<const uint4*>(static_cast<const bf16*>(base) + off);
-      }
+    const bool ok = gr < rows_total && gk < kdim;
+    const int grc = ok ? gr : 0, gkc = ok ? gk : 0;  // (0,0) is always in range: m, n, k > 0
+    long long off;
+    if (KMAJ) {
+      const long long rr = map ? (long long)map[grc] : (long long)grc;
+      off = rr * ld + gkc;
+    } else {
+      const long long kr = map ? (long long)map[gkc] : (long long)gkc;
+      off = kr * ld + grc;
     }
+    uint4 val;
+    if (F32) {
+      const float4* q = reinterpret_cast<const float4*>(static_cast<const float*>(base) + off);
+      float4 x0 = q[0], x1 = q[1];
+      if (rsc) {
+        const float f = rsc[(KMAJ ? grc : gkc) / rps];
+        x0.x *= f; x0.y *= f; x0.z *= f; x0.w *= f; x1.x *= f; x1.y *= f; x1.z *= f; x1.w *= f;
+      }
+      bf16x8 t;
+      t[0] = f2bf(x0.x); t[1] = f2bf(x0.y); t[2] = f2bf(x0.z); t[3] = f2bf(x0.w);
+      t[4] = f2bf(x1.x); t[5] = f2bf(x1.y); t[6] = f2bf(x1.z); t[7] = f2bf(x1.w);
+      val = *reinterpret_cast<uint4*>(&t);
+    } else {
+      val = *reinterpret_cast<const uint4*>(static_cast<const bf16*>(base) + off);
+    }
+    if (!ok) val = make_uint4(0, 0, 0, 0);
     st.v[i] = val;
   }
 }
@@ -133,6 +136,109 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16* lds, int r0, int ks, int
       out[4 * h + 0] = bv[0]; out[4 * h + 1] = bv[1]; out[4 * h + 2] = bv[2]; out[4 * h + 3] = bv[3];
     }
     return out;
+  }
+}
+
+constexpr int EP = 68;  // padded fp32 row of the epilogue staging tile (conflict-free writes)
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Fused epilogue for one element (row = c_map-resolved output row).
+__device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row, int m, int nn, bool first, float rs,
+                                          char* cbase) {
+  const int fl = p.flags;
+  x = x * p.alpha + (((fl & LRCE_EPI_BIAS) && first) ? p.bias[nn] : 0.f);
+  x *= (nn < p.scale_cols) ? p.scale_val : 1.f;
+  if (fl & LRCE_EPI_GELU) {
+    if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + nn] = f2bf(x);
+    x = gelu_f(x);
+  }
+  if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + nn]));
+  x *= rs;
+  if ((fl & LRCE_EPI_RESID) && first) x += static_cast<const float*>(p.aux)[row * p.ld_aux + nn];
+  if (fl & LRCE_EPI_ATOMIC) {
+    __hip_atomic_fetch_add(reinterpret_cast<float*>(cbase) + row * p.ldc + nn, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (fl & LRCE_EPI_ACCUM) {
+    reinterpret_cast<float*>(cbase)[row * p.ldc + nn] += x;
+  } else if (fl & LRCE_EPI_OUT_F32) {
+    reinterpret_cast<float*>(cbase)[row * p.ldc + nn] = x;
+    if (fl & LRCE_EPI_OUT_BOTH) p.aux_out[row * p.ld_aux_out + nn] = f2bf(x);
+  } else {
+    reinterpret_cast<bf16*>(cbase)[row * p.ldc + nn] = f2bf(x);
+  }
+}
+
+// Fused epilogue for 8 consecutive columns n..n+7 of output row m (see LrceGemmDesc flags).
+__device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int n, int sk, char* cbase) {
+  if (m >= p.m || n >= p.n) return;
+  const int fl = p.flags;
+  const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
+  const bool first = sk == 0;
+  const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
+  if (p.vec && n + 8 <= p.n) {
+    float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if ((fl & LRCE_EPI_BIAS) && first) {
+      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n), b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+      bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w; bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (v[e] * p.alpha + bias[e]) * ((n + e < p.scale_cols) ? p.scale_val : 1.f);
+    if (fl & LRCE_EPI_GELU) {
+      if (fl & LRCE_EPI_AUX_OUT) {
+        bf16x8 pre;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pre[e] = f2bf(v[e]);
+        *reinterpret_cast<bf16x8*>(p.aux_out + row * p.ld_aux_out + n) = pre;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+    }
+    if (fl & LRCE_EPI_DGELU) {
+      const bf16x8 pre = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(p.aux) + row * p.ld_aux + n);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(bf2f(pre[e]));
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= rs;
+    if ((fl & LRCE_EPI_RESID) && first) {
+      const float* ap = static_cast<const float*>(p.aux) + row * p.ld_aux + n;
+      const float4 r0 = *reinterpret_cast<const float4*>(ap), r1 = *reinterpret_cast<const float4*>(ap + 4);
+      v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w; v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+    }
+    if (fl & LRCE_EPI_ATOMIC) {
+      float* cp = reinterpret_cast<float*>(cbase) + row * p.ldc + n;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) __hip_atomic_fetch_add(cp + e, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (fl & (LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) {
+      float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(cbase) + row * p.ldc + n);
+      float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
+      if (fl & LRCE_EPI_ACCUM) {
+        const float4 c0 = cp[0], c1 = cp[1];
+        o0.x += c0.x; o0.y += c0.y; o0.z += c0.z; o0.w += c0.w; o1.x += c1.x; o1.y += c1.y; o1.z += c1.z; o1.w += c1.w;
+      }
+      cp[0] = o0; cp[1] = o1;
+      if ((fl & LRCE_EPI_OUT_BOTH) && !(fl & LRCE_EPI_ACCUM)) {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+        *reinterpret_cast<bf16x8*>(p.aux_out + row * p.ld_aux_out + n) = o;
+      }
+    } else {
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(cbase) + row * p.ldc + n) = o;
+    }
+    return;
+  }
+  // ragged / unaligned edge: element by element
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if (n + e >= p.n) break;
+    epilogue1(p, v[e], row, m, n + e, first, rs, cbase);
   }
 }
 
@@ -199,44 +305,47 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds rows (lane>>4)*4 + r, column lane&15 of each 16x16 tile
-  const int fl = p.flags;
-  char* cbase = static_cast<char*>(p.c) + (long long)bz * p.sc * ((fl & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
+  // ---- epilogue through LDS (the K loop ended with a barrier: every wave is done with the tiles)
+  char* cbase = static_cast<char*>(p.c) +
+                (long long)bz * p.sc * ((p.flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
+  float* E = reinterpret_cast<float*>(&lds[0][0][0]) + wave * (32 * EP);
+  const int cc = (lane & 7) * 8;
+  auto half = [&](auto hc) {
+    constexpr int h = decltype(hc)::value;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-    if (n >= p.n) continue;
-    float bias = ((fl & LRCE_EPI_BIAS) && sk == 0) ? p.bias[n] : 0.f;
-    const float csc = (n < p.scale_cols) ? p.scale_val : 1.f;
+    for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        if (m >= p.m) continue;
-        const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
-        float v = acc[i][j][r] * p.alpha + bias;
-        v *= csc;
-        if (fl & LRCE_EPI_GELU) {
-          if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + n] = f2bf(v);
-          v = gelu_f(v);
-        }
-        if (fl & LRCE_EPI_DGELU) v *= gelu_grad_f(bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]));
-        if (p.row_scale) v *= p.row_scale[m / p.rows_per_scale];
-        if ((fl & LRCE_EPI_RESID) && sk == 0) v += static_cast<const float*>(p.aux)[row * p.ld_aux + n];
-        if (fl & LRCE_EPI_ATOMIC) {
-          atomicAdd(reinterpret_cast<float*>(cbase) + row * p.ldc + n, v);
-        } else if (fl & LRCE_EPI_ACCUM) {
-          reinterpret_cast<float*>(cbase)[row * p.ldc + n] += v;
-        } else if (fl & LRCE_EPI_OUT_F32) {
-          reinterpret_cast<float*>(cbase)[row * p.ldc + n] = v;
-          if (fl & LRCE_EPI_OUT_BOTH) p.aux_out[row * p.ld_aux_out + n] = f2bf(v);
-        } else {
-          reinterpret_cast<bf16*>(cbase)[row * p.ldc + n] = f2bf(v);
+        for (int r = 0; r < 4; ++r)
+          E[(ii * 16 + (lane >> 4) * 4 + r) * EP + j * 16 + (lane & 15)] = acc[2 * h + ii][j][r];
+    wave_lds_fence();
+    if (p.flags & LRCE_EPI_ATOMIC) {
+      // split-K partial sums: one row per instruction, 64 consecutive columns (coalesced atomics)
+      const int n = n0 + wn * 64 + lane;
+      if (n < p.n) {
+        for (int rr = 0; rr < 32; ++rr) {
+          const int m = m0 + wm * 64 + h * 32 + rr;
+          if (m >= p.m) break;
+          const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
+          const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
+          epilogue1(p, E[rr * EP + lane], row, m, n, sk == 0, rs, cbase);
         }
       }
+    } else {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int rr = it * 8 + (lane >> 3);
+        const float4 x0 = *reinterpret_cast<const float4*>(E + rr * EP + cc);
+        const float4 x1 = *reinterpret_cast<const float4*>(E + rr * EP + cc + 4);
+        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        epilogue8(p, v, m0 + wm * 64 + h * 32 + rr, n0 + wn * 64 + cc, sk, cbase);
+      }
     }
-  }
+    wave_lds_fence();
+  };
+  half(std::integral_constant<int, 0>{});
+  half(std::integral_constant<int, 1>{});
 }
 
 }  // namespace
@@ -279,6 +388,12 @@ extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
   p.a_row_scale = d->a_row_scale; p.a_rows_per_scale = d->a_rows_per_scale > 0 ? d->a_rows_per_scale : 1;
   if (p.a_row_scale && !d->a_f32) return lrce_fail(LRCE_E_ARG, "gemm: a_row_scale needs f32 A");
   p.tiles_m = (d->m + BM - 1) / BM; p.tiles_n = (d->n + BN - 1) / BN;
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool out32 = d->flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM);
+  p.vec = (d->n % 8 == 0) && (d->ldc % 8 == 0) && al16(d->c) && (d->stride_c % 8 == 0) &&
+          (!d->bias || al16(d->bias)) && (!d->aux || (al16(d->aux) && d->ld_aux % 8 == 0)) &&
+          (!d->aux_out || (al16(d->aux_out) && d->ld_aux_out % 8 == 0));
+  (void)out32;
   dim3 grid(p.tiles_m * p.tiles_n, d->batch * split);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int key = (d->a_kmajor ? 4 : 0) | (d->b_kmajor ? 2 : 0) | (d->a_f32 ? 1 : 0);

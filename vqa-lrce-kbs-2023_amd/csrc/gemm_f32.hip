@@ -130,6 +130,136 @@ __global__ void __launch_bounds__(NT) gemm_f32_kernel(GemmF32P p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Skinny-M exact-f32 kernels (M <= 64: the decoder's B or 5B summary-token rows).  The tiled kernel
+// above puts a 64x64 tile per block, i.e. only N/64 blocks for these shapes; here a block owns 16
+// output columns for ALL rows and its 4 waves split the reduction, so a 768-wide linear is 48
+// blocks that each stream a 16-row slab of the weight once (float4 / 64-B row segments), and the
+// 4 partial 16x16 tiles are combined through LDS before the fused epilogue.
+
+constexpr int SK_NT = 256;
+
+struct SkinnyP {
+  const float* a;
+  const float* b;
+  void* c;
+  long long lda, ldb, ldc;
+  int m, n, k;
+  int flags;
+  const float* bias;
+  const void* aux;
+  long long ld_aux;
+  bf16* aux_out;
+  long long ld_aux_out;
+  float alpha;
+  const float* row_scale;
+  int rows_per_scale;
+  int scale_cols;
+  float scale_val;
+};
+
+__device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, int n) {
+  const int fl = p.flags;
+  const long long row = m;
+  x = x * p.alpha + ((fl & LRCE_EPI_BIAS) ? p.bias[n] : 0.f);
+  x *= (n < p.scale_cols) ? p.scale_val : 1.f;
+  if (fl & LRCE_EPI_GELU) {
+    if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + n] = f2bf(x);
+    x = gelu_f(x);
+  }
+  if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]));
+  if (p.row_scale) x *= p.row_scale[m / p.rows_per_scale];
+  if (fl & LRCE_EPI_RESID) x += static_cast<const float*>(p.aux)[row * p.ld_aux + n];
+  if (fl & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) {
+    static_cast<float*>(p.c)[row * p.ldc + n] += x;   // one owner per element: a plain RMW suffices
+  } else if (fl & LRCE_EPI_OUT_F32) {
+    static_cast<float*>(p.c)[row * p.ldc + n] = x;
+    if (fl & LRCE_EPI_OUT_BOTH) p.aux_out[row * p.ld_aux_out + n] = f2bf(x);
+  } else {
+    static_cast<bf16*>(p.c)[row * p.ldc + n] = f2bf(x);
+  }
+}
+
+// C[m][n] = sum_k A[m][k] * B(k, n); B_KM: B stored [n][k] (forward, W), else [k][n] (dX = dY W).
+template <int MT, bool B_KM>
+__global__ void __launch_bounds__(SK_NT) skinny_kernel(SkinnyP p) {
+  __shared__ float red[4][MT][16][17];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int n = n0 + col;
+  const bool n_ok = n < p.n;
+  const int nc = n_ok ? n : 0;
+  int kchunk = (p.k + 3) / 4;
+  kchunk = (kchunk + 15) & ~15;
+  const int kb = wave * kchunk, ke = min(p.k, kb + kchunk);
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int k = kb; k < ke; k += 16) {
+    const int kk = k + 4 * grp;
+    const bool k_ok = kk < ke;             // k % 4 == 0: a float4 is all in or all out
+    const int kc = k_ok ? kk : 0;
+    float4 bv;
+    if (B_KM) {
+      bv = *reinterpret_cast<const float4*>(p.b + (long long)nc * p.ldb + kc);
+    } else {
+      const float* bp = p.b + (long long)kc * p.ldb + nc;
+      bv = make_float4(bp[0], bp[p.ldb], bp[2 * p.ldb], bp[3 * p.ldb]);
+    }
+    if (!(k_ok && n_ok)) bv = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = t * 16 + col;
+      const bool ok = k_ok && m < p.m;
+      float4 av = *reinterpret_cast<const float4*>(p.a + (long long)(ok ? m : 0) * p.lda + kc);
+      if (!ok) av = make_float4(0.f, 0.f, 0.f, 0.f);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][t][grp * 4 + r][col] = acc[t][r];
+  __syncthreads();
+  const int ml = threadIdx.x >> 4, nl = threadIdx.x & 15;
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = t * 16 + ml, nn = n0 + nl;
+    if (m < p.m && nn < p.n) {
+      const float x = red[0][t][ml][nl] + red[1][t][ml][nl] + red[2][t][ml][nl] + red[3][t][ml][nl];
+      sk_epilogue(p, x, m, nn);
+    }
+  }
+}
+
+// C[m][n] (+)= alpha * sum_{r < R} A[r][m] * B[r][n] with R <= 64 (dW of a skinny linear):
+// one thread per 4 consecutive columns, the R-term outer-product sum in registers, one RMW.
+__global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int nq = p.n >> 2;
+  if (q >= (long long)p.m * nq) return;
+  const int m = (int)(q / nq), n = (int)(q % nq) * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < p.k; ++r) {
+    const float av = p.a[(long long)r * p.lda + m];
+    const float4 bv = *reinterpret_cast<const float4*>(p.b + (long long)r * p.ldb + n);
+    acc.x = fmaf(av, bv.x, acc.x); acc.y = fmaf(av, bv.y, acc.y); acc.z = fmaf(av, bv.z, acc.z); acc.w = fmaf(av, bv.w, acc.w);
+  }
+  float4* cp = reinterpret_cast<float4*>(static_cast<float*>(p.c) + (long long)m * p.ldc + n);
+  acc.x *= p.alpha; acc.y *= p.alpha; acc.z *= p.alpha; acc.w *= p.alpha;
+  if (p.flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) {
+    const float4 o = *cp;
+    acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+  }
+  *cp = acc;
+}
+
 }  // namespace
 
 int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
@@ -138,6 +268,43 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
   if (d->a_kmajor ? (d->k % 4) : (d->m % 4)) return lrce_fail(LRCE_E_ARG, "gemm(f32): A contiguous dim %% 4 != 0");
   if (d->b_kmajor ? (d->k % 4) : (d->n % 4)) return lrce_fail(LRCE_E_ARG, "gemm(f32): B contiguous dim %% 4 != 0");
   if ((d->lda % 4) || (d->ldb % 4)) return lrce_fail(LRCE_E_ARG, "gemm(f32): lda/ldb %% 4 != 0");
+  const bool plain = !d->a_map && !d->c_map && !d->a_row_scale && d->split_k <= 1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (plain) {
+    SkinnyP q;
+    q.a = static_cast<const float*>(d->a); q.b = static_cast<const float*>(d->b); q.c = d->c;
+    q.lda = d->lda; q.ldb = d->ldb; q.ldc = d->ldc;
+    q.m = d->m; q.n = d->n; q.k = d->k; q.flags = d->flags; q.bias = d->bias;
+    q.aux = d->aux; q.ld_aux = d->ld_aux; q.aux_out = static_cast<bf16*>(d->aux_out); q.ld_aux_out = d->ld_aux_out;
+    q.alpha = d->alpha; q.row_scale = d->row_scale; q.rows_per_scale = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
+    q.scale_cols = d->scale_cols; q.scale_val = d->scale_val;
+    const bool outer_ok = !d->a_kmajor && !d->b_kmajor && d->k <= 64 && (d->n % 4) == 0 && (d->ldc % 4) == 0 &&
+                          (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) == 0 &&
+                          (d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) && !d->row_scale &&
+                          d->scale_cols == 0 && (reinterpret_cast<uintptr_t>(d->c) & 15) == 0 &&
+                          (reinterpret_cast<uintptr_t>(d->b) & 15) == 0;
+    if (outer_ok) {
+      const long long work = (long long)d->m * (d->n / 4);
+      outer_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(q);
+      return lrce_check_launch("gemm_f32(outer)");
+    }
+    if (d->a_kmajor && d->m <= 64 && (reinterpret_cast<uintptr_t>(d->a) & 15) == 0 &&
+        (!d->b_kmajor || (reinterpret_cast<uintptr_t>(d->b) & 15) == 0)) {
+      const int mt = (d->m + 15) / 16;
+      dim3 grid((d->n + 15) / 16);
+#define LRCE_SK(MT)                                                                          \
+  if (d->b_kmajor) skinny_kernel<MT, true><<<grid, SK_NT, 0, st>>>(q);                      \
+  else skinny_kernel<MT, false><<<grid, SK_NT, 0, st>>>(q);
+      switch (mt) {
+        case 1: LRCE_SK(1) break;
+        case 2: LRCE_SK(2) break;
+        case 3: LRCE_SK(3) break;
+        default: LRCE_SK(4) break;
+      }
+#undef LRCE_SK
+      return lrce_check_launch("gemm_f32(skinny)");
+    }
+  }
   GemmF32P p;
   p.a = static_cast<const float*>(d->a); p.b = static_cast<const float*>(d->b); p.c = d->c;
   p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc;

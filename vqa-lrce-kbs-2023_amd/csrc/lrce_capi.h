@@ -5,3 +5,4 @@
 
 int lrce_fail(int code, const char* fmt, ...);
 int lrce_check_launch(const char* what);
+const uint64_t* lrce_rng_offset();  // registered device RNG offset (or nullptr)

@@ -19,6 +19,7 @@ constexpr int MAXK = 192;
 
 struct MhaP {
   LrceMhaDesc d;
+  const uint64_t* off;  // device RNG offset (lrce_set_rng_offset)
 };
 
 __device__ __forceinline__ const bf16* key_row(const LrceMhaDesc& d, const uint16_t* p1, const uint16_t* p2, int b, int j, int h) {
@@ -30,10 +31,10 @@ __device__ __forceinline__ float ld_io(const LrceMhaDesc& d, const void* p, long
   return d.f32_io ? static_cast<const float*>(p)[i] : bf2f(static_cast<const bf16*>(p)[i]);
 }
 
-__device__ __forceinline__ float drop_factor(const LrceMhaDesc& d, int b, int h, int i, int j, int Lk) {
+__device__ __forceinline__ float drop_factor(const LrceMhaDesc& d, const uint64_t* off, int b, int h, int i, int j, int Lk) {
   if (d.drop_p <= 0.f) return 1.f;
   const uint64_t idx = (((uint64_t)b * d.H + h) * d.Lq + i) * (uint64_t)Lk + j;
-  return lrce_uniform(d.seed, idx) >= d.drop_p ? 1.0f / (1.0f - d.drop_p) : 0.f;
+  return lrce_uniform(lrce_seed(d.seed, off), idx) >= d.drop_p ? 1.0f / (1.0f - d.drop_p) : 0.f;
 }
 
 __global__ void __launch_bounds__(256) mha_fwd_kernel(MhaP P) {
@@ -78,7 +79,7 @@ __global__ void __launch_bounds__(256) mha_fwd_kernel(MhaP P) {
     for (int t = 0; t < MAXK / 64; ++t) {
       const int j = lane + 64 * t;
       const float p = keep[t] ? __expf(sc[t] - m) : 0.f;
-      if (j < Lk) ps[wave][j] = p * drop_factor(d, b, h, i, j, Lk);
+      if (j < Lk) ps[wave][j] = p * drop_factor(d, P.off, b, h, i, j, Lk);
       s += p;
     }
     s = wave_sum(s);
@@ -139,7 +140,7 @@ __global__ void __launch_bounds__(256) mha_bwd_kernel(MhaP P) {
       if (j < Lk) {
         const bool keep = !d.key_mask || d.key_mask[(long long)b * Lk + j] != 0;
         const float p = keep ? __expf(sc[t] - l) : 0.f;
-        const float f = drop_factor(d, b, h, i, j, Lk);
+        const float f = drop_factor(d, P.off, b, h, i, j, Lk);
         ps[wave][j] = p * f;                 // dV uses the dropped probabilities
         dss[wave][j] = p * (f * dp[t] - delta);
       }
@@ -188,14 +189,14 @@ int check(const LrceMhaDesc* d, bool bwd) {
 
 extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, false)) return rc;
-  MhaP p{*d};
+  MhaP p{*d, lrce_rng_offset()};
   mha_fwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
   return lrce_check_launch("mha_fwd");
 }
 
 extern "C" int lrce_mha_bwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, true)) return rc;
-  MhaP p{*d};
+  MhaP p{*d, lrce_rng_offset()};
   mha_bwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
   return lrce_check_launch("mha_bwd");
 }

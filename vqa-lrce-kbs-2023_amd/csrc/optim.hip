@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
                                                     float* __restrict__ v, const int* __restrict__ chunk_tensor,
                                                     const float* __restrict__ tensor_lr, const float* __restrict__ sumsq,
                                                     bf16* __restrict__ pb, int n_chunks, float b1, float b2, float eps, float wd,
-                                                    float gscale, float reg, float bc1, float bc2) {
+                                                    float gscale, float reg, float bc1, float bc2, const float* __restrict__ step_dev) {
   const int c = blockIdx.x;
   if (c >= n_chunks) return;
   const int t = chunk_tensor[c];
@@ -39,6 +39,11 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
   const float4 gg = *reinterpret_cast<const float4*>(g + i);
   float4 mm = *reinterpret_cast<float4*>(m + i);
   float4 vv = *reinterpret_cast<float4*>(v + i);
+  if (step_dev) {
+    const float t = *step_dev;
+    bc1 = 1.0f - powf(b1, t);
+    bc2 = 1.0f - powf(b2, t);
+  }
   const float step = lr / bc1, isb2 = rsqrtf(bc2), decay = 1.0f - lr * wd;
   float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
   bf16x4 ob;
@@ -70,11 +75,12 @@ extern "C" int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, in
 
 extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
                                const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
-                               float weight_decay, float grad_scale, float reg, float bc1, float bc2, void* stream) {
+                               float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
+                               void* stream) {
   if (!p || !g || !m || !v || !chunk_tensor || !tensor_lr) return lrce_fail(LRCE_E_ARG, "adamw_step: null pointer");
   if (n_chunks > 0)
     adamw_kernel<<<n_chunks, 256, 0, static_cast<hipStream_t>(stream)>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq,
                                                                          reinterpret_cast<bf16*>(p_bf16), n_chunks, beta1, beta2, eps,
-                                                                         weight_decay, grad_scale, reg, bc1, bc2);
+                                                                         weight_decay, grad_scale, reg, bc1, bc2, step);
   return lrce_check_launch("adamw_step");
 }

@@ -75,6 +75,13 @@ class GradReducer:
         return 1.0 / self.world
 
 
+    def reduce_all(self):
+        """All buckets now (graph mode: the backward ran inside a HIP graph with no reducer attached);
+        async per bucket on RCCL's stream, then wait.  Returns the optimizer's grad_scale."""
+        self.begin()
+        return self.finish()
+
+
 def broadcast_parameters(flat, src=0, group=None):
     """One collective for all 312 M parameters (DDP construction broadcast, agent_base.py:76)."""
     if dist.is_initialized() and dist.get_world_size(group) > 1:

@@ -335,6 +335,30 @@ def l2norm_multi(p, chunk_tensor, n_chunks, sumsq, n_tensors):
 
 
 def adamw_step(p, g, m, v, chunk_tensor, tensor_lr, sumsq, p_bf16, n_chunks, beta1, beta2, eps, wd, grad_scale, reg,
-               bc1, bc2):
+               bc1, bc2, step=None):
+    """step: optional f32 device scalar holding t (bias corrections computed on device: graph-safe)."""
     call("lrce_adamw_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(chunk_tensor), ptr(tensor_lr), ptr(sumsq), ptr(p_bf16),
-         n_chunks, beta1, beta2, eps, wd, grad_scale, reg, bc1, bc2, stream_of(p))
+         n_chunks, beta1, beta2, eps, wd, grad_scale, reg, bc1, bc2, ptr(step), stream_of(p))
+
+
+_RNG_OFFSETS = {}
+_RNG_STRIDE = 0x2545F4914F6CDD1D & ((1 << 62) - 1)
+
+
+def rng_offset(device):
+    """The device RNG offset (int64 scalar) registered with lrce_set_rng_offset (one per process:
+    the native library keeps a single pointer, so the first device registered wins)."""
+    dev = torch.device(device)
+    t = _RNG_OFFSETS.get(dev)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int64, device=dev)
+        _RNG_OFFSETS[dev] = t
+        if len(_RNG_OFFSETS) == 1:
+            call("lrce_set_rng_offset", ptr(t))
+    return t
+
+
+def rng_advance(device):
+    """New masks for the next training step: one device add (captured into a graph it runs on every
+    replay).  Forward and backward of one step see the same offset."""
+    rng_offset(device).add_(_RNG_STRIDE)

@@ -15,6 +15,7 @@ import torch.nn as nn
 
 from ..feature_extractor.text import TextExtractor
 from ..feature_extractor.video import VideoExtractor, SWIN_B_CKPT
+from .. import kernels as K
 from ..runtime import prepare
 from .fusionv3 import LRCEOpenEnded, LRCEMultipleChoice, LRCECount
 
@@ -42,7 +43,9 @@ class E2EBase(nn.Module):
         return self.video_extractor(video_clips)
 
     def forward(self, video_clips, texts, texts_attention_mask, texts_type_ids):
-        prepare(self)
+        flat = prepare(self)
+        if self.training:
+            K.rng_advance(flat.device)   # fresh dropout masks per step, also under HIP-graph replay
         video_features = self.extract_video_features(video_clips)
         texts_features = self.extract_text_features(texts, texts_attention_mask, texts_type_ids)
         return self.fusion_model(video_features, texts_features, texts_attention_mask)

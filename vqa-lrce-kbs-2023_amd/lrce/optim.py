@@ -38,6 +38,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.tensor_lr = torch.zeros(len(flat.params), device=dev)
         self._lr_cache = None
         self.step_count = 0
+        self.step_t = torch.zeros(1, device=dev)   # device step count t (graph-safe bias corrections)
         self.last_l2 = None
 
     def _sync_lrs(self):
@@ -58,12 +59,13 @@ class FusedAdamW(torch.optim.Optimizer):
         flat = self.flat
         self._sync_lrs()
         self.step_count += 1
+        self.step_t.add_(1.0)
         b1, b2 = self.defaults["betas"]
         t = self.step_count
         K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params))
         K.adamw_step(flat.f32, flat.grad, self.exp_avg, self.exp_avg_sq, flat.chunk_tensor, self.tensor_lr, self.sumsq,
                      flat.bf16, flat.n_chunks, b1, b2, self.defaults["eps"], self.defaults["weight_decay"],
-                     float(grad_scale), self.reg_strength, 1.0 - b1 ** t, 1.0 - b2 ** t)
+                     float(grad_scale), self.reg_strength, 1.0 - b1 ** t, 1.0 - b2 ** t, step=self.step_t)
         flat.mark_bf16_fresh()
         return loss
 
