@@ -47,7 +47,9 @@ enum {
   LRCE_EPI_ATOMIC = 32,   /* f32 atomicAdd into C (split-K / gradient accumulation) */
   LRCE_EPI_ACCUM = 64,    /* C(f32) += y, non-atomic */
   LRCE_EPI_AUX_OUT = 128, /* store pre-activation (bf16) into aux_out */
-  LRCE_EPI_OUT_BOTH = 256 /* also write a bf16 copy of y into aux_out (f32 C + bf16 shadow) */
+  LRCE_EPI_OUT_BOTH = 256, /* also write a bf16 copy of y into aux_out (f32 C + bf16 shadow) */
+  LRCE_EPI_BIAS_GRAD = 512 /* weight-gradient GEMMs (A M-major = dY^T): also bias[m] += sum_k A(m,k)
+                              (the nn.Linear bias gradient, with A's row map / row scale applied) */
 };
 
 typedef struct LrceGemmDesc {
@@ -213,7 +215,10 @@ int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks,
 int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
                     const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
                     float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
-                    void* stream); /* step: optional device step count t; when set, bc1/bc2 are computed from it */
+                    float* sumsq_next, void* stream);
+/* step: optional device step count t (bc1/bc2 then computed from it: graph-safe).  sumsq_next:
+ * optional zeroed buffer that receives ||p_t||^2 of the UPDATED parameters, i.e. the next step's
+ * sumsq without a separate norm pass over the 1.25 GB master copy. */
 
 /* BERT embeddings before their LayerNorm (HF BertEmbeddings): out[r] = word[ids[r]] + pos[r % L] +
  * type[types[r]] (f32 tables, int64 ids), and the scatter-add backward into the three tables. */

@@ -393,3 +393,31 @@ def test_rng_offset_changes_masks_and_backward_agrees():
     assert torch.equal(dx != 0, y1 != 0)
     off.zero_()
     assert torch.equal(k.dropout(x, 0.5, 9), y0)
+
+
+def test_fused_adamw_optimizer_matches_torch_over_steps():
+    """FusedAdamW (flat store, device step count, norms carried from the previous update) against
+    torch.optim.AdamW + the reference's L2 term (agent_base.py:103-108) on a small module."""
+    from lrce.optim import FusedAdamW
+    from lrce.runtime import ensure
+    torch.manual_seed(3)
+    net = torch.nn.Sequential(torch.nn.Linear(24, 40), torch.nn.LayerNorm(40), torch.nn.Linear(40, 8)).to(dev)
+    ref = [p.detach().clone().requires_grad_(True) for p in net.parameters()]
+    flat = ensure(net)
+    groups = [{"params": list(net[0].parameters()), "lr": 2e-3}, {"params": list(net[1:].parameters()), "lr": 1e-3}]
+    opt = FusedAdamW(net, groups, lr=1e-3, reg_strength=0.001)
+    n0 = len(list(net[0].parameters()))
+    topt = torch.optim.AdamW([{"params": ref[:n0], "lr": 2e-3}, {"params": ref[n0:], "lr": 1e-3}])
+    for step in range(4):
+        gs = [torch.randn_like(r) for r in ref]
+        for p, g in zip(net.parameters(), gs):
+            flat.g32(p).copy_(g)
+        opt.step()
+        opt.zero_grad()
+        topt.zero_grad()
+        loss = sum((r * g).sum() for r, g in zip(ref, gs)) + 0.001 * sum(r.norm() for r in ref)
+        loss.backward()
+        topt.step()
+    for p, r in zip(net.parameters(), ref):
+        assert rel(p.detach(), r.detach()) < 1e-5
+    assert abs(float(opt.l2_term()) - float(sum(r.norm() for r in ref))) < 1e-3

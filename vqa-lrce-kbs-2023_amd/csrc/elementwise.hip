@@ -1,6 +1,8 @@
 // Memory-bound helpers on the LRCE path: patch im2col (+ImageNet normalise +T padding), bias
 // column sums, casts, dropout, and the embedding sums of BERT / LRCE positional embeddings.
 // All vectorised 16 B per lane where the layout allows; HBM-bound by construction.
+#include <algorithm>
+
 #include "common.h"
 #include "lrce_capi.h"
 
@@ -44,25 +46,47 @@ __global__ void im2col_kernel(const float* __restrict__ clips, bf16* __restrict_
 }
 
 // ---------------------------------------------------------------- column sums
-template <typename T>
+// block: 256 threads = 64 lanes x V consecutive columns x 4 row groups; grid.x over column blocks,
+// grid.y over row chunks; V = 4 (16-B f32 / 8-B bf16 loads) when rows are aligned.
+template <typename T, int V>
 __global__ void colsum_kernel(const T* __restrict__ x, const int* __restrict__ map, long long ld, int m, int n,
                               const float* __restrict__ rsc, int rps, float* __restrict__ out) {
-  // block: 256 threads = 64 columns x 4 row-groups; grid.x over column blocks, grid.y over row chunks
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int col = (blockIdx.x * 64 + (threadIdx.x & 63)) * V;
   const int rg = threadIdx.x >> 6;
   const int rows_per = (m + gridDim.y - 1) / gridDim.y;
   const int r0 = blockIdx.y * rows_per, r1 = min(m, r0 + rows_per);
-  float s = 0.f;
-  if (col < n)
+  float s[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) s[i] = 0.f;
+  if (col < n) {
     for (int r = r0 + rg; r < r1; r += 4) {
       const long long rr = map ? (long long)map[r] : (long long)r;
       const float f = rsc ? rsc[r / rps] : 1.0f;
-      s += (float)x[rr * ld + col] * f;
+      const T* src = x + rr * ld + col;
+      if constexpr (V == 4) {
+        if constexpr (sizeof(T) == 4) {
+          const float4 v = *reinterpret_cast<const float4*>(src);
+          s[0] += v.x * f; s[1] += v.y * f; s[2] += v.z * f; s[3] += v.w * f;
+        } else {
+          const bf16x4 v = *reinterpret_cast<const bf16x4*>(src);
+          s[0] += bf2f(v[0]) * f; s[1] += bf2f(v[1]) * f; s[2] += bf2f(v[2]) * f; s[3] += bf2f(v[3]) * f;
+        }
+      } else {
+        s[0] += (float)src[0] * f;
+      }
     }
-  __shared__ float red[4][64];
-  red[rg][threadIdx.x & 63] = s;
+  }
+  __shared__ float red[4][64 * V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) red[rg][(threadIdx.x & 63) * V + i] = s[i];
   __syncthreads();
-  if (rg == 0 && col < n) atomicAdd(out + col, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+  if (rg == 0) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int c = (threadIdx.x & 63) * V + i;
+      if (col + i < n) atomicAdd(out + col + i, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    }
+  }
 }
 
 __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
@@ -214,12 +238,20 @@ extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int
   if (rows_per_scale < 1) rows_per_scale = 1;
   if (!x || !out) return lrce_fail(LRCE_E_ARG, "colsum: null pointer");
   if (m <= 0 || n <= 0) return LRCE_OK;
-  int chunks = (m + 255) / 256;
-  if (chunks > 256) chunks = 256;
-  dim3 grid((n + 63) / 64, chunks);
+  const bool vec = (n % 4 == 0) && (ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & (x_f32 ? 15 : 7)) == 0);
+  const int V = vec ? 4 : 1;
+  const int cblocks = (n + 64 * V - 1) / (64 * V);
+  int chunks = (m + 63) / 64;                       // >= 16 rows per row group
+  chunks = std::max(1, std::min(chunks, (1024 + cblocks - 1) / cblocks));
+  dim3 grid(cblocks, chunks);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (x_f32) colsum_kernel<float><<<grid, 256, 0, s>>>(static_cast<const float*>(x), row_map, ld, m, n, row_scale, rows_per_scale, out);
-  else colsum_kernel<bf16><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), row_map, ld, m, n, row_scale, rows_per_scale, out);
+  if (x_f32) {
+    if (vec) colsum_kernel<float, 4><<<grid, 256, 0, s>>>(static_cast<const float*>(x), row_map, ld, m, n, row_scale, rows_per_scale, out);
+    else colsum_kernel<float, 1><<<grid, 256, 0, s>>>(static_cast<const float*>(x), row_map, ld, m, n, row_scale, rows_per_scale, out);
+  } else {
+    if (vec) colsum_kernel<bf16, 4><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), row_map, ld, m, n, row_scale, rows_per_scale, out);
+    else colsum_kernel<bf16, 1><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), row_map, ld, m, n, row_scale, rows_per_scale, out);
+  }
   return lrce_check_launch("colsum");
 }
 

@@ -352,8 +352,30 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
 
 int lrce_gemm_f32(const LrceGemmDesc* d, void* stream);
 
+extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, int m, int n, const float* row_scale,
+                           int rows_per_scale, float* out, void* stream);
+
+static int gemm_dispatch(const LrceGemmDesc* d, void* stream);
+bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
+
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
   if (!d || !d->a || !d->b || !d->c) return lrce_fail(LRCE_E_ARG, "gemm: null pointer");
+  if (!(d->flags & LRCE_EPI_BIAS_GRAD)) return gemm_dispatch(d, stream);
+  // bias gradient of a weight-gradient GEMM: db[m] += sum_k A(m, k)
+  if (d->a_kmajor || !d->bias || d->batch != 1) return lrce_fail(LRCE_E_ARG, "gemm: BIAS_GRAD needs M-major A, bias, batch 1");
+  if (d->flags & LRCE_EPI_BIAS) return lrce_fail(LRCE_E_ARG, "gemm: BIAS and BIAS_GRAD are exclusive");
+  const bool fused = lrce_gemm_f32_outer_ok(d);
+  if (fused) return gemm_dispatch(d, stream);   // the skinny outer-product kernel sums A as it goes
+  LrceGemmDesc g = *d;
+  g.flags &= ~LRCE_EPI_BIAS_GRAD;
+  g.bias = nullptr;
+  if (int rc = gemm_dispatch(&g, stream)) return rc;
+  if (d->alpha != 1.0f) return lrce_fail(LRCE_E_ARG, "gemm: BIAS_GRAD with alpha != 1");
+  return lrce_colsum(d->a, d->a_f32, d->a_map, d->lda, d->k, d->m, d->a_row_scale, d->a_rows_per_scale,
+                     const_cast<float*>(d->bias), stream);
+}
+
+static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   if (d->m <= 0 || d->n <= 0 || d->k <= 0 || d->batch <= 0) return lrce_fail(LRCE_E_ARG, "gemm: empty shape");
   if ((d->flags & (LRCE_EPI_DGELU | LRCE_EPI_RESID)) && !d->aux) return lrce_fail(LRCE_E_ARG, "gemm: aux missing");
   if ((d->flags & (LRCE_EPI_AUX_OUT | LRCE_EPI_OUT_BOTH)) && !d->aux_out) return lrce_fail(LRCE_E_ARG, "gemm: aux_out missing");

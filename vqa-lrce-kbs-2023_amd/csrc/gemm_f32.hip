@@ -157,6 +157,7 @@ struct SkinnyP {
   int rows_per_scale;
   int scale_cols;
   float scale_val;
+  float* bias_grad;
 };
 
 __device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, int n) {
@@ -197,30 +198,38 @@ __global__ void __launch_bounds__(SK_NT) skinny_kernel(SkinnyP p) {
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int k = kb; k < ke; k += 16) {
-    const int kk = k + 4 * grp;
-    const bool k_ok = kk < ke;             // k % 4 == 0: a float4 is all in or all out
-    const int kc = k_ok ? kk : 0;
-    float4 bv;
-    if (B_KM) {
-      bv = *reinterpret_cast<const float4*>(p.b + (long long)nc * p.ldb + kc);
-    } else {
-      const float* bp = p.b + (long long)kc * p.ldb + nc;
-      bv = make_float4(bp[0], bp[p.ldb], bp[2 * p.ldb], bp[3 * p.ldb]);
-    }
-    if (!(k_ok && n_ok)) bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = kb; k < ke; k += 64) {
+    // 4 k-steps of 16 per trip: all loads issued before the MFMAs (memory-level parallelism)
+    float4 bv[4], av[4][MT];
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const int m = t * 16 + col;
-      const bool ok = k_ok && m < p.m;
-      float4 av = *reinterpret_cast<const float4*>(p.a + (long long)(ok ? m : 0) * p.lda + kc);
-      if (!ok) av = make_float4(0.f, 0.f, 0.f, 0.f);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc[t], 0, 0, 0);
+    for (int u = 0; u < 4; ++u) {
+      const int kk = k + 16 * u + 4 * grp;
+      const bool k_ok = kk < ke;           // k % 4 == 0: a float4 is all in or all out
+      const int kc = k_ok ? kk : 0;
+      if (B_KM) {
+        bv[u] = *reinterpret_cast<const float4*>(p.b + (long long)nc * p.ldb + kc);
+      } else {
+        const float* bp = p.b + (long long)kc * p.ldb + nc;
+        bv[u] = make_float4(bp[0], bp[p.ldb], bp[2 * p.ldb], bp[3 * p.ldb]);
+      }
+      if (!(k_ok && n_ok)) bv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = t * 16 + col;
+        const bool ok = k_ok && m < p.m;
+        av[u][t] = *reinterpret_cast<const float4*>(p.a + (long long)(ok ? m : 0) * p.lda + kc);
+        if (!ok) av[u][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][t].x, bv[u].x, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][t].y, bv[u].y, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][t].z, bv[u].z, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][t].w, bv[u].w, acc[t], 0, 0, 0);
+      }
   }
 #pragma unroll
   for (int t = 0; t < MT; ++t)
@@ -246,8 +255,10 @@ __global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
   if (q >= (long long)p.m * nq) return;
   const int m = (int)(q / nq), n = (int)(q % nq) * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float asum = 0.f;
   for (int r = 0; r < p.k; ++r) {
     const float av = p.a[(long long)r * p.lda + m];
+    asum += av;
     const float4 bv = *reinterpret_cast<const float4*>(p.b + (long long)r * p.ldb + n);
     acc.x = fmaf(av, bv.x, acc.x); acc.y = fmaf(av, bv.y, acc.y); acc.z = fmaf(av, bv.z, acc.z); acc.w = fmaf(av, bv.w, acc.w);
   }
@@ -258,9 +269,19 @@ __global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
     acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
   }
   *cp = acc;
+  if ((p.flags & LRCE_EPI_BIAS_GRAD) && n == 0) p.bias_grad[m] += p.alpha * asum;   // db (one owner per m)
 }
 
 }  // namespace
+
+// the dW shape the outer-product kernel takes: A M-major, B N-major, reduction <= 64 rows
+bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d) {
+  return d->b_f32 && d->a_f32 && !d->a_kmajor && !d->b_kmajor && d->k <= 64 && (d->n % 4) == 0 && (d->ldc % 4) == 0 &&
+         (d->ldb % 4) == 0 && d->batch == 1 && !d->a_map && !d->c_map && !d->a_row_scale && d->split_k <= 1 &&
+         (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32 | LRCE_EPI_BIAS_GRAD)) == 0 &&
+         (d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) && !d->row_scale && d->scale_cols == 0 &&
+         (reinterpret_cast<uintptr_t>(d->c) & 15) == 0 && (reinterpret_cast<uintptr_t>(d->b) & 15) == 0;
+}
 
 int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
   if (!d->a_f32) return lrce_fail(LRCE_E_ARG, "gemm(f32 B): A must be f32 too");
@@ -278,16 +299,14 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
     q.aux = d->aux; q.ld_aux = d->ld_aux; q.aux_out = static_cast<bf16*>(d->aux_out); q.ld_aux_out = d->ld_aux_out;
     q.alpha = d->alpha; q.row_scale = d->row_scale; q.rows_per_scale = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
     q.scale_cols = d->scale_cols; q.scale_val = d->scale_val;
-    const bool outer_ok = !d->a_kmajor && !d->b_kmajor && d->k <= 64 && (d->n % 4) == 0 && (d->ldc % 4) == 0 &&
-                          (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) == 0 &&
-                          (d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) && !d->row_scale &&
-                          d->scale_cols == 0 && (reinterpret_cast<uintptr_t>(d->c) & 15) == 0 &&
-                          (reinterpret_cast<uintptr_t>(d->b) & 15) == 0;
+    q.bias_grad = const_cast<float*>(d->bias);
+    const bool outer_ok = lrce_gemm_f32_outer_ok(d);
     if (outer_ok) {
       const long long work = (long long)d->m * (d->n / 4);
       outer_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(q);
       return lrce_check_launch("gemm_f32(outer)");
     }
+    if (d->flags & LRCE_EPI_BIAS_GRAD) return lrce_fail(LRCE_E_ARG, "gemm(f32): internal: bias grad on a fused path");
     if (d->a_kmajor && d->m <= 64 && (reinterpret_cast<uintptr_t>(d->a) & 15) == 0 &&
         (!d->b_kmajor || (reinterpret_cast<uintptr_t>(d->b) & 15) == 0)) {
       const int mt = (d->m + 15) / 16;

@@ -173,6 +173,138 @@ __global__ void __launch_bounds__(256) mha_bwd_kernel(MhaP P) {
   }
 }
 
+// ---- single-query path (the recurrent decoder: Lq = 1, fusionv3.py:44-49) --------------------
+// One wave per (batch row, head), 4 per workgroup.  Scores: lane j reads key row j as 8 x 16 B
+// (q broadcast from LDS); softmax by wave reductions; output / dQ: lane = head dim, key rows read
+// coalesced (128 B per row).  dK/dV: one coalesced 64-float atomic row per key (rows are shared by
+// the bdiv answer choices and, for the question segment, by every recurrent step).
+constexpr int KT = MAXK / 64;
+
+__device__ __forceinline__ float dot_row64(const bf16* row, const float* qs) {
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const bf16x8 kv = *reinterpret_cast<const bf16x8*>(row + 8 * c);
+    const float4 q0 = *reinterpret_cast<const float4*>(qs + 8 * c);
+    const float4 q1 = *reinterpret_cast<const float4*>(qs + 8 * c + 4);
+    acc += bf2f(kv[0]) * q0.x + bf2f(kv[1]) * q0.y + bf2f(kv[2]) * q0.z + bf2f(kv[3]) * q0.w +
+           bf2f(kv[4]) * q1.x + bf2f(kv[5]) * q1.y + bf2f(kv[6]) * q1.z + bf2f(kv[7]) * q1.w;
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(256) mha1_fwd_kernel(MhaP P) {
+  const LrceMhaDesc& d = P.d;
+  __shared__ __attribute__((aligned(16))) float qs[4][D];
+  __shared__ float ps[4][MAXK];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.x * 4 + wave;
+  if (bh >= d.B * d.H) return;
+  const int b = bh / d.H, h = bh % d.H;
+  const int Lk = d.lk1 + d.lk2;
+  qs[wave][lane] = ld_io(d, d.q, (long long)b * d.ld_q + h * D + lane) * d.scale;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  float sc[KT];
+  bool keep[KT];
+  float m = -1.0e30f;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int j = lane + 64 * t;
+    keep[t] = j < Lk && (!d.key_mask || d.key_mask[(long long)b * Lk + j] != 0);
+    sc[t] = j < Lk ? dot_row64(key_row(d, d.k1, d.k2, b, j, h), qs[wave]) : 0.f;
+    if (keep[t]) m = fmaxf(m, sc[t]);
+  }
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int j = lane + 64 * t;
+    const float p = keep[t] ? __expf(sc[t] - m) : 0.f;
+    s += p;
+    if (j < Lk) ps[wave][j] = p * drop_factor(d, P.off, b, h, 0, j, Lk);
+  }
+  s = wave_sum(s);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+  int j = 0;
+  for (; j + 4 <= Lk; j += 4) {
+    o0 += ps[wave][j] * bf2f(key_row(d, d.v1, d.v2, b, j, h)[lane]);
+    o1 += ps[wave][j + 1] * bf2f(key_row(d, d.v1, d.v2, b, j + 1, h)[lane]);
+    o2 += ps[wave][j + 2] * bf2f(key_row(d, d.v1, d.v2, b, j + 2, h)[lane]);
+    o3 += ps[wave][j + 3] * bf2f(key_row(d, d.v1, d.v2, b, j + 3, h)[lane]);
+  }
+  for (; j < Lk; ++j) o0 += ps[wave][j] * bf2f(key_row(d, d.v1, d.v2, b, j, h)[lane]);
+  const float o = (o0 + o1) + (o2 + o3);
+  const long long oi = (long long)b * d.ld_o + h * D + lane;
+  if (d.f32_io) reinterpret_cast<float*>(d.out)[oi] = o / s;
+  else reinterpret_cast<bf16*>(d.out)[oi] = f2bf(o / s);
+  if (lane == 0) d.lse[(long long)b * d.H + h] = m + __logf(s);
+}
+
+__global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
+  const LrceMhaDesc& d = P.d;
+  __shared__ __attribute__((aligned(16))) float qs[4][D];
+  __shared__ __attribute__((aligned(16))) float gs[4][D];
+  __shared__ float ps[4][MAXK];
+  __shared__ float dss[4][MAXK];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.x * 4 + wave;
+  if (bh >= d.B * d.H) return;
+  const int b = bh / d.H, h = bh % d.H;
+  const int Lk = d.lk1 + d.lk2;
+  const float qd = ld_io(d, d.q, (long long)b * d.ld_q + h * D + lane) * d.scale;
+  const float dod = ld_io(d, d.dout, (long long)b * d.ld_o + h * D + lane);
+  const float od = ld_io(d, d.out, (long long)b * d.ld_o + h * D + lane);
+  const float delta = wave_sum(dod * od);
+  const float l = d.lse[(long long)b * d.H + h];
+  qs[wave][lane] = qd;
+  gs[wave][lane] = dod;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int j = lane + 64 * t;
+    if (j < Lk) {
+      const float sc = dot_row64(key_row(d, d.k1, d.k2, b, j, h), qs[wave]);
+      const float dp = dot_row64(key_row(d, d.v1, d.v2, b, j, h), gs[wave]);
+      const bool keep = !d.key_mask || d.key_mask[(long long)b * Lk + j] != 0;
+      const float p = keep ? __expf(sc - l) : 0.f;
+      const float f = drop_factor(d, P.off, b, h, 0, j, Lk);
+      ps[wave][j] = p * f;                  // dV uses the dropped probabilities
+      dss[wave][j] = p * (f * dp - delta);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  float g = 0.f;
+  for (int j = 0; j < Lk; ++j) {
+    const float ds = dss[wave][j];
+    g += ds * bf2f(key_row(d, d.k1, d.k2, b, j, h)[lane]);
+    float* dk;
+    float* dv;
+    if (j < d.lk1) {
+      const long long o = (long long)(b / d.kv1_bdiv) * d.stride_dkv1_b + (long long)j * d.ld_dkv1 + h * D + lane;
+      dk = d.dk1 + o; dv = d.dv1 + o;
+    } else {
+      const long long o = (long long)(b / d.kv2_bdiv) * d.stride_dkv2_b + (long long)(j - d.lk1) * d.ld_dkv2 + h * D + lane;
+      dk = d.dk2 + o; dv = d.dv2 + o;
+    }
+    __hip_atomic_fetch_add(dk, ds * qd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(dv, ps[wave][j] * dod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  d.dq[(long long)b * d.ld_dq + h * D + lane] = g * d.scale;
+}
+
+// key/value rows readable as 16-B vectors (single-query path)
+bool aligned_rows(const LrceMhaDesc* d) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  bool ok = al(d->k1) && al(d->v1) && d->ld_kv1 % 8 == 0 && d->stride_kv1_b % 8 == 0;
+  if (d->lk2 > 0) ok = ok && al(d->k2) && al(d->v2) && d->ld_kv2 % 8 == 0 && d->stride_kv2_b % 8 == 0;
+  return ok;
+}
+
 int check(const LrceMhaDesc* d, bool bwd) {
   if (!d || !d->q || !d->k1 || !d->v1 || !d->out || !d->lse) return lrce_fail(LRCE_E_ARG, "mha: null pointer");
   if (d->d != D) return lrce_fail(LRCE_E_ARG, "mha: head dim %d unsupported (64)", d->d);
@@ -190,6 +322,10 @@ int check(const LrceMhaDesc* d, bool bwd) {
 extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, false)) return rc;
   MhaP p{*d, lrce_rng_offset()};
+  if (d->Lq == 1 && aligned_rows(d)) {
+    mha1_fwd_kernel<<<(d->B * d->H + 3) / 4, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
+    return lrce_check_launch("mha_fwd");
+  }
   mha_fwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
   return lrce_check_launch("mha_fwd");
 }
@@ -197,6 +333,10 @@ extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
 extern "C" int lrce_mha_bwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, true)) return rc;
   MhaP p{*d, lrce_rng_offset()};
+  if (d->Lq == 1 && aligned_rows(d)) {
+    mha1_bwd_kernel<<<(d->B * d->H + 3) / 4, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
+    return lrce_check_launch("mha_bwd");
+  }
   mha_bwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
   return lrce_check_launch("mha_bwd");
 }

@@ -27,7 +27,8 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
                                                     float* __restrict__ v, const int* __restrict__ chunk_tensor,
                                                     const float* __restrict__ tensor_lr, const float* __restrict__ sumsq,
                                                     bf16* __restrict__ pb, int n_chunks, float b1, float b2, float eps, float wd,
-                                                    float gscale, float reg, float bc1, float bc2, const float* __restrict__ step_dev) {
+                                                    float gscale, float reg, float bc1, float bc2, const float* __restrict__ step_dev,
+                                                    float* __restrict__ sumsq_next) {
   const int c = blockIdx.x;
   if (c >= n_chunks) return;
   const int t = chunk_tensor[c];
@@ -60,6 +61,14 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
   *reinterpret_cast<float4*>(m + i) = mm;
   *reinterpret_cast<float4*>(v + i) = vv;
   if (pb) *reinterpret_cast<bf16x4*>(pb + i) = ob;
+  if (sumsq_next) {
+    float q = pp.x * pp.x + pp.y * pp.y + pp.z * pp.z + pp.w * pp.w;
+    q = wave_sum(q);
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(sumsq_next + t, red[0] + red[1] + red[2] + red[3]);
+  }
 }
 
 }  // namespace
@@ -68,7 +77,7 @@ extern "C" int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, in
                                  void* stream) {
   if (!p || !chunk_tensor || !sumsq) return lrce_fail(LRCE_E_ARG, "l2norm_multi: null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipMemsetAsync(sumsq, 0, sizeof(float) * n_tensors, s);
+  (void)hipMemsetAsync(sumsq, 0, sizeof(float) * n_tensors, s);
   if (n_chunks > 0) sumsq_kernel<<<n_chunks, 256, 0, s>>>(p, chunk_tensor, n_chunks, sumsq);
   return lrce_check_launch("l2norm_multi");
 }
@@ -76,11 +85,11 @@ extern "C" int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, in
 extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
                                const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
                                float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
-                               void* stream) {
+                               float* sumsq_next, void* stream) {
   if (!p || !g || !m || !v || !chunk_tensor || !tensor_lr) return lrce_fail(LRCE_E_ARG, "adamw_step: null pointer");
   if (n_chunks > 0)
     adamw_kernel<<<n_chunks, 256, 0, static_cast<hipStream_t>(stream)>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq,
                                                                          reinterpret_cast<bf16*>(p_bf16), n_chunks, beta1, beta2, eps,
-                                                                         weight_decay, grad_scale, reg, bc1, bc2, step);
+                                                                         weight_decay, grad_scale, reg, bc1, bc2, step, sumsq_next);
   return lrce_check_launch("adamw_step");
 }

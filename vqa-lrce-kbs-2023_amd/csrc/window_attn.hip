@@ -365,20 +365,37 @@ __global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restric
 }
 
 // sum dS over windows (per head, per padded (q,k)) and scatter-add into the bias table gradient
+// Relative-position-bias gradient: sum dS over the windows of a window chunk (grid.y) for 8
+// consecutive per-lane-ordered elements per thread (16-B loads), then scatter-add to the table.
 __global__ void dbias_kernel(const bf16* __restrict__ ds, int n_win, int n, int nH, const int64_t* __restrict__ index,
-                             int ld, float* __restrict__ tgrad) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long long)nH * PH_ELEMS) return;
-  const int h = e / PH_ELEMS, el = e % PH_ELEMS;
-  const int reg = el & 15, lane = (el >> 4) & 63, tile = el / TILE_ELEMS;
-  const int qt = tile / NTILE, kt = tile % NTILE;
-  const int qi = qt * TQ + crow(reg, lane >> 5), kj = kt * TQ + (lane & 31);
-  if (qi >= n || kj >= n) return;
-  float s = 0.f;
-  const bf16* p = ds + (long long)h * PH_ELEMS + el;
+                             int ld, float* __restrict__ tgrad, int win_per_chunk) {
+  const long long e8 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (e8 >= (long long)nH * PH_ELEMS) return;
+  const int h = e8 / PH_ELEMS, el0 = e8 % PH_ELEMS;
+  const int w0 = blockIdx.y * win_per_chunk, w1 = min(n_win, w0 + win_per_chunk);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bf16* p = ds + (long long)h * PH_ELEMS + el0;
   const long long stride = (long long)nH * PH_ELEMS;
-  for (int w = 0; w < n_win; ++w) s += bf2f(p[w * stride]);
-  atomicAdd(tgrad + index[(long long)qi * ld + kj] * nH + h, s);
+  int w = w0;
+  for (; w + 2 <= w1; w += 2) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(p + w * stride);
+    const bf16x8 c = *reinterpret_cast<const bf16x8*>(p + (w + 1) * stride);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] += bf2f(a[i]) + bf2f(c[i]);
+  }
+  if (w < w1) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(p + w * stride);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] += bf2f(a[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int el = el0 + i;
+    const int reg = el & 15, lane = (el >> 4) & 63, tile = el / TILE_ELEMS;
+    const int qt = tile / NTILE, kt = tile % NTILE;
+    const int qi = qt * TQ + crow(reg, lane >> 5), kj = kt * TQ + (lane & 31);
+    if (qi < n && kj < n) atomicAdd(tgrad + index[(long long)qi * ld + kj] * nH + h, s[i]);
+  }
 }
 
 }  // namespace
@@ -425,7 +442,14 @@ extern "C" int lrce_wattn_dbias(const uint16_t* ds_scratch, int n_win, int n, in
                                 float* table_grad, void* stream) {
   if (!ds_scratch || !index || !table_grad) return lrce_fail(LRCE_E_ARG, "wattn_dbias: null pointer");
   const long long total = (long long)nH * PH_ELEMS;
-  dbias_kernel<<<(total + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const bf16*>(ds_scratch), n_win,
-                                                                                   n, nH, index, index_ld, table_grad);
+  // enough (element-group, window-chunk) blocks to fill the chip, >= 8 windows per chunk
+  const long long groups = (total / 8 + 255) / 256;
+  int chunks = (int)((2048 + groups - 1) / groups);
+  chunks = max(1, min(chunks, (n_win + 7) / 8));
+  const int per = (n_win + chunks - 1) / chunks;
+  chunks = (n_win + per - 1) / per;
+  dim3 grid((unsigned)groups, chunks);
+  dbias_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const bf16*>(ds_scratch), n_win, n, nH, index,
+                                                                  index_ld, table_grad, per);
   return lrce_check_launch("wattn_dbias");
 }

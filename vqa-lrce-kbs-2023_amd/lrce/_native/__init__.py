@@ -69,6 +69,7 @@ class MhaDesc(ctypes.Structure):
 
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = 1, 2, 4, 8
 EPI_OUT_F32, EPI_ATOMIC, EPI_ACCUM, EPI_AUX_OUT, EPI_OUT_BOTH = 16, 32, 64, 128, 256
+EPI_BIAS_GRAD = 512
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -98,7 +99,7 @@ _SIGS = {
     "lrce_text_posembed_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_text_posembed_bwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_l2norm_multi": [_P, _P, _I, _P, _I, _P],
-    "lrce_adamw_step": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _F, _P, _P],
+    "lrce_adamw_step": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _F, _P, _P, _P],
     "lrce_set_rng_offset": [_P],
     "lrce_version": [],
     "lrce_last_error": [],

@@ -173,14 +173,17 @@ def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows
     return out
 
 
-def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_scale=1):
-    """dW[N,K] += dY^T X ; dY [M,N] (bf16/f32, rows optionally gathered by a_map), X [M,K] bf16."""
+def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_scale=1, bias_grad=None):
+    """dW[N,K] += dY^T X ; dY [M,N] (bf16/f32, rows optionally gathered by a_map), X [M,K] bf16.
+    bias_grad: also db[N] += colsum(dY) (fused into the skinny f32 path, a column-sum launch otherwise)."""
     M = rows if rows is not None else x.shape[0]
     Nn = dw.shape[0]
     K = dw.shape[1]
     split = _split_for(Nn, K, M)
+    flags = N.EPI_ATOMIC | (N.EPI_BIAS_GRAD if bias_grad is not None else 0)
     gemm(dy, x, dw, Nn, K, M, a_kmajor=False, b_kmajor=False, lda=dy.shape[-1], ldb=x.shape[-1], ldc=K,
-         flags=N.EPI_ATOMIC, a_map=a_map, split_k=split, a_row_scale=a_row_scale, a_rows_per_scale=a_rows_per_scale)
+         flags=flags, bias=bias_grad, a_map=a_map, split_k=split, a_row_scale=a_row_scale,
+         a_rows_per_scale=a_rows_per_scale)
 
 
 def colsum(x, out, *, row_map=None, rows=None, row_scale=None, rows_per_scale=1):
@@ -335,10 +338,11 @@ def l2norm_multi(p, chunk_tensor, n_chunks, sumsq, n_tensors):
 
 
 def adamw_step(p, g, m, v, chunk_tensor, tensor_lr, sumsq, p_bf16, n_chunks, beta1, beta2, eps, wd, grad_scale, reg,
-               bc1, bc2, step=None):
-    """step: optional f32 device scalar holding t (bias corrections computed on device: graph-safe)."""
+               bc1, bc2, step=None, sumsq_next=None):
+    """step: optional f32 device scalar holding t (bias corrections computed on device: graph-safe).
+    sumsq_next: optional zeroed [n_tensors] buffer receiving ||p_t||^2 of the updated parameters."""
     call("lrce_adamw_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(chunk_tensor), ptr(tensor_lr), ptr(sumsq), ptr(p_bf16),
-         n_chunks, beta1, beta2, eps, wd, grad_scale, reg, bc1, bc2, ptr(step), stream_of(p))
+         n_chunks, beta1, beta2, eps, wd, grad_scale, reg, bc1, bc2, ptr(step), ptr(sumsq_next), stream_of(p))
 
 
 _RNG_OFFSETS = {}

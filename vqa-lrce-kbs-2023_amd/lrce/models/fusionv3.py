@@ -40,8 +40,12 @@ def _rows(t, a, b):
 
 
 def _wgrad(flat, w, b, dy, x16, rows=None):
-    """dW (+)= dy^T x16 (rows [a,b) of a stacked weight if given), db (+)= colsum(dy)."""
+    """dW (+)= dy^T x16 (rows [a,b) of a stacked weight if given), db (+)= colsum(dy) — one launch on
+    the skinny exact-f32 path (the bias sum rides along the outer product)."""
     gw = _g(flat, w)
+    gb = _g(flat, b) if b is not None else None
+    if gb is not None and rows is not None:
+        gb = gb[rows[0]:rows[1]]
     if gw is not None:
         if rows is not None:
             gw = gw[rows[0]:rows[1]]
@@ -52,13 +56,10 @@ def _wgrad(flat, w, b, dy, x16, rows=None):
             K.linear_dw(dyp, x16, tmp)
             gw.add_(tmp[:n])
         else:
-            K.linear_dw(dy, x16, gw)
-    if b is not None:
-        gb = _g(flat, b)
-        if gb is not None:
-            if rows is not None:
-                gb = gb[rows[0]:rows[1]]
-            K.colsum(dy, gb)
+            K.linear_dw(dy, x16, gw, bias_grad=gb)
+            gb = None
+    if gb is not None:
+        K.colsum(dy, gb)
 
 
 class MultiheadAttentionParams(nn.Module):

@@ -33,7 +33,9 @@ class FusedAdamW(torch.optim.Optimizer):
         dev = flat.device
         self.exp_avg = torch.zeros_like(flat.f32)
         self.exp_avg_sq = torch.zeros_like(flat.f32)
-        self.sumsq = torch.zeros(len(flat.params), device=dev)
+        self.sumsq = torch.zeros(len(flat.params), device=dev)        # ||p_t||^2 of the current parameters
+        self.sumsq_next = torch.zeros(len(flat.params), device=dev)   # accumulated by the update kernel
+        self._norm_version = None   # flat.f32._version the norms belong to (None: never computed)
         self._index = {id(p): i for i, p in enumerate(flat.params)}
         self.tensor_lr = torch.zeros(len(flat.params), device=dev)
         self._lr_cache = None
@@ -62,15 +64,22 @@ class FusedAdamW(torch.optim.Optimizer):
         self.step_t.add_(1.0)
         b1, b2 = self.defaults["betas"]
         t = self.step_count
-        K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params))
+        if self._norm_version != flat.f32._version:
+            # parameters changed outside the optimizer (init / load): one norm pass; afterwards the
+            # update kernel itself produces the next step's norms
+            K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params))
+        self.sumsq_next.zero_()
         K.adamw_step(flat.f32, flat.grad, self.exp_avg, self.exp_avg_sq, flat.chunk_tensor, self.tensor_lr, self.sumsq,
                      flat.bf16, flat.n_chunks, b1, b2, self.defaults["eps"], self.defaults["weight_decay"],
-                     float(grad_scale), self.reg_strength, 1.0 - b1 ** t, 1.0 - b2 ** t, step=self.step_t)
+                     float(grad_scale), self.reg_strength, 1.0 - b1 ** t, 1.0 - b2 ** t, step=self.step_t,
+                     sumsq_next=self.sumsq_next)
+        self.sumsq.copy_(self.sumsq_next)
+        self._norm_version = flat.f32._version
         flat.mark_bf16_fresh()
         return loss
 
     def l2_term(self):
-        """sum_t ||p_t||_2 of the parameters before the last step (device scalar; no sync)."""
+        """sum_t ||p_t||_2 of the current parameters (device scalar; no sync)."""
         return self.sumsq.sqrt().sum()
 
     def zero_grad(self, set_to_none=False):
