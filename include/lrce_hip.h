@@ -102,12 +102,15 @@ int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_map, int nseg
 
 /* dy row r (read from dy_map[r] if given), x/mean/rstd as in forward.  dx for segment s is written
  * to row in_map[r*nseg+s] of dx (f32): dx = LN_bwd + (dres ? dres[same row] : 0).  dw/db (f32,
- * may be NULL) are accumulated with atomics. */
+ * may be NULL) are accumulated with atomics.  Optional dx_bf16: a bf16 copy of LN row r's dx,
+ * times dx_scale[r / dx_scale_rps] (DropPath of the branch the copy feeds), stored row-major at row
+ * dx_bf16_map[r] (e.g. window order) — the A operand of the following weight/input-gradient GEMMs. */
 int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map,
                        const void* x, int x_f32, const int32_t* in_map, int nseg,
                        const float* mean, const float* rstd, const float* w,
                        float* dx, const float* dres, float* dw, float* db,
-                       int rows, int cols, void* stream);
+                       int rows, int cols, uint16_t* dx_bf16, const int32_t* dx_bf16_map,
+                       const float* dx_scale, int dx_scale_rps, void* stream);
 
 /* ---------------------------------------------------------------- Swin 3D window attention
  * Replaces WindowAttention3D.forward video_swin_ori.py:164-186 (QK^T, relative-position bias,
@@ -192,6 +195,10 @@ int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, in
                 int rows_per_scale, float* out, void* stream);
 /* f32 -> bf16 cast (n elements) */
 int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
+/* y[r][:] = bf16(x[r][:] * row_scale[r / rows_per_scale]) for a (rows x cols) f32 matrix (cols % 4 == 0):
+ * a DropPath-scaled bf16 copy of a residual-stream gradient, the A operand of the branch's GEMMs. */
+int lrce_scale_cast_bf16(const float* x, int64_t rows, int cols, const float* row_scale, int rows_per_scale, uint16_t* y,
+                         void* stream);
 /* Dropout (nn.Dropout / F.dropout semantics, train mode): y = (res ? res : 0) + x * keep / (1-p),
  * keep = hash(seed, i / group) >= p (group > 1 drops whole groups, e.g. per attention head);
  * p = 0 copies.  Optional bf16 copy of y.  In place allowed.  Backward: dx = dy * keep / (1-p)

@@ -192,6 +192,27 @@ def test_layernorm_fwd_bwd(C, nseg, x_f32):
     assert rel(dx, ref_dx) < 1e-4
     assert rel(dw, wr.grad) < 1e-4
     assert rel(db, br.grad) < 1e-4
+    if nseg == 1:
+        # bf16 copy of each LN row's dx, row-scaled (DropPath) and row-permuted (window order)
+        sc = torch.rand(7, device=dev) + 0.5
+        perm = torch.randperm(R, device=dev).int()
+        dx16 = torch.empty(R, C, device=dev, dtype=torch.bfloat16)
+        dx2 = torch.zeros(R, C, device=dev)
+        k.layernorm_bwd(dy, src, mean, rstd, w, dx2, in_map=in_map, dres=None, rows=R, cols=C, dx16=dx16,
+                        dx16_map=perm, dx_scale=sc, dx_scale_rps=50)
+        rows_dx = torch.zeros(R, C, device=dev)
+        rows_dx = xr.grad * sc[torch.arange(R, device=dev) // 50][:, None]
+        ref16 = torch.empty(R, C, device=dev)
+        ref16[perm.long()] = rows_dx
+        assert rel(dx16, ref16) < 1e-2
+
+
+def test_scale_cast_bf16():
+    k = K()
+    x = torch.randn(300, 96, device=dev)
+    sc = torch.rand(3, device=dev)
+    y = k.scale_cast_bf16(x, sc, 100)
+    assert torch.equal(y, bf(x * sc[torch.arange(300, device=dev) // 100][:, None]))
 
 
 def _wattn_reference(qkv, table, index, region, win_pat, nH, n, c):

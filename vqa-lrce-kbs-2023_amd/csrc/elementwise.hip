@@ -101,6 +101,18 @@ __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, l
   }
 }
 
+__global__ void scale_cast_kernel(const float* __restrict__ x, long long n4, int cols, const float* __restrict__ rsc, int rps,
+                                  bf16* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const long long e = i * 4;
+  const float f = rsc ? rsc[(e / cols) / rps] : 1.f;
+  const float4 v = *reinterpret_cast<const float4*>(x + e);
+  bf16x4 o;
+  o[0] = f2bf(v.x * f); o[1] = f2bf(v.y * f); o[2] = f2bf(v.z * f); o[3] = f2bf(v.w * f);
+  *reinterpret_cast<bf16x4*>(y + e) = o;
+}
+
 __global__ void dropout_kernel(const float* __restrict__ x, const float* __restrict__ res, float* __restrict__ y,
                                bf16* __restrict__ yb, long long n, float p, uint64_t seed, long long group,
                                const uint64_t* __restrict__ off) {
@@ -253,6 +265,18 @@ extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int
     else colsum_kernel<bf16, 1><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), row_map, ld, m, n, row_scale, rows_per_scale, out);
   }
   return lrce_check_launch("colsum");
+}
+
+extern "C" int lrce_scale_cast_bf16(const float* x, int64_t rows, int cols, const float* row_scale, int rows_per_scale,
+                                    uint16_t* y, void* stream) {
+  if (!x || !y) return lrce_fail(LRCE_E_ARG, "scale_cast_bf16: null pointer");
+  if (cols % 4) return lrce_fail(LRCE_E_ARG, "scale_cast_bf16: cols %% 4 != 0");
+  if (rows_per_scale < 1) rows_per_scale = 1;
+  const long long n4 = rows * (long long)cols / 4;
+  if (n4 <= 0) return LRCE_OK;
+  scale_cast_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, static_cast<hipStream_t>(stream)>>>(x, n4, cols, row_scale, rows_per_scale,
+                                                                                               reinterpret_cast<bf16*>(y));
+  return lrce_check_launch("scale_cast_bf16");
 }
 
 extern "C" int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream) {

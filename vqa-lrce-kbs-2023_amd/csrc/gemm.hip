@@ -15,6 +15,7 @@
 // so every global access of the epilogue is a 16-B vector (scalar fallback for ragged / unaligned
 // edges).  All operand loads are unconditional (out-of-range lanes read a clamped in-bounds address
 // and are zeroed by a select), which keeps the global loads of a K-tile batched.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -138,6 +139,17 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16* lds, int r0, int ks, int
     return out;
   }
 }
+
+// compile-time loop: f(integral_constant<int, I>) for I = 0..N-1 (keeps accumulator indices static)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_impl(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_impl<I + 1, N>(f);
+  }
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_impl<0, N>(f); }
 
 constexpr int EP = 68;  // padded fp32 row of the epilogue staging tile (conflict-free writes)
 
@@ -348,6 +360,242 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
   half(std::integral_constant<int, 1>{});
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// bf16 x bf16 path with LDS-DMA staging (global_load_lds_dwordx4): operand tiles go HBM/L2 -> LDS
+// without passing through VGPRs, two LDS stages, the next K tile in flight while the current one
+// is consumed (counted vmcnt + raw s_barrier, cdna_hip_programming.md §5 "Pipelining across
+// barriers").  The LDS images are the same swizzled layouts as above; glds writes lane-linearly,
+// so each lane fetches the global chunk that the swizzle places at its linear position.
+// The MFMA operands are swapped (B fragment first) so the accumulator holds C^T blocks: a lane
+// owns 4 consecutive output columns of one row, and the epilogue stores 8/16-B vectors straight
+// from registers (no LDS round trip).  A K tail (< 64) is staged through registers with zeros.
+
+__device__ __forceinline__ void glds16(const void* src, bf16* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (LRCE_LDS void*)lds_dst, 16, 0, 0);
+}
+
+// Per-lane source pointers of the 4 glds instructions a wave issues per operand tile.
+// K-major tile [128 rows][64 k]: instruction i (0..15) covers rows 8i..8i+7 (1 KB).
+// M-major tile [64 k][128 m]: instruction i covers k rows 4i..4i+3 (1 KB).
+template <bool KMAJ>
+struct GldsOperand {
+  const bf16* ptr[4];   // advanced by `step` elements per K tile
+  long long step;
+
+  __device__ __forceinline__ void init(const bf16* base, long long ld, int rows_total, int row0, int k0, const int* map,
+                                       int wave, int lane) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ins = wave + 4 * q;
+      if (KMAJ) {
+        const int r = ins * 8 + (lane >> 3), pos = lane & 7;
+        const int kc = pos ^ ((r >> 1) & 7);
+        int gr = row0 + r;
+        gr = gr < rows_total ? gr : rows_total - 1;    // rows past the edge: any valid row (never stored)
+        const long long rr = map ? (long long)map[gr] : (long long)gr;
+        ptr[q] = base + rr * ld + k0 + kc * 8;
+      } else {
+        const int kr = ins * 4 + (lane >> 4), pos = lane & 15;
+        const int c = pos ^ (mm_swz(kr) >> 1);
+        int gm = row0 + c * 8;
+        gm = gm < rows_total ? gm : 0;
+        ptr[q] = base + (long long)(k0 + kr) * ld + gm;
+      }
+    }
+    step = KMAJ ? BK : (long long)BK * ld;
+  }
+  __device__ __forceinline__ void issue(bf16* tile, int wave) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) glds16(ptr[q], tile + (wave + 4 * q) * 512);
+  }
+  __device__ __forceinline__ void advance() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ptr[q] += step;
+  }
+};
+
+// epilogue for 4 consecutive columns n..n+3 of row m (swapped-operand accumulator layout)
+__device__ __forceinline__ void epilogue4(const GemmP& p, const f32x4& a, int m, int n, int sk, char* cbase) {
+  if (m >= p.m || n >= p.n) return;
+  const int fl = p.flags;
+  const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
+  const bool first = sk == 0;
+  const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
+  float v[4] = {a[0], a[1], a[2], a[3]};
+  if (p.vec && n + 4 <= p.n) {
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if ((fl & LRCE_EPI_BIAS) && first) {
+      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+      bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (v[e] * p.alpha + bias[e]) * ((n + e < p.scale_cols) ? p.scale_val : 1.f);
+    if (fl & LRCE_EPI_GELU) {
+      if (fl & LRCE_EPI_AUX_OUT) {
+        bf16x4 pre;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pre[e] = f2bf(v[e]);
+        *reinterpret_cast<bf16x4*>(p.aux_out + row * p.ld_aux_out + n) = pre;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+    }
+    if (fl & LRCE_EPI_DGELU) {
+      const bf16x4 pre = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(p.aux) + row * p.ld_aux + n);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] *= gelu_grad_f(bf2f(pre[e]));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] *= rs;
+    if ((fl & LRCE_EPI_RESID) && first) {
+      const float4 r0 = *reinterpret_cast<const float4*>(static_cast<const float*>(p.aux) + row * p.ld_aux + n);
+      v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+    }
+    if (fl & (LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) {
+      float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(cbase) + row * p.ldc + n);
+      float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      if (fl & LRCE_EPI_ACCUM) {
+        const float4 c0 = *cp;
+        o.x += c0.x; o.y += c0.y; o.z += c0.z; o.w += c0.w;
+      }
+      *cp = o;
+      if ((fl & LRCE_EPI_OUT_BOTH) && !(fl & LRCE_EPI_ACCUM)) {
+        bf16x4 ob;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ob[e] = f2bf(v[e]);
+        *reinterpret_cast<bf16x4*>(p.aux_out + row * p.ld_aux_out + n) = ob;
+      }
+    } else {
+      bf16x4 ob;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ob[e] = f2bf(v[e]);
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(cbase) + row * p.ldc + n) = ob;
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (n + e >= p.n) break;
+    epilogue1(p, v[e], row, m, n + e, first, rs, cbase);
+  }
+}
+
+template <bool A_KM, bool B_KM>
+__global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[2][2][BM * BK];  // [stage][A/B]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int z = blockIdx.y;
+  const int bz = z / p.split_k, sk = z % p.split_k;
+  const int lin = xcd_remap(blockIdx.x, tiles);
+  const int tn = lin % p.tiles_n, tm = lin / p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const bf16* abase = static_cast<const bf16*>(p.a) + (long long)bz * p.sa;
+  const bf16* bbase = p.b + (long long)bz * p.sb;
+  const int kb = sk * p.k_chunk;
+  const int ke = min(p.k, kb + p.k_chunk);
+  const int nfull = ke > kb ? (ke - kb) / BK : 0;
+  const bool tail = ke > kb + nfull * BK;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const bf16* la, const bf16* lb) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<A_KM>(la, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<B_KM>(lb, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (nfull > 0) {
+    GldsOperand<A_KM> ga;
+    GldsOperand<B_KM> gb;
+    ga.init(abase, p.lda, p.m, m0, kb, p.a_map, wave, lane);
+    gb.init(bbase, p.ldb, p.n, n0, kb, nullptr, wave, lane);
+    ga.issue(lds[0][0], wave);
+    gb.issue(lds[0][1], wave);
+    for (int kt = 0; kt < nfull; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nfull) {
+        ga.advance(); gb.advance();
+        ga.issue(lds[cur ^ 1][0], wave);
+        gb.issue(lds[cur ^ 1][1], wave);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // this wave's tile kt landed, kt+1 in flight
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();                          // ... and every other wave's part of it
+      __builtin_amdgcn_sched_barrier(0);
+      compute(lds[cur][0], lds[cur][1]);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                          // stage `cur` free for tile kt+2
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (tail) {
+    const int k0 = kb + nfull * BK;
+    Stage sa, sb;
+    load_tile<A_KM, false>(sa, abase, p.lda, p.m, ke, m0, k0, p.a_map);
+    load_tile<B_KM, false>(sb, bbase, p.ldb, p.n, ke, n0, k0, nullptr);
+    store_tile<A_KM>(sa, lds[nfull & 1][0]);
+    store_tile<B_KM>(sb, lds[nfull & 1][1]);
+    __syncthreads();
+    compute(lds[nfull & 1][0], lds[nfull & 1][1]);
+    __syncthreads();
+  }
+
+  char* cbase = static_cast<char*>(p.c) +
+                (long long)bz * p.sc * ((p.flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
+  if (p.flags & LRCE_EPI_ATOMIC) {
+    // split-K partials: stage through LDS (free now) so each atomic instruction covers one row's
+    // 64 consecutive columns.  acc[i][j][r] = C[m = i*16 + (lane&15)][n = j*16 + 4*(lane>>4) + r]
+    float* E = reinterpret_cast<float*>(&lds[0][0][0]) + wave * (32 * EP);
+    auto half = [&](auto hc) {
+      constexpr int h = decltype(hc)::value;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            E[(ii * 16 + (lane & 15)) * EP + j * 16 + 4 * (lane >> 4) + r] = acc[2 * h + ii][j][r];
+      wave_lds_fence();
+      const int n = n0 + wn * 64 + lane;
+      if (n < p.n) {
+        for (int rr = 0; rr < 32; ++rr) {
+          const int m = m0 + wm * 64 + h * 32 + rr;
+          if (m >= p.m) break;
+          const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
+          const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
+          epilogue1(p, E[rr * EP + lane], row, m, n, sk == 0, rs, cbase);
+        }
+      }
+      wave_lds_fence();
+    };
+    half(std::integral_constant<int, 0>{});
+    half(std::integral_constant<int, 1>{});
+    return;
+  }
+  static_for<16>([&](auto ij) {
+    constexpr int i = decltype(ij)::value / 4, j = decltype(ij)::value % 4;
+    epilogue4(p, acc[i][j], m0 + wm * 64 + i * 16 + (lane & 15), n0 + wn * 64 + j * 16 + 4 * (lane >> 4), sk, cbase);
+  });
+}
+
 }  // namespace
 
 int lrce_gemm_f32(const LrceGemmDesc* d, void* stream);
@@ -356,6 +604,7 @@ extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int
                            int rows_per_scale, float* out, void* stream);
 
 static int gemm_dispatch(const LrceGemmDesc* d, void* stream);
+static bool g_force_legacy_gemm = getenv("LRCE_LEGACY_GEMM") != nullptr;   // A/B switch for benchmarking
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
 
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
@@ -418,6 +667,19 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   (void)out32;
   dim3 grid(p.tiles_m * p.tiles_n, d->batch * split);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // LDS-DMA path: bf16 operands with 16-B aligned rows; K-major A may carry a row map
+  const bool glds = !d->a_f32 && al16(d->a) && al16(d->b) && (d->stride_a % 8 == 0) && (d->stride_b % 8 == 0) &&
+                    (d->a_kmajor || !d->a_map) && !g_force_legacy_gemm;
+  if (glds) {
+    const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0);
+    switch (gk) {
+      case 3: gemm_glds_kernel<true, true><<<grid, NT, 0, s>>>(p); break;
+      case 2: gemm_glds_kernel<true, false><<<grid, NT, 0, s>>>(p); break;
+      case 1: gemm_glds_kernel<false, true><<<grid, NT, 0, s>>>(p); break;
+      case 0: gemm_glds_kernel<false, false><<<grid, NT, 0, s>>>(p); break;
+    }
+    return lrce_check_launch("gemm(glds)");
+  }
   const int key = (d->a_kmajor ? 4 : 0) | (d->b_kmajor ? 2 : 0) | (d->a_f32 ? 1 : 0);
   switch (key) {
     case 6: gemm_kernel<true, true, false><<<grid, NT, 0, s>>>(p); break;

@@ -41,41 +41,52 @@ __device__ __forceinline__ long long src_off(const int* in_map, int nseg, int se
   return (long long)src * seg + (e - s * seg);
 }
 
-template <typename TX, typename TY>
+// Reductions over the LPR lanes that share one row (LPR = 64: whole wave; 32: half wave).
+template <int LPR>
+__device__ __forceinline__ float row_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// CH float4 chunks per lane, LPR lanes per row (rows of <= 128 columns use half a wave each).
+template <typename TX, typename TY, int CH, int LPR>
 __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, int nseg, const float* w, const float* b,
                                               float eps, TY* y, bf16* y2, const int* out_map, float* mean_o, float* rstd_o,
                                               int rows, int cols) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sl = lane % LPR;
+  const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
   if (r >= rows) return;
   const int nch = cols >> 2, seg = cols / nseg;
-  float4 v[MAXC];
+  float4 v[CH];
   float s = 0.f;
 #pragma unroll
-  for (int t = 0; t < MAXC; ++t) {
-    const int c = lane + 64 * t;
+  for (int t = 0; t < CH; ++t) {
+    const int c = sl + LPR * t;
+    v[t] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c < nch) {
       int ok;
       const long long o = src_off(in_map, nseg, seg, r, c, ok);
-      v[t] = ok ? ld4<TX>(x + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok) v[t] = ld4<TX>(x + o);
       s += v[t].x + v[t].y + v[t].z + v[t].w;
     }
   }
-  const float mean = wave_sum(s) / cols;
+  const float mean = row_sum<LPR>(s) / cols;
   float q = 0.f;
 #pragma unroll
-  for (int t = 0; t < MAXC; ++t) {
-    const int c = lane + 64 * t;
+  for (int t = 0; t < CH; ++t) {
+    const int c = sl + LPR * t;
     if (c < nch) {
       const float a = v[t].x - mean, b2 = v[t].y - mean, c2 = v[t].z - mean, d = v[t].w - mean;
       q += a * a + b2 * b2 + c2 * c2 + d * d;
     }
   }
-  const float rstd = rsqrtf(wave_sum(q) / cols + eps);
+  const float rstd = rsqrtf(row_sum<LPR>(q) / cols + eps);
   const long long orow = out_map ? (long long)out_map[r] : (long long)r;
 #pragma unroll
-  for (int t = 0; t < MAXC; ++t) {
-    const int c = lane + 64 * t;
+  for (int t = 0; t < CH; ++t) {
+    const int c = sl + LPR * t;
     if (c < nch) {
       const float4 ww = *reinterpret_cast<const float4*>(w + 4 * c);
       const float4 bb = *reinterpret_cast<const float4*>(b + 4 * c);
@@ -88,34 +99,40 @@ __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, in
       if (y2) st4<bf16>(y2 + orow * cols + 4 * c, o);
     }
   }
-  if (lane == 0) {
+  if (sl == 0) {
     if (mean_o) mean_o[r] = mean;
     if (rstd_o) rstd_o[r] = rstd;
   }
 }
 
-template <typename TD, typename TX>
+template <typename TD, typename TX, int CH, int LPR>
 __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, const TX* x, const int* in_map, int nseg,
                                               const float* mean_i, const float* rstd_i, const float* w, float* dx,
-                                              const float* dres, float* dw, float* db, int rows, int cols) {
-  __shared__ float red[2][4][1024 + 4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                                              const float* dres, float* dw, float* db, int rows, int cols, bf16* dx16,
+                                              const int* dx16_map, const float* dsc, int dsc_rps) {
+  constexpr int RPW = 64 / LPR;
+  __shared__ float red[2][4][4 * CH * LPR + 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sl = lane % LPR;
   const int nch = cols >> 2, seg = cols / nseg;
-  float4 aw[MAXC], ab[MAXC];  // dw/db partials for up to 8 chunks per lane (cols<=2048)
+  float4 aw[CH], ab[CH];  // dw/db partials of this lane's columns
 #pragma unroll
-  for (int t = 0; t < 8; ++t) { aw[t] = make_float4(0.f, 0.f, 0.f, 0.f); ab[t] = aw[t]; }
-  for (int r = blockIdx.x * 4 + wave; r < rows; r += gridDim.x * 4) {
-    const float mean = mean_i[r], rstd = rstd_i[r];
-    const long long dyr = dy_map ? (long long)dy_map[r] : (long long)r;
-    float4 xh[8], g[8];
+  for (int t = 0; t < CH; ++t) { aw[t] = make_float4(0.f, 0.f, 0.f, 0.f); ab[t] = aw[t]; }
+  for (int r0 = (blockIdx.x * 4 + wave) * RPW; r0 < rows; r0 += gridDim.x * 4 * RPW) {
+    const int r = r0 + lane / LPR;
+    const bool live = r < rows;
+    const float mean = live ? mean_i[r] : 0.f, rstd = live ? rstd_i[r] : 0.f;
+    const long long dyr = !live ? 0 : (dy_map ? (long long)dy_map[r] : (long long)r);
+    float4 xh[CH], g[CH];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int c = lane + 64 * t;
-      if (c < nch) {
+    for (int t = 0; t < CH; ++t) {
+      const int c = sl + LPR * t;
+      xh[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+      g[t] = xh[t];
+      if (live && c < nch) {
         int ok;
         const long long o = src_off(in_map, nseg, seg, r, c, ok);
-        float4 xv = ok ? ld4<TX>(x + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 xv = ok ? ld4<TX>(x + o) : make_float4(0.f, 0.f, 0.f, 0.f);
         xh[t] = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd);
         const float4 d = ld4<TD>(dy + dyr * cols + 4 * c);
         const float4 ww = *reinterpret_cast<const float4*>(w + 4 * c);
@@ -126,11 +143,11 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
         ab[t].x += d.x; ab[t].y += d.y; ab[t].z += d.z; ab[t].w += d.w;
       }
     }
-    const float c1 = wave_sum(s1) / cols, c2 = wave_sum(s2) / cols;
+    const float c1 = row_sum<LPR>(s1) / cols, c2 = row_sum<LPR>(s2) / cols;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int c = lane + 64 * t;
-      if (c < nch) {
+    for (int t = 0; t < CH; ++t) {
+      const int c = sl + LPR * t;
+      if (live && c < nch) {
         int ok;
         const long long o = src_off(in_map, nseg, seg, r, c, ok);
         if (!ok) continue;
@@ -144,29 +161,38 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
           out.x += rr.x; out.y += rr.y; out.z += rr.z; out.w += rr.w;
         }
         *reinterpret_cast<float4*>(dx + o) = out;
+        if (dx16) {   // bf16 copy (optionally row-scaled / row-permuted) for the next GEMMs' A operand
+          const float f = dsc ? dsc[r / dsc_rps] : 1.f;
+          const long long orow = dx16_map ? (long long)dx16_map[r] : (long long)r;
+          st4<bf16>(dx16 + orow * cols + 4 * c, make_float4(out.x * f, out.y * f, out.z * f, out.w * f));
+        }
       }
     }
   }
   if (!dw && !db) return;
-  // reduce the 4 waves' partials through LDS in 1024-column slabs, then one atomic per column
-  for (int base = 0; base < cols; base += 1024) {
+  if (LPR == 32) {  // fold the two half-wave row slots onto lanes 0..31
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int c = lane + 64 * t;
-      const int e = 4 * c - base;
-      if (c < nch && e >= 0 && e < 1024) {
-        red[0][wave][e] = aw[t].x; red[0][wave][e + 1] = aw[t].y; red[0][wave][e + 2] = aw[t].z; red[0][wave][e + 3] = aw[t].w;
-        red[1][wave][e] = ab[t].x; red[1][wave][e + 1] = ab[t].y; red[1][wave][e + 2] = ab[t].z; red[1][wave][e + 3] = ab[t].w;
-      }
+    for (int t = 0; t < CH; ++t) {
+      aw[t].x += __shfl_xor(aw[t].x, 32, 64); aw[t].y += __shfl_xor(aw[t].y, 32, 64);
+      aw[t].z += __shfl_xor(aw[t].z, 32, 64); aw[t].w += __shfl_xor(aw[t].w, 32, 64);
+      ab[t].x += __shfl_xor(ab[t].x, 32, 64); ab[t].y += __shfl_xor(ab[t].y, 32, 64);
+      ab[t].z += __shfl_xor(ab[t].z, 32, 64); ab[t].w += __shfl_xor(ab[t].w, 32, 64);
     }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 1024 && base + e < cols; e += 256) {
-      const float sw = red[0][0][e] + red[0][1][e] + red[0][2][e] + red[0][3][e];
-      const float sb = red[1][0][e] + red[1][1][e] + red[1][2][e] + red[1][3][e];
-      if (dw) atomicAdd(dw + base + e, sw);
-      if (db) atomicAdd(db + base + e, sb);
+  }
+  if (lane < LPR) {
+#pragma unroll
+    for (int t = 0; t < CH; ++t) {
+      const int e = 4 * (sl + LPR * t);
+      red[0][wave][e] = aw[t].x; red[0][wave][e + 1] = aw[t].y; red[0][wave][e + 2] = aw[t].z; red[0][wave][e + 3] = aw[t].w;
+      red[1][wave][e] = ab[t].x; red[1][wave][e + 1] = ab[t].y; red[1][wave][e + 2] = ab[t].z; red[1][wave][e + 3] = ab[t].w;
     }
-    __syncthreads();
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < cols; e += 256) {
+    const float sw = red[0][0][e] + red[0][1][e] + red[0][2][e] + red[0][3][e];
+    const float sb = red[1][0][e] + red[1][1][e] + red[1][2][e] + red[1][3][e];
+    if (dw) atomicAdd(dw + e, sw);
+    if (db) atomicAdd(db + e, sb);
   }
 }
 
@@ -180,33 +206,62 @@ extern "C" int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_ma
   if (cols % 4 || (cols / nseg) % 4 || cols % nseg || cols > 64 * 4 * MAXC)
     return lrce_fail(LRCE_E_ARG, "layernorm_fwd: cols=%d nseg=%d unsupported", cols, nseg);
   if (rows <= 0) return LRCE_OK;
-  dim3 grid((rows + 3) / 4);
   hipStream_t s = static_cast<hipStream_t>(stream);
-#define LNF(TX, TY) ln_fwd<TX, TY><<<grid, 256, 0, s>>>(static_cast<const TX*>(x), in_map, nseg, w, b, eps, static_cast<TY*>(y), reinterpret_cast<bf16*>(y2), out_map, mean, rstd, rows, cols)
-  if (x_f32 && y_f32) LNF(float, float);
-  else if (x_f32) LNF(float, bf16);
-  else if (y_f32) LNF(bf16, float);
-  else LNF(bf16, bf16);
+  const int nch = cols / 4;
+#define LNF3(TX, TY, CH, LPR)                                                                                          \
+  ln_fwd<TX, TY, CH, LPR><<<(rows + 4 * (64 / LPR) - 1) / (4 * (64 / LPR)), 256, 0, s>>>(                              \
+      static_cast<const TX*>(x), in_map, nseg, w, b, eps, static_cast<TY*>(y), reinterpret_cast<bf16*>(y2), out_map, mean, \
+      rstd, rows, cols)
+#define LNF(TX, TY)                                   \
+  if (nch <= 32) LNF3(TX, TY, 1, 32);                 \
+  else if (nch <= 64) LNF3(TX, TY, 1, 64);            \
+  else if (nch <= 128) LNF3(TX, TY, 2, 64);           \
+  else if (nch <= 192) LNF3(TX, TY, 3, 64);           \
+  else if (nch <= 256) LNF3(TX, TY, 4, 64);           \
+  else LNF3(TX, TY, 8, 64);
+  if (x_f32 && y_f32) { LNF(float, float) }
+  else if (x_f32) { LNF(float, bf16) }
+  else if (y_f32) { LNF(bf16, float) }
+  else { LNF(bf16, bf16) }
 #undef LNF
+#undef LNF3
   return lrce_check_launch("layernorm_fwd");
 }
 
 extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map, const void* x, int x_f32,
                                   const int32_t* in_map, int nseg, const float* mean, const float* rstd, const float* w,
-                                  float* dx, const float* dres, float* dw, float* db, int rows, int cols, void* stream) {
+                                  float* dx, const float* dres, float* dw, float* db, int rows, int cols, uint16_t* dx_bf16,
+                                  const int32_t* dx_bf16_map, const float* dx_scale, int dx_scale_rps, void* stream) {
   if (!dy || !x || !mean || !rstd || !w || !dx) return lrce_fail(LRCE_E_ARG, "layernorm_bwd: null pointer");
+  if (dx_scale_rps < 1) dx_scale_rps = 1;
   if (nseg < 1) nseg = 1;
   if (cols % 4 || (cols / nseg) % 4 || cols % nseg || cols > 64 * 4 * MAXC)
     return lrce_fail(LRCE_E_ARG, "layernorm_bwd: cols=%d nseg=%d unsupported", cols, nseg);
   if (rows <= 0) return LRCE_OK;
-  int nblk = (rows + 3) / 4;
-  if (nblk > 1024) nblk = 1024;
   hipStream_t s = static_cast<hipStream_t>(stream);
-#define LNB(TD, TX) ln_bwd<TD, TX><<<nblk, 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, nseg, mean, rstd, w, dx, dres, dw, db, rows, cols)
-  if (dy_f32 && x_f32) LNB(float, float);
-  else if (dy_f32) LNB(float, bf16);
-  else if (x_f32) LNB(bf16, float);
-  else LNB(bf16, bf16);
+  const int nch = cols / 4;
+  // >= 8 rows per wave keeps the per-block dw/db atomics small; <= 2048 blocks
+  auto blocks = [&](int lpr) {
+    const int rpb = 4 * (64 / lpr);
+    int nb = (rows + rpb * 8 - 1) / (rpb * 8);
+    return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+  };
+#define LNB3(TD, TX, CH, LPR)                                                                                          \
+  ln_bwd<TD, TX, CH, LPR><<<blocks(LPR), 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, \
+                                                     nseg, mean, rstd, w, dx, dres, dw, db, rows, cols,      \
+                                                     reinterpret_cast<bf16*>(dx_bf16), dx_bf16_map, dx_scale, dx_scale_rps)
+#define LNB(TD, TX)                                   \
+  if (nch <= 32) LNB3(TD, TX, 1, 32);                 \
+  else if (nch <= 64) LNB3(TD, TX, 1, 64);            \
+  else if (nch <= 128) LNB3(TD, TX, 2, 64);           \
+  else if (nch <= 192) LNB3(TD, TX, 3, 64);           \
+  else if (nch <= 256) LNB3(TD, TX, 4, 64);           \
+  else LNB3(TD, TX, 8, 64);
+  if (dy_f32 && x_f32) { LNB(float, float) }
+  else if (dy_f32) { LNB(float, bf16) }
+  else if (x_f32) { LNB(bf16, float) }
+  else { LNB(bf16, bf16) }
 #undef LNB
+#undef LNB3
   return lrce_check_launch("layernorm_bwd");
 }

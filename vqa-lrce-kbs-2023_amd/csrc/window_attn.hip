@@ -365,43 +365,60 @@ __global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restric
 }
 
 // sum dS over windows (per head, per padded (q,k)) and scatter-add into the bias table gradient
-// Relative-position-bias gradient: sum dS over the windows of a window chunk (grid.y) for 8
-// consecutive per-lane-ordered elements per thread (16-B loads), then scatter-add to the table.
-__global__ void dbias_kernel(const bf16* __restrict__ ds, int n_win, int n, int nH, const int64_t* __restrict__ index,
-                             int ld, float* __restrict__ tgrad, int win_per_chunk) {
+// Relative-position-bias gradient, two passes with no contended atomics:
+//  1. dbias_partial: each thread sums 8 consecutive per-lane-ordered dS elements (16-B loads) over
+//     the windows of one window chunk (grid.y) and stores the 8 partial sums (plain stores);
+//  2. dbias_scatter: one thread per (head, element) sums the chunk partials and adds the result to
+//     its table entry (one atomic per element, as many as the table has uses per window).
+constexpr int DB_CHUNKS = 64;
+
+__global__ void dbias_partial_kernel(const bf16* __restrict__ ds, int n_win, int nH, float* __restrict__ part,
+                                     int win_per_chunk) {
   const long long e8 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (e8 >= (long long)nH * PH_ELEMS) return;
-  const int h = e8 / PH_ELEMS, el0 = e8 % PH_ELEMS;
+  const long long per_chunk = (long long)nH * PH_ELEMS;
+  if (e8 >= per_chunk) return;
   const int w0 = blockIdx.y * win_per_chunk, w1 = min(n_win, w0 + win_per_chunk);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const bf16* p = ds + (long long)h * PH_ELEMS + el0;
-  const long long stride = (long long)nH * PH_ELEMS;
+  const bf16* p = ds + e8;
   int w = w0;
   for (; w + 2 <= w1; w += 2) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(p + w * stride);
-    const bf16x8 c = *reinterpret_cast<const bf16x8*>(p + (w + 1) * stride);
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(p + w * per_chunk);
+    const bf16x8 c = *reinterpret_cast<const bf16x8*>(p + (w + 1) * per_chunk);
 #pragma unroll
     for (int i = 0; i < 8; ++i) s[i] += bf2f(a[i]) + bf2f(c[i]);
   }
   if (w < w1) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(p + w * stride);
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(p + w * per_chunk);
 #pragma unroll
     for (int i = 0; i < 8; ++i) s[i] += bf2f(a[i]);
   }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int el = el0 + i;
-    const int reg = el & 15, lane = (el >> 4) & 63, tile = el / TILE_ELEMS;
-    const int qt = tile / NTILE, kt = tile % NTILE;
-    const int qi = qt * TQ + crow(reg, lane >> 5), kj = kt * TQ + (lane & 31);
-    if (qi < n && kj < n) atomicAdd(tgrad + index[(long long)qi * ld + kj] * nH + h, s[i]);
-  }
+  float4* o = reinterpret_cast<float4*>(part + blockIdx.y * per_chunk + e8);
+  o[0] = make_float4(s[0], s[1], s[2], s[3]);
+  o[1] = make_float4(s[4], s[5], s[6], s[7]);
+}
+
+__global__ void dbias_scatter_kernel(const float* __restrict__ part, int chunks, int n, int nH,
+                                     const int64_t* __restrict__ index, int ld, float* __restrict__ tgrad) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long per_chunk = (long long)nH * PH_ELEMS;
+  if (e >= per_chunk) return;
+  const int h = e / PH_ELEMS, el = e % PH_ELEMS;
+  const int reg = el & 15, lane = (el >> 4) & 63, tile = el / TILE_ELEMS;
+  const int qt = tile / NTILE, kt = tile % NTILE;
+  const int qi = qt * TQ + crow(reg, lane >> 5), kj = kt * TQ + (lane & 31);
+  if (qi >= n || kj >= n) return;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += part[c * per_chunk + e];
+  atomicAdd(tgrad + index[(long long)qi * ld + kj] * nH + h, s);
 }
 
 }  // namespace
 
 extern "C" int64_t lrce_wattn_bias_elems(int n_pat, int nH) { return (int64_t)n_pat * nH * PH_ELEMS; }
-extern "C" int64_t lrce_wattn_ds_elems(int n_win, int nH) { return (int64_t)n_win * nH * PH_ELEMS; }
+// dS scratch (bf16 units): the per-window dS images + the f32 chunk partials of the bias reduction
+extern "C" int64_t lrce_wattn_ds_elems(int n_win, int nH) {
+  return (int64_t)n_win * nH * PH_ELEMS + 2LL * DB_CHUNKS * nH * PH_ELEMS;
+}
 
 extern "C" int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
                                      const int32_t* region, int n_pat, float* bias_fwd, float* bias_bwd, void* stream) {
@@ -441,15 +458,16 @@ extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const ui
 extern "C" int lrce_wattn_dbias(const uint16_t* ds_scratch, int n_win, int n, int nH, const int64_t* index, int index_ld,
                                 float* table_grad, void* stream) {
   if (!ds_scratch || !index || !table_grad) return lrce_fail(LRCE_E_ARG, "wattn_dbias: null pointer");
-  const long long total = (long long)nH * PH_ELEMS;
-  // enough (element-group, window-chunk) blocks to fill the chip, >= 8 windows per chunk
-  const long long groups = (total / 8 + 255) / 256;
-  int chunks = (int)((2048 + groups - 1) / groups);
-  chunks = max(1, min(chunks, (n_win + 7) / 8));
+  const long long per_chunk = (long long)nH * PH_ELEMS;
+  const long long groups = (per_chunk / 8 + 255) / 256;
+  int chunks = (int)((2048 + groups - 1) / groups);   // fill the chip with (group, chunk) blocks
+  chunks = max(1, min(min(chunks, DB_CHUNKS), n_win));
   const int per = (n_win + chunks - 1) / chunks;
   chunks = (n_win + per - 1) / per;
-  dim3 grid((unsigned)groups, chunks);
-  dbias_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const bf16*>(ds_scratch), n_win, n, nH, index,
-                                                                  index_ld, table_grad, per);
+  const bf16* ds = reinterpret_cast<const bf16*>(ds_scratch);
+  float* part = reinterpret_cast<float*>(const_cast<bf16*>(ds) + (long long)n_win * per_chunk);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  dbias_partial_kernel<<<dim3((unsigned)groups, chunks), 256, 0, st>>>(ds, n_win, nH, part, per);
+  dbias_scatter_kernel<<<(unsigned)((per_chunk + 255) / 256), 256, 0, st>>>(part, chunks, n, nH, index, index_ld, table_grad);
   return lrce_check_launch("wattn_dbias");
 }

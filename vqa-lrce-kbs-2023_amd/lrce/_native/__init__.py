@@ -80,7 +80,8 @@ _U64 = ctypes.c_uint64
 _SIGS = {
     "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
     "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _P],
-    "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
+    "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P],
+    "lrce_scale_cast_bf16": [_P, _I64, _I, _P, _I, _P, _P],
     "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _P, _P],
     "lrce_wattn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],

@@ -63,9 +63,11 @@ class StageGeometry:
         self.M = nc * D * H * W
         self.rows_per_clip = D * H * W
         self.win2sp = self._win_map((0, 0, 0), device)
+        self.sp2win = self._inverse(self.win2sp)
         self.shifted = any(s > 0 for s in ss)
         if self.shifted:
             self.win2sp_shift = self._win_map(ss, device)
+            self.sp2win_shift = self._inverse(self.win2sp_shift)
             self.region, self.win_pat, self.n_pat = self._mask_patterns(device)
         self.merge_map = self._merge_map(device) if (H % 2 == 0 and W % 2 == 0) else None
 
@@ -79,6 +81,12 @@ class StageGeometry:
         h = (iwh * wh + th + shift[1]) % H
         w = (iww * ww + tw + shift[2]) % W
         return (((b * D + d) * H + h) * W + w).reshape(-1).to(torch.int32).contiguous()
+
+    @staticmethod
+    def _inverse(perm):
+        inv = torch.empty_like(perm)
+        inv[perm.long()] = torch.arange(perm.numel(), device=perm.device, dtype=perm.dtype)
+        return inv
 
     def _mask_patterns(self, device):
         """Region labels of compute_mask (video_swin_ori.py:346-359) over the rolled volume, as
@@ -270,6 +278,7 @@ class _SwinBlockFn(torch.autograd.Function):
             ctx.save = (x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_b)
             ctx.blk, ctx.geo, ctx.flat, ctx.dp1, ctx.dp2 = blk, geo, flat, dp1, dp2
             ctx.wmap, ctx.win_pat = wmap, win_pat
+            ctx.sp2win = geo.sp2win_shift if shifted else geo.sp2win
         return out
 
     @staticmethod
@@ -280,16 +289,17 @@ class _SwinBlockFn(torch.autograd.Function):
         C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
         rpc = geo.rows_per_clip
         dout = dout.contiguous()
-        # MLP branch: y = x_mid + s2 * fc2(gelu(fc1(LN2(x_mid))))
+        # MLP branch: y = x_mid + s2 * fc2(gelu(fc1(LN2(x_mid)))).  The branch's GEMMs read the
+        # DropPath-scaled gradient as one bf16 copy (the A operand of both dW and dX).
+        dout16 = K.scale_cast_bf16(dout, dp2, rpc)
         gw = _g(flat, blk.mlp.fc2.weight)
         if gw is not None:
-            K.linear_dw(dout, g, gw, a_row_scale=dp2, a_rows_per_scale=rpc)
+            K.linear_dw(dout16, g, gw)
         gb = _g(flat, blk.mlp.fc2.bias)
         if gb is not None:
-            K.colsum(dout, gb, row_scale=dp2, rows_per_scale=rpc)
-        dpre = K.linear_dx(dout, flat.w16(blk.mlp.fc2.weight), out_f32=False, dgelu_pre=pre, a_row_scale=dp2,
-                           a_rows_per_scale=rpc)
-        del g, pre
+            K.colsum(dout16, gb)
+        dpre = K.linear_dx(dout16, flat.w16(blk.mlp.fc2.weight), out_f32=False, dgelu_pre=pre)
+        del g, pre, dout16
         gw = _g(flat, blk.mlp.fc1.weight)
         if gw is not None:
             K.linear_dw(dpre, h2, gw)
@@ -299,18 +309,21 @@ class _SwinBlockFn(torch.autograd.Function):
         dh2 = K.linear_dx(dpre, flat.w16(blk.mlp.fc1.weight))
         del dpre, h2
         dx_mid = torch.empty_like(x_mid)
+        # attention branch input gradient s1 * dx_mid, as bf16 in window order (rows of o / qkv)
+        dmid16 = torch.empty(M, C, dtype=torch.bfloat16, device=dout.device)
         K.layernorm_bwd(dh2, x_mid, m2, r2, blk.norm2.weight, dx_mid, dres=dout,
-                        dw=_g(flat, blk.norm2.weight), db=_g(flat, blk.norm2.bias))
+                        dw=_g(flat, blk.norm2.weight), db=_g(flat, blk.norm2.bias),
+                        dx16=dmid16, dx16_map=ctx.sp2win, dx_scale=dp1, dx_scale_rps=rpc)
         del dh2
         # attention branch: x_mid = x + s1 * unwindow(proj(attn(qkv(LN1(window(x))))))
         gw = _g(flat, at.proj.weight)
         if gw is not None:
-            K.linear_dw(dx_mid, o, gw, a_map=wmap, a_row_scale=dp1, a_rows_per_scale=rpc)
+            K.linear_dw(dmid16, o, gw)
         gb = _g(flat, at.proj.bias)
         if gb is not None:
-            K.colsum(dx_mid, gb, row_scale=dp1, rows_per_scale=rpc)
-        do = K.linear_dx(dx_mid, flat.w16(at.proj.weight), out_f32=False, a_map=wmap, rows=M, a_row_scale=dp1,
-                         a_rows_per_scale=rpc)
+            K.colsum(dmid16, gb)
+        do = K.linear_dx(dmid16, flat.w16(at.proj.weight), out_f32=False)
+        del dmid16
         dqkv = torch.empty_like(qkv)
         ds = torch.empty(K.wattn_ds_elems(geo.n_win, nH), dtype=torch.bfloat16, device=dout.device)
         K.wattn_bwd(qkv, o, do, lse, bias_b, ctx.win_pat, dqkv, ds, geo.n_win, n, nH)
@@ -353,11 +366,11 @@ class _PatchMergeFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, xl, mean, rstd = ctx.save
         pm, geo, flat = ctx.pm, ctx.geo, ctx.flat
-        dy = dy.contiguous()
+        dy16 = K.scale_cast_bf16(dy.contiguous().view(-1, dy.shape[-1]))
         gw = _g(flat, pm.reduction.weight)
         if gw is not None:
-            K.linear_dw(dy, xl, gw)
-        dxl = K.linear_dx(dy, flat.w16(pm.reduction.weight))
+            K.linear_dw(dy16, xl, gw)
+        dxl = K.linear_dx(dy16, flat.w16(pm.reduction.weight))
         dx = torch.empty_like(x)
         K.layernorm_bwd(dxl, x, mean, rstd, pm.norm.weight, dx, in_map=geo.merge_map, nseg=4, rows=geo.M // 4,
                         cols=4 * pm.dim, dw=_g(flat, pm.norm.weight), db=_g(flat, pm.norm.bias))

@@ -206,12 +206,23 @@ def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out
 
 
 def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1, dres=None, dw=None, db=None,
-                  rows=None, cols=None):
+                  rows=None, cols=None, dx16=None, dx16_map=None, dx_scale=None, dx_scale_rps=1):
+    """dx16: optional bf16 copy of dx (times dx_scale[r / dx_scale_rps], at row dx16_map[r])."""
     R = rows if rows is not None else mean.shape[0]
     Cc = cols if cols is not None else w.shape[0]
     call("lrce_layernorm_bwd", ptr(dy), int(dy.dtype == F32), ptr(dy_map), ptr(x), int(x.dtype == F32), ptr(in_map),
-         nseg, ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dres), ptr(dw), ptr(db), R, Cc, stream_of(dx))
+         nseg, ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dres), ptr(dw), ptr(db), R, Cc, ptr(dx16), ptr(dx16_map),
+         ptr(dx_scale), dx_scale_rps, stream_of(dx))
     return dx
+
+
+def scale_cast_bf16(x, row_scale=None, rows_per_scale=1, out=None):
+    """bf16(x[r] * row_scale[r // rows_per_scale]) for a 2-D f32 x."""
+    rows, cols = x.shape[0], x.shape[-1]
+    if out is None:
+        out = torch.empty(rows, cols, dtype=BF16, device=x.device)
+    call("lrce_scale_cast_bf16", ptr(x), rows, cols, ptr(row_scale), rows_per_scale, ptr(out), stream_of(out))
+    return out
 
 
 def wattn_bias_elems(n_pat, nH):

@@ -243,13 +243,19 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             K.colsum(ds, gt.view(E))
         dv = torch.zeros(B * S * 150, E, device=dev)
         dtt = torch.zeros(Bq * Lt, E, device=dev)
+        dk16 = torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev)
+        dt16 = torch.empty(Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev)
         for l, lay in enumerate(layers):
             ca = lay.multihead_attn
-            _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dkvv[l], v16, rows=(E, 3 * E))
-            _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dkvt[l], t16, rows=(E, 3 * E))
+            # the memory-side K/V gradients (accumulated in f32 over steps / answer choices) enter
+            # their big-M GEMMs as bf16, like every other activation gradient
+            K.cast_bf16(dkvv[l], dk16)
+            K.cast_bf16(dkvt[l], dt16)
+            _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16, v16, rows=(E, 3 * E))
+            _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16, t16, rows=(E, 3 * E))
             w = flat.w16(ca.in_proj_weight)[E:]
-            K.linear_dx(dkvv[l], w, out=dv, accumulate=True)
-            K.linear_dx(dkvt[l], w, out=dtt, accumulate=True)
+            K.linear_dx(dk16, w, out=dv, accumulate=True)
+            K.linear_dx(dt16, w, out=dtt, accumulate=True)
         ctx.save = None
         flat.notify(ft.parameters())
         return (dv.view(B, S, 150, E), None, dtt.view(Bq, Lt, E)) + (None,) * (8 + len(ctx.needs_input_grad[11:]))
