@@ -505,6 +505,16 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // bias gradient (dW GEMMs, A = dY^T): the waves of the first column tile also multiply A by a
+  // ones operand, i.e. sum_k A(m, k) falls out of the MFMA pipe (4 extra MFMAs per 16)
+  const bool bias_block = !A_KM && (p.flags & LRCE_EPI_BIAS_GRAD) && tn == 0 && wn == 0;
+  f32x4 accb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = f2bf(1.0f);
+
   auto compute = [&](const bf16* la, const bf16* lb) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -517,6 +527,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      if (bias_block) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
+      }
     }
   };
 
@@ -558,6 +572,14 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     __syncthreads();
   }
 
+  if (bias_block && (lane >> 4) == 0) {   // accb row 0 of each C^T block: sum_k A(m, k), m = lane&15
+    float* db = const_cast<float*>(p.bias);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+      if (m < p.m) __hip_atomic_fetch_add(db + m, p.alpha * accb[i][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   char* cbase = static_cast<char*>(p.c) +
                 (long long)bz * p.sc * ((p.flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
   if (p.flags & LRCE_EPI_ATOMIC) {
@@ -604,6 +626,7 @@ extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int
                            int rows_per_scale, float* out, void* stream);
 
 static int gemm_dispatch(const LrceGemmDesc* d, void* stream);
+static bool glds_ok(const LrceGemmDesc* d);
 static bool g_force_legacy_gemm = getenv("LRCE_LEGACY_GEMM") != nullptr;   // A/B switch for benchmarking
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
 
@@ -613,7 +636,7 @@ extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
   // bias gradient of a weight-gradient GEMM: db[m] += sum_k A(m, k)
   if (d->a_kmajor || !d->bias || d->batch != 1) return lrce_fail(LRCE_E_ARG, "gemm: BIAS_GRAD needs M-major A, bias, batch 1");
   if (d->flags & LRCE_EPI_BIAS) return lrce_fail(LRCE_E_ARG, "gemm: BIAS and BIAS_GRAD are exclusive");
-  const bool fused = lrce_gemm_f32_outer_ok(d);
+  const bool fused = d->b_f32 ? lrce_gemm_f32_outer_ok(d) : glds_ok(d);
   if (fused) return gemm_dispatch(d, stream);   // the skinny outer-product kernel sums A as it goes
   LrceGemmDesc g = *d;
   g.flags &= ~LRCE_EPI_BIAS_GRAD;
@@ -622,6 +645,13 @@ extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
   if (d->alpha != 1.0f) return lrce_fail(LRCE_E_ARG, "gemm: BIAS_GRAD with alpha != 1");
   return lrce_colsum(d->a, d->a_f32, d->a_map, d->lda, d->k, d->m, d->a_row_scale, d->a_rows_per_scale,
                      const_cast<float*>(d->bias), stream);
+}
+
+// LDS-DMA path: bf16 operands with 16-B aligned rows; K-major A may carry a row map
+static bool glds_ok(const LrceGemmDesc* d) {
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  return !d->a_f32 && !d->b_f32 && al16(d->a) && al16(d->b) && (d->stride_a % 8 == 0) && (d->stride_b % 8 == 0) &&
+         (d->lda % 8 == 0) && (d->ldb % 8 == 0) && (d->a_kmajor || !d->a_map) && !g_force_legacy_gemm;
 }
 
 static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
@@ -667,10 +697,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   (void)out32;
   dim3 grid(p.tiles_m * p.tiles_n, d->batch * split);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // LDS-DMA path: bf16 operands with 16-B aligned rows; K-major A may carry a row map
-  const bool glds = !d->a_f32 && al16(d->a) && al16(d->b) && (d->stride_a % 8 == 0) && (d->stride_b % 8 == 0) &&
-                    (d->a_kmajor || !d->a_map) && !g_force_legacy_gemm;
-  if (glds) {
+  if (glds_ok(d)) {
     const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0);
     switch (gk) {
       case 3: gemm_glds_kernel<true, true><<<grid, NT, 0, s>>>(p); break;

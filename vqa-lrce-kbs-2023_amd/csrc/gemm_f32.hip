@@ -183,26 +183,30 @@ __device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, in
 }
 
 // C[m][n] = sum_k A[m][k] * B(k, n); B_KM: B stored [n][k] (forward, W), else [k][n] (dX = dY W).
+// 8 waves split the reduction; each wave issues all loads of a trip of TS k-steps (16 deep) before
+// its MFMAs, so a whole 768-deep reduction is one memory round trip per wave.
+constexpr int SK_WAVES = 8;
+
 template <int MT, bool B_KM>
-__global__ void __launch_bounds__(SK_NT) skinny_kernel(SkinnyP p) {
-  __shared__ float red[4][MT][16][17];
+__global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p) {
+  constexpr int TS = MT <= 2 ? 8 : 4;
+  __shared__ float red[SK_WAVES][MT][16][17];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const int n = n0 + col;
   const bool n_ok = n < p.n;
   const int nc = n_ok ? n : 0;
-  int kchunk = (p.k + 3) / 4;
+  int kchunk = (p.k + SK_WAVES - 1) / SK_WAVES;
   kchunk = (kchunk + 15) & ~15;
   const int kb = wave * kchunk, ke = min(p.k, kb + kchunk);
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k = kb; k < ke; k += 64) {
-    // 4 k-steps of 16 per trip: all loads issued before the MFMAs (memory-level parallelism)
-    float4 bv[4], av[4][MT];
+  for (int k = kb; k < ke; k += 16 * TS) {
+    float4 bv[TS], av[TS][MT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < TS; ++u) {
       const int kk = k + 16 * u + 4 * grp;
       const bool k_ok = kk < ke;           // k % 4 == 0: a float4 is all in or all out
       const int kc = k_ok ? kk : 0;
@@ -222,7 +226,7 @@ __global__ void __launch_bounds__(SK_NT) skinny_kernel(SkinnyP p) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < TS; ++u)
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][t].x, bv[u].x, acc[t], 0, 0, 0);
@@ -236,12 +240,15 @@ __global__ void __launch_bounds__(SK_NT) skinny_kernel(SkinnyP p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][t][grp * 4 + r][col] = acc[t][r];
   __syncthreads();
-  const int ml = threadIdx.x >> 4, nl = threadIdx.x & 15;
+  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, half = threadIdx.x >> 8;
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
+    if ((t & 1) != half) continue;   // threads 0-255 finish even m-tiles, 256-511 odd ones
     const int m = t * 16 + ml, nn = n0 + nl;
     if (m < p.m && nn < p.n) {
-      const float x = red[0][t][ml][nl] + red[1][t][ml][nl] + red[2][t][ml][nl] + red[3][t][ml][nl];
+      float x = 0.f;
+#pragma unroll
+      for (int w = 0; w < SK_WAVES; ++w) x += red[w][t][ml][nl];
       sk_epilogue(p, x, m, nn);
     }
   }
@@ -312,8 +319,8 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
       const int mt = (d->m + 15) / 16;
       dim3 grid((d->n + 15) / 16);
 #define LRCE_SK(MT)                                                                          \
-  if (d->b_kmajor) skinny_kernel<MT, true><<<grid, SK_NT, 0, st>>>(q);                      \
-  else skinny_kernel<MT, false><<<grid, SK_NT, 0, st>>>(q);
+  if (d->b_kmajor) skinny_kernel<MT, true><<<grid, SK_WAVES * 64, 0, st>>>(q);              \
+  else skinny_kernel<MT, false><<<grid, SK_WAVES * 64, 0, st>>>(q);
       switch (mt) {
         case 1: LRCE_SK(1) break;
         case 2: LRCE_SK(2) break;

@@ -174,10 +174,12 @@ __global__ void __launch_bounds__(256) mha_bwd_kernel(MhaP P) {
 }
 
 // ---- single-query path (the recurrent decoder: Lq = 1, fusionv3.py:44-49) --------------------
-// One wave per (batch row, head), 4 per workgroup.  Scores: lane j reads key row j as 8 x 16 B
-// (q broadcast from LDS); softmax by wave reductions; output / dQ: lane = head dim, key rows read
-// coalesced (128 B per row).  dK/dV: one coalesced 64-float atomic row per key (rows are shared by
-// the bdiv answer choices and, for the question segment, by every recurrent step).
+// One workgroup (4 waves) per (batch row, head).  Scores / probabilities: thread t owns key t
+// (reads key row t as 8 x 16 B, q broadcast from LDS); block-wide max / sum through LDS.  Output,
+// dQ, dK, dV: lane = head dim, the 4 waves split the keys, rows read / written coalesced (128 B).
+// dK/dV rows are updated with plain read-modify-writes when this workgroup is their only writer
+// (bdiv == 1: the question segment accumulates over the recurrent steps, which are separate
+// launches), with atomics when bdiv answer choices share a video memory row.
 constexpr int KT = MAXK / 64;
 
 __device__ __forceinline__ float dot_row64(const bf16* row, const float* qs) {
@@ -193,108 +195,123 @@ __device__ __forceinline__ float dot_row64(const bf16* row, const float* qs) {
   return acc;
 }
 
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return r;
+}
+
 __global__ void __launch_bounds__(256) mha1_fwd_kernel(MhaP P) {
   const LrceMhaDesc& d = P.d;
-  __shared__ __attribute__((aligned(16))) float qs[4][D];
-  __shared__ float ps[4][MAXK];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bh = blockIdx.x * 4 + wave;
-  if (bh >= d.B * d.H) return;
-  const int b = bh / d.H, h = bh % d.H;
+  __shared__ __attribute__((aligned(16))) float qs[D];
+  __shared__ float ps[MAXK + 64];
+  __shared__ float part[4][D];
+  __shared__ float red[4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x / d.H, h = blockIdx.x % d.H;
   const int Lk = d.lk1 + d.lk2;
-  qs[wave][lane] = ld_io(d, d.q, (long long)b * d.ld_q + h * D + lane) * d.scale;
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  float sc[KT];
-  bool keep[KT];
-  float m = -1.0e30f;
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    const int j = lane + 64 * t;
-    keep[t] = j < Lk && (!d.key_mask || d.key_mask[(long long)b * Lk + j] != 0);
-    sc[t] = j < Lk ? dot_row64(key_row(d, d.k1, d.k2, b, j, h), qs[wave]) : 0.f;
-    if (keep[t]) m = fmaxf(m, sc[t]);
+  if (t < D) qs[t] = ld_io(d, d.q, (long long)b * d.ld_q + h * D + t) * d.scale;
+  __syncthreads();
+  const bool live = t < Lk;
+  const bool keep = live && (!d.key_mask || d.key_mask[(long long)b * Lk + t] != 0);
+  const float sc = live ? dot_row64(key_row(d, d.k1, d.k2, b, t, h), qs) : 0.f;
+  const float m = block_max(keep ? sc : -1.0e30f, red);
+  const float pe = keep ? __expf(sc - m) : 0.f;
+  const float s = block_sum(pe, red);
+  ps[t] = live ? pe * drop_factor(d, P.off, b, h, 0, t, Lk) : 0.f;
+  __syncthreads();
+  // o[lane] = sum_j ps[j] V[j][lane]; wave w takes keys w, w+4, ...
+  float o0 = 0.f, o1 = 0.f;
+  int j = wave;
+  for (; j + 4 < Lk; j += 8) {
+    o0 += ps[j] * bf2f(key_row(d, d.v1, d.v2, b, j, h)[lane]);
+    o1 += ps[j + 4] * bf2f(key_row(d, d.v1, d.v2, b, j + 4, h)[lane]);
   }
-  m = wave_max(m);
-  float s = 0.f;
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    const int j = lane + 64 * t;
-    const float p = keep[t] ? __expf(sc[t] - m) : 0.f;
-    s += p;
-    if (j < Lk) ps[wave][j] = p * drop_factor(d, P.off, b, h, 0, j, Lk);
+  if (j < Lk) o0 += ps[j] * bf2f(key_row(d, d.v1, d.v2, b, j, h)[lane]);
+  part[wave][lane] = o0 + o1;
+  __syncthreads();
+  if (wave == 0) {
+    const float o = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    const long long oi = (long long)b * d.ld_o + h * D + lane;
+    if (d.f32_io) reinterpret_cast<float*>(d.out)[oi] = o / s;
+    else reinterpret_cast<bf16*>(d.out)[oi] = f2bf(o / s);
+    if (lane == 0) d.lse[(long long)b * d.H + h] = m + __logf(s);
   }
-  s = wave_sum(s);
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-  int j = 0;
-  for (; j + 4 <= Lk; j += 4) {
-    o0 += ps[wave][j] * bf2f(key_row(d, d.v1, d.v2, b, j, h)[lane]);
-    o1 += ps[wave][j + 1] * bf2f(key_row(d, d.v1, d.v2, b, j + 1, h)[lane]);
-    o2 += ps[wave][j + 2] * bf2f(key_row(d, d.v1, d.v2, b, j + 2, h)[lane]);
-    o3 += ps[wave][j + 3] * bf2f(key_row(d, d.v1, d.v2, b, j + 3, h)[lane]);
-  }
-  for (; j < Lk; ++j) o0 += ps[wave][j] * bf2f(key_row(d, d.v1, d.v2, b, j, h)[lane]);
-  const float o = (o0 + o1) + (o2 + o3);
-  const long long oi = (long long)b * d.ld_o + h * D + lane;
-  if (d.f32_io) reinterpret_cast<float*>(d.out)[oi] = o / s;
-  else reinterpret_cast<bf16*>(d.out)[oi] = f2bf(o / s);
-  if (lane == 0) d.lse[(long long)b * d.H + h] = m + __logf(s);
+}
+
+__device__ __forceinline__ void rmw_add(float* p, float v, bool atomic) {
+  if (atomic) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p += v;
 }
 
 __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
   const LrceMhaDesc& d = P.d;
-  __shared__ __attribute__((aligned(16))) float qs[4][D];
-  __shared__ __attribute__((aligned(16))) float gs[4][D];
-  __shared__ float ps[4][MAXK];
-  __shared__ float dss[4][MAXK];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bh = blockIdx.x * 4 + wave;
-  if (bh >= d.B * d.H) return;
-  const int b = bh / d.H, h = bh % d.H;
+  __shared__ __attribute__((aligned(16))) float qs[D];
+  __shared__ __attribute__((aligned(16))) float gs[D];
+  __shared__ float ps[MAXK + 64];
+  __shared__ float dss[MAXK + 64];
+  __shared__ float part[4][D];
+  __shared__ float red[4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x / d.H, h = blockIdx.x % d.H;
   const int Lk = d.lk1 + d.lk2;
-  const float qd = ld_io(d, d.q, (long long)b * d.ld_q + h * D + lane) * d.scale;
-  const float dod = ld_io(d, d.dout, (long long)b * d.ld_o + h * D + lane);
-  const float od = ld_io(d, d.out, (long long)b * d.ld_o + h * D + lane);
-  const float delta = wave_sum(dod * od);
-  const float l = d.lse[(long long)b * d.H + h];
-  qs[wave][lane] = qd;
-  gs[wave][lane] = dod;
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    const int j = lane + 64 * t;
-    if (j < Lk) {
-      const float sc = dot_row64(key_row(d, d.k1, d.k2, b, j, h), qs[wave]);
-      const float dp = dot_row64(key_row(d, d.v1, d.v2, b, j, h), gs[wave]);
-      const bool keep = !d.key_mask || d.key_mask[(long long)b * Lk + j] != 0;
-      const float p = keep ? __expf(sc - l) : 0.f;
-      const float f = drop_factor(d, P.off, b, h, 0, j, Lk);
-      ps[wave][j] = p * f;                  // dV uses the dropped probabilities
-      dss[wave][j] = p * (f * dp - delta);
-    }
+  float dod = 0.f, od = 0.f;
+  if (t < D) {
+    qs[t] = ld_io(d, d.q, (long long)b * d.ld_q + h * D + t) * d.scale;
+    dod = ld_io(d, d.dout, (long long)b * d.ld_o + h * D + t);
+    od = ld_io(d, d.out, (long long)b * d.ld_o + h * D + t);
+    gs[t] = dod;
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  float g = 0.f;
-  for (int j = 0; j < Lk; ++j) {
-    const float ds = dss[wave][j];
-    g += ds * bf2f(key_row(d, d.k1, d.k2, b, j, h)[lane]);
-    float* dk;
-    float* dv;
+  const float delta = block_sum(dod * od, red);   // also orders the qs / gs writes
+  const float l = d.lse[(long long)b * d.H + h];
+  const bool live = t < Lk;
+  float pf = 0.f, ds = 0.f;
+  if (live) {
+    const float sc = dot_row64(key_row(d, d.k1, d.k2, b, t, h), qs);
+    const float dp = dot_row64(key_row(d, d.v1, d.v2, b, t, h), gs);
+    const bool keep = !d.key_mask || d.key_mask[(long long)b * Lk + t] != 0;
+    const float p = keep ? __expf(sc - l) : 0.f;
+    const float f = drop_factor(d, P.off, b, h, 0, t, Lk);
+    pf = p * f;                       // dV uses the dropped probabilities
+    ds = p * (f * dp - delta);
+  }
+  ps[t] = pf;
+  dss[t] = ds;
+  __syncthreads();
+  const float q = qs[lane], g = gs[lane];
+  float dq0 = 0.f, dq1 = 0.f;
+  const bool at1 = d.kv1_bdiv > 1, at2 = d.kv2_bdiv > 1;
+  for (int j = wave; j < Lk; j += 4) {
+    const float dsj = dss[j], pj = ps[j];
+    const bf16* kr = key_row(d, d.k1, d.k2, b, j, h);
+    if (j & 4) dq1 += dsj * bf2f(kr[lane]);
+    else dq0 += dsj * bf2f(kr[lane]);
     if (j < d.lk1) {
       const long long o = (long long)(b / d.kv1_bdiv) * d.stride_dkv1_b + (long long)j * d.ld_dkv1 + h * D + lane;
-      dk = d.dk1 + o; dv = d.dv1 + o;
+      rmw_add(d.dk1 + o, dsj * q, at1);
+      rmw_add(d.dv1 + o, pj * g, at1);
     } else {
       const long long o = (long long)(b / d.kv2_bdiv) * d.stride_dkv2_b + (long long)(j - d.lk1) * d.ld_dkv2 + h * D + lane;
-      dk = d.dk2 + o; dv = d.dv2 + o;
+      rmw_add(d.dk2 + o, dsj * q, at2);
+      rmw_add(d.dv2 + o, pj * g, at2);
     }
-    __hip_atomic_fetch_add(dk, ds * qd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(dv, ps[wave][j] * dod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  d.dq[(long long)b * d.ld_dq + h * D + lane] = g * d.scale;
+  part[wave][lane] = dq0 + dq1;
+  __syncthreads();
+  if (wave == 0)
+    d.dq[(long long)b * d.ld_dq + h * D + lane] =
+        ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane])) * d.scale;
 }
 
 // key/value rows readable as 16-B vectors (single-query path)
@@ -323,7 +340,7 @@ extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, false)) return rc;
   MhaP p{*d, lrce_rng_offset()};
   if (d->Lq == 1 && aligned_rows(d)) {
-    mha1_fwd_kernel<<<(d->B * d->H + 3) / 4, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
+    mha1_fwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
     return lrce_check_launch("mha_fwd");
   }
   mha_fwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
@@ -334,7 +351,7 @@ extern "C" int lrce_mha_bwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, true)) return rc;
   MhaP p{*d, lrce_rng_offset()};
   if (d->Lq == 1 && aligned_rows(d)) {
-    mha1_bwd_kernel<<<(d->B * d->H + 3) / 4, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
+    mha1_bwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
     return lrce_check_launch("mha_bwd");
   }
   mha_bwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);

@@ -244,6 +244,16 @@ def _drop_path_scale(rate, nc, device, training):
     return torch.floor(keep + torch.rand(nc, device=device)) / keep
 
 
+def _wgrad(flat, lin, dy16, x16):
+    """dW += dY^T X and db += colsum(dY) in one GEMM launch (bias sum fused via LRCE_EPI_BIAS_GRAD)."""
+    gw = _g(flat, lin.weight)
+    gb = _g(flat, lin.bias) if lin.bias is not None else None
+    if gw is not None:
+        K.linear_dw(dy16, x16, gw, bias_grad=gb)
+    elif gb is not None:
+        K.colsum(dy16, gb)
+
+
 class _SwinBlockFn(torch.autograd.Function):
     """One SwinTransformerBlock3D (video_swin_ori.py:248-306) forward / backward."""
 
@@ -292,20 +302,10 @@ class _SwinBlockFn(torch.autograd.Function):
         # MLP branch: y = x_mid + s2 * fc2(gelu(fc1(LN2(x_mid)))).  The branch's GEMMs read the
         # DropPath-scaled gradient as one bf16 copy (the A operand of both dW and dX).
         dout16 = K.scale_cast_bf16(dout, dp2, rpc)
-        gw = _g(flat, blk.mlp.fc2.weight)
-        if gw is not None:
-            K.linear_dw(dout16, g, gw)
-        gb = _g(flat, blk.mlp.fc2.bias)
-        if gb is not None:
-            K.colsum(dout16, gb)
+        _wgrad(flat, blk.mlp.fc2, dout16, g)
         dpre = K.linear_dx(dout16, flat.w16(blk.mlp.fc2.weight), out_f32=False, dgelu_pre=pre)
         del g, pre, dout16
-        gw = _g(flat, blk.mlp.fc1.weight)
-        if gw is not None:
-            K.linear_dw(dpre, h2, gw)
-        gb = _g(flat, blk.mlp.fc1.bias)
-        if gb is not None:
-            K.colsum(dpre, gb)
+        _wgrad(flat, blk.mlp.fc1, dpre, h2)
         dh2 = K.linear_dx(dpre, flat.w16(blk.mlp.fc1.weight))
         del dpre, h2
         dx_mid = torch.empty_like(x_mid)
@@ -316,12 +316,7 @@ class _SwinBlockFn(torch.autograd.Function):
                         dx16=dmid16, dx16_map=ctx.sp2win, dx_scale=dp1, dx_scale_rps=rpc)
         del dh2
         # attention branch: x_mid = x + s1 * unwindow(proj(attn(qkv(LN1(window(x))))))
-        gw = _g(flat, at.proj.weight)
-        if gw is not None:
-            K.linear_dw(dmid16, o, gw)
-        gb = _g(flat, at.proj.bias)
-        if gb is not None:
-            K.colsum(dmid16, gb)
+        _wgrad(flat, at.proj, dmid16, o)
         do = K.linear_dx(dmid16, flat.w16(at.proj.weight), out_f32=False)
         del dmid16
         dqkv = torch.empty_like(qkv)
@@ -332,12 +327,7 @@ class _SwinBlockFn(torch.autograd.Function):
         if gt is not None:
             K.wattn_dbias(ds, geo.n_win, n, nH, at.relative_position_index, gt)
         del ds
-        gw = _g(flat, at.qkv.weight)
-        if gw is not None:
-            K.linear_dw(dqkv, xw, gw)
-        gb = _g(flat, at.qkv.bias)
-        if gb is not None:
-            K.colsum(dqkv, gb)
+        _wgrad(flat, at.qkv, dqkv, xw)
         dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight))
         del dqkv, qkv, xw
         dx = torch.empty_like(x)
