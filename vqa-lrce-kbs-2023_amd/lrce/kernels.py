@@ -22,11 +22,12 @@ class KernelTimer:
     `with KernelTimer("wattn_fwd") as kt: ...` then kt.mean_ms(), kt.calls, kt.flops."""
     active = None
 
-    def __init__(self, *names):
+    def __init__(self, *names, detail=False):
         self.names = set(names)
         self.events = {n: [] for n in names}
         self.flops = {n: 0.0 for n in names}
         self.bytes = {n: 0.0 for n in names}
+        self.detail = {} if detail else None   # (name, key) -> [events], flops per launch
 
     def __enter__(self):
         KernelTimer.active = self
@@ -35,7 +36,7 @@ class KernelTimer:
     def __exit__(self, *a):
         KernelTimer.active = None
 
-    def wrap(self, name, stream_tensor, fn, flops=0.0, nbytes=0.0):
+    def wrap(self, name, stream_tensor, fn, flops=0.0, nbytes=0.0, key=None):
         if name not in self.names:
             return fn()
         s = torch.cuda.current_stream(stream_tensor.device)
@@ -44,6 +45,10 @@ class KernelTimer:
         r = fn()
         e1.record(s)
         self.events[name].append((e0, e1))
+        if self.detail is not None:
+            ent = self.detail.setdefault((name, key), [[], 0.0])
+            ent[0].append((e0, e1))
+            ent[1] += flops
         self.flops[name] += flops
         self.bytes[name] += nbytes
         return r
@@ -65,12 +70,21 @@ class KernelTimer:
             return n, None, None, None
         return n, t / n, self.flops[name] / t / 1e9, self.bytes[name] / t / 1e6
 
+    def breakdown(self):
+        """[(name, key, calls, total ms, TFLOP/s)] per launch shape, largest total first (detail=True)."""
+        torch.cuda.synchronize()
+        rows = []
+        for (name, key), (evs, fl) in (self.detail or {}).items():
+            t = sum(a.elapsed_time(b) for a, b in evs)
+            rows.append((name, key, len(evs), t, fl / max(t, 1e-9) / 1e9))
+        return sorted(rows, key=lambda r: -r[3])
 
-def _timed(name, stream_tensor, fn, flops=0.0, nbytes=0.0):
+
+def _timed(name, stream_tensor, fn, flops=0.0, nbytes=0.0, key=None):
     kt = KernelTimer.active
     if kt is None:
         return fn()
-    return kt.wrap(name, stream_tensor, fn, flops, nbytes)
+    return kt.wrap(name, stream_tensor, fn, flops, nbytes, key)
 
 
 def _chk(t, dtype=None, name="tensor"):
@@ -113,7 +127,9 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.a_row_scale, d.a_rows_per_scale = ptr(a_row_scale), a_rows_per_scale
     d.b_f32 = int(b_f32)
     _timed("gemm_f32" if b_f32 else "gemm", c, lambda: call("lrce_gemm", ctypes.byref(d), stream_of(c)),
-           flops=2.0 * m * n * k * batch)
+           flops=2.0 * m * n * k * batch,
+           key=(m, n, k, batch, "AK" if a_kmajor else "AM", "BK" if b_kmajor else "BN", "a32" if a_f32 else "a16",
+                split_k, flags))
 
 
 def _split_for(m_out, n_out, k_red):
