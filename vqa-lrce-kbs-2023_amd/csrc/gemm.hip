@@ -415,72 +415,6 @@ struct GldsOperand {
   }
 };
 
-// epilogue for 4 consecutive columns n..n+3 of row m (swapped-operand accumulator layout)
-__device__ __forceinline__ void epilogue4(const GemmP& p, const f32x4& a, int m, int n, int sk, char* cbase) {
-  if (m >= p.m || n >= p.n) return;
-  const int fl = p.flags;
-  const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
-  const bool first = sk == 0;
-  const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
-  float v[4] = {a[0], a[1], a[2], a[3]};
-  if (p.vec && n + 4 <= p.n) {
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if ((fl & LRCE_EPI_BIAS) && first) {
-      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
-      bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (v[e] * p.alpha + bias[e]) * ((n + e < p.scale_cols) ? p.scale_val : 1.f);
-    if (fl & LRCE_EPI_GELU) {
-      if (fl & LRCE_EPI_AUX_OUT) {
-        bf16x4 pre;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) pre[e] = f2bf(v[e]);
-        *reinterpret_cast<bf16x4*>(p.aux_out + row * p.ld_aux_out + n) = pre;
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
-    }
-    if (fl & LRCE_EPI_DGELU) {
-      const bf16x4 pre = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(p.aux) + row * p.ld_aux + n);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] *= gelu_grad_f(bf2f(pre[e]));
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] *= rs;
-    if ((fl & LRCE_EPI_RESID) && first) {
-      const float4 r0 = *reinterpret_cast<const float4*>(static_cast<const float*>(p.aux) + row * p.ld_aux + n);
-      v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
-    }
-    if (fl & (LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) {
-      float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(cbase) + row * p.ldc + n);
-      float4 o = make_float4(v[0], v[1], v[2], v[3]);
-      if (fl & LRCE_EPI_ACCUM) {
-        const float4 c0 = *cp;
-        o.x += c0.x; o.y += c0.y; o.z += c0.z; o.w += c0.w;
-      }
-      *cp = o;
-      if ((fl & LRCE_EPI_OUT_BOTH) && !(fl & LRCE_EPI_ACCUM)) {
-        bf16x4 ob;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) ob[e] = f2bf(v[e]);
-        *reinterpret_cast<bf16x4*>(p.aux_out + row * p.ld_aux_out + n) = ob;
-      }
-    } else {
-      bf16x4 ob;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ob[e] = f2bf(v[e]);
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(cbase) + row * p.ldc + n) = ob;
-    }
-    return;
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (n + e >= p.n) break;
-    epilogue1(p, v[e], row, m, n + e, first, rs, cbase);
-  }
-}
-
 template <bool A_KM, bool B_KM>
 __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2][2][BM * BK];  // [stage][A/B]
@@ -612,9 +546,42 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     half(std::integral_constant<int, 1>{});
     return;
   }
-  static_for<16>([&](auto ij) {
-    constexpr int i = decltype(ij)::value / 4, j = decltype(ij)::value % 4;
-    epilogue4(p, acc[i][j], m0 + wm * 64 + i * 16 + (lane & 15), n0 + wn * 64 + j * 16 + 4 * (lane >> 4), sk, cbase);
+  // Transpose the 4x4 (lane group g, block j) arrangement of 4-column pieces across the four
+  // 16-lane groups with permlane32/16 swaps (cdna_hip_programming.md T21): before, lane (g, rho)
+  // holds columns 16j + 4g + r of row rho; after, columns 16g + 4j + r, i.e. 16 contiguous columns,
+  // so the epilogue reads/writes 16-B vectors (bias, residual, GELU pre-activation, output).
+  const int ncol = n0 + wn * 64 + 16 * (lane >> 4);
+  static_for<4>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    uint32_t u[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) u[j][r] = __float_as_uint(acc[i][j][r]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto s32 = __builtin_amdgcn_permlane32_swap(u[j][r], u[j + 2][r], false, false);
+        u[j][r] = s32[0];
+        u[j + 2][r] = s32[1];
+      }
+#pragma unroll
+    for (int j = 0; j < 4; j += 2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto s16 = __builtin_amdgcn_permlane16_swap(u[j][r], u[j + 1][r], false, false);
+        u[j][r] = s16[0];
+        u[j + 1][r] = s16[1];
+      }
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(u[2 * h + (e >> 2)][e & 3]);
+      epilogue8(p, v, m, ncol + 8 * h, sk, cbase);
+    }
   });
 }
 
