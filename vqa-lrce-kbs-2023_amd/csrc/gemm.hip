@@ -365,28 +365,90 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
 // bf16 x bf16 path with LDS-DMA staging (global_load_lds_dwordx4): operand tiles go HBM/L2 -> LDS
 // without passing through VGPRs, two LDS stages, the next K tile in flight while the current one
 // is consumed (counted vmcnt + raw s_barrier, cdna_hip_programming.md §5 "Pipelining across
-// barriers").  The LDS images are the same swizzled layouts as above; glds writes lane-linearly,
-// so each lane fetches the global chunk that the swizzle places at its linear position.
-// The MFMA operands are swapped (B fragment first) so the accumulator holds C^T blocks: a lane
-// owns 4 consecutive output columns of one row, and the epilogue stores 8/16-B vectors straight
-// from registers (no LDS round trip).  A K tail (< 64) is staged through registers with zeros.
+// barriers").  The LDS images are swizzled as above; glds writes lane-linearly, so each lane fetches
+// the global chunk that the swizzle places at its linear position.
+// Tile TBM x TBN (128x128 for large problems, 64x64 when the 128-tile grid would not fill the chip),
+// 4 waves as 2x2, each (TBM/2)x(TBN/2).  The MFMA operands are swapped (B fragment first) so the
+// accumulator holds C^T blocks; a permlane transpose then gives each lane 8 or 16 contiguous output
+// columns of one row for 16-B vector epilogues.  A K tail (< 64) is staged through registers.
+
+// M-major LDS image [64 k][R] bf16 (R = 128 or 64 elements per k row), 8-B units XOR-swizzled by an
+// even (16-B-chunk granular, for the DMA) function of k.
+template <int R>
+__device__ __forceinline__ int mm_swz_r(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << (R == 128 ? 2 : 1); }
+template <int R>
+__device__ __forceinline__ int mm_off_r(int k, int unit) { return k * R + ((unit ^ mm_swz_r<R>(k)) << 2); }
+
+template <bool KMAJ, int R>
+__device__ __forceinline__ bf16x8 read_frag_r(const bf16* lds, int r0, int ks, int lane) {
+  if (KMAJ) {
+    const int row = r0 + (lane & 15);
+    const int kc = ks * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(lds + km_off(row, kc));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+    const int unit = (r0 >> 2) + pp;
+    bf16x8 out;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = ks * 32 + 8 * g + 4 * h + q;
+      const LRCE_LDS s16x4* src = (const LRCE_LDS s16x4*)(lds + mm_off_r<R>(k, unit));
+      s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<LRCE_LDS s16x4*>(src));
+      bf16x4 bv = *reinterpret_cast<bf16x4*>(&v);
+      out[4 * h + 0] = bv[0]; out[4 * h + 1] = bv[1]; out[4 * h + 2] = bv[2]; out[4 * h + 3] = bv[3];
+    }
+    return out;
+  }
+}
+
+// register-staged load of an R x 64 operand tile (the K tail), zero outside [rows_total) x [kdim)
+template <bool KMAJ, int R>
+__device__ __forceinline__ void tail_tile(bf16* lds, const bf16* base, long long ld, int rows_total, int kdim, int row0,
+                                          int k0, const int* map) {
+  constexpr int NI = R / 32;  // 16-B pieces per thread
+  uint4 v[NI];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int c = tid + NT * i;
+    int r, kk;
+    if (KMAJ) { r = c >> 3; kk = (c & 7) << 3; }
+    else { kk = c / (R / 8); r = (c % (R / 8)) << 3; }
+    const int gr = row0 + r, gk = k0 + kk;
+    const bool ok = gr < rows_total && gk < kdim;
+    const int grc = ok ? gr : 0, gkc = ok ? gk : 0;
+    long long off;
+    if (KMAJ) off = (map ? (long long)map[grc] : (long long)grc) * ld + gkc;
+    else off = (long long)gkc * ld + grc;
+    uint4 val = *reinterpret_cast<const uint4*>(base + off);
+    if (!ok) val = make_uint4(0, 0, 0, 0);
+    v[i] = val;
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int c = tid + NT * i;
+    const int off = KMAJ ? km_off(c >> 3, c & 7) : mm_off_r<R>(c / (R / 8), (c % (R / 8)) << 1);
+    *reinterpret_cast<uint4*>(lds + off) = v[i];
+  }
+}
 
 __device__ __forceinline__ void glds16(const void* src, bf16* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (LRCE_LDS void*)lds_dst, 16, 0, 0);
 }
 
-// Per-lane source pointers of the 4 glds instructions a wave issues per operand tile.
-// K-major tile [128 rows][64 k]: instruction i (0..15) covers rows 8i..8i+7 (1 KB).
-// M-major tile [64 k][128 m]: instruction i covers k rows 4i..4i+3 (1 KB).
-template <bool KMAJ>
+// Per-lane source pointers of the R/32 glds instructions a wave issues per operand tile (1 KB each).
+// K-major tile [R rows][64 k]: instruction i covers rows 8i..8i+7.
+// M-major tile [64 k][R]: instruction i covers the 1024 / 2R k rows starting at i * 1024 / 2R.
+template <bool KMAJ, int R>
 struct GldsOperand {
-  const bf16* ptr[4];   // advanced by `step` elements per K tile
+  static constexpr int NI = R / 32;
+  const bf16* ptr[NI];   // advanced by `step` elements per K tile
   long long step;
 
   __device__ __forceinline__ void init(const bf16* base, long long ld, int rows_total, int row0, int k0, const int* map,
                                        int wave, int lane) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NI; ++q) {
       const int ins = wave + 4 * q;
       if (KMAJ) {
         const int r = ins * 8 + (lane >> 3), pos = lane & 7;
@@ -396,8 +458,9 @@ struct GldsOperand {
         const long long rr = map ? (long long)map[gr] : (long long)gr;
         ptr[q] = base + rr * ld + k0 + kc * 8;
       } else {
-        const int kr = ins * 4 + (lane >> 4), pos = lane & 15;
-        const int c = pos ^ (mm_swz(kr) >> 1);
+        constexpr int CPR = R / 8;                      // 16-B chunks per k row
+        const int kr = ins * (64 / CPR) + lane / CPR, pos = lane % CPR;
+        const int c = pos ^ (mm_swz_r<R>(kr) >> 1);
         int gm = row0 + c * 8;
         gm = gm < rows_total ? gm : 0;
         ptr[q] = base + (long long)(k0 + kr) * ld + gm;
@@ -407,17 +470,20 @@ struct GldsOperand {
   }
   __device__ __forceinline__ void issue(bf16* tile, int wave) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) glds16(ptr[q], tile + (wave + 4 * q) * 512);
+    for (int q = 0; q < NI; ++q) glds16(ptr[q], tile + (wave + 4 * q) * 512);
   }
   __device__ __forceinline__ void advance() {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ptr[q] += step;
+    for (int q = 0; q < NI; ++q) ptr[q] += step;
   }
 };
 
-template <bool A_KM, bool B_KM>
+template <int TBM, int TBN, bool A_KM, bool B_KM>
 __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[2][2][BM * BK];  // [stage][A/B]
+  constexpr int WM = TBM / 2, WN = TBN / 2;      // per-wave tile
+  constexpr int IM = WM / 16, JN = WN / 16;      // 16x16 accumulator blocks per wave
+  constexpr int A_EL = TBM * BK, B_EL = TBN * BK;
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * (A_EL + B_EL)];  // [stage][A | B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles = p.tiles_m * p.tiles_n;
@@ -425,26 +491,29 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   const int bz = z / p.split_k, sk = z % p.split_k;
   const int lin = xcd_remap(blockIdx.x, tiles);
   const int tn = lin % p.tiles_n, tm = lin / p.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * TBM, n0 = tn * TBN;
   const bf16* abase = static_cast<const bf16*>(p.a) + (long long)bz * p.sa;
   const bf16* bbase = p.b + (long long)bz * p.sb;
   const int kb = sk * p.k_chunk;
   const int ke = min(p.k, kb + p.k_chunk);
   const int nfull = ke > kb ? (ke - kb) / BK : 0;
   const bool tail = ke > kb + nfull * BK;
+  bf16* const sa0 = lds;
+  bf16* const sb0 = lds + A_EL;
+  constexpr int STG = A_EL + B_EL;
 
-  f32x4 acc[4][4];
+  f32x4 acc[IM][JN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < IM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // bias gradient (dW GEMMs, A = dY^T): the waves of the first column tile also multiply A by a
-  // ones operand, i.e. sum_k A(m, k) falls out of the MFMA pipe (4 extra MFMAs per 16)
+  // ones operand, i.e. sum_k A(m, k) falls out of the MFMA pipe (IM extra MFMAs per IM*JN)
   const bool bias_block = !A_KM && (p.flags & LRCE_EPI_BIAS_GRAD) && tn == 0 && wn == 0;
-  f32x4 accb[4];
+  f32x4 accb[IM];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < IM; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = f2bf(1.0f);
@@ -452,42 +521,45 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   auto compute = [&](const bf16* la, const bf16* lb) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[IM], bfr[JN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag<A_KM>(la, wm * 64 + i * 16, ks, lane);
+      for (int i = 0; i < IM; ++i) af[i] = read_frag_r<A_KM, TBM>(la, wm * WM + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<B_KM>(lb, wn * 64 + j * 16, ks, lane);
+      for (int j = 0; j < JN; ++j) bfr[j] = read_frag_r<B_KM, TBN>(lb, wn * WN + j * 16, ks, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < IM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       if (bias_block) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
+        for (int i = 0; i < IM; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
       }
     }
   };
 
   if (nfull > 0) {
-    GldsOperand<A_KM> ga;
-    GldsOperand<B_KM> gb;
+    constexpr int INFLIGHT = (TBM + TBN) / 32;   // glds per wave per K tile
+    GldsOperand<A_KM, TBM> ga;
+    GldsOperand<B_KM, TBN> gb;
     ga.init(abase, p.lda, p.m, m0, kb, p.a_map, wave, lane);
     gb.init(bbase, p.ldb, p.n, n0, kb, nullptr, wave, lane);
-    ga.issue(lds[0][0], wave);
-    gb.issue(lds[0][1], wave);
+    ga.issue(sa0, wave);
+    gb.issue(sb0, wave);
     for (int kt = 0; kt < nfull; ++kt) {
       const int cur = kt & 1;
       if (kt + 1 < nfull) {
         ga.advance(); gb.advance();
-        ga.issue(lds[cur ^ 1][0], wave);
-        gb.issue(lds[cur ^ 1][1], wave);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // this wave's tile kt landed, kt+1 in flight
+        ga.issue(sa0 + (cur ^ 1) * STG, wave);
+        gb.issue(sb0 + (cur ^ 1) * STG, wave);
+        // this wave's tile kt landed, kt+1 in flight
+        if constexpr (INFLIGHT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_s_barrier();                          // ... and every other wave's part of it
       __builtin_amdgcn_sched_barrier(0);
-      compute(lds[cur][0], lds[cur][1]);
+      compute(sa0 + cur * STG, sb0 + cur * STG);
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();                          // stage `cur` free for tile kt+2
@@ -496,87 +568,96 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   }
   if (tail) {
     const int k0 = kb + nfull * BK;
-    Stage sa, sb;
-    load_tile<A_KM, false>(sa, abase, p.lda, p.m, ke, m0, k0, p.a_map);
-    load_tile<B_KM, false>(sb, bbase, p.ldb, p.n, ke, n0, k0, nullptr);
-    store_tile<A_KM>(sa, lds[nfull & 1][0]);
-    store_tile<B_KM>(sb, lds[nfull & 1][1]);
+    const int st = nfull & 1;
+    tail_tile<A_KM, TBM>(sa0 + st * STG, abase, p.lda, p.m, ke, m0, k0, p.a_map);
+    tail_tile<B_KM, TBN>(sb0 + st * STG, bbase, p.ldb, p.n, ke, n0, k0, nullptr);
     __syncthreads();
-    compute(lds[nfull & 1][0], lds[nfull & 1][1]);
+    compute(sa0 + st * STG, sb0 + st * STG);
     __syncthreads();
   }
 
   if (bias_block && (lane >> 4) == 0) {   // accb row 0 of each C^T block: sum_k A(m, k), m = lane&15
     float* db = const_cast<float*>(p.bias);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    for (int i = 0; i < IM; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
       if (m < p.m) __hip_atomic_fetch_add(db + m, p.alpha * accb[i][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   char* cbase = static_cast<char*>(p.c) +
                 (long long)bz * p.sc * ((p.flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
   if (p.flags & LRCE_EPI_ATOMIC) {
-    // split-K partials: stage through LDS (free now) so each atomic instruction covers one row's
-    // 64 consecutive columns.  acc[i][j][r] = C[m = i*16 + (lane&15)][n = j*16 + 4*(lane>>4) + r]
-    float* E = reinterpret_cast<float*>(&lds[0][0][0]) + wave * (32 * EP);
-    auto half = [&](auto hc) {
+    // split-K partials: stage 32-row slabs through LDS (free now) so each atomic instruction covers
+    // consecutive columns of a row.  acc[i][j][r] = C[m = i*16 + (lane&15)][n = j*16 + 4*(lane>>4) + r]
+    constexpr int EPW = WN + 4;
+    float* E = reinterpret_cast<float*>(lds) + wave * (32 * EPW);
+    static_for<IM / 2>([&](auto hc) {
       constexpr int h = decltype(hc)::value;
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < JN; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            E[(ii * 16 + (lane & 15)) * EP + j * 16 + 4 * (lane >> 4) + r] = acc[2 * h + ii][j][r];
+            E[(ii * 16 + (lane & 15)) * EPW + j * 16 + 4 * (lane >> 4) + r] = acc[2 * h + ii][j][r];
       wave_lds_fence();
-      const int n = n0 + wn * 64 + lane;
+      const int col = lane % WN;
+      const int n = n0 + wn * WN + col;
       if (n < p.n) {
-        for (int rr = 0; rr < 32; ++rr) {
-          const int m = m0 + wm * 64 + h * 32 + rr;
+        for (int rr = lane / WN; rr < 32; rr += 64 / WN) {
+          const int m = m0 + wm * WM + h * 32 + rr;
           if (m >= p.m) break;
           const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
           const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
-          epilogue1(p, E[rr * EP + lane], row, m, n, sk == 0, rs, cbase);
+          epilogue1(p, E[rr * EPW + col], row, m, n, sk == 0, rs, cbase);
         }
       }
       wave_lds_fence();
-    };
-    half(std::integral_constant<int, 0>{});
-    half(std::integral_constant<int, 1>{});
+    });
     return;
   }
-  // Transpose the 4x4 (lane group g, block j) arrangement of 4-column pieces across the four
-  // 16-lane groups with permlane32/16 swaps (cdna_hip_programming.md T21): before, lane (g, rho)
-  // holds columns 16j + 4g + r of row rho; after, columns 16g + 4j + r, i.e. 16 contiguous columns,
-  // so the epilogue reads/writes 16-B vectors (bias, residual, GELU pre-activation, output).
-  const int ncol = n0 + wn * 64 + 16 * (lane >> 4);
-  static_for<4>([&](auto ic) {
+  // Transpose the (lane group g, block j) arrangement of 4-column pieces across the four 16-lane
+  // groups with permlane32/16 swaps (cdna_hip_programming.md T21).  JN = 4: lane (g, rho) holds
+  // columns 16j + 4g + r of row rho before and 16g + 4j + r after (16 contiguous columns);
+  // JN = 2: columns 16j + 4g + r before, 8g + 4j + r after (8 contiguous).  The epilogue then
+  // reads/writes 16-B vectors (bias, residual, GELU pre-activation, output).
+  static_for<IM>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
-    uint32_t u[4][4];
+    uint32_t u[JN][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < JN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) u[j][r] = __float_as_uint(acc[i][j][r]);
+    if constexpr (JN == 4) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const auto s32 = __builtin_amdgcn_permlane32_swap(u[j][r], u[j + 2][r], false, false);
+          u[j][r] = s32[0];
+          u[j + 2][r] = s32[1];
+        }
+#pragma unroll
+      for (int j = 0; j < 4; j += 2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const auto s16 = __builtin_amdgcn_permlane16_swap(u[j][r], u[j + 1][r], false, false);
+          u[j][r] = s16[0];
+          u[j + 1][r] = s16[1];
+        }
+    } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const auto s32 = __builtin_amdgcn_permlane32_swap(u[j][r], u[j + 2][r], false, false);
-        u[j][r] = s32[0];
-        u[j + 2][r] = s32[1];
+        const auto s32 = __builtin_amdgcn_permlane32_swap(u[0][r], u[1][r], false, false);
+        const auto s16 = __builtin_amdgcn_permlane16_swap(s32[0], s32[1], false, false);
+        u[0][r] = s16[0];
+        u[1][r] = s16[1];
       }
+    }
+    const int m = m0 + wm * WM + i * 16 + (lane & 15);
+    const int ncol = n0 + wn * WN + (JN * 4) * (lane >> 4);
 #pragma unroll
-    for (int j = 0; j < 4; j += 2)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const auto s16 = __builtin_amdgcn_permlane16_swap(u[j][r], u[j + 1][r], false, false);
-        u[j][r] = s16[0];
-        u[j + 1][r] = s16[1];
-      }
-    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < JN / 2; ++h) {
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(u[2 * h + (e >> 2)][e & 3]);
@@ -595,6 +676,7 @@ extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int
 static int gemm_dispatch(const LrceGemmDesc* d, void* stream);
 static bool glds_ok(const LrceGemmDesc* d);
 static bool g_force_legacy_gemm = getenv("LRCE_LEGACY_GEMM") != nullptr;   // A/B switch for benchmarking
+static int g_gemm_tile = getenv("LRCE_GEMM_TILE") ? atoi(getenv("LRCE_GEMM_TILE")) : 0;   // 0 auto, 64, 128
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
 
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
@@ -665,12 +747,23 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   dim3 grid(p.tiles_m * p.tiles_n, d->batch * split);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (glds_ok(d)) {
-    const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0);
+    // 128x128 tiles when they give every CU work; 64x64 otherwise (small-M / small-N problems)
+    const int t128 = p.tiles_m * p.tiles_n * d->batch * split;
+    const bool small = g_gemm_tile == 64 || (g_gemm_tile == 0 && t128 < 256);
+    if (small) {
+      p.tiles_m = (d->m + 63) / 64; p.tiles_n = (d->n + 63) / 64;
+      grid = dim3(p.tiles_m * p.tiles_n, d->batch * split);
+    }
+    const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0) | (small ? 4 : 0);
     switch (gk) {
-      case 3: gemm_glds_kernel<true, true><<<grid, NT, 0, s>>>(p); break;
-      case 2: gemm_glds_kernel<true, false><<<grid, NT, 0, s>>>(p); break;
-      case 1: gemm_glds_kernel<false, true><<<grid, NT, 0, s>>>(p); break;
-      case 0: gemm_glds_kernel<false, false><<<grid, NT, 0, s>>>(p); break;
+      case 3: gemm_glds_kernel<128, 128, true, true><<<grid, NT, 0, s>>>(p); break;
+      case 2: gemm_glds_kernel<128, 128, true, false><<<grid, NT, 0, s>>>(p); break;
+      case 1: gemm_glds_kernel<128, 128, false, true><<<grid, NT, 0, s>>>(p); break;
+      case 0: gemm_glds_kernel<128, 128, false, false><<<grid, NT, 0, s>>>(p); break;
+      case 7: gemm_glds_kernel<64, 64, true, true><<<grid, NT, 0, s>>>(p); break;
+      case 6: gemm_glds_kernel<64, 64, true, false><<<grid, NT, 0, s>>>(p); break;
+      case 5: gemm_glds_kernel<64, 64, false, true><<<grid, NT, 0, s>>>(p); break;
+      case 4: gemm_glds_kernel<64, 64, false, false><<<grid, NT, 0, s>>>(p); break;
     }
     return lrce_check_launch("gemm(glds)");
   }

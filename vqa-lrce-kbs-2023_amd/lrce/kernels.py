@@ -196,7 +196,8 @@ def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_
     Nn = dw.shape[0]
     K = dw.shape[1]
     split = _split_for(Nn, K, M)
-    flags = N.EPI_ATOMIC | (N.EPI_BIAS_GRAD if bias_grad is not None else 0)
+    # one K slice: plain vector read-modify-write of the gradient (same stream => no race); split-K: atomics
+    flags = (N.EPI_ATOMIC if split > 1 else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if bias_grad is not None else 0)
     gemm(dy, x, dw, Nn, K, M, a_kmajor=False, b_kmajor=False, lda=dy.shape[-1], ldb=x.shape[-1], ldc=K,
          flags=flags, bias=bias_grad, a_map=a_map, split_k=split, a_row_scale=a_row_scale,
          a_rows_per_scale=a_rows_per_scale)
