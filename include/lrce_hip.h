@@ -205,7 +205,8 @@ int lrce_scale_cast_bf16(const float* x, int64_t rows, int cols, const float* ro
  * (the residual's gradient is dy itself). */
 int lrce_dropout(const float* x, const float* res, float* y, uint16_t* y_bf16, int64_t n, float p, uint64_t seed,
                  int64_t group, void* stream);
-int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t seed, int64_t group, void* stream);
+int lrce_dropout_bwd(const float* dy, float* dx, uint16_t* dx_bf16, int64_t n, float p, uint64_t seed, int64_t group,
+                     void* stream);  /* dx and/or its bf16 copy dx_bf16 (either may be NULL) */
 /* Device-side RNG offset for graph replay: every hash-based mask (lrce_dropout*, lrce_mha_* dropout)
  * uses seed + *offset when a device pointer is registered (NULL = 0, the default).  A captured
  * HIP graph bakes the host seeds; advancing *offset (one device add per training step) gives each

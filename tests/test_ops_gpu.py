@@ -281,7 +281,8 @@ def test_window_attention_fwd_bwd(nH, n_win):
 
 @pytest.mark.parametrize("B,H,Lq,Lk,masked,split,bdiv,drop", [
     (3, 12, 32, 32, True, 0, 1, 0.0), (4, 12, 1, 183, False, 150, 1, 0.0), (2, 12, 40, 40, True, 0, 1, 0.0),
-    (10, 12, 1, 191, False, 150, 5, 0.0), (3, 12, 32, 32, True, 0, 1, 0.3), (5, 12, 1, 183, False, 150, 5, 0.5)])
+    (10, 12, 1, 191, False, 150, 5, 0.0), (3, 12, 32, 32, True, 0, 1, 0.3), (5, 12, 1, 183, False, 150, 5, 0.5),
+    (6, 12, 37, 37, True, 0, 1, 0.1), (45, 12, 40, 40, True, 0, 1, 0.0), (1, 12, 20, 20, False, 0, 1, 0.0)])
 def test_mha_fwd_bwd(B, H, Lq, Lk, masked, split, bdiv, drop):
     K().rng_offset(dev).zero_()   # host reference masks assume offset 0
     """Two key segments (video memory shared by `bdiv` rows + text memory), padding mask, dropout."""

@@ -44,6 +44,10 @@ SHAPES = [
     (320, 3072, 768, "fwd", "bias_gelu"),
     (320, 768, 3072, "fwd", "bias"),
     (768, 768, 320, "dw", ""),
+    (320, 768, 768, "dx", ""),
+    (320, 768, 3072, "dx", ""),
+    (320, 3072, 768, "dx", "dgelu"),
+    (4500, 768, 1536, "dx", ""),
     (4500, 1536, 768, "fwd", "bias"),
     (1536, 768, 4500, "dw", ""),
 ]

@@ -125,13 +125,14 @@ __global__ void dropout_kernel(const float* __restrict__ x, const float* __restr
   if (yb) yb[i] = f2bf(v);
 }
 
-__global__ void dropout_bwd_kernel(const float* __restrict__ dy, float* __restrict__ dx, long long n, float p, uint64_t seed,
-                                   long long group, const uint64_t* __restrict__ off) {
+__global__ void dropout_bwd_kernel(const float* __restrict__ dy, float* __restrict__ dx, bf16* __restrict__ dx16, long long n,
+                                   float p, uint64_t seed, long long group, const uint64_t* __restrict__ off) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float v = dy[i];
   if (p > 0.f) v = (lrce_uniform(lrce_seed(seed, off), i / group) >= p) ? v / (1.0f - p) : 0.f;
-  dx[i] = v;
+  if (dx) dx[i] = v;
+  if (dx16) dx16[i] = f2bf(v);
 }
 
 // ---------------------------------------------------------------- embeddings
@@ -297,11 +298,13 @@ extern "C" int lrce_dropout(const float* x, const float* res, float* y, uint16_t
   return lrce_check_launch("dropout");
 }
 
-extern "C" int lrce_dropout_bwd(const float* dy, float* dx, int64_t n, float p, uint64_t seed, int64_t group, void* stream) {
-  if (!dy || !dx) return lrce_fail(LRCE_E_ARG, "dropout_bwd: null pointer");
+extern "C" int lrce_dropout_bwd(const float* dy, float* dx, uint16_t* dx_bf16, int64_t n, float p, uint64_t seed, int64_t group,
+                                void* stream) {
+  if (!dy || (!dx && !dx_bf16)) return lrce_fail(LRCE_E_ARG, "dropout_bwd: null pointer");
   if (n <= 0) return LRCE_OK;
   if (group < 1) group = 1;
-  dropout_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(dy, dx, n, p, seed, group, lrce_rng_offset());
+  dropout_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(
+      dy, dx, reinterpret_cast<bf16*>(dx_bf16), n, p, seed, group, lrce_rng_offset());
   return lrce_check_launch("dropout_bwd");
 }
 

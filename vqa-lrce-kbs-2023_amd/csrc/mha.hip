@@ -17,6 +17,11 @@ namespace {
 constexpr int D = 64;
 constexpr int MAXK = 192;
 
+__device__ __forceinline__ void wave_lds_fence_m() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 struct MhaP {
   LrceMhaDesc d;
   const uint64_t* off;  // device RNG offset (lrce_set_rng_offset)
@@ -314,12 +319,306 @@ __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
         ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane])) * d.scale;
 }
 
+// ---- short self-attention on MFMA (BERT: Lq = Lk = L <= 64, one key segment) ---------------------
+// One wave per (batch row, head); L padded to NTL x 32.  v_mfma_f32_32x32x16_bf16 throughout, the
+// layout recipe of window_attn.hip: the forward computes S^T = K Q^T so a lane owns one query
+// column (in-lane softmax + one cross-half exchange) and the probabilities feed O^T = V^T P^T from
+// registers; the backward recomputes S = Q K^T per 32x32 tile, dV = P^T dO and dK = dS^T Q from
+// registers, dQ = dS K through a 2 KB LDS transpose of dS.  Scores are scaled in f32 (HF order:
+// (q.k) * d^-1/2, then the key mask, softmax, dropout on the probabilities).
+constexpr float LOG2E_F = 1.4426950408889634f;
+
+__device__ __forceinline__ int crow32(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// transposed reads of a [rows][64] bf16 LDS image, columns col0 .. col0 + 31 (see window_attn.hip)
+__device__ __forceinline__ bf16x8 tr_perm64(const bf16* img, int r_base, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int hh = g >> 1, cb = col0 + 16 * (g & 1);
+  bf16x8 out;
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    const int row = r_base + 8 * h2 + 4 * hh + q;
+    const LRCE_LDS s16x4* src = (const LRCE_LDS s16x4*)(img + row * D + cb + 4 * p);
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<LRCE_LDS s16x4*>(src));
+    bf16x4 b = *reinterpret_cast<bf16x4*>(&v);
+    out[4 * h2 + 0] = b[0]; out[4 * h2 + 1] = b[1]; out[4 * h2 + 2] = b[2]; out[4 * h2 + 3] = b[3];
+  }
+  return out;
+}
+template <int STRIDE>
+__device__ __forceinline__ bf16x8 tr_nat(const bf16* img, int r_base, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int hh = g >> 1, cb = col0 + 16 * (g & 1);
+  bf16x8 out;
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    const int row = r_base + 8 * hh + 4 * h2 + q;
+    const LRCE_LDS s16x4* src = (const LRCE_LDS s16x4*)(img + row * STRIDE + cb + 4 * p);
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<LRCE_LDS s16x4*>(src));
+    bf16x4 b = *reinterpret_cast<bf16x4*>(&v);
+    out[4 * h2 + 0] = b[0]; out[4 * h2 + 1] = b[1]; out[4 * h2 + 2] = b[2]; out[4 * h2 + 3] = b[3];
+  }
+  return out;
+}
+__device__ __forceinline__ bf16x8 pack8f(const f32x16& a, int s) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(a[8 * s + j]);
+  return o;
+}
+__device__ __forceinline__ bf16x8 ldrow16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// rows [0, LP) x 64 of a head slice into an LDS image (rows >= n zero)
+template <int LP>
+__device__ __forceinline__ void stage64(bf16* img, const bf16* src, long long ld, int n, int lane) {
+#pragma unroll
+  for (int t = 0; t < LP / 8; ++t) {
+    const int c = lane + 64 * t;
+    const int row = c >> 3, part = c & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < n) v = *reinterpret_cast<const uint4*>(src + row * ld + part * 8);
+    *reinterpret_cast<uint4*>(img + row * D + part * 8) = v;
+  }
+}
+
+template <int NTL>
+__global__ void __launch_bounds__(256) mhaL_fwd_kernel(MhaP P) {
+  constexpr int LP = 32 * NTL;
+  const LrceMhaDesc& d = P.d;
+  __shared__ __attribute__((aligned(16))) bf16 vimg_all[4][LP * D];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.x * 4 + wave;
+  if (bh >= d.B * d.H) return;
+  const int b = bh / d.H, h = bh % d.H;
+  const int L = d.lk1;
+  const bf16* qb = reinterpret_cast<const bf16*>(d.q) + (long long)b * L * d.ld_q + h * D;
+  const bf16* kb = reinterpret_cast<const bf16*>(d.k1) + (long long)b * d.stride_kv1_b + h * D;
+  const bf16* vb = reinterpret_cast<const bf16*>(d.v1) + (long long)b * d.stride_kv1_b + h * D;
+  bf16* vimg = vimg_all[wave];
+  stage64<LP>(vimg, vb, d.ld_kv1, L, lane);
+  const int hh = lane >> 5, r32 = lane & 31;
+  bf16x8 kf[NTL][4];
+#pragma unroll
+  for (int kt = 0; kt < NTL; ++kt) {
+    const int key = kt * 32 + r32;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kf[kt][s] = key < L ? ldrow16(kb + key * d.ld_kv1 + 16 * s + 8 * hh) : bf16x8{};
+  }
+  const int* km = d.key_mask ? d.key_mask + (long long)b * L : nullptr;
+  bool kok[NTL][16];
+#pragma unroll
+  for (int kt = 0; kt < NTL; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kt * 32 + crow32(r, hh);
+      kok[kt][r] = key < L && (!km || km[key] != 0);
+    }
+  wave_lds_fence_m();
+  const float c2 = d.scale * LOG2E_F;
+#pragma unroll
+  for (int qt = 0; qt < NTL; ++qt) {
+    const int qi = qt * 32 + r32;
+    bf16x8 qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = qi < L ? ldrow16(qb + qi * d.ld_q + 16 * s + 8 * hh) : bf16x8{};
+    f32x16 acc[NTL];
+#pragma unroll
+    for (int kt = 0; kt < NTL; ++kt) {
+      acc[kt] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][s], qf[s], acc[kt], 0, 0, 0);
+    }
+    float m = -1.0e30f;
+#pragma unroll
+    for (int kt = 0; kt < NTL; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m = kok[kt][r] ? fmaxf(m, acc[kt][r]) : m;
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NTL; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = kok[kt][r] ? exp2f((acc[kt][r] - m) * c2) : 0.f;
+        sum += p;
+        if (d.drop_p > 0.f) p *= drop_factor(d, P.off, b, h, qi, kt * 32 + crow32(r, hh), L);
+        acc[kt][r] = p;
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    f32x16 o[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+    for (int kt = 0; kt < NTL; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack8f(acc[kt], s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_perm64(vimg, kt * 32 + 16 * s, 32 * dt, lane), pb, o[dt], 0, 0, 0);
+      }
+    if (qi < L) {
+      const float inv = 1.0f / sum;
+      bf16* dst = reinterpret_cast<bf16*>(d.out) + ((long long)b * L + qi) * d.ld_o + h * D + 4 * hh;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          bf16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][4 * rr + e] * inv);
+          *reinterpret_cast<bf16x4*>(dst + 32 * dt + 8 * rr) = v;
+        }
+      if (hh == 0) d.lse[((long long)b * d.H + h) * L + qi] = m * d.scale + __logf(sum);
+    }
+  }
+}
+
+template <int LP>
+struct MhaLBwdLds {
+  bf16 q[LP * D];
+  bf16 k[LP * D];
+  bf16 dout[LP * D];
+  bf16 t[32 * 32];
+  float lse2[LP];
+  float delta[LP];
+};
+
+template <int NTL>
+__global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
+  constexpr int LP = 32 * NTL;
+  const LrceMhaDesc& d = P.d;
+  __shared__ __attribute__((aligned(16))) MhaLBwdLds<LP> S_all[2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.x * 2 + wave;
+  if (bh >= d.B * d.H) return;
+  MhaLBwdLds<LP>& S = S_all[wave];
+  const int b = bh / d.H, h = bh % d.H;
+  const int L = d.lk1;
+  const bf16* qb = reinterpret_cast<const bf16*>(d.q) + (long long)b * L * d.ld_q + h * D;
+  const bf16* kb = reinterpret_cast<const bf16*>(d.k1) + (long long)b * d.stride_kv1_b + h * D;
+  const bf16* vb = reinterpret_cast<const bf16*>(d.v1) + (long long)b * d.stride_kv1_b + h * D;
+  const bf16* ob = reinterpret_cast<const bf16*>(d.out) + (long long)b * L * d.ld_o + h * D;
+  const bf16* gb = reinterpret_cast<const bf16*>(d.dout) + (long long)b * L * d.ld_o + h * D;
+  stage64<LP>(S.q, qb, d.ld_q, L, lane);
+  stage64<LP>(S.k, kb, d.ld_kv1, L, lane);
+  stage64<LP>(S.dout, gb, d.ld_o, L, lane);
+  for (int i = lane; i < LP; i += 64) {
+    float dl = 0.f, l2 = 0.f;
+    if (i < L) {
+#pragma unroll
+      for (int part = 0; part < 8; ++part) {
+        const bf16x8 a = ldrow16(ob + i * d.ld_o + part * 8), g = ldrow16(gb + i * d.ld_o + part * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dl += bf2f(a[j]) * bf2f(g[j]);
+      }
+      l2 = d.lse[((long long)b * d.H + h) * L + i] * LOG2E_F;
+    }
+    S.delta[i] = dl;
+    S.lse2[i] = l2;
+  }
+  wave_lds_fence_m();
+  const int hh = lane >> 5, r32 = lane & 31;
+  const int* km = d.key_mask ? d.key_mask + (long long)b * L : nullptr;
+  const float c2 = d.scale * LOG2E_F;
+  f32x16 dq[NTL][2];
+#pragma unroll
+  for (int qt = 0; qt < NTL; ++qt) dq[qt][0] = dq[qt][1] = f32x16{};
+#pragma unroll
+  for (int kt = 0; kt < NTL; ++kt) {
+    const int key = kt * 32 + r32;
+    const bool kok = key < L && (!km || km[key] != 0);
+    bf16x8 kf[4], vf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = key < L ? ldrow16(kb + key * d.ld_kv1 + 16 * s + 8 * hh) : bf16x8{};
+      vf[s] = key < L ? ldrow16(vb + key * d.ld_kv1 + 16 * s + 8 * hh) : bf16x8{};
+    }
+    f32x16 dv[2] = {f32x16{}, f32x16{}}, dk[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+    for (int qt = 0; qt < NTL; ++qt) {
+      f32x16 sacc = f32x16{}, dp = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(S.q + (qt * 32 + r32) * D + 16 * s + 8 * hh);
+        const bf16x8 ga = *reinterpret_cast<const bf16x8*>(S.dout + (qt * 32 + r32) * D + 16 * s + 8 * hh);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[s], dp, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = qt * 32 + crow32(r, hh);
+        const float p = (kok && qi < L) ? exp2f(sacc[r] * c2 - S.lse2[qi]) : 0.f;
+        const float f = d.drop_p > 0.f ? drop_factor(d, P.off, b, h, qi, key, L) : 1.f;
+        sacc[r] = p * f;                        // dV uses the dropped probabilities
+        dp[r] = p * (f * dp[r] - S.delta[qi]);  // dS (w.r.t. the scaled scores)
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pa = pack8f(sacc, s), da = pack8f(dp, s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, tr_perm64(S.dout, qt * 32 + 16 * s, 32 * dt, lane), dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, tr_perm64(S.q, qt * 32 + 16 * s, 32 * dt, lane), dk[dt], 0, 0, 0);
+        }
+      }
+      // dS^T -> LDS T[key][query], then dQ[qt] += dS K
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f2bf(dp[4 * rr + e]);
+        *reinterpret_cast<bf16x4*>(S.t + r32 * 32 + 8 * rr + 4 * hh) = v;
+      }
+      wave_lds_fence_m();
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 a = tr_nat<32>(S.t, 16 * s, 0, lane);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          dq[qt][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, tr_nat<D>(S.k, kt * 32 + 16 * s, 32 * dt, lane), dq[qt][dt], 0, 0, 0);
+      }
+      wave_lds_fence_m();
+    }
+    // dK, dV rows of this key tile (this wave is their only writer): rows crow, column d = r32
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kk = kt * 32 + crow32(r, hh);
+      if (kk < L) {
+        const long long o = (long long)b * d.stride_dkv1_b + (long long)kk * d.ld_dkv1 + h * D + r32;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          d.dk1[o + 32 * dt] += dk[dt][r] * d.scale;
+          d.dv1[o + 32 * dt] += dv[dt][r];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < NTL; ++qt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = qt * 32 + crow32(r, hh);
+      if (qi < L) {
+        float* dst = d.dq + ((long long)b * L + qi) * d.ld_dq + h * D + r32;
+        dst[0] = dq[qt][0][r] * d.scale;
+        dst[32] = dq[qt][1][r] * d.scale;
+      }
+    }
+}
+
 // key/value rows readable as 16-B vectors (single-query path)
 bool aligned_rows(const LrceMhaDesc* d) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   bool ok = al(d->k1) && al(d->v1) && d->ld_kv1 % 8 == 0 && d->stride_kv1_b % 8 == 0;
   if (d->lk2 > 0) ok = ok && al(d->k2) && al(d->v2) && d->ld_kv2 % 8 == 0 && d->stride_kv2_b % 8 == 0;
   return ok;
+}
+
+// BERT-shaped self-attention: one key segment, Lq = Lk <= 64, bf16 io, 16-B aligned rows
+bool short_self(const LrceMhaDesc* d) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return d->lk2 == 0 && d->Lq == d->lk1 && d->Lq <= 64 && d->kv1_bdiv == 1 && !d->f32_io && aligned_rows(d) &&
+         al(d->q) && d->ld_q % 8 == 0 && al(d->out) && d->ld_o % 8 == 0 && (!d->dout || al(d->dout)) &&
+         d->stride_kv1_b == (long long)d->lk1 * d->ld_kv1 && getenv("LRCE_MHA_VALU") == nullptr;
 }
 
 int check(const LrceMhaDesc* d, bool bwd) {
@@ -339,6 +638,12 @@ int check(const LrceMhaDesc* d, bool bwd) {
 extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, false)) return rc;
   MhaP p{*d, lrce_rng_offset()};
+  if (short_self(d)) {
+    const unsigned nb = (d->B * d->H + 3) / 4;
+    if (d->Lq <= 32) mhaL_fwd_kernel<1><<<nb, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
+    else mhaL_fwd_kernel<2><<<nb, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
+    return lrce_check_launch("mha_fwd(mfma)");
+  }
   if (d->Lq == 1 && aligned_rows(d)) {
     mha1_fwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
     return lrce_check_launch("mha_fwd");
@@ -350,6 +655,12 @@ extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
 extern "C" int lrce_mha_bwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, true)) return rc;
   MhaP p{*d, lrce_rng_offset()};
+  if (short_self(d)) {
+    const unsigned nb = (d->B * d->H + 1) / 2;
+    if (d->Lq <= 32) mhaL_bwd_kernel<1><<<nb, 128, 0, static_cast<hipStream_t>(stream)>>>(p);
+    else mhaL_bwd_kernel<2><<<nb, 128, 0, static_cast<hipStream_t>(stream)>>>(p);
+    return lrce_check_launch("mha_bwd(mfma)");
+  }
   if (d->Lq == 1 && aligned_rows(d)) {
     mha1_bwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
     return lrce_check_launch("mha_bwd");

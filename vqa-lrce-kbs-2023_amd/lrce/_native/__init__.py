@@ -92,7 +92,7 @@ _SIGS = {
     "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _I, _P, _P],
     "lrce_cast_bf16": [_P, _P, _I64, _P],
     "lrce_dropout": [_P, _P, _P, _P, _I64, _F, _U64, _I64, _P],
-    "lrce_dropout_bwd": [_P, _P, _I64, _F, _U64, _I64, _P],
+    "lrce_dropout_bwd": [_P, _P, _P, _I64, _F, _U64, _I64, _P],
     "lrce_bert_embed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_bert_embed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I64, _P],
     "lrce_video_posembed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],

@@ -161,40 +161,50 @@ class _LayerFn(torch.autograd.Function):
         do2 = torch.empty_like(o2)
         K.layernorm_bwd(dout, o2, m2, r2, oo.LayerNorm.weight, do2, dw=_g(flat, oo.LayerNorm.weight),
                         db=_g(flat, oo.LayerNorm.bias))
-        do = K.dropout_bwd(do2, p, seed + 2) if p > 0 else do2
+        # the backward GEMMs read bf16 gradients (glds MFMA path); residual sums stay f32
+        do = _grad16(do2, p, seed + 2)
         _wgrad(flat, oo.dense, do, g)
-        dh1 = K.linear_dx(do, flat.w16(oo.dense.weight), out_f32=True, dgelu_pre=pre)   # d(pre) in f32
+        dh1 = K.linear_dx(do, flat.w16(oo.dense.weight), out_f32=False, dgelu_pre=pre)   # d(pre), bf16
         _wgrad(flat, it.dense, dh1, h1b)
         dh1x = K.linear_dx(dh1, flat.w16(it.dense.weight), resid=do2)
         da2 = torch.empty_like(a2)
         K.layernorm_bwd(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, dw=_g(flat, ao.LayerNorm.weight),
                         db=_g(flat, ao.LayerNorm.bias))
-        da = K.dropout_bwd(da2, p, seed + 1) if p > 0 else da2
+        da = _grad16(da2, p, seed + 1)
         _wgrad(flat, ao.dense, da, ctxt)
         dctx = K.linear_dx(da, flat.w16(ao.dense.weight), out_f32=False)
         rows = B * L
-        dq = torch.empty(rows, HIDDEN, device=dout.device)
-        dk = torch.zeros(rows, HIDDEN, device=dout.device)
-        dv = torch.zeros(rows, HIDDEN, device=dout.device)
-        K.mha_bwd(ctx.desc, dout=dctx, dq=dq, dk1=dk, dv1=dv, ld_dkv1=HIDDEN, stride_dkv1_b=L * HIDDEN)
-        for lin, dg in ((sa.query, dq), (sa.key, dk), (sa.value, dv)):
-            _wgrad(flat, lin, dg, xb)
-        dx = K.linear_dx(dq, flat.w16(sa.query.weight), resid=da2)
-        K.linear_dx(dk, flat.w16(sa.key.weight), out=dx, accumulate=True)
-        K.linear_dx(dv, flat.w16(sa.value.weight), out=dx, accumulate=True)
+        dqkv = torch.zeros(3, rows, HIDDEN, device=dout.device)
+        K.mha_bwd(ctx.desc, dout=dctx, dq=dqkv[0], dk1=dqkv[1], dv1=dqkv[2], ld_dkv1=HIDDEN, stride_dkv1_b=L * HIDDEN)
+        dqkv16 = torch.empty(3, rows, HIDDEN, dtype=torch.bfloat16, device=dout.device)
+        K.cast_bf16(dqkv, dqkv16)
+        for i, lin in enumerate((sa.query, sa.key, sa.value)):
+            _wgrad(flat, lin, dqkv16[i], xb)
+        dx = K.linear_dx(dqkv16[0], flat.w16(sa.query.weight), resid=da2)
+        K.linear_dx(dqkv16[1], flat.w16(sa.key.weight), out=dx, accumulate=True)
+        K.linear_dx(dqkv16[2], flat.w16(sa.value.weight), out=dx, accumulate=True)
         ctx.save = ctx.desc = None
         flat.notify(layer.parameters())
         return (dx,) + (None,) * (7 + len(ctx.needs_input_grad[8:]))
 
 
+def _grad16(d32, p, seed):
+    """bf16 copy of the dropout-backward of an f32 gradient (the operand of the backward GEMMs)."""
+    if p > 0:
+        return K.dropout_bwd(d32, p, seed, f32=False)
+    out = torch.empty(d32.shape, dtype=torch.bfloat16, device=d32.device)
+    K.cast_bf16(d32, out)
+    return out
+
+
 def _wgrad(flat, lin, dy, x16):
+    """dW += dY^T X with the bias gradient (column sums of dY) fused into the same GEMM."""
     gw = _g(flat, lin.weight)
+    gb = _g(flat, lin.bias) if lin.bias is not None else None
     if gw is not None:
-        K.linear_dw(dy, x16, gw)
-    if lin.bias is not None:
-        gb = _g(flat, lin.bias)
-        if gb is not None:
-            K.colsum(dy, gb)
+        K.linear_dw(dy, x16, gw, bias_grad=gb)
+    elif gb is not None:
+        K.colsum(dy, gb)
 
 
 class BertModel(nn.Module):

@@ -327,11 +327,17 @@ def dropout(x, p, seed, out=None, out_bf16=None, res=None, group=1):
     return out
 
 
-def dropout_bwd(dy, p, seed, out=None, group=1):
-    if out is None:
+def dropout_bwd(dy, p, seed, out=None, group=1, out_bf16=None, f32=True):
+    """dx = dy * keep / (1-p); out_bf16: also (or, f32=False: only) a bf16 copy for the GEMMs."""
+    if out is None and f32:
         out = torch.empty_like(dy)
-    call("lrce_dropout_bwd", ptr(dy), ptr(out), dy.numel(), float(p), seed & (2 ** 64 - 1), group, stream_of(out))
-    return out
+    if not f32:
+        out = None
+        if out_bf16 is None:
+            out_bf16 = torch.empty(dy.shape, dtype=BF16, device=dy.device)
+    call("lrce_dropout_bwd", ptr(dy), ptr(out), ptr(out_bf16), dy.numel(), float(p), seed & (2 ** 64 - 1), group,
+         stream_of(dy))
+    return out if f32 else out_bf16
 
 
 def bert_embed_fwd(ids, types, word, pos, typ, out, rows, L, C):
