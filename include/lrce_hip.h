@@ -82,6 +82,12 @@ typedef struct LrceGemmDesc {
   /* b_f32 = 1: B is f32 (then A must be f32): exact-f32 MFMA path (v_mfma_f32_16x16x4_f32) for the
    * small-M recurrent-decoder linears that read the f32 master weights directly. */
   int32_t b_f32;
+  /* Split-K workspace (optional, f32, >= split_k * m * n elements, batch 1, flags = ATOMIC [+ BIAS_GRAD]
+   * with no other epilogue): each K slice stores its partial tile with plain vector stores and a
+   * second launch adds the slices into C -- no f32 atomics on C (their throughput bounds the
+   * weight-gradient GEMMs otherwise). */
+  float* workspace;
+  int64_t workspace_elems;
 } LrceGemmDesc;
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);

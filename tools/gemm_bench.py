@@ -110,5 +110,37 @@ def main():
             run(*s, a.iters)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("DW_SWEEP"):
     main()
+
+
+def dw_split_sweep(iters=20):
+    """dW = dY^T X at the Swin stage-3 shapes: split-K factor vs time (atomic f32 accumulation)."""
+    dev = "cuda"
+    for (M, Nn, Kk) in [(512, 2048, 17640), (2048, 512, 17640), (512, 512, 17640), (1536, 512, 17640),
+                        (512, 128, 282240), (256, 1024, 70560)]:
+        dy = torch.rand(Kk, M, device=dev).sub_(0.5).to(torch.bfloat16)
+        x = torch.rand(Kk, Nn, device=dev).sub_(0.5).to(torch.bfloat16)
+        dw = torch.zeros(M, Nn, device=dev)
+        line = f"dw {M:5d} {Nn:5d} {Kk:6d}: auto {K._split_for(M, Nn, Kk)}"
+        ws = torch.empty(128 * M * Nn, device=dev) if os.environ.get("DW_SLAB") else None
+        for split in (1, 2, 4, 8, 16, 32, 64, 128):
+            fl = N.EPI_ATOMIC if split > 1 else N.EPI_ACCUM
+            f = lambda: K.gemm(dy, x, dw, M, Nn, Kk, a_kmajor=False, b_kmajor=False, lda=M, ldb=Nn, ldc=Nn,  # noqa
+                               flags=fl, split_k=split, workspace=ws)
+            for _ in range(2):
+                f()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                f()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / iters
+            line += f"  s{split}:{ms * 1e3:6.1f}us"
+        print(line, flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("DW_SWEEP"):
+    dw_split_sweep()

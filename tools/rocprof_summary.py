@@ -15,10 +15,12 @@ def main(path, top=40):
     rows = c.execute("select name, count(*), sum(duration), avg(duration), min(duration), max(duration) "
                      "from kernels group by name order by sum(duration) desc").fetchall()
     total = sum(r[2] for r in rows)
+    steps = sum(r[1] for r in rows if "adamw_kernel" in r[0]) or 1   # one optimizer launch per training step
     print(f"# rocprofv3 --kernel-trace --stats summary: {path}")
-    print(f"# total kernel time {total / 1e6:.3f} ms over {sum(r[1] for r in rows)} dispatches\n")
-    print("| kernel | calls | total_us | avg_us | min_us | max_us | pct |")
-    print("|---|---|---|---|---|---|---|")
+    print(f"# total kernel time {total / 1e6:.3f} ms over {sum(r[1] for r in rows)} dispatches; "
+          f"{steps} training steps (adamw launches) -> {total / 1e6 / steps:.2f} ms of kernels per step\n")
+    print("| kernel | calls | total_us | avg_us | min_us | max_us | pct | us/step |")
+    print("|---|---|---|---|---|---|---|---|")
     for name, n, s, a, lo, hi in rows[:top]:
         mg = re.match(r"_ZN12_GLOBAL__N_1(\d+)", name)   # mangled (bf16 args defeat c++filt): keep the name
         if mg:
@@ -27,7 +29,7 @@ def main(path, top=40):
         short = re.sub(r"\(anonymous namespace\)::", "", name)
         short = re.sub(r"\((?:[^()]|\([^()]*\))*\)$", "", short).replace("void ", "")
         short = short if len(short) <= 90 else short[:87] + "..."
-        print(f"| `{short}` | {n} | {s / 1e3:.1f} | {a / 1e3:.2f} | {lo / 1e3:.2f} | {hi / 1e3:.2f} | {100 * s / total:.2f} |")
+        print(f"| `{short}` | {n} | {s / 1e3:.1f} | {a / 1e3:.2f} | {lo / 1e3:.2f} | {hi / 1e3:.2f} | {100 * s / total:.2f} | {s / 1e3 / steps:.1f} |")
 
 
 if __name__ == "__main__":

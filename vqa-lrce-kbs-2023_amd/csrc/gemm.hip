@@ -48,6 +48,7 @@ struct GemmP {
   int a_rows_per_scale;
   int tiles_m, tiles_n;
   int vec;  // 1: c/aux/aux_out/bias rows are 16-B aligned and n % 8 == 0 (vector epilogue)
+  float* ws; // split-K slabs [split][m][n] (plain stores, reduced by splitk_reduce_kernel), or null
 };
 
 // ---- LDS addressing --------------------------------------------------------------------------
@@ -586,7 +587,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   }
   char* cbase = static_cast<char*>(p.c) +
                 (long long)bz * p.sc * ((p.flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
-  if (p.flags & LRCE_EPI_ATOMIC) {
+  if ((p.flags & LRCE_EPI_ATOMIC) && !p.ws) {
     // split-K partials: stage 32-row slabs through LDS (free now) so each atomic instruction covers
     // consecutive columns of a row.  acc[i][j][r] = C[m = i*16 + (lane&15)][n = j*16 + 4*(lane>>4) + r]
     constexpr int EPW = WN + 4;
@@ -621,9 +622,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   // columns 16j + 4g + r of row rho before and 16g + 4j + r after (16 contiguous columns);
   // JN = 2: columns 16j + 4g + r before, 8g + 4j + r after (8 contiguous).  The epilogue then
   // reads/writes 16-B vectors (bias, residual, GELU pre-activation, output).
-  static_for<IM>([&](auto ic) {
+  auto transpose = [&](auto ic, uint32_t (&u)[JN][4]) {
     constexpr int i = decltype(ic)::value;
-    uint32_t u[JN][4];
 #pragma unroll
     for (int j = 0; j < JN; ++j)
 #pragma unroll
@@ -654,8 +654,40 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
         u[1][r] = s16[1];
       }
     }
-    const int m = m0 + wm * WM + i * 16 + (lane & 15);
-    const int ncol = n0 + wn * WN + (JN * 4) * (lane >> 4);
+  };
+  const int ncol = n0 + wn * WN + (JN * 4) * (lane >> 4);
+  if (p.ws) {
+    // split-K slab: this slice's alpha * partial tile, plain stores (reduced by splitk_reduce_kernel)
+    float* slab = p.ws + (long long)sk * p.m * p.n;
+    const bool vec4 = (p.n & 3) == 0;
+    static_for<IM>([&](auto ic) {
+      uint32_t u[JN][4];
+      transpose(ic, u);
+      const int m = m0 + wm * WM + decltype(ic)::value * 16 + (lane & 15);
+      if (m < p.m) {
+        float* row = slab + (long long)m * p.n;
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          const int n = ncol + 4 * j;
+          const float4 v = make_float4(__uint_as_float(u[j][0]) * p.alpha, __uint_as_float(u[j][1]) * p.alpha,
+                                       __uint_as_float(u[j][2]) * p.alpha, __uint_as_float(u[j][3]) * p.alpha);
+          if (vec4 && n + 4 <= p.n) {
+            *reinterpret_cast<float4*>(row + n) = v;
+          } else {
+            if (n < p.n) row[n] = v.x;
+            if (n + 1 < p.n) row[n + 1] = v.y;
+            if (n + 2 < p.n) row[n + 2] = v.z;
+            if (n + 3 < p.n) row[n + 3] = v.w;
+          }
+        }
+      }
+    });
+    return;
+  }
+  static_for<IM>([&](auto ic) {
+    uint32_t u[JN][4];
+    transpose(ic, u);
+    const int m = m0 + wm * WM + decltype(ic)::value * 16 + (lane & 15);
 #pragma unroll
     for (int h = 0; h < JN / 2; ++h) {
       float v[8];
@@ -664,6 +696,22 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       epilogue8(p, v, m, ncol + 8 * h, sk, cbase);
     }
   });
+}
+
+// C[m][n] += sum_s ws[s][m][n]  (n % 4 == 0, ldc % 4 == 0)
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, int m, int n, float* __restrict__ c, long long ldc) {
+  const long long mn = (long long)m * n;
+  const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e >= mn) return;
+  float4 s = *reinterpret_cast<const float4*>(ws + e);
+  for (int k = 1; k < split; ++k) {
+    const float4 t = *reinterpret_cast<const float4*>(ws + k * mn + e);
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  }
+  float4* cp = reinterpret_cast<float4*>(c + (e / n) * ldc + (e % n));
+  float4 o = *cp;
+  o.x += s.x; o.y += s.y; o.z += s.z; o.w += s.w;
+  *cp = o;
 }
 
 }  // namespace
@@ -744,6 +792,12 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
           (!d->bias || al16(d->bias)) && (!d->aux || (al16(d->aux) && d->ld_aux % 8 == 0)) &&
           (!d->aux_out || (al16(d->aux_out) && d->ld_aux_out % 8 == 0));
   (void)out32;
+  p.ws = nullptr;
+  const bool use_ws = d->workspace && split > 1 && (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)) == 0 &&
+                      (d->flags & LRCE_EPI_ATOMIC) && d->batch == 1 && !d->c_map && !d->row_scale && d->scale_cols == 0 &&
+                      d->n % 4 == 0 && d->ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(d->c) & 15) == 0 &&
+                      d->workspace_elems >= (int64_t)split * d->m * d->n && glds_ok(d);
+  if (use_ws) p.ws = d->workspace;
   dim3 grid(p.tiles_m * p.tiles_n, d->batch * split);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (glds_ok(d)) {
@@ -764,6 +818,10 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
       case 6: gemm_glds_kernel<64, 64, true, false><<<grid, NT, 0, s>>>(p); break;
       case 5: gemm_glds_kernel<64, 64, false, true><<<grid, NT, 0, s>>>(p); break;
       case 4: gemm_glds_kernel<64, 64, false, false><<<grid, NT, 0, s>>>(p); break;
+    }
+    if (p.ws) {
+      const long long q4 = (long long)d->m * d->n / 4;
+      splitk_reduce_kernel<<<(unsigned)((q4 + 255) / 256), 256, 0, s>>>(p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
     }
     return lrce_check_launch("gemm(glds)");
   }

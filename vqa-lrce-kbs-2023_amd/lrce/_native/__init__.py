@@ -48,6 +48,7 @@ class GemmDesc(ctypes.Structure):
         ("row_scale", ctypes.c_void_p), ("rows_per_scale", ctypes.c_int32),
         ("a_row_scale", ctypes.c_void_p), ("a_rows_per_scale", ctypes.c_int32),
         ("b_f32", ctypes.c_int32),
+        ("workspace", ctypes.c_void_p), ("workspace_elems", ctypes.c_int64),
     ]
 
 

@@ -99,7 +99,7 @@ def _chk(t, dtype=None, name="tensor"):
 def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, flags=0, bias=None,
          aux=None, ld_aux=0, aux_out=None, ld_aux_out=0, a_map=None, c_map=None, alpha=1.0, split_k=1,
          scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, a_row_scale=None, a_rows_per_scale=1,
-         batch=1, stride_a=0, stride_b=0, stride_c=0):
+         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None):
     """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc."""
     _chk(a, None, "A"); _chk(b, None, "B"); _chk(c, None, "C")
     a_f32 = a.dtype == F32
@@ -126,6 +126,8 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.row_scale, d.rows_per_scale = ptr(row_scale), rows_per_scale
     d.a_row_scale, d.a_rows_per_scale = ptr(a_row_scale), a_rows_per_scale
     d.b_f32 = int(b_f32)
+    if workspace is not None:
+        d.workspace, d.workspace_elems = ptr(workspace), workspace.numel()
     _timed("gemm_f32" if b_f32 else "gemm", c, lambda: call("lrce_gemm", ctypes.byref(d), stream_of(c)),
            flops=2.0 * m * n * k * batch,
            key=(m, n, k, batch, "AK" if a_kmajor else "AM", "BK" if b_kmajor else "BN", "a32" if a_f32 else "a16",
@@ -133,9 +135,10 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
 
 
 def _split_for(m_out, n_out, k_red):
+    """Split-K factor of a weight-gradient GEMM: ~2 blocks of 128x128 per CU, K slices >= 1024 deep."""
     tiles = math.ceil(m_out / 128) * math.ceil(n_out / 128)
-    want = max(1, (2 * NUM_CU * 2) // tiles)
-    return int(max(1, min(want, k_red // 512)))
+    want = max(1, math.ceil(2 * NUM_CU / tiles))
+    return int(max(1, min(want, k_red // 1024)))
 
 
 def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None, resid=None, c_map=None,
@@ -196,11 +199,15 @@ def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_
     Nn = dw.shape[0]
     K = dw.shape[1]
     split = _split_for(Nn, K, M)
-    # one K slice: plain vector read-modify-write of the gradient (same stream => no race); split-K: atomics
+    # one K slice: plain vector read-modify-write of the gradient (same stream => no race); split-K:
+    # per-slice f32 slabs in a workspace + one reduce launch (bf16 operands), atomics otherwise
     flags = (N.EPI_ATOMIC if split > 1 else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if bias_grad is not None else 0)
+    ws = None
+    if split > 1 and dy.dtype == BF16 and x.dtype == BF16:
+        ws = torch.empty(split * Nn * K, dtype=F32, device=dw.device)
     gemm(dy, x, dw, Nn, K, M, a_kmajor=False, b_kmajor=False, lda=dy.shape[-1], ldb=x.shape[-1], ldc=K,
          flags=flags, bias=bias_grad, a_map=a_map, split_k=split, a_row_scale=a_row_scale,
-         a_rows_per_scale=a_rows_per_scale)
+         a_rows_per_scale=a_rows_per_scale, workspace=ws)
 
 
 def colsum(x, out, *, row_map=None, rows=None, row_scale=None, rows_per_scale=1):
