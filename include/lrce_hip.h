@@ -132,6 +132,12 @@ int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld
                           const int32_t* region, int n_pat, float* bias_fwd, float* bias_bwd, void* stream);
 int lrce_wattn_fwd(const uint16_t* qkv, const float* bias_fwd, const int32_t* win_pat,
                    uint16_t* out, float* lse, int n_win, int n, int nH, void* stream);
+/* Same forward with windows grouped by mask pattern, GW = 4 windows per group: win_list int32
+ * [n_groups*4] (window ids, -1 = empty slot; NULL = identity 0,1,2,...), grp_pat int32 [n_groups]
+ * (the group's mask pattern; NULL = pattern 0).  The bias row of a query tile is staged once per
+ * group in LDS: build the grouping once per stage geometry (lrce/feature_extractor/video_swin.py). */
+int lrce_wattn_fwd_grouped(const uint16_t* qkv, const float* bias_fwd, const int32_t* win_list, const int32_t* grp_pat,
+                           int n_groups, uint16_t* out, float* lse, int n_win, int n, int nH, void* stream);
 /* dqkv: bf16 [n_win*n][3C] (d/dq, d/dk, d/dv w.r.t. the UNSCALED q).  ds_scratch: bf16,
  * lrce_wattn_ds_elems(n_win, nH) elements; table_grad (f32 [table_rows][nH]) is accumulated. */
 int64_t lrce_wattn_ds_elems(int n_win, int nH);

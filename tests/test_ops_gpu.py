@@ -265,6 +265,16 @@ def test_window_attention_fwd_bwd(nH, n_win):
     k.wattn_fwd(qkv, bf_, win_pat, out, lse, n_win, n, nH)
     ref, (q, kk, v, tab) = _wattn_reference(qkv, table, index, region, win_pat, nH, n, c)
     assert rel(out, ref) < 1e-2
+    # grouped-by-pattern forward (the product path): same result up to the f32 summation order
+    out_g = torch.full_like(out, float("nan"))
+    lse_g = torch.zeros_like(lse)
+    k.wattn_fwd_grouped(qkv, bf_, k.wattn_groups(win_pat, n_win, dev), out_g, lse_g, n_win, n, nH)
+    assert rel(out_g, ref) < 1e-2 and rel(out_g, out) < 1e-2   # bf16 outputs: 1 ulp apart at most
+    assert (lse_g[..., :n] - lse[..., :n]).abs().max().item() < 1e-4
+    out_i = torch.full_like(out, float("nan"))
+    k.wattn_fwd_grouped(qkv, bf_, k.wattn_groups(None, n_win, dev), out_i, lse_g, n_win, n, nH)   # identity grouping
+    ref_i, _ = _wattn_reference(qkv, table, index, region, torch.zeros_like(win_pat), nH, n, c)
+    assert rel(out_i, ref_i) < 1e-2
     dout = bf(torch.randn(n_win * n, C, device=dev))
     ref.backward(dout.float())
     dqkv = torch.empty(n_win * n, 3 * C, device=dev, dtype=torch.bfloat16)

@@ -439,7 +439,7 @@ __global__ void __launch_bounds__(256) mhaL_fwd_kernel(MhaP P) {
     for (int kt = 0; kt < NTL; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = kok[kt][r] ? exp2f((acc[kt][r] - m) * c2) : 0.f;
+        float p = kok[kt][r] ? __builtin_amdgcn_exp2f((acc[kt][r] - m) * c2) : 0.f;
         sum += p;
         if (d.drop_p > 0.f) p *= drop_factor(d, P.off, b, h, qi, kt * 32 + crow32(r, hh), L);
         acc[kt][r] = p;
@@ -546,7 +546,7 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = qt * 32 + crow32(r, hh);
-        const float p = (kok && qi < L) ? exp2f(sacc[r] * c2 - S.lse2[qi]) : 0.f;
+        const float p = (kok && qi < L) ? __builtin_amdgcn_exp2f(sacc[r] * c2 - S.lse2[qi]) : 0.f;
         const float f = d.drop_p > 0.f ? drop_factor(d, P.off, b, h, qi, key, L) : 1.f;
         sacc[r] = p * f;                        // dV uses the dropped probabilities
         dp[r] = p * (f * dp[r] - S.delta[qi]);  // dS (w.r.t. the scaled scores)

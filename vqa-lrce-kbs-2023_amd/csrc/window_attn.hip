@@ -16,6 +16,9 @@
 // dK = dS^T Q with P / dS straight from registers as A operands, dQ = dS K through a 2 KB LDS
 // transpose of dS; dQ accumulates across key tiles in registers.  dS (bf16) is also written in
 // per-lane tile order for the bias-table gradient (lrce_wattn_dbias sums it over windows).
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 #include "lrce_capi.h"
 
@@ -99,6 +102,8 @@ __global__ void bias_build_kernel(const float* table, const int64_t* index, int 
   const long long total = (long long)n_pat * nH * PH_ELEMS;
   if (e >= total) return;
   const int reg = e & 15, lane = (e >> 4) & 63;
+  const int et = e % TILE_ELEMS;                                   // forward tiles: [u][lane][4]
+  const int lane_f = (et >> 2) & 63, reg_f = 4 * (et >> 8) + (et & 3);
   const int tile = (e / TILE_ELEMS) % (NTILE * NTILE);
   const int ph = e / PH_ELEMS;
   const int h = ph % nH, pat = ph / nH;
@@ -111,9 +116,9 @@ __global__ void bias_build_kernel(const float* table, const int64_t* index, int 
     if (rg && rg[i] != rg[j]) v += -100.0f;
     return v * LOG2E;
   };
-  const int hh = lane >> 5, col = lane & 31;
   // forward: S^T tile (rows = keys, cols = queries)
-  bf[e] = val(qt * TQ + col, kt * TQ + crow(reg, hh));
+  bf[e] = val(qt * TQ + (lane_f & 31), kt * TQ + crow(reg_f, lane_f >> 5));
+  const int hh = lane >> 5, col = lane & 31;
   // backward: S tile (rows = queries, cols = keys)
   bb[e] = val(qt * TQ + crow(reg, hh), kt * TQ + col);
 }
@@ -124,7 +129,9 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd_kernel(const bf16* __restric
                                                            float* __restrict__ lse, int n_win, int n, int nH) {
   __shared__ __attribute__((aligned(16))) bf16 vimg_all[4][NPAD * HD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int w = blockIdx.x * 4 + wave, h = blockIdx.y;
+  // head-fastest block order: the nH blocks of a window group run together and share the 128-B
+  // lines of the qkv rows (each head reads a 64-B slice) in L2
+  const int w = (blockIdx.x / nH) * 4 + wave, h = blockIdx.x % nH;
   if (w >= n_win) return;
   const int C = nH * HD;
   const long long ld = 3LL * C;
@@ -146,7 +153,7 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd_kernel(const bf16* __restric
   }
   wave_lds_fence();
   const int pat = win_pat ? win_pat[w] : 0;
-  const float* bp = biasf + (long long)(pat * nH + h) * PH_ELEMS + lane * 16;
+  const float* bp = biasf + (long long)(pat * nH + h) * PH_ELEMS;
 
   for (int qt = 0; qt < NTILE; ++qt) {
     if (qt * TQ >= n) break;
@@ -161,10 +168,11 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd_kernel(const bf16* __restric
     f32x16 acc[NTILE];
 #pragma unroll
     for (int kt = 0; kt < NTILE; ++kt) {
-      const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + kt) * TILE_ELEMS);
+      // forward bias tiles are stored register-group-major ([u][lane][4]): each load is 1 KB contiguous
+      const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + kt) * TILE_ELEMS) + lane;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float4 b = src[u];
+        const float4 b = src[64 * u];
         acc[kt][4 * u] = b.x; acc[kt][4 * u + 1] = b.y; acc[kt][4 * u + 2] = b.z; acc[kt][4 * u + 3] = b.w;
       }
       acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][0], qf[0], acc[kt], 0, 0, 0);
@@ -181,7 +189,7 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd_kernel(const bf16* __restric
     for (int kt = 0; kt < NTILE; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(acc[kt][r] - m);
+        const float p = __builtin_amdgcn_exp2f(acc[kt][r] - m);
         acc[kt][r] = p;
         sum += p;
       }
@@ -209,6 +217,274 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd_kernel(const bf16* __restric
   }
 }
 
+// ------------------------------------------------------------------------------ forward, v2
+// One workgroup per (window, head), one wave per 32-query tile (5 waves, 320 threads): 5x the
+// waves of a wave-per-window kernel in flight, so the L2 latency of the bias tiles (issued first,
+// straight into the accumulators) and of the Q/K/V rows overlaps across waves instead of stalling
+// every query tile of one wave.  K and V are staged once per workgroup in LDS (K rows XOR-swizzled
+// by 16-B chunk for conflict-free row reads, V plain for the transposed reads of O^T = V^T P^T).
+__device__ __forceinline__ int kswz(int row, int chunk) { return row * HD + ((chunk ^ ((row >> 2) & 3)) << 3); }
+
+__global__ void __launch_bounds__(320, 3) wattn_fwd2_kernel(const bf16* __restrict__ qkv, const float* __restrict__ biasf,
+                                                            const int* __restrict__ win_pat, bf16* __restrict__ out,
+                                                            float* __restrict__ lse, int n_win, int n, int nH) {
+  __shared__ __attribute__((aligned(16))) bf16 kimg[NPAD * HD];
+  __shared__ __attribute__((aligned(16))) bf16 vimg[NPAD * HD];
+  const int lane = threadIdx.x & 63, qt = threadIdx.x >> 6;
+  // head-fastest over an XCD-contiguous block order: a window's heads run on one XCD and share the
+  // 128-B lines of its qkv rows (each head reads a 64-B slice) in that XCD's L2
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int h = lin % nH, w = lin / nH;
+  const int C = nH * HD;
+  const long long ld = 3LL * C;
+  const bf16* base = qkv + (long long)w * n * ld;
+  const int pat = win_pat ? win_pat[w] : 0;
+  // 1. this wave's 5 bias tiles -> accumulators (register-group-major tiles: 1 KB per load)
+  f32x16 acc[NTILE];
+  {
+    const float4* src = reinterpret_cast<const float4*>(biasf + (long long)(pat * nH + h) * PH_ELEMS +
+                                                        (long long)qt * NTILE * TILE_ELEMS) + lane;
+#pragma unroll
+    for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 b = src[kt * (TILE_ELEMS / 4) + 64 * u];
+        acc[kt][4 * u] = b.x; acc[kt][4 * u + 1] = b.y; acc[kt][4 * u + 2] = b.z; acc[kt][4 * u + 3] = b.w;
+      }
+  }
+  // 2. Q fragments of this wave's query tile
+  const int hh = lane >> 5, r32 = lane & 31;
+  const int qi = qt * TQ + r32;
+  bf16x8 qf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) qf[s] = qi < n ? ld_row16(base + qi * ld + h * HD + 16 * s + 8 * hh) : bf16x8{};
+  // 3. K, V rows [0,160) -> LDS (zero past n): 2 x 640 16-B chunks over 320 threads
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int c = threadIdx.x + 320 * t;
+    const int row = c >> 2, part = c & 3;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (row < n) {
+      kv = *reinterpret_cast<const uint4*>(base + row * ld + C + h * HD + part * 8);
+      vv = *reinterpret_cast<const uint4*>(base + row * ld + 2 * C + h * HD + part * 8);
+    }
+    *reinterpret_cast<uint4*>(kimg + kswz(row, part)) = kv;
+    *reinterpret_cast<uint4*>(vimg + row * HD + part * 8) = vv;
+  }
+  __syncthreads();
+  // 4. S^T = K Q^T (+ bias): rows = keys, cols = queries
+#pragma unroll
+  for (int kt = 0; kt < NTILE; ++kt) {
+    const int key = kt * TQ + r32;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kimg + kswz(key, 2 * s + hh));
+      acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], acc[kt], 0, 0, 0);
+    }
+  }
+  // 5. softmax over keys (in-lane + one cross-half exchange), exp2 domain (q pre-scaled by log2 e)
+  float m = NEG_BIG;
+#pragma unroll
+  for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[kt][r]);
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(acc[kt][r] - m);
+      acc[kt][r] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  // 6. O^T = V^T P^T
+  f32x16 o = {};
+#pragma unroll
+  for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(vimg, kt * TQ + 16 * s, lane), pack8(acc[kt], s), o, 0, 0, 0);
+  if (qi < n) {
+    const float inv = 1.0f / sum;
+    bf16* dst = out + ((long long)w * n + qi) * C + h * HD + 4 * hh;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      bf16x4 v;
+      v[0] = f2bf(o[4 * rr] * inv); v[1] = f2bf(o[4 * rr + 1] * inv);
+      v[2] = f2bf(o[4 * rr + 2] * inv); v[3] = f2bf(o[4 * rr + 3] * inv);
+      *reinterpret_cast<bf16x4*>(dst + 8 * rr) = v;
+    }
+    if (hh == 0) lse[((long long)w * nH + h) * NPAD + qi] = m + __log2f(sum);
+  }
+}
+
+// ------------------------------------------------------------------------------ forward, grouped
+// Four windows of ONE (mask pattern, head) per workgroup, one wave each: the 20 KB bias row of the
+// current query tile is staged ONCE per workgroup in LDS (LDS-DMA, prefetched one query tile
+// ahead) instead of being re-read from L2 by every window, and every operand of the loop body comes
+// from LDS or registers filled a tile ahead (V and the next Q tile by LDS-DMA), so no wave stalls on
+// a global load inside the loop.  Windows are grouped by pattern on the host (win_list, -1 = empty
+// slot; grp_pat = the group's pattern); unshifted stages use the identity grouping.
+constexpr int GW = 4;                         // windows (waves) per workgroup
+constexpr int BIAS_ROW = NTILE * TILE_ELEMS;  // floats of one query tile's bias row (20 KB)
+
+struct Fwd3Lds {
+  float bias[BIAS_ROW];
+  bf16 v[GW][NPAD * HD];
+  bf16 q[GW][2][TQ * HD];
+};
+
+__device__ __forceinline__ void glds16w(const void* src, void* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (LRCE_LDS void*)lds_dst, 16, 0, 0);
+}
+// The same LDS-DMA hidden from hipcc's wait bookkeeping (cdna_hip_programming.md §5.7): a builtin DMA
+// in flight makes hipcc drain vmcnt(0) before every later LDS read, which would serialize the
+// prefetch with the PV reads of V.  Completion is ordered by the loop's own vmcnt(0) + s_barrier.
+__device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)((LRCE_LDS const void*)p); }
+__device__ __forceinline__ void glds16_asm(const void* src, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+}
+
+__global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restrict__ qkv, const float* __restrict__ biasf,
+                                                            const int* __restrict__ win_list, const int* __restrict__ grp_pat,
+                                                            bf16* __restrict__ out, float* __restrict__ lse, int n_win, int n,
+                                                            int nH) {
+  __shared__ __attribute__((aligned(16))) Fwd3Lds S;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);   // a group's heads run on one XCD (shared qkv lines)
+  const int h = lin % nH, g = lin / nH;
+  const int wraw = win_list ? win_list[g * GW + wave] : g * GW + wave;
+  const bool valid = wraw >= 0 && wraw < n_win;
+  const int w = valid ? wraw : 0;
+  const int pat = grp_pat ? grp_pat[g] : 0;
+  const int C = nH * HD;
+  const long long ld = 3LL * C;
+  const bf16* base = qkv + (long long)w * n * ld;
+  const float* bias_ph = biasf + (long long)(pat * nH + h) * PH_ELEMS;
+  const int hh = lane >> 5, r32 = lane & 31;
+
+  // LDS-DMA issue helpers (lane-linear destinations, 1 KB per wave-instruction); ASM: hidden from hipcc
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  auto issue_bias = [&](int qt, auto asm_c) {   // 20 x 1 KB, 5 per wave
+    const float* src = bias_ph + (long long)qt * BIAS_ROW;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int ins = wv * 5 + i;
+      if constexpr (decltype(asm_c)::value) glds16_asm(src + ins * 256 + lane * 4, lds_u32(S.bias + ins * 256));
+      else glds16w(src + ins * 256 + lane * 4, S.bias + ins * 256);
+    }
+  };
+  auto issue_q = [&](int qt, auto asm_c) {      // 32 rows x 64 B = 2 x 1 KB, chunks XOR-swizzled by row (kswz)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = i * 16 + (lane >> 2), pos = lane & 3;
+      const int c = pos ^ ((row >> 2) & 3);
+      const int tok = min(qt * TQ + row, n - 1);
+      if constexpr (decltype(asm_c)::value) glds16_asm(base + tok * ld + h * HD + c * 8, lds_u32(&S.q[wv][qt & 1][i * 512]));
+      else glds16w(base + tok * ld + h * HD + c * 8, &S.q[wv][qt & 1][i * 512]);
+    }
+  };
+  constexpr std::false_type BUILTIN{};
+  constexpr std::true_type ASM{};
+
+  // prologue: bias row 0 (whole workgroup), this wave's V image and Q tile 0, K fragments
+  issue_bias(0, BUILTIN);
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < NPAD / 16; ++i) {       // V rows 16i .. 16i+15, rows >= n clamped (never weighted)
+      const int tok = min(i * 16 + (lane >> 2), n - 1);
+      glds16w(base + tok * ld + 2 * C + h * HD + (lane & 3) * 8, &S.v[wave][i * 512]);
+    }
+    issue_q(0, BUILTIN);
+  }
+  bf16x8 kf[NTILE][2];
+#pragma unroll
+  for (int kt = 0; kt < NTILE; ++kt) {
+    const int key = kt * TQ + r32;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) kf[kt][s] = (valid && key < n) ? ld_row16(base + key * ld + C + h * HD + 16 * s + 8 * hh) : bf16x8{};
+  }
+
+  for (int qt = 0; qt < NTILE; ++qt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA for tile qt (and its stores)
+    __builtin_amdgcn_s_barrier();                        // ... and every other wave's part of the bias row
+    f32x16 acc[NTILE];
+    {
+      const float4* src = reinterpret_cast<const float4*>(S.bias) + lane;
+#pragma unroll
+      for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 b = src[kt * (TILE_ELEMS / 4) + 64 * u];
+          acc[kt][4 * u] = b.x; acc[kt][4 * u + 1] = b.y; acc[kt][4 * u + 2] = b.z; acc[kt][4 * u + 3] = b.w;
+        }
+    }
+    bf16x8 qf[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(&S.q[wave][qt & 1][kswz(r32, 2 * s + hh)]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                        // bias row consumed by every wave: refill it
+    if (qt + 1 < NTILE) {
+      issue_bias(qt + 1, ASM);
+      if (valid) issue_q(qt + 1, ASM);
+    }
+    if (valid) {
+      const int qi = qt * TQ + r32;
+#pragma unroll
+      for (int kt = 0; kt < NTILE; ++kt) {
+        acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][0], qf[0], acc[kt], 0, 0, 0);
+        acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][1], qf[1], acc[kt], 0, 0, 0);
+      }
+      // softmax over keys.  Row max: 4 independent v_max3 chains + the cross-half exchange.  When
+      // every row max of the wave lies in [-64, 64] (always, short of pathological logits) the
+      // exponent needs no shift: exp2(s) / sum exp2(s) == exp2(s - m) / sum exp2(s - m), and f32
+      // exp2 of [-inf, 64] neither overflows nor loses a row to underflow.
+      float mp[4] = {NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};
+#pragma unroll
+      for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mp[r & 3] = fmaxf(mp[r & 3], acc[kt][r]);
+      float m = fmaxf(fmaxf(mp[0], mp[1]), fmaxf(mp[2], mp[3]));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      if (__all(m <= 64.f && m >= -64.f)) m = 0.f;
+      float sp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(acc[kt][r] - m);
+          acc[kt][r] = p;
+          sp[r & 3] += p;
+        }
+      float sum = (sp[0] + sp[1]) + (sp[2] + sp[3]);
+      sum += __shfl_xor(sum, 32, 64);
+      f32x16 o = {};
+      const bf16* vimg = S.v[wave];
+#pragma unroll
+      for (int kt = 0; kt < NTILE; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(vimg, kt * TQ + 16 * s, lane), pack8(acc[kt], s), o, 0, 0, 0);
+      if (qi < n) {
+        const float inv = 1.0f / sum;
+        bf16* dst = out + ((long long)w * n + qi) * C + h * HD + 4 * hh;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          bf16x4 v;
+          v[0] = f2bf(o[4 * rr] * inv); v[1] = f2bf(o[4 * rr + 1] * inv);
+          v[2] = f2bf(o[4 * rr + 2] * inv); v[3] = f2bf(o[4 * rr + 3] * inv);
+          *reinterpret_cast<bf16x4*>(dst + 8 * rr) = v;
+        }
+        if (hh == 0) lse[((long long)w * nH + h) * NPAD + qi] = m + __log2f(sum);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ backward
 struct BwdLds {
   bf16 q[NPAD * HD];
@@ -226,7 +502,7 @@ __global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restric
                                                            int n_win, int n, int nH, float scale) {
   __shared__ __attribute__((aligned(16))) BwdLds L_all[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int w = blockIdx.x * 2 + wave, h = blockIdx.y;
+  const int w = (blockIdx.x / nH) * 2 + wave, h = blockIdx.x % nH;   // head-fastest (see the forward)
   if (w >= n_win) return;
   BwdLds& L = L_all[wave];
   const int C = nH * HD;
@@ -308,7 +584,7 @@ __global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restric
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int qi = qt * TQ + crow(r, hh);
-            const float p = exp2f(sacc[r] - L.lse[qi]);
+            const float p = __builtin_amdgcn_exp2f(sacc[r] - L.lse[qi]);
             sacc[r] = p;
             dp[r] = p * (dp[r] - L.delta[qi]);
           }
@@ -435,10 +711,28 @@ extern "C" int lrce_wattn_fwd(const uint16_t* qkv, const float* bias_fwd, const 
   if (!qkv || !bias_fwd || !out || !lse) return lrce_fail(LRCE_E_ARG, "wattn_fwd: null pointer");
   if (n <= 4 * TQ || n > NPAD) return lrce_fail(LRCE_E_ARG, "wattn_fwd: n=%d outside (128,160]", n);
   if (n_win <= 0) return LRCE_OK;
-  dim3 grid((n_win + 3) / 4, nH);
-  wattn_fwd_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const bf16*>(qkv), bias_fwd, win_pat,
-                                                                      reinterpret_cast<bf16*>(out), lse, n_win, n, nH);
+  static const bool v1 = getenv("LRCE_WATTN_V1") != nullptr;
+  if (v1) {
+    dim3 grid((unsigned)(((n_win + 3) / 4) * nH));
+    wattn_fwd_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const bf16*>(qkv), bias_fwd, win_pat,
+                                                                        reinterpret_cast<bf16*>(out), lse, n_win, n, nH);
+  } else {
+    wattn_fwd2_kernel<<<(unsigned)(n_win * nH), 320, 0, static_cast<hipStream_t>(stream)>>>(
+        reinterpret_cast<const bf16*>(qkv), bias_fwd, win_pat, reinterpret_cast<bf16*>(out), lse, n_win, n, nH);
+  }
   return lrce_check_launch("wattn_fwd");
+}
+
+extern "C" int lrce_wattn_fwd_grouped(const uint16_t* qkv, const float* bias_fwd, const int32_t* win_list,
+                                      const int32_t* grp_pat, int n_groups, uint16_t* out, float* lse, int n_win, int n,
+                                      int nH, void* stream) {
+  if (!qkv || !bias_fwd || !out || !lse) return lrce_fail(LRCE_E_ARG, "wattn_fwd_grouped: null pointer");
+  if (n <= 4 * TQ || n > NPAD) return lrce_fail(LRCE_E_ARG, "wattn_fwd_grouped: n=%d outside (128,160]", n);
+  if (!win_list && n_groups * GW < n_win) return lrce_fail(LRCE_E_ARG, "wattn_fwd_grouped: %d groups < %d windows", n_groups, n_win);
+  if (n_win <= 0 || n_groups <= 0) return LRCE_OK;
+  wattn_fwd3_kernel<<<(unsigned)(n_groups * nH), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      reinterpret_cast<const bf16*>(qkv), bias_fwd, win_list, grp_pat, reinterpret_cast<bf16*>(out), lse, n_win, n, nH);
+  return lrce_check_launch("wattn_fwd_grouped");
 }
 
 extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
@@ -447,7 +741,7 @@ extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const ui
   if (!qkv || !out || !dout || !lse || !bias_bwd || !dqkv || !ds_scratch) return lrce_fail(LRCE_E_ARG, "wattn_bwd: null pointer");
   if (n <= 4 * TQ || n > NPAD) return lrce_fail(LRCE_E_ARG, "wattn_bwd: n=%d outside (128,160]", n);
   if (n_win <= 0) return LRCE_OK;
-  dim3 grid((n_win + 1) / 2, nH);
+  dim3 grid((unsigned)(((n_win + 1) / 2) * nH));
   const float scale = 1.0f / sqrtf((float)HD);
   wattn_bwd_kernel<<<grid, 128, 0, static_cast<hipStream_t>(stream)>>>(
       reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const bf16*>(out), reinterpret_cast<const bf16*>(dout), lse, bias_bwd,

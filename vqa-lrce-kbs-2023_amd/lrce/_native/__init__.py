@@ -85,6 +85,7 @@ _SIGS = {
     "lrce_scale_cast_bf16": [_P, _I64, _I, _P, _I, _P, _P],
     "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _P, _P],
     "lrce_wattn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lrce_wattn_fwd_grouped": [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_dbias": [_P, _I, _I, _I, _P, _I, _P, _P],
     "lrce_mha_fwd": [ctypes.POINTER(MhaDesc), _P],

@@ -69,6 +69,8 @@ class StageGeometry:
             self.win2sp_shift = self._win_map(ss, device)
             self.sp2win_shift = self._inverse(self.win2sp_shift)
             self.region, self.win_pat, self.n_pat = self._mask_patterns(device)
+            self.groups_shift = K.wattn_groups(self.win_pat, self.n_win, device)
+        self.groups = K.wattn_groups(None, self.n_win, device)
         self.merge_map = self._merge_map(device) if (H % 2 == 0 and W % 2 == 0) else None
 
     def _win_map(self, shift, device):
@@ -274,7 +276,7 @@ class _SwinBlockFn(torch.autograd.Function):
         qkv = K.linear(xw, flat.w16(at.qkv.weight), at.qkv.bias, scale_cols=C, scale_val=c)
         o = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
         lse = torch.empty(geo.n_win, nH, 160, device=dev)
-        K.wattn_fwd(qkv, bias_f, win_pat, o, lse, geo.n_win, n, nH)
+        K.wattn_fwd_grouped(qkv, bias_f, geo.groups_shift if shifted else geo.groups, o, lse, geo.n_win, n, nH)
         x_mid = torch.empty(M, C, device=dev)
         K.linear(o, flat.w16(at.proj.weight), at.proj.bias, out=x_mid, resid=x, c_map=wmap, row_scale=dp1,
                  rows_per_scale=geo.rows_per_clip)

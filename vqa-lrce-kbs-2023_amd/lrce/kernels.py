@@ -265,11 +265,40 @@ def wattn_fwd(qkv, bias_fwd, win_pat, out, lse, n_win, n, nH):
            flops=4.0 * n * n * 32 * n_win * nH)
 
 
+WATTN_GROUP = 4   # windows per workgroup of lrce_wattn_fwd_grouped
+
+
+def wattn_groups(win_pat, n_win, device):
+    """Group windows by mask pattern, WATTN_GROUP per group (lrce_wattn_fwd_grouped): returns
+    (win_list int32 [n_groups*G] with -1 in empty slots | None for the identity, grp_pat | None, n_groups)."""
+    G = WATTN_GROUP
+    if win_pat is None:
+        return None, None, (n_win + G - 1) // G
+    wp = win_pat.detach().to("cpu", torch.int64)
+    lists, pats = [], []
+    for pat in torch.unique(wp).tolist():
+        ids = torch.nonzero(wp == pat).flatten()
+        pad = (-ids.numel()) % G
+        ids = torch.cat([ids, torch.full((pad,), -1, dtype=torch.int64)])
+        lists.append(ids)
+        pats += [pat] * (ids.numel() // G)
+    win_list = torch.cat(lists).to(torch.int32).to(device)
+    grp_pat = torch.tensor(pats, dtype=torch.int32).to(device)
+    return win_list, grp_pat, len(pats)
+
+
+def wattn_fwd_grouped(qkv, bias_fwd, groups, out, lse, n_win, n, nH):
+    win_list, grp_pat, n_groups = groups
+    _timed("wattn_fwd", out, lambda: call("lrce_wattn_fwd_grouped", ptr(qkv), ptr(bias_fwd), ptr(win_list), ptr(grp_pat),
+                                           n_groups, ptr(out), ptr(lse), n_win, n, nH, stream_of(out)),
+           flops=4.0 * n * n * 32 * n_win * nH, key=(n_win, nH))
+
+
 def wattn_bwd(qkv, out, dout, lse, bias_bwd, win_pat, dqkv, ds, n_win, n, nH):
     # algorithmic work: dV, dP, dQ, dK = 8 n^2 d per (window, head)
     _timed("wattn_bwd", dqkv, lambda: call("lrce_wattn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(bias_bwd),
                                             ptr(win_pat), ptr(dqkv), ptr(ds), n_win, n, nH, stream_of(dqkv)),
-           flops=8.0 * n * n * 32 * n_win * nH)
+           flops=8.0 * n * n * 32 * n_win * nH, key=(n_win, nH))
 
 
 def wattn_ds_elems(n_win, nH):
