@@ -10,7 +10,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblrce_hip.so")
+LIB_PATH = os.environ.get("LRCE_NATIVE_LIB") or os.path.join(_HERE, "liblrce_hip.so")   # override: A/B dev builds
 
 _lib = None
 
