@@ -502,7 +502,8 @@ __global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restric
                                                            int n_win, int n, int nH, float scale) {
   __shared__ __attribute__((aligned(16))) BwdLds L_all[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int w = (blockIdx.x / nH) * 2 + wave, h = blockIdx.x % nH;   // head-fastest (see the forward)
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);   // a window pair's heads on one XCD (shared qkv/dO lines)
+  const int w = (lin / nH) * 2 + wave, h = lin % nH;
   if (w >= n_win) return;
   BwdLds& L = L_all[wave];
   const int C = nH * HD;
@@ -513,6 +514,7 @@ __global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restric
   stage_img(L.q, base + h * HD, ld, n, lane);
   stage_img(L.k, base + C + h * HD, ld, n, lane);
   stage_img(L.dout, dobase, C, n, lane);
+  wave_lds_fence();
   const float* lsep = lse_g + ((long long)w * nH + h) * NPAD;
   for (int qi = lane; qi < NPAD; qi += 64) {
     float d = 0.f, l = 0.f;
@@ -520,7 +522,7 @@ __global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restric
 #pragma unroll
       for (int part = 0; part < 4; ++part) {
         const bf16x8 a = ld_row16(obase + qi * C + part * 8);
-        const bf16x8 b = ld_row16(dobase + qi * C + part * 8);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(L.dout + qi * HD + part * 8);   // staged dO row
 #pragma unroll
         for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
       }
@@ -551,7 +553,7 @@ __global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restric
       for (int s = 0; s < 2; ++s) {
         bf16x8 a = {}, b = {};
         if (key < n) {
-          a = ld_row16(base + key * ld + C + h * HD + 16 * s + 8 * hh);
+          a = *reinterpret_cast<const bf16x8*>(L.k + key * HD + 16 * s + 8 * hh);   // staged K row
           b = ld_row16(base + key * ld + 2 * C + h * HD + 16 * s + 8 * hh);
         }
         kf[s] = a;
