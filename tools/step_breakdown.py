@@ -36,8 +36,8 @@ def main():
     print(f"total timed {tot:.2f} ms/step over {sum(r[2] for r in rows)} launches")
     print(f"{'kernel':10s} {'M':>7s} {'N':>6s} {'K':>7s} {'bt':>3s} lay      sk flags calls   ms   TF/s")
     for name, key, n, t, tf in rows[:a.top]:
-        if key is None:
-            print(f"{name:10s} {'':48s} {n:5d} {t:6.3f} {tf:7.1f}")
+        if key is None or len(key) != 9:
+            print(f"{name:10s} {str(key or ''):48s} {n:5d} {t:6.3f} {tf:7.1f}")
             continue
         m, nn, k, b, la, lb, ad, sk, fl = key
         print(f"{name:10s} {m:7d} {nn:6d} {k:7d} {b:3d} {la}{lb}{ad} {sk:3d} {fl:5d} {n:5d} {t:6.3f} {tf:7.1f}")

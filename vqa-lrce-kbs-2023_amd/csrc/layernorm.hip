@@ -117,11 +117,44 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
   float4 aw[CH], ab[CH];  // dw/db partials of this lane's columns
 #pragma unroll
   for (int t = 0; t < CH; ++t) { aw[t] = make_float4(0.f, 0.f, 0.f, 0.f); ab[t] = aw[t]; }
-  for (int r0 = (blockIdx.x * 4 + wave) * RPW; r0 < rows; r0 += gridDim.x * 4 * RPW) {
+  // The raw operands of the NEXT row of this wave (x, dy, dres, stats) are fetched before the
+  // current row is reduced and written, so a wave keeps one row of loads in flight (large inputs
+  // run >= 8 rows per wave: without it each row is a full memory round trip).
+  const int stride = gridDim.x * 4 * RPW;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto fetch = [&](int rb, float4 (&xv)[CH], float4 (&dv)[CH], float4 (&rv)[CH], float& mu, float& rs) {
+    const int r = rb + lane / LPR;
+    const bool live = r < rows;
+    mu = live ? mean_i[r] : 0.f;
+    rs = live ? rstd_i[r] : 0.f;
+    const long long dyr = !live ? 0 : (dy_map ? (long long)dy_map[r] : (long long)r);
+#pragma unroll
+    for (int t = 0; t < CH; ++t) {
+      const int c = sl + LPR * t;
+      xv[t] = z4; dv[t] = z4; rv[t] = z4;
+      if (live && c < nch) {
+        int ok;
+        const long long o = src_off(in_map, nseg, seg, r, c, ok);
+        if (ok) {
+          xv[t] = ld4<TX>(x + o);
+          if (dres) rv[t] = *reinterpret_cast<const float4*>(dres + o);
+        }
+        dv[t] = ld4<TD>(dy + dyr * cols + 4 * c);
+      }
+    }
+  };
+  int r0 = (blockIdx.x * 4 + wave) * RPW;
+  float4 xcur[CH], dcur[CH], rcur[CH];
+  float mcur = 0.f, scur = 0.f;
+  if (r0 < rows) fetch(r0, xcur, dcur, rcur, mcur, scur);
+  for (; r0 < rows; r0 += stride) {
+    float4 xnx[CH], dnx[CH], rnx[CH];
+    float mnx = 0.f, snx = 0.f;
+    const bool more = r0 + stride < rows;
+    if (more) fetch(r0 + stride, xnx, dnx, rnx, mnx, snx);
     const int r = r0 + lane / LPR;
     const bool live = r < rows;
-    const float mean = live ? mean_i[r] : 0.f, rstd = live ? rstd_i[r] : 0.f;
-    const long long dyr = !live ? 0 : (dy_map ? (long long)dy_map[r] : (long long)r);
+    const float mean = mcur, rstd = scur;
     float4 xh[CH], g[CH];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -130,11 +163,9 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
       xh[t] = make_float4(0.f, 0.f, 0.f, 0.f);
       g[t] = xh[t];
       if (live && c < nch) {
-        int ok;
-        const long long o = src_off(in_map, nseg, seg, r, c, ok);
-        const float4 xv = ok ? ld4<TX>(x + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 xv = xcur[t];
         xh[t] = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd);
-        const float4 d = ld4<TD>(dy + dyr * cols + 4 * c);
+        const float4 d = dcur[t];
         const float4 ww = *reinterpret_cast<const float4*>(w + 4 * c);
         g[t] = make_float4(d.x * ww.x, d.y * ww.y, d.z * ww.z, d.w * ww.w);
         s1 += g[t].x + g[t].y + g[t].z + g[t].w;
@@ -157,7 +188,7 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
         out.z = rstd * (g[t].z - c1 - xh[t].z * c2);
         out.w = rstd * (g[t].w - c1 - xh[t].w * c2);
         if (dres) {
-          const float4 rr = *reinterpret_cast<const float4*>(dres + o);
+          const float4 rr = rcur[t];
           out.x += rr.x; out.y += rr.y; out.z += rr.z; out.w += rr.w;
         }
         *reinterpret_cast<float4*>(dx + o) = out;
@@ -167,6 +198,12 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
           st4<bf16>(dx16 + orow * cols + 4 * c, make_float4(out.x * f, out.y * f, out.z * f, out.w * f));
         }
       }
+    }
+    if (more) {
+#pragma unroll
+      for (int t = 0; t < CH; ++t) { xcur[t] = xnx[t]; dcur[t] = dnx[t]; rcur[t] = rnx[t]; }
+      mcur = mnx;
+      scur = snx;
     }
   }
   if (!dw && !db) return;
@@ -240,10 +277,13 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
   if (rows <= 0) return LRCE_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nch = cols / 4;
-  // >= 8 rows per wave keeps the per-block dw/db atomics small; <= 2048 blocks
+  // Rows per wave: small inputs (the decoder / BERT rows) get one row per wave (latency-bound: as
+  // many waves as rows); large ones >= 8 rows per wave and <= 2048 blocks, because every block adds
+  // its dw/db partials into the SAME 2 x cols addresses (contended atomics: more blocks is slower).
   auto blocks = [&](int lpr) {
-    const int rpb = 4 * (64 / lpr);
-    int nb = (rows + rpb * 8 - 1) / (rpb * 8);
+    const int rpb = 4 * (64 / lpr);                 // rows per block per pass
+    const int per_wave = rows <= 8192 ? 1 : 8;
+    int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
     return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
   };
 #define LNB3(TD, TX, CH, LPR)                                                                                          \

@@ -255,11 +255,6 @@ __global__ void __launch_bounds__(256) mha1_fwd_kernel(MhaP P) {
   }
 }
 
-__device__ __forceinline__ void rmw_add(float* p, float v, bool atomic) {
-  if (atomic) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p += v;
-}
-
 __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
   const LrceMhaDesc& d = P.d;
   __shared__ __attribute__((aligned(16))) float qs[D];
@@ -297,19 +292,44 @@ __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
   const float q = qs[lane], g = gs[lane];
   float dq0 = 0.f, dq1 = 0.f;
   const bool at1 = d.kv1_bdiv > 1, at2 = d.kv2_bdiv > 1;
-  for (int j = wave; j < Lk; j += 4) {
-    const float dsj = dss[j], pj = ps[j];
-    const bf16* kr = key_row(d, d.k1, d.k2, b, j, h);
-    if (j & 4) dq1 += dsj * bf2f(kr[lane]);
-    else dq0 += dsj * bf2f(kr[lane]);
-    if (j < d.lk1) {
-      const long long o = (long long)(b / d.kv1_bdiv) * d.stride_dkv1_b + (long long)j * d.ld_dkv1 + h * D + lane;
-      rmw_add(d.dk1 + o, dsj * q, at1);
-      rmw_add(d.dv1 + o, pj * g, at1);
-    } else {
-      const long long o = (long long)(b / d.kv2_bdiv) * d.stride_dkv2_b + (long long)(j - d.lk1) * d.ld_dkv2 + h * D + lane;
-      rmw_add(d.dk2 + o, dsj * q, at2);
-      rmw_add(d.dv2 + o, pj * g, at2);
+  // Keys in batches of UB per wave: every K-row load and dK/dV read of a batch is issued before its
+  // first store, so the read-modify-writes overlap instead of forming one serial memory round trip
+  // per key (single writer per row); rows shared by bdiv > 1 rows use no-return atomics.
+  constexpr int UB = 8;
+  for (int j0 = wave; j0 < Lk; j0 += 4 * UB) {
+    float kv[UB], okk[UB], ovv[UB];
+    float* pk[UB];
+    float* pv[UB];
+    bool at[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int j = min(j0 + 4 * u, Lk - 1);
+      kv[u] = bf2f(key_row(d, d.k1, d.k2, b, j, h)[lane]);
+      if (j < d.lk1) {
+        const long long o = (long long)(b / d.kv1_bdiv) * d.stride_dkv1_b + (long long)j * d.ld_dkv1 + h * D + lane;
+        pk[u] = d.dk1 + o; pv[u] = d.dv1 + o; at[u] = at1;
+      } else {
+        const long long o = (long long)(b / d.kv2_bdiv) * d.stride_dkv2_b + (long long)(j - d.lk1) * d.ld_dkv2 + h * D + lane;
+        pk[u] = d.dk2 + o; pv[u] = d.dv2 + o; at[u] = at2;
+      }
+      okk[u] = at[u] ? 0.f : *pk[u];
+      ovv[u] = at[u] ? 0.f : *pv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int j = j0 + 4 * u;
+      if (j < Lk) {
+        const float dsj = dss[j], pj = ps[j];
+        if (u & 1) dq1 += dsj * kv[u];
+        else dq0 += dsj * kv[u];
+        if (at[u]) {
+          __hip_atomic_fetch_add(pk[u], dsj * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(pv[u], pj * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          *pk[u] = okk[u] + dsj * q;
+          *pv[u] = ovv[u] + pj * g;
+        }
+      }
     }
   }
   part[wave][lane] = dq0 + dq1;

@@ -240,10 +240,29 @@ class _PatchEmbedFn(torch.autograd.Function):
 
 
 def _drop_path_scale(rate, nc, device, training):
+    """timm DropPath (video_swin_ori.py:243,299): per-sample keep mask / keep_prob, here per clip."""
     if not training or rate <= 0.0:
         return None
     keep = 1.0 - rate
     return torch.floor(keep + torch.rand(nc, device=device)) / keep
+
+
+_KEEP_CACHE = {}
+
+
+def _drop_path_scales(swin, nc, device):
+    """Both DropPath scale vectors of every block of one forward, drawn in ONE batch (4 launches per
+    step instead of 4 per DropPath): [(dp1, dp2) per block] or None in eval mode.  Blocks whose rate
+    is 0 (the first, linspace(0, 0.2, 24)[0]) get None, as in _drop_path_scale."""
+    if not swin.training:
+        return None
+    rates = [blk.drop_path for layer in swin.layers for blk in layer.blocks]
+    key = (tuple(rates), str(device))
+    keep = _KEEP_CACHE.get(key)
+    if keep is None:
+        keep = _KEEP_CACHE[key] = torch.tensor([[1.0 - r] for r in rates for _ in range(2)], device=device)
+    s = torch.floor(keep + torch.rand(len(rates) * 2, nc, device=device)) / keep
+    return [(s[2 * i], s[2 * i + 1]) if r > 0.0 else (None, None) for i, r in enumerate(rates)]
 
 
 def _wgrad(flat, lin, dy16, x16):
@@ -423,11 +442,13 @@ class SwinTransformer3D(nn.Module):
             B, _, T, H, W = clips.shape
             nc = B
         D, H, W = (T + 1) // 2, H // 4, W // 4
+        scales = _drop_path_scales(self, nc, dev)
+        bi = 0
         for layer in self.layers:
             geo = stage_geometry(nc, D, H, W, self.window_size, dev)
             for blk in layer.blocks:
-                dp1 = _drop_path_scale(blk.drop_path, nc, dev, self.training)
-                dp2 = _drop_path_scale(blk.drop_path, nc, dev, self.training)
+                dp1, dp2 = scales[bi] if scales is not None else (None, None)
+                bi += 1
                 x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, *blk.parameters())
             if layer.downsample is not None:
                 x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())

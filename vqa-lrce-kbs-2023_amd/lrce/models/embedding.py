@@ -89,13 +89,15 @@ class VideoEmbedFn(torch.autograd.Function):
                for g, t in zip(gs, (pe.emb_cls, pe.emb_pos, pe.emb_len, pe.emb_clip))]
         K.video_posembed_bwd(dz, dy, tmp[0], tmp[1], tmp[2], tmp[3], B, S, Tg, P, C)
         if proj is not None:
-            gw = _g(flat, proj.weight)
+            # the projection's backward GEMMs read a bf16 copy of dy (LDS-DMA MFMA path); the bias
+            # gradient rides in the weight-gradient GEMM
+            dy16 = K.scale_cast_bf16(dy)
+            gw, gb = _g(flat, proj.weight), _g(flat, proj.bias)
             if gw is not None:
-                K.linear_dw(dy, vf16, gw)
-            gb = _g(flat, proj.bias)
-            if gb is not None:
-                K.colsum(dy, gb)
-            dvf = K.linear_dx(dy, flat.w16(proj.weight))
+                K.linear_dw(dy16, vf16, gw, bias_grad=gb)
+            elif gb is not None:
+                K.colsum(dy16, gb)
+            dvf = K.linear_dx(dy16, flat.w16(proj.weight))
         else:
             dvf = dy
         ctx.save = None
