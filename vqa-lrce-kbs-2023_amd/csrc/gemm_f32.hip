@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p) {
   }
 }
 
-// C[m][n] (+)= alpha * sum_{r < R} A[r][m] * B[r][n] with R <= 64 (dW of a skinny linear):
+// C[m][n] (+)= alpha * sum_{r < R} A[r][m] * B[r][n] with R <= 256 (dW of a skinny linear):
 // one thread per 4 consecutive columns, the R-term outer-product sum in registers, one RMW.
 __global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
   const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -281,9 +281,9 @@ __global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
 
 }  // namespace
 
-// the dW shape the outer-product kernel takes: A M-major, B N-major, reduction <= 64 rows
+// the dW shape the outer-product kernel takes: A M-major, B N-major, reduction <= 256 rows
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d) {
-  return d->b_f32 && d->a_f32 && !d->a_kmajor && !d->b_kmajor && d->k <= 64 && (d->n % 4) == 0 && (d->ldc % 4) == 0 &&
+  return d->b_f32 && d->a_f32 && !d->a_kmajor && !d->b_kmajor && d->k <= 256 && (d->n % 4) == 0 && (d->ldc % 4) == 0 &&
          (d->ldb % 4) == 0 && d->batch == 1 && !d->a_map && !d->c_map && !d->a_row_scale && d->split_k <= 1 &&
          (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32 | LRCE_EPI_BIAS_GRAD)) == 0 &&
          (d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) && !d->row_scale && d->scale_cols == 0 &&

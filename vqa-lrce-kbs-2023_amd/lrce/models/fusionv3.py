@@ -102,21 +102,41 @@ class _Step:
                  "gd", "x3p", "m3", "r3")
 
 
-def _layer_fwd(lay, flat, x0, kvv, kvt, step, S, Lt, nmc, p, seed, save):
-    """One TransformerDecoderLayer (post-norm) on the summary-token rows x0 (Bq, E) f32.
+class _LayerActs:
+    """Per-layer [S, Bq, .] buffers of the query-side GEMM inputs of every recurrent step: the
+    forward writes step i's activations into row block i, so the weight gradients of all S steps
+    are ONE GEMM per weight after the backward sweep (K = S*Bq) instead of S small ones."""
+    __slots__ = ("x0", "sad", "x1", "ctx", "x2", "gd")
+
+    def __init__(self, S, Bq, dev):
+        for name in self.__slots__:
+            setattr(self, name, torch.empty(S, Bq, FF if name == "gd" else E, device=dev))
+
+
+class _LayerGrads:
+    """Per-layer [S, Bq, .] buffers of the matching output gradients (dY of each query-side GEMM)."""
+    __slots__ = ("df", "dgp", "dcao", "dq", "dsao", "dsav")
+
+    def __init__(self, S, Bq, dev):
+        for name in self.__slots__:
+            setattr(self, name, torch.empty(S, Bq, FF if name == "dgp" else E, device=dev))
+
+
+def _layer_fwd(lay, flat, x0, kvv, kvt, step, S, Lt, nmc, p, seed, save, acts, x3_out=None):
+    """One TransformerDecoderLayer (post-norm) on the summary-token rows x0 (Bq, E) f32 (= acts.x0[step]).
     Query-side linears run on the exact-f32 MFMA path with the f32 master weights (M = Bq is tiny,
     the recurrence is precision-critical); only the memory K/V (big-M GEMMs) are bf16."""
     sa, ca = lay.self_attn, lay.multihead_attn
     # self-attention over one token: out_proj(dropout_head(v_proj(x)))
-    sad = K.linear(x0, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out_f32=True)
+    sad = K.linear(x0, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step])
     K.dropout(sad, p, seed, out=sad, group=E // NHEAD)
     sao = K.linear(sad, sa.out_proj.weight, sa.out_proj.bias, out_f32=True)
     x1p = K.dropout(sao, p, seed + 1, res=x0)
-    x1, m1, r1 = K.layernorm(x1p, lay.norm1.weight, lay.norm1.bias, EPS, out_f32=True)
+    x1, m1, r1 = K.layernorm(x1p, lay.norm1.weight, lay.norm1.bias, EPS, out=acts.x1[step])
     # cross-attention to [video tokens of this step ; question tokens]
     q = K.linear(x1, ca.in_proj_weight[:E], ca.in_proj_bias[:E], out_f32=True)
     Bq = x0.shape[0]
-    ctx = torch.empty(Bq, E, device=x0.device)
+    ctx = acts.ctx[step]
     lse = torch.empty(Bq, NHEAD, 1, device=x0.device)
     lv = 150
     kv1 = kvv[step * lv * 2 * E:]
@@ -126,14 +146,14 @@ def _layer_fwd(lay, flat, x0, kvv, kvt, step, S, Lt, nmc, p, seed, save):
     K.mha_fwd(desc, ctx)
     cao = K.linear(ctx, ca.out_proj.weight, ca.out_proj.bias, out_f32=True)
     x2p = K.dropout(cao, p, seed + 3, res=x1)
-    x2, m2, r2 = K.layernorm(x2p, lay.norm2.weight, lay.norm2.bias, EPS, out_f32=True)
+    x2, m2, r2 = K.layernorm(x2p, lay.norm2.weight, lay.norm2.bias, EPS, out=acts.x2[step])
     # FFN: linear2(dropout(gelu(linear1(x))))
     pre = torch.empty(Bq, FF, dtype=torch.bfloat16, device=x0.device)
-    gd = K.linear(x2, lay.linear1.weight, lay.linear1.bias, gelu=True, pre_out=pre, out_f32=True)
+    gd = K.linear(x2, lay.linear1.weight, lay.linear1.bias, gelu=True, pre_out=pre, out=acts.gd[step])
     K.dropout(gd, p, seed + 4, out=gd)
     f = K.linear(gd, lay.linear2.weight, lay.linear2.bias, out_f32=True)
     x3p = K.dropout(f, p, seed + 5, res=x2)
-    x3, m3, r3 = K.layernorm(x3p, lay.norm3.weight, lay.norm3.bias, EPS, out_f32=True)
+    x3, m3, r3 = K.layernorm(x3p, lay.norm3.weight, lay.norm3.bias, EPS, out=x3_out, out_f32=True)
     if save is not None:
         st = _Step()
         st.x0, st.sad, st.x1p, st.m1, st.r1, st.x1, st.q, st.ctx, st.lse, st.desc = \
@@ -143,41 +163,49 @@ def _layer_fwd(lay, flat, x0, kvv, kvt, step, S, Lt, nmc, p, seed, save):
     return x3
 
 
-def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed):
-    """Backward of _layer_fwd; accumulates into the layer's dK/dV buffers, returns d(x0)."""
+def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step):
+    """Backward of _layer_fwd; accumulates into the layer's dK/dV buffers and leaves the dY of its
+    six query-side GEMMs in grads[.][step] (weight gradients: _layer_wgrads), returns d(x0)."""
     sa, ca = lay.self_attn, lay.multihead_attn
-    Bq = dx3.shape[0]
     dx3p = torch.empty_like(st.x3p)
     K.layernorm_bwd(dx3, st.x3p, st.m3, st.r3, lay.norm3.weight, dx3p, dw=_g(flat, lay.norm3.weight),
                     db=_g(flat, lay.norm3.bias))
-    df = K.dropout_bwd(dx3p, p, seed + 5) if p > 0 else dx3p
-    _wgrad(flat, lay.linear2.weight, lay.linear2.bias, df, st.gd)
-    dgp = K.linear_dx(df, lay.linear2.weight, dgelu_pre=st.pre)
+    df = K.dropout_bwd(dx3p, p, seed + 5, out=grads.df[step])
+    dgp = K.linear_dx(df, lay.linear2.weight, dgelu_pre=st.pre, out=grads.dgp[step])
     if p > 0:
         K.dropout_bwd(dgp, p, seed + 4, out=dgp)
-    _wgrad(flat, lay.linear1.weight, lay.linear1.bias, dgp, st.x2)
     dx2 = K.linear_dx(dgp, lay.linear1.weight, resid=dx3p)
     dx2p = torch.empty_like(st.x2p)
     K.layernorm_bwd(dx2, st.x2p, st.m2, st.r2, lay.norm2.weight, dx2p, dw=_g(flat, lay.norm2.weight),
                     db=_g(flat, lay.norm2.bias))
-    dcao = K.dropout_bwd(dx2p, p, seed + 3) if p > 0 else dx2p
-    _wgrad(flat, ca.out_proj.weight, ca.out_proj.bias, dcao, st.ctx)
+    dcao = K.dropout_bwd(dx2p, p, seed + 3, out=grads.dcao[step])
     dctx = K.linear_dx(dcao, ca.out_proj.weight)
-    dq = torch.empty(Bq, E, device=dx3.device)
+    dq = grads.dq[step]
     K.mha_bwd(st.desc, dout=dctx, dq=dq, dk1=dkvv_step, dv1=dkvv_step[E:], ld_dkv1=2 * E,
               stride_dkv1_b=S * 150 * 2 * E, dk2=dkvt, dv2=dkvt[E:], ld_dkv2=2 * E, stride_dkv2_b=Lt * 2 * E)
-    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dq, st.x1, rows=(0, E))
     dx1 = K.linear_dx(dq, ca.in_proj_weight[:E], resid=dx2p)
     dx1p = torch.empty_like(st.x1p)
     K.layernorm_bwd(dx1, st.x1p, st.m1, st.r1, lay.norm1.weight, dx1p, dw=_g(flat, lay.norm1.weight),
                     db=_g(flat, lay.norm1.bias))
-    dsao = K.dropout_bwd(dx1p, p, seed + 1) if p > 0 else dx1p
-    _wgrad(flat, sa.out_proj.weight, sa.out_proj.bias, dsao, st.sad)
-    dsav = K.linear_dx(dsao, sa.out_proj.weight)
+    dsao = K.dropout_bwd(dx1p, p, seed + 1, out=grads.dsao[step])
+    dsav = K.linear_dx(dsao, sa.out_proj.weight, out=grads.dsav[step])
     if p > 0:
         K.dropout_bwd(dsav, p, seed, out=dsav, group=E // NHEAD)
-    _wgrad(flat, sa.in_proj_weight, sa.in_proj_bias, dsav, st.x0, rows=(2 * E, 3 * E))
     return K.linear_dx(dsav, sa.in_proj_weight[2 * E:], resid=dx1p)
+
+
+def _layer_wgrads(lay, flat, acts, grads):
+    """The six query-side weight (+bias) gradients of one layer over all S recurrent steps at once:
+    dW += dY[S*Bq, out]^T X[S*Bq, in] (one exact-f32 outer-product launch each)."""
+    sa, ca = lay.self_attn, lay.multihead_attn
+    R = acts.x0.shape[0] * acts.x0.shape[1]
+    v = lambda t: t.view(R, t.shape[-1])  # noqa: E731
+    _wgrad(flat, lay.linear2.weight, lay.linear2.bias, v(grads.df), v(acts.gd))
+    _wgrad(flat, lay.linear1.weight, lay.linear1.bias, v(grads.dgp), v(acts.x2))
+    _wgrad(flat, ca.out_proj.weight, ca.out_proj.bias, v(grads.dcao), v(acts.ctx))
+    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, v(grads.dq), v(acts.x1), rows=(0, E))
+    _wgrad(flat, sa.out_proj.weight, sa.out_proj.bias, v(grads.dsao), v(acts.sad))
+    _wgrad(flat, sa.in_proj_weight, sa.in_proj_bias, v(grads.dsav), v(acts.x0), rows=(2 * E, 3 * E))
 
 
 class _RecurrentDecoderFn(torch.autograd.Function):
@@ -198,7 +226,10 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             w = flat.w16(ca.in_proj_weight)[E:]
             kvv.append(K.linear(v16, w, ca.in_proj_bias[E:]))
             kvt.append(K.linear(t16, w, ca.in_proj_bias[E:]))
-        s = ft.summarization_token.detach().reshape(1, E).expand(Bq, E).contiguous()
+        nL = len(layers)
+        acts = [_LayerActs(S, Bq, dev) for _ in layers]
+        s = acts[0].x0[0]
+        s.copy_(ft.summarization_token.detach().reshape(1, E).expand(Bq, E))
         saves = []
         fused = []
         for i in range(S):
@@ -206,19 +237,20 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             step_saves = []
             for l, lay in enumerate(layers):
                 x = _layer_fwd(lay, flat, x, kvv[l].view(-1), kvt[l].view(-1), i, S, Lt, nmc, p,
-                               seed + 64 * (i * len(layers) + l), step_saves)
+                               seed + 64 * (i * nL + l), step_saves, acts[l],
+                               x3_out=acts[l + 1].x0[i] if l + 1 < nL else None)
             tsum = K.dropout(x, 0.0, 0, res=s)
             u, mu, ru = K.layernorm(tsum, ft.fusion_layer_norm.weight, ft.fusion_layer_norm.bias, EPS, out_f32=True)
-            s = K.dropout(u, p, seed + 7 + 64 * 1000 * (i + 1))
+            s = K.dropout(u, p, seed + 7 + 64 * 1000 * (i + 1), out=acts[0].x0[i + 1] if i + 1 < S else None)
             saves.append(step_saves)
             fused.append((tsum, mu, ru))
-        ctx.save = (kvv, kvt, saves, fused, v16, t16)
+        ctx.save = (kvv, kvt, saves, fused, v16, t16, acts)
         ctx.ft, ctx.flat, ctx.p, ctx.seed, ctx.dims = ft, flat, p, seed, (B, S, nmc, Bq, Lt)
         return s
 
     @staticmethod
     def backward(ctx, ds):
-        kvv, kvt, saves, fused, v16, t16 = ctx.save
+        kvv, kvt, saves, fused, v16, t16, acts = ctx.save
         ft, flat, p, seed = ctx.ft, ctx.flat, ctx.p, ctx.seed
         B, S, nmc, Bq, Lt = ctx.dims
         layers = ft.transformer.layers
@@ -226,6 +258,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         dkvv = [torch.zeros(B * S * 150, 2 * E, device=dev) for _ in layers]
         dkvt = [torch.zeros(Bq * Lt, 2 * E, device=dev) for _ in layers]
         ds = ds.contiguous()
+        grads = [_LayerGrads(S, Bq, dev) for _ in layers]
         for i in reversed(range(S)):
             tsum, mu, ru = fused[i]
             du = K.dropout_bwd(ds, p, seed + 7 + 64 * 1000 * (i + 1)) if p > 0 else ds
@@ -235,9 +268,12 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             dx = dt
             for l in reversed(range(len(layers))):
                 dx = _layer_bwd(layers[l], flat, saves[i][l], dx, dkvv[l].view(-1)[i * 150 * 2 * E:],
-                                dkvt[l].view(-1), S, Lt, p, seed + 64 * (i * len(layers) + l))
+                                dkvt[l].view(-1), S, Lt, p, seed + 64 * (i * len(layers) + l), grads[l], i)
             ds = K.dropout(dx, 0.0, 0, res=dt)   # s fed both the residual and the decoder
             saves[i] = None
+        for l, lay in enumerate(layers):
+            _layer_wgrads(lay, flat, acts[l], grads[l])
+        del grads, acts
         gt = _g(flat, ft.summarization_token)
         if gt is not None:
             K.colsum(ds, gt.view(E))
