@@ -116,7 +116,12 @@ int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map,
                        const float* mean, const float* rstd, const float* w,
                        float* dx, const float* dres, float* dw, float* db,
                        int rows, int cols, uint16_t* dx_bf16, const int32_t* dx_bf16_map,
-                       const float* dx_scale, int dx_scale_rps, void* stream);
+                       const float* dx_scale, int dx_scale_rps, float* workspace,
+                       int64_t workspace_elems, void* stream);
+/* f32 elements of the dw/db partials workspace lrce_layernorm_bwd uses for (rows, cols): with it
+ * the weight/bias gradients are a deterministic two-pass sum instead of same-address atomics from
+ * every block (a NULL or smaller workspace falls back to the atomics). */
+int64_t lrce_layernorm_bwd_workspace(int rows, int cols);
 
 /* ---------------------------------------------------------------- Swin 3D window attention
  * Replaces WindowAttention3D.forward video_swin_ori.py:164-186 (QK^T, relative-position bias,

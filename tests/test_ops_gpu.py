@@ -54,6 +54,23 @@ def test_gemm_layouts(M, N, Kd, a_km, b_km, a_f32):
     assert rel(C, ref) < 2e-3
 
 
+@pytest.mark.parametrize("M,N,Kd", [(17640, 512, 256), (17001, 520, 200)])
+@pytest.mark.parametrize("b_km", [1, 0])
+def test_gemm_tall_tiles(M, N, Kd, b_km):
+    """Shapes whose 128x128 grid overshoots one round of the chip: the 192x128 tile path (ragged M,
+    N and K tails included), with the bias + residual epilogue."""
+    k = K()
+    A = bf(torch.randn(M, Kd, device=dev))
+    B = bf(torch.randn(N, Kd, device=dev))
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    b_store = B.contiguous() if b_km else B.t().contiguous()
+    C = torch.empty(M, N, device=dev, dtype=torch.float32)
+    k.gemm(A, b_store, C, M, N, Kd, a_kmajor=True, b_kmajor=bool(b_km), flags=16 | 1 | 8, bias=bias, aux=res, ld_aux=N)
+    ref = A.float() @ B.float().t() + bias + res
+    assert rel(C, ref) < 2e-3
+
+
 @pytest.mark.parametrize("M,N,Kd", [(10, 768, 768), (50, 3072, 768), (45, 768, 3072), (128, 200, 96)])
 @pytest.mark.parametrize("a_km,b_km", [(1, 1), (1, 0), (0, 0)])
 def test_gemm_exact_f32_path(M, N, Kd, a_km, b_km):
@@ -170,6 +187,33 @@ def test_gemm_epilogues_and_maps():
     cs = torch.zeros(N, device=dev)
     k.colsum(dy, cs, row_map=gat)
     assert rel(cs, dy.sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("R,C", [(3000, 128), (20000, 256), (5000, 1024), (70000, 128)])
+def test_layernorm_bwd_param_grads_two_pass(R, C):
+    """dw/db through the per-block partials workspace + reduce (block counts of the big Swin LNs)
+    against torch and against the atomic fallback."""
+    k = K()
+    x = torch.randn(R, C, device=dev)
+    w = torch.randn(C, device=dev) * 0.2 + 1
+    b = torch.randn(C, device=dev) * 0.1
+    _, mean, rstd = k.layernorm(x, w, b, 1e-5, out_f32=True)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    dy = torch.randn(R, C, device=dev)
+    F.layer_norm(xr, (C,), wr, br, 1e-5).backward(dy)
+    outs = []
+    for ws in (True, False):
+        dx = torch.empty(R, C, device=dev)
+        dw = torch.full((C,), 0.5, device=dev)     # accumulates into existing gradients
+        db = torch.full((C,), -0.5, device=dev)
+        k.layernorm_bwd(dy, x, mean, rstd, w, dx, dw=dw, db=db, workspace=ws)
+        assert rel(dx, xr.grad) < 1e-4
+        assert rel(dw - 0.5, wr.grad) < 1e-4
+        assert rel(db + 0.5, br.grad) < 1e-4
+        outs.append((dw, db))
+    assert rel(outs[0][0], outs[1][0]) < 1e-5 and rel(outs[0][1], outs[1][1]) < 1e-5
 
 
 @pytest.mark.parametrize("C,nseg,x_f32", [(128, 1, True), (768, 1, False), (2048, 4, True), (1024, 1, True)])

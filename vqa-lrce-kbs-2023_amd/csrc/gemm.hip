@@ -437,46 +437,62 @@ __device__ __forceinline__ void glds16(const void* src, bf16* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (LRCE_LDS void*)lds_dst, 16, 0, 0);
 }
 
-// Per-lane source pointers of the R/32 glds instructions a wave issues per operand tile (1 KB each).
+// LDS-DMA with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset (the saddr
+// form), M0 = the wave's 1-KB LDS destination.  Written as asm so the per-K-tile address update is
+// ONE scalar add (a builtin takes a per-lane 64-bit pointer: 2 VALU adds + copies per instruction
+// per tile) and so hipcc does not drain vmcnt(0) before every LDS read while a DMA is in flight;
+// completion is ordered by the main loop's explicit vmcnt waits + s_barrier.
+__device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, uint32_t lds_dst) {
+  unsigned keep;
+  const uint64_t a = reinterpret_cast<uintptr_t>(sbase);
+  // (readfirstlane returns int: go through uint32_t, or the low word would sign-extend)
+  const uint64_t su = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a) |
+                      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32);
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(su), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)((LRCE_LDS const void*)p); }
+
+// Per-lane source offsets of the R/32 glds instructions a wave issues per operand tile (1 KB each).
 // K-major tile [R rows][64 k]: instruction i covers rows 8i..8i+7.
 // M-major tile [64 k][R]: instruction i covers the 1024 / 2R k rows starting at i * 1024 / 2R.
+// The offsets are loop-invariant; only the uniform base advances (glds_ok bounds them to 31 bits).
 template <bool KMAJ, int R>
 struct GldsOperand {
   static constexpr int NI = R / 32;
-  const bf16* ptr[NI];   // advanced by `step` elements per K tile
-  long long step;
+  const char* base;      // wave-uniform
+  uint32_t off[NI];      // bytes from base
+  uint32_t step;         // bytes per K tile
 
-  __device__ __forceinline__ void init(const bf16* base, long long ld, int rows_total, int row0, int k0, const int* map,
-                                       int wave, int lane) {
+  __device__ __forceinline__ void init(const bf16* b, long long ld, int rows_total, int row0, int k0, int wave, int lane) {
+    base = reinterpret_cast<const char*>(b);
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       const int ins = wave + 4 * q;
+      long long e;
       if (KMAJ) {
         const int r = ins * 8 + (lane >> 3), pos = lane & 7;
         const int kc = pos ^ ((r >> 1) & 7);
         int gr = row0 + r;
         gr = gr < rows_total ? gr : rows_total - 1;    // rows past the edge: any valid row (never stored)
-        const long long rr = map ? (long long)map[gr] : (long long)gr;
-        ptr[q] = base + rr * ld + k0 + kc * 8;
+        e = (long long)gr * ld + k0 + kc * 8;
       } else {
         constexpr int CPR = R / 8;                      // 16-B chunks per k row
         const int kr = ins * (64 / CPR) + lane / CPR, pos = lane % CPR;
         const int c = pos ^ (mm_swz_r<R>(kr) >> 1);
         int gm = row0 + c * 8;
         gm = gm < rows_total ? gm : 0;
-        ptr[q] = base + (long long)(k0 + kr) * ld + gm;
+        e = (long long)(k0 + kr) * ld + gm;
       }
+      off[q] = (uint32_t)(e * 2);
     }
-    step = KMAJ ? BK : (long long)BK * ld;
+    step = (uint32_t)(KMAJ ? BK * 2 : (long long)BK * ld * 2);
   }
-  __device__ __forceinline__ void issue(bf16* tile, int wave) {
+  __device__ __forceinline__ void issue(uint32_t tile, int wave_u) {
 #pragma unroll
-    for (int q = 0; q < NI; ++q) glds16(ptr[q], tile + (wave + 4 * q) * 512);
+    for (int q = 0; q < NI; ++q) glds16_s(base, off[q], tile + (uint32_t)(wave_u + 4 * q) * 1024u);
   }
-  __device__ __forceinline__ void advance() {
-#pragma unroll
-    for (int q = 0; q < NI; ++q) ptr[q] += step;
-  }
+  __device__ __forceinline__ void advance() { base += step; }
 };
 
 template <int TBM, int TBN, bool A_KM, bool B_KM>
@@ -542,19 +558,41 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     constexpr int INFLIGHT = (TBM + TBN) / 32;   // glds per wave per K tile
     GldsOperand<A_KM, TBM> ga;
     GldsOperand<B_KM, TBN> gb;
-    ga.init(abase, p.lda, p.m, m0, kb, p.a_map, wave, lane);
-    gb.init(bbase, p.ldb, p.n, n0, kb, nullptr, wave, lane);
-    ga.issue(sa0, wave);
-    gb.issue(sb0, wave);
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const uint32_t la0 = lds_addr(sa0), lb0 = lds_addr(sb0);
+    ga.init(abase, p.lda, p.m, m0, kb, wave, lane);
+    gb.init(bbase, p.ldb, p.n, n0, kb, wave, lane);
+    ga.issue(la0, wave_u);
+    gb.issue(lb0, wave_u);
+#ifdef LRCE_GEMM_ONEBAR
+    // one barrier per K tile: it publishes tile kt (every wave waited for its own DMAs) AND retires
+    // compute(kt-1), so the DMA of kt+1 may then overwrite that stage
+    for (int kt = 0; kt < nfull; ++kt) {
+      const int cur = kt & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nfull) {
+        ga.advance(); gb.advance();
+        ga.issue(la0 + (uint32_t)((cur ^ 1) * STG * 2), wave_u);
+        gb.issue(lb0 + (uint32_t)((cur ^ 1) * STG * 2), wave_u);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      compute(sa0 + cur * STG, sb0 + cur * STG);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#else
     for (int kt = 0; kt < nfull; ++kt) {
       const int cur = kt & 1;
       if (kt + 1 < nfull) {
         ga.advance(); gb.advance();
-        ga.issue(sa0 + (cur ^ 1) * STG, wave);
-        gb.issue(sb0 + (cur ^ 1) * STG, wave);
+        ga.issue(la0 + (uint32_t)((cur ^ 1) * STG * 2), wave_u);
+        gb.issue(lb0 + (uint32_t)((cur ^ 1) * STG * 2), wave_u);
         // this wave's tile kt landed, kt+1 in flight
-        if constexpr (INFLIGHT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -566,6 +604,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       __builtin_amdgcn_s_barrier();                          // stage `cur` free for tile kt+2
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
   }
   if (tail) {
     const int k0 = kb + nfull * BK;
@@ -745,10 +784,14 @@ extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
 }
 
 // LDS-DMA path: bf16 operands with 16-B aligned rows; K-major A may carry a row map
+// (no row map: the DMA addresses are 32-bit byte offsets from the operand base, bounded here)
 static bool glds_ok(const LrceGemmDesc* d) {
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const long long ext_a = d->a_kmajor ? (long long)d->m * d->lda + d->k : (long long)d->k * d->lda + d->m;
+  const long long ext_b = d->b_kmajor ? (long long)d->n * d->ldb + d->k : (long long)d->k * d->ldb + d->n;
   return !d->a_f32 && !d->b_f32 && al16(d->a) && al16(d->b) && (d->stride_a % 8 == 0) && (d->stride_b % 8 == 0) &&
-         (d->lda % 8 == 0) && (d->ldb % 8 == 0) && (d->a_kmajor || !d->a_map) && !g_force_legacy_gemm;
+         (d->lda % 8 == 0) && (d->ldb % 8 == 0) && !d->a_map && ext_a * 2 < (1LL << 31) && ext_b * 2 < (1LL << 31) &&
+         !g_force_legacy_gemm;
 }
 
 static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
@@ -804,12 +847,26 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     // 128x128 tiles when they give every CU work; 64x64 otherwise (small-M / small-N problems)
     const int t128 = p.tiles_m * p.tiles_n * d->batch * split;
     const bool small = g_gemm_tile == 64 || (g_gemm_tile == 0 && t128 < 256);
+    // 192x128 tiles (K-major A): 1.5x the work per tile, so fewer rounds of the 2-blocks-per-CU
+    // grid when the 128x128 tile count overshoots a round (e.g. 552 tiles on 512 slots -> 368)
+    bool tall = false;
+    if (!small && d->a_kmajor && g_gemm_tile != 128) {
+      const int slots = 2 * 256;
+      const long long t192 = (long long)((d->m + 191) / 192) * p.tiles_n * d->batch * split;
+      const long long r128 = (t128 + slots - 1) / slots, r192 = (t192 + slots - 1) / slots;
+      tall = g_gemm_tile == 192 || 2 * r128 > 3 * r192;
+    }
     if (small) {
       p.tiles_m = (d->m + 63) / 64; p.tiles_n = (d->n + 63) / 64;
       grid = dim3(p.tiles_m * p.tiles_n, d->batch * split);
+    } else if (tall) {
+      p.tiles_m = (d->m + 191) / 192;
+      grid = dim3(p.tiles_m * p.tiles_n, d->batch * split);
     }
-    const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0) | (small ? 4 : 0);
+    const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0) | (small ? 4 : 0) | (tall ? 8 : 0);
     switch (gk) {
+      case 11: gemm_glds_kernel<192, 128, true, true><<<grid, NT, 0, s>>>(p); break;
+      case 10: gemm_glds_kernel<192, 128, true, false><<<grid, NT, 0, s>>>(p); break;
       case 3: gemm_glds_kernel<128, 128, true, true><<<grid, NT, 0, s>>>(p); break;
       case 2: gemm_glds_kernel<128, 128, true, false><<<grid, NT, 0, s>>>(p); break;
       case 1: gemm_glds_kernel<128, 128, false, true><<<grid, NT, 0, s>>>(p); break;

@@ -185,11 +185,11 @@ __device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, in
 // C[m][n] = sum_k A[m][k] * B(k, n); B_KM: B stored [n][k] (forward, W), else [k][n] (dX = dY W).
 // 8 waves split the reduction; each wave issues all loads of a trip of TS k-steps (16 deep) before
 // its MFMAs, so a whole 768-deep reduction is one memory round trip per wave.
-constexpr int SK_WAVES = 8;
-
-template <int MT, bool B_KM>
+// (16 waves for reductions >= 2048 deep: the 3072-deep decoder linear2 is then one trip per wave)
+template <int MT, bool B_KM, int SK_WAVES>
 __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p) {
   constexpr int TS = MT <= 2 ? 8 : 4;
+  constexpr int NPART = SK_WAVES * 64 / 256;   // 256-thread groups finishing the m-tiles
   __shared__ float red[SK_WAVES][MT][16][17];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
@@ -240,10 +240,10 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][t][grp * 4 + r][col] = acc[t][r];
   __syncthreads();
-  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, half = threadIdx.x >> 8;
+  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, part = threadIdx.x >> 8;
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
-    if ((t & 1) != half) continue;   // threads 0-255 finish even m-tiles, 256-511 odd ones
+    if (t % NPART != part) continue;   // 256-thread group g finishes m-tiles t = g (mod NPART)
     const int m = t * 16 + ml, nn = n0 + nl;
     if (m < p.m && nn < p.n) {
       float x = 0.f;
@@ -255,26 +255,46 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p) {
 }
 
 // C[m][n] (+)= alpha * sum_{r < R} A[r][m] * B[r][n] with R <= 256 (dW of a skinny linear):
-// one thread per 4 consecutive columns, the R-term outer-product sum in registers, one RMW.
+// one thread per 4 consecutive columns, the R-term outer-product sum in registers, one RMW.  The
+// C read is issued first and the A/B rows are fetched 8 reduction steps per batch, so a thread has
+// ~17 loads in flight instead of one dependent round trip per step.
 __global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
+  constexpr int U = 8;
   const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
   const int nq = p.n >> 2;
   if (q >= (long long)p.m * nq) return;
   const int m = (int)(q / nq), n = (int)(q % nq) * 4;
+  float4* cp = reinterpret_cast<float4*>(static_cast<float*>(p.c) + (long long)m * p.ldc + n);
+  const bool acc_c = p.flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM);
+  const float4 o = acc_c ? *cp : make_float4(0.f, 0.f, 0.f, 0.f);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   float asum = 0.f;
-  for (int r = 0; r < p.k; ++r) {
-    const float av = p.a[(long long)r * p.lda + m];
+  const float* ap = p.a + m;
+  const float* bp = p.b + n;
+  int r = 0;
+  for (; r + U <= p.k; r += U) {
+    float av[U];
+    float4 bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      av[u] = ap[(long long)(r + u) * p.lda];
+      bv[u] = *reinterpret_cast<const float4*>(bp + (long long)(r + u) * p.ldb);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      asum += av[u];
+      acc.x = fmaf(av[u], bv[u].x, acc.x); acc.y = fmaf(av[u], bv[u].y, acc.y);
+      acc.z = fmaf(av[u], bv[u].z, acc.z); acc.w = fmaf(av[u], bv[u].w, acc.w);
+    }
+  }
+  for (; r < p.k; ++r) {
+    const float av = ap[(long long)r * p.lda];
     asum += av;
-    const float4 bv = *reinterpret_cast<const float4*>(p.b + (long long)r * p.ldb + n);
+    const float4 bv = *reinterpret_cast<const float4*>(bp + (long long)r * p.ldb);
     acc.x = fmaf(av, bv.x, acc.x); acc.y = fmaf(av, bv.y, acc.y); acc.z = fmaf(av, bv.z, acc.z); acc.w = fmaf(av, bv.w, acc.w);
   }
-  float4* cp = reinterpret_cast<float4*>(static_cast<float*>(p.c) + (long long)m * p.ldc + n);
-  acc.x *= p.alpha; acc.y *= p.alpha; acc.z *= p.alpha; acc.w *= p.alpha;
-  if (p.flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) {
-    const float4 o = *cp;
-    acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
-  }
+  acc.x = fmaf(acc.x, p.alpha, o.x); acc.y = fmaf(acc.y, p.alpha, o.y);
+  acc.z = fmaf(acc.z, p.alpha, o.z); acc.w = fmaf(acc.w, p.alpha, o.w);
   *cp = acc;
   if ((p.flags & LRCE_EPI_BIAS_GRAD) && n == 0) p.bias_grad[m] += p.alpha * asum;   // db (one owner per m)
 }
@@ -319,8 +339,13 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
       const int mt = (d->m + 15) / 16;
       dim3 grid((d->n + 15) / 16);
 #define LRCE_SK(MT)                                                                          \
-  if (d->b_kmajor) skinny_kernel<MT, true><<<grid, SK_WAVES * 64, 0, st>>>(q);              \
-  else skinny_kernel<MT, false><<<grid, SK_WAVES * 64, 0, st>>>(q);
+  if (d->k >= 2048) {                                                                        \
+    if (d->b_kmajor) skinny_kernel<MT, true, 16><<<grid, 16 * 64, 0, st>>>(q);               \
+    else skinny_kernel<MT, false, 16><<<grid, 16 * 64, 0, st>>>(q);                          \
+  } else {                                                                                   \
+    if (d->b_kmajor) skinny_kernel<MT, true, 8><<<grid, 8 * 64, 0, st>>>(q);                 \
+    else skinny_kernel<MT, false, 8><<<grid, 8 * 64, 0, st>>>(q);                            \
+  }
       switch (mt) {
         case 1: LRCE_SK(1) break;
         case 2: LRCE_SK(2) break;

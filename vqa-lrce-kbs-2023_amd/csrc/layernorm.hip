@@ -109,7 +109,7 @@ template <typename TD, typename TX, int CH, int LPR>
 __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, const TX* x, const int* in_map, int nseg,
                                               const float* mean_i, const float* rstd_i, const float* w, float* dx,
                                               const float* dres, float* dw, float* db, int rows, int cols, bf16* dx16,
-                                              const int* dx16_map, const float* dsc, int dsc_rps) {
+                                              const int* dx16_map, const float* dsc, int dsc_rps, float* part) {
   constexpr int RPW = 64 / LPR;
   __shared__ float red[2][4][4 * CH * LPR + 4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sl = lane % LPR;
@@ -225,13 +225,52 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
     }
   }
   __syncthreads();
+  float* pb = part ? part + (long long)blockIdx.x * 2 * cols : nullptr;
   for (int e = threadIdx.x; e < cols; e += 256) {
     const float sw = red[0][0][e] + red[0][1][e] + red[0][2][e] + red[0][3][e];
     const float sb = red[1][0][e] + red[1][1][e] + red[1][2][e] + red[1][3][e];
-    if (dw) atomicAdd(dw + e, sw);
-    if (db) atomicAdd(db + e, sb);
+    if (pb) {            // per-block partials, summed by ln_bwd_reduce (no same-address atomics here)
+      pb[e] = sw;
+      pb[cols + e] = sb;
+    } else {
+      if (dw) atomicAdd(dw + e, sw);
+      if (db) atomicAdd(db + e, sb);
+    }
   }
 }
+
+// dw[e] += sum_b part[b][e], db[e] += sum_b part[b][cols + e]: block (x, y) sums 32 partial rows of
+// 64 columns (8 per wave, loads in flight together) and adds once, so an address sees nb/32 adds.
+__global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ part, int nb, int cols, float* dw, float* db) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  const int b0 = blockIdx.y * 32 + wave * 8;
+  float v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = (e < 2 * cols && b0 + u < nb) ? part[(long long)(b0 + u) * 2 * cols + e] : 0.f;
+  float t = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) t += v[u];
+  red[wave][lane] = t;
+  __syncthreads();
+  if (wave == 0 && e < 2 * cols) {
+    t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    float* dst = e < cols ? (dw ? dw + e : nullptr) : (db ? db + (e - cols) : nullptr);
+    if (dst) atomicAdd(dst, t);
+  }
+}
+
+// rows per wave of ln_bwd: small inputs (the decoder / BERT rows) one row per wave (latency-bound:
+// as many waves as rows); larger ones 4-8 with the next row prefetched.  Without a partials
+// workspace every block adds its dw/db into the SAME 2 x cols addresses, so blocks are capped.
+int ln_bwd_blocks(int rows, int lpr, bool ws) {
+  const int rpb = 4 * (64 / lpr);                 // rows per block per pass
+  const int per_wave = ws ? (rows <= 2048 ? 1 : rows <= 8192 ? 4 : 8) : (rows <= 8192 ? 1 : 8);
+  const int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
+  return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+}
+int ln_bwd_lpr(int cols) { return cols / 4 <= 32 ? 32 : 64; }
 
 }  // namespace
 
@@ -268,7 +307,8 @@ extern "C" int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_ma
 extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map, const void* x, int x_f32,
                                   const int32_t* in_map, int nseg, const float* mean, const float* rstd, const float* w,
                                   float* dx, const float* dres, float* dw, float* db, int rows, int cols, uint16_t* dx_bf16,
-                                  const int32_t* dx_bf16_map, const float* dx_scale, int dx_scale_rps, void* stream) {
+                                  const int32_t* dx_bf16_map, const float* dx_scale, int dx_scale_rps, float* workspace,
+                                  int64_t workspace_elems, void* stream) {
   if (!dy || !x || !mean || !rstd || !w || !dx) return lrce_fail(LRCE_E_ARG, "layernorm_bwd: null pointer");
   if (dx_scale_rps < 1) dx_scale_rps = 1;
   if (nseg < 1) nseg = 1;
@@ -277,19 +317,16 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
   if (rows <= 0) return LRCE_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nch = cols / 4;
-  // Rows per wave: small inputs (the decoder / BERT rows) get one row per wave (latency-bound: as
-  // many waves as rows); large ones >= 8 rows per wave and <= 2048 blocks, because every block adds
-  // its dw/db partials into the SAME 2 x cols addresses (contended atomics: more blocks is slower).
-  auto blocks = [&](int lpr) {
-    const int rpb = 4 * (64 / lpr);                 // rows per block per pass
-    const int per_wave = rows <= 8192 ? 1 : 8;
-    int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
-    return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
-  };
+  const int lpr = ln_bwd_lpr(cols);
+  const bool want = dw || db;
+  const int nb_ws = ln_bwd_blocks(rows, lpr, true);
+  float* part = want && workspace && workspace_elems >= (int64_t)nb_ws * 2 * cols ? workspace : nullptr;
+  const int nb = part ? nb_ws : ln_bwd_blocks(rows, lpr, false);
 #define LNB3(TD, TX, CH, LPR)                                                                                          \
-  ln_bwd<TD, TX, CH, LPR><<<blocks(LPR), 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, \
+  ln_bwd<TD, TX, CH, LPR><<<nb, 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, \
                                                      nseg, mean, rstd, w, dx, dres, dw, db, rows, cols,      \
-                                                     reinterpret_cast<bf16*>(dx_bf16), dx_bf16_map, dx_scale, dx_scale_rps)
+                                                     reinterpret_cast<bf16*>(dx_bf16), dx_bf16_map, dx_scale, dx_scale_rps, \
+                                                     part)
 #define LNB(TD, TX)                                   \
   if (nch <= 32) LNB3(TD, TX, 1, 32);                 \
   else if (nch <= 64) LNB3(TD, TX, 1, 64);            \
@@ -303,5 +340,11 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
   else { LNB(bf16, bf16) }
 #undef LNB
 #undef LNB3
+  if (part) ln_bwd_reduce<<<dim3((2 * cols + 63) / 64, (nb + 31) / 32), 256, 0, s>>>(part, nb, cols, dw, db);
   return lrce_check_launch("layernorm_bwd");
+}
+
+extern "C" int64_t lrce_layernorm_bwd_workspace(int rows, int cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return (int64_t)ln_bwd_blocks(rows, ln_bwd_lpr(cols), true) * 2 * cols;
 }

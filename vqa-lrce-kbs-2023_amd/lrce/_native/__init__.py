@@ -81,7 +81,8 @@ _U64 = ctypes.c_uint64
 _SIGS = {
     "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
     "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _P],
-    "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P],
+    "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _I64,
+                           _P],
     "lrce_scale_cast_bf16": [_P, _I64, _I, _P, _I, _P, _P],
     "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _P, _P],
     "lrce_wattn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
@@ -107,9 +108,11 @@ _SIGS = {
     "lrce_version": [],
     "lrce_last_error": [],
 }
-_RET = {"lrce_last_error": ctypes.c_char_p, "lrce_wattn_bias_elems": _I64, "lrce_wattn_ds_elems": _I64}
+_RET = {"lrce_last_error": ctypes.c_char_p, "lrce_wattn_bias_elems": _I64, "lrce_wattn_ds_elems": _I64,
+        "lrce_layernorm_bwd_workspace": _I64}
 _SIGS["lrce_wattn_bias_elems"] = [_I, _I]
 _SIGS["lrce_wattn_ds_elems"] = [_I, _I]
+_SIGS["lrce_layernorm_bwd_workspace"] = [_I, _I]
 
 
 def _declare(L):

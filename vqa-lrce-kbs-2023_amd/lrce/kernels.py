@@ -230,13 +230,18 @@ def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out
 
 
 def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1, dres=None, dw=None, db=None,
-                  rows=None, cols=None, dx16=None, dx16_map=None, dx_scale=None, dx_scale_rps=1):
-    """dx16: optional bf16 copy of dx (times dx_scale[r / dx_scale_rps], at row dx16_map[r])."""
+                  rows=None, cols=None, dx16=None, dx16_map=None, dx_scale=None, dx_scale_rps=1, workspace=True):
+    """dx16: optional bf16 copy of dx (times dx_scale[r / dx_scale_rps], at row dx16_map[r]).
+    workspace=False: dw/db by per-block atomics instead of the two-pass partials sum."""
     R = rows if rows is not None else mean.shape[0]
     Cc = cols if cols is not None else w.shape[0]
+    ws, nws = None, 0
+    if workspace and (dw is not None or db is not None):
+        nws = N.lib().lrce_layernorm_bwd_workspace(R, Cc)
+        ws = torch.empty(nws, dtype=F32, device=dx.device)
     call("lrce_layernorm_bwd", ptr(dy), int(dy.dtype == F32), ptr(dy_map), ptr(x), int(x.dtype == F32), ptr(in_map),
          nseg, ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dres), ptr(dw), ptr(db), R, Cc, ptr(dx16), ptr(dx16_map),
-         ptr(dx_scale), dx_scale_rps, stream_of(dx))
+         ptr(dx_scale), dx_scale_rps, ptr(ws), nws, stream_of(dx))
     return dx
 
 
