@@ -185,7 +185,7 @@ __device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, in
 // C[m][n] = sum_k A[m][k] * B(k, n); B_KM: B stored [n][k] (forward, W), else [k][n] (dX = dY W).
 // 8 waves split the reduction; each wave issues all loads of a trip of TS k-steps (16 deep) before
 // its MFMAs, so a whole 768-deep reduction is one memory round trip per wave.
-// (16 waves for reductions >= 2048 deep: the 3072-deep decoder linear2 is then one trip per wave)
+// (8 waves: a 16-wave variant measured slower on the 3072-deep decoder linear2, 18.8 vs ~9 us)
 template <int MT, bool B_KM, int SK_WAVES>
 __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p) {
   constexpr int TS = MT <= 2 ? 8 : 4;
@@ -339,13 +339,8 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
       const int mt = (d->m + 15) / 16;
       dim3 grid((d->n + 15) / 16);
 #define LRCE_SK(MT)                                                                          \
-  if (d->k >= 2048) {                                                                        \
-    if (d->b_kmajor) skinny_kernel<MT, true, 16><<<grid, 16 * 64, 0, st>>>(q);               \
-    else skinny_kernel<MT, false, 16><<<grid, 16 * 64, 0, st>>>(q);                          \
-  } else {                                                                                   \
-    if (d->b_kmajor) skinny_kernel<MT, true, 8><<<grid, 8 * 64, 0, st>>>(q);                 \
-    else skinny_kernel<MT, false, 8><<<grid, 8 * 64, 0, st>>>(q);                            \
-  }
+  if (d->b_kmajor) skinny_kernel<MT, true, 8><<<grid, 8 * 64, 0, st>>>(q);                   \
+  else skinny_kernel<MT, false, 8><<<grid, 8 * 64, 0, st>>>(q);
       switch (mt) {
         case 1: LRCE_SK(1) break;
         case 2: LRCE_SK(2) break;

@@ -320,7 +320,8 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
   const int lpr = ln_bwd_lpr(cols);
   const bool want = dw || db;
   const int nb_ws = ln_bwd_blocks(rows, lpr, true);
-  float* part = want && workspace && workspace_elems >= (int64_t)nb_ws * 2 * cols ? workspace : nullptr;
+  // (a few blocks -- the decoder / BERT rows -- add directly: a second launch would cost more)
+  float* part = want && nb_ws > 64 && workspace && workspace_elems >= (int64_t)nb_ws * 2 * cols ? workspace : nullptr;
   const int nb = part ? nb_ws : ln_bwd_blocks(rows, lpr, false);
 #define LNB3(TD, TX, CH, LPR)                                                                                          \
   ln_bwd<TD, TX, CH, LPR><<<nb, 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, \
@@ -346,5 +347,6 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
 
 extern "C" int64_t lrce_layernorm_bwd_workspace(int rows, int cols) {
   if (rows <= 0 || cols <= 0) return 0;
-  return (int64_t)ln_bwd_blocks(rows, ln_bwd_lpr(cols), true) * 2 * cols;
+  const int nb = ln_bwd_blocks(rows, ln_bwd_lpr(cols), true);
+  return nb > 64 ? (int64_t)nb * 2 * cols : 0;
 }

@@ -238,7 +238,7 @@ def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1,
     ws, nws = None, 0
     if workspace and (dw is not None or db is not None):
         nws = N.lib().lrce_layernorm_bwd_workspace(R, Cc)
-        ws = torch.empty(nws, dtype=F32, device=dx.device)
+        ws = torch.empty(nws, dtype=F32, device=dx.device) if nws > 0 else None
     call("lrce_layernorm_bwd", ptr(dy), int(dy.dtype == F32), ptr(dy_map), ptr(x), int(x.dtype == F32), ptr(in_map),
          nseg, ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dres), ptr(dw), ptr(db), R, Cc, ptr(dx16), ptr(dx16_map),
          ptr(dx_scale), dx_scale_rps, ptr(ws), nws, stream_of(dx))
