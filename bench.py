@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch-size", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-baseline-batch", type=int, default=3)
+    ap.add_argument("--cpu-baseline-batch", type=int, default=6)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph",
                     help="graph: the step replayed from a HIP graph (N>1: graph(fwd+bwd) -> RCCL bucket "
@@ -240,18 +240,42 @@ def main():
         dist.destroy_process_group()
 
 
+HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r1_pmc_wattn_fwd.json")   # tools/pmc_traffic.py output
+
+
+def _pmc_traffic():
+    """HBM bytes per launch of lrce_wattn_fwd from the committed rocprofv3 --pmc passes of this same
+    command (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH_SIZE doubled for gfx950)."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+        return round(d["traffic_bytes_per_launch"]), os.path.relpath(PMC_TRAFFIC, REPO)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def _roofline(timer):
-    """Roofline of the Swin window-attention forward kernel (the kernel the north star names):
-    algorithmic flops per launch = 4 * n^2 * d per (window, head), n = 147 tokens (8x7x7 window clamped to
-    the 3x7x7 token grid of a 5-frame clip),
-    d = 32, x windows x heads of the stage; duration = HIP events recorded around
-    every launch on its stream during the timed steps.  Bound: MFMA (dense bf16 peak)."""
-    n, mean_ms, tflops, _ = timer.summary("wattn_fwd")
+    """Roofline of the Swin window-attention forward kernel (the kernel the north star names).
+    Algorithmic work per (window, head), n = 147 tokens (8x7x7 window clamped to the 3x7x7 token grid of
+    a 5-frame clip), d = 32: flops 4 n^2 d (QK^T + PV); bytes 8 n d (Q, K, V read and
+    O written, bf16).  Arithmetic intensity n / 2 = 73.5 flop/B is below the bf16 ridge point
+    (2.5 PF/s / 8 TB/s = 312 flop/B), so the kernel is HBM-bound: `bound`/`frac` are against HBM peak,
+    and the MFMA fraction the north-star metric names is reported beside it (its ceiling at this
+    intensity is 73.5 x 8 TB/s = 588 TF/s = 0.235 of peak).  Duration = HIP events recorded around
+    every launch on its stream during eager steps of the same workload."""
+    n, mean_ms, tflops, gbs = timer.summary("wattn_fwd")
     if not n:
         return None
-    roof = {"kernel": "lrce_wattn_fwd", "bound": "mfma", "achieved": round(tflops, 2),
-            "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / MFMA_BF16_PEAK_TFLOPS, 4),
-            "traffic": None, "launches": n, "mean_launch_ms": round(mean_ms, 4)}
+    traffic, src = _pmc_traffic()
+    alg_bytes = timer.bytes["wattn_fwd"] / n
+    roof = {"kernel": "lrce_wattn_fwd", "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_launch": round(alg_bytes), "traffic_source": src,
+            "launches": n, "mean_launch_ms": round(mean_ms, 4),
+            "mfma": {"achieved": round(tflops, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+                     "ceiling_frac_at_this_intensity": round(73.5 * HBM_PEAK_GBS / 1000.0 / MFMA_BF16_PEAK_TFLOPS, 4)}}
     extra = {}
     for name in ("wattn_bwd", "gemm", "gemm_f32"):
         if name in timer.names:

@@ -1,0 +1,128 @@
+"""GPU tests of the agent / CLI layer on the native path (reference lrce/agent/*.py, train_ddp.py,
+eval.py): the reported loss is the reference's task loss + reg * sum ||p||_2, a train step updates the
+weights, hinge / MSE heads, checkpoint round trip in the `{'model_state_dict'}` format, and the
+train_ddp.py -> eval.py scripts end to end on synthetic data (one rank, RCCL process group)."""
+import argparse
+import glob
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import PKG, gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
+
+
+def _args(tmp_path, **kw):
+    a = dict(lr=[1e-4] * 3, reg_strength=0.001, lr_decay_factor=0.5, patience=0.5, min_lr=1e-8,
+             use_cosine_scheduler=False, dataset="msvd-qa-oe", log_dir=str(tmp_path), epoch=1, ckpt_interval=1,
+             use_hinge_loss=False, margin=1.0, debug_mode=True)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def _batch(task, L, n=2, ncls=50):
+    from lrce.dataset import SyntheticQADataset
+    d = SyntheticQADataset(n, task, L, [1], num_classes=ncls, seed=5)
+    items = [d[i] for i in range(n)]
+    return [torch.stack([it[k] for it in items]) for k in range(5)]
+
+
+def _l2(model):
+    return sum(p.detach().double().norm(2) for p in model.parameters() if p.requires_grad).item()
+
+
+def _model(task, ncls, L):
+    from lrce.models.e2e import E2ECount, E2EMultipleChoice, E2EOpenEnded
+    cls = {"oe": E2EOpenEnded, "mc": E2EMultipleChoice, "count": E2ECount}[task]
+    torch.manual_seed(0)
+    return cls(768, ncls, 0.5, (7, 7), 1024, 5, [1], L)
+
+
+def test_agent_oe_loss_and_update(tmp_path):
+    from lrce.agent import AgentOE
+    agent = AgentOE(_model("oe", 50, 32), 0, _args(tmp_path), log_enabled=False)
+    b = _batch("oe", 32)
+    with torch.no_grad():
+        agent.model.eval()
+        out = agent.model(*(t.cuda() for t in b[:4])).float()
+        loss, correct, total = agent.step(*b, is_train=False)
+    expect = F.cross_entropy(out, b[4].cuda()).item() + 0.001 * _l2(agent.model.module)
+    assert abs(loss - expect) < 1e-3 * abs(expect), (loss, expect)
+    assert total == 2 and 0 <= correct <= 2
+    w0 = agent.model.module.fusion_model.final_fc.weight.detach().clone()
+    agent.model.train()
+    loss_t, _, _ = agent.step(*b, is_train=True)
+    torch.cuda.synchronize()
+    assert loss_t == loss_t and not torch.equal(w0, agent.model.module.fusion_model.final_fc.weight.detach())
+    # the L2 value after the update comes from the optimizer kernel's norms: must equal a fresh count
+    assert abs(agent.calculate_l2_reg().item() - _l2(agent.model.module)) < 1e-4 * _l2(agent.model.module)
+
+
+def test_agent_mc_hinge_and_count_mse(tmp_path):
+    from lrce.agent import AgentCount, AgentMC
+    from lrce.agent.agent_mc import hinge_loss
+    agent = AgentMC(_model("mc", 1, 40), 0, _args(tmp_path, use_hinge_loss=True, margin=1.0), log_enabled=False)
+    b = _batch("mc", 40)
+    with torch.no_grad():
+        agent.model.eval()
+        out = agent.model(*(t.cuda() for t in b[:4])).float()
+        loss, correct, total = agent.step(*b, is_train=False)
+    assert out.shape == (2, 5)
+    expect = hinge_loss(out, b[4].cuda(), 1.0).item() + 0.001 * _l2(agent.model.module)
+    assert abs(loss - expect) < 1e-3 * abs(expect)
+    loss_t, _, _ = agent.step(*b, is_train=True)
+    assert loss_t == loss_t
+    del agent
+    agent = AgentCount(_model("count", 1, 30), 0, _args(tmp_path, dataset="tgif-count"), log_enabled=False)
+    b = _batch("count", 30)
+    with torch.no_grad():
+        agent.model.eval()
+        out = agent.model(*(t.cuda() for t in b[:4])).float()
+        loss, mse = agent.step(*b, is_train=False)
+    assert mse.shape == (2,)
+    assert torch.allclose(mse, (out - b[4].cuda()) ** 2, rtol=1e-5)
+    loss_t, mse_t = agent.step(*b, is_train=True)
+    assert loss_t == loss_t and mse_t.shape == (2,)
+
+
+def test_checkpoint_round_trip(tmp_path):
+    from lrce.agent import AgentOE
+    a = _args(tmp_path)
+    a.ckpt_dir = str(tmp_path)
+    agent = AgentOE(_model("oe", 50, 32), 0, a, log_enabled=False)
+    b = _batch("oe", 32)
+    agent.model.train()
+    agent.step(*b, is_train=True)
+    path = agent.save_checkpoint(1, "best")
+    assert set(torch.load(path, weights_only=True)) == {"model_state_dict"}
+    agent.model.eval()
+    with torch.no_grad():
+        y0 = agent.model(*(t.cuda() for t in b[:4])).float()
+    fresh = AgentOE(_model("oe", 50, 32), 0, _args(tmp_path, reg_strength=0.0), log_enabled=False, is_eval=True)
+    fresh.load_checkpoint(path)
+    fresh.model.eval()
+    with torch.no_grad():
+        y1 = fresh.model(*(t.cuda() for t in b[:4])).float()
+    assert torch.allclose(y0, y1, atol=1e-5, rtol=1e-5)
+
+
+def test_train_ddp_then_eval_scripts(tmp_path):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29517", HIP_VISIBLE_DEVICES="0")
+    common = ["--temporal-scale", "1", "--batch-size", "2", "--num-workers", "0"]
+    r = subprocess.run([sys.executable, os.path.join(PKG, "train_ddp.py"), "--dataset", "msvd-qa-oe", "--synthetic", "4",
+                        "--synthetic-val", "2", "--epoch", "1", "--log-dir", str(tmp_path), "--lr", "1e-4"] + common,
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ckpts = glob.glob(os.path.join(str(tmp_path), "*_msvd-qa-oe", "weights", "*.pt"))
+    assert any(c.endswith("best.pt") for c in ckpts) and len(ckpts) == 2, ckpts
+    assert os.path.exists(glob.glob(os.path.join(str(tmp_path), "*_msvd-qa-oe", "config.json"))[0])
+    best = [c for c in ckpts if c.endswith("best.pt")][0]
+    r = subprocess.run([sys.executable, os.path.join(PKG, "eval.py"), "--dataset", "msvd-qa-oe", "--model-path", best,
+                        "--synthetic", "2"] + common, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Accuracy:" in r.stderr + r.stdout

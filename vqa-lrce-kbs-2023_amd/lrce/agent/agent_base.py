@@ -1,0 +1,283 @@
+"""Training / evaluation agent (reference lrce/agent/agent_base.py) on the native gfx950 path.
+
+Same class name, constructor `(model, gpu_id, args, log_enabled=True, is_eval=False)`, attributes
+(`model` with `.module`, `optim`, `scheduler`, `args`, `last_loss`, `last_metric_val`, `best_*`) and
+methods (`step`, `process_data` generator, `do_training`, `do_sanity_check`, `do_evaluation`,
+`save_checkpoint` / `load_checkpoint` with the `{'model_state_dict': ...}` format,
+`calculate_l2_reg`, `is_metric_val_better`, `save_config`, `write_summary`).
+
+What differs, MI355X-first:
+* optimizer: FusedAdamW over the flat parameter store, three groups (fusion, text, video) with the
+  per-group learning rates of args.lr (agent_base.py:27-44).  The loss's L2 term
+  reg_strength * sum_t ||p_t||_2 (agent_base.py:103-108) is not back-propagated through 783 norm
+  kernels: its gradient reg * p_t / ||p_t|| is added inside the update kernel, and its value comes
+  from the norms that kernel already produces — the reported loss is the reference's loss;
+* precision: bf16 MFMA with f32 master weights instead of fp16 autocast + GradScaler (no loss scale is
+  needed for bf16; `self.scaler` is kept as None);
+* data parallel: instead of torch DDP (agent_base.py:75-76), `DataParallel` below attaches the
+  bucketed RCCL gradient reducer of lrce/distributed.py (all-reduce overlapped with backward, 1/world
+  folded into the optimizer's gradient scale, one parameter broadcast at construction);
+* summaries: tensorboard is not in this image; scalars go to `<log_dir>/scalars.jsonl` (same tags).
+"""
+import json
+import logging
+import os
+import time
+from collections import deque
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..optim import FusedAdamW
+from ..runtime import ensure
+from .schedulers import CosineAnnealingWarmupRestarts, ReduceLROnPlateau
+
+IGNORE_INDEX = -100   # constants.py:10
+
+
+def get_logger(name, rank):
+    """utils.py:163-175: a real logger on rank 0, a silent one elsewhere."""
+    logger = logging.getLogger(name)
+    if rank != 0:
+        logger.disabled = True
+    return logger
+
+
+class ScalarLog:
+    """Minimal stand-in for torch.utils.tensorboard.SummaryWriter.add_scalar (JSON lines)."""
+
+    def __init__(self, log_dir):
+        os.makedirs(log_dir, exist_ok=True)
+        self.path = os.path.join(log_dir, "scalars.jsonl")
+
+    def add_scalar(self, tag, value, step):
+        with open(self.path, "a") as f:
+            f.write(json.dumps({"tag": tag, "value": float(value), "step": step}) + "\n")
+
+
+class DataParallel(nn.Module):
+    """The agent's replacement for DistributedDataParallel: `.module` is the model; when a process
+    group with more than one rank exists, gradients are averaged by the flat-buffer RCCL reducer."""
+
+    def __init__(self, module, bucket_mb=64):
+        super().__init__()
+        self.module = module
+        self.reducer = None
+        ensure(module)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            from ..distributed import attach
+            self.reducer = attach(module, bucket_mb=bucket_mb)
+
+    def forward(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
+
+    def finish_gradients(self):
+        """Wait for the all-reduce of every bucket; returns the optimizer's gradient scale (1/world)."""
+        return self.reducer.finish() if self.reducer is not None else 1.0
+
+
+class AgentBase:
+    def __init__(self, model, gpu_id, args, log_enabled=True, is_eval=False):
+        self.args = args
+        self.gpu_id = gpu_id
+        self.log_enabled = log_enabled
+        self.is_eval = is_eval
+        self.uid = int(time.time())
+        self.device = torch.device("cuda", gpu_id) if isinstance(gpu_id, int) else torch.device(gpu_id)
+        self.loss_func = nn.CrossEntropyLoss(ignore_index=IGNORE_INDEX)
+        self.scaler = None
+
+        model = model.to(self.device)
+        self.model = DataParallel(model)
+        self.reg_strength = float(getattr(args, "reg_strength", 0.0))
+        self.optim = None
+        self.scheduler = None
+        if not is_eval:
+            lrs = list(args.lr) * (3 if len(args.lr) == 1 else 1)
+            self.optim = FusedAdamW(
+                model,
+                [{"params": model.fusion_model.parameters(), "lr": lrs[0]},
+                 {"params": model.text_extractor.parameters(), "lr": lrs[1]},
+                 {"params": model.video_extractor.parameters(), "lr": lrs[2]}],
+                lr=lrs[0], betas=(0.9, 0.999), reg_strength=self.reg_strength)
+            if getattr(args, "use_cosine_scheduler", False):
+                self.scheduler = CosineAnnealingWarmupRestarts(
+                    self.optim, first_cycle_steps=args.lr_restart_epoch, cycle_mult=args.lr_restart_mul,
+                    max_lr=lrs[0], min_lr=args.min_lr, warmup_steps=args.lr_warm_up, gamma=args.lr_decay_factor)
+            else:
+                self.scheduler = ReduceLROnPlateau(self.optim, mode="max", factor=args.lr_decay_factor,
+                                                   patience=args.patience, min_lr=args.min_lr)
+
+        self.logger = get_logger(__name__, gpu_id)
+        self.summary_writer = None
+        if log_enabled and gpu_id == 0:
+            self.args.log_dir = os.path.join(args.log_dir, f"{self.uid}_{args.dataset}")
+            self.summary_writer = ScalarLog(self.args.log_dir)
+            self.args.ckpt_dir = os.path.join(self.args.log_dir, "weights")
+            os.makedirs(self.args.ckpt_dir, exist_ok=True)
+            self.save_config()
+
+        self.last_loss = None
+        self.last_metric_val = None
+        self.counter = 0
+        self.best_epoch = None
+        self.best_metric_val = None
+
+    # ------------------------------------------------------------------ helpers (agent_base.py:90-108)
+    def is_metric_val_better(self, epoch=None):
+        if self.best_metric_val is None or self.last_metric_val > self.best_metric_val:
+            self.best_metric_val = self.last_metric_val
+            self.best_epoch = epoch
+            return True
+        return False
+
+    def write_summary(self, title, value, step):
+        if self.summary_writer is not None:
+            self.summary_writer.add_scalar(title, value, step)
+
+    def calculate_l2_reg(self):
+        """sum over trainable parameters of ||p||_2 (device scalar, no autograd graph)."""
+        if self.optim is not None:
+            return self.optim.l2_value()
+        with torch.no_grad():
+            return sum(p.float().norm(2) for p in self.model.module.parameters() if p.requires_grad)
+
+    def _regularised(self, task_loss):
+        """The reference's `loss = task + reg * L2` as a value; only `task_loss` is back-propagated
+        (the L2 gradient is applied by the optimizer kernel)."""
+        if self.reg_strength == 0.0:
+            return task_loss.detach()
+        return task_loss.detach() + self.reg_strength * self.calculate_l2_reg()
+
+    def _backward_and_update(self, task_loss):
+        """optim.zero_grad -> backward -> (all-reduce) -> optimizer step (agent_oe.py:38-42)."""
+        self.optim.zero_grad()
+        task_loss.backward()
+        scale = self.model.finish_gradients()
+        self.optim.step(grad_scale=scale)
+
+    def _forward(self, video_clips, texts, texts_attention_mask, texts_type_ids):
+        d = self.device
+        return self.model(video_clips.to(d, non_blocking=True), texts.to(d, non_blocking=True),
+                          texts_attention_mask.to(d, non_blocking=True), texts_type_ids.to(d, non_blocking=True))
+
+    def step(self, *args, is_train):
+        raise NotImplementedError()
+
+    @staticmethod
+    def _reduce(t):
+        if dist.is_available() and dist.is_initialized():
+            dist.reduce(t, dst=0)
+
+    # ------------------------------------------------------------------ loops (agent_base.py:110-171)
+    def process_data(self, dl, is_train, epoch):
+        if is_train:
+            self.logger.info("Training Phase")
+        elif not self.is_eval:
+            self.logger.info("Validation Phase")
+        correct_counter = torch.zeros(2, device=self.device)
+        batch_losses = torch.zeros(len(dl), device=self.device)
+        avg_losses, avg_acc = float("nan"), float("nan")
+        for i, batch_data in enumerate(dl):
+            if not is_train:
+                self.model.eval()
+                with torch.no_grad():
+                    b_loss, b_total_correct, b_total_data = self.step(*batch_data, is_train=False)
+            else:
+                self.model.train()
+                b_loss, b_total_correct, b_total_data = self.step(*batch_data, is_train=True)
+                self.counter += 1
+                if getattr(self.args, "use_cosine_scheduler", False):
+                    self.scheduler.step(epoch + i / len(dl))
+                for k in range(len(self.optim.param_groups)):
+                    self.write_summary(f"LR Scheduler/{k}", self.optim.param_groups[k]["lr"], self.counter)
+                self.write_summary("Training/Batch Loss", b_loss, self.counter)
+                self.write_summary("Training/Batch Accuracy", b_total_correct / b_total_data, self.counter)
+                yield i
+            if self.gpu_id != 0:   # ranks > 0 contribute only their current batch to the reduce
+                correct_counter.zero_()
+            correct_counter[0] += b_total_correct
+            correct_counter[1] += b_total_data
+            batch_losses[i] = b_loss
+            self._reduce(correct_counter)
+            nz = batch_losses[batch_losses.nonzero()]
+            avg_losses = nz.mean().item() if nz.numel() else 0.0
+            avg_acc = (correct_counter[0] / correct_counter[1]).item()
+        if not is_train:
+            self.last_loss = avg_losses
+            self.last_metric_val = avg_acc
+            if not self.is_eval and not getattr(self.args, "use_cosine_scheduler", False):
+                self.scheduler.step(avg_acc)
+            self.write_summary("Validation/Loss", avg_losses, epoch)
+            self.write_summary("Validation/Accuracy", avg_acc, epoch)
+        else:
+            self.write_summary("Training/Loss", avg_losses, epoch)
+            self.write_summary("Training/Accuracy", avg_acc, epoch)
+        yield -1
+
+    # ------------------------------------------------------------------ persistence (agent_base.py:173-217)
+    def save_config(self):
+        if not getattr(self.args, "debug_mode", True):
+            vars(self.args).pop("debug_mode", None)
+        config = {**vars(self.args)}
+        self.logger.info("======CONFIGURATIONS======")
+        for k, v in config.items():
+            self.logger.info(f"{k.upper()}: {v}")
+        path = os.path.join(self.args.log_dir, "config.json")
+        with open(path, "w") as f:
+            json.dump(config, f)
+        self.logger.info(f"Training config saved to {path}")
+
+    def save_checkpoint(self, epoch, name="", only_model=True):
+        if self.gpu_id != 0 or not hasattr(self.args, "ckpt_dir"):
+            return None   # (the reference raises AttributeError here when logging is disabled)
+        ckpt = {"model_state_dict": self.model.module.state_dict()}
+        if not only_model:
+            ckpt["optimizer_state_dict"] = self.optim.state_dict()
+            ckpt["scheduler_state_dict"] = self.scheduler.state_dict()
+        if name != "":
+            path = os.path.join(self.args.ckpt_dir, f"{name}.pt")
+        else:
+            path = os.path.join(self.args.ckpt_dir,
+                                f"epoch{epoch:02}_loss{self.last_loss:.4f}_metric{self.last_metric_val:.4f}.pt")
+        torch.save(ckpt, path)
+        self.logger.info(f"Checkpoint saved to {path}")
+        return path
+
+    def load_checkpoint(self, ckpt_path, only_model=True):
+        """Loads a reference `{'model_state_dict': ...}` checkpoint (tensors only: weights_only=True)."""
+        assert os.path.exists(ckpt_path), ckpt_path
+        ckpt = torch.load(ckpt_path, map_location="cpu", weights_only=True)
+        self.model.module.load_state_dict(ckpt["model_state_dict"])
+        if not only_model:
+            self.optim.load_state_dict(ckpt["optimizer_state_dict"])
+            self.scheduler.load_state_dict(ckpt["scheduler_state_dict"])
+        self.logger.info(f"Succesfully loaded model in {ckpt_path}")
+
+    # ------------------------------------------------------------------ drivers (agent_base.py:219-254)
+    def do_training(self, train_dataloader, val_dataloader, eval_per_epoch=1):
+        eval_idx = [len(train_dataloader) // eval_per_epoch * i for i in range(1, eval_per_epoch)]
+        for i in range(self.args.epoch):
+            self.logger.info(f"Epoch {i + 1}/{self.args.epoch}")
+            k = 0
+            for step in self.process_data(train_dataloader, True, i):
+                if step in eval_idx or step == -1:
+                    deque(self.process_data(val_dataloader, False, eval_per_epoch * i + k), maxlen=0)
+                    if self.is_metric_val_better(i + 1):
+                        self.save_checkpoint(i + 1, "best")
+                    k += 1
+            if (i + 1) % self.args.ckpt_interval == 0 or i == self.args.epoch - 1:
+                self.save_checkpoint(i + 1)
+            self.logger.info("Epoch complete\n")
+        self.logger.info(f"Best result was seen in epoch {self.best_epoch}")
+
+    def do_sanity_check(self, sanity_check_dataloader):
+        for i in range(self.args.epoch):
+            self.logger.info(f"Epoch {i + 1}/{self.args.epoch}")
+            deque(self.process_data(sanity_check_dataloader, True, i), maxlen=0)
+
+    def do_evaluation(self, test_dataloader):
+        deque(self.process_data(test_dataloader, False, 0), maxlen=0)
+        self.logger.info(f"Accuracy: {self.last_metric_val * 100:.5f}%")
+        self.logger.info(f"Loss: {self.last_loss:.5f}")

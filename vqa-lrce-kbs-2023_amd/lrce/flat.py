@@ -77,16 +77,26 @@ class FlatParams:
         return id(p) in self._index
 
     # ------------------------------------------------------------------ sync
+    def _versions(self):
+        """(version of the f32 buffer, sum of the parameters' own version counters).  Writes through
+        slices of f32 bump the first; in-place writes through a parameter (load_state_dict's copy_,
+        `p.mul_()` under no_grad) bump only that parameter's counter, because `p.data = view` keeps
+        the parameter's own counter — hence both."""
+        return self.f32._version, sum(p._version for p in self.params)
+
     def refresh_bf16(self):
-        """Re-cast the bf16 shadow if the masters changed (optimizer step, load_state_dict, ...).
-        Views share the base's version counter, so one check covers every parameter."""
-        v = self.f32._version
+        """Re-cast the bf16 shadow if the masters changed (optimizer step, load_state_dict, ...)."""
+        v = self._versions()
         if v != self._bf16_version:
             K.cast_bf16(self.f32, self.bf16)
-            self._bf16_version = self.f32._version
+            self._bf16_version = self._versions()
 
     def mark_bf16_fresh(self):
-        self._bf16_version = self.f32._version
+        self._bf16_version = self._versions()
+
+    def master_version(self):
+        """Changes whenever any master weight changed (the optimizer's norm cache key)."""
+        return self._versions()
 
     def attach_grads(self, zero=False):
         """Make every p.grad the flat view (torch's zero_grad(set_to_none=True) drops them)."""

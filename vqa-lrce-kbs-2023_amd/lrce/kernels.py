@@ -267,7 +267,7 @@ def wattn_fwd(qkv, bias_fwd, win_pat, out, lse, n_win, n, nH):
     # algorithmic work: QK^T + PV = 4 n^2 d per (window, head), d = 32
     _timed("wattn_fwd", out, lambda: call("lrce_wattn_fwd", ptr(qkv), ptr(bias_fwd), ptr(win_pat), ptr(out), ptr(lse),
                                            n_win, n, nH, stream_of(out)),
-           flops=4.0 * n * n * 32 * n_win * nH)
+           flops=4.0 * n * n * 32 * n_win * nH, nbytes=8.0 * n * 32 * n_win * nH)
 
 
 WATTN_GROUP = 4   # windows per workgroup of lrce_wattn_fwd_grouped
@@ -293,10 +293,11 @@ def wattn_groups(win_pat, n_win, device):
 
 
 def wattn_fwd_grouped(qkv, bias_fwd, groups, out, lse, n_win, n, nH):
+    # algorithmic bytes: Q, K, V read + O written, bf16: 8 n d per (window, head)
     win_list, grp_pat, n_groups = groups
     _timed("wattn_fwd", out, lambda: call("lrce_wattn_fwd_grouped", ptr(qkv), ptr(bias_fwd), ptr(win_list), ptr(grp_pat),
                                            n_groups, ptr(out), ptr(lse), n_win, n, nH, stream_of(out)),
-           flops=4.0 * n * n * 32 * n_win * nH, key=(n_win, nH))
+           flops=4.0 * n * n * 32 * n_win * nH, nbytes=8.0 * n * 32 * n_win * nH, key=(n_win, nH))
 
 
 def wattn_bwd(qkv, out, dout, lse, bias_bwd, win_pat, dqkv, ds, n_win, n, nH):

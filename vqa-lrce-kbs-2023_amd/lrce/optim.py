@@ -35,7 +35,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros_like(flat.f32)
         self.sumsq = torch.zeros(len(flat.params), device=dev)        # ||p_t||^2 of the current parameters
         self.sumsq_next = torch.zeros(len(flat.params), device=dev)   # accumulated by the update kernel
-        self._norm_version = None   # flat.f32._version the norms belong to (None: never computed)
+        self._norm_version = None   # flat.master_version() the norms belong to (None: never computed)
         self._index = {id(p): i for i, p in enumerate(flat.params)}
         self.tensor_lr = torch.zeros(len(flat.params), device=dev)
         self._lr_cache = None
@@ -64,7 +64,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.step_t.add_(1.0)
         b1, b2 = self.defaults["betas"]
         t = self.step_count
-        if self._norm_version != flat.f32._version:
+        if self._norm_version != flat.master_version():
             # parameters changed outside the optimizer (init / load): one norm pass; afterwards the
             # update kernel itself produces the next step's norms
             K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params))
@@ -74,13 +74,23 @@ class FusedAdamW(torch.optim.Optimizer):
                      float(grad_scale), self.reg_strength, 1.0 - b1 ** t, 1.0 - b2 ** t, step=self.step_t,
                      sumsq_next=self.sumsq_next)
         self.sumsq.copy_(self.sumsq_next)
-        self._norm_version = flat.f32._version
+        self._norm_version = flat.master_version()
         flat.mark_bf16_fresh()
         return loss
 
     def l2_term(self):
         """sum_t ||p_t||_2 of the current parameters (device scalar; no sync)."""
         return self.sumsq.sqrt().sum()
+
+    @torch.no_grad()
+    def l2_value(self):
+        """The reference's calculate_l2_reg() value (agent_base.py:103-108) for the parameters as they
+        are now: the update kernel's norms when they are current, else one multi-tensor norm pass."""
+        flat = self.flat
+        if self._norm_version != flat.master_version():
+            K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params))
+            self._norm_version = flat.master_version()
+        return self.l2_term()
 
     def zero_grad(self, set_to_none=False):
         self.flat.grad.zero_()
