@@ -151,6 +151,12 @@ int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dou
                    int n_win, int n, int nH, void* stream);
 int lrce_wattn_dbias(const uint16_t* ds_scratch, int n_win, int n, int nH, const int64_t* index, int index_ld,
                      float* table_grad, void* stream);
+/* Same bias-table gradient without atomics: csr_off int32 [n_bins+1] / csr_el int32 list, per table
+ * row, the positions (per-lane tile order, 25 tiles x 1024) of the (query, key) pairs whose
+ * relative_position_index is that row (built once per stage geometry: lrce.kernels.wattn_dbias_csr).
+ * Deterministic: every table entry is written by one thread. */
+int lrce_wattn_dbias_csr(const uint16_t* ds_scratch, int n_win, int nH, const int32_t* csr_off, const int32_t* csr_el,
+                         int n_bins, float* table_grad, void* stream);
 
 /* ---------------------------------------------------------------- small multi-head attention
  * Masked SDPA, head_dim 64, for BERT self-attention (text.py:12-17 -> HF BertSelfAttention, L<=64)

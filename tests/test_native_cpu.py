@@ -48,3 +48,25 @@ def test_kernels_refuse_cpu_tensors():
     x = torch.zeros(8, 8, dtype=torch.bfloat16)
     with pytest.raises(_native.NativeError):
         kernels.linear(x, x)
+
+
+def test_dbias_csr_inverts_relative_position_index():
+    """The bias-gradient CSR (host-built) lists every valid (query, key) pair of the padded 160x160
+    per-lane tile layout exactly once, under its relative_position_index row, ascending per row."""
+    import torch
+    from lrce import kernels as K
+    from lrce.feature_extractor.video_swin import relative_position_index
+    n = 147
+    index = relative_position_index((8, 7, 7))
+    off, el, n_bins = K.wattn_dbias_csr(index, n, 2535)
+    assert n_bins == 2535 and off.shape == (2536,) and int(off[-1]) == n * n == el.numel()
+    assert el.unique().numel() == el.numel()
+    reg, lane, tile = el & 15, (el >> 4) & 63, el // 1024
+    qi = (tile // 5) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+    kj = (tile % 5) * 32 + (lane & 31)
+    assert int(qi.max()) < n and int(kj.max()) < n
+    rows = torch.repeat_interleave(torch.arange(2535), (off[1:] - off[:-1]).long())
+    assert torch.equal(index[qi.long(), kj.long()], rows)
+    for b in range(0, 2535, 97):
+        seg = el[off[b]:off[b + 1]]
+        assert torch.equal(seg, seg.sort().values)

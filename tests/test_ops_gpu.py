@@ -326,6 +326,9 @@ def test_window_attention_fwd_bwd(nH, n_win):
     k.wattn_bwd(qkv, out, dout, lse, bb_, win_pat, dqkv, ds, n_win, n, nH)
     tg = torch.zeros(2535, nH, device=dev)
     k.wattn_dbias(ds, n_win, n, nH, index, tg)
+    tg2 = torch.zeros(2535, nH, device=dev)   # atomic-free CSR gather (the product path)
+    k.wattn_dbias_gather(ds, n_win, nH, k.wattn_dbias_csr(index, n, 2535), tg2)
+    assert rel(tg2, tab.grad) < 2e-2 and rel(tg2, tg) < 1e-5
     d = dqkv.float().view(n_win, n, 3, nH, hd).permute(2, 0, 3, 1, 4)
     assert rel(d[0], q.grad) < 2e-2
     assert rel(d[1], kk.grad) < 2e-2

@@ -367,25 +367,34 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restri
   const float* bias_ph = biasf + (long long)(pat * nH + h) * PH_ELEMS;
   const int hh = lane >> 5, r32 = lane & 31;
 
-  // LDS-DMA issue helpers (lane-linear destinations, 1 KB per wave-instruction); ASM: hidden from hipcc
+  // LDS-DMA issue helpers (lane-linear destinations, 1 KB per wave-instruction); ASM: hidden from hipcc.
+  // Per-lane source offsets are loop-invariant 32-bit element offsets; only the query-tile term
+  // (a multiple of the row stride) changes per tile, so the loop body does one add per address.
   const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const float* bias_lane = bias_ph + wv * 5 * 256 + lane * 4;
+  int qoff[2], qoff_last[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = i * 16 + (lane >> 2), pos = lane & 3;
+    const int c = pos ^ ((row >> 2) & 3);
+    qoff[i] = row * (int)ld + h * HD + c * 8;                                   // tiles 0..3: never clamped
+    qoff_last[i] = min((NTILE - 1) * TQ + row, n - 1) * (int)ld + h * HD + c * 8;   // tile 4: rows >= n clamped
+  }
   auto issue_bias = [&](int qt, auto asm_c) {   // 20 x 1 KB, 5 per wave
-    const float* src = bias_ph + (long long)qt * BIAS_ROW;
+    const float* src = bias_lane + qt * BIAS_ROW;
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       const int ins = wv * 5 + i;
-      if constexpr (decltype(asm_c)::value) glds16_asm(src + ins * 256 + lane * 4, lds_u32(S.bias + ins * 256));
-      else glds16w(src + ins * 256 + lane * 4, S.bias + ins * 256);
+      if constexpr (decltype(asm_c)::value) glds16_asm(src + i * 256, lds_u32(S.bias + ins * 256));
+      else glds16w(src + i * 256, S.bias + ins * 256);
     }
   };
   auto issue_q = [&](int qt, auto asm_c) {      // 32 rows x 64 B = 2 x 1 KB, chunks XOR-swizzled by row (kswz)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int row = i * 16 + (lane >> 2), pos = lane & 3;
-      const int c = pos ^ ((row >> 2) & 3);
-      const int tok = min(qt * TQ + row, n - 1);
-      if constexpr (decltype(asm_c)::value) glds16_asm(base + tok * ld + h * HD + c * 8, lds_u32(&S.q[wv][qt & 1][i * 512]));
-      else glds16w(base + tok * ld + h * HD + c * 8, &S.q[wv][qt & 1][i * 512]);
+      const bf16* src = base + (qt == NTILE - 1 ? qoff_last[i] : qt * TQ * (int)ld + qoff[i]);
+      if constexpr (decltype(asm_c)::value) glds16_asm(src, lds_u32(&S.q[wv][qt & 1][i * 512]));
+      else glds16w(src, &S.q[wv][qt & 1][i * 512]);
     }
   };
   constexpr std::false_type BUILTIN{};
@@ -409,9 +418,23 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restri
     for (int s = 0; s < 2; ++s) kf[kt][s] = (valid && key < n) ? ld_row16(base + key * ld + C + h * HD + 16 * s + 8 * hh) : bf16x8{};
   }
 
+  // The output rows of tile qt are stored one iteration late (right after the next tile's wait), so
+  // the vmcnt(0) that waits for the next tile's DMA never also waits on this tile's fresh stores.
+  bf16x4 pend[4];
+  float pend_lse = 0.f;
+  int pend_qi = NPAD;   // >= n: nothing pending
+  auto flush = [&]() {
+    if (valid && pend_qi < n) {
+      bf16* dst = out + ((long long)w * n + pend_qi) * C + h * HD + 4 * hh;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) *reinterpret_cast<bf16x4*>(dst + 8 * rr) = pend[rr];
+      if (hh == 0) lse[((long long)w * nH + h) * NPAD + pend_qi] = pend_lse;
+    }
+  };
   for (int qt = 0; qt < NTILE; ++qt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA for tile qt (and its stores)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA for tile qt (and tile qt-2's stores)
     __builtin_amdgcn_s_barrier();                        // ... and every other wave's part of the bias row
+    flush();
     f32x16 acc[NTILE];
     {
       const float4* src = reinterpret_cast<const float4*>(S.bias) + lane;
@@ -451,38 +474,39 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restri
       float m = fmaxf(fmaxf(mp[0], mp[1]), fmaxf(mp[2], mp[3]));
       m = fmaxf(m, __shfl_xor(m, 32, 64));
       if (__all(m <= 64.f && m >= -64.f)) m = 0.f;
-      float sp[4] = {0.f, 0.f, 0.f, 0.f};
+      f32x2 sp[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
+      const f32x2 mm = {m, m};
 #pragma unroll
       for (int kt = 0; kt < NTILE; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(acc[kt][r] - m);
-          acc[kt][r] = p;
-          sp[r & 3] += p;
+        for (int r = 0; r < 16; r += 2) {
+          const f32x2 d = f32x2{acc[kt][r], acc[kt][r + 1]} - mm;   // packed subtract / sum: one op per pair
+          const f32x2 p = {__builtin_amdgcn_exp2f(d[0]), __builtin_amdgcn_exp2f(d[1])};
+          acc[kt][r] = p[0];
+          acc[kt][r + 1] = p[1];
+          sp[(r >> 1) & 1] += p;
         }
-      float sum = (sp[0] + sp[1]) + (sp[2] + sp[3]);
+      float sum = (sp[0][0] + sp[0][1]) + (sp[1][0] + sp[1][1]);
       sum += __shfl_xor(sum, 32, 64);
-      f32x16 o = {};
+      f32x16 o0 = {}, o1 = {};   // two independent accumulation chains, summed once
       const bf16* vimg = S.v[wave];
 #pragma unroll
-      for (int kt = 0; kt < NTILE; ++kt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(vimg, kt * TQ + 16 * s, lane), pack8(acc[kt], s), o, 0, 0, 0);
-      if (qi < n) {
-        const float inv = 1.0f / sum;
-        bf16* dst = out + ((long long)w * n + qi) * C + h * HD + 4 * hh;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          bf16x4 v;
-          v[0] = f2bf(o[4 * rr] * inv); v[1] = f2bf(o[4 * rr + 1] * inv);
-          v[2] = f2bf(o[4 * rr + 2] * inv); v[3] = f2bf(o[4 * rr + 3] * inv);
-          *reinterpret_cast<bf16x4*>(dst + 8 * rr) = v;
-        }
-        if (hh == 0) lse[((long long)w * nH + h) * NPAD + qi] = m + __log2f(sum);
+      for (int kt = 0; kt < NTILE; ++kt) {
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(vimg, kt * TQ, lane), pack8(acc[kt], 0), o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(vimg, kt * TQ + 16, lane), pack8(acc[kt], 1), o1, 0, 0, 0);
       }
+      const f32x16 o = o0 + o1;
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        pend[rr][0] = f2bf(o[4 * rr] * inv); pend[rr][1] = f2bf(o[4 * rr + 1] * inv);
+        pend[rr][2] = f2bf(o[4 * rr + 2] * inv); pend[rr][3] = f2bf(o[4 * rr + 3] * inv);
+      }
+      pend_lse = m + __log2f(sum);
+      pend_qi = qi;
     }
   }
+  flush();
 }
 
 // ------------------------------------------------------------------------------ backward
@@ -690,6 +714,61 @@ __global__ void dbias_scatter_kernel(const float* __restrict__ part, int chunks,
   atomicAdd(tgrad + index[(long long)qi * ld + kj] * nH + h, s);
 }
 
+// Deterministic, atomic-free variant of the scatter: (1) sum the chunk partials in place into
+// chunk 0 (coalesced float4), (2) one thread per (table row, head) gathers the elements that use
+// that row through a CSR built once per stage geometry (csr_off [n_bins+1], csr_el = element
+// positions in per-lane tile order, ascending within a row) and adds the sum to its gradient entry —
+// each entry has exactly one writer, so no atomics and no run-to-run variation.
+__global__ void dbias_reduce_kernel(float* __restrict__ part, int chunks, long long per_chunk) {
+  const long long e4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e4 >= per_chunk) return;
+  float4 s = *reinterpret_cast<const float4*>(part + e4);
+  for (int c = 1; c < chunks; ++c) {
+    const float4 v = *reinterpret_cast<const float4*>(part + c * per_chunk + e4);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  *reinterpret_cast<float4*>(part + e4) = s;
+}
+
+__global__ void dbias_gather_kernel(const float* __restrict__ red, int nH, const int* __restrict__ csr_off,
+                                    const int* __restrict__ csr_el, int n_bins, float* __restrict__ tgrad) {
+  // one wave per table row: lanes split the row's elements (<= 3 per lane for 147-token windows),
+  // heads loop inside (independent loads), one cross-lane sum per head
+  const int lane = threadIdx.x & 63;
+  const int bin = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (bin >= n_bins) return;
+  const int k0 = csr_off[bin], k1 = csr_off[bin + 1];
+  if (k0 == k1) return;
+  int els[3];
+  int cnt = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int k = k0 + lane + 64 * i;
+    els[i] = k < k1 ? csr_el[k] : -1;
+  }
+  for (int k = k0 + lane + 192; k < k1; k += 64) ++cnt;   // tail of rows longer than 192 entries (larger windows)
+  for (int h0 = 0; h0 < nH; h0 += 4) {     // 4 heads in flight (nH is a multiple of 4 in Swin-B)
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (h0 + j >= nH) break;
+      const float* r = red + (long long)(h0 + j) * PH_ELEMS;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) s[j] += els[i] >= 0 ? r[els[i]] : 0.f;
+      if (cnt)
+        for (int k = k0 + lane + 192; k < k1; k += 64) s[j] += r[csr_el[k]];
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] += __shfl_xor(s[j], o, 64);
+    if (lane < 4 && h0 + lane < nH) {
+      const float v = lane == 0 ? s[0] : lane == 1 ? s[1] : lane == 2 ? s[2] : s[3];
+      tgrad[(long long)bin * nH + h0 + lane] += v;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int64_t lrce_wattn_bias_elems(int n_pat, int nH) { return (int64_t)n_pat * nH * PH_ELEMS; }
@@ -749,6 +828,25 @@ extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const ui
       reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const bf16*>(out), reinterpret_cast<const bf16*>(dout), lse, bias_bwd,
       win_pat, reinterpret_cast<bf16*>(dqkv), reinterpret_cast<bf16*>(ds_scratch), n_win, n, nH, scale);
   return lrce_check_launch("wattn_bwd");
+}
+
+extern "C" int lrce_wattn_dbias_csr(const uint16_t* ds_scratch, int n_win, int nH, const int32_t* csr_off,
+                                    const int32_t* csr_el, int n_bins, float* table_grad, void* stream) {
+  if (!ds_scratch || !csr_off || !csr_el || !table_grad) return lrce_fail(LRCE_E_ARG, "wattn_dbias_csr: null pointer");
+  if (n_win <= 0 || nH <= 0 || n_bins <= 0) return lrce_fail(LRCE_E_ARG, "wattn_dbias_csr: n_win=%d nH=%d", n_win, nH);
+  const long long per_chunk = (long long)nH * PH_ELEMS;
+  const long long groups = (per_chunk / 8 + 255) / 256;
+  int chunks = (int)((2048 + groups - 1) / groups);
+  chunks = max(1, min(min(chunks, DB_CHUNKS), n_win));
+  const int per = (n_win + chunks - 1) / chunks;
+  chunks = (n_win + per - 1) / per;
+  const bf16* ds = reinterpret_cast<const bf16*>(ds_scratch);
+  float* part = reinterpret_cast<float*>(const_cast<bf16*>(ds) + (long long)n_win * per_chunk);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  dbias_partial_kernel<<<dim3((unsigned)groups, chunks), 256, 0, st>>>(ds, n_win, nH, part, per);
+  if (chunks > 1) dbias_reduce_kernel<<<(unsigned)((per_chunk / 4 + 255) / 256), 256, 0, st>>>(part, chunks, per_chunk);
+  dbias_gather_kernel<<<(unsigned)((n_bins + 3) / 4), 256, 0, st>>>(part, nH, csr_off, csr_el, n_bins, table_grad);
+  return lrce_check_launch("wattn_dbias_csr");
 }
 
 extern "C" int lrce_wattn_dbias(const uint16_t* ds_scratch, int n_win, int n, int nH, const int64_t* index, int index_ld,

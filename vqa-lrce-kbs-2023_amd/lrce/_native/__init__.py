@@ -89,6 +89,7 @@ _SIGS = {
     "lrce_wattn_fwd_grouped": [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_dbias": [_P, _I, _I, _I, _P, _I, _P, _P],
+    "lrce_wattn_dbias_csr": [_P, _I, _I, _P, _P, _I, _P, _P],
     "lrce_mha_fwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_mha_bwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_patch_im2col": [_P, _I, _I, _I, _I, _I64, _I64, _I64, _I, _P, _P],

@@ -275,6 +275,17 @@ def _wgrad(flat, lin, dy16, x16):
         K.colsum(dy16, gb)
 
 
+def _dbias_csr(at, n):
+    """Bias-table gradient CSR of one attention module, cached against its index buffer's identity."""
+    idx = at.relative_position_index
+    key = (idx.data_ptr(), idx._version, n, idx.device)
+    hit = getattr(at, "_lrce_dbias_csr", None)
+    if hit is None or hit[0] != key:
+        hit = (key, K.wattn_dbias_csr(idx, n, at.relative_position_bias_table.shape[0]))
+        object.__setattr__(at, "_lrce_dbias_csr", hit)
+    return hit[1]
+
+
 class _SwinBlockFn(torch.autograd.Function):
     """One SwinTransformerBlock3D (video_swin_ori.py:248-306) forward / backward."""
 
@@ -346,7 +357,7 @@ class _SwinBlockFn(torch.autograd.Function):
         del do, o
         gt = _g(flat, at.relative_position_bias_table)
         if gt is not None:
-            K.wattn_dbias(ds, geo.n_win, n, nH, at.relative_position_index, gt)
+            K.wattn_dbias_gather(ds, geo.n_win, nH, _dbias_csr(at, n), gt)
         del ds
         _wgrad(flat, at.qkv, dqkv, xw)
         dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight))

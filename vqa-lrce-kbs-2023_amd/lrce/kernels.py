@@ -315,6 +315,37 @@ def wattn_dbias(ds, n_win, n, nH, index, table_grad):
     call("lrce_wattn_dbias", ptr(ds), n_win, n, nH, ptr(index), index.shape[-1], ptr(table_grad), stream_of(table_grad))
 
 
+def wattn_dbias_csr(index, n, n_bins):
+    """Inverse of relative_position_index[:n, :n] in the kernels' per-lane tile order: for every
+    table row, the positions of the (query, key) pairs using it, ascending (csr_off, csr_el int32,
+    on index's device).  Built once per (block, geometry) on the host: index is a constant buffer."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("wattn_dbias_csr: build the bias-gradient CSR before HIP-graph capture (run one eager step)")
+    idx = index.detach().to("cpu", torch.int64)
+    el = torch.arange(25 * 1024)
+    reg, lane, tile = el & 15, (el >> 4) & 63, el // 1024
+    qt, kt = tile // 5, tile % 5
+    qi = qt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+    kj = kt * 32 + (lane & 31)
+    valid = (qi < n) & (kj < n)
+    el, qi, kj = el[valid], qi[valid], kj[valid]
+    bins = idx[qi, kj]
+    if int(bins.min()) < 0 or int(bins.max()) >= n_bins:
+        raise ValueError("relative_position_index entry outside the bias table")
+    order = torch.sort(bins, stable=True).indices
+    csr_el = el[order].to(torch.int32)
+    counts = torch.bincount(bins, minlength=n_bins)
+    csr_off = torch.zeros(n_bins + 1, dtype=torch.int32)
+    csr_off[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return csr_off.to(index.device), csr_el.to(index.device), n_bins
+
+
+def wattn_dbias_gather(ds, n_win, nH, csr, table_grad):
+    csr_off, csr_el, n_bins = csr
+    call("lrce_wattn_dbias_csr", ptr(ds), n_win, nH, ptr(csr_off), ptr(csr_el), n_bins, ptr(table_grad),
+         stream_of(table_grad))
+
+
 def mha_desc(q, Lq, *, k1, v1, lk1, ld_kv1, stride_kv1_b, kv1_bdiv=1, k2=None, v2=None, lk2=0, ld_kv2=0,
              stride_kv2_b=0, kv2_bdiv=1, key_mask=None, out, lse, B, H, scale, ld_q=None, ld_o=None, drop_p=0.0,
              seed=0, d=64):
@@ -429,6 +460,8 @@ def rng_offset(device):
     """The device RNG offset (int64 scalar) registered with lrce_set_rng_offset (one per process:
     the native library keeps a single pointer, so the first device registered wins)."""
     dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:   # "cuda" and "cuda:0" must name the same offset
+        dev = torch.device("cuda", torch.cuda.current_device())
     t = _RNG_OFFSETS.get(dev)
     if t is None:
         t = torch.zeros(1, dtype=torch.int64, device=dev)
