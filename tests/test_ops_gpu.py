@@ -129,6 +129,11 @@ def test_gemm_f32_skinny_epilogues(M):
     assert rel(dgp, ((dy.double() @ w2.double()) * pr.grad).float()) < 1e-5
     dx = k.linear_dx(dgp, w1, resid=res)
     assert rel(dx, (dgp.double() @ w1.double() + res.double()).float()) < 1e-5
+    # N = 768 launches split K across workgroups (last arriver reduces in split order): repeated
+    # launches — the arrival counters must reset themselves — give bit-identical results
+    for _ in range(3):
+        assert torch.equal(k.linear_dx(dgp, w1, resid=res), dx)
+        assert torch.equal(k.linear(g, w2, None, resid=res, out_f32=True), y)
 
 
 def test_gemm_epilogues_and_maps():

@@ -5,6 +5,9 @@
 // dominant rounding error of the recurrence (36 sequential layer-steps).
 // Same operand layouts / epilogues / split-K contract as lrce_gemm's bf16 path.
 // Tile 64x64x32, 256 threads = 4 waves (2x2), 32x32 per wave = 2x2 MFMA blocks of 16x16.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "lrce_capi.h"
 
@@ -186,20 +189,30 @@ __device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, in
 // 8 waves split the reduction; each wave issues all loads of a trip of TS k-steps (16 deep) before
 // its MFMAs, so a whole 768-deep reduction is one memory round trip per wave.
 // (8 waves: a 16-wave variant measured slower on the 3072-deep decoder linear2, 18.8 vs ~9 us)
+// Split-K (gridDim.y = KS > 1): workgroup (tile, ks) reduces k in [ks*kspan, (ks+1)*kspan), stores
+// its 16 x 16*MT partial to `part`, and the LAST workgroup of the tile to arrive (device-scope
+// counter, reset by that workgroup: graph-replay safe) sums the KS partials in ks order and runs
+// the epilogue — so nonlinear epilogues (GELU, dGELU, residual) still see the full sum, and the
+// result does not depend on arrival order.  Narrow-N decoder linears (N = 768 -> 48 tiles) get
+// 3-4x the workgroups, deep ones (K = 3072) a quarter of the reduction per workgroup.
 template <int MT, bool B_KM, int SK_WAVES>
-__global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p) {
+__global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p, float* __restrict__ part,
+                                                               unsigned* __restrict__ counters, int kspan) {
   constexpr int TS = MT <= 2 ? 8 : 4;
   constexpr int NPART = SK_WAVES * 64 / 256;   // 256-thread groups finishing the m-tiles
   __shared__ float red[SK_WAVES][MT][16][17];
+  __shared__ unsigned last_flag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const int n = n0 + col;
   const bool n_ok = n < p.n;
   const int nc = n_ok ? n : 0;
-  int kchunk = (p.k + SK_WAVES - 1) / SK_WAVES;
+  const int ks = blockIdx.y, KS = gridDim.y;
+  const int kbase = ks * kspan, kend = min(p.k, kbase + kspan);
+  int kchunk = (kend - kbase + SK_WAVES - 1) / SK_WAVES;
   kchunk = (kchunk + 15) & ~15;
-  const int kb = wave * kchunk, ke = min(p.k, kb + kchunk);
+  const int kb = kbase + wave * kchunk, ke = min(kend, kb + kchunk);
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -240,18 +253,51 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][t][grp * 4 + r][col] = acc[t][r];
   __syncthreads();
-  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, part = threadIdx.x >> 8;
+  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, grp256 = threadIdx.x >> 8;
+  if (KS == 1) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      if (t % NPART != grp256) continue;   // 256-thread group g finishes m-tiles t = g (mod NPART)
+      const int m = t * 16 + ml, nn = n0 + nl;
+      if (m < p.m && nn < p.n) {
+        float x = 0.f;
+#pragma unroll
+        for (int w = 0; w < SK_WAVES; ++w) x += red[w][t][ml][nl];
+        sk_epilogue(p, x, m, nn);
+      }
+    }
+    return;
+  }
+  // split-K: partial tile -> part[tile][ks][t][16][16]; the last arriver reduces + epilogue
+  float* mine = part + ((long long)blockIdx.x * KS + ks) * (MT * 256);
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
-    if (t % NPART != part) continue;   // 256-thread group g finishes m-tiles t = g (mod NPART)
-    const int m = t * 16 + ml, nn = n0 + nl;
-    if (m < p.m && nn < p.n) {
-      float x = 0.f;
+    if (t % NPART != grp256) continue;
+    float x = 0.f;
 #pragma unroll
-      for (int w = 0; w < SK_WAVES; ++w) x += red[w][t][ml][nl];
-      sk_epilogue(p, x, m, nn);
-    }
+    for (int w = 0; w < SK_WAVES; ++w) x += red[w][t][ml][nl];
+    // agent-scope relaxed stores go to the device coherence point (not this XCD's L2), so no L2
+    // writeback fence (buffer_wbl2) is needed; the vmcnt wait below orders them before the counter
+    __hip_atomic_store(mine + t * 256 + ml * 16 + nl, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last_flag = __hip_atomic_fetch_add(&counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                (unsigned)(KS - 1);
+  __syncthreads();
+  if (!last_flag) return;
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    if (t % NPART != grp256) continue;
+    const int m = t * 16 + ml, nn = n0 + nl;
+    float x = 0.f;
+    float* src = part + (long long)blockIdx.x * KS * (MT * 256) + t * 256 + ml * 16 + nl;
+    for (int j = 0; j < KS; ++j) x += __hip_atomic_load(src + j * (MT * 256), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (m < p.m && nn < p.n) sk_epilogue(p, x, m, nn);
+  }
+  if (threadIdx.x == 0)   // ready for the next launch / graph replay
+    __hip_atomic_store(&counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // C[m][n] (+)= alpha * sum_{r < R} A[r][m] * B[r][n] with R <= 256 (dW of a skinny linear):
@@ -301,6 +347,48 @@ __global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
 
 }  // namespace
 
+namespace {
+bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && *v && *v != '0';
+}
+
+// Per-device split-K scratch of the skinny kernel: partial tiles + zero-initialised arrival
+// counters (self-resetting).  Allocated once, outside stream capture; one stream per device uses it
+// at a time (kernels on one stream serialise), so reuse across launches is race-free.
+struct SkinnySplitWs {
+  float* part = nullptr;
+  unsigned* counters = nullptr;
+  long long part_elems = 0;
+  int n_counters = 0;
+};
+constexpr long long SK_PART_ELEMS = 192LL * 4 * 4 * 256;   // tiles x KS x MT x 256 (max shapes routed here)
+constexpr int SK_COUNTERS = 4096;
+
+SkinnySplitWs* skinny_split_ws(hipStream_t st, int tiles, int ks, int mt) {
+  static SkinnySplitWs per_dev[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SkinnySplitWs& w = per_dev[dev];
+  if (!w.part) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    if (hipMalloc(&w.part, SK_PART_ELEMS * sizeof(float)) != hipSuccess) { w.part = nullptr; return nullptr; }
+    if (hipMalloc(&w.counters, SK_COUNTERS * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(w.counters, 0, SK_COUNTERS * sizeof(unsigned)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(w.part);
+      w.part = nullptr;
+      return nullptr;
+    }
+    w.part_elems = SK_PART_ELEMS;
+    w.n_counters = SK_COUNTERS;
+  }
+  if ((long long)tiles * ks * mt * 256 > w.part_elems || tiles > w.n_counters) return nullptr;
+  return &w;
+}
+}  // namespace
+
 // the dW shape the outer-product kernel takes: A M-major, B N-major, reduction <= 256 rows
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d) {
   return d->b_f32 && d->a_f32 && !d->a_kmajor && !d->b_kmajor && d->k <= 256 && (d->n % 4) == 0 && (d->ldc % 4) == 0 &&
@@ -337,10 +425,24 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
     if (d->a_kmajor && d->m <= 64 && (reinterpret_cast<uintptr_t>(d->a) & 15) == 0 &&
         (!d->b_kmajor || (reinterpret_cast<uintptr_t>(d->b) & 15) == 0)) {
       const int mt = (d->m + 15) / 16;
-      dim3 grid((d->n + 15) / 16);
-#define LRCE_SK(MT)                                                                          \
-  if (d->b_kmajor) skinny_kernel<MT, true, 8><<<grid, 8 * 64, 0, st>>>(q);                   \
-  else skinny_kernel<MT, false, 8><<<grid, 8 * 64, 0, st>>>(q);
+      const int tiles = (d->n + 15) / 16;
+      // split K for deep reductions (K >= 2048: the decoder FFN linear2 / linear1-dX) while the grid is under
+      // ~192 workgroups (A/B on the full step: splitting the K = 768 linears too cost 0.4 %, K >= 2048 gained 1.4 %)
+      int ks = 1;
+      SkinnySplitWs* ws = nullptr;
+      static const int min_k = getenv("LRCE_SKINNY_MINK") ? atoi(getenv("LRCE_SKINNY_MINK")) : 2048;
+      if (tiles < 192 && d->k >= min_k && !getenv_flag("LRCE_SKINNY_NOSPLIT")) {
+        ks = std::min(std::min(4, d->k / 256), std::max(1, 192 / tiles));
+        if (ks > 1 && !(ws = skinny_split_ws(st, tiles, ks, mt))) ks = 1;
+      }
+      int kspan = (d->k + ks - 1) / ks;
+      kspan = (kspan + 15) & ~15;
+      dim3 grid(tiles, ks);
+      float* part = ws ? ws->part : nullptr;
+      unsigned* ctr = ws ? ws->counters : nullptr;
+#define LRCE_SK(MT)                                                                                   \
+  if (d->b_kmajor) skinny_kernel<MT, true, 8><<<grid, 8 * 64, 0, st>>>(q, part, ctr, kspan);          \
+  else skinny_kernel<MT, false, 8><<<grid, 8 * 64, 0, st>>>(q, part, ctr, kspan);
       switch (mt) {
         case 1: LRCE_SK(1) break;
         case 2: LRCE_SK(2) break;
