@@ -847,26 +847,37 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     // 128x128 tiles when they give every CU work; 64x64 otherwise (small-M / small-N problems)
     const int t128 = p.tiles_m * p.tiles_n * d->batch * split;
     const bool small = g_gemm_tile == 64 || (g_gemm_tile == 0 && t128 < 256);
-    // 192x128 tiles (K-major A): 1.5x the work per tile, so fewer rounds of the 2-blocks-per-CU
-    // grid when the 128x128 tile count overshoots a round (e.g. 552 tiles on 512 slots -> 368)
-    bool tall = false;
+    // Taller tiles (K-major A only): 160 or 192 rows x 128 do 1.25x / 1.5x the work of a 128x128
+    // tile, so they win when the 128-row tile count overshoots a round of the 2-blocks-per-CU grid.
+    // Pick the height minimising rounds x rows (e.g. M 17 640, N 512: 552 -> 444 tiles in ONE round
+    // at 160 rows; N 2048: 3 rounds of 192-row tiles beat 4 of 160 and 5 of 128).
+    int tall_m = 0;
     if (!small && d->a_kmajor && g_gemm_tile != 128) {
       const int slots = 2 * 256;
-      const long long t192 = (long long)((d->m + 191) / 192) * p.tiles_n * d->batch * split;
-      const long long r128 = (t128 + slots - 1) / slots, r192 = (t192 + slots - 1) / slots;
-      tall = g_gemm_tile == 192 || 2 * r128 > 3 * r192;
+      const bool atomic_rows = (d->flags & LRCE_EPI_ATOMIC) && !p.ws;   // its LDS-slab epilogue wants an even row-block count
+      long long best = (long long)((t128 + slots - 1) / slots) * 128;
+      for (int h : {160, 192}) {
+        if (h == 160 && atomic_rows) continue;
+        const long long th = (long long)((d->m + h - 1) / h) * p.tiles_n * d->batch * split;
+        const long long cost = (th + slots - 1) / slots * h;
+        if (g_gemm_tile == h || (g_gemm_tile == 0 && cost < best)) { best = cost; tall_m = h; }
+        if (g_gemm_tile == h) break;
+      }
     }
     if (small) {
       p.tiles_m = (d->m + 63) / 64; p.tiles_n = (d->n + 63) / 64;
       grid = dim3(p.tiles_m * p.tiles_n, d->batch * split);
-    } else if (tall) {
-      p.tiles_m = (d->m + 191) / 192;
+    } else if (tall_m) {
+      p.tiles_m = (d->m + tall_m - 1) / tall_m;
       grid = dim3(p.tiles_m * p.tiles_n, d->batch * split);
     }
-    const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0) | (small ? 4 : 0) | (tall ? 8 : 0);
+    const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0) | (small ? 4 : 0) | (tall_m == 192 ? 8 : 0) |
+                   (tall_m == 160 ? 16 : 0);
     switch (gk) {
       case 11: gemm_glds_kernel<192, 128, true, true><<<grid, NT, 0, s>>>(p); break;
       case 10: gemm_glds_kernel<192, 128, true, false><<<grid, NT, 0, s>>>(p); break;
+      case 19: gemm_glds_kernel<160, 128, true, true><<<grid, NT, 0, s>>>(p); break;
+      case 18: gemm_glds_kernel<160, 128, true, false><<<grid, NT, 0, s>>>(p); break;
       case 3: gemm_glds_kernel<128, 128, true, true><<<grid, NT, 0, s>>>(p); break;
       case 2: gemm_glds_kernel<128, 128, true, false><<<grid, NT, 0, s>>>(p); break;
       case 1: gemm_glds_kernel<128, 128, false, true><<<grid, NT, 0, s>>>(p); break;
