@@ -212,6 +212,12 @@ int lrce_mha_bwd(const LrceMhaDesc* desc, void* stream);
  * patches: bf16 [n_clips*D'*H'*W'][96], rows (n, d, h, w), cols (c, kt, kh, kw). */
 int lrce_patch_im2col(const float* clips, int n_clips, int T, int H, int W, int64_t s_clip, int64_t s_t, int64_t s_c,
                       int normalize, uint16_t* patches, void* stream);
+/* Clip assembly (e2e_dataset.py:60-116 -> torchvision Resize((h, w)) on PIL + ToTensor): frames is
+ * uint8 [n_frames][H][W][3] (decoded RGB); output clip-frame f is frame frame_idx[f] (0 <= idx <
+ * n_frames, the caller's multi-scale selection) resampled with Pillow's antialiased BILINEAR filter,
+ * bit-exact, and written as f32 [n_out][3][out_h][out_w] in [0, 1]. */
+int lrce_frames_resize(const uint8_t* frames, int n_frames, int H, int W, const int32_t* frame_idx, int n_out, int out_h,
+                       int out_w, float* out, void* stream);
 /* column sums: out[n] += sum_m x[row_map[m]][n] * row_scale[m / rows_per_scale] (x f32 or bf16; map and
  * scale optional): bias gradients (nn.Linear bias, incl. DropPath-scaled branches) */
 int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, int m, int n, const float* row_scale,

@@ -1,5 +1,7 @@
 """Pin the CPU oracle (oracle/lrce_oracle.py) against golden vectors produced by running the
 reference implementation itself (tests/golden/make_golden.py).  CPU only."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -217,3 +219,32 @@ def test_e2e_golden(name, task, L, ncls):
         y = O.e2e_forward(sd, clips, torch.from_numpy(g["ids"]), torch.from_numpy(g["mask"]),
                           torch.from_numpy(g["types"]), task)
     assert rel(y, torch.from_numpy(g["logits"])) < 1e-4
+
+
+def test_pil_bilinear_restatement_matches_pillow_fixture():
+    """oracle/video_resize.py (Pillow's fixed-point antialiased bilinear) == Pillow 12.2.0's output."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_video_golden import CASES, frames_for
+    from oracle.video_resize import pil_bilinear_resize
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "frames_resize.npz"))
+    for name, n, h, w, pick, oh, ow in CASES:
+        fr = frames_for(name, n, h, w)
+        assert np.array_equal(pil_bilinear_resize(fr[pick], oh, ow), g[name]), name
+
+
+def test_multiscale_indices_restatement():
+    """16 frames, 5 per clip, scale 3 -> frames 0-4, 5-9, 10-14; product == oracle."""
+    from oracle.video_resize import multiscale_frame_indices as ref
+    from lrce.dataset.video import multiscale_frame_indices as ours, extracted_scale_index
+    assert ref(16, 5, [3]) == list(range(15))
+    for T in (5, 6, 9, 16, 17, 40, 121, 300):
+        for ts in ([1], [2], [3], [1, 2, 3], [3, 1]):
+            try:
+                r = ref(T, 5, ts)
+            except AssertionError:
+                with pytest.raises(ValueError):
+                    ours(T, 5, ts)
+                continue
+            assert ours(T, 5, ts) == r, (T, ts)
+    assert extracted_scale_index([1, 2, 3]) == [0, 1, 2, 3, 4, 5] and extracted_scale_index([3]) == [3, 4, 5]

@@ -92,6 +92,7 @@ _SIGS = {
     "lrce_wattn_dbias_csr": [_P, _I, _I, _P, _P, _I, _P, _P],
     "lrce_mha_fwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_mha_bwd": [ctypes.POINTER(MhaDesc), _P],
+    "lrce_frames_resize": [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P],
     "lrce_patch_im2col": [_P, _I, _I, _I, _I, _I64, _I64, _I64, _I, _P, _P],
     "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _I, _P, _P],
     "lrce_cast_bf16": [_P, _P, _I64, _P],

@@ -307,6 +307,22 @@ def wattn_bwd(qkv, out, dout, lse, bias_bwd, win_pat, dqkv, ds, n_win, n, nH):
            flops=8.0 * n * n * 32 * n_win * nH, key=(n_win, nH))
 
 
+def frames_resize(frames, frame_idx, out_h=224, out_w=224, out=None):
+    """frames uint8 [T, H, W, 3] (device), frame_idx int32 [n] (device, values < T) -> f32
+    [n, 3, out_h, out_w]: Pillow-exact antialiased bilinear resample + ToTensor (csrc/video_io.hip)."""
+    _chk(frames, torch.uint8, "frames")
+    frames = frames.contiguous()
+    _chk(frame_idx, torch.int32, "frame_idx")
+    T, H, W, C = frames.shape
+    if C != 3:
+        raise N.NativeError("frames_resize: frames must be [T, H, W, 3] RGB")
+    n = frame_idx.numel()
+    if out is None:
+        out = torch.empty(n, 3, out_h, out_w, device=frames.device)
+    call("lrce_frames_resize", ptr(frames), T, H, W, ptr(frame_idx), n, out_h, out_w, ptr(out), stream_of(out))
+    return out
+
+
 def wattn_ds_elems(n_win, nH):
     return N.lib().lrce_wattn_ds_elems(n_win, nH)
 
