@@ -287,6 +287,31 @@ def fusion_transformer(video, text, sd, p="fusion_model.fusion_transformer.", n_
     return s
 
 
+def fusion_video(video, sd, p="fusion_model.fusion_transformer.", n_layers=12):
+    """fusionv3.py:70-88 (FusionVideo): the recurrent decoder with the step's video tokens as the only
+    memory.  video (B,S,150,768) -> (B,1,768)."""
+    B, S = video.shape[:2]
+    s = sd[p + "summarization_token"].expand(B, 1, -1)
+    for i in range(S):
+        o = s
+        for k in range(n_layers):
+            o = decoder_layer(o, video[:, i], sd, f"{p}transformer.layers.{k}.")
+        s = _ln(s + o, sd, p + "fusion_layer_norm.", LN_EPS_FUSION)
+    return s
+
+
+def lrce_mc_sim(video_feats, text_feats, sd, p="fusion_model."):
+    """fusionv3.py:301-333 (LRCEMultipleChoiceSim.forward), eval mode: cosine between the projected
+    mean text embedding of each choice and the FusionVideo summary.  text (B,5,L,768) -> (B,5)."""
+    B, n_mc = text_feats.shape[:2]
+    v = _lin(video_feats, sd, p + "projection_layer.")
+    v = video_pos_embed(v, sd, p + "video_pos_embed.")
+    t = text_pos_embed(text_feats.flatten(0, 1), sd, p + "question_pos_embed.")
+    tf = _lin(t.mean(1), sd, p + "text_projection.")
+    vf = fusion_video(v, sd).expand(-1, n_mc, -1).flatten(0, 1)
+    return F.cosine_similarity(tf, vf, dim=1, eps=1e-8).view(B, n_mc)
+
+
 def lrce_head(video_feats, text_feats, sd, task, p="fusion_model."):
     """fusionv3.py:168-198 (OE), 230-265 (MC), 360-369 (Count).
     OE/Count: video_feats (B,S,Tg,49,1024), text (B,L,768).  MC: text (B,5,L,768)."""

@@ -158,6 +158,21 @@ def fusion_fixture(seed):
     np.savez_compressed(os.path.join(HERE, "fusion_mc.npz"), vf_csum=csum(vf1), tf_csum=csum(tf1), y=y1.numpy(), seed=seed)
 
 
+def fusion_mcsim_fixture(seed):
+    """LRCEMultipleChoiceSim (fusionv3.py:268-333): FusionVideo + text projection + cosine."""
+    from lrce.models.fusionv3 import LRCEMultipleChoiceSim
+    r = W.input_rng(seed)
+    m = LRCEMultipleChoiceSim(768, 1, 0.1, (7, 7), 1024, 5, [3], 40)
+    fill(m, "fusion_model.")
+    m.eval()
+    vf = torch.from_numpy(r.standard_normal((2, 3, 3, 49, 1024), dtype=np.float32))
+    tf = torch.from_numpy(r.standard_normal((2, 5, 40, 768), dtype=np.float32))
+    y = m(vf, tf, torch.ones(2, 5, 40, dtype=torch.int64))
+    keys = sorted(m.state_dict())
+    np.savez_compressed(os.path.join(HERE, "fusion_mcsim.npz"), vf_csum=csum(vf), tf_csum=csum(tf), y=y.numpy(),
+                        seed=seed, keys=np.array(keys))
+
+
 def bert_fixture(seed):
     b = transformers.BertModel(transformers.BertConfig())
     fill(b, "text_extractor.bert.")
@@ -194,6 +209,8 @@ if __name__ == "__main__":
         swin_stage_fixture("stage4_7", 3, 1024, 32, 7, False, 14)
         bert_fixture(15)
         fusion_fixture(16)
+    if "mcsim" in which or "ops" in which:
+        fusion_mcsim_fixture(17)
     if "e2e" in which:
         full_model("msvd-qa-oe", 2, 1)
         full_model("tgif-transition", 1, 2)

@@ -180,3 +180,38 @@ def test_e2e_train_step_grads_match_oracle():
               "fusion_model.fusion_transformer.transformer.layers.0.linear2.weight", "fusion_model.final_fc.weight"):
         worst[k] = rel(named[k].grad, sd[k].grad)
     assert max(worst.values()) < 5e-2, worst
+
+
+def _mcsim_inputs(g):
+    r = W.input_rng(int(g["seed"]))
+    vf = torch.from_numpy(r.standard_normal((2, 3, 3, 49, 1024), dtype=np.float32))
+    tf = torch.from_numpy(r.standard_normal((2, 5, 40, 768), dtype=np.float32))
+    return vf, tf
+
+
+def test_fusion_mc_sim_matches_reference_golden_and_oracle_grads():
+    """LRCEMultipleChoiceSim (fusionv3.py:268-333): FusionVideo (video-only memory) on the native
+    recurrent decoder + text projection + cosine.  Outputs vs the reference's golden (the cosines
+    are ~0.05 in size: tolerance is absolute, 1e-3, as for fp32 logits); gradients vs the oracle."""
+    from lrce.models.fusionv3 import LRCEMultipleChoiceSim
+    m = LRCEMultipleChoiceSim(768, 1, 0.1, (7, 7), 1024, 5, [3], 40)
+    filled = load_recipe(m, "fusion_model.")
+    m = m.cuda().eval()
+    g = load_golden("fusion_mcsim.npz")
+    vf, tf = _mcsim_inputs(g)
+    mask = torch.ones(2, 5, 40, dtype=torch.int64, device="cuda")
+    with torch.no_grad():
+        y = m(vf.cuda(), tf.cuda(), mask).float().cpu()
+    assert float((y - torch.from_numpy(g["y"])).abs().max()) < 1e-3
+    # backward (eval mode, deterministic) vs the oracle's autograd
+    R = torch.randn(2, 5)
+    sd = oracle_sd(filled, requires_grad=True)
+    (O.lrce_mc_sim(vf, tf, sd) * R).sum().backward()
+    out = m(vf.cuda(), tf.cuda(), mask)
+    (out * R.cuda()).sum().backward()
+    named = dict(m.named_parameters())
+    for k in ("text_projection.weight", "text_projection.bias", "fusion_transformer.summarization_token",
+              "fusion_transformer.transformer.layers.11.linear2.weight",
+              "fusion_transformer.transformer.layers.0.multihead_attn.in_proj_weight",
+              "video_pos_embed.emb_pos", "question_pos_embed.emb_pos", "projection_layer.weight"):
+        assert rel(named[k].grad, sd["fusion_model." + k].grad) < 5e-2, k

@@ -248,3 +248,20 @@ def test_multiscale_indices_restatement():
                 continue
             assert ours(T, 5, ts) == r, (T, ts)
     assert extracted_scale_index([1, 2, 3]) == [0, 1, 2, 3, 4, 5] and extracted_scale_index([3]) == [3, 4, 5]
+
+
+def test_mc_sim_oracle_matches_reference_golden():
+    """LRCEMultipleChoiceSim (fusionv3.py:268-333): oracle vs the reference's own output; our module's
+    state-dict keys == the reference's (text_projection added, no final_fc)."""
+    from lrce.models.fusionv3 import LRCEMultipleChoiceSim
+    g = load_golden("fusion_mcsim.npz")
+    m = LRCEMultipleChoiceSim(768, 1, 0.1, (7, 7), 1024, 5, [3], 40)
+    assert sorted(m.state_dict()) == [str(k) for k in g["keys"]]
+    sd = W.fill_state_dict({"fusion_model." + k: v for k, v in m.state_dict().items()})
+    r = W.input_rng(int(g["seed"]))
+    vf = torch.from_numpy(r.standard_normal((2, 3, 3, 49, 1024), dtype=np.float32))
+    tf = torch.from_numpy(r.standard_normal((2, 5, 40, 768), dtype=np.float32))
+    np.testing.assert_allclose(csum(vf), g["vf_csum"], rtol=1e-9)
+    with torch.no_grad():
+        y = O.lrce_mc_sim(vf, tf, sd)
+    assert float((y - torch.from_numpy(g["y"])).abs().max()) < 1e-5

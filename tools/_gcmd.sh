@@ -1,3 +1,3 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 200 python -u -m pytest tests/test_video_gpu.py -m gpu -x -v --timeout 100 --timeout-method thread > gpurun_out/t_video.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_model_gpu.py -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/t_model.log 2>&1

@@ -141,7 +141,8 @@ def _layer_fwd(lay, flat, x0, kvv, kvt, step, S, Lt, nmc, p, seed, save, acts, x
     lv = 150
     kv1 = kvv[step * lv * 2 * E:]
     desc = K.mha_desc(q, 1, k1=kv1, v1=kv1[E:], lk1=lv, ld_kv1=2 * E, stride_kv1_b=S * lv * 2 * E, kv1_bdiv=nmc,
-                      k2=kvt, v2=kvt[E:], lk2=Lt, ld_kv2=2 * E, stride_kv2_b=Lt * 2 * E, kv2_bdiv=1, out=ctx, lse=lse,
+                      k2=kvt if Lt else None, v2=kvt[E:] if Lt else None, lk2=Lt, ld_kv2=2 * E,
+                      stride_kv2_b=Lt * 2 * E, kv2_bdiv=1, out=ctx, lse=lse,
                       B=Bq, H=NHEAD, scale=(E // NHEAD) ** -0.5, drop_p=p, seed=seed + 2)
     K.mha_fwd(desc, ctx)
     cao = K.linear(ctx, ca.out_proj.weight, ca.out_proj.bias, out_f32=True)
@@ -182,7 +183,8 @@ def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step)
     dctx = K.linear_dx(dcao, ca.out_proj.weight)
     dq = grads.dq[step]
     K.mha_bwd(st.desc, dout=dctx, dq=dq, dk1=dkvv_step, dv1=dkvv_step[E:], ld_dkv1=2 * E,
-              stride_dkv1_b=S * 150 * 2 * E, dk2=dkvt, dv2=dkvt[E:], ld_dkv2=2 * E, stride_dkv2_b=Lt * 2 * E)
+              stride_dkv1_b=S * 150 * 2 * E, dk2=dkvt if Lt else None, dv2=dkvt[E:] if Lt else None,
+              ld_dkv2=2 * E, stride_dkv2_b=Lt * 2 * E)
     dx1 = K.linear_dx(dq, ca.in_proj_weight[:E], resid=dx2p)
     dx1p = torch.empty_like(st.x1p)
     K.layernorm_bwd(dx1, st.x1p, st.m1, st.r1, lay.norm1.weight, dx1p, dw=_g(flat, lay.norm1.weight),
@@ -209,23 +211,24 @@ def _layer_wgrads(lay, flat, acts, grads):
 
 
 class _RecurrentDecoderFn(torch.autograd.Function):
-    """FusionTransformer.forward (fusionv3.py:27-51) as one autograd node."""
+    """FusionTransformer.forward (fusionv3.py:27-51) as one autograd node; with t = None the memory
+    is the video tokens alone (FusionVideo.forward, fusionv3.py:70-88)."""
 
     @staticmethod
     def forward(ctx, v, v16, t, t16, ft, flat, p, seed, B, S, nmc, *params):
         dev = v.device
         layers = ft.transformer.layers
-        Lt = t.shape[1]
-        Bq = t.shape[0]
+        Lt = t.shape[1] if t is not None else 0
+        Bq = t.shape[0] if t is not None else B * nmc
         rows_v = B * S * 150
         v16 = v16.view(rows_v, E)
-        t16 = t16.view(Bq * Lt, E)
+        t16 = t16.view(Bq * Lt, E) if Lt else None
         kvv, kvt = [], []
         for lay in layers:
             ca = lay.multihead_attn
             w = flat.w16(ca.in_proj_weight)[E:]
             kvv.append(K.linear(v16, w, ca.in_proj_bias[E:]))
-            kvt.append(K.linear(t16, w, ca.in_proj_bias[E:]))
+            kvt.append(K.linear(t16, w, ca.in_proj_bias[E:]) if Lt else None)
         nL = len(layers)
         acts = [_LayerActs(S, Bq, dev) for _ in layers]
         s = acts[0].x0[0]
@@ -236,7 +239,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             x = s
             step_saves = []
             for l, lay in enumerate(layers):
-                x = _layer_fwd(lay, flat, x, kvv[l].view(-1), kvt[l].view(-1), i, S, Lt, nmc, p,
+                x = _layer_fwd(lay, flat, x, kvv[l].view(-1), kvt[l].view(-1) if Lt else None, i, S, Lt, nmc, p,
                                seed + 64 * (i * nL + l), step_saves, acts[l],
                                x3_out=acts[l + 1].x0[i] if l + 1 < nL else None)
             tsum = K.dropout(x, 0.0, 0, res=s)
@@ -256,7 +259,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         layers = ft.transformer.layers
         dev = ds.device
         dkvv = [torch.zeros(B * S * 150, 2 * E, device=dev) for _ in layers]
-        dkvt = [torch.zeros(Bq * Lt, 2 * E, device=dev) for _ in layers]
+        dkvt = [torch.zeros(Bq * Lt, 2 * E, device=dev) if Lt else None for _ in layers]
         ds = ds.contiguous()
         grads = [_LayerGrads(S, Bq, dev) for _ in layers]
         for i in reversed(range(S)):
@@ -268,7 +271,8 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             dx = dt
             for l in reversed(range(len(layers))):
                 dx = _layer_bwd(layers[l], flat, saves[i][l], dx, dkvv[l].view(-1)[i * 150 * 2 * E:],
-                                dkvt[l].view(-1), S, Lt, p, seed + 64 * (i * len(layers) + l), grads[l], i)
+                                dkvt[l].view(-1) if Lt else None, S, Lt, p, seed + 64 * (i * len(layers) + l),
+                                grads[l], i)
             ds = K.dropout(dx, 0.0, 0, res=dt)   # s fed both the residual and the decoder
             saves[i] = None
         for l, lay in enumerate(layers):
@@ -278,23 +282,25 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         if gt is not None:
             K.colsum(ds, gt.view(E))
         dv = torch.zeros(B * S * 150, E, device=dev)
-        dtt = torch.zeros(Bq * Lt, E, device=dev)
+        dtt = torch.zeros(Bq * Lt, E, device=dev) if Lt else None
         dk16 = torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev)
-        dt16 = torch.empty(Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev)
+        dt16 = torch.empty(Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None
         for l, lay in enumerate(layers):
             ca = lay.multihead_attn
             # the memory-side K/V gradients (accumulated in f32 over steps / answer choices) enter
             # their big-M GEMMs as bf16, like every other activation gradient
             K.cast_bf16(dkvv[l], dk16)
-            K.cast_bf16(dkvt[l], dt16)
             _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16, v16, rows=(E, 3 * E))
-            _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16, t16, rows=(E, 3 * E))
             w = flat.w16(ca.in_proj_weight)[E:]
             K.linear_dx(dk16, w, out=dv, accumulate=True)
-            K.linear_dx(dt16, w, out=dtt, accumulate=True)
+            if Lt:
+                K.cast_bf16(dkvt[l], dt16)
+                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16, t16, rows=(E, 3 * E))
+                K.linear_dx(dt16, w, out=dtt, accumulate=True)
         ctx.save = None
         flat.notify(ft.parameters())
-        return (dv.view(B, S, 150, E), None, dtt.view(Bq, Lt, E)) + (None,) * (8 + len(ctx.needs_input_grad[11:]))
+        return (dv.view(B, S, 150, E), None, dtt.view(Bq, Lt, E) if Lt else None) + \
+            (None,) * (8 + len(ctx.needs_input_grad[11:]))
 
 
 class _LinearFn(torch.autograd.Function):
@@ -341,6 +347,20 @@ class FusionTransformer(nn.Module):
         p = self.drop_out_rate if self.training else 0.0
         seed = int(torch.randint(0, 2 ** 40, (1,)).item())
         return _RecurrentDecoderFn.apply(v, v16, t, t16, self, flat, p, seed, B, S, nmc, *self.parameters())
+
+
+class FusionVideo(FusionTransformer):
+    """fusionv3.py:53-88: the same recurrent 12-layer decoder with the video tokens of each step as the
+    only memory (no question tokens); used by LRCEMultipleChoiceSim.  Same parameter tree as
+    FusionTransformer."""
+
+    def forward(self, video_features):
+        """video_features (B, S, 150, E), already embedded -> (B, 1, E)."""
+        B, S = video_features.shape[:2]
+        v = video_features.float().contiguous()
+        v16 = torch.empty(v.shape, dtype=torch.bfloat16, device=v.device)
+        K.cast_bf16(v, v16)
+        return self.run(v, v16, None, None, B, 1).view(B, 1, E)
 
 
 class LRCEOpenEnded(nn.Module):
@@ -407,3 +427,26 @@ class LRCECount(LRCEOpenEnded):
         batch = video_features.shape[0]
         out = super().forward(video_features, text_features, texts_attention_mask)
         return torch.relu(out.view(batch))
+
+
+class LRCEMultipleChoiceSim(LRCEOpenEnded):
+    """fusionv3.py:268-333: multiple choice by similarity — the video summary of FusionVideo against
+    the projected mean of each (question + answer) embedding, cosine over the feature dim -> (B, 5).
+    No final_fc (the reference sets it to None); adds text_projection (Linear E -> E)."""
+
+    def __init__(self, feature_dim, num_classes, drop_out_rate=0.1, video_feature_res=(7, 7), video_feature_dim=768,
+                 frame_sample_size=5, temporal_scale=[1, 2, 3], qa_seq_len=40):
+        super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
+                         frame_sample_size, temporal_scale, qa_seq_len)
+        self.text_projection = nn.Linear(feature_dim, feature_dim)
+        self.fusion_transformer = FusionVideo(feature_dim, drop_out_rate=drop_out_rate)
+        self.final_fc = None
+
+    def forward(self, video_features, text_features, texts_attention_mask):
+        batch, total_mc = text_features.shape[:2]
+        flat, v, v16, t, _ = self._embed(video_features, text_features.flatten(0, 1))
+        text_fused = t.mean(dim=1)                                                        # (B*5, E)
+        text_fused = _LinearFn.apply(text_fused, self.text_projection, flat, *self.text_projection.parameters())
+        video_fused = self.fusion_transformer.run(v, v16, None, None, batch, 1)          # (B, E)
+        video_fused = video_fused.view(batch, 1, E).expand(-1, total_mc, -1).flatten(0, 1)
+        return torch.nn.functional.cosine_similarity(text_fused, video_fused, dim=1, eps=1e-8).view(batch, total_mc)
