@@ -49,3 +49,22 @@ def test_param_count_matches_survey():
     m = e2e.E2EOpenEnded(768, 1000, 0.1, (7, 7), 1024, 5, [3], 32)
     n = sum(p.numel() for p in m.parameters())
     assert abs(n / 1e6 - 312.2) < 0.1
+
+
+def test_kinetics_backbone_checkpoint_loads(tmp_path):
+    """video.py:20-26: the Swin-B Kinetics-600 checkpoint is {'state_dict': {'backbone.*', 'cls_head.*'}};
+    only backbone.* (prefix stripped) goes into the extractor, strictly, via a weights_only load."""
+    from lrce.feature_extractor.video import VideoExtractor
+    from oracle import weights as W
+    tmpl = VideoExtractor().swin.state_dict()
+    filled = W.fill_state_dict({"video_extractor.swin." + k: v for k, v in tmpl.items()}, seed=3)
+    ckpt = {"state_dict": {"backbone." + k[len("video_extractor.swin."):]: v for k, v in filled.items()},
+            "meta": {"epoch": 30}}
+    ckpt["state_dict"]["cls_head.fc_cls.weight"] = torch.zeros(600, 1024)
+    path = tmp_path / "swin_base_patch244_window877_kinetics600_22k.pth"
+    torch.save(ckpt, path)
+    ve = VideoExtractor(str(path))
+    got = ve.swin.state_dict()
+    for k in ("patch_embed.proj.weight", "layers.2.blocks.17.attn.relative_position_bias_table",
+              "layers.3.blocks.1.mlp.fc2.bias", "norm.weight"):
+        assert torch.equal(got[k], filled["video_extractor.swin." + k]), k
