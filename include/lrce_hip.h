@@ -88,6 +88,14 @@ typedef struct LrceGemmDesc {
    * weight-gradient GEMMs otherwise). */
   float* workspace;
   int64_t workspace_elems;
+  /* nn.Dropout fused into the epilogue (the recurrent decoder's dropouts, fusionv3.py:8-17): after
+   * the bias / GELU / dGELU / row scale and before the RESID add, y = keep ? y / (1 - drop_p) : 0 with
+   * keep = lrce_uniform(drop_seed + device RNG offset, (m * n_cols + n) / drop_group) >= drop_p — the
+   * mask lrce_dropout / lrce_dropout_bwd draw for the same contiguous [m][n] tensor.  drop_p = 0: off.
+   * Exact-f32 skinny path only (B f32, M <= 64); other paths reject drop_p > 0. */
+  float drop_p;
+  int32_t drop_group;
+  uint64_t drop_seed;
 } LrceGemmDesc;
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);

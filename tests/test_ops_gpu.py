@@ -514,3 +514,31 @@ def test_fused_adamw_optimizer_matches_torch_over_steps():
     for p, r in zip(net.parameters(), ref):
         assert rel(p.detach(), r.detach()) < 1e-5
     assert abs(float(opt.l2_term()) - float(sum(r.norm() for r in ref))) < 1e-3
+
+
+@pytest.mark.parametrize("M", [10, 45, 100])
+def test_fused_dropout_epilogue_matches_separate_launch(M):
+    """Decoder linears with the dropout fused into the skinny-GEMM epilogue (M <= 64; M = 100 falls
+    back to a dropout launch) give the same bits as GEMM + lrce_dropout / lrce_dropout_bwd."""
+    k = K()
+    k.rng_offset(dev).zero_()
+    E, FF, p = 768, 3072, 0.3
+    x = torch.randn(M, E, device=dev)
+    w = torch.randn(E, E, device=dev) / math.sqrt(E)
+    b = torch.randn(E, device=dev)
+    res = torch.randn(M, E, device=dev)
+    fused = k.linear(x, w, b, out_f32=True, resid=res, drop=(p, 77, 1))
+    ref = k.dropout(k.linear(x, w, b, out_f32=True), p, 77, res=res)
+    assert torch.equal(fused, ref)
+    head = k.linear(x, w, b, out_f32=True, drop=(p, 78, 64))            # per-head mask (attention-prob dropout)
+    assert torch.equal(head, k.dropout(k.linear(x, w, b, out_f32=True), p, 78, group=64))
+    w1 = torch.randn(FF, E, device=dev) / math.sqrt(E)
+    pre = torch.empty(M, FF, dtype=torch.bfloat16, device=dev)
+    g = k.linear(x, w1, None, gelu=True, pre_out=pre, out_f32=True, drop=(p, 79, 1))
+    pre2 = torch.empty_like(pre)
+    assert torch.equal(g, k.dropout(k.linear(x, w1, None, gelu=True, pre_out=pre2, out_f32=True), p, 79))
+    assert torch.equal(pre, pre2)
+    dy = torch.randn(M, E, device=dev)
+    w2 = torch.randn(E, FF, device=dev) / math.sqrt(FF)
+    dg = k.linear_dx(dy, w2, dgelu_pre=pre, drop=(p, 79, 1))
+    assert torch.equal(dg, k.dropout_bwd(k.linear_dx(dy, w2, dgelu_pre=pre), p, 79))

@@ -767,6 +767,7 @@ static int g_gemm_tile = getenv("LRCE_GEMM_TILE") ? atoi(getenv("LRCE_GEMM_TILE"
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
 
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
+  if (d && d->drop_p > 0.f && !d->b_f32) return lrce_fail(LRCE_E_ARG, "gemm: fused dropout is only on the exact-f32 skinny path");
   if (!d || !d->a || !d->b || !d->c) return lrce_fail(LRCE_E_ARG, "gemm: null pointer");
   if (!(d->flags & LRCE_EPI_BIAS_GRAD)) return gemm_dispatch(d, stream);
   // bias gradient of a weight-gradient GEMM: db[m] += sum_k A(m, k)

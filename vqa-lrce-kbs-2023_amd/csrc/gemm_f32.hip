@@ -161,6 +161,10 @@ struct SkinnyP {
   int scale_cols;
   float scale_val;
   float* bias_grad;
+  float drop_p;
+  int drop_group;
+  uint64_t drop_seed;
+  const uint64_t* rng_off;
 };
 
 __device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, int n) {
@@ -174,6 +178,9 @@ __device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, in
   }
   if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]));
   if (p.row_scale) x *= p.row_scale[m / p.rows_per_scale];
+  if (p.drop_p > 0.f)   // same mask as lrce_dropout on the contiguous [m][n] result
+    x = lrce_uniform(lrce_seed(p.drop_seed, p.rng_off), ((long long)m * p.n + n) / p.drop_group) >= p.drop_p
+            ? x / (1.0f - p.drop_p) : 0.f;
   if (fl & LRCE_EPI_RESID) x += static_cast<const float*>(p.aux)[row * p.ld_aux + n];
   if (fl & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) {
     static_cast<float*>(p.c)[row * p.ldc + n] += x;   // one owner per element: a plain RMW suffices
@@ -415,7 +422,9 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
     q.alpha = d->alpha; q.row_scale = d->row_scale; q.rows_per_scale = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
     q.scale_cols = d->scale_cols; q.scale_val = d->scale_val;
     q.bias_grad = const_cast<float*>(d->bias);
-    const bool outer_ok = lrce_gemm_f32_outer_ok(d);
+    q.drop_p = d->drop_p; q.drop_group = d->drop_group > 0 ? d->drop_group : 1; q.drop_seed = d->drop_seed;
+    q.rng_off = lrce_rng_offset();
+    const bool outer_ok = lrce_gemm_f32_outer_ok(d) && d->drop_p <= 0.f;
     if (outer_ok) {
       const long long work = (long long)d->m * (d->n / 4);
       outer_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(q);
@@ -453,6 +462,7 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
       return lrce_check_launch("gemm_f32(skinny)");
     }
   }
+  if (d->drop_p > 0.f) return lrce_fail(LRCE_E_ARG, "gemm(f32): fused dropout needs the skinny path (K-major A, M <= 64)");
   GemmF32P p;
   p.a = static_cast<const float*>(d->a); p.b = static_cast<const float*>(d->b); p.c = d->c;
   p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc;

@@ -49,6 +49,7 @@ class GemmDesc(ctypes.Structure):
         ("a_row_scale", ctypes.c_void_p), ("a_rows_per_scale", ctypes.c_int32),
         ("b_f32", ctypes.c_int32),
         ("workspace", ctypes.c_void_p), ("workspace_elems", ctypes.c_int64),
+        ("drop_p", ctypes.c_float), ("drop_group", ctypes.c_int32), ("drop_seed", ctypes.c_uint64),
     ]
 
 

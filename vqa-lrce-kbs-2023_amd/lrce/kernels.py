@@ -99,8 +99,9 @@ def _chk(t, dtype=None, name="tensor"):
 def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, flags=0, bias=None,
          aux=None, ld_aux=0, aux_out=None, ld_aux_out=0, a_map=None, c_map=None, alpha=1.0, split_k=1,
          scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, a_row_scale=None, a_rows_per_scale=1,
-         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None):
-    """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc."""
+         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None):
+    """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc.  drop = (p, seed, group):
+    nn.Dropout fused into the epilogue (exact-f32 skinny path; same mask as dropout())."""
     _chk(a, None, "A"); _chk(b, None, "B"); _chk(c, None, "C")
     a_f32 = a.dtype == F32
     b_f32 = b.dtype == F32
@@ -128,6 +129,8 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.b_f32 = int(b_f32)
     if workspace is not None:
         d.workspace, d.workspace_elems = ptr(workspace), workspace.numel()
+    if drop is not None and drop[0] > 0:
+        d.drop_p, d.drop_seed, d.drop_group = float(drop[0]), drop[1] & (2 ** 64 - 1), int(drop[2])
     _timed("gemm_f32" if b_f32 else "gemm", c, lambda: call("lrce_gemm", ctypes.byref(d), stream_of(c)),
            flops=2.0 * m * n * k * batch,
            key=(m, n, k, batch, "AK" if a_kmajor else "AM", "BK" if b_kmajor else "BN", "a32" if a_f32 else "a16",
@@ -141,10 +144,24 @@ def _split_for(m_out, n_out, k_red):
     return int(max(1, min(want, k_red // 1024)))
 
 
+def _skinny_drop_ok(x, w, M, a_map=None):
+    """Does lrce_gemm route this linear to the exact-f32 skinny kernel (the only one with the fused
+    dropout epilogue)?  Mirrors the launcher's test: f32 A and W, K-major A, M <= 64, 16-B aligned."""
+    return (x.dtype == F32 and w.dtype == F32 and M <= 64 and a_map is None and x.data_ptr() % 16 == 0
+            and w.data_ptr() % 16 == 0)
+
+
 def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None, resid=None, c_map=None,
-           a_map=None, rows=None, scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, bf16_shadow=None):
-    """y = x W^T (+b) [gelu] [*row_scale] [+resid]; x [M,K] bf16/f32, W [N,K] bf16."""
+           a_map=None, rows=None, scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, bf16_shadow=None,
+           drop=None):
+    """y = x W^T (+b) [gelu] [*row_scale] [dropout] [+resid]; x [M,K] bf16/f32, W [N,K] bf16 (or f32:
+    exact path).  drop = (p, seed, group): fused into the skinny epilogue, else a dropout launch."""
     M = rows if rows is not None else x.shape[0]
+    if drop is not None and drop[0] > 0 and not (_skinny_drop_ok(x, w, M, a_map) and c_map is None):
+        y = linear(x, w, bias, out=out if resid is None else None, out_f32=out_f32, gelu=gelu, pre_out=pre_out,
+                   c_map=c_map, a_map=a_map, rows=rows, scale_cols=scale_cols, scale_val=scale_val,
+                   row_scale=row_scale, rows_per_scale=rows_per_scale)
+        return dropout(y, drop[0], drop[1], out=out if out is not None else y, res=resid, group=drop[2])
     K = x.shape[-1]
     Nn = w.shape[0]
     flags = 0
@@ -167,14 +184,20 @@ def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None
     aux_out = pre_out if gelu else bf16_shadow
     gemm(x, w, out, M, Nn, K, flags=flags, bias=bias, aux=aux, ld_aux=Nn, aux_out=aux_out, ld_aux_out=Nn,
          a_map=a_map, c_map=c_map, scale_cols=scale_cols, scale_val=scale_val, row_scale=row_scale,
-         rows_per_scale=rows_per_scale)
+         rows_per_scale=rows_per_scale, drop=drop)
     return out
 
 
 def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows=None, a_row_scale=None,
-              a_rows_per_scale=1, accumulate=False, resid=None):
-    """dX = dY W (+ resid) ; dY [M,N] (bf16/f32), W [N,K] bf16 -> [M,K]; optional *gelu'(pre)."""
+              a_rows_per_scale=1, accumulate=False, resid=None, drop=None):
+    """dX = dY W (+ resid) ; dY [M,N] (bf16/f32), W [N,K] bf16 -> [M,K]; optional *gelu'(pre), and
+    drop = (p, seed, group): the dropout backward mask (fused on the skinny path, else a launch)."""
     M = rows if rows is not None else dy.shape[0]
+    if drop is not None and drop[0] > 0 and not (_skinny_drop_ok(dy, w, M, a_map) and not accumulate
+                                                 and resid is None and a_row_scale is None):
+        y = linear_dx(dy, w, out=out, out_f32=out_f32, dgelu_pre=dgelu_pre, a_map=a_map, rows=rows,
+                      a_row_scale=a_row_scale, a_rows_per_scale=a_rows_per_scale, accumulate=accumulate, resid=resid)
+        return dropout_bwd(y, drop[0], drop[1], out=y, group=drop[2])
     Nn, K = w.shape
     flags = 0
     if dgelu_pre is not None:
@@ -188,7 +211,7 @@ def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows
         flags |= N.EPI_ACCUM if accumulate else N.EPI_OUT_F32
     gemm(dy, w, out, M, K, Nn, a_kmajor=True, b_kmajor=False, lda=dy.shape[-1], ldb=K, flags=flags,
          aux=dgelu_pre if dgelu_pre is not None else resid, ld_aux=K, a_map=a_map, a_row_scale=a_row_scale,
-         a_rows_per_scale=a_rows_per_scale)
+         a_rows_per_scale=a_rows_per_scale, drop=drop)
     return out
 
 

@@ -128,10 +128,10 @@ def _layer_fwd(lay, flat, x0, kvv, kvt, step, S, Lt, nmc, p, seed, save, acts, x
     the recurrence is precision-critical); only the memory K/V (big-M GEMMs) are bf16."""
     sa, ca = lay.self_attn, lay.multihead_attn
     # self-attention over one token: out_proj(dropout_head(v_proj(x)))
-    sad = K.linear(x0, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step])
-    K.dropout(sad, p, seed, out=sad, group=E // NHEAD)
-    sao = K.linear(sad, sa.out_proj.weight, sa.out_proj.bias, out_f32=True)
-    x1p = K.dropout(sao, p, seed + 1, res=x0)
+    # (every dropout of the layer rides in the epilogue of the GEMM producing its input)
+    sad = K.linear(x0, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step],
+                   drop=(p, seed, E // NHEAD))
+    x1p = K.linear(sad, sa.out_proj.weight, sa.out_proj.bias, out_f32=True, resid=x0, drop=(p, seed + 1, 1))
     x1, m1, r1 = K.layernorm(x1p, lay.norm1.weight, lay.norm1.bias, EPS, out=acts.x1[step])
     # cross-attention to [video tokens of this step ; question tokens]
     q = K.linear(x1, ca.in_proj_weight[:E], ca.in_proj_bias[:E], out_f32=True)
@@ -145,15 +145,13 @@ def _layer_fwd(lay, flat, x0, kvv, kvt, step, S, Lt, nmc, p, seed, save, acts, x
                       stride_kv2_b=Lt * 2 * E, kv2_bdiv=1, out=ctx, lse=lse,
                       B=Bq, H=NHEAD, scale=(E // NHEAD) ** -0.5, drop_p=p, seed=seed + 2)
     K.mha_fwd(desc, ctx)
-    cao = K.linear(ctx, ca.out_proj.weight, ca.out_proj.bias, out_f32=True)
-    x2p = K.dropout(cao, p, seed + 3, res=x1)
+    x2p = K.linear(ctx, ca.out_proj.weight, ca.out_proj.bias, out_f32=True, resid=x1, drop=(p, seed + 3, 1))
     x2, m2, r2 = K.layernorm(x2p, lay.norm2.weight, lay.norm2.bias, EPS, out=acts.x2[step])
     # FFN: linear2(dropout(gelu(linear1(x))))
     pre = torch.empty(Bq, FF, dtype=torch.bfloat16, device=x0.device)
-    gd = K.linear(x2, lay.linear1.weight, lay.linear1.bias, gelu=True, pre_out=pre, out=acts.gd[step])
-    K.dropout(gd, p, seed + 4, out=gd)
-    f = K.linear(gd, lay.linear2.weight, lay.linear2.bias, out_f32=True)
-    x3p = K.dropout(f, p, seed + 5, res=x2)
+    gd = K.linear(x2, lay.linear1.weight, lay.linear1.bias, gelu=True, pre_out=pre, out=acts.gd[step],
+                  drop=(p, seed + 4, 1))
+    x3p = K.linear(gd, lay.linear2.weight, lay.linear2.bias, out_f32=True, resid=x2, drop=(p, seed + 5, 1))
     x3, m3, r3 = K.layernorm(x3p, lay.norm3.weight, lay.norm3.bias, EPS, out=x3_out, out_f32=True)
     if save is not None:
         st = _Step()
@@ -172,9 +170,7 @@ def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step)
     K.layernorm_bwd(dx3, st.x3p, st.m3, st.r3, lay.norm3.weight, dx3p, dw=_g(flat, lay.norm3.weight),
                     db=_g(flat, lay.norm3.bias))
     df = K.dropout_bwd(dx3p, p, seed + 5, out=grads.df[step])
-    dgp = K.linear_dx(df, lay.linear2.weight, dgelu_pre=st.pre, out=grads.dgp[step])
-    if p > 0:
-        K.dropout_bwd(dgp, p, seed + 4, out=dgp)
+    dgp = K.linear_dx(df, lay.linear2.weight, dgelu_pre=st.pre, out=grads.dgp[step], drop=(p, seed + 4, 1))
     dx2 = K.linear_dx(dgp, lay.linear1.weight, resid=dx3p)
     dx2p = torch.empty_like(st.x2p)
     K.layernorm_bwd(dx2, st.x2p, st.m2, st.r2, lay.norm2.weight, dx2p, dw=_g(flat, lay.norm2.weight),
@@ -190,9 +186,7 @@ def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step)
     K.layernorm_bwd(dx1, st.x1p, st.m1, st.r1, lay.norm1.weight, dx1p, dw=_g(flat, lay.norm1.weight),
                     db=_g(flat, lay.norm1.bias))
     dsao = K.dropout_bwd(dx1p, p, seed + 1, out=grads.dsao[step])
-    dsav = K.linear_dx(dsao, sa.out_proj.weight, out=grads.dsav[step])
-    if p > 0:
-        K.dropout_bwd(dsav, p, seed, out=dsav, group=E // NHEAD)
+    dsav = K.linear_dx(dsao, sa.out_proj.weight, out=grads.dsav[step], drop=(p, seed, E // NHEAD))
     return K.linear_dx(dsav, sa.in_proj_weight[2 * E:], resid=dx1p)
 
 
