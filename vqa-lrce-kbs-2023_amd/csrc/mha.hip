@@ -236,14 +236,24 @@ __global__ void __launch_bounds__(256) mha1_fwd_kernel(MhaP P) {
   const float s = block_sum(pe, red);
   ps[t] = live ? pe * drop_factor(d, P.off, b, h, 0, t, Lk) : 0.f;
   __syncthreads();
-  // o[lane] = sum_j ps[j] V[j][lane]; wave w takes keys w, w+4, ...
+  // o[lane] = sum_j ps[j] V[j][lane]; wave w takes keys w, w+4, ..., in batches of UF whose V-row
+  // loads are all issued before the first FMA (one memory round trip per batch, not per key:
+  // 183 keys = 3 batches per wave instead of 23 dependent trips)
+  constexpr int UF = 16;
   float o0 = 0.f, o1 = 0.f;
-  int j = wave;
-  for (; j + 4 < Lk; j += 8) {
-    o0 += ps[j] * bf2f(key_row(d, d.v1, d.v2, b, j, h)[lane]);
-    o1 += ps[j + 4] * bf2f(key_row(d, d.v1, d.v2, b, j + 4, h)[lane]);
+  for (int j0 = wave; j0 < Lk; j0 += 4 * UF) {
+    float vv[UF];
+#pragma unroll
+    for (int u = 0; u < UF; ++u) vv[u] = bf2f(key_row(d, d.v1, d.v2, b, min(j0 + 4 * u, Lk - 1), h)[lane]);
+#pragma unroll
+    for (int u = 0; u < UF; ++u) {
+      const int j = j0 + 4 * u;
+      if (j < Lk) {
+        if (u & 1) o1 += ps[j] * vv[u];
+        else o0 += ps[j] * vv[u];
+      }
+    }
   }
-  if (j < Lk) o0 += ps[j] * bf2f(key_row(d, d.v1, d.v2, b, j, h)[lane]);
   part[wave][lane] = o0 + o1;
   __syncthreads();
   if (wave == 0) {
@@ -295,7 +305,7 @@ __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
   // Keys in batches of UB per wave: every K-row load and dK/dV read of a batch is issued before its
   // first store, so the read-modify-writes overlap instead of forming one serial memory round trip
   // per key (single writer per row); rows shared by bdiv > 1 rows use no-return atomics.
-  constexpr int UB = 8;
+  constexpr int UB = 16;
   for (int j0 = wave; j0 < Lk; j0 += 4 * UB) {
     float kv[UB], okk[UB], ovv[UB];
     float* pk[UB];
