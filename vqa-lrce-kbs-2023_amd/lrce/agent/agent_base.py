@@ -124,11 +124,28 @@ class AgentBase:
         self.best_epoch = None
         self.best_metric_val = None
 
+    # ------------------------------------------------------------------ task hooks
+    # A task agent supplies: the loss (task_loss), what step() returns (pack_step) and how a step's
+    # result feeds the epoch metric (unpack_step -> (loss, numerator, denominator)); METRIC names the
+    # summary tag and HIGHER_IS_BETTER the direction (best checkpoint, plateau scheduler).
+    METRIC = "Accuracy"
+    HIGHER_IS_BETTER = True
+
+    def task_loss(self, out, gt):
+        return self.loss_func(out, gt)
+
+    def pack_step(self, loss_value, out, gt, task_terms):
+        prediction = torch.argmax(out, dim=1)
+        return loss_value, torch.sum(prediction == gt).item(), prediction.shape[0]
+
+    def unpack_step(self, result):
+        return result
+
     # ------------------------------------------------------------------ helpers (agent_base.py:90-108)
     def is_metric_val_better(self, epoch=None):
-        if self.best_metric_val is None or self.last_metric_val > self.best_metric_val:
-            self.best_metric_val = self.last_metric_val
-            self.best_epoch = epoch
+        last, best = self.last_metric_val, self.best_metric_val
+        if best is None or (last > best if self.HIGHER_IS_BETTER else last < best):
+            self.best_metric_val, self.best_epoch = last, epoch
             return True
         return False
 
@@ -143,77 +160,68 @@ class AgentBase:
         with torch.no_grad():
             return sum(p.float().norm(2) for p in self.model.module.parameters() if p.requires_grad)
 
-    def _regularised(self, task_loss):
-        """The reference's `loss = task + reg * L2` as a value; only `task_loss` is back-propagated
-        (the L2 gradient is applied by the optimizer kernel)."""
-        if self.reg_strength == 0.0:
-            return task_loss.detach()
-        return task_loss.detach() + self.reg_strength * self.calculate_l2_reg()
-
-    def _backward_and_update(self, task_loss):
-        """optim.zero_grad -> backward -> (all-reduce) -> optimizer step (agent_oe.py:38-42)."""
-        self.optim.zero_grad()
-        task_loss.backward()
-        scale = self.model.finish_gradients()
-        self.optim.step(grad_scale=scale)
-
-    def _forward(self, video_clips, texts, texts_attention_mask, texts_type_ids):
+    def step(self, video_clips, texts, texts_attention_mask, texts_type_ids, ground_truth, is_train):
+        """One batch (agent_oe.py:19-48 and its MC / count twins): forward on the native path, task
+        loss, the reported loss = task + reg * L2, and for training zero_grad -> backward ->
+        (all-reduce) -> fused AdamW.  Only the task loss is back-propagated: the optimizer kernel adds
+        the L2 term's gradient reg * p / ||p||."""
         d = self.device
-        return self.model(video_clips.to(d, non_blocking=True), texts.to(d, non_blocking=True),
-                          texts_attention_mask.to(d, non_blocking=True), texts_type_ids.to(d, non_blocking=True))
-
-    def step(self, *args, is_train):
-        raise NotImplementedError()
-
-    @staticmethod
-    def _reduce(t):
-        if dist.is_available() and dist.is_initialized():
-            dist.reduce(t, dst=0)
+        out = self.model(video_clips.to(d, non_blocking=True), texts.to(d, non_blocking=True),
+                         texts_attention_mask.to(d, non_blocking=True), texts_type_ids.to(d, non_blocking=True))
+        gt = ground_truth.to(d, non_blocking=True)
+        terms = self.task_loss(out.float(), gt)
+        task = terms.mean() if terms.dim() else terms
+        value = task.detach()
+        if self.reg_strength != 0.0:
+            value = value + self.reg_strength * self.calculate_l2_reg()
+        if is_train:
+            self.optim.zero_grad()
+            task.backward()
+            self.optim.step(grad_scale=self.model.finish_gradients())
+        return self.pack_step(value.item(), out.detach(), gt, terms.detach())
 
     # ------------------------------------------------------------------ loops (agent_base.py:110-171)
     def process_data(self, dl, is_train, epoch):
-        if is_train:
-            self.logger.info("Training Phase")
-        elif not self.is_eval:
-            self.logger.info("Validation Phase")
-        correct_counter = torch.zeros(2, device=self.device)
-        batch_losses = torch.zeros(len(dl), device=self.device)
-        avg_losses, avg_acc = float("nan"), float("nan")
-        for i, batch_data in enumerate(dl):
-            if not is_train:
-                self.model.eval()
-                with torch.no_grad():
-                    b_loss, b_total_correct, b_total_data = self.step(*batch_data, is_train=False)
-            else:
-                self.model.train()
-                b_loss, b_total_correct, b_total_data = self.step(*batch_data, is_train=True)
+        """Generator over one pass of `dl`; in training yields each batch index (the evaluation hook
+        of do_training), then -1.  Rank 0 accumulates the metric over the pass; other ranks send
+        their current batch only (reduce to rank 0 after every batch, as the reference does)."""
+        phase = "Training" if is_train else "Validation"
+        if is_train or not self.is_eval:
+            self.logger.info(f"{phase} Phase")
+        acc = torch.zeros(2, device=self.device)         # metric numerator, denominator
+        losses = []
+        avg_loss = avg_metric = float("nan")
+        for i, batch in enumerate(dl):
+            self.model.train(is_train)
+            with torch.set_grad_enabled(is_train):
+                loss, num, den = self.unpack_step(self.step(*batch, is_train=is_train))
+            if is_train:
                 self.counter += 1
                 if getattr(self.args, "use_cosine_scheduler", False):
                     self.scheduler.step(epoch + i / len(dl))
-                for k in range(len(self.optim.param_groups)):
-                    self.write_summary(f"LR Scheduler/{k}", self.optim.param_groups[k]["lr"], self.counter)
-                self.write_summary("Training/Batch Loss", b_loss, self.counter)
-                self.write_summary("Training/Batch Accuracy", b_total_correct / b_total_data, self.counter)
+                for k, g in enumerate(self.optim.param_groups):
+                    self.write_summary(f"LR Scheduler/{k}", g["lr"], self.counter)
+                self.write_summary("Training/Batch Loss", loss, self.counter)
+                self.write_summary(f"Training/Batch {self.METRIC}", num / den, self.counter)
                 yield i
-            if self.gpu_id != 0:   # ranks > 0 contribute only their current batch to the reduce
-                correct_counter.zero_()
-            correct_counter[0] += b_total_correct
-            correct_counter[1] += b_total_data
-            batch_losses[i] = b_loss
-            self._reduce(correct_counter)
-            nz = batch_losses[batch_losses.nonzero()]
-            avg_losses = nz.mean().item() if nz.numel() else 0.0
-            avg_acc = (correct_counter[0] / correct_counter[1]).item()
-        if not is_train:
-            self.last_loss = avg_losses
-            self.last_metric_val = avg_acc
-            if not self.is_eval and not getattr(self.args, "use_cosine_scheduler", False):
-                self.scheduler.step(avg_acc)
-            self.write_summary("Validation/Loss", avg_losses, epoch)
-            self.write_summary("Validation/Accuracy", avg_acc, epoch)
+            if self.gpu_id != 0:
+                acc.zero_()
+            acc += torch.tensor([num, den], device=self.device, dtype=acc.dtype)
+            if dist.is_available() and dist.is_initialized():
+                dist.reduce(acc, dst=0)
+            losses.append(loss)
+            nonzero = [x for x in losses if x != 0]     # the reference averages the nonzero batch losses
+            avg_loss = sum(nonzero) / len(nonzero) if nonzero else 0.0
+            avg_metric = (acc[0] / acc[1]).item()
+        if is_train:
+            self.write_summary("Training/Loss", avg_loss, epoch)
+            self.write_summary(f"Training/{self.METRIC}", avg_metric, epoch)
         else:
-            self.write_summary("Training/Loss", avg_losses, epoch)
-            self.write_summary("Training/Accuracy", avg_acc, epoch)
+            self.last_loss, self.last_metric_val = avg_loss, avg_metric
+            if not self.is_eval and not getattr(self.args, "use_cosine_scheduler", False):
+                self.scheduler.step(avg_metric if self.HIGHER_IS_BETTER else -avg_metric)
+            self.write_summary("Validation/Loss", avg_loss, epoch)
+            self.write_summary(f"Validation/{self.METRIC}", avg_metric, epoch)
         yield -1
 
     # ------------------------------------------------------------------ persistence (agent_base.py:173-217)

@@ -1,18 +1,17 @@
-"""Multiple-choice agent (reference lrce/agent/agent_mc.py): cross-entropy over the 5 choices, or
-with --use-hinge-loss the multi-class hinge loss of agent_mc.py:20-41 (a per-sample Python loop
-there, one vectorised expression here — same value and gradient)."""
+"""Multiple choice (reference lrce/agent/agent_mc.py): cross-entropy over the choices, or with
+--use-hinge-loss the multi-class hinge loss of agent_mc.py:20-41 — a per-sample Python loop there,
+one vectorised expression here (same value and gradient, tests/test_agent_cpu.py)."""
 import torch
 
 from .agent_base import AgentBase, get_logger
 
 
 def hinge_loss(out, gt, margin):
-    """mean_i sum_{j != gt_i} max(0, out[i, j] - out[i, gt_i] + margin)   (agent_mc.py:20-41)."""
+    """mean_i sum_{j != gt_i} max(0, out[i, j] - out[i, gt_i] + margin)."""
     out = out.float()
-    correct = out.gather(1, gt.view(-1, 1))
-    terms = torch.clamp(out - correct + margin, min=0.0)
-    keep = torch.ones_like(terms).scatter_(1, gt.view(-1, 1), 0.0)
-    return (terms * keep).sum(dim=1).mean()
+    margins = torch.clamp(out - out.gather(1, gt.view(-1, 1)) + margin, min=0.0)
+    others = torch.ones_like(margins).scatter_(1, gt.view(-1, 1), 0.0)
+    return (margins * others).sum(dim=1).mean()
 
 
 class AgentMC(AgentBase):
@@ -24,15 +23,3 @@ class AgentMC(AgentBase):
 
     def hinge_loss(self, out, gt):
         return hinge_loss(out, gt, self.args.margin)
-
-    def step(self, video_clips, texts, texts_attention_mask, texts_type_ids, ground_truth, is_train):
-        out = self._forward(video_clips, texts, texts_attention_mask, texts_type_ids)
-        gt = ground_truth.to(self.device)
-        task_loss = self.loss_func(out.float(), gt)
-        loss = self._regularised(task_loss)
-        if is_train:
-            self._backward_and_update(task_loss)
-        prediction = torch.argmax(out, dim=1)
-        total_data = prediction.shape[0]
-        total_correct = torch.sum(prediction == gt).item()
-        return loss.item(), total_correct, total_data
