@@ -59,8 +59,16 @@ __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, in
   const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
   if (r >= rows) return;
   const int nch = cols >> 2, seg = cols / nseg;
-  float4 v[CH];
+  float4 v[CH], ww[CH], bb[CH];
   float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {   // gamma / beta issued with the row (one memory round trip, not two)
+    const int c = sl + LPR * t;
+    if (c < nch) {
+      ww[t] = *reinterpret_cast<const float4*>(w + 4 * c);
+      bb[t] = *reinterpret_cast<const float4*>(b + 4 * c);
+    }
+  }
 #pragma unroll
   for (int t = 0; t < CH; ++t) {
     const int c = sl + LPR * t;
@@ -88,13 +96,11 @@ __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, in
   for (int t = 0; t < CH; ++t) {
     const int c = sl + LPR * t;
     if (c < nch) {
-      const float4 ww = *reinterpret_cast<const float4*>(w + 4 * c);
-      const float4 bb = *reinterpret_cast<const float4*>(b + 4 * c);
       float4 o;
-      o.x = (v[t].x - mean) * rstd * ww.x + bb.x;
-      o.y = (v[t].y - mean) * rstd * ww.y + bb.y;
-      o.z = (v[t].z - mean) * rstd * ww.z + bb.z;
-      o.w = (v[t].w - mean) * rstd * ww.w + bb.w;
+      o.x = (v[t].x - mean) * rstd * ww[t].x + bb[t].x;
+      o.y = (v[t].y - mean) * rstd * ww[t].y + bb[t].y;
+      o.z = (v[t].z - mean) * rstd * ww[t].z + bb[t].z;
+      o.w = (v[t].w - mean) * rstd * ww[t].w + bb[t].w;
       st4<TY>(y + orow * cols + 4 * c, o);
       if (y2) st4<bf16>(y2 + orow * cols + 4 * c, o);
     }
@@ -144,6 +150,12 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
     }
   };
   int r0 = (blockIdx.x * 4 + wave) * RPW;
+  float4 wcol[CH];   // gamma of this lane's columns: loaded once, with the first row
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const int c = sl + LPR * t;
+    wcol[t] = c < nch ? *reinterpret_cast<const float4*>(w + 4 * c) : z4;
+  }
   float4 xcur[CH], dcur[CH], rcur[CH];
   float mcur = 0.f, scur = 0.f;
   if (r0 < rows) fetch(r0, xcur, dcur, rcur, mcur, scur);
@@ -166,7 +178,7 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
         const float4 xv = xcur[t];
         xh[t] = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd);
         const float4 d = dcur[t];
-        const float4 ww = *reinterpret_cast<const float4*>(w + 4 * c);
+        const float4 ww = wcol[t];
         g[t] = make_float4(d.x * ww.x, d.y * ww.y, d.z * ww.z, d.w * ww.w);
         s1 += g[t].x + g[t].y + g[t].z + g[t].w;
         s2 += g[t].x * xh[t].x + g[t].y * xh[t].y + g[t].z * xh[t].z + g[t].w * xh[t].w;

@@ -20,11 +20,24 @@ from ..runtime import prepare
 from .fusionv3 import LRCEOpenEnded, LRCEMultipleChoice, LRCECount
 
 
+def _head_args(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim, frame_sample_size,
+               temporal_scale, text_seq_len):
+    """The positional argument list every LRCE head takes (fusionv3.py:137-151)."""
+    return (feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim, frame_sample_size,
+            temporal_scale, text_seq_len)
+
+
 class E2EBase(nn.Module):
-    def __init__(self, swin_ckpt=SWIN_B_CKPT) -> None:
+    """Swin3D video extractor + BERT text extractor + an LRCE head (HEAD, set by the subclasses);
+    forward(clips, texts, mask, types) -> head(video features, text features, mask)."""
+    HEAD = None
+
+    def __init__(self, *head_args, swin_ckpt=SWIN_B_CKPT) -> None:
         super().__init__()
         self.text_extractor = TextExtractor()
         self.video_extractor = VideoExtractor(swin_ckpt)
+        if self.HEAD is not None:
+            self.fusion_model = self.HEAD(*_head_args(*head_args))
 
     def extract_text_features(self, texts, attention_mask, texts_type_ids):
         return self.text_extractor(texts, attention_mask, texts_type_ids)
@@ -46,39 +59,44 @@ class E2EBase(nn.Module):
         flat = prepare(self)
         if self.training:
             K.rng_advance(flat.device)   # fresh dropout masks per step, also under HIP-graph replay
-        video_features = self.extract_video_features(video_clips)
-        texts_features = self.extract_text_features(texts, texts_attention_mask, texts_type_ids)
-        return self.fusion_model(video_features, texts_features, texts_attention_mask)
+        return self.fusion_model(self.extract_video_features(video_clips),
+                                 self.extract_text_features(texts, texts_attention_mask, texts_type_ids),
+                                 texts_attention_mask)
 
 
+# Constructor defaults differ per task (question length 30 vs 40, one output for counting), so each
+# class restates the signature (positional order of train_ddp.py:89-98, keywords of eval.py:66-74).
 class E2EOpenEnded(E2EBase):
+    HEAD = LRCEOpenEnded
+
     def __init__(self, feature_dim: int, num_classes: int, drop_out_rate: float = 0.1,
                  video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
                  temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 30) -> None:
-        super().__init__()
-        self.fusion_model = LRCEOpenEnded(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
-                                          frame_sample_size, temporal_scale, text_seq_len)
+        super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
+                         frame_sample_size, temporal_scale, text_seq_len)
 
 
 class E2EMultipleChoice(E2EBase):
+    HEAD = LRCEMultipleChoice
+
     def __init__(self, feature_dim: int, num_classes: int, drop_out_rate: float = 0.1,
                  video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
                  temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 40) -> None:
-        super().__init__()
-        self.fusion_model = LRCEMultipleChoice(feature_dim, num_classes, drop_out_rate, video_feature_res,
-                                               video_feature_dim, frame_sample_size, temporal_scale, text_seq_len)
+        super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
+                         frame_sample_size, temporal_scale, text_seq_len)
 
     def extract_text_features(self, texts, attention_mask, texts_type_ids):
         """e2e.py:77-81: the 5 question+answer sequences go through BERT as B*5 rows."""
-        batch_size, total_choice, seq_len = texts.shape
-        out = self.text_extractor(texts.flatten(0, 1), attention_mask.flatten(0, 1), texts_type_ids.flatten(0, 1))
-        return out.view(batch_size, total_choice, seq_len, -1)
+        b, n_choice, seq = texts.shape
+        feats = self.text_extractor(texts.flatten(0, 1), attention_mask.flatten(0, 1), texts_type_ids.flatten(0, 1))
+        return feats.view(b, n_choice, seq, -1)
 
 
 class E2ECount(E2EBase):
+    HEAD = LRCECount
+
     def __init__(self, feature_dim: int, num_classes: int = 1, drop_out_rate: float = 0.1,
                  video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
                  temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 30) -> None:
-        super().__init__()
-        self.fusion_model = LRCECount(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
-                                      frame_sample_size, temporal_scale, text_seq_len)
+        super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
+                         frame_sample_size, temporal_scale, text_seq_len)
