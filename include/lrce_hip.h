@@ -90,12 +90,16 @@ typedef struct LrceGemmDesc {
   int64_t workspace_elems;
   /* nn.Dropout fused into the epilogue (the recurrent decoder's dropouts, fusionv3.py:8-17): after
    * the bias / GELU / dGELU / row scale and before the RESID add, y = keep ? y / (1 - drop_p) : 0 with
-   * keep = lrce_uniform(drop_seed + device RNG offset, (m * n_cols + n) / drop_group) >= drop_p — the
+   * keep = uniform hash of (drop_seed + device RNG offset, (m * n_cols + n) / drop_group) >= drop_p — the
    * mask lrce_dropout / lrce_dropout_bwd draw for the same contiguous [m][n] tensor.  drop_p = 0: off.
    * Exact-f32 skinny path only (B f32, M <= 64); other paths reject drop_p > 0. */
   float drop_p;
   int32_t drop_group;
   uint64_t drop_seed;
+  /* f16 = 1: every 16-bit tensor of the call (A, B, a 16-bit C, aux_out, the DGELU aux) is IEEE
+   * fp16 instead of bf16 and the MFMAs are the f16 forms (v_mfma_f32_*_f16): the BERT forward runs
+   * in fp16 like the reference's fp16 autocast (agent_oe.py:28).  bf16 x bf16 LDS-DMA path only. */
+  int32_t f16;
 } LrceGemmDesc;
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);
@@ -112,7 +116,8 @@ int lrce_gemm(const LrceGemmDesc* desc, void* stream);
 int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_map, int nseg,
                        const float* w, const float* b, float eps,
                        void* y, int y_f32, uint16_t* y_bf16_copy, const int32_t* out_map,
-                       float* mean, float* rstd, int rows, int cols, void* stream);
+                       float* mean, float* rstd, int rows, int cols, int copy_f16, void* stream);
+/* copy_f16 = 1: the 16-bit copy is IEEE fp16 (the BERT forward operands) instead of bf16. */
 
 /* dy row r (read from dy_map[r] if given), x/mean/rstd as in forward.  dx for segment s is written
  * to row in_map[r*nseg+s] of dx (f32): dx = LN_bwd + (dres ? dres[same row] : 0).  dw/db (f32,
@@ -207,6 +212,9 @@ typedef struct LrceMhaDesc {
   float* dk2;
   float* dv2;
   int64_t ld_dkv2, stride_dkv2_b;
+  /* forward only: 1 = q, k, v and out are IEEE fp16 (BERT self-attention under the reference's
+   * fp16 autocast); f16 MFMA forms.  The backward reads bf16. */
+  int32_t f16;
 } LrceMhaDesc;
 
 int lrce_mha_fwd(const LrceMhaDesc* desc, void* stream);
@@ -232,6 +240,11 @@ int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, in
                 int rows_per_scale, float* out, void* stream);
 /* f32 -> bf16 cast (n elements) */
 int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
+/* f32 -> IEEE fp16 cast (n elements): the BERT forward's GEMM operands */
+int lrce_cast_f16(const float* x, uint16_t* y, int64_t n, void* stream);
+/* IEEE fp16 -> bf16 (n elements): the fp16 activations a BERT layer saved for its backward become
+ * the bf16 operands of the backward GEMMs / attention kernel (one pass over the layer's buffer) */
+int lrce_cast_f16_bf16(const uint16_t* x, uint16_t* y, int64_t n, void* stream);
 /* y[r][:] = bf16(x[r][:] * row_scale[r / rows_per_scale]) for a (rows x cols) f32 matrix (cols % 4 == 0):
  * a DropPath-scaled bf16 copy of a residual-stream gradient, the A operand of the branch's GEMMs. */
 int lrce_scale_cast_bf16(const float* x, int64_t rows, int cols, const float* row_scale, int rows_per_scale, uint16_t* y,
@@ -260,10 +273,12 @@ int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks,
 int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
                     const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
                     float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
-                    float* sumsq_next, void* stream);
+                    float* sumsq_next, uint16_t* p_f16, int64_t f16_lo, int64_t f16_hi, void* stream);
 /* step: optional device step count t (bc1/bc2 then computed from it: graph-safe).  sumsq_next:
  * optional zeroed buffer that receives ||p_t||^2 of the UPDATED parameters, i.e. the next step's
- * sumsq without a separate norm pass over the 1.25 GB master copy. */
+ * sumsq without a separate norm pass over the 1.25 GB master copy.  p_f16 (optional): an IEEE fp16
+ * shadow of elements [f16_lo, f16_hi) (multiples of 1024; element i at p_f16[i - f16_lo]) — the
+ * BERT weights the fp16 forward reads — written in the same pass. */
 
 /* BERT embeddings before their LayerNorm (HF BertEmbeddings): out[r] = word[ids[r]] + pos[r % L] +
  * type[types[r]] (f32 tables, int64 ids), and the scatter-add backward into the three tables. */

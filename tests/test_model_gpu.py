@@ -36,7 +36,8 @@ def test_bert_forward_matches_reference_golden():
         ids, mask, types = (torch.from_numpy(g[k + sfx]).cuda() for k in ("ids", "mask", "types"))
         with torch.no_grad():
             y = t(ids, mask, types)
-        assert rel(y, torch.from_numpy(g["y" + sfx])) < 2e-2
+        err = rel(y, torch.from_numpy(g["y" + sfx]))
+        assert err < 5e-3, err   # fp16 forward (reference: fp16 autocast)
 
 
 def test_bert_backward_matches_oracle():
@@ -143,19 +144,35 @@ def test_e2e_logits_match_reference_golden(name, batch):
         y = m(clips.cuda(), *(torch.from_numpy(g[k]).cuda() for k in ("ids", "mask", "types")))
     ref = torch.from_numpy(g["logits"])
     assert y.shape == ref.shape
-    # bf16 bar (BASELINE north_star "1e-2 bf16"), relative to max|logit|.  The single-output MC /
-    # Count heads are ill-conditioned for this metric (|logit| ~0.5, a 768-term cancellation): there
-    # the bar is the reference's OWN bf16 drift — the same model run by the oracle under bf16
-    # autocast — whichever is larger.  Measured: ours 0.92e-2 / 1.50e-2 / 1.43e-2 (OE/MC/Count) vs
-    # reference-bf16 1.07e-2 / 1.89e-2 / 2.97e-2.
+    # BASELINE north_star bar "1e-2 bf16", relative to max|logit|, for every head (no per-head
+    # escape hatch).  The BERT forward runs in fp16 like the reference's fp16 autocast; Swin and
+    # the decoder memory path in bf16, the decoder query side in exact f32.
     err = rel(y, ref)
-    if task == "oe":
-        assert err < 1e-2
+    assert err < 1e-2, (name, err)
+
+
+@pytest.mark.parametrize("name,batch", [("msvd-qa-oe", 10), ("msrvtt-qa-oe", 10), ("tgif-transition", 9)])
+def test_baseline_config_forward_matches_oracle(name, batch):
+    """BASELINE.json configs 2-5 at their own batch sizes (bs 10 msvd / msrvtt with temporal scale 3,
+    bs 9 tgif-transition 5-way MC; reference shapes e2e.py:22-25, fusionv3.py:230-265): eval-mode
+    logits of the HIP path vs the fp32 CPU oracle on the same synthetic batch, within the north-star
+    1e-2 (relative to max|logit|).  These are the tile / split choices the bench runs at bs 10."""
+    m, filled, task = _e2e(name, (3,))
+    L = CFG[name][2]
+    clips = W.synthetic_clips(batch, 3, seed=21)
+    if task == "mc":
+        ids, mask, types = W.synthetic_question(batch, L, seed=21, n_choice=5, ans_tokens=8)
     else:
-        ids, mask, types = (torch.from_numpy(g[k]) for k in ("ids", "mask", "types"))
-        with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
-            yb = O.e2e_forward(oracle_sd(filled), clips, ids, mask, types, task)
-        assert err < max(1e-2, rel(yb.float(), ref)), (err, rel(yb.float(), ref))
+        ids, mask, types = W.synthetic_question(batch, L, seed=21)
+    with torch.no_grad():
+        y = m(clips.cuda(), ids.cuda(), mask.cuda(), types.cuda()).float().cpu()
+    del m
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    with torch.no_grad():
+        yr = O.e2e_forward(oracle_sd(filled), clips, ids, mask, types, task)
+    assert y.shape == yr.shape
+    err = rel(y, yr)
+    assert err < 1e-2, (name, batch, err)
 
 
 def test_e2e_train_step_grads_match_oracle():

@@ -71,6 +71,57 @@ def test_gemm_tall_tiles(M, N, Kd, b_km):
     assert rel(C, ref) < 2e-3
 
 
+@pytest.mark.parametrize("M,N,Kd", [(320, 768, 768), (1800, 3072, 768), (300, 768, 3072), (17640, 512, 256)])
+def test_gemm_f16_forward(M, N, Kd):
+    """fp16 operands (the BERT forward, reference fp16 autocast): f16 MFMA, bias + GELU with the fp16
+    pre-activation, fp16 and f32 outputs; the 64x64, 128x128 and tall tiles all have an f16 form."""
+    k = K()
+    h = torch.float16
+    A = torch.randn(M, Kd, device=dev).to(h)
+    B = (torch.randn(N, Kd, device=dev) / math.sqrt(Kd)).to(h)
+    bias = torch.randn(N, device=dev)
+    ref_pre = A.double() @ B.double().t() + bias.double()
+    pre = torch.empty(M, N, device=dev, dtype=h)
+    g = k.linear(A, B, bias, gelu=True, pre_out=pre)
+    assert g.dtype == h and pre.dtype == h
+    assert rel(pre, ref_pre.float()) < 1e-3          # fp16 storage: 2^-11 relative
+    assert rel(g, F.gelu(ref_pre).float()) < 1e-3
+    y = k.linear(A, B, bias, out_f32=True)
+    assert rel(y, ref_pre.float()) < 1e-5            # exact products, f32 accumulation
+    with pytest.raises(Exception):
+        k.linear(A, B.to(torch.bfloat16), bias)      # mixed encodings are rejected
+
+
+def test_f16_casts():
+    k = K()
+    x = torch.randn(1000, 768, device=dev) * 3
+    h = torch.empty(x.shape, device=dev, dtype=torch.float16)
+    k.cast_f16(x, h)
+    assert torch.equal(h, x.to(torch.float16))
+    b = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    k.cast_f16_bf16(h, b)
+    assert torch.equal(b, h.float().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("L", [32, 40])
+def test_mha_self_f16_forward(L):
+    """BERT self-attention with fp16 q/k/v/out: vs an fp64 reference of HF's masked SDPA."""
+    k = K()
+    B, H, D = 6, 12, 64
+    q, kk, v = (torch.randn(B * L, H * D, device=dev).to(torch.float16) for _ in range(3))
+    mask = torch.ones(B, L, dtype=torch.int32, device=dev)
+    mask[:, 20:] = 0
+    out = torch.empty(B * L, H * D, device=dev, dtype=torch.float16)
+    lse = torch.empty(B, H, L, device=dev)
+    desc = k.mha_desc(q, L, k1=kk, v1=v, lk1=L, ld_kv1=H * D, stride_kv1_b=L * H * D, key_mask=mask, out=out, lse=lse,
+                      B=B, H=H, scale=0.125)
+    k.mha_fwd(desc, out)
+    qh, kh, vh = (t.double().view(B, L, H, D).transpose(1, 2) for t in (q, kk, v))
+    s = qh @ kh.transpose(-1, -2) * 0.125 + (1 - mask.double())[:, None, None, :] * -1e30
+    ref = (s.softmax(-1) @ vh).transpose(1, 2).reshape(B * L, H * D)
+    assert rel(out, ref.float()) < 2e-3
+
+
 @pytest.mark.parametrize("M,N,Kd", [(10, 768, 768), (50, 3072, 768), (45, 768, 3072), (128, 200, 96)])
 @pytest.mark.parametrize("a_km,b_km", [(1, 1), (1, 0), (0, 0)])
 def test_gemm_exact_f32_path(M, N, Kd, a_km, b_km):

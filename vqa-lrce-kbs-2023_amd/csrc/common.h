@@ -19,6 +19,42 @@ __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 
 __device__ __forceinline__ float bfbits2f(unsigned short u) { return __uint_as_float(((unsigned)u) << 16); }
 
+// IEEE fp16: the BERT forward operands (the reference runs under fp16 autocast, agent_oe.py:28).
+// 16-bit operands travel as bf16x8 bit patterns; these reinterpret them for the f16 MFMA forms.
+typedef _Float16 f16;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+__device__ __forceinline__ float h2f(f16 x) { return (float)x; }
+__device__ __forceinline__ f16 f2h(float x) { return (f16)x; }
+// one 16-bit storage element from f32 (bf16 or f16 encoding) and back
+template <bool F16>
+__device__ __forceinline__ bf16 to16(float x) {
+  if constexpr (F16) return __builtin_bit_cast(bf16, f2h(x));
+  else return f2bf(x);
+}
+template <bool F16>
+__device__ __forceinline__ float from16(bf16 x) {
+  if constexpr (F16) return h2f(__builtin_bit_cast(f16, x));
+  else return bf2f(x);
+}
+__device__ __forceinline__ bf16 to16r(float x, bool f16) { return f16 ? to16<true>(x) : to16<false>(x); }
+__device__ __forceinline__ float from16r(bf16 x, bool f16) { return f16 ? from16<true>(x) : from16<false>(x); }
+
+// 32x32x16 / 16x16x32 MFMA on 16-bit operands of either encoding
+template <bool F16>
+__device__ __forceinline__ f32x16 mfma32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 // GELU, erf form (torch F.gelu default, approximate='none'), and its derivative.
 // Phi(x) = 0.5 erfc(-x/sqrt2) from Abramowitz-Stegun 7.1.26 (|err(erf)| <= 1.5e-7): one rcp, one exp2,
 // five FMAs — libm erff is a two-range polynomial with branches and dominated the GELU-epilogue GEMMs.

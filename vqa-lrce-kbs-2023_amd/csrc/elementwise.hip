@@ -101,6 +101,32 @@ __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, l
   }
 }
 
+__global__ void cast_f16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    const float4 v = *reinterpret_cast<const float4*>(x + i);
+    bf16x4 o;
+    o[0] = to16<true>(v.x); o[1] = to16<true>(v.y); o[2] = to16<true>(v.z); o[3] = to16<true>(v.w);
+    *reinterpret_cast<bf16x4*>(y + i) = o;
+  } else {
+    for (long long j = i; j < n; ++j) y[j] = to16<true>(x[j]);
+  }
+}
+
+// fp16 -> bf16, 8 elements per thread (16-B loads / stores)
+__global__ void f16_bf16_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i + 7 < n) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(from16<true>(v[e]));
+    *reinterpret_cast<bf16x8*>(y + i) = o;
+  } else {
+    for (long long j = i; j < n; ++j) y[j] = f2bf(from16<true>(x[j]));
+  }
+}
+
 __global__ void scale_cast_kernel(const float* __restrict__ x, long long n4, int cols, const float* __restrict__ rsc, int rps,
                                   bf16* __restrict__ y) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -286,6 +312,25 @@ extern "C" int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stre
   const long long thr = (n + 3) / 4;
   cast_kernel<<<(thr + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(x, reinterpret_cast<bf16*>(y), n);
   return lrce_check_launch("cast_bf16");
+}
+
+extern "C" int lrce_cast_f16(const float* x, uint16_t* y, int64_t n, void* stream) {
+  if (!x || !y) return lrce_fail(LRCE_E_ARG, "cast_f16: null pointer");
+  if (n <= 0) return LRCE_OK;
+  const long long thr = (n + 3) / 4;
+  cast_f16_kernel<<<(thr + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(x, reinterpret_cast<bf16*>(y), n);
+  return lrce_check_launch("cast_f16");
+}
+
+extern "C" int lrce_cast_f16_bf16(const uint16_t* x, uint16_t* y, int64_t n, void* stream) {
+  if (!x || !y) return lrce_fail(LRCE_E_ARG, "cast_f16_bf16: null pointer");
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15)
+    return lrce_fail(LRCE_E_ARG, "cast_f16_bf16: buffers must be 16-B aligned");
+  if (n <= 0) return LRCE_OK;
+  const long long thr = (n + 7) / 8;
+  f16_bf16_kernel<<<(thr + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const bf16*>(x),
+                                                                                  reinterpret_cast<bf16*>(y), n);
+  return lrce_check_launch("cast_f16_bf16");
 }
 
 extern "C" int lrce_dropout(const float* x, const float* res, float* y, uint16_t* y_bf16, int64_t n, float p, uint64_t seed,

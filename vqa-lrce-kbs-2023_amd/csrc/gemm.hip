@@ -49,6 +49,7 @@ struct GemmP {
   int tiles_m, tiles_n;
   int vec;  // 1: c/aux/aux_out/bias rows are 16-B aligned and n % 8 == 0 (vector epilogue)
   float* ws; // split-K slabs [split][m][n] (plain stores, reduced by splitk_reduce_kernel), or null
+  int f16;   // 16-bit tensors are IEEE fp16 (LrceGemmDesc.f16)
 };
 
 // ---- LDS addressing --------------------------------------------------------------------------
@@ -166,10 +167,10 @@ __device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row
   x = x * p.alpha + (((fl & LRCE_EPI_BIAS) && first) ? p.bias[nn] : 0.f);
   x *= (nn < p.scale_cols) ? p.scale_val : 1.f;
   if (fl & LRCE_EPI_GELU) {
-    if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + nn] = f2bf(x);
+    if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + nn] = to16r(x, p.f16);
     x = gelu_f(x);
   }
-  if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + nn]));
+  if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(from16r(static_cast<const bf16*>(p.aux)[row * p.ld_aux + nn], p.f16));
   x *= rs;
   if ((fl & LRCE_EPI_RESID) && first) x += static_cast<const float*>(p.aux)[row * p.ld_aux + nn];
   if (fl & LRCE_EPI_ATOMIC) {
@@ -178,9 +179,9 @@ __device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row
     reinterpret_cast<float*>(cbase)[row * p.ldc + nn] += x;
   } else if (fl & LRCE_EPI_OUT_F32) {
     reinterpret_cast<float*>(cbase)[row * p.ldc + nn] = x;
-    if (fl & LRCE_EPI_OUT_BOTH) p.aux_out[row * p.ld_aux_out + nn] = f2bf(x);
+    if (fl & LRCE_EPI_OUT_BOTH) p.aux_out[row * p.ld_aux_out + nn] = to16r(x, p.f16);
   } else {
-    reinterpret_cast<bf16*>(cbase)[row * p.ldc + nn] = f2bf(x);
+    reinterpret_cast<bf16*>(cbase)[row * p.ldc + nn] = to16r(x, p.f16);
   }
 }
 
@@ -203,7 +204,7 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
       if (fl & LRCE_EPI_AUX_OUT) {
         bf16x8 pre;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) pre[e] = f2bf(v[e]);
+        for (int e = 0; e < 8; ++e) pre[e] = to16r(v[e], p.f16);
         *reinterpret_cast<bf16x8*>(p.aux_out + row * p.ld_aux_out + n) = pre;
       }
 #pragma unroll
@@ -212,7 +213,7 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
     if (fl & LRCE_EPI_DGELU) {
       const bf16x8 pre = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(p.aux) + row * p.ld_aux + n);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(bf2f(pre[e]));
+      for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(from16r(pre[e], p.f16));
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] *= rs;
@@ -236,13 +237,13 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
       if ((fl & LRCE_EPI_OUT_BOTH) && !(fl & LRCE_EPI_ACCUM)) {
         bf16x8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+        for (int e = 0; e < 8; ++e) o[e] = to16r(v[e], p.f16);
         *reinterpret_cast<bf16x8*>(p.aux_out + row * p.ld_aux_out + n) = o;
       }
     } else {
       bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+      for (int e = 0; e < 8; ++e) o[e] = to16r(v[e], p.f16);
       *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(cbase) + row * p.ldc + n) = o;
     }
     return;
@@ -495,7 +496,7 @@ struct GldsOperand {
   __device__ __forceinline__ void advance() { base += step; }
 };
 
-template <int TBM, int TBN, bool A_KM, bool B_KM>
+template <int TBM, int TBN, bool A_KM, bool B_KM, bool F16 = false>
 __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   constexpr int WM = TBM / 2, WN = TBN / 2;      // per-wave tile
   constexpr int IM = WM / 16, JN = WN / 16;      // 16x16 accumulator blocks per wave
@@ -533,7 +534,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   for (int i = 0; i < IM; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 ones;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = f2bf(1.0f);
+  for (int e = 0; e < 8; ++e) ones[e] = to16<F16>(1.0f);
 
   auto compute = [&](const bf16* la, const bf16* lb) {
 #pragma unroll
@@ -546,10 +547,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
 #pragma unroll
       for (int i = 0; i < IM; ++i)
 #pragma unroll
-        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < JN; ++j) acc[i][j] = mfma16x16x32<F16>(bfr[j], af[i], acc[i][j]);
       if (bias_block) {
 #pragma unroll
-        for (int i = 0; i < IM; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
+        for (int i = 0; i < IM; ++i) accb[i] = mfma16x16x32<F16>(ones, af[i], accb[i]);
       }
     }
   };
@@ -769,6 +770,7 @@ bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
   if (d && d->drop_p > 0.f && !d->b_f32) return lrce_fail(LRCE_E_ARG, "gemm: fused dropout is only on the exact-f32 skinny path");
   if (!d || !d->a || !d->b || !d->c) return lrce_fail(LRCE_E_ARG, "gemm: null pointer");
+  if (d->f16 && (d->a_f32 || d->b_f32)) return lrce_fail(LRCE_E_ARG, "gemm: f16 operands cannot be combined with f32 A/B");
   if (!(d->flags & LRCE_EPI_BIAS_GRAD)) return gemm_dispatch(d, stream);
   // bias gradient of a weight-gradient GEMM: db[m] += sum_k A(m, k)
   if (d->a_kmajor || !d->bias || d->batch != 1) return lrce_fail(LRCE_E_ARG, "gemm: BIAS_GRAD needs M-major A, bias, batch 1");
@@ -837,6 +839,9 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
           (!d->aux_out || (al16(d->aux_out) && d->ld_aux_out % 8 == 0));
   (void)out32;
   p.ws = nullptr;
+  p.f16 = d->f16 ? 1 : 0;
+  if (p.f16 && !(glds_ok(d) && d->a_kmajor && d->b_kmajor))
+    return lrce_fail(LRCE_E_ARG, "gemm: f16 needs 16-B aligned K-major bf16-layout operands (LDS-DMA path)");
   const bool use_ws = d->workspace && split > 1 && (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)) == 0 &&
                       (d->flags & LRCE_EPI_ATOMIC) && d->batch == 1 && !d->c_map && !d->row_scale && d->scale_cols == 0 &&
                       d->n % 4 == 0 && d->ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(d->c) & 15) == 0 &&
@@ -873,8 +878,12 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
       grid = dim3(p.tiles_m * p.tiles_n, d->batch * split);
     }
     const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0) | (small ? 4 : 0) | (tall_m == 192 ? 8 : 0) |
-                   (tall_m == 160 ? 16 : 0);
+                   (tall_m == 160 ? 16 : 0) | (p.f16 ? 32 : 0);
     switch (gk) {
+      case 32 + 11: gemm_glds_kernel<192, 128, true, true, true><<<grid, NT, 0, s>>>(p); break;
+      case 32 + 19: gemm_glds_kernel<160, 128, true, true, true><<<grid, NT, 0, s>>>(p); break;
+      case 32 + 3: gemm_glds_kernel<128, 128, true, true, true><<<grid, NT, 0, s>>>(p); break;
+      case 32 + 7: gemm_glds_kernel<64, 64, true, true, true><<<grid, NT, 0, s>>>(p); break;
       case 11: gemm_glds_kernel<192, 128, true, true><<<grid, NT, 0, s>>>(p); break;
       case 10: gemm_glds_kernel<192, 128, true, false><<<grid, NT, 0, s>>>(p); break;
       case 19: gemm_glds_kernel<160, 128, true, true><<<grid, NT, 0, s>>>(p); break;

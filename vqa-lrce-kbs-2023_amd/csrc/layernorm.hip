@@ -31,6 +31,12 @@ __device__ __forceinline__ void st4<bf16>(bf16* p, float4 v) {
   *reinterpret_cast<bf16x4*>(p) = o;
 }
 
+__device__ __forceinline__ void st4_16(bf16* p, float4 v, bool f16) {
+  bf16x4 o;
+  o[0] = to16r(v.x, f16); o[1] = to16r(v.y, f16); o[2] = to16r(v.z, f16); o[3] = to16r(v.w, f16);
+  *reinterpret_cast<bf16x4*>(p) = o;
+}
+
 // address of the 4-chunk c (element 4c) of LN row r inside x
 __device__ __forceinline__ long long src_off(const int* in_map, int nseg, int seg, int r, int c, int& valid) {
   const int e = c * 4;
@@ -53,7 +59,7 @@ __device__ __forceinline__ float row_sum(float v) {
 template <typename TX, typename TY, int CH, int LPR>
 __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, int nseg, const float* w, const float* b,
                                               float eps, TY* y, bf16* y2, const int* out_map, float* mean_o, float* rstd_o,
-                                              int rows, int cols) {
+                                              int rows, int cols, int y2_f16) {
   constexpr int RPW = 64 / LPR;
   const int lane = threadIdx.x & 63, sl = lane % LPR;
   const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
@@ -102,7 +108,7 @@ __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, in
       o.z = (v[t].z - mean) * rstd * ww[t].z + bb[t].z;
       o.w = (v[t].w - mean) * rstd * ww[t].w + bb[t].w;
       st4<TY>(y + orow * cols + 4 * c, o);
-      if (y2) st4<bf16>(y2 + orow * cols + 4 * c, o);
+      if (y2) st4_16(y2 + orow * cols + 4 * c, o, y2_f16 != 0);
     }
   }
   if (sl == 0) {
@@ -288,7 +294,7 @@ int ln_bwd_lpr(int cols) { return cols / 4 <= 32 ? 32 : 64; }
 
 extern "C" int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_map, int nseg, const float* w,
                                   const float* b, float eps, void* y, int y_f32, uint16_t* y2, const int32_t* out_map,
-                                  float* mean, float* rstd, int rows, int cols, void* stream) {
+                                  float* mean, float* rstd, int rows, int cols, int copy_f16, void* stream) {
   if (!x || !y || !w || !b) return lrce_fail(LRCE_E_ARG, "layernorm_fwd: null pointer");
   if (nseg < 1) nseg = 1;
   if (cols % 4 || (cols / nseg) % 4 || cols % nseg || cols > 64 * 4 * MAXC)
@@ -299,7 +305,7 @@ extern "C" int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_ma
 #define LNF3(TX, TY, CH, LPR)                                                                                          \
   ln_fwd<TX, TY, CH, LPR><<<(rows + 4 * (64 / LPR) - 1) / (4 * (64 / LPR)), 256, 0, s>>>(                              \
       static_cast<const TX*>(x), in_map, nseg, w, b, eps, static_cast<TY*>(y), reinterpret_cast<bf16*>(y2), out_map, mean, \
-      rstd, rows, cols)
+      rstd, rows, cols, copy_f16)
 #define LNF(TX, TY)                                   \
   if (nch <= 32) LNF3(TX, TY, 1, 32);                 \
   else if (nch <= 64) LNF3(TX, TY, 1, 64);            \

@@ -396,6 +396,13 @@ __device__ __forceinline__ bf16x8 pack8f(const f32x16& a, int s) {
   for (int j = 0; j < 8; ++j) o[j] = f2bf(a[8 * s + j]);
   return o;
 }
+template <bool F16>
+__device__ __forceinline__ bf16x8 pack8t(const f32x16& a, int s) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = to16<F16>(a[8 * s + j]);
+  return o;
+}
 __device__ __forceinline__ bf16x8 ldrow16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 // rows [0, LP) x 64 of a head slice into an LDS image (rows >= n zero)
@@ -411,7 +418,7 @@ __device__ __forceinline__ void stage64(bf16* img, const bf16* src, long long ld
   }
 }
 
-template <int NTL>
+template <int NTL, bool F16>
 __global__ void __launch_bounds__(256) mhaL_fwd_kernel(MhaP P) {
   constexpr int LP = 32 * NTL;
   const LrceMhaDesc& d = P.d;
@@ -456,7 +463,7 @@ __global__ void __launch_bounds__(256) mhaL_fwd_kernel(MhaP P) {
     for (int kt = 0; kt < NTL; ++kt) {
       acc[kt] = f32x16{};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][s], qf[s], acc[kt], 0, 0, 0);
+      for (int s = 0; s < 4; ++s) acc[kt] = mfma32x32x16<F16>(kf[kt][s], qf[s], acc[kt]);
     }
     float m = -1.0e30f;
 #pragma unroll
@@ -480,10 +487,9 @@ __global__ void __launch_bounds__(256) mhaL_fwd_kernel(MhaP P) {
     for (int kt = 0; kt < NTL; ++kt)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 pb = pack8f(acc[kt], s);
+        const bf16x8 pb = pack8t<F16>(acc[kt], s);
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_perm64(vimg, kt * 32 + 16 * s, 32 * dt, lane), pb, o[dt], 0, 0, 0);
+        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32x32x16<F16>(tr_perm64(vimg, kt * 32 + 16 * s, 32 * dt, lane), pb, o[dt]);
       }
     if (qi < L) {
       const float inv = 1.0f / sum;
@@ -494,7 +500,7 @@ __global__ void __launch_bounds__(256) mhaL_fwd_kernel(MhaP P) {
         for (int rr = 0; rr < 4; ++rr) {
           bf16x4 v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][4 * rr + e] * inv);
+          for (int e = 0; e < 4; ++e) v[e] = to16<F16>(o[dt][4 * rr + e] * inv);
           *reinterpret_cast<bf16x4*>(dst + 32 * dt + 8 * rr) = v;
         }
       if (hh == 0) d.lse[((long long)b * d.H + h) * L + qi] = m * d.scale + __logf(sum);
@@ -670,10 +676,17 @@ extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
   MhaP p{*d, lrce_rng_offset()};
   if (short_self(d)) {
     const unsigned nb = (d->B * d->H + 3) / 4;
-    if (d->Lq <= 32) mhaL_fwd_kernel<1><<<nb, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
-    else mhaL_fwd_kernel<2><<<nb, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (d->f16) {
+      if (d->Lq <= 32) mhaL_fwd_kernel<1, true><<<nb, 256, 0, st>>>(p);
+      else mhaL_fwd_kernel<2, true><<<nb, 256, 0, st>>>(p);
+    } else {
+      if (d->Lq <= 32) mhaL_fwd_kernel<1, false><<<nb, 256, 0, st>>>(p);
+      else mhaL_fwd_kernel<2, false><<<nb, 256, 0, st>>>(p);
+    }
     return lrce_check_launch("mha_fwd(mfma)");
   }
+  if (d->f16) return lrce_fail(LRCE_E_ARG, "mha_fwd: f16 io only on the short self-attention path (Lq = Lk <= 64)");
   if (d->Lq == 1 && aligned_rows(d)) {
     mha1_fwd_kernel<<<d->B * d->H, 256, 0, static_cast<hipStream_t>(stream)>>>(p);
     return lrce_check_launch("mha_fwd");
@@ -684,6 +697,7 @@ extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
 
 extern "C" int lrce_mha_bwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, true)) return rc;
+  if (d->f16) return lrce_fail(LRCE_E_ARG, "mha_bwd: the backward reads bf16 (cast the fp16 forward tensors)");
   MhaP p{*d, lrce_rng_offset()};
   if (short_self(d)) {
     const unsigned nb = (d->B * d->H + 1) / 2;

@@ -35,7 +35,8 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
                                                     const float* __restrict__ tensor_lr, const float* __restrict__ sumsq,
                                                     bf16* __restrict__ pb, int n_chunks, float b1, float b2, float eps, float wd,
                                                     float gscale, float reg, float bc1, float bc2, const float* __restrict__ step_dev,
-                                                    float* __restrict__ sumsq_next) {
+                                                    float* __restrict__ sumsq_next, bf16* __restrict__ ph, long long h_lo,
+                                                    long long h_hi) {
   const int c0 = blockIdx.x * ADAMW_CH;
   if (step_dev) {
     const float t = *step_dev;
@@ -87,6 +88,11 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
     *reinterpret_cast<float4*>(m + i) = mm;
     *reinterpret_cast<float4*>(v + i) = vv;
     if (pb) *reinterpret_cast<bf16x4*>(pb + i) = ob;
+    if (ph && i >= h_lo && i < h_hi) {   // fp16 shadow of the BERT range (chunk-uniform branch)
+      bf16x4 oh;
+      oh[0] = to16<true>(pp.x); oh[1] = to16<true>(pp.y); oh[2] = to16<true>(pp.z); oh[3] = to16<true>(pp.w);
+      *reinterpret_cast<bf16x4*>(ph + (i - h_lo)) = oh;
+    }
     q += pp.x * pp.x + pp.y * pp.y + pp.z * pp.z + pp.w * pp.w;
   }
   flush();
@@ -106,11 +112,14 @@ extern "C" int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, in
 extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
                                const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
                                float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
-                               float* sumsq_next, void* stream) {
+                               float* sumsq_next, uint16_t* p_f16, int64_t f16_lo, int64_t f16_hi, void* stream) {
   if (!p || !g || !m || !v || !chunk_tensor || !tensor_lr) return lrce_fail(LRCE_E_ARG, "adamw_step: null pointer");
+  if (p_f16 && (f16_lo % 1024 || f16_hi % 1024 || f16_lo < 0 || f16_hi < f16_lo))
+    return lrce_fail(LRCE_E_ARG, "adamw_step: f16 shadow range [%lld, %lld) not chunk aligned", (long long)f16_lo, (long long)f16_hi);
   if (n_chunks > 0)
     adamw_kernel<<<(n_chunks + ADAMW_CH - 1) / ADAMW_CH, 256, 0, static_cast<hipStream_t>(stream)>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq,
                                                                          reinterpret_cast<bf16*>(p_bf16), n_chunks, beta1, beta2, eps,
-                                                                         weight_decay, grad_scale, reg, bc1, bc2, step, sumsq_next);
+                                                                         weight_decay, grad_scale, reg, bc1, bc2, step, sumsq_next,
+                                                                         reinterpret_cast<bf16*>(p_f16), f16_lo, f16_hi);
   return lrce_check_launch("adamw_step");
 }

@@ -50,6 +50,7 @@ class GemmDesc(ctypes.Structure):
         ("b_f32", ctypes.c_int32),
         ("workspace", ctypes.c_void_p), ("workspace_elems", ctypes.c_int64),
         ("drop_p", ctypes.c_float), ("drop_group", ctypes.c_int32), ("drop_seed", ctypes.c_uint64),
+        ("f16", ctypes.c_int32),
     ]
 
 
@@ -66,6 +67,7 @@ class MhaDesc(ctypes.Structure):
         ("dout", ctypes.c_void_p), ("dq", ctypes.c_void_p), ("ld_dq", ctypes.c_int64),
         ("dk1", ctypes.c_void_p), ("dv1", ctypes.c_void_p), ("ld_dkv1", ctypes.c_int64), ("stride_dkv1_b", ctypes.c_int64),
         ("dk2", ctypes.c_void_p), ("dv2", ctypes.c_void_p), ("ld_dkv2", ctypes.c_int64), ("stride_dkv2_b", ctypes.c_int64),
+        ("f16", ctypes.c_int32),
     ]
 
 
@@ -81,7 +83,7 @@ _U64 = ctypes.c_uint64
 
 _SIGS = {
     "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
-    "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _P],
+    "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _I64,
                            _P],
     "lrce_scale_cast_bf16": [_P, _I64, _I, _P, _I, _P, _P],
@@ -97,6 +99,8 @@ _SIGS = {
     "lrce_patch_im2col": [_P, _I, _I, _I, _I, _I64, _I64, _I64, _I, _P, _P],
     "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _I, _P, _P],
     "lrce_cast_bf16": [_P, _P, _I64, _P],
+    "lrce_cast_f16": [_P, _P, _I64, _P],
+    "lrce_cast_f16_bf16": [_P, _P, _I64, _P],
     "lrce_dropout": [_P, _P, _P, _P, _I64, _F, _U64, _I64, _P],
     "lrce_dropout_bwd": [_P, _P, _P, _I64, _F, _U64, _I64, _P],
     "lrce_bert_embed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
@@ -106,7 +110,8 @@ _SIGS = {
     "lrce_text_posembed_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_text_posembed_bwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_l2norm_multi": [_P, _P, _I, _P, _I, _P],
-    "lrce_adamw_step": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _F, _P, _P, _P],
+    "lrce_adamw_step": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _F, _P, _P, _P, _I64, _I64,
+                        _P],
     "lrce_set_rng_offset": [_P],
     "lrce_version": [],
     "lrce_last_error": [],

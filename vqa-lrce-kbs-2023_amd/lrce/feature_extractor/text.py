@@ -9,7 +9,8 @@ branches in train mode) with the SAME parameter names (`bert.embeddings.*`, `ber
 `bert.pooler.dense`), so HF checkpoints load unchanged (`bert.embeddings.position_ids`, a persistent
 buffer in 4.20, is accepted and ignored).  The pooler is kept for the schema but, as in the
 reference (its output is never used by the loss), not computed.  No network fetch: weights come
-from a checkpoint or the caller.
+from a checkpoint or the caller.  The encoder's forward operands are fp16 (the reference runs
+BERT under fp16 autocast), its backward bf16.
 """
 import torch
 import torch.nn as nn
@@ -121,42 +122,52 @@ class _EmbedFn(torch.autograd.Function):
 
 
 class _LayerFn(torch.autograd.Function):
-    """One post-norm BERT layer (HF BertLayer): x -> LN(x + drop(attn_out)) -> LN(. + drop(FFN))."""
+    """One post-norm BERT layer (HF BertLayer): x -> LN(x + drop(attn_out)) -> LN(. + drop(FFN)).
+
+    Forward GEMM / attention operands are IEEE fp16, as under the reference's fp16 autocast
+    (agent_oe.py:28; bf16 here would put BERT's rounding error at ~1e-2 of the MC / Count logits).
+    Every 16-bit activation the backward needs lives in ONE fp16 buffer that the backward casts to
+    bf16 in one pass: the backward GEMMs keep bf16's range for the small gradients."""
 
     @staticmethod
     def forward(ctx, x, mask, layer, flat, p, seed, B, L, *params):
         dev = x.device
         rows = B * L
         sa, ao, it, oo = layer.attention.self, layer.attention.output, layer.intermediate, layer.output
-        xb = torch.empty(rows, HIDDEN, dtype=torch.bfloat16, device=dev)
-        K.cast_bf16(x, xb)
-        q = K.linear(xb, flat.w16(sa.query.weight), sa.query.bias)
-        k = K.linear(xb, flat.w16(sa.key.weight), sa.key.bias)
-        v = K.linear(xb, flat.w16(sa.value.weight), sa.value.bias)
-        ctxt = torch.empty(rows, HIDDEN, dtype=torch.bfloat16, device=dev)
+        sizes = [rows * HIDDEN] * 6 + [rows * INTER] * 2
+        buf = torch.empty(sum(sizes), dtype=torch.float16, device=dev)
+        xb, q, k, v, ctxt, h1b, g, pre = _views(buf, rows)
+        w = flat.w16h
+        K.cast_f16(x, xb)
+        K.linear(xb, w(sa.query.weight), sa.query.bias, out=q)
+        K.linear(xb, w(sa.key.weight), sa.key.bias, out=k)
+        K.linear(xb, w(sa.value.weight), sa.value.bias, out=v)
         lse = torch.empty(B, HEADS, L, device=dev)
         desc = K.mha_desc(q, L, k1=k, v1=v, lk1=L, ld_kv1=HIDDEN, stride_kv1_b=L * HIDDEN, key_mask=mask, out=ctxt,
                           lse=lse, B=B, H=HEADS, scale=0.125, drop_p=p, seed=seed)
         K.mha_fwd(desc, ctxt)
-        a = K.linear(ctxt, flat.w16(ao.dense.weight), ao.dense.bias, out_f32=True)
+        a = K.linear(ctxt, w(ao.dense.weight), ao.dense.bias, out_f32=True)
         a2 = K.dropout(a, p, seed + 1, res=x)
-        h1b = torch.empty(rows, HIDDEN, dtype=torch.bfloat16, device=dev)
         h1, m1, r1 = K.layernorm(a2, ao.LayerNorm.weight, ao.LayerNorm.bias, EPS, out_f32=True, bf16_copy=h1b)
-        pre = torch.empty(rows, INTER, dtype=torch.bfloat16, device=dev)
-        g = K.linear(h1b, flat.w16(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre)
-        o = K.linear(g, flat.w16(oo.dense.weight), oo.dense.bias, out_f32=True)
+        K.linear(h1b, w(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre, out=g)
+        o = K.linear(g, w(oo.dense.weight), oo.dense.bias, out_f32=True)
         o2 = K.dropout(o, p, seed + 2, res=h1)
         out, m2, r2 = K.layernorm(o2, oo.LayerNorm.weight, oo.LayerNorm.bias, EPS, out_f32=True)
-        ctx.save = (xb, q, k, v, mask, ctxt, lse, a2, m1, r1, h1b, pre, g, o2, m2, r2)
+        ctx.save = (buf, mask, lse, a2, m1, r1, o2, m2, r2)
         ctx.desc = desc
         ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L = layer, flat, p, seed, B, L
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        xb, q, k, v, mask, ctxt, lse, a2, m1, r1, h1b, pre, g, o2, m2, r2 = ctx.save
+        buf, mask, lse, a2, m1, r1, o2, m2, r2 = ctx.save
         layer, flat, p, seed, B, L = ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L
         sa, ao, it, oo = layer.attention.self, layer.attention.output, layer.intermediate, layer.output
+        rows = B * L
+        b16 = torch.empty(buf.shape, dtype=torch.bfloat16, device=buf.device)
+        K.cast_f16_bf16(buf, b16)
+        del buf
+        xb, q, k, v, ctxt, h1b, g, pre = _views(b16, rows)
         dout = dout.contiguous()
         do2 = torch.empty_like(o2)
         K.layernorm_bwd(dout, o2, m2, r2, oo.LayerNorm.weight, do2, dw=_g(flat, oo.LayerNorm.weight),
@@ -173,9 +184,9 @@ class _LayerFn(torch.autograd.Function):
         da = _grad16(da2, p, seed + 1)
         _wgrad(flat, ao.dense, da, ctxt)
         dctx = K.linear_dx(da, flat.w16(ao.dense.weight), out_f32=False)
-        rows = B * L
         dqkv = torch.zeros(3, rows, HIDDEN, device=dout.device)
-        K.mha_bwd(ctx.desc, dout=dctx, dq=dqkv[0], dk1=dqkv[1], dv1=dqkv[2], ld_dkv1=HIDDEN, stride_dkv1_b=L * HIDDEN)
+        desc = K.mha_rebind(ctx.desc, q=q, k1=k, v1=v, out=ctxt)
+        K.mha_bwd(desc, dout=dctx, dq=dqkv[0], dk1=dqkv[1], dv1=dqkv[2], ld_dkv1=HIDDEN, stride_dkv1_b=L * HIDDEN)
         dqkv16 = torch.empty(3, rows, HIDDEN, dtype=torch.bfloat16, device=dout.device)
         K.cast_bf16(dqkv, dqkv16)
         for i, lin in enumerate((sa.query, sa.key, sa.value)):
@@ -186,6 +197,15 @@ class _LayerFn(torch.autograd.Function):
         ctx.save = ctx.desc = None
         flat.notify(layer.parameters())
         return (dx,) + (None,) * (7 + len(ctx.needs_input_grad[8:]))
+
+
+def _views(buf, rows):
+    """xb, q, k, v, ctxt, h1b [rows, 768] and g, pre [rows, 3072] of one layer's 16-bit buffer."""
+    out, o = [], 0
+    for cols in (HIDDEN,) * 6 + (INTER,) * 2:
+        out.append(buf[o:o + rows * cols].view(rows, cols))
+        o += rows * cols
+    return out
 
 
 def _grad16(d32, p, seed):
@@ -216,6 +236,10 @@ class BertModel(nn.Module):
         self.hidden_dropout, self.attention_dropout = hidden_dropout, attention_dropout
         if hidden_dropout != attention_dropout:
             raise ValueError("bert-base uses one dropout rate (0.1) for hidden states and attention probs")
+
+    def lrce_f16_params(self):
+        """Parameters whose fp16 shadow the forward reads (the encoder linears; runtime.bind)."""
+        return list(self.encoder.parameters())
 
     def forward(self, input_ids, attention_mask=None, token_type_ids=None):
         flat = ensure(self)

@@ -47,7 +47,33 @@ class FlatParams:
         self.chunk_tensor = chunk_tensor.to(self.device)
         self.n_chunks = self.total // ALIGN
         self._bf16_version = -1
+        self.f16 = None            # optional IEEE fp16 shadow of [f16_lo, f16_hi) (enable_f16)
+        self.f16_lo = self.f16_hi = 0
         self.attach_grads(zero=True)
+
+    def enable_f16(self, params):
+        """Keep an fp16 shadow of the flat range spanning `params` (the BERT weights: its forward
+        runs in fp16 like the reference's autocast).  The optimizer refreshes it with the bf16 one."""
+        params = [p for p in params if self.owns(p)]
+        if not params:
+            return
+        lo = min(self.range_of(p)[0] for p in params)
+        hi = max(self.range_of(p)[1] for p in params)
+        self.f16_lo, self.f16_hi = lo, hi
+        self.f16 = torch.empty(hi - lo, dtype=torch.float16, device=self.device)
+        K.cast_f16(self.f16_src(), self.f16)
+        self._bf16_version = -1
+
+    def f16_src(self):
+        return self.f32[self.f16_lo:self.f16_hi]
+
+    def w16h(self, p):
+        """fp16 shadow of p (enable_f16 must cover it)."""
+        i = self._index[id(p)]
+        off = self.offsets[i] - self.f16_lo
+        if self.f16 is None or off < 0 or off + p.numel() > self.f16.numel():
+            raise RuntimeError(f"no fp16 shadow for {self.names.get(id(p), '?')}: call enable_f16 first")
+        return self.f16[off:off + p.numel()].view(p.shape)
 
     def notify(self, params):
         """Called by native autograd Functions when their parameters' gradients are final."""
@@ -89,6 +115,8 @@ class FlatParams:
         v = self._versions()
         if v != self._bf16_version:
             K.cast_bf16(self.f32, self.bf16)
+            if self.f16 is not None:
+                K.cast_f16(self.f16_src(), self.f16)
             self._bf16_version = self._versions()
 
     def mark_bf16_fresh(self):

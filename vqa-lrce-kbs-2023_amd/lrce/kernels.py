@@ -13,6 +13,7 @@ from . import _native as N
 from ._native import ptr, stream_of, call
 
 BF16 = torch.bfloat16
+F16 = torch.float16
 F32 = torch.float32
 NUM_CU = 256
 
@@ -99,14 +100,16 @@ def _chk(t, dtype=None, name="tensor"):
 def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, flags=0, bias=None,
          aux=None, ld_aux=0, aux_out=None, ld_aux_out=0, a_map=None, c_map=None, alpha=1.0, split_k=1,
          scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, a_row_scale=None, a_rows_per_scale=1,
-         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None):
+         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None, f16=False):
     """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc.  drop = (p, seed, group):
-    nn.Dropout fused into the epilogue (exact-f32 skinny path; same mask as dropout())."""
+    nn.Dropout fused into the epilogue (exact-f32 skinny path; same mask as dropout()).  f16: every
+    16-bit tensor (A, B, 16-bit C, aux_out) is torch.float16 (the BERT forward)."""
     _chk(a, None, "A"); _chk(b, None, "B"); _chk(c, None, "C")
     a_f32 = a.dtype == F32
     b_f32 = b.dtype == F32
-    if (not a_f32 and a.dtype != BF16) or (not b_f32 and b.dtype != BF16):
-        raise N.NativeError("gemm: operands must be bf16 or f32")
+    h = F16 if f16 else BF16
+    if (not a_f32 and a.dtype != h) or (not b_f32 and b.dtype != h):
+        raise N.NativeError(f"gemm: operands must be {h} or f32")
     if lda is None:
         lda = k if a_kmajor else m
     if ldb is None:
@@ -127,6 +130,7 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.row_scale, d.rows_per_scale = ptr(row_scale), rows_per_scale
     d.a_row_scale, d.a_rows_per_scale = ptr(a_row_scale), a_rows_per_scale
     d.b_f32 = int(b_f32)
+    d.f16 = int(f16)
     if workspace is not None:
         d.workspace, d.workspace_elems = ptr(workspace), workspace.numel()
     if drop is not None and drop[0] > 0:
@@ -154,6 +158,7 @@ def _skinny_drop_ok(x, w, M, a_map=None):
 def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None, resid=None, c_map=None,
            a_map=None, rows=None, scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, bf16_shadow=None,
            drop=None):
+    f16 = x.dtype == F16
     """y = x W^T (+b) [gelu] [*row_scale] [dropout] [+resid]; x [M,K] bf16/f32, W [N,K] bf16 (or f32:
     exact path).  drop = (p, seed, group): fused into the skinny epilogue, else a dropout launch."""
     M = rows if rows is not None else x.shape[0]
@@ -175,7 +180,7 @@ def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None
         flags |= N.EPI_RESID
     if out is None:
         out = torch.empty((M if c_map is None else resid.shape[0] if resid is not None else M, Nn),
-                          dtype=F32 if out_f32 else BF16, device=x.device)
+                          dtype=F32 if out_f32 else (F16 if f16 else BF16), device=x.device)
     if out.dtype == F32:
         flags |= N.EPI_OUT_F32
         if bf16_shadow is not None:
@@ -184,7 +189,7 @@ def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None
     aux_out = pre_out if gelu else bf16_shadow
     gemm(x, w, out, M, Nn, K, flags=flags, bias=bias, aux=aux, ld_aux=Nn, aux_out=aux_out, ld_aux_out=Nn,
          a_map=a_map, c_map=c_map, scale_cols=scale_cols, scale_val=scale_val, row_scale=row_scale,
-         rows_per_scale=rows_per_scale, drop=drop)
+         rows_per_scale=rows_per_scale, drop=drop, f16=f16)
     return out
 
 
@@ -241,6 +246,7 @@ def colsum(x, out, *, row_map=None, rows=None, row_scale=None, rows_per_scale=1)
 
 def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out_map=None, rows=None, cols=None,
               stats=True, out_rows=None, bf16_copy=None):
+    """bf16_copy: optional 16-bit copy of y (bf16, or torch.float16 for the fp16 BERT forward)."""
     R = rows if rows is not None else x.shape[0]
     Cc = cols if cols is not None else x.shape[-1] * nseg
     if out is None:
@@ -248,7 +254,8 @@ def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out
     mean = torch.empty(R, dtype=F32, device=x.device) if stats else None
     rstd = torch.empty(R, dtype=F32, device=x.device) if stats else None
     call("lrce_layernorm_fwd", ptr(x), int(x.dtype == F32), ptr(in_map), nseg, ptr(w), ptr(b), eps, ptr(out),
-         int(out.dtype == F32), ptr(bf16_copy), ptr(out_map), ptr(mean), ptr(rstd), R, Cc, stream_of(out))
+         int(out.dtype == F32), ptr(bf16_copy), ptr(out_map), ptr(mean), ptr(rstd), R, Cc,
+         int(bf16_copy is not None and bf16_copy.dtype == F16), stream_of(out))
     return out, mean, rstd
 
 
@@ -388,6 +395,7 @@ def wattn_dbias_gather(ds, n_win, nH, csr, table_grad):
 def mha_desc(q, Lq, *, k1, v1, lk1, ld_kv1, stride_kv1_b, kv1_bdiv=1, k2=None, v2=None, lk2=0, ld_kv2=0,
              stride_kv2_b=0, kv2_bdiv=1, key_mask=None, out, lse, B, H, scale, ld_q=None, ld_o=None, drop_p=0.0,
              seed=0, d=64):
+    """q/k/v/out torch.float16 selects the fp16 forward (BERT); the backward reads bf16 tensors."""
     m = N.MhaDesc()
     m.q, m.ld_q = ptr(q), ld_q if ld_q is not None else H * d
     m.k1, m.v1, m.ld_kv1, m.stride_kv1_b, m.kv1_bdiv, m.lk1 = ptr(k1), ptr(v1), ld_kv1, stride_kv1_b, kv1_bdiv, lk1
@@ -396,6 +404,7 @@ def mha_desc(q, Lq, *, k1, v1, lk1, ld_kv1, stride_kv1_b, kv1_bdiv=1, k2=None, v
     m.B, m.H, m.Lq, m.d, m.scale = B, H, Lq, d, scale
     m.drop_p, m.seed = float(drop_p), seed & (2 ** 64 - 1)
     m.f32_io = int(q.dtype == F32)
+    m.f16 = int(q.dtype == F16)
     if (out.dtype == F32) != (q.dtype == F32):
         raise N.NativeError("mha: q and out must share dtype (bf16, or f32 for the decoder path)")
     return m
@@ -403,6 +412,14 @@ def mha_desc(q, Lq, *, k1, v1, lk1, ld_kv1, stride_kv1_b, kv1_bdiv=1, k2=None, v
 
 def mha_fwd(desc, stream_tensor):
     call("lrce_mha_fwd", ctypes.byref(desc), stream_of(stream_tensor))
+
+
+def mha_rebind(desc, *, q, k1, v1, out):
+    """Point a forward descriptor at bf16 copies of its q / k / v / out (the backward of an fp16
+    forward reads bf16)."""
+    desc.q, desc.k1, desc.v1, desc.out = ptr(q), ptr(k1), ptr(v1), ptr(out)
+    desc.f16 = 0
+    return desc
 
 
 def mha_bwd(desc, *, dout, dq, dk1, dv1, ld_dkv1, stride_dkv1_b, dk2=None, dv2=None, ld_dkv2=0, stride_dkv2_b=0,
@@ -428,6 +445,15 @@ def patch_im2col(clips, patches, *, layout="BSTCHW", normalize=True):
 
 def cast_bf16(x, y):
     call("lrce_cast_bf16", ptr(x), ptr(y), x.numel(), stream_of(y))
+
+
+def cast_f16(x, y):
+    call("lrce_cast_f16", ptr(x), ptr(y), x.numel(), stream_of(y))
+
+
+def cast_f16_bf16(x, y):
+    _chk(x, F16, "x"); _chk(y, BF16, "y")
+    call("lrce_cast_f16_bf16", ptr(x), ptr(y), x.numel(), stream_of(y))
 
 
 def dropout(x, p, seed, out=None, out_bf16=None, res=None, group=1):
@@ -484,11 +510,12 @@ def l2norm_multi(p, chunk_tensor, n_chunks, sumsq, n_tensors):
 
 
 def adamw_step(p, g, m, v, chunk_tensor, tensor_lr, sumsq, p_bf16, n_chunks, beta1, beta2, eps, wd, grad_scale, reg,
-               bc1, bc2, step=None, sumsq_next=None):
+               bc1, bc2, step=None, sumsq_next=None, p_f16=None, f16_range=(0, 0)):
     """step: optional f32 device scalar holding t (bias corrections computed on device: graph-safe).
     sumsq_next: optional zeroed [n_tensors] buffer receiving ||p_t||^2 of the updated parameters."""
     call("lrce_adamw_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(chunk_tensor), ptr(tensor_lr), ptr(sumsq), ptr(p_bf16),
-         n_chunks, beta1, beta2, eps, wd, grad_scale, reg, bc1, bc2, ptr(step), ptr(sumsq_next), stream_of(p))
+         n_chunks, beta1, beta2, eps, wd, grad_scale, reg, bc1, bc2, ptr(step), ptr(sumsq_next), ptr(p_f16),
+         int(f16_range[0]), int(f16_range[1]), stream_of(p))
 
 
 _RNG_OFFSETS = {}

@@ -72,7 +72,7 @@ class FusedAdamW(torch.optim.Optimizer):
         K.adamw_step(flat.f32, flat.grad, self.exp_avg, self.exp_avg_sq, flat.chunk_tensor, self.tensor_lr, self.sumsq,
                      flat.bf16, flat.n_chunks, b1, b2, self.defaults["eps"], self.defaults["weight_decay"],
                      float(grad_scale), self.reg_strength, 1.0 - b1 ** t, 1.0 - b2 ** t, step=self.step_t,
-                     sumsq_next=self.sumsq_next)
+                     sumsq_next=self.sumsq_next, p_f16=flat.f16, f16_range=(flat.f16_lo, flat.f16_hi))
         self.sumsq.copy_(self.sumsq_next)
         self._norm_version = flat.master_version()
         flat.mark_bf16_fresh()

@@ -30,6 +30,9 @@ def bind(root, device=None):
             raise RuntimeError(f"buffer {name} not on {device}: call model.to(device) first")
     order = root.lrce_param_order() if hasattr(root, "lrce_param_order") else None
     flat = FlatParams(root, device, order)
+    f16 = [p for m in root.modules() if hasattr(m, "lrce_f16_params") for p in m.lrce_f16_params()]
+    if f16:
+        flat.enable_f16(f16)
     _set_flat(root, flat)
     object.__setattr__(root, "_lrce_root", True)
     return flat
