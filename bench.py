@@ -4,10 +4,13 @@
 One step = the reference's train_ddp.py step (agent_oe.py:19-48) on a synthetic MSVD-QA batch:
 E2EOpenEnded forward (Video Swin-B 3D on 3 clips x 5 frames x 224^2 -> BERT-base on a 20-token
 question padded to 32 -> 3-step x 12-layer recurrent LRCE decoder -> 1000-way head), cross-entropy,
-backward, gradient all-reduce (N>1, RCCL buckets overlapped with backward), and the fused AdamW step
-with the L2 regulariser (reg 0.001) over all 312 M parameters.  Train mode: dropout 0.5 in the fusion
-model (train_ddp default drop-out-rate), BERT dropout 0.1, Swin DropPath 0.2.  Inputs resident in
-HBM before the timed region.  bf16 MFMA compute with f32 master weights / residual stream.
+backward, gradient all-reduce (N>1: bf16 RCCL buckets after the replayed backward), and the fused
+AdamW step with the L2 regulariser (reg 0.001) over all 312 M parameters, replayed from HIP graphs by
+the same TrainStepGraph the train_ddp.py agent uses.  Train mode: dropout 0.5 in the fusion model
+(train_ddp default drop-out-rate), BERT dropout 0.1, Swin DropPath 0.2.  Inputs resident in HBM
+before the timed region.  bf16 MFMA compute (fp16 for the BERT forward, like the reference's fp16
+autocast) with f32 master weights / residual stream.  The agent path itself (pinned host batches,
+process_data) is timed after the main measurement and reported as `agent_path`.
 
     python bench.py [--gpus N --steps K --warmup W]
 N>1: launched by torch.distributed.run (one process per GPU, RCCL); each rank runs bs=10 (weak
@@ -45,43 +48,52 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch-size", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-baseline-batch", type=int, default=6)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may run on")
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph",
-                    help="graph: the step replayed from a HIP graph (N>1: graph(fwd+bwd) -> RCCL bucket "
-                         "all-reduce -> graph(optimizer)); eager: launched from Python, all-reduce overlapped "
-                         "with backward")
+                    help="graph: the step replayed from HIP graphs (lrce/graph.TrainStepGraph, the agent's "
+                         "step; N>1: graph(fwd+bwd, bf16 bucket casts) -> RCCL bucket all-reduce -> "
+                         "graph(optimizer)); eager: launched from Python, all-reduce overlapped with backward")
+    ap.add_argument("--grad-reduce-dtype", choices=["bf16", "f32"], default="bf16")
+    ap.add_argument("--agent-steps", type=int, default=6, help="steps of the train_ddp agent path (0: skip)")
     ap.add_argument("--roofline-steps", type=int, default=2)
     return ap.parse_args()
 
 
-def build(batch, device, seed=0):
+def synthetic_batch(batch, seed):
+    """msvd-qa-oe item contract: clips U[0,1) (16 frames -> 3 clips x 5), 20-token questions."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    clips = torch.rand(batch, 3, 5, 3, 224, 224, generator=g)
+    ids = torch.zeros(batch, 32, dtype=torch.int64)
+    ids[:, 0], ids[:, 19] = 101, 102
+    ids[:, 1:19] = torch.randint(1000, 30522, (batch, 18), generator=g)
+    mask = (ids != 0).long()
+    types = torch.zeros_like(ids)
+    labels = torch.randint(0, 1000, (batch,), generator=g)
+    return clips, ids, mask, types, labels
+
+
+def build(batch, device, grad_dtype, seed=0):
     from lrce.models.e2e import E2EOpenEnded
     from lrce.optim import FusedAdamW
     from lrce.runtime import prepare
     torch.manual_seed(seed)
     # msvd-qa-oe config (configs/msvd-qa-oe.json): feature 768, 1000 answers, text_seq_len 32,
-    # video_feature_dim 1024; train_ddp defaults: drop-out-rate 0.5, temporal-scale [3]
-    model = E2EOpenEnded(768, 1000, 0.5, (7, 7), 1024, 5, [3], 32).to(device).train()
+    # video_feature_dim 1024; train_ddp defaults: drop-out-rate 0.5, temporal-scale [3].  Random init
+    # (no checkpoints offline): swin_ckpt / bert_dir None.
+    model = E2EOpenEnded(768, 1000, 0.5, (7, 7), 1024, 5, [3], 32, swin_ckpt=None, bert_dir=None).to(device).train()
     prepare(model)
     reducer = None
     if dist.is_initialized() and dist.get_world_size() > 1:
         from lrce.distributed import attach
-        reducer = attach(model, bucket_mb=64)
+        reducer = attach(model, bucket_mb=64, grad_dtype=grad_dtype)
     lr = 5e-6  # args.py default --lr, expanded to 3 groups (args.py:110-111)
     opt = FusedAdamW(model, [{"params": model.fusion_model.parameters(), "lr": lr},
                              {"params": model.text_extractor.parameters(), "lr": lr},
                              {"params": model.video_extractor.parameters(), "lr": lr}],
                      lr=lr, betas=(0.9, 0.999), reg_strength=0.001)
-    g = torch.Generator(device="cpu").manual_seed(1000 + (dist.get_rank() if dist.is_initialized() else 0))
-    clips = torch.rand(batch, 3, 5, 3, 224, 224, generator=g).to(device)   # 16-frame clip -> 3 x 5 frames
-    ids = torch.zeros(batch, 32, dtype=torch.int64)
-    ids[:, 0], ids[:, 19] = 101, 102
-    ids[:, 1:19] = torch.randint(1000, 30522, (batch, 18), generator=g)     # 20-token question
-    mask = (ids != 0).long()
-    types = torch.zeros_like(ids)
-    labels = torch.randint(0, 1000, (batch,), generator=g)
-    return model, opt, reducer, (clips, ids.to(device), mask.to(device), types.to(device), labels.to(device))
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    batch_dev = tuple(t.to(device) for t in synthetic_batch(batch, 1000 + rank))
+    return model, opt, reducer, batch_dev
 
 
 def train_step(model, opt, reducer, batch):
@@ -96,66 +108,104 @@ def train_step(model, opt, reducer, batch):
 
 
 def make_step(model, opt, reducer, batch, mode, world):
-    from lrce.graph import CapturedStep
+    from lrce.graph import TrainStepGraph
     if mode == "eager":
         return lambda: train_step(model, opt, reducer, batch)
-    if reducer is None:
-        def whole():
-            opt.zero_grad()
-            clips, ids, mask, types, labels = batch
-            loss = F.cross_entropy(model(clips, ids, mask, types), labels, ignore_index=-100)
-            loss.backward()
-            opt.step()
-            return loss
-        return CapturedStep(whole).replay
-    flat = reducer.flat
-    flat.reducer = None
 
-    def fwd_bwd():
+    def body(clips, ids, mask, types, labels):
         opt.zero_grad()
-        clips, ids, mask, types, labels = batch
         loss = F.cross_entropy(model(clips, ids, mask, types), labels, ignore_index=-100)
         loss.backward()
-        return loss
-    g1 = CapturedStep(fwd_bwd)
-    g2 = CapturedStep(lambda: opt.step(grad_scale=1.0 / world) or opt.step_t, warmup=1)
-
-    def step():
-        loss = g1.replay()
-        reducer.reduce_all()
-        g2.replay()
-        return loss
-    return step
+        return loss.detach()
+    step = TrainStepGraph(body, opt, reducer, world)
+    return lambda: step(*batch)
 
 
-def cpu_baseline(batch, threads):
+def agent_path(args, device, world, rank):
+    """The train_ddp.py path itself (lrce/cli.py -> AgentOE.process_data): pinned host batches from
+    an in-memory loader, H2D copies overlapped with the previous step, the agent's graph-replayed step,
+    device-side metrics.  Returns (QA-samples/s over all ranks, ms per step)."""
+    import argparse as _ap
+    from lrce.agent import AgentOE
+    from lrce.models.e2e import E2EOpenEnded
+    torch.manual_seed(1)
+    model = E2EOpenEnded(768, 1000, 0.5, (7, 7), 1024, 5, [3], 32, swin_ckpt=None, bert_dir=None)
+    a = _ap.Namespace(lr=[5e-6] * 3, reg_strength=0.001, lr_decay_factor=0.5, patience=0.5, min_lr=1e-8,
+                      use_cosine_scheduler=False, dataset="msvd-qa-oe", log_dir="/tmp", epoch=1, ckpt_interval=1,
+                      debug_mode=True, grad_reduce_dtype=args.grad_reduce_dtype, log_interval=50)
+    agent = AgentOE(model, device.index, a, log_enabled=False, rank=rank)
+    batches = [tuple(t.pin_memory() for t in synthetic_batch(args.batch_size, 2000 + 17 * rank + i)) for i in range(4)]
+    warm = 2                      # eager step + capture
+    loader = [batches[i % len(batches)] for i in range(warm + args.agent_steps)]
+    gen = agent.process_data(loader, True, 0)
+    for _ in range(warm):
+        next(gen)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.agent_steps):
+        next(gen)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    for _ in gen:   # the pass's end-of-epoch reduce (outside the timed region)
+        pass
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    del agent, model
+    torch.cuda.empty_cache()
+    return world * args.batch_size * args.agent_steps / dt, 1000.0 * dt / args.agent_steps
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(threads, batch=10):
     """CPU leg: the oracle (oracle/lrce_oracle.py, the fp32 PyTorch restatement of the reference
-    pinned by tests/golden) running the same training step — forward, CE + L2 loss, backward,
-    AdamW — on a bounded sample (`batch` QA-samples, no dropout).  Checker/baseline only."""
+    pinned by tests/golden) on the host cores, same workload shape: a cold training step at batch 2
+    (thread pool / allocator warm-up, not reported), then ONE warm training step at the config's batch
+    (forward, CE + L2 loss, backward, AdamW; no dropout) and one eval forward at that batch.
+    Checker/baseline only: nothing here runs on the product path."""
     from oracle import lrce_oracle as O
     from lrce.models.e2e import E2EOpenEnded
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    tmpl = E2EOpenEnded(768, 1000, 0.5, (7, 7), 1024, 5, [3], 32)
+    tmpl = E2EOpenEnded(768, 1000, 0.5, (7, 7), 1024, 5, [3], 32, swin_ckpt=None, bert_dir=None)
     sd = {k: (v.detach().clone().requires_grad_(True) if v.is_floating_point() else v)
           for k, v in tmpl.state_dict().items()}
     del tmpl
     params = [v for v in sd.values() if v.requires_grad]
-    g = torch.Generator().manual_seed(7)
-    clips = torch.rand(batch, 3, 5, 3, 224, 224, generator=g)
-    ids = torch.zeros(batch, 32, dtype=torch.int64)
-    ids[:, 0], ids[:, 19] = 101, 102
-    ids[:, 1:19] = torch.randint(1000, 30522, (batch, 18), generator=g)
-    mask, types = (ids != 0).long(), torch.zeros_like(ids)
-    labels = torch.randint(0, 1000, (batch,), generator=g)
     opt = torch.optim.AdamW(params, lr=5e-6, weight_decay=0.01)
-    t0 = time.perf_counter()
-    out = O.e2e_forward(sd, clips, ids, mask, types, "oe")
-    loss = F.cross_entropy(out, labels) + 0.001 * O.l2_reg(params)
-    loss.backward()
-    opt.step()
-    dt = time.perf_counter() - t0
-    return batch / dt, dt
+
+    def train(b, seed):
+        clips, ids, mask, types, labels = synthetic_batch(b, seed)
+        t0 = time.perf_counter()
+        out = O.e2e_forward(sd, clips, ids, mask, types, "oe")
+        loss = F.cross_entropy(out, labels) + 0.001 * O.l2_reg(params)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return time.perf_counter() - t0
+    train(2, 7)
+    dt_train = train(batch, 8)
+    clips, ids, mask, types, _ = synthetic_batch(batch, 9)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        O.e2e_forward(sd, clips, ids, mask, types, "oe")
+        dt_eval = time.perf_counter() - t0
+    return batch / dt_train, dt_train, batch / dt_eval, dt_eval
 
 
 def main():
@@ -170,16 +220,10 @@ def main():
     from lrce import kernels as K
     from lrce import _native
     _native.lib()
+    gdt = torch.bfloat16 if args.grad_reduce_dtype == "bf16" else torch.float32
     log(f"rank {rank}/{world}: building model (bs={args.batch_size})")
-    model, opt, reducer, batch = build(args.batch_size, device)
-    try:
-        step = make_step(model, opt, reducer, batch, args.mode, world)
-    except Exception as e:  # capture failure must not hide the measurement: fall back loudly
-        log(f"graph capture failed ({e!r}); timing eager steps")
-        args.mode = "eager"
-        if reducer is not None:
-            reducer.flat.reducer = reducer
-        step = make_step(model, opt, reducer, batch, "eager", world)
+    model, opt, reducer, batch = build(args.batch_size, device, gdt)
+    step = make_step(model, opt, reducer, batch, args.mode, world)
     for i in range(args.warmup):
         step()
         torch.cuda.synchronize()
@@ -206,32 +250,54 @@ def main():
     # per-kernel roofline: HIP events around every launch of the timed kernels, on their launch
     # stream, over eager steps of the same workload (a graph replay hides individual launches)
     timer = K.KernelTimer("wattn_fwd", "wattn_bwd", "gemm", "gemm_f32")
-    if reducer is not None:
-        reducer.flat.reducer = reducer
     with timer:
         for i in range(args.roofline_steps):
             train_step(model, opt, reducer, batch)
     torch.cuda.synchronize()
+    roof = _roofline(timer)
+    del step, model, opt, reducer, batch
+    torch.cuda.empty_cache()
+    agent = None
+    if args.agent_steps > 0:
+        try:
+            v, m = agent_path(args, device, world, rank)
+            agent = {"value": round(v, 3), "ms_per_step": round(m, 3), "steps": args.agent_steps,
+                     "vs_graph_bench": round(v / value, 4),
+                     "path": "train_ddp.py agent: AgentOE.process_data over pinned host batches (H2D overlapped), "
+                             "TrainStepGraph replay, device-side metrics"}
+        except Exception as e:  # the agent leg must not hide the measurement
+            agent = {"value": None, "error": repr(e)[:300]}
+        log(f"agent path: {agent}")
 
     out = {"metric": METRIC,
            "value": round(value, 3), "unit": "QA-samples/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights, U[0,1) clips, 20-token questions)",
+           "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic (random-init weights, U[0,1) clips, 20-token questions)",
            "config": {"workload": "msvd-qa-oe train_ddp step: Swin-B 3D + BERT-base + LRCE-12 decoder, temporal-scale 3",
                       "global_batch": samples // args.steps, "per_gpu_batch": args.batch_size, "frames": 16,
                       "resolution": 224, "question_tokens": 20, "text_seq_len": 32,
-                      "parallelism": f"dp{world}", "launch": args.mode},
+                      "parallelism": f"dp{world}", "launch": args.mode,
+                      "grad_reduce": args.grad_reduce_dtype if world > 1 else None,
+                      "precision": "bf16 MFMA (Swin, decoder memory, backward), fp16 MFMA BERT forward, "
+                                   "exact-f32 decoder query side, f32 masters"},
            "loss": round(loss_v, 4),
            "model_tflops": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0, 2),
            "model_mfu": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0 / (MFMA_BF16_PEAK_TFLOPS * world), 4)}
-    out["roofline"] = _roofline(timer)
+    out["roofline"] = roof
+    if agent is not None:
+        out["agent_path"] = agent
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("cpu baseline (oracle, fp32) ...")
+        threads = args.cpu_threads or len(os.sched_getaffinity(0))
+        log(f"cpu baseline (oracle, fp32, {threads} threads) ...")
         try:
-            v, dt = cpu_baseline(args.cpu_baseline_batch, args.cpu_threads)
-            out["cpu_baseline"] = {"value": round(v, 4), "unit": "QA-samples/s", "cores": args.cpu_threads, "kind": "port",
-                                   "sample": f"1 full training step (fwd+bwd+AdamW, fp32) of the CPU oracle at batch "
-                                             f"{args.cpu_baseline_batch}, {dt:.1f} s"}
+            v, dt, ve, dte = cpu_baseline(threads, args.batch_size)
+            out["cpu_baseline"] = {"value": round(v, 4), "unit": "QA-samples/s", "cores": threads, "kind": "port",
+                                   "cpu": _cpu_model(),
+                                   "sample": f"one warm training step (fwd+bwd+AdamW, fp32) of the CPU oracle at batch "
+                                             f"{args.batch_size}: {dt:.1f} s (after a cold batch-2 step)",
+                                   "eval_forward": {"value": round(ve, 4), "unit": "QA-samples/s",
+                                                    "sample": f"one eval forward at batch {args.batch_size}: {dte:.1f} s"}}
         except Exception as e:  # the baseline must not hide the GPU number
             out["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
     if rank == 0:

@@ -269,16 +269,23 @@ int lrce_set_rng_offset(const uint64_t* offset);
  * (decoupled weight decay, bias corrections bc1 = 1-beta1^t, bc2 = 1-beta2^t) on the gradient
  * grad_scale * g + reg * p / ||p|| (the L2-regulariser term), tensor_lr[t] per tensor; also writes
  * the bf16 shadow copy of p (p_bf16, optional) used by the next forward. */
-int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks, float* sumsq, int n_tensors, void* stream);
+int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks, float* sumsq, int n_tensors,
+                      const int32_t* tensor_chunk_off, float* chunk_sq, void* stream);
 int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
                     const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
                     float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
-                    float* sumsq_next, uint16_t* p_f16, int64_t f16_lo, int64_t f16_hi, void* stream);
+                    float* sumsq_next, uint16_t* p_f16, int64_t f16_lo, int64_t f16_hi, const uint16_t* g_bf16,
+                    const int32_t* tensor_chunk_off, float* chunk_sq, int n_tensors, void* stream);
 /* step: optional device step count t (bc1/bc2 then computed from it: graph-safe).  sumsq_next:
  * optional zeroed buffer that receives ||p_t||^2 of the UPDATED parameters, i.e. the next step's
  * sumsq without a separate norm pass over the 1.25 GB master copy.  p_f16 (optional): an IEEE fp16
  * shadow of elements [f16_lo, f16_hi) (multiples of 1024; element i at p_f16[i - f16_lo]) — the
- * BERT weights the fp16 forward reads — written in the same pass. */
+ * BERT weights the fp16 forward reads — written in the same pass.  g_bf16 (optional): read the
+ * gradient from this bf16 buffer (the all-reduced bf16 gradient buckets) instead of g (g may be NULL).
+ * tensor_chunk_off int32 [n_tensors+1] (first chunk of each tensor) + chunk_sq f32 [n_chunks] scratch
+ * (both or neither, here and in lrce_l2norm_multi): the per-tensor norms are summed per chunk with
+ * plain stores and then per tensor in a fixed order — bitwise reproducible, so data-parallel replicas
+ * (whose L2-term gradient reg * p / ||p|| depends on them) stay identical; without them, float atomics. */
 
 /* BERT embeddings before their LayerNorm (HF BertEmbeddings): out[r] = word[ids[r]] + pos[r % L] +
  * type[types[r]] (f32 tables, int64 ids), and the scatter-add backward into the three tables. */

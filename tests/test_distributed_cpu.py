@@ -64,7 +64,7 @@ def _worker(rank, world, port, mode, q):
             scale = red.reduce_all()
         out["scale"] = scale
         out["grad_sum"] = flat.grad.double().sum().item()
-        out["grad_head"] = flat.grad[:8].clone()
+        out["grad_head"] = flat.grad[:8].tolist()   # plain data: no shared-memory handle outlives the child
         out["param_view_is_flat"] = all(p.grad.data_ptr() == flat.g32(p).data_ptr() for p in model.parameters())
         q.put((rank, out))
     finally:
@@ -92,9 +92,9 @@ def test_grad_reducer_sums_over_ranks_gloo(mode):
     assert r0["n_buckets"] >= 2                       # bucketing actually splits the flat buffer
     assert r0["scale"] == pytest.approx(0.5) and r1["scale"] == pytest.approx(0.5)
     # all-reduce (sum) of (r+1)*base over 2 ranks = 3*base on both ranks; the optimizer applies 1/world
-    assert torch.equal(r0["grad_head"], r1["grad_head"])
+    assert r0["grad_head"] == r1["grad_head"]
     base_head = torch.arange(8, dtype=torch.float32) % 97
-    assert torch.equal(r0["grad_head"], 3 * base_head)
+    assert r0["grad_head"] == (3 * base_head).tolist()
     assert r0["grad_sum"] == pytest.approx(r1["grad_sum"])
     assert r0["param_view_is_flat"] and r1["param_view_is_flat"]
     if mode == "notify":

@@ -1,0 +1,189 @@
+"""Data parallelism on the real model (reference: DDP in agent_base.py:75-76 / train_ddp.py:10-13;
+SURVEY §4 test plan): two processes on the leased GPU, a gloo process group over device tensors
+(RCCL needs one device per rank), the native E2E model, GradReducer driven by the native backward's
+notify() calls.  Checks, dropout / DropPath off (eval-mode numerics, gradients still computed):
+  * parameter broadcast: ranks start from different seeds and end up with rank 0's weights (their
+    forward outputs on the same input agree bit for bit), shadows refreshed;
+  * averaged gradients of 2 ranks x bs == one process's gradients on the 2*bs batch, with f32
+    buckets (tight) and bf16 buckets (bf16 tolerance);
+  * the agent's HIP-graph training step (TrainStepGraph: graph(fwd+bwd with bucket casts) ->
+    bucket all-reduces -> graph(optimizer)) keeps the ranks' weights identical and moves them like a
+    single-process step on the 2*bs batch.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+from conftest import PKG, REPO, gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
+
+KEYS = ("video_extractor.swin.patch_embed.proj.weight", "video_extractor.swin.layers.2.blocks.5.attn.qkv.weight",
+        "video_extractor.swin.layers.1.blocks.1.attn.relative_position_bias_table",
+        "text_extractor.bert.encoder.layer.3.attention.self.query.weight",
+        "fusion_model.fusion_transformer.transformer.layers.7.linear1.weight", "fusion_model.final_fc.bias")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _batch(n, seed=3):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    from oracle import weights as W
+    clips = W.synthetic_clips(n, 1, seed=seed)
+    ids, mask, types = W.synthetic_question(n, 32, seed=seed)
+    labels = torch.arange(n) * 7 % 50
+    return clips, ids, mask, types, labels
+
+
+def _model(seed):
+    from lrce.models.e2e import E2EOpenEnded
+    torch.manual_seed(seed)
+    return E2EOpenEnded(768, 50, 0.0, (7, 7), 1024, 5, [1], 32, swin_ckpt=None, bert_dir=None).cuda().eval()
+
+
+def _grads(model, names):
+    g = dict(model.named_parameters())
+    return {k: g[k].grad.detach().float().cpu().clone() for k in names}
+
+
+def _worker(rank, world, port, mode, q):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    try:
+        from lrce.agent.agent_base import DataParallel
+        gdt = torch.bfloat16 if mode in ("bf16", "graph") else torch.float32
+        model = _model(seed=100 + rank)                 # different init per rank: the broadcast must fix it
+        dp = DataParallel(model, bucket_mb=32, grad_dtype=gdt)
+        flat = dp.reducer.flat
+        n = 2 * world
+        clips, ids, mask, types, labels = _batch(n)
+        half = slice(rank * 2, rank * 2 + 2)
+        probe = [t[:1].cuda() for t in (clips, ids, mask, types)]
+        with torch.no_grad():
+            out["probe"] = dp(*probe).float().cpu()
+        sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        if mode in ("f32", "bf16"):
+            flat.grad.zero_()
+            y = dp(clips[half].cuda(), ids[half].cuda(), mask[half].cuda(), types[half].cuda())
+            F.cross_entropy(y.float(), labels[half].cuda()).backward()
+            scale = dp.finish_gradients()
+            red = dp.reducer.reduced_grad().float() * scale            # the averaged gradient
+            gview = {k: flat._slice(red, p).cpu().clone() for k, p in model.named_parameters() if k in KEYS}
+            out["dp"] = gview
+            if rank == 0:                                              # one process, full 2*bs batch
+                flat.reducer = None
+                flat.grad.zero_()
+                y = model(clips.cuda(), ids.cuda(), mask.cuda(), types.cuda())
+                F.cross_entropy(y.float(), labels.cuda()).backward()
+                out["ref"] = _grads(model, KEYS)
+        else:   # graph-mode training steps through the agent's TrainStepGraph
+            from lrce.graph import TrainStepGraph
+            from lrce.optim import FusedAdamW
+            opt = FusedAdamW(model, [model.parameters()], lr=1e-4, reg_strength=0.001)
+
+            def body(c, i, m, t, g):
+                opt.zero_grad()
+                y = model(c, i, m, t)
+                loss = F.cross_entropy(y.float(), g)
+                loss.backward()
+                return loss.detach()
+            step = TrainStepGraph(body, opt, dp.reducer, world)
+            batch = (clips[half], ids[half], mask[half], types[half], labels[half])
+            for _ in range(3):
+                step(*batch)
+            torch.cuda.synchronize()
+            named = dict(model.named_parameters())
+            out["after"] = {k: named[k].detach().cpu().clone() for k in KEYS}
+            out["before"] = {k: sd0[k].cpu() for k in KEYS}
+            if rank == 0:   # single-process reference: same init, full batch, eager steps
+                dist.barrier()
+                flat.reducer = None
+                flat.grad_reducer = None
+                model.load_state_dict(sd0)
+                opt2 = FusedAdamW(model, [model.parameters()], lr=1e-4, reg_strength=0.001)
+                for _ in range(3):
+                    opt2.zero_grad()
+                    y = model(clips.cuda(), ids.cuda(), mask.cuda(), types.cuda())
+                    F.cross_entropy(y.float(), labels.cuda()).backward()
+                    opt2.step()
+                torch.cuda.synchronize()
+                out["ref_after"] = {k: named[k].detach().cpu().clone() for k in KEYS}
+            else:
+                dist.barrier()
+        q.put((rank, _plain(out)))
+    except Exception as e:   # report, do not hang the peer
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()[-3000:]}))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _plain(x):
+    """Tensors -> numpy (pickled by value: no shared-memory handle may outlive the child)."""
+    if isinstance(x, dict):
+        return {k: _plain(v) for k, v in x.items()}
+    return x.detach().cpu().numpy() if torch.is_tensor(x) else x
+
+
+def _run(mode, world=2):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert "error" not in res[r], res[r]["error"]
+
+    def back(x):
+        return {k: back(v) for k, v in x.items()} if isinstance(x, dict) else torch.from_numpy(x)
+    return {r: back({k: v for k, v in res[r].items()}) for r in res}
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-20))
+
+
+@pytest.mark.parametrize("mode,tol", [("f32", 2e-3), ("bf16", 2e-2)])
+def test_dp_gradients_equal_full_batch(mode, tol):
+    res = _run(mode)
+    assert torch.equal(res[0]["probe"], res[1]["probe"])        # broadcast: identical replicas
+    for k in KEYS:
+        assert torch.equal(res[0]["dp"][k], res[1]["dp"][k]), k   # every rank holds the same average
+        assert _rel(res[0]["dp"][k], res[0]["ref"][k]) < tol, (k, _rel(res[0]["dp"][k], res[0]["ref"][k]))
+
+
+def test_dp_graph_training_steps_match_single_process():
+    res = _run("graph")
+    for k in KEYS:
+        a0, a1 = res[0]["after"][k], res[1]["after"][k]
+        assert torch.equal(a0, a1), k                            # replicas stay identical
+        upd = a0 - res[0]["before"][k]
+        ref = res[0]["ref_after"][k] - res[0]["before"][k]
+        assert upd.abs().max() > 0, k
+        # AdamW's first steps are ~lr * sign(g): compare the updates in aggregate
+        assert float((upd - ref).abs().mean() / ref.abs().mean()) < 0.1, k

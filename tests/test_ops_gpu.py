@@ -156,6 +156,30 @@ def test_gemm_f32_outer_accumulate(M, N, R):
     assert rel(dw, ref.float()) < 1e-5
 
 
+def test_gemm_f32_splitk_repeatable():
+    """The exact-f32 skinny path splits K >= 2048 over workgroups whose partials are handed to the
+    last arriver through sc1 stores / loads (gemm_f32.hip).  Re-run it 200 times with a big GEMM on
+    another stream (uneven load: arrival order varies) and check every output word each time."""
+    k = K()
+    M, N, Kd = 10, 768, 3072
+    A = torch.randn(M, Kd, device=dev)
+    W = torch.randn(N, Kd, device=dev) / math.sqrt(Kd)
+    bias = torch.randn(N, device=dev)
+    ref = k.linear(A, W, bias, out_f32=True).clone()
+    assert rel(ref, (A.double() @ W.double().t() + bias.double()).float()) < 1e-5
+    noise = torch.cuda.Stream()
+    big = torch.randn(4096, 4096, device=dev)
+    bad = 0
+    for i in range(200):
+        if i % 20 == 0:
+            with torch.cuda.stream(noise):
+                big = (big @ big).mul_(1e-4)
+        y = k.linear(A, W, bias, out_f32=True)
+        bad += int(not torch.equal(y, ref))
+    torch.cuda.synchronize()
+    assert bad == 0
+
+
 @pytest.mark.parametrize("M", [1, 10, 50])
 def test_gemm_f32_skinny_epilogues(M):
     """Decoder query-side linears: GELU + bf16 pre-activation, residual, dGELU on the skinny path."""

@@ -283,8 +283,15 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p, float*
     float x = 0.f;
 #pragma unroll
     for (int w = 0; w < SK_WAVES; ++w) x += red[w][t][ml][nl];
-    // agent-scope relaxed stores go to the device coherence point (not this XCD's L2), so no L2
-    // writeback fence (buffer_wbl2) is needed; the vmcnt wait below orders them before the counter
+    // Hand-off protocol (MI355X_MICROARCH.md "Valid forms", first row of the sc1 hand-off table, in
+    // place of a release/acquire pair): every partial is an agent-scope relaxed store (global_store
+    // ... sc1, write-through past this XCD's L2), every storing wave drains it with s_waitcnt
+    // vmcnt(0), a workgroup barrier follows, then ONE lane's agent-scope atomic add signals; the
+    // block whose add returns KS-1 reduces, reading EVERY partial with agent-scope relaxed loads
+    // (global_load ... sc1, L2 bypass) after the barrier that publishes last_flag.  All four
+    // conditions of that row hold, so no buffer_wbl2 / buffer_inv (~1.7 us each per launch on these
+    // latency-bound decoder linears) is needed.  tests/test_ops_gpu.py
+    // test_gemm_f32_splitk_repeatable re-runs the split launches and checks every output word.
     __hip_atomic_store(mine + t * 256 + ml * 16 + nl, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

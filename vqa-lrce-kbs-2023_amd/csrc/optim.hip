@@ -10,8 +10,12 @@
 
 namespace {
 
+// Per-tensor squared norms are reduced DETERMINISTICALLY: each 1024-element chunk's sum is stored
+// (plain store, chunk_sq[c]), then segsum_kernel adds the chunks of every tensor in a fixed order.
+// (Float atomics would make ||p|| — and through the L2 term reg * p / ||p|| every update — differ in
+// the last bits from run to run and from rank to rank: data-parallel replicas would drift apart.)
 __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ p, const int* __restrict__ chunk_tensor, int n_chunks,
-                                                    float* __restrict__ sumsq) {
+                                                    float* __restrict__ sumsq, float* __restrict__ chunk_sq) {
   const int c = blockIdx.x;
   if (c >= n_chunks) return;
   const float4 v = reinterpret_cast<const float4*>(p + (long long)c * 1024)[threadIdx.x];
@@ -20,7 +24,30 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ p,
   __shared__ float red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(sumsq + chunk_tensor[c], red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) {
+    const float t = (red[0] + red[1]) + (red[2] + red[3]);
+    if (chunk_sq) chunk_sq[c] = t;
+    else atomicAdd(sumsq + chunk_tensor[c], t);
+  }
+}
+
+// out[t] = sum of chunk_sq over tensor t's chunks [off[t], off[t+1]), fixed order (one block per tensor)
+__global__ void __launch_bounds__(256) segsum_kernel(const float* __restrict__ chunk_sq, const int* __restrict__ off,
+                                                     int n_tensors, float* __restrict__ out) {
+  const int t = blockIdx.x;
+  if (t >= n_tensors) return;
+  const int c0 = off[t], c1 = off[t + 1];
+  float s = 0.f;
+  for (int c = c0 + (int)threadIdx.x; c < c1; c += 256) s += chunk_sq[c];
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+#pragma unroll
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[t] = red[0];
 }
 
 // CH consecutive 1024-element chunks per workgroup (4 parameters per thread per chunk): the
@@ -36,7 +63,8 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
                                                     bf16* __restrict__ pb, int n_chunks, float b1, float b2, float eps, float wd,
                                                     float gscale, float reg, float bc1, float bc2, const float* __restrict__ step_dev,
                                                     float* __restrict__ sumsq_next, bf16* __restrict__ ph, long long h_lo,
-                                                    long long h_hi) {
+                                                    long long h_hi, const bf16* __restrict__ g16,
+                                                    float* __restrict__ chunk_sq) {
   const int c0 = blockIdx.x * ADAMW_CH;
   if (step_dev) {
     const float t = *step_dev;
@@ -56,11 +84,19 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
     if (threadIdx.x == 0) atomicAdd(sumsq_next + t_run, red[0] + red[1] + red[2] + red[3]);
     q = 0.f;
   };
+  auto chunk_flush = [&](int c) {   // deterministic form: this chunk's sum -> chunk_sq[c]
+    float w = wave_sum(q);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) chunk_sq[c] = (red[0] + red[1]) + (red[2] + red[3]);
+    q = 0.f;
+  };
   for (int k = 0; k < ADAMW_CH; ++k) {
     const int c = c0 + k;
     if (c >= n_chunks) break;
     const int t = chunk_tensor[c];
-    if (t != t_run) {
+    if (t != t_run && !chunk_sq) {
       flush();
       t_run = t;
     }
@@ -70,7 +106,13 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
     const float step = lr / bc1, decay = 1.0f - lr * wd;
     const long long i = (long long)c * 1024 + threadIdx.x * 4;
     float4 pp = *reinterpret_cast<float4*>(p + i);
-    const float4 gg = *reinterpret_cast<const float4*>(g + i);
+    float4 gg;
+    if (g16) {   // bf16 gradient (the all-reduced bf16 buckets of lrce/distributed.py)
+      const bf16x4 t = *reinterpret_cast<const bf16x4*>(g16 + i);
+      gg = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
+    } else {
+      gg = *reinterpret_cast<const float4*>(g + i);
+    }
     float4 mm = *reinterpret_cast<float4*>(m + i);
     float4 vv = *reinterpret_cast<float4*>(v + i);
     float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
@@ -94,32 +136,41 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
       *reinterpret_cast<bf16x4*>(ph + (i - h_lo)) = oh;
     }
     q += pp.x * pp.x + pp.y * pp.y + pp.z * pp.z + pp.w * pp.w;
+    if (chunk_sq) chunk_flush(c);
   }
-  flush();
+  if (!chunk_sq) flush();
 }
 
 }  // namespace
 
 extern "C" int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks, float* sumsq, int n_tensors,
-                                 void* stream) {
+                                 const int32_t* tensor_chunk_off, float* chunk_sq, void* stream) {
   if (!p || !chunk_tensor || !sumsq) return lrce_fail(LRCE_E_ARG, "l2norm_multi: null pointer");
+  if (!tensor_chunk_off != !chunk_sq) return lrce_fail(LRCE_E_ARG, "l2norm_multi: tensor_chunk_off and chunk_sq go together");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  (void)hipMemsetAsync(sumsq, 0, sizeof(float) * n_tensors, s);
-  if (n_chunks > 0) sumsq_kernel<<<n_chunks, 256, 0, s>>>(p, chunk_tensor, n_chunks, sumsq);
+  if (!chunk_sq) (void)hipMemsetAsync(sumsq, 0, sizeof(float) * n_tensors, s);
+  if (n_chunks > 0) sumsq_kernel<<<n_chunks, 256, 0, s>>>(p, chunk_tensor, n_chunks, sumsq, chunk_sq);
+  if (chunk_sq && n_tensors > 0) segsum_kernel<<<n_tensors, 256, 0, s>>>(chunk_sq, tensor_chunk_off, n_tensors, sumsq);
   return lrce_check_launch("l2norm_multi");
 }
 
 extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
                                const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
                                float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
-                               float* sumsq_next, uint16_t* p_f16, int64_t f16_lo, int64_t f16_hi, void* stream) {
-  if (!p || !g || !m || !v || !chunk_tensor || !tensor_lr) return lrce_fail(LRCE_E_ARG, "adamw_step: null pointer");
+                               float* sumsq_next, uint16_t* p_f16, int64_t f16_lo, int64_t f16_hi, const uint16_t* g_bf16,
+                               const int32_t* tensor_chunk_off, float* chunk_sq, int n_tensors, void* stream) {
+  if (!tensor_chunk_off != !chunk_sq) return lrce_fail(LRCE_E_ARG, "adamw_step: tensor_chunk_off and chunk_sq go together");
+  if (!p || (!g && !g_bf16) || !m || !v || !chunk_tensor || !tensor_lr) return lrce_fail(LRCE_E_ARG, "adamw_step: null pointer");
   if (p_f16 && (f16_lo % 1024 || f16_hi % 1024 || f16_lo < 0 || f16_hi < f16_lo))
     return lrce_fail(LRCE_E_ARG, "adamw_step: f16 shadow range [%lld, %lld) not chunk aligned", (long long)f16_lo, (long long)f16_hi);
   if (n_chunks > 0)
     adamw_kernel<<<(n_chunks + ADAMW_CH - 1) / ADAMW_CH, 256, 0, static_cast<hipStream_t>(stream)>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq,
                                                                          reinterpret_cast<bf16*>(p_bf16), n_chunks, beta1, beta2, eps,
                                                                          weight_decay, grad_scale, reg, bc1, bc2, step, sumsq_next,
-                                                                         reinterpret_cast<bf16*>(p_f16), f16_lo, f16_hi);
+                                                                         reinterpret_cast<bf16*>(p_f16), f16_lo, f16_hi,
+                                                                         reinterpret_cast<const bf16*>(g_bf16),
+                                                                         sumsq_next ? chunk_sq : nullptr);
+  if (sumsq_next && chunk_sq && n_tensors > 0)
+    segsum_kernel<<<n_tensors, 256, 0, static_cast<hipStream_t>(stream)>>>(chunk_sq, tensor_chunk_off, n_tensors, sumsq_next);
   return lrce_check_launch("adamw_step");
 }

@@ -15,8 +15,15 @@ What differs, MI355X-first:
 * precision: bf16 MFMA with f32 master weights instead of fp16 autocast + GradScaler (no loss scale is
   needed for bf16; `self.scaler` is kept as None);
 * data parallel: instead of torch DDP (agent_base.py:75-76), `DataParallel` below attaches the
-  bucketed RCCL gradient reducer of lrce/distributed.py (all-reduce overlapped with backward, 1/world
-  folded into the optimizer's gradient scale, one parameter broadcast at construction);
+  bucketed RCCL gradient reducer of lrce/distributed.py (bf16 buckets by default, eager: all-reduce
+  overlapped with backward; 1/world folded into the optimizer's gradient scale, one parameter
+  broadcast at construction);
+* launch: a training step is replayed from HIP graphs (lrce/graph.TrainStepGraph: the first batch of
+  a shape runs eagerly, the next one is captured) — the same step bench.py times; `args.eager = True`
+  (CLI --eager) keeps Python-launched steps;
+* no per-step host syncs: the batch loss / metric stay on the device; the per-step summaries are
+  read back every `log_interval` steps (same tags and step indices) and the epoch metric is reduced
+  to rank 0 once per pass instead of after every batch (same value: sum over ranks and batches);
 * summaries: tensorboard is not in this image; scalars go to `<log_dir>/scalars.jsonl` (same tags).
 """
 import json
@@ -29,6 +36,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..graph import TrainStepGraph
 from ..optim import FusedAdamW
 from ..runtime import ensure
 from .schedulers import CosineAnnealingWarmupRestarts, ReduceLROnPlateau
@@ -60,14 +68,14 @@ class DataParallel(nn.Module):
     """The agent's replacement for DistributedDataParallel: `.module` is the model; when a process
     group with more than one rank exists, gradients are averaged by the flat-buffer RCCL reducer."""
 
-    def __init__(self, module, bucket_mb=64):
+    def __init__(self, module, bucket_mb=64, grad_dtype=torch.bfloat16):
         super().__init__()
         self.module = module
         self.reducer = None
         ensure(module)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             from ..distributed import attach
-            self.reducer = attach(module, bucket_mb=bucket_mb)
+            self.reducer = attach(module, bucket_mb=bucket_mb, grad_dtype=grad_dtype)
 
     def forward(self, *args, **kwargs):
         return self.module(*args, **kwargs)
@@ -78,9 +86,17 @@ class DataParallel(nn.Module):
 
 
 class AgentBase:
-    def __init__(self, model, gpu_id, args, log_enabled=True, is_eval=False):
+    def __init__(self, model, gpu_id, args, log_enabled=True, is_eval=False, rank=None):
+        """gpu_id: this process's device (LOCAL_RANK); rank: its global rank (default: the process
+        group's rank, else gpu_id) — rank 0 logs and writes checkpoints."""
         self.args = args
         self.gpu_id = gpu_id
+        if rank is None:
+            rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else gpu_id
+        self.rank = rank if isinstance(rank, int) else 0
+        self.log_interval = int(getattr(args, "log_interval", 50))
+        self.use_graph = not getattr(args, "eager", False)
+        self._graph = None
         self.log_enabled = log_enabled
         self.is_eval = is_eval
         self.uid = int(time.time())
@@ -89,7 +105,8 @@ class AgentBase:
         self.scaler = None
 
         model = model.to(self.device)
-        self.model = DataParallel(model)
+        gdt = torch.float32 if getattr(args, "grad_reduce_dtype", "bf16") == "f32" else torch.bfloat16
+        self.model = DataParallel(model, grad_dtype=gdt)
         self.reg_strength = float(getattr(args, "reg_strength", 0.0))
         self.optim = None
         self.scheduler = None
@@ -109,9 +126,9 @@ class AgentBase:
                 self.scheduler = ReduceLROnPlateau(self.optim, mode="max", factor=args.lr_decay_factor,
                                                    patience=args.patience, min_lr=args.min_lr)
 
-        self.logger = get_logger(__name__, gpu_id)
+        self.logger = get_logger(__name__, self.rank)
         self.summary_writer = None
-        if log_enabled and gpu_id == 0:
+        if log_enabled and self.rank == 0:
             self.args.log_dir = os.path.join(args.log_dir, f"{self.uid}_{args.dataset}")
             self.summary_writer = ScalarLog(self.args.log_dir)
             self.args.ckpt_dir = os.path.join(self.args.log_dir, "weights")
@@ -135,8 +152,14 @@ class AgentBase:
         return self.loss_func(out, gt)
 
     def pack_step(self, loss_value, out, gt, task_terms):
+        """step()'s return value (agent_oe.py:44-48): (loss, correct, total)."""
+        num, den = self.metric_terms(out, gt, task_terms)
+        return loss_value, int(num.item()), den
+
+    def metric_terms(self, out, gt, task_terms):
+        """(numerator as a device scalar, denominator) of the epoch metric for one batch."""
         prediction = torch.argmax(out, dim=1)
-        return loss_value, torch.sum(prediction == gt).item(), prediction.shape[0]
+        return torch.sum(prediction == gt), prediction.shape[0]
 
     def unpack_step(self, result):
         return result
@@ -160,58 +183,103 @@ class AgentBase:
         with torch.no_grad():
             return sum(p.float().norm(2) for p in self.model.module.parameters() if p.requires_grad)
 
-    def step(self, video_clips, texts, texts_attention_mask, texts_type_ids, ground_truth, is_train):
-        """One batch (agent_oe.py:19-48 and its MC / count twins): forward on the native path, task
-        loss, the reported loss = task + reg * L2, and for training zero_grad -> backward ->
-        (all-reduce) -> fused AdamW.  Only the task loss is back-propagated: the optimizer kernel adds
-        the L2 term's gradient reg * p / ||p||."""
-        d = self.device
-        out = self.model(video_clips.to(d, non_blocking=True), texts.to(d, non_blocking=True),
-                         texts_attention_mask.to(d, non_blocking=True), texts_type_ids.to(d, non_blocking=True))
-        gt = ground_truth.to(d, non_blocking=True)
+    def _train_body(self, video_clips, texts, texts_attention_mask, texts_type_ids, gt):
+        """Forward, task loss, L2 value of the current weights, backward (no optimizer step): the
+        part of agent_oe.py:27-40 a HIP graph captures.  Returns device tensors."""
+        self.optim.zero_grad()
+        out = self.model(video_clips, texts, texts_attention_mask, texts_type_ids)
         terms = self.task_loss(out.float(), gt)
         task = terms.mean() if terms.dim() else terms
-        value = task.detach()
-        if self.reg_strength != 0.0:
-            value = value + self.reg_strength * self.calculate_l2_reg()
+        l2 = self.calculate_l2_reg() if self.reg_strength != 0.0 else None
+        task.backward()
+        return out.detach(), terms.detach(), task.detach(), l2
+
+    def _step_dev(self, video_clips, texts, texts_attention_mask, texts_type_ids, ground_truth, is_train):
+        """One batch on the device: (reported loss, logits, labels, per-sample loss terms), all device
+        tensors (no host sync).  Training: zero_grad -> forward -> backward -> (all-reduce) -> fused
+        AdamW, replayed from HIP graphs unless args.eager.  Only the task loss is back-propagated:
+        the optimizer kernel adds the L2 term's gradient reg * p / ||p||."""
+        d = self.device
         if is_train:
-            self.optim.zero_grad()
-            task.backward()
-            self.optim.step(grad_scale=self.model.finish_gradients())
-        return self.pack_step(value.item(), out.detach(), gt, terms.detach())
+            inputs = (video_clips, texts, texts_attention_mask, texts_type_ids, ground_truth)
+            if self.use_graph:
+                if self._graph is None:
+                    red = self.model.reducer
+                    self._graph = TrainStepGraph(self._train_body, self.optim, red, red.world if red else 1)
+                out, terms, task, l2 = self._graph(*inputs)
+                gt = self._graph.static[4]
+            else:
+                inputs = [t.to(d, non_blocking=True) for t in inputs]
+                out, terms, task, l2 = self._train_body(*inputs)
+                self.optim.step(grad_scale=self.model.finish_gradients())
+                gt = inputs[4]
+        else:
+            out = self.model(video_clips.to(d, non_blocking=True), texts.to(d, non_blocking=True),
+                             texts_attention_mask.to(d, non_blocking=True), texts_type_ids.to(d, non_blocking=True))
+            gt = ground_truth.to(d, non_blocking=True)
+            terms = self.task_loss(out.float(), gt)
+            task = terms.mean() if terms.dim() else terms
+            l2 = self.calculate_l2_reg() if self.reg_strength != 0.0 else None
+            out, terms = out.detach(), terms.detach()
+        value = task.detach() if l2 is None else task.detach() + self.reg_strength * l2
+        return value, out, gt, terms
+
+    def step(self, video_clips, texts, texts_attention_mask, texts_type_ids, ground_truth, is_train):
+        """agent_oe.py:19-48 (and its MC / count twins): one batch, host-side results."""
+        value, out, gt, terms = self._step_dev(video_clips, texts, texts_attention_mask, texts_type_ids, ground_truth,
+                                               is_train)
+        return self.pack_step(value.item(), out, gt, terms)
 
     # ------------------------------------------------------------------ loops (agent_base.py:110-171)
+    def _flush(self, pend):
+        """Write the buffered per-step summaries (one device->host read for all of them)."""
+        if not pend:
+            return
+        if self.summary_writer is not None:
+            vals = torch.stack([torch.stack([l.float(), n.float()]) for _, l, n, _, _ in pend]).tolist()
+            for (counter, _, _, den, lrs), (loss, num) in zip(pend, vals):
+                for k, lr in enumerate(lrs):
+                    self.write_summary(f"LR Scheduler/{k}", lr, counter)
+                self.write_summary("Training/Batch Loss", loss, counter)
+                self.write_summary(f"Training/Batch {self.METRIC}", num / den, counter)
+        pend.clear()
+
     def process_data(self, dl, is_train, epoch):
         """Generator over one pass of `dl`; in training yields each batch index (the evaluation hook
-        of do_training), then -1.  Rank 0 accumulates the metric over the pass; other ranks send
-        their current batch only (reduce to rank 0 after every batch, as the reference does)."""
+        of do_training), then -1.  Batch losses and metric terms accumulate on the device; the
+        metric is reduced to rank 0 once per pass (the reference reduces after every batch: same
+        sum), per-step summaries are flushed every log_interval steps."""
         phase = "Training" if is_train else "Validation"
         if is_train or not self.is_eval:
             self.logger.info(f"{phase} Phase")
         acc = torch.zeros(2, device=self.device)         # metric numerator, denominator
         losses = []
-        avg_loss = avg_metric = float("nan")
+        pend = []
         for i, batch in enumerate(dl):
             self.model.train(is_train)
             with torch.set_grad_enabled(is_train):
-                loss, num, den = self.unpack_step(self.step(*batch, is_train=is_train))
+                value, out, gt, terms = self._step_dev(*batch, is_train=is_train)
+            num, den = self.metric_terms(out, gt, terms)
+            num = num.detach().float().reshape(())
+            acc[0] += num
+            acc[1] += den
+            losses.append(value.detach().float().reshape(()).clone())
             if is_train:
                 self.counter += 1
                 if getattr(self.args, "use_cosine_scheduler", False):
                     self.scheduler.step(epoch + i / len(dl))
-                for k, g in enumerate(self.optim.param_groups):
-                    self.write_summary(f"LR Scheduler/{k}", g["lr"], self.counter)
-                self.write_summary("Training/Batch Loss", loss, self.counter)
-                self.write_summary(f"Training/Batch {self.METRIC}", num / den, self.counter)
+                pend.append((self.counter, losses[-1], num.clone(), den, [g["lr"] for g in self.optim.param_groups]))
+                if len(pend) >= self.log_interval:
+                    self._flush(pend)
                 yield i
-            if self.gpu_id != 0:
-                acc.zero_()
-            acc += torch.tensor([num, den], device=self.device, dtype=acc.dtype)
-            if dist.is_available() and dist.is_initialized():
-                dist.reduce(acc, dst=0)
-            losses.append(loss)
-            nonzero = [x for x in losses if x != 0]     # the reference averages the nonzero batch losses
-            avg_loss = sum(nonzero) / len(nonzero) if nonzero else 0.0
+        self._flush(pend)
+        if dist.is_available() and dist.is_initialized():
+            dist.reduce(acc, dst=0)
+        avg_loss = avg_metric = float("nan")
+        if losses:
+            lt = torch.stack(losses)
+            nz = lt != 0                                 # the reference averages the nonzero batch losses
+            avg_loss = float((lt * nz).sum() / nz.sum().clamp(min=1)) if bool(nz.any()) else 0.0
             avg_metric = (acc[0] / acc[1]).item()
         if is_train:
             self.write_summary("Training/Loss", avg_loss, epoch)
@@ -238,7 +306,7 @@ class AgentBase:
         self.logger.info(f"Training config saved to {path}")
 
     def save_checkpoint(self, epoch, name="", only_model=True):
-        if self.gpu_id != 0 or not hasattr(self.args, "ckpt_dir"):
+        if self.rank != 0 or not hasattr(self.args, "ckpt_dir"):
             return None   # (the reference raises AttributeError here when logging is disabled)
         ckpt = {"model_state_dict": self.model.module.state_dict()}
         if not only_model:

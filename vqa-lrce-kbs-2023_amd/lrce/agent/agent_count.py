@@ -10,9 +10,9 @@ class AgentCount(AgentBase):
     METRIC = "MSE"
     HIGHER_IS_BETTER = False
 
-    def __init__(self, model, gpu_id, args, log_enabled=True, is_eval=False):
-        super().__init__(model, gpu_id, args, log_enabled, is_eval)
-        self.logger = get_logger(__name__, gpu_id)
+    def __init__(self, model, gpu_id, args, log_enabled=True, is_eval=False, rank=None):
+        super().__init__(model, gpu_id, args, log_enabled, is_eval, rank)
+        self.logger = get_logger(__name__, self.rank)
         self.loss_func = nn.MSELoss(reduction="none")
 
     def task_loss(self, out, gt):
@@ -20,6 +20,9 @@ class AgentCount(AgentBase):
 
     def pack_step(self, loss_value, out, gt, task_terms):
         return loss_value, task_terms
+
+    def metric_terms(self, out, gt, task_terms):
+        return task_terms.sum(), task_terms.numel()
 
     def unpack_step(self, result):
         loss, sq_err = result

@@ -15,11 +15,11 @@ def hinge_loss(out, gt, margin):
 
 
 class AgentMC(AgentBase):
-    def __init__(self, model, gpu_id, args, log_enabled=True, is_eval=False):
-        super().__init__(model, gpu_id, args, log_enabled, is_eval)
+    def __init__(self, model, gpu_id, args, log_enabled=True, is_eval=False, rank=None):
+        super().__init__(model, gpu_id, args, log_enabled, is_eval, rank)
         if getattr(self.args, "use_hinge_loss", False):
             self.loss_func = self.hinge_loss
-        self.logger = get_logger(__name__, gpu_id)
+        self.logger = get_logger(__name__, self.rank)
 
     def hinge_loss(self, out, gt):
         return hinge_loss(out, gt, self.args.margin)

@@ -4,6 +4,6 @@ from .agent_base import AgentBase, get_logger
 
 
 class AgentOE(AgentBase):
-    def __init__(self, model, gpu_id, args, log_enabled=True, is_eval=False):
-        super().__init__(model, gpu_id, args, log_enabled, is_eval)
-        self.logger = get_logger(__name__, gpu_id)
+    def __init__(self, model, gpu_id, args, log_enabled=True, is_eval=False, rank=None):
+        super().__init__(model, gpu_id, args, log_enabled, is_eval, rank)
+        self.logger = get_logger(__name__, self.rank)

@@ -15,9 +15,11 @@ Additive flags (absent from the reference, no effect on its flags):
                        not needed.  Video decoding and tokenisation are out of scope for this build.
   --synthetic-val N    size of the synthetic validation / test split (default max(N // 4, batch)).
   --seed S             synthetic data seed.
-Launch: under torchrun (RANK / WORLD_SIZE / LOCAL_RANK in the environment) each process is one rank;
-otherwise one process per visible GPU is spawned, as the reference's mp.spawn does.  The process
-group is "nccl" (RCCL over xGMI) with MASTER_ADDR 127.0.0.1.
+  --allow-random-init  train although the Swin checkpoint / local BERT weights are missing (the
+                       reference asserts the checkpoint, e2e.py:11); implied by --synthetic.
+Launch: under torchrun (RANK / WORLD_SIZE / LOCAL_RANK in the environment) each process is one rank
+on device LOCAL_RANK; otherwise one process per visible GPU is spawned, as the reference's mp.spawn
+does.  The process group is "nccl" (RCCL over xGMI) with MASTER_ADDR 127.0.0.1.
 """
 import argparse
 import copy
@@ -41,6 +43,8 @@ def _additive(p):
     p.add_argument("--synthetic", type=int, default=0, help="use N synthetic items (no video decoding)")
     p.add_argument("--synthetic-val", type=int, default=0, help="synthetic validation/test items")
     p.add_argument("--seed", type=int, default=0, help="synthetic data seed")
+    p.add_argument("--allow-random-init", action="store_true",
+                   help="train from random backbones when the pretrained Swin / BERT weights are missing")
 
 
 def _merge_config(result):
@@ -167,27 +171,40 @@ def _loader(ds, a):
                                        pin_memory=True, sampler=DistributedSampler(ds))
 
 
+def local_rank(rank):
+    """Device index of this process: LOCAL_RANK under torchrun (multi-node safe), else the rank
+    (mp.spawn on one node, train_ddp.py:17-18)."""
+    return int(os.environ.get("LOCAL_RANK", rank))
+
+
 def _setup(rank, world):
-    """One node: the rank is also the device index (train_ddp.py:10-13, 17-18)."""
+    """Process group over RCCL; the global rank joins the group, the local rank picks the device
+    (train_ddp.py:10-13, 17-18)."""
     import torch
     import torch.distributed as dist
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "12355")
-    torch.cuda.set_device(rank)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    dev = local_rank(rank)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+    return dev
 
 
 def train_main(rank, world, a, val_split="test"):
     """train_ddp.py:16-131 (val_split 'test') / train.py (val_split 'val')."""
     import logging
     import torch.distributed as dist
-    _setup(rank, world)
+    dev = _setup(rank, world)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(message)s")
     model_factory, agent_factory = factories(a.task_type)
     train_ds, val_ds = datasets(a, ["train", val_split])
     model = model_factory(a.feature_dim, a.num_classes, a.drop_out_rate, a.video_feature_res, a.video_feature_dim,
                           a.frame_sample_size, a.temporal_scale, a.text_seq_len)
-    trainer = agent_factory(model, rank, a, not a.debug_mode and not a.sanity_check)
+    if not (model.pretrained_loaded or a.model_path or a.synthetic or a.allow_random_init):
+        raise SystemExit("pretrained Swin (./pretrained_models/swin_base_patch244_window877_kinetics600_22k.pth) "
+                         "and BERT (./pretrained_models/bert-base-uncased) weights are required for a real run "
+                         "(reference e2e.py:11); pass --allow-random-init to train from random backbones")
+    trainer = agent_factory(model, dev, a, not a.debug_mode and not a.sanity_check, rank=rank)
     if a.model_path:
         trainer.load_checkpoint(a.model_path)
     train_dl, val_dl = _loader(train_ds, a), _loader(val_ds, a)
@@ -203,14 +220,14 @@ def eval_main(rank, world, a):
     """eval.py:16-95."""
     import logging
     import torch.distributed as dist
-    _setup(rank, world)
+    dev = _setup(rank, world)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(message)s")
     model_factory, agent_factory = factories(a.task_type)
     (test_ds,) = datasets(a, ["test"])
     model = model_factory(feature_dim=a.feature_dim, num_classes=a.num_classes, video_feature_res=a.video_feature_res,
                           video_feature_dim=a.video_feature_dim, frame_sample_size=a.frame_sample_size,
                           temporal_scale=a.temporal_scale, text_seq_len=a.text_seq_len)
-    evaluator = agent_factory(model, rank, a, False, True)
+    evaluator = agent_factory(model, dev, a, False, True, rank=rank)
     evaluator.load_checkpoint(a.model_path)
     evaluator.do_evaluation(_loader(test_ds, a))
     dist.destroy_process_group()

@@ -12,6 +12,9 @@ reference (its output is never used by the loss), not computed.  No network fetc
 from a checkpoint or the caller.  The encoder's forward operands are fp16 (the reference runs
 BERT under fp16 autocast), its backward bf16.
 """
+import os
+import warnings
+
 import torch
 import torch.nn as nn
 
@@ -257,10 +260,60 @@ class BertModel(nn.Module):
         return x.view(B, L, HIDDEN)
 
 
+BERT_DIR = "./pretrained_models/bert-base-uncased"
+
+
+def load_bert_weights(bert, path):
+    """Load a local bert-base-uncased checkpoint into `bert` (BertModel): a directory holding
+    model.safetensors or pytorch_model.bin, or one of those files.  Tensors only (safetensors /
+    torch.load(weights_only=True)); HF key prefixes `bert.` and the pretraining heads (`cls.`) are
+    handled, TF-era `LayerNorm.gamma/beta` names mapped.  Every encoder / embedding key must be
+    present; the pooler may be absent (it is unused by the reference's loss)."""
+    if os.path.isdir(path):
+        for name in ("model.safetensors", "pytorch_model.bin"):
+            if os.path.exists(os.path.join(path, name)):
+                path = os.path.join(path, name)
+                break
+        else:
+            raise FileNotFoundError(f"no model.safetensors / pytorch_model.bin under {path}")
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        raw = load_file(path)
+    else:
+        raw = torch.load(path, map_location="cpu", weights_only=True)
+        raw = raw.get("state_dict", raw) if isinstance(raw, dict) else raw
+    sd = {}
+    for k, v in raw.items():
+        if k.startswith("cls.") or not torch.is_tensor(v):
+            continue
+        k = k[5:] if k.startswith("bert.") else k
+        k = k.replace("LayerNorm.gamma", "LayerNorm.weight").replace("LayerNorm.beta", "LayerNorm.bias")
+        sd[k] = v
+    own = bert.state_dict()
+    missing = [k for k in own if k not in sd and not k.startswith("pooler.")]
+    if missing:
+        raise KeyError(f"BERT checkpoint {path} lacks {len(missing)} keys, e.g. {missing[:3]}")
+    bert.load_state_dict({k: v for k, v in sd.items() if k in own or k.endswith("position_ids")}, strict=False)
+
+
 class TextExtractor(nn.Module):
-    def __init__(self, bert=None):
+    """text.py:5-17.  The reference fetches bert-base-uncased by name (text.py:9); this build never
+    touches the network: `bert_dir` (a local copy, see load_bert_weights) is loaded when present,
+    otherwise the encoder keeps its initialisation with a warning and `pretrained_loaded = False`
+    (the training CLI then refuses a non-synthetic run without --allow-random-init).  bert_dir=None:
+    random initialisation on purpose (tests, benchmarks)."""
+
+    def __init__(self, bert=None, bert_dir=None):
         super().__init__()
         self.bert = bert if bert is not None else BertModel()
+        self.pretrained_loaded = False
+        if bert is None and bert_dir:
+            if os.path.exists(bert_dir):
+                load_bert_weights(self.bert, bert_dir)
+                self.pretrained_loaded = True
+            else:
+                warnings.warn(f"BERT weights {bert_dir} not found: the text encoder keeps its random "
+                              "initialisation", stacklevel=2)
 
     def forward(self, input_ids, attention_mask, token_type_ids):
         return self.bert(input_ids, attention_mask, token_type_ids)

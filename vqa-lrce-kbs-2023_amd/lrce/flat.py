@@ -23,7 +23,8 @@ class FlatParams:
             ids = {id(p) for p in self.params}
             assert len(order) == len(self.params) and {id(p) for p in order} == ids, "order must permute parameters"
             self.params = list(order)
-        self.reducer = None
+        self.reducer = None          # notify target during a backward (lrce/distributed.py)
+        self.grad_reducer = None     # its GradReducer, whose reduced gradient the optimizer reads
         self.names = {id(p): n for n, p in module.named_parameters()}
         offs, o = [], 0
         for p in self.params:
@@ -46,7 +47,11 @@ class FlatParams:
             chunk_tensor[off // ALIGN: off // ALIGN + n] = i
         self.chunk_tensor = chunk_tensor.to(self.device)
         self.n_chunks = self.total // ALIGN
+        # first chunk of every tensor (+ end): the deterministic per-tensor norm sums (csrc/optim.hip)
+        off = torch.tensor([o // ALIGN for o in offs] + [self.n_chunks], dtype=torch.int32)
+        self.tensor_chunk_off = off.to(self.device)
         self._bf16_version = -1
+        self._epoch = 0            # bumped by writes the version counters cannot see (collectives)
         self.f16 = None            # optional IEEE fp16 shadow of [f16_lo, f16_hi) (enable_f16)
         self.f16_lo = self.f16_hi = 0
         self.attach_grads(zero=True)
@@ -108,7 +113,7 @@ class FlatParams:
         slices of f32 bump the first; in-place writes through a parameter (load_state_dict's copy_,
         `p.mul_()` under no_grad) bump only that parameter's counter, because `p.data = view` keeps
         the parameter's own counter — hence both."""
-        return self.f32._version, sum(p._version for p in self.params)
+        return self.f32._version, sum(p._version for p in self.params), self._epoch
 
     def refresh_bf16(self):
         """Re-cast the bf16 shadow if the masters changed (optimizer step, load_state_dict, ...)."""
@@ -118,6 +123,15 @@ class FlatParams:
             if self.f16 is not None:
                 K.cast_f16(self.f16_src(), self.f16)
             self._bf16_version = self._versions()
+
+    def masters_written(self):
+        """The f32 masters were overwritten behind torch's back (e.g. an in-place broadcast): refresh
+        the 16-bit shadows now and invalidate every cache keyed on master_version()."""
+        self._epoch += 1
+        K.cast_bf16(self.f32, self.bf16)
+        if self.f16 is not None:
+            K.cast_f16(self.f16_src(), self.f16)
+        self._bf16_version = self._versions()
 
     def mark_bf16_fresh(self):
         self._bf16_version = self._versions()

@@ -5,9 +5,9 @@ A training step of this model issues a few thousand native launches (24 Swin blo
 costs host time; captured once into a HIP graph (torch.cuda.CUDAGraph over the same HIP stream the
 native kernels launch on) a replay costs one launch.  Everything a step needs is graph-safe:
 allocations come from the graph's private pool, dropout masks use seed + a device offset advanced by
-a captured add (kernels.rng_advance), DropPath uses torch's graph-aware Philox, and the optimizer's
-bias corrections read a device step counter.  Inputs are static buffers: copy a new batch into
-`static_inputs` before `replay()` when training on real data.
+a captured add (kernels.rng_advance), DropPath uses torch's graph-aware Philox, the optimizer's
+bias corrections read a device step counter and its learning rates a device table refreshed before
+each replay.  Inputs are static buffers: TrainStepGraph copies each batch into them.
 """
 import torch
 
@@ -30,3 +30,118 @@ class CapturedStep:
     def replay(self):
         self.graph.replay()
         return self.out
+
+
+class _Captured:
+    __slots__ = ("static", "out", "g_step", "g_opt", "warm", "order", "stage", "turn", "free")
+
+    def __init__(self, inputs, device):
+        self.static = [torch.empty_like(t, device=device) for t in inputs]
+        self.out = self.g_step = self.g_opt = self.order = None
+        self.warm = False
+        # two device staging sets for host batches: the H2D copy of batch i+1 runs on a side stream
+        # while step i is still replaying, and never overwrites a set the main stream still reads
+        self.stage = [[torch.empty_like(t, device=device) for t in inputs] for _ in range(2)] \
+            if any(not t.is_cuda for t in inputs) else None
+        self.turn = 0
+        self.free = [None, None]   # main-stream events: staging set k has been copied out
+
+
+class TrainStepGraph:
+    """The agent's training step (agent_oe.py:19-48 and its MC / count twins) replayed from HIP
+    graphs: forward -> task loss -> backward [-> all-reduce of the gradient buckets] -> fused AdamW.
+
+    body(*static_inputs) runs forward + loss + backward and returns the tensors the caller reads
+    (logits, per-sample loss terms, ...).  On one rank the optimizer step is captured into the same
+    graph; with a GradReducer (world > 1) the step is graph(forward + backward, with the bf16 bucket
+    casts) -> the bucket all-reduces in capture order -> graph(optimizer).  The first call with a
+    new input signature (shapes / dtypes) runs the step eagerly (allocator / kernel warm-up, a real
+    training step) and captures on the next one; graphs are kept per signature (a short last batch
+    gets its own).  Every call is exactly one training step."""
+
+    def __init__(self, body, optim, reducer=None, world=1):
+        self.body, self.optim, self.reducer, self.world = body, optim, reducer, world
+        self.states = {}
+        self.static = None   # static inputs of the last call (the agent reads the labels from it)
+        self.copy_stream = None
+
+    def _load(self, st, inputs):
+        """Batch -> the static input buffers.  Host tensors (pinned by the DataLoader) go H2D on a
+        side stream into a staging set, overlapping the previous step's replay; the main stream
+        then waits for that copy and moves the batch with a device-to-device copy."""
+        cur = torch.cuda.current_stream(self.optim.flat.device)
+        if st.stage is None:
+            for s, t in zip(st.static, inputs):
+                s.copy_(t, non_blocking=True)
+            return
+        if self.copy_stream is None:
+            self.copy_stream = torch.cuda.Stream(self.optim.flat.device)
+        k = st.turn
+        st.turn ^= 1
+        stage = st.stage[k]
+        cs = self.copy_stream
+        if st.free[k] is not None:
+            cs.wait_event(st.free[k])          # the main stream has moved this set's last batch out
+        with torch.cuda.stream(cs):
+            for d, t in zip(stage, inputs):
+                d.copy_(t, non_blocking=True)
+        cur.wait_event(cs.record_event())
+        for s, d in zip(st.static, stage):
+            s.copy_(d, non_blocking=True)
+        st.free[k] = cur.record_event()
+
+    @staticmethod
+    def _sig(inputs):
+        return tuple((tuple(t.shape), t.dtype) for t in inputs)
+
+    def _eager(self, st):
+        st.out = self.body(*st.static)
+        scale = self.reducer.finish() if self.reducer is not None else 1.0
+        self.optim.step(grad_scale=scale)
+        return st.out
+
+    def _capture(self, st):
+        torch.cuda.synchronize()
+        self.optim._sync_lrs()          # no host->device copy may land inside the capture
+        steps = self.optim.step_count   # the host-side count of a captured step() is not a real step
+        pool = torch.cuda.graph_pool_handle()
+        st.g_step = torch.cuda.CUDAGraph()
+        if self.reducer is None:
+            with torch.cuda.graph(st.g_step, pool=pool):
+                st.out = self.body(*st.static)
+                self.optim.step(grad_scale=1.0)
+        else:
+            self.reducer.capture_begin()
+            try:
+                with torch.cuda.graph(st.g_step, pool=pool):
+                    st.out = self.body(*st.static)
+                    self.reducer.finish()            # captures the remaining buckets' bf16 casts
+                st.order = list(self.reducer.captured)
+            finally:
+                self.reducer.capture_end()
+            st.g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(st.g_opt, pool=pool):
+                self.optim.step(grad_scale=1.0 / self.world)
+        self.optim.step_count = steps
+        self.optim.flat.mark_bf16_fresh()
+        torch.cuda.synchronize()
+
+    def __call__(self, *inputs):
+        key = self._sig(inputs)
+        st = self.states.get(key)
+        if st is None:
+            st = self.states[key] = _Captured(inputs, self.optim.flat.device)
+        self.static = st.static
+        self._load(st, inputs)
+        if not st.warm:
+            st.warm = True
+            return self._eager(st)
+        if st.g_step is None:
+            self._capture(st)
+        self.optim._sync_lrs()
+        st.g_step.replay()
+        if st.g_opt is not None:
+            self.reducer.replay_allreduce(st.order)
+            st.g_opt.replay()
+        self.optim.step_count += 1      # host bookkeeping the captured optimizer step cannot do
+        return st.out

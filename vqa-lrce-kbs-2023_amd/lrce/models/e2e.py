@@ -5,15 +5,17 @@ attributes (`text_extractor`, `video_extractor`, `fusion_model`) and forward con
     forward(video_clips (B,S,T,3,H,W) f32, texts (B,L)|(B,5,L) int64, texts_attention_mask,
             texts_type_ids) -> (B,num_classes) | (B,5) | (B,)
 The reference asserts the Kinetics-600 Swin checkpoint exists (e2e.py:11) and downloads BERT by
-name (text.py:9); this build loads the checkpoint when present and otherwise keeps its own
-initialisation (synthetic benchmarking / tests), and never touches the network.
+name (text.py:9); this build loads the Swin checkpoint and a local BERT copy when present (keyword
+arguments swin_ckpt / bert_dir; None = random initialisation on purpose), warns otherwise, never
+touches the network, and exposes `pretrained_loaded` so the training CLI can refuse a real run that
+would start from random backbones.
 """
 from typing import Iterable, List
 
 import torch
 import torch.nn as nn
 
-from ..feature_extractor.text import TextExtractor
+from ..feature_extractor.text import TextExtractor, BERT_DIR
 from ..feature_extractor.video import VideoExtractor, SWIN_B_CKPT
 from .. import kernels as K
 from ..runtime import prepare
@@ -32,15 +34,20 @@ class E2EBase(nn.Module):
     forward(clips, texts, mask, types) -> head(video features, text features, mask)."""
     HEAD = None
 
-    def __init__(self, *head_args, swin_ckpt=SWIN_B_CKPT) -> None:
+    def __init__(self, *head_args, swin_ckpt=SWIN_B_CKPT, bert_dir=BERT_DIR) -> None:
         super().__init__()
-        self.text_extractor = TextExtractor()
+        self.text_extractor = TextExtractor(bert_dir=bert_dir)
         self.video_extractor = VideoExtractor(swin_ckpt)
         if self.HEAD is not None:
             self.fusion_model = self.HEAD(*_head_args(*head_args))
 
     def extract_text_features(self, texts, attention_mask, texts_type_ids):
         return self.text_extractor(texts, attention_mask, texts_type_ids)
+
+    @property
+    def pretrained_loaded(self):
+        """Both backbones came from checkpoints (Swin Kinetics-600 + BERT)."""
+        return self.video_extractor.pretrained_loaded and self.text_extractor.pretrained_loaded
 
     def lrce_param_order(self):
         """Flat-store layout = reverse forward order (fusion, BERT top-down, Swin top-down), so the
@@ -71,9 +78,9 @@ class E2EOpenEnded(E2EBase):
 
     def __init__(self, feature_dim: int, num_classes: int, drop_out_rate: float = 0.1,
                  video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
-                 temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 30) -> None:
+                 temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 30, **pretrained) -> None:
         super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
-                         frame_sample_size, temporal_scale, text_seq_len)
+                         frame_sample_size, temporal_scale, text_seq_len, **pretrained)
 
 
 class E2EMultipleChoice(E2EBase):
@@ -81,9 +88,9 @@ class E2EMultipleChoice(E2EBase):
 
     def __init__(self, feature_dim: int, num_classes: int, drop_out_rate: float = 0.1,
                  video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
-                 temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 40) -> None:
+                 temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 40, **pretrained) -> None:
         super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
-                         frame_sample_size, temporal_scale, text_seq_len)
+                         frame_sample_size, temporal_scale, text_seq_len, **pretrained)
 
     def extract_text_features(self, texts, attention_mask, texts_type_ids):
         """e2e.py:77-81: the 5 question+answer sequences go through BERT as B*5 rows."""
@@ -97,6 +104,6 @@ class E2ECount(E2EBase):
 
     def __init__(self, feature_dim: int, num_classes: int = 1, drop_out_rate: float = 0.1,
                  video_feature_res: Iterable[int] = (7, 7), video_feature_dim: int = 768, frame_sample_size: int = 5,
-                 temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 30) -> None:
+                 temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 30, **pretrained) -> None:
         super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
-                         frame_sample_size, temporal_scale, text_seq_len)
+                         frame_sample_size, temporal_scale, text_seq_len, **pretrained)

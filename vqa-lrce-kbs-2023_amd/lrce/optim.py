@@ -34,7 +34,8 @@ class FusedAdamW(torch.optim.Optimizer):
         self.exp_avg = torch.zeros_like(flat.f32)
         self.exp_avg_sq = torch.zeros_like(flat.f32)
         self.sumsq = torch.zeros(len(flat.params), device=dev)        # ||p_t||^2 of the current parameters
-        self.sumsq_next = torch.zeros(len(flat.params), device=dev)   # accumulated by the update kernel
+        self.sumsq_next = torch.zeros(len(flat.params), device=dev)   # written by the update step
+        self.chunk_sq = torch.zeros(flat.n_chunks, device=dev)        # per-chunk sums (deterministic norms)
         self._norm_version = None   # flat.master_version() the norms belong to (None: never computed)
         self._index = {id(p): i for i, p in enumerate(flat.params)}
         self.tensor_lr = torch.zeros(len(flat.params), device=dev)
@@ -67,12 +68,15 @@ class FusedAdamW(torch.optim.Optimizer):
         if self._norm_version != flat.master_version():
             # parameters changed outside the optimizer (init / load): one norm pass; afterwards the
             # update kernel itself produces the next step's norms
-            K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params))
+            self._norms()
         self.sumsq_next.zero_()
-        K.adamw_step(flat.f32, flat.grad, self.exp_avg, self.exp_avg_sq, flat.chunk_tensor, self.tensor_lr, self.sumsq,
+        red = getattr(flat, "grad_reducer", None)
+        g16 = red.grad16 if red is not None else None    # all-reduced bf16 gradient buckets
+        K.adamw_step(flat.f32, flat.grad if g16 is None else None, self.exp_avg, self.exp_avg_sq, flat.chunk_tensor, self.tensor_lr, self.sumsq,
                      flat.bf16, flat.n_chunks, b1, b2, self.defaults["eps"], self.defaults["weight_decay"],
                      float(grad_scale), self.reg_strength, 1.0 - b1 ** t, 1.0 - b2 ** t, step=self.step_t,
-                     sumsq_next=self.sumsq_next, p_f16=flat.f16, f16_range=(flat.f16_lo, flat.f16_hi))
+                     sumsq_next=self.sumsq_next, p_f16=flat.f16, f16_range=(flat.f16_lo, flat.f16_hi), g_bf16=g16,
+                     tensor_chunk_off=flat.tensor_chunk_off, chunk_sq=self.chunk_sq)
         self.sumsq.copy_(self.sumsq_next)
         self._norm_version = flat.master_version()
         flat.mark_bf16_fresh()
@@ -88,9 +92,52 @@ class FusedAdamW(torch.optim.Optimizer):
         are now: the update kernel's norms when they are current, else one multi-tensor norm pass."""
         flat = self.flat
         if self._norm_version != flat.master_version():
-            K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params))
+            self._norms()
             self._norm_version = flat.master_version()
         return self.l2_term()
 
+    def _norms(self):
+        flat = self.flat
+        K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params),
+                       tensor_chunk_off=flat.tensor_chunk_off, chunk_sq=self.chunk_sq)
+
     def zero_grad(self, set_to_none=False):
         self.flat.grad.zero_()
+
+    # ------------------------------------------------------------------ checkpoints
+    # torch.optim.AdamW's format: state[i] = {'step', 'exp_avg', 'exp_avg_sq'} per parameter index.
+    # The moments are views of the two flat buffers, so torch.save writes each buffer once.
+    def state_dict(self):
+        flat = self.flat
+        step = torch.tensor(float(self._device_step()))
+        self.state.clear()
+        for p in flat.params:
+            if p.requires_grad:
+                self.state[p] = {"step": step.clone(), "exp_avg": flat._slice(self.exp_avg, p),
+                                 "exp_avg_sq": flat._slice(self.exp_avg_sq, p)}
+        try:
+            return super().state_dict()
+        finally:
+            self.state.clear()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        flat = self.flat
+        steps = []
+        with torch.no_grad():
+            for p in flat.params:
+                st = self.state.get(p)
+                if not st:
+                    continue
+                flat._slice(self.exp_avg, p).copy_(st["exp_avg"].reshape(p.shape))
+                flat._slice(self.exp_avg_sq, p).copy_(st["exp_avg_sq"].reshape(p.shape))
+                steps.append(float(st["step"]))
+        self.state.clear()
+        t = max(steps) if steps else 0.0
+        self.step_count = int(t)
+        self.step_t.fill_(t)
+        self._lr_cache = None
+        self._norm_version = None
+
+    def _device_step(self):
+        return float(self.step_t.item())
