@@ -177,3 +177,44 @@ def test_datasets_builder_requires_synthetic():
     a = cli.parse_arg_train(["--dataset", "tgif-transition", "--synthetic", "12", "--batch-size", "2"])
     tr, va = cli.datasets(a, ["train", "test"])
     assert len(tr) == 12 and len(va) == 3 and tr[0][1].shape == (5, 40)
+
+
+class _StubOE(torch.nn.Module):
+    """Stands in for the native E2E model in the CPU plumbing test (the product model runs on the GPU
+    only): deterministic logits from the inputs."""
+
+    def __init__(self, ncls):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.linspace(-1, 1, ncls))
+
+
+    def forward(self, clips, ids, mask, types):
+        key = clips.mean(dim=(1, 2, 3, 4, 5)) * 1000 + ids.float().sum(1)
+        return torch.outer(key, self.w)
+
+
+def test_config1_cpu_eval_plumbing(monkeypatch):
+    """BASELINE config 1 (msvd-qa-oe, batch 2, temporal scale 3, eval on 4 synthetic clips): the
+    eval.py plumbing — parser -> dataset -> loader -> agent.process_data -> metric reduction — on
+    the CPU with a stub model.  The product model itself has no CPU path by design."""
+    import lrce.agent.agent_base as AB
+    from lrce.agent import AgentOE
+    monkeypatch.setattr(AB, "ensure", lambda m: None)      # the stub has no native flat store
+    a = cli.parse_arg_eval(["--dataset", "msvd-qa-oe", "--model-path", "unused.pt", "--batch-size", "2",
+                            "--temporal-scale", "3", "--synthetic", "4", "--num-workers", "0"])
+    (test_ds,) = cli.datasets(a, ["test"])
+    assert len(test_ds) == 4
+    dl = torch.utils.data.DataLoader(test_ds, batch_size=a.batch_size, shuffle=False)
+    model = _StubOE(a.num_classes)
+    agent = AgentOE(model, "cpu", a, False, True)
+    agent.do_evaluation(dl)
+    correct, total, losses = 0, 0, []
+    with torch.no_grad():
+        for clips, ids, mask, types, gt in dl:
+            out = model(clips, ids, mask, types)
+            correct += int((out.argmax(1) == gt).sum())
+            total += gt.numel()
+            losses.append(float(torch.nn.functional.cross_entropy(out, gt)))
+    assert agent.last_metric_val == pytest.approx(correct / total)
+    nz = [x for x in losses if x != 0]
+    assert agent.last_loss == pytest.approx(sum(nz) / len(nz), rel=1e-5)

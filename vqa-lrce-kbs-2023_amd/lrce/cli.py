@@ -149,13 +149,14 @@ def factories(task_type):
 
 def datasets(a, splits):
     """The reference builds E2EMicrosoftDataset / E2ETGIFDataset from annotation files and videos
-    (train_ddp.py:24-75); this build serves the same item contract from SyntheticQADataset."""
+    (train_ddp.py:24-75); this build serves the same item contract from SyntheticQADataset.  For
+    eval.py (the only split is 'test') --synthetic N is the size of that split."""
     from .dataset import SyntheticQADataset
     if not a.synthetic:
         raise NotImplementedError("video/annotation readers are out of scope for this build (SURVEY §8 f); "
                                   "run with --synthetic N")
-    sizes = {"train": a.synthetic, "val": a.synthetic_val or max(a.synthetic // 4, a.batch_size),
-             "test": a.synthetic_val or max(a.synthetic // 4, a.batch_size)}
+    held = a.synthetic_val or max(a.synthetic // 4, a.batch_size)
+    sizes = {"train": a.synthetic, "val": held, "test": a.synthetic if list(splits) == ["test"] else held}
     out = []
     for i, s in enumerate(splits):
         out.append(SyntheticQADataset(sizes[s], task_type=a.task_type, max_text_token_len=a.text_seq_len,
