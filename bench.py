@@ -249,7 +249,7 @@ def main():
     log(f"loss {loss_v:.4f}  {value:.2f} samples/s  {ms:.1f} ms/step ({args.mode})")
     # per-kernel roofline: HIP events around every launch of the timed kernels, on their launch
     # stream, over eager steps of the same workload (a graph replay hides individual launches)
-    timer = K.KernelTimer("wattn_fwd", "wattn_bwd", "gemm", "gemm_f32")
+    timer = K.KernelTimer("wattn_qkv_fwd", "wattn_bwd", "gemm", "gemm_f32", detail=True)
     with timer:
         for i in range(args.roofline_steps):
             train_step(model, opt, reducer, batch)
@@ -307,12 +307,13 @@ def main():
 
 
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E ~8 TB/s
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r1_pmc_wattn_fwd.json")   # tools/pmc_traffic.py output
+RIDGE = MFMA_BF16_PEAK_TFLOPS * 1000.0 / HBM_PEAK_GBS   # 312.5 flop/B
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r2_pmc_wattn_qkv_fwd.json")   # tools/pmc_traffic.py output
 
 
 def _pmc_traffic():
-    """HBM bytes per launch of lrce_wattn_fwd from the committed rocprofv3 --pmc passes of this same
-    command (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH_SIZE doubled for gfx950)."""
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 --pmc passes of this
+    same command (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH_SIZE doubled for gfx950)."""
     try:
         with open(PMC_TRAFFIC) as f:
             d = json.load(f)
@@ -322,26 +323,44 @@ def _pmc_traffic():
 
 
 def _roofline(timer):
-    """Roofline of the Swin window-attention forward kernel (the kernel the north star names).
-    Algorithmic work per (window, head), n = 147 tokens (8x7x7 window clamped to the 3x7x7 token grid of
-    a 5-frame clip), d = 32: flops 4 n^2 d (QK^T + PV); bytes 8 n d (Q, K, V read and
-    O written, bf16).  Arithmetic intensity n / 2 = 73.5 flop/B is below the bf16 ridge point
-    (2.5 PF/s / 8 TB/s = 312 flop/B), so the kernel is HBM-bound: `bound`/`frac` are against HBM peak,
-    and the MFMA fraction the north-star metric names is reported beside it (its ceiling at this
-    intensity is 73.5 x 8 TB/s = 588 TF/s = 0.235 of peak).  Duration = HIP events recorded around
-    every launch on its stream during eager steps of the same workload."""
-    n, mean_ms, tflops, gbs = timer.summary("wattn_fwd")
+    """Roofline of the Swin window-attention kernel the north star names, which here is ONE kernel:
+    the QKV projection fused with the 3D shifted-window attention (csrc/window_fused.hip).
+    Algorithmic work per launch (no credit for padding): the qkv Linear
+    2 * (windows * 147) * C * 3C plus QK^T + PV 4 * 147^2 * 32 per (window, head); algorithmic bytes:
+    the LN1 rows read, W_qkv read, qkv (kept for the backward) and O written, bf16.  The kernel is
+    MFMA-bound where its intensity passes the bf16 ridge (2.5 PF/s / 8 TB/s = 312 flop/B: stages 3-4,
+    C >= 512) and HBM-bound below it (stages 1-2): `bound` follows the step's aggregate intensity over
+    all 24 launches, and both fractions are reported, plus the MFMA fraction of the attention products
+    alone (the part the reference runs as bmm + softmax).  Durations: HIP events around every launch
+    on its stream during eager steps of the same workload (a graph replay hides launches)."""
+    n, mean_ms, tflops, gbs = timer.summary("wattn_qkv_fwd")
     if not n:
         return None
     traffic, src = _pmc_traffic()
-    alg_bytes = timer.bytes["wattn_fwd"] / n
-    roof = {"kernel": "lrce_wattn_fwd", "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "algorithmic_bytes_per_launch": round(alg_bytes), "traffic_source": src,
+    fl, by = timer.flops["wattn_qkv_fwd"], timer.bytes["wattn_qkv_fwd"]
+    ai = fl / by
+    mf, hf = tflops / MFMA_BF16_PEAK_TFLOPS, gbs / HBM_PEAK_GBS
+    attn_fl = sum(4.0 * 147 * 147 * 32 * nw * nh * len(ev) for (name, (nw, nh)), (ev, _) in timer.detail.items()
+                  if name == "wattn_qkv_fwd") if timer.detail is not None else None
+    total_ms = timer.total_ms("wattn_qkv_fwd")
+    roof = {"kernel": "lrce_wattn_qkv_fwd (qkv Linear + window attention fused)",
+            "bound": "mfma" if ai >= RIDGE else "hbm",
+            "achieved": round(tflops if ai >= RIDGE else gbs, 2), "peak": MFMA_BF16_PEAK_TFLOPS if ai >= RIDGE else HBM_PEAK_GBS,
+            "unit": "TFLOP/s" if ai >= RIDGE else "GB/s", "frac": round(mf if ai >= RIDGE else hf, 4),
+            "traffic": traffic, "traffic_source": src,
+            "algorithmic_bytes_per_launch": round(by / n), "algorithmic_flops_per_launch": round(fl / n),
+            "intensity_flop_per_byte": round(ai, 1), "ridge_flop_per_byte": RIDGE,
             "launches": n, "mean_launch_ms": round(mean_ms, 4),
-            "mfma": {"achieved": round(tflops, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(tflops / MFMA_BF16_PEAK_TFLOPS, 4),
-                     "ceiling_frac_at_this_intensity": round(73.5 * HBM_PEAK_GBS / 1000.0 / MFMA_BF16_PEAK_TFLOPS, 4)}}
+            "mfma_frac": round(mf, 4), "hbm_frac": round(hf, 4)}
+    if attn_fl is not None and total_ms > 0:
+        roof["attention_only_mfma_frac"] = round(attn_fl / total_ms / 1e9 / MFMA_BF16_PEAK_TFLOPS, 4)
+    per = {}
+    for (name, key), (ev, f) in (timer.detail or {}).items():
+        if name == "wattn_qkv_fwd":
+            t = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+            per[f"windows{key[0]}_heads{key[1]}"] = {"mean_launch_ms": round(t, 4),
+                                                     "tflops": round(f / len(ev) / t / 1e9, 1)}
+    roof["per_stage"] = per
     extra = {}
     for name in ("wattn_bwd", "gemm", "gemm_f32"):
         if name in timer.names:

@@ -138,36 +138,43 @@ int64_t lrce_layernorm_bwd_workspace(int rows, int cols);
 
 /* ---------------------------------------------------------------- Swin 3D window attention
  * Replaces WindowAttention3D.forward video_swin_ori.py:164-186 (QK^T, relative-position bias,
- * shift mask, softmax, PV) for windows of n <= 160 tokens and head_dim 32.
+ * shift mask, softmax, PV) for windows of n in (128, 160] tokens and head_dim 32.
  * qkv: bf16 [n_win*n][3C] window-ordered rows (q columns pre-scaled by head_dim^-0.5*log2(e)),
  * out: bf16 [n_win*n][C], lse: f32 [n_win][nH][160] (log2 domain).
  * bias tiles are built once per layer by lrce_wattn_bias_build from the f32 table
  * (relative_position_bias_table) and the int64 relative_position_index (ld = index_ld), with the
  * shift mask of each window pattern given as per-token region ids region[n_pat][n] (-100 between
- * different regions, video_swin_ori.py:346-359); win_pat[w] selects the pattern of window w. */
+ * different regions, video_swin_ori.py:346-359); bias_fwd holds the S^T-oriented tiles (forward and
+ * the dQ backward kernel), bias_bwd the S-oriented ones (the dK / dV backward kernel). */
 int64_t lrce_wattn_bias_elems(int n_pat, int nH);
 int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
                           const int32_t* region, int n_pat, float* bias_fwd, float* bias_bwd, void* stream);
-int lrce_wattn_fwd(const uint16_t* qkv, const float* bias_fwd, const int32_t* win_pat,
-                   uint16_t* out, float* lse, int n_win, int n, int nH, void* stream);
-/* Same forward with windows grouped by mask pattern, GW = 4 windows per group: win_list int32
+/* Forward with windows grouped by mask pattern, GW = 4 windows per group: win_list int32
  * [n_groups*4] (window ids, -1 = empty slot; NULL = identity 0,1,2,...), grp_pat int32 [n_groups]
  * (the group's mask pattern; NULL = pattern 0).  The bias row of a query tile is staged once per
  * group in LDS: build the grouping once per stage geometry (lrce/feature_extractor/video_swin.py). */
 int lrce_wattn_fwd_grouped(const uint16_t* qkv, const float* bias_fwd, const int32_t* win_list, const int32_t* grp_pat,
                            int n_groups, uint16_t* out, float* lse, int n_win, int n, int nH, void* stream);
-/* dqkv: bf16 [n_win*n][3C] (d/dq, d/dk, d/dv w.r.t. the UNSCALED q).  ds_scratch: bf16,
- * lrce_wattn_ds_elems(n_win, nH) elements; table_grad (f32 [table_rows][nH]) is accumulated. */
+/* Fused QKV projection + window attention forward (WindowAttention3D.forward video_swin_ori.py:158-189
+ * including the qkv Linear :150,165): x bf16 [n_win*n][C] (LN1 output in window order), w_qkv bf16
+ * [3C][C], b_qkv f32 [3C]; q is scaled by qscale (= head_dim^-0.5 * log2(e)) after the bias.  Writes
+ * qkv bf16 [n_win*n][3C] (the backward's input, same layout as above), out and lse as
+ * lrce_wattn_fwd_grouped.  One workgroup per (window, 4 heads); nH % 4 == 0, C % 64 == 0. */
+int lrce_wattn_qkv_fwd(const uint16_t* x, const uint16_t* w_qkv, const float* b_qkv, float qscale,
+                       const float* bias_fwd, const int32_t* win_pat, uint16_t* qkv, uint16_t* out, float* lse,
+                       int n_win, int n, int nH, void* stream);
+/* dqkv: bf16 [n_win*n][3C] (d/dq, d/dk, d/dv w.r.t. the UNSCALED q).  win_pat int32 [n_win] (the
+ * window's mask pattern, NULL = 0).  ds_scratch: bf16, lrce_wattn_ds_elems(n_win, nH) elements (dS per
+ * (window, head) for the bias-table gradient, then lrce_wattn_dbias_csr). */
 int64_t lrce_wattn_ds_elems(int n_win, int nH);
 int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                   const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv, uint16_t* ds_scratch,
-                   int n_win, int n, int nH, void* stream);
-int lrce_wattn_dbias(const uint16_t* ds_scratch, int n_win, int n, int nH, const int64_t* index, int index_ld,
-                     float* table_grad, void* stream);
-/* Same bias-table gradient without atomics: csr_off int32 [n_bins+1] / csr_el int32 list, per table
- * row, the positions (per-lane tile order, 25 tiles x 1024) of the (query, key) pairs whose
- * relative_position_index is that row (built once per stage geometry: lrce.kernels.wattn_dbias_csr).
- * Deterministic: every table entry is written by one thread. */
+                   const float* bias_fwd, const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv,
+                   uint16_t* ds_scratch, int n_win, int n, int nH, void* stream);
+/* Bias-table gradient (relative_position_bias_table, f32 [table_rows][nH], accumulated):
+ * csr_off int32 [n_bins+1] / csr_el int32 list, per table row, the positions (per-lane tile order,
+ * 25 tiles x 1024) of the (query, key) pairs whose relative_position_index is that row (built once per
+ * stage geometry: lrce.kernels.wattn_dbias_csr).  Deterministic: every table entry is written by one
+ * thread, no atomics. */
 int lrce_wattn_dbias_csr(const uint16_t* ds_scratch, int n_win, int nH, const int32_t* csr_off, const int32_t* csr_el,
                          int n_bins, float* table_grad, void* stream);
 

@@ -37,7 +37,7 @@ def test_gemm_rejects_bad_shapes_without_launching():
 
 def test_wattn_rejects_unsupported_window():
     from lrce import _native
-    rc = _native.lib().lrce_wattn_fwd(0x1000, 0x1000, None, 0x1000, 0x1000, 4, 100, 4, None)
+    rc = _native.lib().lrce_wattn_fwd_grouped(0x1000, 0x1000, None, None, 1, 0x1000, 0x1000, 4, 100, 4, None)
     assert rc == 1
     assert b"outside" in _native.lib().lrce_last_error()
 

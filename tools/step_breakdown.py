@@ -24,11 +24,11 @@ def main():
     ap.add_argument("--top", type=int, default=60)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    model, opt, reducer, batch = bench.build(a.batch_size, dev)
+    model, opt, reducer, batch = bench.build(a.batch_size, dev, torch.bfloat16)
     for _ in range(2):
         bench.train_step(model, opt, reducer, batch)
     torch.cuda.synchronize()
-    kt = K.KernelTimer("gemm", "gemm_f32", "wattn_fwd", "wattn_bwd", detail=True)
+    kt = K.KernelTimer("gemm", "gemm_f32", "wattn_fwd", "wattn_qkv_fwd", "wattn_bwd", detail=True)
     with kt:
         bench.train_step(model, opt, reducer, batch)
     rows = kt.breakdown()

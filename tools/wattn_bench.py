@@ -52,12 +52,17 @@ def main():
         dqkv = torch.empty_like(qkv)
         ds = torch.empty(K.wattn_ds_elems(n_win, nH), device=dev, dtype=torch.bfloat16)
         groups = K.wattn_groups(win_pat, n_win, dev)
-        if os.environ.get("WATTN_V1"):
-            tf = timeit(lambda: K.wattn_fwd(qkv, bf_, win_pat, out, lse, n_win, n, nH))
-        else:
-            tf = timeit(lambda: K.wattn_fwd_grouped(qkv, bf_, groups, out, lse, n_win, n, nH))
+        tf = timeit(lambda: K.wattn_fwd_grouped(qkv, bf_, groups, out, lse, n_win, n, nH))
+        x = (torch.randn(n_win * n, C, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+        wq = (torch.randn(3 * C, C, device=dev, generator=g) / C ** 0.5).to(torch.bfloat16)
+        bq = torch.zeros(3 * C, device=dev)
+        tq = timeit(lambda: K.wattn_qkv_fwd(x, wq, bq, 0.25, bf_, win_pat, qkv, out, lse, n_win, n, nH))
+        tg = timeit(lambda: K.linear(x, wq, bq, out=qkv, scale_cols=C, scale_val=0.25))
+        fq = 2.0 * n_win * n * C * 3 * C + 4.0 * n * n * hd * n_win * nH
+        print(f"win {n_win:5d} heads {nH:3d}: fused qkv+attn {tq * 1e3:7.1f} us {fq / tq / 1e9:6.1f} TF/s   "
+              f"(unfused: qkv GEMM {tg * 1e3:6.1f} us + attn {tf * 1e3:6.1f} us)", flush=True)
         tb = 1e-9 if os.environ.get("WATTN_FWD_ONLY") else \
-            timeit(lambda: K.wattn_bwd(qkv, out, dout, lse, bb_, win_pat, dqkv, ds, n_win, n, nH))
+            timeit(lambda: K.wattn_bwd(qkv, out, dout, lse, bf_, bb_, win_pat, dqkv, ds, n_win, n, nH))
         ff, fb = 4.0 * n * n * hd * n_win * nH, 8.0 * n * n * hd * n_win * nH
         tot_f += tf; tot_b += tb; fl_f += ff; fl_b += fb
         print(f"win {n_win:5d} heads {nH:3d}: fwd {tf * 1e3:7.1f} us {ff / tf / 1e9:6.1f} TF/s   "

@@ -565,27 +565,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     gb.init(bbase, p.ldb, p.n, n0, kb, wave, lane);
     ga.issue(la0, wave_u);
     gb.issue(lb0, wave_u);
-#ifdef LRCE_GEMM_ONEBAR
-    // one barrier per K tile: it publishes tile kt (every wave waited for its own DMAs) AND retires
-    // compute(kt-1), so the DMA of kt+1 may then overwrite that stage
-    for (int kt = 0; kt < nfull; ++kt) {
-      const int cur = kt & 1;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt + 1 < nfull) {
-        ga.advance(); gb.advance();
-        ga.issue(la0 + (uint32_t)((cur ^ 1) * STG * 2), wave_u);
-        gb.issue(lb0 + (uint32_t)((cur ^ 1) * STG * 2), wave_u);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      compute(sa0 + cur * STG, sb0 + cur * STG);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-#else
     for (int kt = 0; kt < nfull; ++kt) {
       const int cur = kt & 1;
       if (kt + 1 < nfull) {
@@ -605,7 +584,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       __builtin_amdgcn_s_barrier();                          // stage `cur` free for tile kt+2
       __builtin_amdgcn_sched_barrier(0);
     }
-#endif
   }
   if (tail) {
     const int k0 = kb + nfull * BK;

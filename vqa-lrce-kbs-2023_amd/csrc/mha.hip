@@ -654,7 +654,7 @@ bool short_self(const LrceMhaDesc* d) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return d->lk2 == 0 && d->Lq == d->lk1 && d->Lq <= 64 && d->kv1_bdiv == 1 && !d->f32_io && aligned_rows(d) &&
          al(d->q) && d->ld_q % 8 == 0 && al(d->out) && d->ld_o % 8 == 0 && (!d->dout || al(d->dout)) &&
-         d->stride_kv1_b == (long long)d->lk1 * d->ld_kv1 && getenv("LRCE_MHA_VALU") == nullptr;
+         d->stride_kv1_b == (long long)d->lk1 * d->ld_kv1;
 }
 
 int check(const LrceMhaDesc* d, bool bwd) {

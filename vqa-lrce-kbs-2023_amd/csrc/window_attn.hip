@@ -1,21 +1,18 @@
 // Fused 3D shifted-window attention for Video Swin (WindowAttention3D.forward,
 // video_swin_ori.py:158-189) on gfx950.
 //
-// One wave owns one (window, head) problem: n <= 160 tokens (147 = 3x7x7 padded to 5 tiles of
-// 32), head_dim 32.  All products use v_mfma_f32_32x32x16_bf16.
+// Problems are (window, head) pairs: n <= 160 tokens (147 = 3x7x7 padded to 5 tiles of 32), head_dim
+// 32.  All products use v_mfma_f32_32x32x16_bf16.
 //
-// Forward computes S^T = K Q^T so each lane owns one query column and 80 key rows: the softmax
-// row reductions are in-lane plus one cross-half exchange, and the probabilities are already the
-// B operand of O^T = V^T P^T (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's
+// Forward (wattn_fwd3): S^T = K Q^T so each lane owns one query column and 80 key rows: the softmax
+// row reductions are in-lane plus one cross-half exchange, and the probabilities are already the B
+// operand of O^T = V^T P^T (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's
 // operand").  The relative-position bias, the shift mask (-100) and the key padding (-1e30) are
-// pre-combined per (mask pattern, head), pre-multiplied by log2(e) and stored in the exact
-// per-lane accumulator order, so the MFMA chain starts from the bias: no VALU for scale/bias/mask.
-// q is pre-scaled by head_dim^-0.5 * log2(e) in the QKV GEMM epilogue, so p = exp2(s - max).
+// pre-combined per (mask pattern, head), pre-multiplied by log2(e) and stored in the exact per-lane
+// accumulator order, so the MFMA chain starts from the bias: no VALU for scale/bias/mask.  q is
+// pre-scaled by head_dim^-0.5 * log2(e) in the QKV GEMM epilogue, so p = exp2(s - max).
 //
-// Backward recomputes S = Q K^T (rows = queries) tile by tile, and produces dV = P^T dO and
-// dK = dS^T Q with P / dS straight from registers as A operands, dQ = dS K through a 2 KB LDS
-// transpose of dS; dQ accumulates across key tiles in registers.  dS (bf16) is also written in
-// per-lane tile order for the bias-table gradient (lrce_wattn_dbias sums it over windows).
+// Backward: two kernels (dK/dV by key tile, dQ by query tile) described above wattn_bwd_kv_kernel.
 #include <cstdlib>
 #include <type_traits>
 
@@ -32,11 +29,6 @@ constexpr int TILE_ELEMS = 64 * 16;
 constexpr int PH_ELEMS = NTILE * NTILE * TILE_ELEMS;  // per (pattern, head)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;
-
-__device__ __forceinline__ void wave_lds_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
 
 // row index (inside a 32x32 C tile) held in register `reg` by lane half `h`
 __device__ __forceinline__ int crow(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
@@ -60,39 +52,11 @@ __device__ __forceinline__ bf16x8 tr_read_perm(const bf16* img, int r_base, int 
   }
   return out;
 }
-// same, natural k order: element j = img[r_base + 8*hh + 4*(j>>2) + (j&3)][c]
-__device__ __forceinline__ bf16x8 tr_read_nat(const bf16* img, int r_base, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int hh = g >> 1, cb = 16 * (g & 1);
-  bf16x8 out;
-#pragma unroll
-  for (int h2 = 0; h2 < 2; ++h2) {
-    const int row = r_base + 8 * hh + 4 * h2 + q;
-    const LRCE_LDS s16x4* src = (const LRCE_LDS s16x4*)(img + row * 32 + cb + 4 * p);
-    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<LRCE_LDS s16x4*>(src));
-    bf16x4 b = *reinterpret_cast<bf16x4*>(&v);
-    out[4 * h2 + 0] = b[0]; out[4 * h2 + 1] = b[1]; out[4 * h2 + 2] = b[2]; out[4 * h2 + 3] = b[3];
-  }
-  return out;
-}
-
 __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int s) {
   bf16x8 o;
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = f2bf(a[8 * s + j]);
   return o;
-}
-
-// stage rows [0,160) x 32 cols of a head slice into an LDS image (zero rows >= n)
-__device__ __forceinline__ void stage_img(bf16* img, const bf16* src, long long ld, int n, int lane) {
-#pragma unroll
-  for (int t = 0; t < 10; ++t) {
-    const int c = lane + 64 * t;
-    const int row = c >> 2, part = c & 3;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (row < n) v = *reinterpret_cast<const uint4*>(src + row * ld + part * 8);
-    *reinterpret_cast<uint4*>(img + row * 32 + part * 8) = v;
-  }
 }
 
 // ------------------------------------------------------------------------------ bias tiles
@@ -123,202 +87,8 @@ __global__ void bias_build_kernel(const float* table, const int64_t* index, int 
   bb[e] = val(qt * TQ + crow(reg, hh), kt * TQ + col);
 }
 
-// ------------------------------------------------------------------------------ forward
-__global__ void __launch_bounds__(256, 2) wattn_fwd_kernel(const bf16* __restrict__ qkv, const float* __restrict__ biasf,
-                                                           const int* __restrict__ win_pat, bf16* __restrict__ out,
-                                                           float* __restrict__ lse, int n_win, int n, int nH) {
-  __shared__ __attribute__((aligned(16))) bf16 vimg_all[4][NPAD * HD];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // head-fastest block order: the nH blocks of a window group run together and share the 128-B
-  // lines of the qkv rows (each head reads a 64-B slice) in L2
-  const int w = (blockIdx.x / nH) * 4 + wave, h = blockIdx.x % nH;
-  if (w >= n_win) return;
-  const int C = nH * HD;
-  const long long ld = 3LL * C;
-  const bf16* base = qkv + (long long)w * n * ld;
-  bf16* vimg = vimg_all[wave];
-  stage_img(vimg, base + 2 * C + h * HD, ld, n, lane);
-
-  const int hh = lane >> 5, r32 = lane & 31;
-  bf16x8 kf[NTILE][2];
-#pragma unroll
-  for (int kt = 0; kt < NTILE; ++kt) {
-    const int key = kt * TQ + r32;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 v = {};
-      if (key < n) v = ld_row16(base + key * ld + C + h * HD + 16 * s + 8 * hh);
-      kf[kt][s] = v;
-    }
-  }
-  wave_lds_fence();
-  const int pat = win_pat ? win_pat[w] : 0;
-  const float* bp = biasf + (long long)(pat * nH + h) * PH_ELEMS;
-
-  for (int qt = 0; qt < NTILE; ++qt) {
-    if (qt * TQ >= n) break;
-    const int qi = qt * TQ + r32;
-    bf16x8 qf[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 v = {};
-      if (qi < n) v = ld_row16(base + qi * ld + h * HD + 16 * s + 8 * hh);
-      qf[s] = v;
-    }
-    f32x16 acc[NTILE];
-#pragma unroll
-    for (int kt = 0; kt < NTILE; ++kt) {
-      // forward bias tiles are stored register-group-major ([u][lane][4]): each load is 1 KB contiguous
-      const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + kt) * TILE_ELEMS) + lane;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 b = src[64 * u];
-        acc[kt][4 * u] = b.x; acc[kt][4 * u + 1] = b.y; acc[kt][4 * u + 2] = b.z; acc[kt][4 * u + 3] = b.w;
-      }
-      acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][0], qf[0], acc[kt], 0, 0, 0);
-      acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][1], qf[1], acc[kt], 0, 0, 0);
-    }
-    float m = NEG_BIG;
-#pragma unroll
-    for (int kt = 0; kt < NTILE; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[kt][r]);
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NTILE; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(acc[kt][r] - m);
-        acc[kt][r] = p;
-        sum += p;
-      }
-    sum += __shfl_xor(sum, 32, 64);
-    f32x16 o = {};
-#pragma unroll
-    for (int kt = 0; kt < NTILE; ++kt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 a = tr_read_perm(vimg, kt * TQ + 16 * s, lane);
-        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pack8(acc[kt], s), o, 0, 0, 0);
-      }
-    if (qi < n) {
-      const float inv = 1.0f / sum;
-      bf16* dst = out + ((long long)w * n + qi) * C + h * HD + 4 * hh;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        bf16x4 v;
-        v[0] = f2bf(o[4 * rr] * inv); v[1] = f2bf(o[4 * rr + 1] * inv);
-        v[2] = f2bf(o[4 * rr + 2] * inv); v[3] = f2bf(o[4 * rr + 3] * inv);
-        *reinterpret_cast<bf16x4*>(dst + 8 * rr) = v;
-      }
-      if (hh == 0) lse[((long long)w * nH + h) * NPAD + qi] = m + __log2f(sum);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------ forward, v2
-// One workgroup per (window, head), one wave per 32-query tile (5 waves, 320 threads): 5x the
-// waves of a wave-per-window kernel in flight, so the L2 latency of the bias tiles (issued first,
-// straight into the accumulators) and of the Q/K/V rows overlaps across waves instead of stalling
-// every query tile of one wave.  K and V are staged once per workgroup in LDS (K rows XOR-swizzled
-// by 16-B chunk for conflict-free row reads, V plain for the transposed reads of O^T = V^T P^T).
+// K rows XOR-swizzled by 16-B chunk (conflict-free row reads of the grouped forward's Q tiles)
 __device__ __forceinline__ int kswz(int row, int chunk) { return row * HD + ((chunk ^ ((row >> 2) & 3)) << 3); }
-
-__global__ void __launch_bounds__(320, 3) wattn_fwd2_kernel(const bf16* __restrict__ qkv, const float* __restrict__ biasf,
-                                                            const int* __restrict__ win_pat, bf16* __restrict__ out,
-                                                            float* __restrict__ lse, int n_win, int n, int nH) {
-  __shared__ __attribute__((aligned(16))) bf16 kimg[NPAD * HD];
-  __shared__ __attribute__((aligned(16))) bf16 vimg[NPAD * HD];
-  const int lane = threadIdx.x & 63, qt = threadIdx.x >> 6;
-  // head-fastest over an XCD-contiguous block order: a window's heads run on one XCD and share the
-  // 128-B lines of its qkv rows (each head reads a 64-B slice) in that XCD's L2
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int h = lin % nH, w = lin / nH;
-  const int C = nH * HD;
-  const long long ld = 3LL * C;
-  const bf16* base = qkv + (long long)w * n * ld;
-  const int pat = win_pat ? win_pat[w] : 0;
-  // 1. this wave's 5 bias tiles -> accumulators (register-group-major tiles: 1 KB per load)
-  f32x16 acc[NTILE];
-  {
-    const float4* src = reinterpret_cast<const float4*>(biasf + (long long)(pat * nH + h) * PH_ELEMS +
-                                                        (long long)qt * NTILE * TILE_ELEMS) + lane;
-#pragma unroll
-    for (int kt = 0; kt < NTILE; ++kt)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 b = src[kt * (TILE_ELEMS / 4) + 64 * u];
-        acc[kt][4 * u] = b.x; acc[kt][4 * u + 1] = b.y; acc[kt][4 * u + 2] = b.z; acc[kt][4 * u + 3] = b.w;
-      }
-  }
-  // 2. Q fragments of this wave's query tile
-  const int hh = lane >> 5, r32 = lane & 31;
-  const int qi = qt * TQ + r32;
-  bf16x8 qf[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) qf[s] = qi < n ? ld_row16(base + qi * ld + h * HD + 16 * s + 8 * hh) : bf16x8{};
-  // 3. K, V rows [0,160) -> LDS (zero past n): 2 x 640 16-B chunks over 320 threads
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int c = threadIdx.x + 320 * t;
-    const int row = c >> 2, part = c & 3;
-    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-    if (row < n) {
-      kv = *reinterpret_cast<const uint4*>(base + row * ld + C + h * HD + part * 8);
-      vv = *reinterpret_cast<const uint4*>(base + row * ld + 2 * C + h * HD + part * 8);
-    }
-    *reinterpret_cast<uint4*>(kimg + kswz(row, part)) = kv;
-    *reinterpret_cast<uint4*>(vimg + row * HD + part * 8) = vv;
-  }
-  __syncthreads();
-  // 4. S^T = K Q^T (+ bias): rows = keys, cols = queries
-#pragma unroll
-  for (int kt = 0; kt < NTILE; ++kt) {
-    const int key = kt * TQ + r32;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kimg + kswz(key, 2 * s + hh));
-      acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], acc[kt], 0, 0, 0);
-    }
-  }
-  // 5. softmax over keys (in-lane + one cross-half exchange), exp2 domain (q pre-scaled by log2 e)
-  float m = NEG_BIG;
-#pragma unroll
-  for (int kt = 0; kt < NTILE; ++kt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[kt][r]);
-  m = fmaxf(m, __shfl_xor(m, 32, 64));
-  float sum = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < NTILE; ++kt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(acc[kt][r] - m);
-      acc[kt][r] = p;
-      sum += p;
-    }
-  sum += __shfl_xor(sum, 32, 64);
-  // 6. O^T = V^T P^T
-  f32x16 o = {};
-#pragma unroll
-  for (int kt = 0; kt < NTILE; ++kt)
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-      o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(vimg, kt * TQ + 16 * s, lane), pack8(acc[kt], s), o, 0, 0, 0);
-  if (qi < n) {
-    const float inv = 1.0f / sum;
-    bf16* dst = out + ((long long)w * n + qi) * C + h * HD + 4 * hh;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      bf16x4 v;
-      v[0] = f2bf(o[4 * rr] * inv); v[1] = f2bf(o[4 * rr + 1] * inv);
-      v[2] = f2bf(o[4 * rr + 2] * inv); v[3] = f2bf(o[4 * rr + 3] * inv);
-      *reinterpret_cast<bf16x4*>(dst + 8 * rr) = v;
-    }
-    if (hh == 0) lse[((long long)w * nH + h) * NPAD + qi] = m + __log2f(sum);
-  }
-}
 
 // ------------------------------------------------------------------------------ forward, grouped
 // Four windows of ONE (mask pattern, head) per workgroup, one wave each: the 20 KB bias row of the
@@ -510,215 +280,259 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restri
 }
 
 // ------------------------------------------------------------------------------ backward
-struct BwdLds {
+// Two kernels, one workgroup per (window, head), five waves each (one per 32-row tile), no
+// cross-wave reduction and no LDS transpose (FlashAttention-2 split, P and dP recomputed in each):
+//  * wattn_bwd_kv: wave kt owns key tile kt and sweeps the query tiles.  S = Q K^T + bias (rows =
+//    queries, key on the lane), P = exp2(S - lse), dS = P (dP - delta); the transposed products
+//    dV^T = dO^T P and dK^T = Q~^T dS take P / dS straight from the accumulators as B operands and
+//    dO / Q~ by transposed LDS reads, so the results have the key on the lane and 4 consecutive head
+//    dims per register group: 8-B vector stores of whole row pieces.  dS (bf16) goes to the
+//    bias-table gradient scratch in the tile order lrce_wattn_dbias_csr reads.
+//  * wattn_bwd_q: wave qt owns query tile qt and sweeps the key tiles in the forward's orientation
+//    S^T = K Q~^T + bias (query on the lane, so lse / delta are per-lane registers), dQ^T = K^T dS^T
+//    with dS^T from the accumulators and K^T by transposed reads of the staged K image.
+// P / dP are recomputed by both (7 products per tile instead of 5); in exchange every wave runs an
+// independent chain and a CU holds ~15 waves (21 KB of LDS per workgroup) to hide its latency.
+constexpr int BW = 5;   // waves per backward workgroup (= tiles of 32 rows)
+constexpr int GDS = 8;  // windows per dK/dV workgroup: their dS is summed in registers for the bias gradient
+
+struct BwdKVLds {
   bf16 q[NPAD * HD];
-  bf16 k[NPAD * HD];
   bf16 dout[NPAD * HD];
-  bf16 t[TQ * TQ];
   float lse[NPAD];
   float delta[NPAD];
 };
 
-__global__ void __launch_bounds__(128, 1) wattn_bwd_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
-                                                           const bf16* __restrict__ dout, const float* __restrict__ lse_g,
-                                                           const float* __restrict__ biasb, const int* __restrict__ win_pat,
-                                                           bf16* __restrict__ dqkv, bf16* __restrict__ ds_out,
-                                                           int n_win, int n, int nH, float scale) {
-  __shared__ __attribute__((aligned(16))) BwdLds L_all[2];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);   // a window pair's heads on one XCD (shared qkv/dO lines)
-  const int w = (lin / nH) * 2 + wave, h = lin % nH;
-  if (w >= n_win) return;
-  BwdLds& L = L_all[wave];
+// Workgroup = (group of GDS consecutive windows, head), windows in sequence.  The bias-table gradient
+// needs only sum_w dS_w per (query, key) position (the mask is constant), so each wave keeps its key
+// tile's dS summed over the group's windows in f32 registers and writes ONE partial image per
+// (group, head) — instead of a bf16 dS image per (window, head) (2 B x 160^2 each: 3 GB per training
+// step at bs 10).  lrce_wattn_dbias_csr then sums the group partials and gathers them per table row.
+__global__ void __launch_bounds__(BW * 64, 2) wattn_bwd_kv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
+                                                                 const bf16* __restrict__ dout, const float* __restrict__ lse_g,
+                                                                 const float* __restrict__ biasb, const int* __restrict__ win_pat,
+                                                                 bf16* __restrict__ dqkv, float* __restrict__ ds_part, int n_win,
+                                                                 int n, int nH) {
+  __shared__ __attribute__((aligned(16))) BwdKVLds L;
+  const int lane = threadIdx.x & 63, kt = threadIdx.x >> 6;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);   // a group's heads on one XCD (shared qkv / dO lines)
+  const int h = lin % nH, grp = lin / nH;
+  const int C = nH * HD;
+  const long long ld = 3LL * C;
+  const int hh = lane >> 5, r32 = lane & 31;
+  const int key = kt * TQ + r32;
+  const bool kt_live = kt * TQ < n;
+  const int nqt = (n + TQ - 1) / TQ;
+  f32x16 dsum[NTILE];
+#pragma unroll
+  for (int t = 0; t < NTILE; ++t) dsum[t] = f32x16{};
+  const int w_end = min(n_win, (grp + 1) * GDS);
+  for (int w = grp * GDS; w < w_end; ++w) {
+    const bf16* base = qkv + (long long)w * n * ld;
+    const bf16* obase = outp + (long long)w * n * C + h * HD;
+    const bf16* dobase = dout + (long long)w * n * C + h * HD;
+    __syncthreads();   // every wave is done with the previous window's images
+    // Q~ and dO images [160][32] (rows >= n zero): 640 16-B chunks each over 320 threads
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int c = threadIdx.x + BW * 64 * t;
+      const int row = c >> 2, part = c & 3;
+      uint4 qv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
+      if (row < n) {
+        qv = *reinterpret_cast<const uint4*>(base + row * ld + h * HD + part * 8);
+        dv = *reinterpret_cast<const uint4*>(dobase + (long long)row * C + part * 8);
+      }
+      *reinterpret_cast<uint4*>(L.q + row * HD + part * 8) = qv;
+      *reinterpret_cast<uint4*>(L.dout + row * HD + part * 8) = dv;
+    }
+    // delta[q] = dO[q] . O[q] and lse[q] (0 past n: padded queries then contribute nothing)
+    if (threadIdx.x < NPAD) {
+      const int q = threadIdx.x;
+      float d = 0.f, l = 0.f;
+      if (q < n) {
+#pragma unroll
+        for (int part = 0; part < 4; ++part) {
+          const bf16x8 a = ld_row16(obase + (long long)q * C + part * 8);
+          const bf16x8 b = ld_row16(dobase + (long long)q * C + part * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
+        }
+        l = lse_g[((long long)w * nH + h) * NPAD + q];
+      }
+      L.delta[q] = d;
+      L.lse[q] = l;
+    }
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      kf[s] = key < n ? ld_row16(base + key * ld + C + h * HD + 16 * s + 8 * hh) : bf16x8{};
+      vf[s] = key < n ? ld_row16(base + key * ld + 2 * C + h * HD + 16 * s + 8 * hh) : bf16x8{};
+    }
+    __syncthreads();
+    if (!kt_live) continue;
+    const int pat = win_pat ? win_pat[w] : 0;
+    const float* bp = biasb + (long long)(pat * nH + h) * PH_ELEMS + lane * 16;
+    f32x16 dkT = {}, dvT = {};
+#pragma unroll
+    for (int qt = 0; qt < NTILE; ++qt) {
+      if (qt >= nqt) break;
+      f32x16 sacc;
+      {
+        const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + kt) * TILE_ELEMS);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 b = src[u];
+          sacc[4 * u] = b.x; sacc[4 * u + 1] = b.y; sacc[4 * u + 2] = b.z; sacc[4 * u + 3] = b.w;
+        }
+      }
+      f32x16 dp = {};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(L.q + (qt * TQ + r32) * HD + 16 * s + 8 * hh);
+        const bf16x8 da = *reinterpret_cast<const bf16x8*>(L.dout + (qt * TQ + r32) * HD + 16 * s + 8 * hh);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dp, 0, 0, 0);
+      }
+      // P and dS (natural-log scale); rows = queries crow(r, hh), key on the lane
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = qt * TQ + crow(r, hh);
+        const float p = __builtin_amdgcn_exp2f(sacc[r] - L.lse[qi]);
+        sacc[r] = p;
+        dp[r] = p * (dp[r] - L.delta[qi]);
+      }
+      dsum[qt] += dp;
+      // dV^T += dO^T P ; dK^T += Q~^T dS  (the accumulators as B operands, permuted k order)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        dvT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(L.dout, qt * TQ + 16 * s, lane), pack8(sacc, s), dvT, 0, 0, 0);
+        dkT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(L.q, qt * TQ + 16 * s, lane), pack8(dp, s), dkT, 0, 0, 0);
+      }
+    }
+    // dK^T / dV^T: rows = head dims crow(r, hh), key on the lane -> 4 x 8-B stores per row piece
+    if (key < n) {
+      const float kscale = 1.0f / LOG2E;   // q~ = q d^-1/2 log2(e): dK = dS^T q d^-1/2 = dS^T q~ / log2(e)
+      bf16* row = dqkv + ((long long)w * n + key) * ld + h * HD + 4 * hh;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 a, b;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = f2bf(dkT[4 * g + e] * kscale);
+          b[e] = f2bf(dvT[4 * g + e]);
+        }
+        *reinterpret_cast<bf16x4*>(row + C + 8 * g) = a;
+        *reinterpret_cast<bf16x4*>(row + 2 * C + 8 * g) = b;
+      }
+    }
+  }
+  if (!kt_live) return;
+  // this wave's (qt, kt) tiles of the group's dS sum, f32, in the per-lane tile order of bias_bwd
+  float* dst = ds_part + ((long long)grp * nH + h) * PH_ELEMS + lane * 16;
+#pragma unroll
+  for (int qt = 0; qt < NTILE; ++qt) {
+    float4* o = reinterpret_cast<float4*>(dst + (qt * NTILE + kt) * TILE_ELEMS);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      o[u] = make_float4(dsum[qt][4 * u], dsum[qt][4 * u + 1], dsum[qt][4 * u + 2], dsum[qt][4 * u + 3]);
+  }
+}
+
+struct BwdQLds {
+  bf16 k[NPAD * HD];
+  bf16 v[NPAD * HD];
+};
+
+__global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_q_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
+                                                                const bf16* __restrict__ dout, const float* __restrict__ lse_g,
+                                                                const float* __restrict__ biasf, const int* __restrict__ win_pat,
+                                                                bf16* __restrict__ dqkv, int n_win, int n, int nH, float scale) {
+  __shared__ __attribute__((aligned(16))) BwdQLds L;
+  const int lane = threadIdx.x & 63, qt = threadIdx.x >> 6;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int h = lin % nH, w = lin / nH;
   const int C = nH * HD;
   const long long ld = 3LL * C;
   const bf16* base = qkv + (long long)w * n * ld;
-  const bf16* obase = outp + (long long)w * n * C + h * HD;
-  const bf16* dobase = dout + (long long)w * n * C + h * HD;
-  stage_img(L.q, base + h * HD, ld, n, lane);
-  stage_img(L.k, base + C + h * HD, ld, n, lane);
-  stage_img(L.dout, dobase, C, n, lane);
-  wave_lds_fence();
-  const float* lsep = lse_g + ((long long)w * nH + h) * NPAD;
-  for (int qi = lane; qi < NPAD; qi += 64) {
-    float d = 0.f, l = 0.f;
-    if (qi < n) {
 #pragma unroll
-      for (int part = 0; part < 4; ++part) {
-        const bf16x8 a = ld_row16(obase + qi * C + part * 8);
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(L.dout + qi * HD + part * 8);   // staged dO row
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
-      }
-      l = lsep[qi];
+  for (int t = 0; t < 2; ++t) {
+    const int c = threadIdx.x + BW * 64 * t;
+    const int row = c >> 2, part = c & 3;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (row < n) {
+      kv = *reinterpret_cast<const uint4*>(base + row * ld + C + h * HD + part * 8);
+      vv = *reinterpret_cast<const uint4*>(base + row * ld + 2 * C + h * HD + part * 8);
     }
-    L.delta[qi] = d;
-    L.lse[qi] = l;
+    *reinterpret_cast<uint4*>(L.k + row * HD + part * 8) = kv;
+    *reinterpret_cast<uint4*>(L.v + row * HD + part * 8) = vv;
   }
-  wave_lds_fence();
-
   const int hh = lane >> 5, r32 = lane & 31;
+  const int q = qt * TQ + r32;
+  const bool live = q < n;
+  // this lane's query: Q~ / dO fragments (B operands), delta = dO . O, lse (per lane: query on the lane)
+  bf16x8 qf[2], df[2];
+  float delta = 0.f, lse2 = 0.f;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    qf[s] = live ? ld_row16(base + q * ld + h * HD + 16 * s + 8 * hh) : bf16x8{};
+    df[s] = live ? ld_row16(dout + ((long long)w * n + q) * C + h * HD + 16 * s + 8 * hh) : bf16x8{};
+    const bf16x8 of = live ? ld_row16(outp + ((long long)w * n + q) * C + h * HD + 16 * s + 8 * hh) : bf16x8{};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) delta += bf2f(of[j]) * bf2f(df[s][j]);
+  }
+  delta += __shfl_xor(delta, 32, 64);
+  if (live) lse2 = lse_g[((long long)w * nH + h) * NPAD + q];
+  __syncthreads();
+  if (qt * TQ >= n) return;   // (no barrier follows)
   const int pat = win_pat ? win_pat[w] : 0;
-  const float* bp = biasb + (long long)(pat * nH + h) * PH_ELEMS + lane * 16;
-  bf16* dsp = ds_out + ((long long)w * nH + h) * PH_ELEMS + lane * 16;
-  const float kscale = 1.0f / LOG2E;
-  const int nqt = (n + TQ - 1) / TQ;
-
-  f32x16 dq[NTILE];
+  const float* bp = biasf + (long long)(pat * nH + h) * PH_ELEMS + (long long)qt * NTILE * TILE_ELEMS;
+  f32x16 dqT = {};
+  const int nkt = (n + TQ - 1) / TQ;
+  for (int kt = 0; kt < nkt; ++kt) {
+    f32x16 st;   // S^T tile (rows = keys, query on the lane), forward bias layout [u][lane][4]
+    {
+      const float4* src = reinterpret_cast<const float4*>(bp + kt * TILE_ELEMS) + lane;
 #pragma unroll
-  for (int t = 0; t < NTILE; ++t) dq[t] = f32x16{};
-
-#pragma unroll
-  for (int kt = 0; kt < NTILE; ++kt) {
-    if (kt < nqt) {
-      const int key = kt * TQ + r32;
-      bf16x8 kf[2], vf[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 a = {}, b = {};
-        if (key < n) {
-          a = *reinterpret_cast<const bf16x8*>(L.k + key * HD + 16 * s + 8 * hh);   // staged K row
-          b = ld_row16(base + key * ld + 2 * C + h * HD + 16 * s + 8 * hh);
-        }
-        kf[s] = a;
-        vf[s] = b;
-      }
-      f32x16 dv = {}, dk = {};
-#pragma unroll
-      for (int qt = 0; qt < NTILE; ++qt) {
-        if (qt < nqt) {
-          // S tile: rows = queries, cols = keys
-          f32x16 sacc;
-          const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + kt) * TILE_ELEMS);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float4 b = src[u];
-            sacc[4 * u] = b.x; sacc[4 * u + 1] = b.y; sacc[4 * u + 2] = b.z; sacc[4 * u + 3] = b.w;
-          }
-          bf16x8 qa[2], da[2];
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            qa[s] = *reinterpret_cast<const bf16x8*>(L.q + (qt * TQ + r32) * HD + 16 * s + 8 * hh);
-            da[s] = *reinterpret_cast<const bf16x8*>(L.dout + (qt * TQ + r32) * HD + 16 * s + 8 * hh);
-          }
-          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[0], kf[0], sacc, 0, 0, 0);
-          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[1], kf[1], sacc, 0, 0, 0);
-          f32x16 dp = {};
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[0], vf[0], dp, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[1], vf[1], dp, 0, 0, 0);
-          // P and dS (natural-log scale)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int qi = qt * TQ + crow(r, hh);
-            const float p = __builtin_amdgcn_exp2f(sacc[r] - L.lse[qi]);
-            sacc[r] = p;
-            dp[r] = p * (dp[r] - L.delta[qi]);
-          }
-          // dV += P^T dO ; dK += dS^T Q~
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pack8(sacc, s), tr_read_perm(L.dout, qt * TQ + 16 * s, lane), dv, 0, 0, 0);
-            dk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pack8(dp, s), tr_read_perm(L.q, qt * TQ + 16 * s, lane), dk, 0, 0, 0);
-          }
-          // dS -> global scratch (bias gradient) and LDS transpose image T[key][query]
-          {
-            bf16x8 lo = pack8(dp, 0), hi = pack8(dp, 1);
-            bf16* o = dsp + (qt * NTILE + kt) * TILE_ELEMS;
-            *reinterpret_cast<bf16x8*>(o) = lo;
-            *reinterpret_cast<bf16x8*>(o + 8) = hi;
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              bf16x4 v;
-              v[0] = f2bf(dp[4 * rr]); v[1] = f2bf(dp[4 * rr + 1]); v[2] = f2bf(dp[4 * rr + 2]); v[3] = f2bf(dp[4 * rr + 3]);
-              *reinterpret_cast<bf16x4*>(L.t + r32 * TQ + 8 * rr + 4 * hh) = v;
-            }
-          }
-          wave_lds_fence();
-          // dQ[qt] += dS K : A = dS rows (from T, transposed read), B = K rows (transposed read)
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const bf16x8 a = tr_read_nat(L.t, 16 * s, lane);
-            const bf16x8 b = tr_read_nat(L.k, kt * TQ + 16 * s, lane);
-            dq[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, dq[qt], 0, 0, 0);
-          }
-          wave_lds_fence();
-        }
-      }
-      // write dK, dV rows (keys) of this tile: rows = crow(r,hh), col = d = r32
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kk = kt * TQ + crow(r, hh);
-        if (kk < n) {
-          bf16* row = dqkv + ((long long)w * n + kk) * ld + h * HD + r32;
-          row[C] = f2bf(dk[r] * kscale);
-          row[2 * C] = f2bf(dv[r]);
-        }
+      for (int u = 0; u < 4; ++u) {
+        const float4 b = src[64 * u];
+        st[4 * u] = b.x; st[4 * u + 1] = b.y; st[4 * u + 2] = b.z; st[4 * u + 3] = b.w;
       }
     }
-  }
+    f32x16 dpt = {};
 #pragma unroll
-  for (int qt = 0; qt < NTILE; ++qt) {
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 ka = *reinterpret_cast<const bf16x8*>(L.k + (kt * TQ + r32) * HD + 16 * s + 8 * hh);
+      const bf16x8 va = *reinterpret_cast<const bf16x8*>(L.v + (kt * TQ + r32) * HD + 16 * s + 8 * hh);
+      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], st, 0, 0, 0);
+      dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dpt, 0, 0, 0);
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int qi = qt * TQ + crow(r, hh);
-      if (qi < n) dqkv[((long long)w * n + qi) * ld + h * HD + r32] = f2bf(dq[qt][r] * scale);
+      const float p = __builtin_amdgcn_exp2f(st[r] - lse2);
+      dpt[r] = p * (dpt[r] - delta);   // dS^T
+    }
+    // dQ^T += K^T dS^T (K^T by transposed reads in the accumulator's permuted key order)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      dqT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(L.k, kt * TQ + 16 * s, lane), pack8(dpt, s), dqT, 0, 0, 0);
+  }
+  if (live) {
+    bf16* row = dqkv + ((long long)w * n + q) * ld + h * HD + 4 * hh;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 a;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = f2bf(dqT[4 * g + e] * scale);
+      *reinterpret_cast<bf16x4*>(row + 8 * g) = a;
     }
   }
 }
 
-// sum dS over windows (per head, per padded (q,k)) and scatter-add into the bias table gradient
-// Relative-position-bias gradient, two passes with no contended atomics:
-//  1. dbias_partial: each thread sums 8 consecutive per-lane-ordered dS elements (16-B loads) over
-//     the windows of one window chunk (grid.y) and stores the 8 partial sums (plain stores);
-//  2. dbias_scatter: one thread per (head, element) sums the chunk partials and adds the result to
-//     its table entry (one atomic per element, as many as the table has uses per window).
-constexpr int DB_CHUNKS = 64;
-
-__global__ void dbias_partial_kernel(const bf16* __restrict__ ds, int n_win, int nH, float* __restrict__ part,
-                                     int win_per_chunk) {
-  const long long e8 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  const long long per_chunk = (long long)nH * PH_ELEMS;
-  if (e8 >= per_chunk) return;
-  const int w0 = blockIdx.y * win_per_chunk, w1 = min(n_win, w0 + win_per_chunk);
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const bf16* p = ds + e8;
-  int w = w0;
-  for (; w + 2 <= w1; w += 2) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(p + w * per_chunk);
-    const bf16x8 c = *reinterpret_cast<const bf16x8*>(p + (w + 1) * per_chunk);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] += bf2f(a[i]) + bf2f(c[i]);
-  }
-  if (w < w1) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(p + w * per_chunk);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] += bf2f(a[i]);
-  }
-  float4* o = reinterpret_cast<float4*>(part + blockIdx.y * per_chunk + e8);
-  o[0] = make_float4(s[0], s[1], s[2], s[3]);
-  o[1] = make_float4(s[4], s[5], s[6], s[7]);
-}
-
-__global__ void dbias_scatter_kernel(const float* __restrict__ part, int chunks, int n, int nH,
-                                     const int64_t* __restrict__ index, int ld, float* __restrict__ tgrad) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long per_chunk = (long long)nH * PH_ELEMS;
-  if (e >= per_chunk) return;
-  const int h = e / PH_ELEMS, el = e % PH_ELEMS;
-  const int reg = el & 15, lane = (el >> 4) & 63, tile = el / TILE_ELEMS;
-  const int qt = tile / NTILE, kt = tile % NTILE;
-  const int qi = qt * TQ + crow(reg, lane >> 5), kj = kt * TQ + (lane & 31);
-  if (qi >= n || kj >= n) return;
-  float s = 0.f;
-  for (int c = 0; c < chunks; ++c) s += part[c * per_chunk + e];
-  atomicAdd(tgrad + index[(long long)qi * ld + kj] * nH + h, s);
-}
-
-// Deterministic, atomic-free variant of the scatter: (1) sum the chunk partials in place into
-// chunk 0 (coalesced float4), (2) one thread per (table row, head) gathers the elements that use
-// that row through a CSR built once per stage geometry (csr_off [n_bins+1], csr_el = element
-// positions in per-lane tile order, ascending within a row) and adds the sum to its gradient entry —
-// each entry has exactly one writer, so no atomics and no run-to-run variation.
+// Relative-position-bias gradient from the per-(group, head) dS partial sums of wattn_bwd_kv, no
+// atomics: (1) sum the group partials in place into group 0 (coalesced float4), (2) one wave per
+// table row gathers the (query, key) positions that use that row through a CSR built once per stage
+// geometry (csr_off [n_bins+1], csr_el = element positions in per-lane tile order, ascending within
+// a row) and adds the sum to its gradient entry — each entry has exactly one writer.
 __global__ void dbias_reduce_kernel(float* __restrict__ part, int chunks, long long per_chunk) {
   const long long e4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (e4 >= per_chunk) return;
@@ -774,7 +588,7 @@ __global__ void dbias_gather_kernel(const float* __restrict__ red, int nH, const
 extern "C" int64_t lrce_wattn_bias_elems(int n_pat, int nH) { return (int64_t)n_pat * nH * PH_ELEMS; }
 // dS scratch (bf16 units): the per-window dS images + the f32 chunk partials of the bias reduction
 extern "C" int64_t lrce_wattn_ds_elems(int n_win, int nH) {
-  return (int64_t)n_win * nH * PH_ELEMS + 2LL * DB_CHUNKS * nH * PH_ELEMS;
+  return 2LL * ((n_win + GDS - 1) / GDS) * nH * PH_ELEMS;   // f32 partials, counted in 16-bit units
 }
 
 extern "C" int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
@@ -785,23 +599,6 @@ extern "C" int lrce_wattn_bias_build(const float* table, const int64_t* index, i
   bias_build_kernel<<<(total + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(table, index, index_ld, n, nH, region,
                                                                                     n_pat, bias_fwd, bias_bwd);
   return lrce_check_launch("wattn_bias_build");
-}
-
-extern "C" int lrce_wattn_fwd(const uint16_t* qkv, const float* bias_fwd, const int32_t* win_pat, uint16_t* out, float* lse,
-                              int n_win, int n, int nH, void* stream) {
-  if (!qkv || !bias_fwd || !out || !lse) return lrce_fail(LRCE_E_ARG, "wattn_fwd: null pointer");
-  if (n <= 4 * TQ || n > NPAD) return lrce_fail(LRCE_E_ARG, "wattn_fwd: n=%d outside (128,160]", n);
-  if (n_win <= 0) return LRCE_OK;
-  static const bool v1 = getenv("LRCE_WATTN_V1") != nullptr;
-  if (v1) {
-    dim3 grid((unsigned)(((n_win + 3) / 4) * nH));
-    wattn_fwd_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const bf16*>(qkv), bias_fwd, win_pat,
-                                                                        reinterpret_cast<bf16*>(out), lse, n_win, n, nH);
-  } else {
-    wattn_fwd2_kernel<<<(unsigned)(n_win * nH), 320, 0, static_cast<hipStream_t>(stream)>>>(
-        reinterpret_cast<const bf16*>(qkv), bias_fwd, win_pat, reinterpret_cast<bf16*>(out), lse, n_win, n, nH);
-  }
-  return lrce_check_launch("wattn_fwd");
 }
 
 extern "C" int lrce_wattn_fwd_grouped(const uint16_t* qkv, const float* bias_fwd, const int32_t* win_list,
@@ -817,16 +614,22 @@ extern "C" int lrce_wattn_fwd_grouped(const uint16_t* qkv, const float* bias_fwd
 }
 
 extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                              const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv, uint16_t* ds_scratch, int n_win,
-                              int n, int nH, void* stream) {
-  if (!qkv || !out || !dout || !lse || !bias_bwd || !dqkv || !ds_scratch) return lrce_fail(LRCE_E_ARG, "wattn_bwd: null pointer");
+                              const float* bias_fwd, const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv,
+                              uint16_t* ds_scratch, int n_win, int n, int nH, void* stream) {
+  if (!qkv || !out || !dout || !lse || !bias_fwd || !bias_bwd || !dqkv || !ds_scratch)
+    return lrce_fail(LRCE_E_ARG, "wattn_bwd: null pointer");
   if (n <= 4 * TQ || n > NPAD) return lrce_fail(LRCE_E_ARG, "wattn_bwd: n=%d outside (128,160]", n);
   if (n_win <= 0) return LRCE_OK;
-  dim3 grid((unsigned)(((n_win + 1) / 2) * nH));
-  const float scale = 1.0f / sqrtf((float)HD);
-  wattn_bwd_kernel<<<grid, 128, 0, static_cast<hipStream_t>(stream)>>>(
-      reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const bf16*>(out), reinterpret_cast<const bf16*>(dout), lse, bias_bwd,
-      win_pat, reinterpret_cast<bf16*>(dqkv), reinterpret_cast<bf16*>(ds_scratch), n_win, n, nH, scale);
+  const unsigned grid = (unsigned)(n_win * nH);
+  const unsigned grid_kv = (unsigned)(((n_win + GDS - 1) / GDS) * nH);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bf16* q = reinterpret_cast<const bf16*>(qkv);
+  const bf16* o = reinterpret_cast<const bf16*>(out);
+  const bf16* g = reinterpret_cast<const bf16*>(dout);
+  bf16* d = reinterpret_cast<bf16*>(dqkv);
+  wattn_bwd_kv_kernel<<<grid_kv, BW * 64, 0, st>>>(q, o, g, lse, bias_bwd, win_pat, d, reinterpret_cast<float*>(ds_scratch), n_win,
+                                                  n, nH);
+  wattn_bwd_q_kernel<<<grid, BW * 64, 0, st>>>(q, o, g, lse, bias_fwd, win_pat, d, n_win, n, nH, 1.0f / sqrtf((float)HD));
   return lrce_check_launch("wattn_bwd");
 }
 
@@ -834,34 +637,11 @@ extern "C" int lrce_wattn_dbias_csr(const uint16_t* ds_scratch, int n_win, int n
                                     const int32_t* csr_el, int n_bins, float* table_grad, void* stream) {
   if (!ds_scratch || !csr_off || !csr_el || !table_grad) return lrce_fail(LRCE_E_ARG, "wattn_dbias_csr: null pointer");
   if (n_win <= 0 || nH <= 0 || n_bins <= 0) return lrce_fail(LRCE_E_ARG, "wattn_dbias_csr: n_win=%d nH=%d", n_win, nH);
-  const long long per_chunk = (long long)nH * PH_ELEMS;
-  const long long groups = (per_chunk / 8 + 255) / 256;
-  int chunks = (int)((2048 + groups - 1) / groups);
-  chunks = max(1, min(min(chunks, DB_CHUNKS), n_win));
-  const int per = (n_win + chunks - 1) / chunks;
-  chunks = (n_win + per - 1) / per;
-  const bf16* ds = reinterpret_cast<const bf16*>(ds_scratch);
-  float* part = reinterpret_cast<float*>(const_cast<bf16*>(ds) + (long long)n_win * per_chunk);
+  const long long per_group = (long long)nH * PH_ELEMS;
+  const int groups = (n_win + GDS - 1) / GDS;
+  float* part = reinterpret_cast<float*>(const_cast<uint16_t*>(ds_scratch));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  dbias_partial_kernel<<<dim3((unsigned)groups, chunks), 256, 0, st>>>(ds, n_win, nH, part, per);
-  if (chunks > 1) dbias_reduce_kernel<<<(unsigned)((per_chunk / 4 + 255) / 256), 256, 0, st>>>(part, chunks, per_chunk);
+  if (groups > 1) dbias_reduce_kernel<<<(unsigned)((per_group / 4 + 255) / 256), 256, 0, st>>>(part, groups, per_group);
   dbias_gather_kernel<<<(unsigned)((n_bins + 3) / 4), 256, 0, st>>>(part, nH, csr_off, csr_el, n_bins, table_grad);
   return lrce_check_launch("wattn_dbias_csr");
-}
-
-extern "C" int lrce_wattn_dbias(const uint16_t* ds_scratch, int n_win, int n, int nH, const int64_t* index, int index_ld,
-                                float* table_grad, void* stream) {
-  if (!ds_scratch || !index || !table_grad) return lrce_fail(LRCE_E_ARG, "wattn_dbias: null pointer");
-  const long long per_chunk = (long long)nH * PH_ELEMS;
-  const long long groups = (per_chunk / 8 + 255) / 256;
-  int chunks = (int)((2048 + groups - 1) / groups);   // fill the chip with (group, chunk) blocks
-  chunks = max(1, min(min(chunks, DB_CHUNKS), n_win));
-  const int per = (n_win + chunks - 1) / chunks;
-  chunks = (n_win + per - 1) / per;
-  const bf16* ds = reinterpret_cast<const bf16*>(ds_scratch);
-  float* part = reinterpret_cast<float*>(const_cast<bf16*>(ds) + (long long)n_win * per_chunk);
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  dbias_partial_kernel<<<dim3((unsigned)groups, chunks), 256, 0, st>>>(ds, n_win, nH, part, per);
-  dbias_scatter_kernel<<<(unsigned)((per_chunk + 255) / 256), 256, 0, st>>>(part, chunks, n, nH, index, index_ld, table_grad);
-  return lrce_check_launch("wattn_dbias");
 }

@@ -11,6 +11,7 @@ execution:
   (`win2sp`) fused into the LN1 gather and the proj-GEMM scatter epilogue — no copies;
 * the relative-position bias + shift mask (:171-179, 346-359) are pre-combined per mask pattern
   into accumulator-order tiles that the fused window-attention kernel starts its MFMA chain from;
+* the qkv Linear and the window attention are ONE kernel (csrc/window_fused.hip);
 * one autograd Function per block (forward 6 launches, backward 15) with gradients accumulated
   straight into the flat parameter store (lrce/flat.py).
 """
@@ -303,10 +304,17 @@ class _SwinBlockFn(torch.autograd.Function):
                            bias_f, bias_b)
         xw, m1, r1 = K.layernorm(x, blk.norm1.weight, blk.norm1.bias, 1e-5, in_map=wmap, rows=M)
         c = (C // nH) ** -0.5 * LOG2E
-        qkv = K.linear(xw, flat.w16(at.qkv.weight), at.qkv.bias, scale_cols=C, scale_val=c)
         o = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
         lse = torch.empty(geo.n_win, nH, 160, device=dev)
-        K.wattn_fwd_grouped(qkv, bias_f, geo.groups_shift if shifted else geo.groups, o, lse, geo.n_win, n, nH)
+        if nH % 4 == 0 and C % 64 == 0:
+            # QKV projection fused with the attention (csrc/window_fused.hip); qkv is still written
+            # for the backward
+            qkv = torch.empty(M, 3 * C, dtype=torch.bfloat16, device=dev)
+            K.wattn_qkv_fwd(xw, flat.w16(at.qkv.weight), at.qkv.bias, c, bias_f, win_pat, qkv, o, lse, geo.n_win, n,
+                            nH)
+        else:   # head counts the fused kernel's 4-head groups do not divide (not Swin-B)
+            qkv = K.linear(xw, flat.w16(at.qkv.weight), at.qkv.bias, scale_cols=C, scale_val=c)
+            K.wattn_fwd_grouped(qkv, bias_f, geo.groups_shift if shifted else geo.groups, o, lse, geo.n_win, n, nH)
         x_mid = torch.empty(M, C, device=dev)
         K.linear(o, flat.w16(at.proj.weight), at.proj.bias, out=x_mid, resid=x, c_map=wmap, row_scale=dp1,
                  rows_per_scale=geo.rows_per_clip)
@@ -317,7 +325,7 @@ class _SwinBlockFn(torch.autograd.Function):
         K.linear(g, flat.w16(blk.mlp.fc2.weight), blk.mlp.fc2.bias, out=out, resid=x_mid, row_scale=dp2,
                  rows_per_scale=geo.rows_per_clip)
         if any(t.requires_grad for t in (x,) + params):
-            ctx.save = (x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_b)
+            ctx.save = (x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_f, bias_b)
             ctx.blk, ctx.geo, ctx.flat, ctx.dp1, ctx.dp2 = blk, geo, flat, dp1, dp2
             ctx.wmap, ctx.win_pat = wmap, win_pat
             ctx.sp2win = geo.sp2win_shift if shifted else geo.sp2win
@@ -325,7 +333,7 @@ class _SwinBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_b = ctx.save
+        x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_f, bias_b = ctx.save
         blk, geo, flat, dp1, dp2, wmap = ctx.blk, ctx.geo, ctx.flat, ctx.dp1, ctx.dp2, ctx.wmap
         at = blk.attn
         C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
@@ -353,7 +361,7 @@ class _SwinBlockFn(torch.autograd.Function):
         del dmid16
         dqkv = torch.empty_like(qkv)
         ds = torch.empty(K.wattn_ds_elems(geo.n_win, nH), dtype=torch.bfloat16, device=dout.device)
-        K.wattn_bwd(qkv, o, do, lse, bias_b, ctx.win_pat, dqkv, ds, geo.n_win, n, nH)
+        K.wattn_bwd(qkv, o, do, lse, bias_f, bias_b, ctx.win_pat, dqkv, ds, geo.n_win, n, nH)
         del do, o
         gt = _g(flat, at.relative_position_bias_table)
         if gt is not None:

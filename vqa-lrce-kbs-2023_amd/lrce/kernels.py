@@ -293,13 +293,6 @@ def wattn_bias_build(table, index, n, nH, region, n_pat, bias_fwd, bias_bwd):
          ptr(bias_fwd), ptr(bias_bwd), stream_of(bias_fwd))
 
 
-def wattn_fwd(qkv, bias_fwd, win_pat, out, lse, n_win, n, nH):
-    # algorithmic work: QK^T + PV = 4 n^2 d per (window, head), d = 32
-    _timed("wattn_fwd", out, lambda: call("lrce_wattn_fwd", ptr(qkv), ptr(bias_fwd), ptr(win_pat), ptr(out), ptr(lse),
-                                           n_win, n, nH, stream_of(out)),
-           flops=4.0 * n * n * 32 * n_win * nH, nbytes=8.0 * n * 32 * n_win * nH)
-
-
 WATTN_GROUP = 4   # windows per workgroup of lrce_wattn_fwd_grouped
 
 
@@ -330,10 +323,25 @@ def wattn_fwd_grouped(qkv, bias_fwd, groups, out, lse, n_win, n, nH):
            flops=4.0 * n * n * 32 * n_win * nH, nbytes=8.0 * n * 32 * n_win * nH, key=(n_win, nH))
 
 
-def wattn_bwd(qkv, out, dout, lse, bias_bwd, win_pat, dqkv, ds, n_win, n, nH):
-    # algorithmic work: dV, dP, dQ, dK = 8 n^2 d per (window, head)
-    _timed("wattn_bwd", dqkv, lambda: call("lrce_wattn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(bias_bwd),
-                                            ptr(win_pat), ptr(dqkv), ptr(ds), n_win, n, nH, stream_of(dqkv)),
+def wattn_qkv_fwd(x, w_qkv, b_qkv, qscale, bias_fwd, win_pat, qkv, out, lse, n_win, n, nH):
+    """Fused QKV projection + window attention forward (csrc/window_fused.hip).  Algorithmic work per
+    launch: the QKV GEMM 2 * (n_win n) * C * 3C + attention 4 n^2 d per (window, head); bytes: x read,
+    W_qkv read, qkv + out written (bf16)."""
+    C = x.shape[-1]
+    M = n_win * n
+    _chk(x, BF16, "x"); _chk(w_qkv, BF16, "w_qkv"); _chk(qkv, BF16, "qkv"); _chk(out, BF16, "out")
+    _timed("wattn_qkv_fwd", out, lambda: call("lrce_wattn_qkv_fwd", ptr(x), ptr(w_qkv), ptr(b_qkv), float(qscale),
+                                               ptr(bias_fwd), ptr(win_pat), ptr(qkv), ptr(out), ptr(lse), n_win, n, nH,
+                                               stream_of(out)),
+           flops=2.0 * M * C * 3 * C + 4.0 * n * n * 32 * n_win * nH,
+           nbytes=2.0 * (M * C + 3 * C * C + M * 3 * C + M * C), key=(n_win, nH))
+
+
+def wattn_bwd(qkv, out, dout, lse, bias_fwd, bias_bwd, win_pat, dqkv, ds, n_win, n, nH):
+    # algorithmic work: dV, dP, dQ, dK = 8 n^2 d per (window, head) (the kernels recompute S, dP)
+    _timed("wattn_bwd", dqkv, lambda: call("lrce_wattn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(bias_fwd),
+                                            ptr(bias_bwd), ptr(win_pat), ptr(dqkv), ptr(ds), n_win, n, nH,
+                                            stream_of(dqkv)),
            flops=8.0 * n * n * 32 * n_win * nH, key=(n_win, nH))
 
 
@@ -355,10 +363,6 @@ def frames_resize(frames, frame_idx, out_h=224, out_w=224, out=None):
 
 def wattn_ds_elems(n_win, nH):
     return N.lib().lrce_wattn_ds_elems(n_win, nH)
-
-
-def wattn_dbias(ds, n_win, n, nH, index, table_grad):
-    call("lrce_wattn_dbias", ptr(ds), n_win, n, nH, ptr(index), index.shape[-1], ptr(table_grad), stream_of(table_grad))
 
 
 def wattn_dbias_csr(index, n, n_bins):
