@@ -340,7 +340,7 @@ def _roofline(timer):
     fl, by = timer.flops["wattn_qkv_fwd"], timer.bytes["wattn_qkv_fwd"]
     ai = fl / by
     mf, hf = tflops / MFMA_BF16_PEAK_TFLOPS, gbs / HBM_PEAK_GBS
-    attn_fl = sum(4.0 * 147 * 147 * 32 * nw * nh * len(ev) for (name, (nw, nh)), (ev, _) in timer.detail.items()
+    attn_fl = sum(4.0 * 147 * 147 * 32 * key[0] * key[1] * len(ev) for (name, key), (ev, _) in timer.detail.items()
                   if name == "wattn_qkv_fwd") if timer.detail is not None else None
     total_ms = timer.total_ms("wattn_qkv_fwd")
     roof = {"kernel": "lrce_wattn_qkv_fwd (qkv Linear + window attention fused)",

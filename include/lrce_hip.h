@@ -144,8 +144,8 @@ int64_t lrce_layernorm_bwd_workspace(int rows, int cols);
  * bias tiles are built once per layer by lrce_wattn_bias_build from the f32 table
  * (relative_position_bias_table) and the int64 relative_position_index (ld = index_ld), with the
  * shift mask of each window pattern given as per-token region ids region[n_pat][n] (-100 between
- * different regions, video_swin_ori.py:346-359); bias_fwd holds the S^T-oriented tiles (forward and
- * the dQ backward kernel), bias_bwd the S-oriented ones (the dK / dV backward kernel). */
+ * different regions, video_swin_ori.py:346-359); bias_fwd holds the S^T-oriented tiles (forward),
+ * bias_bwd the S-oriented ones (backward). */
 int64_t lrce_wattn_bias_elems(int n_pat, int nH);
 int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
                           const int32_t* region, int n_pat, float* bias_fwd, float* bias_bwd, void* stream);
@@ -163,20 +163,22 @@ int lrce_wattn_fwd_grouped(const uint16_t* qkv, const float* bias_fwd, const int
 int lrce_wattn_qkv_fwd(const uint16_t* x, const uint16_t* w_qkv, const float* b_qkv, float qscale,
                        const float* bias_fwd, const int32_t* win_pat, uint16_t* qkv, uint16_t* out, float* lse,
                        int n_win, int n, int nH, void* stream);
-/* dqkv: bf16 [n_win*n][3C] (d/dq, d/dk, d/dv w.r.t. the UNSCALED q).  win_pat int32 [n_win] (the
- * window's mask pattern, NULL = 0).  ds_scratch: bf16, lrce_wattn_ds_elems(n_win, nH) elements (dS per
- * (window, head) for the bias-table gradient, then lrce_wattn_dbias_csr). */
-int64_t lrce_wattn_ds_elems(int n_win, int nH);
+/* Backward (one kernel): dqkv bf16 [n_win*n][3C] (d/dq, d/dk, d/dv w.r.t. the UNSCALED q).  win_pat
+ * int32 [n_win] (the window's mask pattern, NULL = 0).  The window is wd x wh x ww tokens (n = wd*wh*ww,
+ * token order (t, h, w)); dbias_part: f32, lrce_wattn_dbias_part_elems(n_win, nH, n_bins) elements with
+ * n_bins = (2wd-1)(2wh-1)(2ww-1) <= 1024: per (window, head) the bias-table gradient binned by relative
+ * position, reduced by lrce_wattn_dbias (NULL: no bias-table gradient, e.g. a frozen table). */
+int64_t lrce_wattn_dbias_part_elems(int n_win, int nH, int n_bins);
 int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                   const float* bias_fwd, const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv,
-                   uint16_t* ds_scratch, int n_win, int n, int nH, void* stream);
-/* Bias-table gradient (relative_position_bias_table, f32 [table_rows][nH], accumulated):
- * csr_off int32 [n_bins+1] / csr_el int32 list, per table row, the positions (per-lane tile order,
- * 25 tiles x 1024) of the (query, key) pairs whose relative_position_index is that row (built once per
- * stage geometry: lrce.kernels.wattn_dbias_csr).  Deterministic: every table entry is written by one
- * thread, no atomics. */
-int lrce_wattn_dbias_csr(const uint16_t* ds_scratch, int n_win, int nH, const int32_t* csr_off, const int32_t* csr_el,
-                         int n_bins, float* table_grad, void* stream);
+                   const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv, float* dbias_part, int n_win,
+                   int n, int nH, int wh, int ww, void* stream);
+/* Bias-table gradient (relative_position_bias_table, f32 [table_rows][nH], accumulated) from
+ * lrce_wattn_bwd's bins: bin_row int32 [n_bins] = the table row of each relative-position bin (the
+ * relative_position_index entry of any (query, key) pair in that bin; -1 = unused), built once per stage
+ * geometry by lrce.kernels.wattn_bin_rows.  Deterministic: windows summed in a fixed order, every table
+ * entry written by one thread, no atomics. */
+int lrce_wattn_dbias(float* dbias_part, int n_win, int nH, int n_bins, const int32_t* bin_row, float* table_grad,
+                     void* stream);
 
 /* ---------------------------------------------------------------- small multi-head attention
  * Masked SDPA, head_dim 64, for BERT self-attention (text.py:12-17 -> HF BertSelfAttention, L<=64)

@@ -50,23 +50,27 @@ def test_kernels_refuse_cpu_tensors():
         kernels.linear(x, x)
 
 
-def test_dbias_csr_inverts_relative_position_index():
-    """The bias-gradient CSR (host-built) lists every valid (query, key) pair of the padded 160x160
-    per-lane tile layout exactly once, under its relative_position_index row, ascending per row."""
+def test_bias_gradient_bins_map_to_relative_position_index():
+    """The window backward bins (query i, key j) by code(i) - code(j) + off; wattn_bin_rows maps every
+    bin to the relative_position_index row all its pairs share (video_swin_ori.py:133-148): every row
+    the index uses is hit by exactly one bin, and each bin's pairs agree with the index."""
     import torch
     from lrce import kernels as K
     from lrce.feature_extractor.video_swin import relative_position_index
-    n = 147
     index = relative_position_index((8, 7, 7))
-    off, el, n_bins = K.wattn_dbias_csr(index, n, 2535)
-    assert n_bins == 2535 and off.shape == (2536,) and int(off[-1]) == n * n == el.numel()
-    assert el.unique().numel() == el.numel()
-    reg, lane, tile = el & 15, (el >> 4) & 63, el // 1024
-    qi = (tile // 5) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
-    kj = (tile % 5) * 32 + (lane & 31)
-    assert int(qi.max()) < n and int(kj.max()) < n
-    rows = torch.repeat_interleave(torch.arange(2535), (off[1:] - off[:-1]).long())
-    assert torch.equal(index[qi.long(), kj.long()], rows)
-    for b in range(0, 2535, 97):
-        seg = el[off[b]:off[b + 1]]
-        assert torch.equal(seg, seg.sort().values)
+    for win in ((3, 7, 7), (2, 7, 7), (8, 7, 7)):
+        wd, wh, ww = win
+        n = wd * wh * ww
+        rows = K.wattn_bin_rows(index, win)
+        assert rows.dtype == torch.int32 and rows.numel() == K.wattn_n_bins(win)
+        used = index[:n, :n].unique()
+        assert torch.equal(rows[rows >= 0].long().sort().values, used)
+        x = torch.arange(n)
+        code = ((x // (wh * ww)) * (2 * wh - 1) + (x // ww) % wh) * (2 * ww - 1) + x % ww
+        off = ((wd - 1) * (2 * wh - 1) + (wh - 1)) * (2 * ww - 1) + (ww - 1)
+        b = code[:, None] - code[None, :] + off
+        assert torch.equal(rows.long()[b], index[:n, :n])
+    bad = index.clone()
+    bad[0, 1], bad[1, 2] = bad[1, 2], bad[0, 1] + 1
+    with pytest.raises(ValueError):
+        K.wattn_bin_rows(bad, (3, 7, 7))

@@ -398,10 +398,17 @@ def test_window_attention_fwd_bwd(nH, n_win):
     dout = bf(torch.randn(n_win * n, C, device=dev))
     ref.backward(dout.float())
     dqkv = torch.full((n_win * n, 3 * C), float("nan"), device=dev, dtype=torch.bfloat16)
-    ds = torch.empty(k.wattn_ds_elems(n_win, nH), device=dev, dtype=torch.bfloat16)
-    k.wattn_bwd(qkv, out, dout, lse, bf_, bb_, win_pat, dqkv, ds, n_win, n, nH)
-    tg = torch.zeros(2535, nH, device=dev)   # atomic-free CSR gather of the window-summed dS
-    k.wattn_dbias_gather(ds, n_win, nH, k.wattn_dbias_csr(index, n, 2535), tg)
+    win = (3, 7, 7)
+    dbp = torch.full((k.wattn_dbias_part_elems(n_win, nH, win),), float("nan"), device=dev)
+    k.wattn_bwd(qkv, out, dout, lse, bb_, win_pat, dqkv, dbp, n_win, n, nH, win)
+    tg = torch.zeros(2535, nH, device=dev)   # relative-position bins, summed over windows, -> table rows
+    k.wattn_dbias(dbp, n_win, nH, win, k.wattn_bin_rows(index, win), tg)
+    # deterministic: a second run gives the same bits
+    dqkv2 = torch.empty_like(dqkv)
+    tg2 = torch.zeros_like(tg)
+    k.wattn_bwd(qkv, out, dout, lse, bb_, win_pat, dqkv2, dbp, n_win, n, nH, win)
+    k.wattn_dbias(dbp, n_win, nH, win, k.wattn_bin_rows(index, win), tg2)
+    assert torch.equal(dqkv, dqkv2) and torch.equal(tg, tg2)
     d = dqkv.float().view(n_win, n, 3, nH, hd).permute(2, 0, 3, 1, 4)
     assert not torch.isnan(d).any()
     for got, want in ((d[0], q.grad), (d[1], kk.grad), (d[2], v.grad), (tg, tab.grad)):

@@ -12,7 +12,7 @@
 // accumulator order, so the MFMA chain starts from the bias: no VALU for scale/bias/mask.  q is
 // pre-scaled by head_dim^-0.5 * log2(e) in the QKV GEMM epilogue, so p = exp2(s - max).
 //
-// Backward: two kernels (dK/dV by key tile, dQ by query tile) described above wattn_bwd_kv_kernel.
+// Backward: one kernel per (window, head) with the bias-table gradient binned in LDS (wattn_bwd_kernel).
 #include <cstdlib>
 #include <type_traits>
 
@@ -46,6 +46,24 @@ __device__ __forceinline__ bf16x8 tr_read_perm(const bf16* img, int r_base, int 
   for (int h2 = 0; h2 < 2; ++h2) {
     const int row = r_base + 8 * h2 + 4 * hh + q;
     const LRCE_LDS s16x4* src = (const LRCE_LDS s16x4*)(img + row * 32 + cb + 4 * p);
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<LRCE_LDS s16x4*>(src));
+    bf16x4 b = *reinterpret_cast<bf16x4*>(&v);
+    out[4 * h2 + 0] = b[0]; out[4 * h2 + 1] = b[1]; out[4 * h2 + 2] = b[2]; out[4 * h2 + 3] = b[3];
+  }
+  return out;
+}
+// tr_read_perm of a 32 x 32 tile stored with its 8-B chunks XOR-swizzled by (row >> 2) & 7 (each
+// lane's 8-B load is the same data, so the transposed result is unchanged; the swizzle spreads the
+// producer's row-strided stores over all banks)
+__device__ __forceinline__ int swz8(int row, int chunk) { return row * 32 + 4 * (chunk ^ ((row >> 2) & 7)); }
+__device__ __forceinline__ bf16x8 tr_read_perm_swz(const bf16* img, int r_base, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int hh = g >> 1, cb = 4 * (g & 1);
+  bf16x8 out;
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    const int row = r_base + 8 * h2 + 4 * hh + q;
+    const LRCE_LDS s16x4* src = (const LRCE_LDS s16x4*)(img + swz8(row, cb + p));
     s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<LRCE_LDS s16x4*>(src));
     bf16x4 b = *reinterpret_cast<bf16x4*>(&v);
     out[4 * h2 + 0] = b[0]; out[4 * h2 + 1] = b[1]; out[4 * h2 + 2] = b[2]; out[4 * h2 + 3] = b[3];
@@ -280,315 +298,239 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restri
 }
 
 // ------------------------------------------------------------------------------ backward
-// Two kernels, one workgroup per (window, head), five waves each (one per 32-row tile), no
-// cross-wave reduction and no LDS transpose (FlashAttention-2 split, P and dP recomputed in each):
-//  * wattn_bwd_kv: wave kt owns key tile kt and sweeps the query tiles.  S = Q K^T + bias (rows =
-//    queries, key on the lane), P = exp2(S - lse), dS = P (dP - delta); the transposed products
-//    dV^T = dO^T P and dK^T = Q~^T dS take P / dS straight from the accumulators as B operands and
-//    dO / Q~ by transposed LDS reads, so the results have the key on the lane and 4 consecutive head
-//    dims per register group: 8-B vector stores of whole row pieces.  dS (bf16) goes to the
-//    bias-table gradient scratch in the tile order lrce_wattn_dbias_csr reads.
-//  * wattn_bwd_q: wave qt owns query tile qt and sweeps the key tiles in the forward's orientation
-//    S^T = K Q~^T + bias (query on the lane, so lse / delta are per-lane registers), dQ^T = K^T dS^T
-//    with dS^T from the accumulators and K^T by transposed reads of the staged K image.
-// P / dP are recomputed by both (7 products per tile instead of 5); in exchange every wave runs an
-// independent chain and a CU holds ~15 waves (21 KB of LDS per workgroup) to hide its latency.
-constexpr int BW = 5;   // waves per backward workgroup (= tiles of 32 rows)
-constexpr int GDS = 8;  // windows per dK/dV workgroup: their dS is summed in registers for the bias gradient
+// One workgroup per (window, head), five waves; wave t owns key tile t (dK, dV) AND query tile t (dQ).
+// Step s = 0..4: wave t computes the tile (qt = t+s mod 5, kt = t) once, in the dK/dV orientation
+//   S = Q~ K^T + bias (rows = queries, key on the lane), dP = dO V^T, P = exp2(S - lse),
+//   dS = P (dP - delta);  dV^T += dO^T P, dK^T += Q~^T dS  (P / dS straight from the accumulators as
+//   B operands, dO / Q~ by transposed LDS reads: results have the key on the lane -> 8-B stores).
+// dQ needs the same dS transposed: each wave parks its dS tile (bf16, key-major [key][query]) in an
+// LDS slot, one barrier, and wave t reads the tile (t, t-s mod 5) that wave t-s wrote this step as the
+// B operand of dQ^T += K^T dS^T (both operands by ds_read_tr16 in the accumulator's permuted key
+// order).  Slots are double-buffered by step parity: one barrier per step, dQ summed in a fixed order.
+// So every product is computed once (S, dP, dV, dK, dQ: 10 MFMAs per tile) and every operand byte is
+// read from HBM once per (window, head).
+// Relative-position-bias gradient: the table row of (query i, key j) is a linear function of the
+// token codes, code(i) - code(j) + off (video_swin_ori.py:133-148 with window (wd, wh, ww)), so dS is
+// binned in LDS by that difference and each (window, head) writes n_bins floats (3.4 KB at 3x7x7)
+// instead of its 160^2 dS image.  The bins are 2^-40 fixed-point int64 (ds_add_u64): integer adds
+// make the sum independent of wave timing, and measured on gfx950 (tools/lds_atomic_bench.hip) an LDS
+// u64 add costs ~9 cycles per wave instruction against ~230 for ds_add_f32.  lrce_wattn_dbias sums
+// the windows in a fixed order and scatters bins to table rows.
+constexpr int BW = 5;        // waves per backward workgroup (= tiles of 32 rows)
+constexpr int NBMAX = 1024;  // relative-position bins per head held in LDS
+constexpr int WCH = 32;      // window chunks of the deterministic bias-gradient reduction
 
-struct BwdKVLds {
+struct BwdLds {
   bf16 q[NPAD * HD];
   bf16 dout[NPAD * HD];
-  float lse[NPAD];
-  float delta[NPAD];
-};
-
-// Workgroup = (group of GDS consecutive windows, head), windows in sequence.  The bias-table gradient
-// needs only sum_w dS_w per (query, key) position (the mask is constant), so each wave keeps its key
-// tile's dS summed over the group's windows in f32 registers and writes ONE partial image per
-// (group, head) — instead of a bf16 dS image per (window, head) (2 B x 160^2 each: 3 GB per training
-// step at bs 10).  lrce_wattn_dbias_csr then sums the group partials and gathers them per table row.
-__global__ void __launch_bounds__(BW * 64, 2) wattn_bwd_kv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
-                                                                 const bf16* __restrict__ dout, const float* __restrict__ lse_g,
-                                                                 const float* __restrict__ biasb, const int* __restrict__ win_pat,
-                                                                 bf16* __restrict__ dqkv, float* __restrict__ ds_part, int n_win,
-                                                                 int n, int nH) {
-  __shared__ __attribute__((aligned(16))) BwdKVLds L;
-  const int lane = threadIdx.x & 63, kt = threadIdx.x >> 6;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);   // a group's heads on one XCD (shared qkv / dO lines)
-  const int h = lin % nH, grp = lin / nH;
-  const int C = nH * HD;
-  const long long ld = 3LL * C;
-  const int hh = lane >> 5, r32 = lane & 31;
-  const int key = kt * TQ + r32;
-  const bool kt_live = kt * TQ < n;
-  const int nqt = (n + TQ - 1) / TQ;
-  f32x16 dsum[NTILE];
-#pragma unroll
-  for (int t = 0; t < NTILE; ++t) dsum[t] = f32x16{};
-  const int w_end = min(n_win, (grp + 1) * GDS);
-  for (int w = grp * GDS; w < w_end; ++w) {
-    const bf16* base = qkv + (long long)w * n * ld;
-    const bf16* obase = outp + (long long)w * n * C + h * HD;
-    const bf16* dobase = dout + (long long)w * n * C + h * HD;
-    __syncthreads();   // every wave is done with the previous window's images
-    // Q~ and dO images [160][32] (rows >= n zero): 640 16-B chunks each over 320 threads
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int c = threadIdx.x + BW * 64 * t;
-      const int row = c >> 2, part = c & 3;
-      uint4 qv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
-      if (row < n) {
-        qv = *reinterpret_cast<const uint4*>(base + row * ld + h * HD + part * 8);
-        dv = *reinterpret_cast<const uint4*>(dobase + (long long)row * C + part * 8);
-      }
-      *reinterpret_cast<uint4*>(L.q + row * HD + part * 8) = qv;
-      *reinterpret_cast<uint4*>(L.dout + row * HD + part * 8) = dv;
-    }
-    // delta[q] = dO[q] . O[q] and lse[q] (0 past n: padded queries then contribute nothing)
-    if (threadIdx.x < NPAD) {
-      const int q = threadIdx.x;
-      float d = 0.f, l = 0.f;
-      if (q < n) {
-#pragma unroll
-        for (int part = 0; part < 4; ++part) {
-          const bf16x8 a = ld_row16(obase + (long long)q * C + part * 8);
-          const bf16x8 b = ld_row16(dobase + (long long)q * C + part * 8);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
-        }
-        l = lse_g[((long long)w * nH + h) * NPAD + q];
-      }
-      L.delta[q] = d;
-      L.lse[q] = l;
-    }
-    bf16x8 kf[2], vf[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      kf[s] = key < n ? ld_row16(base + key * ld + C + h * HD + 16 * s + 8 * hh) : bf16x8{};
-      vf[s] = key < n ? ld_row16(base + key * ld + 2 * C + h * HD + 16 * s + 8 * hh) : bf16x8{};
-    }
-    __syncthreads();
-    if (!kt_live) continue;
-    const int pat = win_pat ? win_pat[w] : 0;
-    const float* bp = biasb + (long long)(pat * nH + h) * PH_ELEMS + lane * 16;
-    f32x16 dkT = {}, dvT = {};
-#pragma unroll
-    for (int qt = 0; qt < NTILE; ++qt) {
-      if (qt >= nqt) break;
-      f32x16 sacc;
-      {
-        const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + kt) * TILE_ELEMS);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float4 b = src[u];
-          sacc[4 * u] = b.x; sacc[4 * u + 1] = b.y; sacc[4 * u + 2] = b.z; sacc[4 * u + 3] = b.w;
-        }
-      }
-      f32x16 dp = {};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(L.q + (qt * TQ + r32) * HD + 16 * s + 8 * hh);
-        const bf16x8 da = *reinterpret_cast<const bf16x8*>(L.dout + (qt * TQ + r32) * HD + 16 * s + 8 * hh);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dp, 0, 0, 0);
-      }
-      // P and dS (natural-log scale); rows = queries crow(r, hh), key on the lane
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = qt * TQ + crow(r, hh);
-        const float p = __builtin_amdgcn_exp2f(sacc[r] - L.lse[qi]);
-        sacc[r] = p;
-        dp[r] = p * (dp[r] - L.delta[qi]);
-      }
-      dsum[qt] += dp;
-      // dV^T += dO^T P ; dK^T += Q~^T dS  (the accumulators as B operands, permuted k order)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        dvT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(L.dout, qt * TQ + 16 * s, lane), pack8(sacc, s), dvT, 0, 0, 0);
-        dkT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(L.q, qt * TQ + 16 * s, lane), pack8(dp, s), dkT, 0, 0, 0);
-      }
-    }
-    // dK^T / dV^T: rows = head dims crow(r, hh), key on the lane -> 4 x 8-B stores per row piece
-    if (key < n) {
-      const float kscale = 1.0f / LOG2E;   // q~ = q d^-1/2 log2(e): dK = dS^T q d^-1/2 = dS^T q~ / log2(e)
-      bf16* row = dqkv + ((long long)w * n + key) * ld + h * HD + 4 * hh;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 a, b;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          a[e] = f2bf(dkT[4 * g + e] * kscale);
-          b[e] = f2bf(dvT[4 * g + e]);
-        }
-        *reinterpret_cast<bf16x4*>(row + C + 8 * g) = a;
-        *reinterpret_cast<bf16x4*>(row + 2 * C + 8 * g) = b;
-      }
-    }
-  }
-  if (!kt_live) return;
-  // this wave's (qt, kt) tiles of the group's dS sum, f32, in the per-lane tile order of bias_bwd
-  float* dst = ds_part + ((long long)grp * nH + h) * PH_ELEMS + lane * 16;
-#pragma unroll
-  for (int qt = 0; qt < NTILE; ++qt) {
-    float4* o = reinterpret_cast<float4*>(dst + (qt * NTILE + kt) * TILE_ELEMS);
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      o[u] = make_float4(dsum[qt][4 * u], dsum[qt][4 * u + 1], dsum[qt][4 * u + 2], dsum[qt][4 * u + 3]);
-  }
-}
-
-struct BwdQLds {
   bf16 k[NPAD * HD];
-  bf16 v[NPAD * HD];
+  bf16 ds[2][BW][TQ * TQ];
+  unsigned long long bins[NBMAX];   // 2^-40 fixed point
+  float4 qinfo[NPAD];   // per query: lse, delta, token code (as bits), -
 };
 
-__global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_q_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
-                                                                const bf16* __restrict__ dout, const float* __restrict__ lse_g,
-                                                                const float* __restrict__ biasf, const int* __restrict__ win_pat,
-                                                                bf16* __restrict__ dqkv, int n_win, int n, int nH, float scale) {
-  __shared__ __attribute__((aligned(16))) BwdQLds L;
-  const int lane = threadIdx.x & 63, qt = threadIdx.x >> 6;
+__global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
+                                                              const bf16* __restrict__ dout, const float* __restrict__ lse_g,
+                                                              const float* __restrict__ biasb, const int* __restrict__ win_pat,
+                                                              bf16* __restrict__ dqkv, float* __restrict__ dbias_part, int n_win,
+                                                              int n, int nH, int wh, int ww, int nb, int boff, float qscale) {
+  __shared__ __attribute__((aligned(16))) BwdLds L;
+  const int lane = threadIdx.x & 63, t = threadIdx.x >> 6;
+  // logical order (head pair, window, head of the pair): the two heads sharing 128-B qkv / dO lines
+  // run next to each other and one XCD's contiguous range covers few heads (their bias tiles stay in
+  // that XCD's L2)
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int h = lin % nH, w = lin / nH;
+  const int hp = (nH & 1) ? 1 : 2;
+  const int h = (lin / hp / n_win) * hp + lin % hp;
+  const int w = (lin / hp) % n_win;
   const int C = nH * HD;
   const long long ld = 3LL * C;
   const bf16* base = qkv + (long long)w * n * ld;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int c = threadIdx.x + BW * 64 * t;
-    const int row = c >> 2, part = c & 3;
-    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-    if (row < n) {
-      kv = *reinterpret_cast<const uint4*>(base + row * ld + C + h * HD + part * 8);
-      vv = *reinterpret_cast<const uint4*>(base + row * ld + 2 * C + h * HD + part * 8);
-    }
-    *reinterpret_cast<uint4*>(L.k + row * HD + part * 8) = kv;
-    *reinterpret_cast<uint4*>(L.v + row * HD + part * 8) = vv;
-  }
+  const bf16* obase = outp + (long long)w * n * C + h * HD;
+  const bf16* dobase = dout + (long long)w * n * C + h * HD;
   const int hh = lane >> 5, r32 = lane & 31;
-  const int q = qt * TQ + r32;
-  const bool live = q < n;
-  // this lane's query: Q~ / dO fragments (B operands), delta = dO . O, lse (per lane: query on the lane)
-  bf16x8 qf[2], df[2];
-  float delta = 0.f, lse2 = 0.f;
+  const int key = t * TQ + r32;
+  // Q~, K and dO images [160][32] (rows >= n zero): 3 x 640 16-B chunks over 320 threads
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    qf[s] = live ? ld_row16(base + q * ld + h * HD + 16 * s + 8 * hh) : bf16x8{};
-    df[s] = live ? ld_row16(dout + ((long long)w * n + q) * C + h * HD + 16 * s + 8 * hh) : bf16x8{};
-    const bf16x8 of = live ? ld_row16(outp + ((long long)w * n + q) * C + h * HD + 16 * s + 8 * hh) : bf16x8{};
-#pragma unroll
-    for (int j = 0; j < 8; ++j) delta += bf2f(of[j]) * bf2f(df[s][j]);
+  for (int i = 0; i < 2; ++i) {
+    const int c = threadIdx.x + BW * 64 * i;
+    const int row = c >> 2, part = c & 3;
+    uint4 qv = make_uint4(0, 0, 0, 0), kv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
+    if (row < n) {
+      qv = *reinterpret_cast<const uint4*>(base + row * ld + h * HD + part * 8);
+      kv = *reinterpret_cast<const uint4*>(base + row * ld + C + h * HD + part * 8);
+      dv = *reinterpret_cast<const uint4*>(dobase + (long long)row * C + part * 8);
+    }
+    *reinterpret_cast<uint4*>(L.q + row * HD + part * 8) = qv;
+    *reinterpret_cast<uint4*>(L.k + row * HD + part * 8) = kv;
+    *reinterpret_cast<uint4*>(L.dout + row * HD + part * 8) = dv;
   }
-  delta += __shfl_xor(delta, 32, 64);
-  if (live) lse2 = lse_g[((long long)w * nH + h) * NPAD + q];
+  // V fragments of this wave's key tile (B operand of dP = dO V^T), straight to registers
+  bf16x8 vf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) vf[s] = key < n ? ld_row16(base + key * ld + 2 * C + h * HD + 16 * s + 8 * hh) : bf16x8{};
+  // delta[q] = dO[q] . O[q], lse[q] (0 past n: padded queries contribute nothing), token codes
+  if (threadIdx.x < NPAD) {
+    const int q = threadIdx.x;
+    float d = 0.f, l = 0.f;
+    int code = 0;
+    if (q < n) {
+#pragma unroll
+      for (int part = 0; part < 4; ++part) {
+        const bf16x8 a = ld_row16(obase + (long long)q * C + part * 8);
+        const bf16x8 b = ld_row16(dobase + (long long)q * C + part * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
+      }
+      l = lse_g[((long long)w * nH + h) * NPAD + q];
+      code = ((q / (wh * ww)) * (2 * wh - 1) + (q / ww) % wh) * (2 * ww - 1) + q % ww;
+    }
+    L.qinfo[q] = make_float4(l, d, __int_as_float(code), 0.f);
+  }
+  for (int i = threadIdx.x; i < NBMAX; i += BW * 64) L.bins[i] = 0ull;
   __syncthreads();
-  if (qt * TQ >= n) return;   // (no barrier follows)
+  bf16x8 kf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) kf[s] = *reinterpret_cast<const bf16x8*>(L.k + key * HD + 16 * s + 8 * hh);
   const int pat = win_pat ? win_pat[w] : 0;
-  const float* bp = biasf + (long long)(pat * nH + h) * PH_ELEMS + (long long)qt * NTILE * TILE_ELEMS;
-  f32x16 dqT = {};
-  const int nkt = (n + TQ - 1) / TQ;
-  for (int kt = 0; kt < nkt; ++kt) {
-    f32x16 st;   // S^T tile (rows = keys, query on the lane), forward bias layout [u][lane][4]
+  const float* bp = biasb + (long long)(pat * nH + h) * PH_ELEMS + lane * 16;
+  const bool key_live = key < n;
+  const int kbin = boff - (key_live ? __float_as_int(L.qinfo[key].z) : 0);
+  const bool want_bins = dbias_part != nullptr;
+  f32x16 dkT = {}, dvT = {}, dqT = {};
+  for (int s = 0; s < NTILE; ++s) {
+    const int qt = t + s < NTILE ? t + s : t + s - NTILE;
+    f32x16 sacc;
     {
-      const float4* src = reinterpret_cast<const float4*>(bp + kt * TILE_ELEMS) + lane;
+      const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + t) * TILE_ELEMS);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float4 b = src[64 * u];
-        st[4 * u] = b.x; st[4 * u + 1] = b.y; st[4 * u + 2] = b.z; st[4 * u + 3] = b.w;
+        const float4 b = src[u];
+        sacc[4 * u] = b.x; sacc[4 * u + 1] = b.y; sacc[4 * u + 2] = b.z; sacc[4 * u + 3] = b.w;
       }
     }
-    f32x16 dpt = {};
+    f32x16 dp = {};
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 ka = *reinterpret_cast<const bf16x8*>(L.k + (kt * TQ + r32) * HD + 16 * s + 8 * hh);
-      const bf16x8 va = *reinterpret_cast<const bf16x8*>(L.v + (kt * TQ + r32) * HD + 16 * s + 8 * hh);
-      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], st, 0, 0, 0);
-      dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dpt, 0, 0, 0);
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 qa = *reinterpret_cast<const bf16x8*>(L.q + (qt * TQ + r32) * HD + 16 * s2 + 8 * hh);
+      const bf16x8 da = *reinterpret_cast<const bf16x8*>(L.dout + (qt * TQ + r32) * HD + 16 * s2 + 8 * hh);
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s2], sacc, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s2], dp, 0, 0, 0);
     }
+    // P and dS (natural-log scale); rows = queries crow(r, hh), key on the lane
+    float4 qi4[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) qi4[r] = L.qinfo[qt * TQ + crow(r, hh)];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(st[r] - lse2);
-      dpt[r] = p * (dpt[r] - delta);   // dS^T
+      const float p = __builtin_amdgcn_exp2f(sacc[r] - qi4[r].x);
+      sacc[r] = p;
+      dp[r] = p * (dp[r] - qi4[r].y);
     }
-    // dQ^T += K^T dS^T (K^T by transposed reads in the accumulator's permuted key order)
+    // bias-table gradient: no predicates needed: dS is exactly 0 for padded queries (zero dO rows,
+    // delta 0) and padded keys (P = 0), and their bins (code 0) stay inside [0, n_bins)
+    if (want_bins) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-      dqT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(L.k, kt * TQ + 16 * s, lane), pack8(dpt, s), dqT, 0, 0, 0);
+      for (int r = 0; r < 16; ++r) {
+        // round(dS * 2^40) to int64: one f64 fma onto 1.5 * 2^52 leaves the integer in the low
+        // mantissa bits (exact for |dS| < 2^11)
+        const double m = __builtin_fma((double)dp[r], 0x1p40, 0x1.8p52);
+        const unsigned long long v =
+            (unsigned long long)(__double_as_longlong(m) - __double_as_longlong(0x1.8p52));
+        atomicAdd(&L.bins[__float_as_int(qi4[r].z) + kbin], v);
+      }
+    }
+    // dV^T += dO^T P ; dK^T += Q~^T dS  (the accumulators as B operands, permuted k order)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      dvT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(L.dout, qt * TQ + 16 * s2, lane), pack8(sacc, s2), dvT, 0, 0, 0);
+      dkT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(L.q, qt * TQ + 16 * s2, lane), pack8(dp, s2), dkT, 0, 0, 0);
+    }
+    // park dS key-major: slot[key][query] (8-B chunks swizzled), register r = 4g + e holds query
+    // 8g + 4hh + e = chunk 2g + hh
+    bf16* slot = L.ds[s & 1][t];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = f2bf(dp[4 * g + e]);
+      *reinterpret_cast<bf16x4*>(slot + swz8(r32, 2 * g + hh)) = v;
+    }
+    __syncthreads();
+    // dQ^T(t) += K(kt2)^T dS(t, kt2)^T with the tile wave kt2 = t - s parked this step
+    const int kt2 = t - s >= 0 ? t - s : t - s + NTILE;
+    const bf16* src = L.ds[s & 1][kt2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      dqT = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_read_perm(L.k, kt2 * TQ + 16 * s2, lane), tr_read_perm_swz(src, 16 * s2, lane),
+                                                    dqT, 0, 0, 0);
   }
-  if (live) {
+  // dK^T / dV^T: rows = head dims crow(r, hh), key on the lane -> 4 x 8-B stores per row piece
+  if (key_live) {
+    const float kscale = 1.0f / LOG2E;   // q~ = q d^-1/2 log2(e): dK = dS^T q d^-1/2 = dS^T q~ / log2(e)
+    bf16* row = dqkv + ((long long)w * n + key) * ld + h * HD + 4 * hh;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 a, b;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = f2bf(dkT[4 * g + e] * kscale);
+        b[e] = f2bf(dvT[4 * g + e]);
+      }
+      *reinterpret_cast<bf16x4*>(row + C + 8 * g) = a;
+      *reinterpret_cast<bf16x4*>(row + 2 * C + 8 * g) = b;
+    }
+  }
+  // dQ^T: rows = head dims, query t*32 + r32 on the lane
+  const int q = t * TQ + r32;
+  if (q < n) {
     bf16* row = dqkv + ((long long)w * n + q) * ld + h * HD + 4 * hh;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       bf16x4 a;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a[e] = f2bf(dqT[4 * g + e] * scale);
+      for (int e = 0; e < 4; ++e) a[e] = f2bf(dqT[4 * g + e] * qscale);
       *reinterpret_cast<bf16x4*>(row + 8 * g) = a;
     }
   }
+  if (!want_bins) return;
+  __syncthreads();   // every wave's bin adds are done
+  float* dst = dbias_part + ((long long)w * nH + h) * nb;
+  for (int b = threadIdx.x; b < nb; b += BW * 64)
+    dst[b] = (float)((double)(long long)L.bins[b] * 0x1p-40);
 }
 
-// Relative-position-bias gradient from the per-(group, head) dS partial sums of wattn_bwd_kv, no
-// atomics: (1) sum the group partials in place into group 0 (coalesced float4), (2) one wave per
-// table row gathers the (query, key) positions that use that row through a CSR built once per stage
-// geometry (csr_off [n_bins+1], csr_el = element positions in per-lane tile order, ascending within
-// a row) and adds the sum to its gradient entry — each entry has exactly one writer.
-__global__ void dbias_reduce_kernel(float* __restrict__ part, int chunks, long long per_chunk) {
-  const long long e4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (e4 >= per_chunk) return;
-  float4 s = *reinterpret_cast<const float4*>(part + e4);
-  for (int c = 1; c < chunks; ++c) {
-    const float4 v = *reinterpret_cast<const float4*>(part + c * per_chunk + e4);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-  }
-  *reinterpret_cast<float4*>(part + e4) = s;
+// Bias-table gradient from the per-(window, head) bin rows, no atomics: (1) WCH chunks of windows
+// summed per (head, bin) into the scratch tail, (2) the chunks summed in order and added to the table
+// row of that bin (bin_row: -1 = no (query, key) pair uses the bin) — one writer per entry.
+__global__ void dbias_chunk_kernel(const float* __restrict__ part, int n_win, int hb, float* __restrict__ red) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= hb) return;
+  const int per = (n_win + WCH - 1) / WCH;
+  const int w0 = blockIdx.y * per, w1 = min(n_win, w0 + per);
+  float s = 0.f;
+  for (int w = w0; w < w1; ++w) s += part[(long long)w * hb + e];
+  red[(long long)blockIdx.y * hb + e] = s;
 }
 
-__global__ void dbias_gather_kernel(const float* __restrict__ red, int nH, const int* __restrict__ csr_off,
-                                    const int* __restrict__ csr_el, int n_bins, float* __restrict__ tgrad) {
-  // one wave per table row: lanes split the row's elements (<= 3 per lane for 147-token windows),
-  // heads loop inside (independent loads), one cross-lane sum per head
-  const int lane = threadIdx.x & 63;
-  const int bin = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (bin >= n_bins) return;
-  const int k0 = csr_off[bin], k1 = csr_off[bin + 1];
-  if (k0 == k1) return;
-  int els[3];
-  int cnt = 0;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int k = k0 + lane + 64 * i;
-    els[i] = k < k1 ? csr_el[k] : -1;
-  }
-  for (int k = k0 + lane + 192; k < k1; k += 64) ++cnt;   // tail of rows longer than 192 entries (larger windows)
-  for (int h0 = 0; h0 < nH; h0 += 4) {     // 4 heads in flight (nH is a multiple of 4 in Swin-B)
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (h0 + j >= nH) break;
-      const float* r = red + (long long)(h0 + j) * PH_ELEMS;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) s[j] += els[i] >= 0 ? r[els[i]] : 0.f;
-      if (cnt)
-        for (int k = k0 + lane + 192; k < k1; k += 64) s[j] += r[csr_el[k]];
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s[j] += __shfl_xor(s[j], o, 64);
-    if (lane < 4 && h0 + lane < nH) {
-      const float v = lane == 0 ? s[0] : lane == 1 ? s[1] : lane == 2 ? s[2] : s[3];
-      tgrad[(long long)bin * nH + h0 + lane] += v;
-    }
-  }
+__global__ void dbias_scatter_kernel(const float* __restrict__ red, int hb, int nb, int nH, const int* __restrict__ bin_row,
+                                     float* __restrict__ tgrad) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= hb) return;
+  const int h = e / nb, row = bin_row[e % nb];
+  if (row < 0) return;
+  float s = 0.f;
+#pragma unroll 8
+  for (int c = 0; c < WCH; ++c) s += red[(long long)c * hb + e];
+  tgrad[(long long)row * nH + h] += s;
 }
 
 }  // namespace
 
 extern "C" int64_t lrce_wattn_bias_elems(int n_pat, int nH) { return (int64_t)n_pat * nH * PH_ELEMS; }
-// dS scratch (bf16 units): the per-window dS images + the f32 chunk partials of the bias reduction
-extern "C" int64_t lrce_wattn_ds_elems(int n_win, int nH) {
-  return 2LL * ((n_win + GDS - 1) / GDS) * nH * PH_ELEMS;   // f32 partials, counted in 16-bit units
+// bias-gradient scratch (f32): one bin row per (window, head) + the WCH chunk sums
+extern "C" int64_t lrce_wattn_dbias_part_elems(int n_win, int nH, int n_bins) {
+  return (int64_t)(n_win + WCH) * nH * n_bins;
 }
 
 extern "C" int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
@@ -614,34 +556,31 @@ extern "C" int lrce_wattn_fwd_grouped(const uint16_t* qkv, const float* bias_fwd
 }
 
 extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                              const float* bias_fwd, const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv,
-                              uint16_t* ds_scratch, int n_win, int n, int nH, void* stream) {
-  if (!qkv || !out || !dout || !lse || !bias_fwd || !bias_bwd || !dqkv || !ds_scratch)
-    return lrce_fail(LRCE_E_ARG, "wattn_bwd: null pointer");
+                              const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv, float* dbias_part, int n_win,
+                              int n, int nH, int wh, int ww, void* stream) {
+  if (!qkv || !out || !dout || !lse || !bias_bwd || !dqkv) return lrce_fail(LRCE_E_ARG, "wattn_bwd: null pointer");
   if (n <= 4 * TQ || n > NPAD) return lrce_fail(LRCE_E_ARG, "wattn_bwd: n=%d outside (128,160]", n);
+  if (wh < 1 || ww < 1 || n % (wh * ww)) return lrce_fail(LRCE_E_ARG, "wattn_bwd: n=%d is not a wd x %d x %d window", n, wh, ww);
+  const int wd = n / (wh * ww);
+  const int nb = (2 * wd - 1) * (2 * wh - 1) * (2 * ww - 1);
+  if (nb > NBMAX) return lrce_fail(LRCE_E_ARG, "wattn_bwd: %d relative-position bins > %d", nb, NBMAX);
   if (n_win <= 0) return LRCE_OK;
-  const unsigned grid = (unsigned)(n_win * nH);
-  const unsigned grid_kv = (unsigned)(((n_win + GDS - 1) / GDS) * nH);
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const bf16* q = reinterpret_cast<const bf16*>(qkv);
-  const bf16* o = reinterpret_cast<const bf16*>(out);
-  const bf16* g = reinterpret_cast<const bf16*>(dout);
-  bf16* d = reinterpret_cast<bf16*>(dqkv);
-  wattn_bwd_kv_kernel<<<grid_kv, BW * 64, 0, st>>>(q, o, g, lse, bias_bwd, win_pat, d, reinterpret_cast<float*>(ds_scratch), n_win,
-                                                  n, nH);
-  wattn_bwd_q_kernel<<<grid, BW * 64, 0, st>>>(q, o, g, lse, bias_fwd, win_pat, d, n_win, n, nH, 1.0f / sqrtf((float)HD));
+  const int boff = ((wd - 1) * (2 * wh - 1) + (wh - 1)) * (2 * ww - 1) + (ww - 1);
+  wattn_bwd_kernel<<<(unsigned)(n_win * nH), BW * 64, 0, static_cast<hipStream_t>(stream)>>>(
+      reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const bf16*>(out), reinterpret_cast<const bf16*>(dout), lse, bias_bwd,
+      win_pat, reinterpret_cast<bf16*>(dqkv), dbias_part, n_win, n, nH, wh, ww, nb, boff, 1.0f / sqrtf((float)HD));
   return lrce_check_launch("wattn_bwd");
 }
 
-extern "C" int lrce_wattn_dbias_csr(const uint16_t* ds_scratch, int n_win, int nH, const int32_t* csr_off,
-                                    const int32_t* csr_el, int n_bins, float* table_grad, void* stream) {
-  if (!ds_scratch || !csr_off || !csr_el || !table_grad) return lrce_fail(LRCE_E_ARG, "wattn_dbias_csr: null pointer");
-  if (n_win <= 0 || nH <= 0 || n_bins <= 0) return lrce_fail(LRCE_E_ARG, "wattn_dbias_csr: n_win=%d nH=%d", n_win, nH);
-  const long long per_group = (long long)nH * PH_ELEMS;
-  const int groups = (n_win + GDS - 1) / GDS;
-  float* part = reinterpret_cast<float*>(const_cast<uint16_t*>(ds_scratch));
+extern "C" int lrce_wattn_dbias(float* dbias_part, int n_win, int nH, int n_bins, const int32_t* bin_row, float* table_grad,
+                                void* stream) {
+  if (!dbias_part || !bin_row || !table_grad) return lrce_fail(LRCE_E_ARG, "wattn_dbias: null pointer");
+  if (n_win <= 0 || nH <= 0 || n_bins <= 0 || n_bins > NBMAX)
+    return lrce_fail(LRCE_E_ARG, "wattn_dbias: n_win=%d nH=%d n_bins=%d", n_win, nH, n_bins);
+  const int hb = nH * n_bins;
+  float* red = dbias_part + (long long)n_win * hb;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (groups > 1) dbias_reduce_kernel<<<(unsigned)((per_group / 4 + 255) / 256), 256, 0, st>>>(part, groups, per_group);
-  dbias_gather_kernel<<<(unsigned)((n_bins + 3) / 4), 256, 0, st>>>(part, nH, csr_off, csr_el, n_bins, table_grad);
-  return lrce_check_launch("wattn_dbias_csr");
+  dbias_chunk_kernel<<<dim3((unsigned)((hb + 255) / 256), WCH), 256, 0, st>>>(dbias_part, n_win, hb, red);
+  dbias_scatter_kernel<<<(unsigned)((hb + 255) / 256), 256, 0, st>>>(red, hb, n_bins, nH, bin_row, table_grad);
+  return lrce_check_launch("wattn_dbias");
 }

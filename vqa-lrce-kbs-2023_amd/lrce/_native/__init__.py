@@ -90,8 +90,8 @@ _SIGS = {
     "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _P, _P],
     "lrce_wattn_fwd_grouped": [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_qkv_fwd": [_P, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P],
-    "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
-    "lrce_wattn_dbias_csr": [_P, _I, _I, _P, _P, _I, _P, _P],
+    "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lrce_wattn_dbias": [_P, _I, _I, _I, _P, _P, _P],
     "lrce_mha_fwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_mha_bwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_frames_resize": [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P],
@@ -115,10 +115,10 @@ _SIGS = {
     "lrce_version": [],
     "lrce_last_error": [],
 }
-_RET = {"lrce_last_error": ctypes.c_char_p, "lrce_wattn_bias_elems": _I64, "lrce_wattn_ds_elems": _I64,
+_RET = {"lrce_last_error": ctypes.c_char_p, "lrce_wattn_bias_elems": _I64, "lrce_wattn_dbias_part_elems": _I64,
         "lrce_layernorm_bwd_workspace": _I64}
 _SIGS["lrce_wattn_bias_elems"] = [_I, _I]
-_SIGS["lrce_wattn_ds_elems"] = [_I, _I]
+_SIGS["lrce_wattn_dbias_part_elems"] = [_I, _I, _I]
 _SIGS["lrce_layernorm_bwd_workspace"] = [_I, _I]
 
 

@@ -276,14 +276,14 @@ def _wgrad(flat, lin, dy16, x16):
         K.colsum(dy16, gb)
 
 
-def _dbias_csr(at, n):
-    """Bias-table gradient CSR of one attention module, cached against its index buffer's identity."""
+def _bin_rows(at, window):
+    """Bias-gradient bin -> table row map of one attention module, cached against its index buffer."""
     idx = at.relative_position_index
-    key = (idx.data_ptr(), idx._version, n, idx.device)
-    hit = getattr(at, "_lrce_dbias_csr", None)
+    key = (idx.data_ptr(), idx._version, tuple(window), idx.device)
+    hit = getattr(at, "_lrce_bin_rows", None)
     if hit is None or hit[0] != key:
-        hit = (key, K.wattn_dbias_csr(idx, n, at.relative_position_bias_table.shape[0]))
-        object.__setattr__(at, "_lrce_dbias_csr", hit)
+        hit = (key, K.wattn_bin_rows(idx, window))
+        object.__setattr__(at, "_lrce_bin_rows", hit)
     return hit[1]
 
 
@@ -325,7 +325,7 @@ class _SwinBlockFn(torch.autograd.Function):
         K.linear(g, flat.w16(blk.mlp.fc2.weight), blk.mlp.fc2.bias, out=out, resid=x_mid, row_scale=dp2,
                  rows_per_scale=geo.rows_per_clip)
         if any(t.requires_grad for t in (x,) + params):
-            ctx.save = (x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_f, bias_b)
+            ctx.save = (x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_b)
             ctx.blk, ctx.geo, ctx.flat, ctx.dp1, ctx.dp2 = blk, geo, flat, dp1, dp2
             ctx.wmap, ctx.win_pat = wmap, win_pat
             ctx.sp2win = geo.sp2win_shift if shifted else geo.sp2win
@@ -333,7 +333,7 @@ class _SwinBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_f, bias_b = ctx.save
+        x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_b = ctx.save
         blk, geo, flat, dp1, dp2, wmap = ctx.blk, ctx.geo, ctx.flat, ctx.dp1, ctx.dp2, ctx.wmap
         at = blk.attn
         C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
@@ -360,13 +360,13 @@ class _SwinBlockFn(torch.autograd.Function):
         do = K.linear_dx(dmid16, flat.w16(at.proj.weight), out_f32=False)
         del dmid16
         dqkv = torch.empty_like(qkv)
-        ds = torch.empty(K.wattn_ds_elems(geo.n_win, nH), dtype=torch.bfloat16, device=dout.device)
-        K.wattn_bwd(qkv, o, do, lse, bias_f, bias_b, ctx.win_pat, dqkv, ds, geo.n_win, n, nH)
+        dbp = torch.empty(K.wattn_dbias_part_elems(geo.n_win, nH, geo.ws), device=dout.device)
+        K.wattn_bwd(qkv, o, do, lse, bias_b, ctx.win_pat, dqkv, dbp, geo.n_win, n, nH, geo.ws)
         del do, o
         gt = _g(flat, at.relative_position_bias_table)
         if gt is not None:
-            K.wattn_dbias_gather(ds, geo.n_win, nH, _dbias_csr(at, n), gt)
-        del ds
+            K.wattn_dbias(dbp, geo.n_win, nH, geo.ws, _bin_rows(at, geo.ws), gt)
+        del dbp
         _wgrad(flat, at.qkv, dqkv, xw)
         dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight))
         del dqkv, qkv, xw

@@ -337,12 +337,16 @@ def wattn_qkv_fwd(x, w_qkv, b_qkv, qscale, bias_fwd, win_pat, qkv, out, lse, n_w
            nbytes=2.0 * (M * C + 3 * C * C + M * 3 * C + M * C), key=(n_win, nH))
 
 
-def wattn_bwd(qkv, out, dout, lse, bias_fwd, bias_bwd, win_pat, dqkv, ds, n_win, n, nH):
-    # algorithmic work: dV, dP, dQ, dK = 8 n^2 d per (window, head) (the kernels recompute S, dP)
-    _timed("wattn_bwd", dqkv, lambda: call("lrce_wattn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(bias_fwd),
-                                            ptr(bias_bwd), ptr(win_pat), ptr(dqkv), ptr(ds), n_win, n, nH,
+def wattn_bwd(qkv, out, dout, lse, bias_bwd, win_pat, dqkv, dbias_part, n_win, n, nH, window):
+    """One-kernel window-attention backward; window = (wd, wh, ww) with n = wd*wh*ww.  dbias_part (f32,
+    wattn_dbias_part_elems) receives the bias-table gradient binned by relative position (wattn_dbias)."""
+    _, wh, ww = window
+    # algorithmic work: dV, dP, dQ, dK = 8 n^2 d per (window, head)
+    _timed("wattn_bwd", dqkv, lambda: call("lrce_wattn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(bias_bwd),
+                                            ptr(win_pat), ptr(dqkv), ptr(dbias_part), n_win, n, nH, wh, ww,
                                             stream_of(dqkv)),
-           flops=8.0 * n * n * 32 * n_win * nH, key=(n_win, nH))
+           flops=8.0 * n * n * 32 * n_win * nH,
+           nbytes=2.0 * n * 32 * n_win * nH * 8, key=(n_win, nH))
 
 
 def frames_resize(frames, frame_idx, out_h=224, out_w=224, out=None):
@@ -361,38 +365,40 @@ def frames_resize(frames, frame_idx, out_h=224, out_w=224, out=None):
     return out
 
 
-def wattn_ds_elems(n_win, nH):
-    return N.lib().lrce_wattn_ds_elems(n_win, nH)
+def wattn_n_bins(window):
+    wd, wh, ww = window
+    return (2 * wd - 1) * (2 * wh - 1) * (2 * ww - 1)
 
 
-def wattn_dbias_csr(index, n, n_bins):
-    """Inverse of relative_position_index[:n, :n] in the kernels' per-lane tile order: for every
-    table row, the positions of the (query, key) pairs using it, ascending (csr_off, csr_el int32,
-    on index's device).  Built once per (block, geometry) on the host: index is a constant buffer."""
+def wattn_dbias_part_elems(n_win, nH, window):
+    return N.lib().lrce_wattn_dbias_part_elems(n_win, nH, wattn_n_bins(window))
+
+
+def wattn_bin_rows(index, window):
+    """Table row of every relative-position bin of lrce_wattn_bwd (int32 [n_bins], -1 = unused, on
+    index's device).  The kernel bins (query i, key j) at code(i) - code(j) + off with
+    code(t, h, w) = (t (2wh-1) + h)(2ww-1) + w; the row is read from relative_position_index[:n, :n]
+    itself (video_swin_ori.py:133-148, 171) and every pair of a bin must agree on it.  Built once per
+    (block, geometry) on the host: the index is a constant buffer."""
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-        raise RuntimeError("wattn_dbias_csr: build the bias-gradient CSR before HIP-graph capture (run one eager step)")
-    idx = index.detach().to("cpu", torch.int64)
-    el = torch.arange(25 * 1024)
-    reg, lane, tile = el & 15, (el >> 4) & 63, el // 1024
-    qt, kt = tile // 5, tile % 5
-    qi = qt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
-    kj = kt * 32 + (lane & 31)
-    valid = (qi < n) & (kj < n)
-    el, qi, kj = el[valid], qi[valid], kj[valid]
-    bins = idx[qi, kj]
-    if int(bins.min()) < 0 or int(bins.max()) >= n_bins:
-        raise ValueError("relative_position_index entry outside the bias table")
-    order = torch.sort(bins, stable=True).indices
-    csr_el = el[order].to(torch.int32)
-    counts = torch.bincount(bins, minlength=n_bins)
-    csr_off = torch.zeros(n_bins + 1, dtype=torch.int32)
-    csr_off[1:] = torch.cumsum(counts, 0).to(torch.int32)
-    return csr_off.to(index.device), csr_el.to(index.device), n_bins
+        raise RuntimeError("wattn_bin_rows: build the bias-gradient bin map before HIP-graph capture (run one eager step)")
+    wd, wh, ww = window
+    n = wd * wh * ww
+    idx = index.detach().to("cpu", torch.int64)[:n, :n]
+    x = torch.arange(n)
+    code = ((x // (wh * ww)) * (2 * wh - 1) + (x // ww) % wh) * (2 * ww - 1) + x % ww
+    off = ((wd - 1) * (2 * wh - 1) + (wh - 1)) * (2 * ww - 1) + (ww - 1)
+    b = (code[:, None] - code[None, :] + off).reshape(-1)
+    nb = wattn_n_bins(window)
+    rows = torch.full((nb,), -1, dtype=torch.int64)
+    rows[b] = idx.reshape(-1)
+    if not torch.equal(rows[b], idx.reshape(-1)):
+        raise ValueError("relative_position_index is not a function of the relative position within the window")
+    return rows.to(torch.int32).to(index.device)
 
 
-def wattn_dbias_gather(ds, n_win, nH, csr, table_grad):
-    csr_off, csr_el, n_bins = csr
-    call("lrce_wattn_dbias_csr", ptr(ds), n_win, nH, ptr(csr_off), ptr(csr_el), n_bins, ptr(table_grad),
+def wattn_dbias(dbias_part, n_win, nH, window, bin_row, table_grad):
+    call("lrce_wattn_dbias", ptr(dbias_part), n_win, nH, wattn_n_bins(window), ptr(bin_row), ptr(table_grad),
          stream_of(table_grad))
 
 
