@@ -104,6 +104,38 @@ typedef struct LrceGemmDesc {
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);
 
+/* Exact-f32 skinny linear (b_f32, M <= 64, K-major f32 A, K % 128 == 0, K <= 1024) whose A operand is
+ * a LayerNorm input or gradient: the post-norm LayerNorms of the recurrent decoder
+ * (nn.TransformerDecoderLayer norm1..3, fusionv3.py:8-17) fold into the GEMM that consumes them.
+ *   mode 1: A = x (pre-norm rows); the GEMM consumes y = LN(x) = (x - mean) rstd gamma + beta (eps);
+ *           mean / rstd f32 [m] written (optional), y materialised into y_out (optional, f32, ld_y).
+ *   mode 2: A = dy (gradient w.r.t. the LN output), x = the pre-norm rows (ld_x), mean / rstd read;
+ *           dx = LN backward of dy goes to y_out (optional); the GEMM consumes dropout_bwd(dx)
+ *           (mask of lrce_dropout over the [m][k] tensor: drop_p / drop_group / drop_seed, 0 = off),
+ *           also written to y2_out (optional); dgamma / dbeta (f32 [k], optional, together) += the
+ *           column sums of dy * xhat and dy.
+ * The epilogue is lrce_gemm's (bias, GELU, dGELU, fused dropout, residual, f32 / bf16 out). */
+typedef struct LrceLnPrologue {
+  int32_t mode;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  const float* x;
+  int64_t ld_x;
+  float* mean;
+  float* rstd;
+  float* y_out;
+  int64_t ld_y;
+  float* y2_out;
+  int64_t ld_y2;
+  float* dgamma;
+  float* dbeta;
+  float drop_p;
+  int32_t drop_group;
+  uint64_t drop_seed;
+} LrceLnPrologue;
+int lrce_gemm_ln(const LrceGemmDesc* desc, const LrceLnPrologue* prologue, void* stream);
+
 /* ---------------------------------------------------------------- LayerNorm
  * Row r of the (rows x cols) LN input is the concatenation of nseg segments of cols/nseg
  * channels, segment s read from source row in_map[r*nseg+s] of x (identity if in_map == NULL;

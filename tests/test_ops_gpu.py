@@ -514,17 +514,19 @@ def test_mha_fwd_bwd(B, H, Lq, Lk, masked, split, bdiv, drop):
 
 
 def _hash_uniform(seed, idx):
-    """Host restatement of lrce_uniform (csrc/common.h): 64-bit mix hash of seed*phi + idx -> [0,1)."""
+    """Host restatement of lrce_uniform (csrc/common.h): 64-bit mix hash of seed*phi + idx/4, 16 bits
+    per index -> [0,1)."""
     import numpy as np
+    ix = idx.numpy().astype(np.uint64)
     with np.errstate(over="ignore"):
-        v = np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + idx.numpy().astype(np.uint64)
+        v = np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + (ix >> np.uint64(2))
         v ^= v >> np.uint64(33)
         v *= np.uint64(0xff51afd7ed558ccd)
         v ^= v >> np.uint64(33)
         v *= np.uint64(0xc4ceb9fe1a85ec53)
         v ^= v >> np.uint64(33)
-    u32 = (v & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-    return torch.from_numpy((u32 >> 8).astype(np.float32) * np.float32(1.0 / 16777216.0))
+    u16 = ((v >> (np.uint64(16) * (ix & np.uint64(3)))) & np.uint64(0xFFFF)).astype(np.float32)
+    return torch.from_numpy(u16 * np.float32(1.0 / 65536.0))
 
 
 def test_dropout_residual_and_groups():
@@ -655,3 +657,46 @@ def test_fused_dropout_epilogue_matches_separate_launch(M):
     w2 = torch.randn(E, FF, device=dev) / math.sqrt(FF)
     dg = k.linear_dx(dy, w2, dgelu_pre=pre, drop=(p, 79, 1))
     assert torch.equal(dg, k.dropout_bwd(k.linear_dx(dy, w2, dgelu_pre=pre), p, 79))
+
+
+@pytest.mark.parametrize("M", [1, 10, 45])
+def test_gemm_ln_prologue_forward_and_backward(M):
+    """lrce_gemm_ln: the decoder's post-norm LayerNorms folded into the consuming exact-f32 GEMM.
+    Mode 1 vs LN then GEMM (f64 torch); mode 2 vs the LN backward + dropout backward then GEMM, with
+    the materialised dx / dropped dx and the accumulated gamma / beta gradients."""
+    k = K()
+    k.rng_offset(dev).zero_()
+    E, FF, eps, p = 768, 3072, 1e-12, 0.3
+    x = torch.randn(M, E, device=dev) * 3 + 1
+    gam = torch.rand(E, device=dev) + 0.5
+    bet = torch.randn(E, device=dev)
+    w = torch.randn(FF, E, device=dev) / math.sqrt(E)
+    b = torch.randn(FF, device=dev)
+    mean, rstd, y = torch.empty(M, device=dev), torch.empty(M, device=dev), torch.full((M, E), float("nan"), device=dev)
+    pro = k.ln_fwd_prologue(gam, bet, eps, mean=mean, rstd=rstd, y_out=y)
+    out = k.linear(x, w, b, out_f32=True, ln=pro)
+    xd = x.double()
+    ln = F.layer_norm(xd, (E,), gam.double(), bet.double(), eps)
+    assert rel(y, ln.float()) < 1e-5
+    assert rel(mean, xd.mean(-1).float()) < 1e-5
+    assert rel(rstd, (1 / (xd.var(-1, unbiased=False) + eps).sqrt()).float()) < 1e-5
+    assert rel(out, (ln @ w.double().t() + b.double()).float()) < 1e-5
+    # mode 2: A = dy of the LN output, GEMM consumes dropout_bwd(LN_bwd(dy)) in the dX orientation
+    dy = torch.randn(M, E, device=dev)
+    w2 = torch.randn(E, FF, device=dev) / math.sqrt(E)    # linear(FF -> E)^T shape [E, FF]: dX = dY' W2
+    dgam, dbet = torch.randn(E, device=dev), torch.randn(E, device=dev)
+    dg0, db0 = dgam.clone(), dbet.clone()
+    dx, dxd = torch.full((M, E), float("nan"), device=dev), torch.full((M, E), float("nan"), device=dev)
+    pro = k.ln_bwd_prologue(x, mean, rstd, gam, dgamma=dgam, dbeta=dbet, y_out=dx, y2_out=dxd, drop=(p, 91, 1))
+    g = k.linear_dx(dy, w2, ln=pro)
+    xr = xd.clone().requires_grad_(True)
+    gr, br = gam.double().requires_grad_(True), bet.double().requires_grad_(True)
+    F.layer_norm(xr, (E,), gr, br, eps).backward(dy.double())
+    assert rel(dx, xr.grad.float()) < 1e-5
+    assert rel(dgam - dg0, gr.grad.float()) < 1e-5 and rel(dbet - db0, br.grad.float()) < 1e-5
+    assert torch.equal(dxd, k.dropout_bwd(dx, p, 91))
+    assert rel(g, (dxd.double() @ w2.double()).float()) < 1e-5
+    for _ in range(2):   # deterministic (one writer per element)
+        dx2 = torch.empty_like(dx)
+        g2 = k.linear_dx(dy, w2, ln=k.ln_bwd_prologue(x, mean, rstd, gam, y_out=dx2, drop=(p, 91, 1)))
+        assert torch.equal(g2, g) and torch.equal(dx2, dx)

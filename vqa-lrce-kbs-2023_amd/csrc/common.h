@@ -100,12 +100,23 @@ __device__ __forceinline__ int xcd_remap(int id, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (id >> 3);
 }
 
-// 64-bit counter-based hash -> uniform float in [0,1): dropout / DropPath masks.
-__device__ __forceinline__ uint32_t lrce_hash(uint64_t x) {
+// 64-bit counter-based hash -> uniform floats in [0,1): dropout / DropPath masks.  One hash serves
+// four consecutive indices (16 bits each: keep-probability granularity 2^-16), so a thread handling
+// a float4 of consecutive elements pays one hash instead of four (lrce_uniform4); every site draws
+// element idx's value the same way, so forward and backward masks agree wherever they are computed.
+__device__ __forceinline__ uint64_t lrce_hash64(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
-  return (uint32_t)x;
+  return x;
 }
 __device__ __forceinline__ float lrce_uniform(uint64_t seed, uint64_t idx) {
-  return (lrce_hash(seed * 0x9E3779B97F4A7C15ULL + idx) >> 8) * (1.0f / 16777216.0f);
+  const uint64_t h = lrce_hash64(seed * 0x9E3779B97F4A7C15ULL + (idx >> 2));
+  return (float)((h >> (16 * (idx & 3))) & 0xFFFFu) * (1.0f / 65536.0f);
+}
+// the uniforms of indices 4*idx4 .. 4*idx4 + 3
+__device__ __forceinline__ float4 lrce_uniform4(uint64_t seed, uint64_t idx4) {
+  const uint64_t h = lrce_hash64(seed * 0x9E3779B97F4A7C15ULL + idx4);
+  const float s = 1.0f / 65536.0f;
+  return make_float4((float)(h & 0xFFFFu) * s, (float)((h >> 16) & 0xFFFFu) * s, (float)((h >> 32) & 0xFFFFu) * s,
+                     (float)((h >> 48) & 0xFFFFu) * s);
 }
 __device__ __forceinline__ uint64_t lrce_seed(uint64_t seed, const uint64_t* off) { return off ? seed + *off : seed; }

@@ -359,6 +359,285 @@ __global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
   if ((p.flags & LRCE_EPI_BIAS_GRAD) && n == 0) p.bias_grad[m] += p.alpha * asum;   // db (one owner per m)
 }
 
+// ---------------------------------------------------------------------------------------------
+// Skinny exact-f32 linear with a LayerNorm prologue on A (lrce_gemm_ln).  The recurrent decoder's
+// post-norm LayerNorms (nn.TransformerDecoderLayer norm1..3, fusionv3.py:8-17) are folded into the
+// GEMM that consumes their output: every workgroup reads whole A rows anyway (K = the LN width), so
+// it computes the row statistics itself (two-pass mean / variance, 8-wave LDS reduction) and
+// normalises in registers before its MFMAs; one launch instead of LayerNorm + GEMM.
+//   PRO = 1 (forward):  A = x (pre-norm), the GEMM consumes y = (x - mean) rstd gamma + beta; mean /
+//                       rstd [m] written by workgroup 0, y materialised (optional) by column slices.
+//   PRO = 2 (backward): A = dy (gradient of the LN output), x = pre-norm rows, mean / rstd read:
+//                       dx = rstd (g - mean(g) - xh mean(g xh)), g = dy gamma, xh = (x - mean) rstd;
+//                       dgamma += colsum(dy xh), dbeta += colsum(dy); the GEMM consumes
+//                       dropout_bwd(dx) (the forward dropout in front of the LN's residual add);
+//                       dx and the dropped dx materialised (optional).
+// Column slices of 16 are owned by workgroup (k / 16) % grid: the owner writes the materialised
+// values and the gamma / beta gradient of its slice (one writer per element, no atomics).
+// K = 8 waves x 16 x nu (nu <= 8): the whole row of A sits in the workgroup's registers.
+struct LnP {
+  const float* gamma;
+  const float* beta;
+  float eps;
+  const float* x;
+  long long ld_x;
+  float* mean;
+  float* rstd;
+  float* y_out;
+  long long ld_y;
+  float* y2_out;
+  long long ld_y2;
+  float* dgamma;
+  float* dbeta;
+  float drop_p;
+  int drop_group;
+  uint64_t drop_seed;
+};
+
+constexpr int LN_W = 8, LN_US = 8;
+
+template <int MT, bool B_KM, int PRO>
+__global__ void __launch_bounds__(LN_W * 64) skinny_ln_kernel(SkinnyP p, LnP q) {
+  __shared__ float red[LN_W][MT][16][17];
+  __shared__ float rsum[2][LN_W][MT * 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int n = n0 + col;
+  const bool n_ok = n < p.n;
+  const int nc = n_ok ? n : 0;
+  const int kw = p.k / LN_W, nu = kw >> 4;
+  const int kb = wave * kw;
+  const float inv_k = 1.0f / (float)p.k;
+  // every global load up front: the weight slab, the A rows, gamma / beta, (PRO 2) x rows + stats
+  float4 bv[LN_US], av[LN_US][MT], gv[LN_US], ev[LN_US];
+  float4 xv[PRO == 2 ? LN_US : 1][MT];
+  float mu[MT], rs[MT];
+#pragma unroll
+  for (int u = 0; u < LN_US; ++u) {
+    if (u >= nu) break;
+    const int k = kb + 16 * u + 4 * grp;
+    if (B_KM) {
+      bv[u] = *reinterpret_cast<const float4*>(p.b + (long long)nc * p.ldb + k);
+    } else {
+      const float* bp = p.b + (long long)k * p.ldb + nc;
+      bv[u] = make_float4(bp[0], bp[p.ldb], bp[2 * p.ldb], bp[3 * p.ldb]);
+    }
+    if (!n_ok) bv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[u] = *reinterpret_cast<const float4*>(q.gamma + k);
+    if (PRO == 1) ev[u] = *reinterpret_cast<const float4*>(q.beta + k);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = t * 16 + col;
+      const bool ok = m < p.m;
+      av[u][t] = ok ? *reinterpret_cast<const float4*>(p.a + (long long)m * p.lda + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (PRO == 2)
+        xv[u][t] = ok ? *reinterpret_cast<const float4*>(q.x + (long long)m * q.ld_x + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  if (PRO == 2) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = min(t * 16 + col, p.m - 1);
+      mu[t] = q.mean[m];
+      rs[t] = q.rstd[m];
+    }
+  }
+  // sum of (s1, s2) over the row: in-lane over the wave's k, across the 4 k-groups, across waves
+  auto row_reduce = [&](float (&s1)[MT], float (&s2)[MT], bool two) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      s1[t] += __shfl_xor(s1[t], 16, 64);
+      s1[t] += __shfl_xor(s1[t], 32, 64);
+      if (two) {
+        s2[t] += __shfl_xor(s2[t], 16, 64);
+        s2[t] += __shfl_xor(s2[t], 32, 64);
+      }
+      if (grp == 0) {
+        rsum[0][wave][t * 16 + col] = s1[t];
+        if (two) rsum[1][wave][t * 16 + col] = s2[t];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < LN_W; ++w) {
+        a += rsum[0][w][t * 16 + col];
+        if (two) b += rsum[1][w][t * 16 + col];
+      }
+      s1[t] = a;
+      s2[t] = b;
+    }
+    __syncthreads();
+  };
+  const int slice0 = kb >> 4;   // this wave's first 16-column slice
+  auto owns = [&](int u) { return (slice0 + u) % (int)gridDim.x == (int)blockIdx.x; };
+  if (PRO == 1) {
+    float s1[MT], s2[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      s1[t] = 0.f;
+      s2[t] = 0.f;
+#pragma unroll
+      for (int u = 0; u < LN_US; ++u) {
+        if (u >= nu) break;
+        s1[t] += (av[u][t].x + av[u][t].y) + (av[u][t].z + av[u][t].w);
+      }
+    }
+    row_reduce(s1, s2, false);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      mu[t] = s1[t] * inv_k;
+      s1[t] = 0.f;
+#pragma unroll
+      for (int u = 0; u < LN_US; ++u) {
+        if (u >= nu) break;
+        const float4 d = make_float4(av[u][t].x - mu[t], av[u][t].y - mu[t], av[u][t].z - mu[t], av[u][t].w - mu[t]);
+        s1[t] += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+      }
+    }
+    row_reduce(s1, s2, false);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      rs[t] = rsqrtf(s1[t] * inv_k + q.eps);
+      const int m = t * 16 + col;
+      if (blockIdx.x == 0 && wave == 0 && grp == 0 && m < p.m) {
+        if (q.mean) q.mean[m] = mu[t];
+        if (q.rstd) q.rstd[m] = rs[t];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < LN_US; ++u) {
+      if (u >= nu) break;
+      const bool own = q.y_out && owns(u);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        float4& a = av[u][t];
+        a.x = (a.x - mu[t]) * rs[t] * gv[u].x + ev[u].x;
+        a.y = (a.y - mu[t]) * rs[t] * gv[u].y + ev[u].y;
+        a.z = (a.z - mu[t]) * rs[t] * gv[u].z + ev[u].z;
+        a.w = (a.w - mu[t]) * rs[t] * gv[u].w + ev[u].w;
+        const int m = t * 16 + col;
+        if (own && m < p.m) *reinterpret_cast<float4*>(q.y_out + (long long)m * q.ld_y + kb + 16 * u + 4 * grp) = a;
+        if (m >= p.m) a = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+  if (PRO == 2) {
+    float s1[MT], s2[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      s1[t] = 0.f;
+      s2[t] = 0.f;
+#pragma unroll
+      for (int u = 0; u < LN_US; ++u) {
+        if (u >= nu) break;
+        // xv <- xh, and the gamma / beta gradient terms of the owned slice before dy is replaced
+        float4& x = xv[u][t];
+        x = make_float4((x.x - mu[t]) * rs[t], (x.y - mu[t]) * rs[t], (x.z - mu[t]) * rs[t], (x.w - mu[t]) * rs[t]);
+        const float4 g = make_float4(av[u][t].x * gv[u].x, av[u][t].y * gv[u].y, av[u][t].z * gv[u].z, av[u][t].w * gv[u].w);
+        s1[t] += (g.x + g.y) + (g.z + g.w);
+        s2[t] += (g.x * x.x + g.y * x.y) + (g.z * x.z + g.w * x.w);
+      }
+    }
+    // dgamma / dbeta of the owned slice: column sums over the rows (16 lanes x MT tiles)
+#pragma unroll
+    for (int u = 0; u < LN_US; ++u) {
+      if (u >= nu) break;
+      if (!(q.dgamma && owns(u))) continue;
+      float4 dg = make_float4(0.f, 0.f, 0.f, 0.f), db = dg;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {   // rows >= m hold dy = 0
+        const float4 d = av[u][t], x = xv[u][t];
+        dg.x += d.x * x.x; dg.y += d.y * x.y; dg.z += d.z * x.z; dg.w += d.w * x.w;
+        db.x += d.x; db.y += d.y; db.z += d.z; db.w += d.w;
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        dg.x += __shfl_xor(dg.x, o, 64); dg.y += __shfl_xor(dg.y, o, 64);
+        dg.z += __shfl_xor(dg.z, o, 64); dg.w += __shfl_xor(dg.w, o, 64);
+        db.x += __shfl_xor(db.x, o, 64); db.y += __shfl_xor(db.y, o, 64);
+        db.z += __shfl_xor(db.z, o, 64); db.w += __shfl_xor(db.w, o, 64);
+      }
+      if (col == 0) {
+        const int k = kb + 16 * u + 4 * grp;
+        float4* pg = reinterpret_cast<float4*>(q.dgamma + k);
+        float4* pb = reinterpret_cast<float4*>(q.dbeta + k);
+        float4 og = *pg, ob = *pb;
+        og.x += dg.x; og.y += dg.y; og.z += dg.z; og.w += dg.w;
+        ob.x += db.x; ob.y += db.y; ob.z += db.z; ob.w += db.w;
+        *pg = og;
+        *pb = ob;
+      }
+    }
+    row_reduce(s1, s2, true);
+    const uint64_t seed = lrce_seed(q.drop_seed, p.rng_off);
+    const float keep_div = 1.0f - q.drop_p;   // x / (1 - p): the bits of lrce_dropout_bwd
+#pragma unroll
+    for (int u = 0; u < LN_US; ++u) {
+      if (u >= nu) break;
+      const bool own = owns(u);
+      const int k = kb + 16 * u + 4 * grp;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const float mg = s1[t] * inv_k, mgx = s2[t] * inv_k;
+        const int m = t * 16 + col;
+        float4& a = av[u][t];
+        const float4 x = xv[u][t];
+        a = make_float4(rs[t] * (a.x * gv[u].x - mg - x.x * mgx), rs[t] * (a.y * gv[u].y - mg - x.y * mgx),
+                        rs[t] * (a.z * gv[u].z - mg - x.z * mgx), rs[t] * (a.w * gv[u].w - mg - x.w * mgx));
+        if (m >= p.m) a = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (own && q.y_out && m < p.m) *reinterpret_cast<float4*>(q.y_out + (long long)m * q.ld_y + k) = a;
+        if (q.drop_p > 0.f) {
+          const long long e = (long long)m * p.k + k;   // k % 4 == 0, K % 4 == 0: one hash per float4
+          float4 uu;
+          if (q.drop_group == 1) uu = lrce_uniform4(seed, (uint64_t)e >> 2);
+          else uu = make_float4(lrce_uniform(seed, (e + 0) / q.drop_group), lrce_uniform(seed, (e + 1) / q.drop_group),
+                                lrce_uniform(seed, (e + 2) / q.drop_group), lrce_uniform(seed, (e + 3) / q.drop_group));
+          a.x = uu.x >= q.drop_p ? a.x / keep_div : 0.f;
+          a.y = uu.y >= q.drop_p ? a.y / keep_div : 0.f;
+          a.z = uu.z >= q.drop_p ? a.z / keep_div : 0.f;
+          a.w = uu.w >= q.drop_p ? a.w / keep_div : 0.f;
+        }
+        if (own && q.y2_out && m < p.m) *reinterpret_cast<float4*>(q.y2_out + (long long)m * q.ld_y2 + k) = a;
+      }
+    }
+  }
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < LN_US; ++u) {
+    if (u >= nu) break;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][t].x, bv[u].x, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][t].y, bv[u].y, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][t].z, bv[u].z, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][t].w, bv[u].w, acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][t][grp * 4 + r][col] = acc[t][r];
+  __syncthreads();
+  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, grp256 = threadIdx.x >> 8;
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    if (t % 2 != grp256) continue;
+    const int m = t * 16 + ml, nn = n0 + nl;
+    if (m < p.m && nn < p.n) {
+      float x = 0.f;
+#pragma unroll
+      for (int w = 0; w < LN_W; ++w) x += red[w][t][ml][nl];
+      sk_epilogue(p, x, m, nn);
+    }
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -491,4 +770,53 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
   dim3 grid(tiles_m * p.tiles_n, split);
   gemm_f32_kernel<<<grid, NT, 0, static_cast<hipStream_t>(stream)>>>(p);
   return lrce_check_launch("gemm_f32");
+}
+
+int lrce_gemm_ln(const LrceGemmDesc* d, const LrceLnPrologue* pro, void* stream) {
+  if (!d || !pro) return lrce_fail(LRCE_E_ARG, "gemm_ln: null descriptor");
+  if (pro->mode != 1 && pro->mode != 2) return lrce_fail(LRCE_E_ARG, "gemm_ln: mode %d", pro->mode);
+  if (!d->b_f32 || !d->a_f32 || !d->a_kmajor || d->batch != 1 || d->a_map || d->c_map || d->a_row_scale ||
+      d->split_k > 1 || d->row_scale || (d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)))
+    return lrce_fail(LRCE_E_ARG, "gemm_ln: f32 K-major A, f32 B, no maps / split / atomics");
+  if (d->m < 1 || d->m > 64) return lrce_fail(LRCE_E_ARG, "gemm_ln: m=%d outside [1, 64]", d->m);
+  if (d->k % (LN_W * 16) || d->k > LN_W * 16 * LN_US) return lrce_fail(LRCE_E_ARG, "gemm_ln: k=%d (multiple of 128, <= 1024)", d->k);
+  if ((d->lda % 4) || (d->ldb % 4) || (reinterpret_cast<uintptr_t>(d->a) & 15) || (reinterpret_cast<uintptr_t>(d->b) & 15))
+    return lrce_fail(LRCE_E_ARG, "gemm_ln: A / B need 16-B alignment");
+  if (!pro->gamma || (pro->mode == 1 && !pro->beta)) return lrce_fail(LRCE_E_ARG, "gemm_ln: gamma / beta");
+  if (pro->mode == 2 && (!pro->x || !pro->mean || !pro->rstd || (pro->ld_x % 4) || (!pro->dgamma != !pro->dbeta)))
+    return lrce_fail(LRCE_E_ARG, "gemm_ln: backward needs x (ld %% 4 == 0), mean, rstd; dgamma with dbeta");
+  if ((pro->y_out && (pro->ld_y % 4)) || (pro->y2_out && (pro->ld_y2 % 4)))
+    return lrce_fail(LRCE_E_ARG, "gemm_ln: materialised outputs need ld %% 4 == 0");
+  const int tiles = (d->n + 15) / 16;
+  SkinnyP q;
+  q.a = static_cast<const float*>(d->a); q.b = static_cast<const float*>(d->b); q.c = d->c;
+  q.lda = d->lda; q.ldb = d->ldb; q.ldc = d->ldc;
+  q.m = d->m; q.n = d->n; q.k = d->k; q.flags = d->flags; q.bias = d->bias;
+  q.aux = d->aux; q.ld_aux = d->ld_aux; q.aux_out = static_cast<bf16*>(d->aux_out); q.ld_aux_out = d->ld_aux_out;
+  q.alpha = d->alpha; q.row_scale = nullptr; q.rows_per_scale = 1;
+  q.scale_cols = d->scale_cols; q.scale_val = d->scale_val; q.bias_grad = nullptr;
+  q.drop_p = d->drop_p; q.drop_group = d->drop_group > 0 ? d->drop_group : 1; q.drop_seed = d->drop_seed;
+  q.rng_off = lrce_rng_offset();
+  LnP l;
+  l.gamma = pro->gamma; l.beta = pro->beta; l.eps = pro->eps; l.x = pro->x; l.ld_x = pro->ld_x;
+  l.mean = pro->mean; l.rstd = pro->rstd; l.y_out = pro->y_out; l.ld_y = pro->ld_y; l.y2_out = pro->y2_out;
+  l.ld_y2 = pro->ld_y2; l.dgamma = pro->dgamma; l.dbeta = pro->dbeta; l.drop_p = pro->drop_p;
+  l.drop_group = pro->drop_group > 0 ? pro->drop_group : 1; l.drop_seed = pro->drop_seed;
+  const int mt = (d->m + 15) / 16;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+#define LRCE_SKLN(MT, PRO)                                                                         \
+  if (d->b_kmajor) skinny_ln_kernel<MT, true, PRO><<<tiles, LN_W * 64, 0, st>>>(q, l);             \
+  else skinny_ln_kernel<MT, false, PRO><<<tiles, LN_W * 64, 0, st>>>(q, l);
+#define LRCE_SKLN_MT(PRO)                    \
+  switch (mt) {                              \
+    case 1: LRCE_SKLN(1, PRO) break;         \
+    case 2: LRCE_SKLN(2, PRO) break;         \
+    case 3: LRCE_SKLN(3, PRO) break;         \
+    default: LRCE_SKLN(4, PRO) break;        \
+  }
+  if (pro->mode == 1) { LRCE_SKLN_MT(1) }
+  else { LRCE_SKLN_MT(2) }
+#undef LRCE_SKLN_MT
+#undef LRCE_SKLN
+  return lrce_check_launch("gemm_ln");
 }

@@ -181,10 +181,11 @@ __global__ void __launch_bounds__(256) mha_bwd_kernel(MhaP P) {
 // ---- single-query path (the recurrent decoder: Lq = 1, fusionv3.py:44-49) --------------------
 // One workgroup (4 waves) per (batch row, head).  Scores / probabilities: thread t owns key t
 // (its key row as 8 x 16 B in registers, q broadcast from LDS); block-wide max / sum through LDS.
-// Output, dQ, dK, dV: lane = head dim, wave w takes keys w, w+4, ...  Every global load of the
-// problem (key rows, the wave's V / K columns, the old dK / dV words) is issued before the first
-// dependent instruction, so a launch is ONE memory round trip plus the LDS reductions instead of
-// a chain of dependent trips.  dK/dV rows are updated with plain read-modify-writes when this
+// Output, dQ, dK, dV: lane = head dim, wave w takes keys w, w+4, ...  The forward issues every
+// global load of the problem (key rows, the wave's V columns) before the first dependent
+// instruction: one memory round trip plus the LDS reductions.  (The backward keeps 16-key batches:
+// holding all 48 keys' K / dK / dV words per lane cost it 2x, 256 VGPRs and AGPR spills.)
+// dK/dV rows are updated with plain read-modify-writes when this
 // workgroup is their only writer (bdiv == 1: the question segment accumulates over the recurrent
 // steps, which are separate launches), with atomics when bdiv answer choices share a video row.
 constexpr int KW = MAXK / 4;   // keys per wave
@@ -197,6 +198,19 @@ __device__ __forceinline__ float dot_regs64(const bf16x8 (&kr)[8], const float* 
     const float4 q1 = *reinterpret_cast<const float4*>(qs + 8 * c + 4);
     acc += bf2f(kr[c][0]) * q0.x + bf2f(kr[c][1]) * q0.y + bf2f(kr[c][2]) * q0.z + bf2f(kr[c][3]) * q0.w +
            bf2f(kr[c][4]) * q1.x + bf2f(kr[c][5]) * q1.y + bf2f(kr[c][6]) * q1.z + bf2f(kr[c][7]) * q1.w;
+  }
+  return acc;
+}
+
+__device__ __forceinline__ float dot_row64(const bf16* row, const float* qs) {
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const bf16x8 kv = *reinterpret_cast<const bf16x8*>(row + 8 * c);
+    const float4 q0 = *reinterpret_cast<const float4*>(qs + 8 * c);
+    const float4 q1 = *reinterpret_cast<const float4*>(qs + 8 * c + 4);
+    acc += bf2f(kv[0]) * q0.x + bf2f(kv[1]) * q0.y + bf2f(kv[2]) * q0.z + bf2f(kv[3]) * q0.w +
+           bf2f(kv[4]) * q1.x + bf2f(kv[5]) * q1.y + bf2f(kv[6]) * q1.z + bf2f(kv[7]) * q1.w;
   }
   return acc;
 }
@@ -264,11 +278,6 @@ __global__ void __launch_bounds__(256) mha1_fwd_kernel(MhaP P) {
   }
 }
 
-__device__ __forceinline__ float* dkv_word(const LrceMhaDesc& d, float* p1, float* p2, int b, int j, int h, int lane) {
-  if (j < d.lk1) return p1 + (long long)(b / d.kv1_bdiv) * d.stride_dkv1_b + (long long)j * d.ld_dkv1 + h * D + lane;
-  return p2 + (long long)(b / d.kv2_bdiv) * d.stride_dkv2_b + (long long)(j - d.lk1) * d.ld_dkv2 + h * D + lane;
-}
-
 __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
   const LrceMhaDesc& d = P.d;
   __shared__ __attribute__((aligned(16))) float qs[D];
@@ -280,24 +289,6 @@ __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int b = blockIdx.x / d.H, h = blockIdx.x % d.H;
   const int Lk = d.lk1 + d.lk2;
-  const bool live = t < Lk;
-  const bool at1 = d.kv1_bdiv > 1, at2 = d.kv2_bdiv > 1;
-  // all loads up front: key / value rows of key t, the wave's K column entries, the old dK / dV
-  // words of the single-writer rows
-  bf16x8 kr[8], vr[8];
-  load_row64(kr, key_row(d, d.k1, d.k2, b, live ? t : 0, h));
-  load_row64(vr, key_row(d, d.v1, d.v2, b, live ? t : 0, h));
-  float kv[KW], okk[KW], ovv[KW];
-#pragma unroll
-  for (int u = 0; u < KW; ++u) {
-    const int j = min(wave + 4 * u, Lk - 1);
-    kv[u] = bf2f(key_row(d, d.k1, d.k2, b, j, h)[lane]);
-    const bool at = j < d.lk1 ? at1 : at2;
-    okk[u] = at ? 0.f : *dkv_word(d, d.dk1, d.dk2, b, j, h, lane);
-    ovv[u] = at ? 0.f : *dkv_word(d, d.dv1, d.dv2, b, j, h, lane);
-  }
-  const bool keep = live && (!d.key_mask || d.key_mask[(long long)b * Lk + t] != 0);
-  const float l = d.lse[(long long)b * d.H + h];
   float dod = 0.f, od = 0.f;
   if (t < D) {
     qs[t] = ld_io(d, d.q, (long long)b * d.ld_q + h * D + t) * d.scale;
@@ -306,10 +297,13 @@ __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
     gs[t] = dod;
   }
   const float delta = block_sum(dod * od, red);   // also orders the qs / gs writes
+  const float l = d.lse[(long long)b * d.H + h];
+  const bool live = t < Lk;
   float pf = 0.f, ds = 0.f;
   if (live) {
-    const float sc = dot_regs64(kr, qs);
-    const float dp = dot_regs64(vr, gs);
+    const float sc = dot_row64(key_row(d, d.k1, d.k2, b, t, h), qs);
+    const float dp = dot_row64(key_row(d, d.v1, d.v2, b, t, h), gs);
+    const bool keep = !d.key_mask || d.key_mask[(long long)b * Lk + t] != 0;
     const float p = keep ? __expf(sc - l) : 0.f;
     const float f = drop_factor(d, P.off, b, h, 0, t, Lk);
     pf = p * f;                       // dV uses the dropped probabilities
@@ -320,21 +314,44 @@ __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
   __syncthreads();
   const float q = qs[lane], g = gs[lane];
   float dq0 = 0.f, dq1 = 0.f;
+  const bool at1 = d.kv1_bdiv > 1, at2 = d.kv2_bdiv > 1;
+  // Keys in batches of UB per wave: every K-row load and dK/dV read of a batch is issued before its
+  // first store, so the read-modify-writes overlap instead of forming one serial memory round trip
+  // per key (single writer per row); rows shared by bdiv > 1 rows use no-return atomics.
+  constexpr int UB = 16;
+  for (int j0 = wave; j0 < Lk; j0 += 4 * UB) {
+    float kv[UB], okk[UB], ovv[UB];
+    float* pk[UB];
+    float* pv[UB];
+    bool at[UB];
 #pragma unroll
-  for (int u = 0; u < KW; ++u) {
-    const int j = wave + 4 * u;
-    if (j < Lk) {
-      const float dsj = dss[j], pj = ps[j];
-      if (u & 1) dq1 += dsj * kv[u];
-      else dq0 += dsj * kv[u];
-      float* pk = dkv_word(d, d.dk1, d.dk2, b, j, h, lane);
-      float* pv = dkv_word(d, d.dv1, d.dv2, b, j, h, lane);
-      if (j < d.lk1 ? at1 : at2) {
-        __hip_atomic_fetch_add(pk, dsj * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(pv, pj * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int u = 0; u < UB; ++u) {
+      const int j = min(j0 + 4 * u, Lk - 1);
+      kv[u] = bf2f(key_row(d, d.k1, d.k2, b, j, h)[lane]);
+      if (j < d.lk1) {
+        const long long o = (long long)(b / d.kv1_bdiv) * d.stride_dkv1_b + (long long)j * d.ld_dkv1 + h * D + lane;
+        pk[u] = d.dk1 + o; pv[u] = d.dv1 + o; at[u] = at1;
       } else {
-        *pk = okk[u] + dsj * q;
-        *pv = ovv[u] + pj * g;
+        const long long o = (long long)(b / d.kv2_bdiv) * d.stride_dkv2_b + (long long)(j - d.lk1) * d.ld_dkv2 + h * D + lane;
+        pk[u] = d.dk2 + o; pv[u] = d.dv2 + o; at[u] = at2;
+      }
+      okk[u] = at[u] ? 0.f : *pk[u];
+      ovv[u] = at[u] ? 0.f : *pv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int j = j0 + 4 * u;
+      if (j < Lk) {
+        const float dsj = dss[j], pj = ps[j];
+        if (u & 1) dq1 += dsj * kv[u];
+        else dq0 += dsj * kv[u];
+        if (at[u]) {
+          __hip_atomic_fetch_add(pk[u], dsj * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(pv[u], pj * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          *pk[u] = okk[u] + dsj * q;
+          *pv[u] = ovv[u] + pj * g;
+        }
       }
     }
   }

@@ -50,12 +50,13 @@ __global__ void __launch_bounds__(256) segsum_kernel(const float* __restrict__ c
   if (threadIdx.x == 0) out[t] = red[0];
 }
 
-// CH consecutive 1024-element chunks per workgroup (4 parameters per thread per chunk): the
-// per-chunk scalars (tensor, lr, norm) are wave-uniform loads, the bias corrections are computed
-// once per thread from the device step (exp2 of t*log2(beta)), and the next-step norms are summed
-// in registers while consecutive chunks belong to one tensor — one atomic per (workgroup, tensor)
-// run instead of one per chunk (783 tensors, 305 K chunks: the per-chunk atomics serialised).
-constexpr int ADAMW_CH = 8;
+// One WAVE per 1024-element chunk (16 parameters per lane as 4 coalesced float4 rows), ADAMW_CPW
+// consecutive chunks per wave, 4 waves per workgroup: the per-chunk scalars (tensor, lr, norm) are
+// wave-uniform loads, every lane has 16 loads of p / g / m / v in flight, and the chunk's sum of
+// squares (the next step's L2 norm, reduced deterministically by segsum_kernel) is one wave_sum —
+// no workgroup barrier anywhere.  The bias corrections are computed from the device step
+// (exp2 of t * log2(beta)), so the launch replays unchanged from a HIP graph.
+constexpr int ADAMW_CPW = 2;
 
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, const int* __restrict__ chunk_tensor,
@@ -65,80 +66,71 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
                                                     float* __restrict__ sumsq_next, bf16* __restrict__ ph, long long h_lo,
                                                     long long h_hi, const bf16* __restrict__ g16,
                                                     float* __restrict__ chunk_sq) {
-  const int c0 = blockIdx.x * ADAMW_CH;
+  const int lane = threadIdx.x & 63;
+  const int wave_id = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (step_dev) {
     const float t = *step_dev;
     bc1 = 1.0f - exp2f(t * __log2f(b1));
     bc2 = 1.0f - exp2f(t * __log2f(b2));
   }
   const float isb2 = rsqrtf(bc2);
-  __shared__ float red[4];
-  float q = 0.f;
-  int t_run = -1;
-  auto flush = [&]() {   // block-wide sum of q into sumsq_next[t_run]
-    if (!sumsq_next || t_run < 0) return;
-    float w = wave_sum(q);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
-    __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(sumsq_next + t_run, red[0] + red[1] + red[2] + red[3]);
-    q = 0.f;
-  };
-  auto chunk_flush = [&](int c) {   // deterministic form: this chunk's sum -> chunk_sq[c]
-    float w = wave_sum(q);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
-    __syncthreads();
-    if (threadIdx.x == 0) chunk_sq[c] = (red[0] + red[1]) + (red[2] + red[3]);
-    q = 0.f;
-  };
-  for (int k = 0; k < ADAMW_CH; ++k) {
-    const int c = c0 + k;
+  for (int k = 0; k < ADAMW_CPW; ++k) {
+    const int c = wave_id * ADAMW_CPW + k;
     if (c >= n_chunks) break;
     const int t = chunk_tensor[c];
-    if (t != t_run && !chunk_sq) {
-      flush();
-      t_run = t;
-    }
     const float lr = tensor_lr[t];
     const float ss = sumsq ? sumsq[t] : 0.f;
     const float rc = (reg != 0.f && ss > 0.f) ? reg * rsqrtf(ss) : 0.f;
     const float step = lr / bc1, decay = 1.0f - lr * wd;
-    const long long i = (long long)c * 1024 + threadIdx.x * 4;
-    float4 pp = *reinterpret_cast<float4*>(p + i);
-    float4 gg;
-    if (g16) {   // bf16 gradient (the all-reduced bf16 buckets of lrce/distributed.py)
-      const bf16x4 t = *reinterpret_cast<const bf16x4*>(g16 + i);
-      gg = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
-    } else {
-      gg = *reinterpret_cast<const float4*>(g + i);
-    }
-    float4 mm = *reinterpret_cast<float4*>(m + i);
-    float4 vv = *reinterpret_cast<float4*>(v + i);
-    float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
-    bf16x4 ob;
+    const long long base = (long long)c * 1024 + lane * 4;
+    float4 pp[4], gg[4], mm[4], vv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float gr = ga[j] * gscale + rc * pa[j];
-      ma[j] = b1 * ma[j] + (1.0f - b1) * gr;
-      va[j] = b2 * va[j] + (1.0f - b2) * gr * gr;
-      const float np = pa[j] * decay - step * ma[j] / (sqrtf(va[j]) * isb2 + eps);
-      pa[j] = np;
-      ob[j] = f2bf(np);
+    for (int r = 0; r < 4; ++r) {
+      const long long i = base + r * 256;
+      pp[r] = *reinterpret_cast<const float4*>(p + i);
+      if (g16) {   // bf16 gradient (the all-reduced bf16 buckets of lrce/distributed.py)
+        const bf16x4 h = *reinterpret_cast<const bf16x4*>(g16 + i);
+        gg[r] = make_float4(bf2f(h[0]), bf2f(h[1]), bf2f(h[2]), bf2f(h[3]));
+      } else {
+        gg[r] = *reinterpret_cast<const float4*>(g + i);
+      }
+      mm[r] = *reinterpret_cast<const float4*>(m + i);
+      vv[r] = *reinterpret_cast<const float4*>(v + i);
     }
-    *reinterpret_cast<float4*>(p + i) = pp;
-    *reinterpret_cast<float4*>(m + i) = mm;
-    *reinterpret_cast<float4*>(v + i) = vv;
-    if (pb) *reinterpret_cast<bf16x4*>(pb + i) = ob;
-    if (ph && i >= h_lo && i < h_hi) {   // fp16 shadow of the BERT range (chunk-uniform branch)
-      bf16x4 oh;
-      oh[0] = to16<true>(pp.x); oh[1] = to16<true>(pp.y); oh[2] = to16<true>(pp.z); oh[3] = to16<true>(pp.w);
-      *reinterpret_cast<bf16x4*>(ph + (i - h_lo)) = oh;
+    float q = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long long i = base + r * 256;
+      float* pa = &pp[r].x; const float* ga = &gg[r].x; float* ma = &mm[r].x; float* va = &vv[r].x;
+      bf16x4 ob;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float gr = ga[j] * gscale + rc * pa[j];
+        ma[j] = b1 * ma[j] + (1.0f - b1) * gr;
+        va[j] = b2 * va[j] + (1.0f - b2) * gr * gr;
+        const float np = pa[j] * decay - step * ma[j] / (sqrtf(va[j]) * isb2 + eps);
+        pa[j] = np;
+        ob[j] = f2bf(np);
+      }
+      *reinterpret_cast<float4*>(p + i) = pp[r];
+      *reinterpret_cast<float4*>(m + i) = mm[r];
+      *reinterpret_cast<float4*>(v + i) = vv[r];
+      if (pb) *reinterpret_cast<bf16x4*>(pb + i) = ob;
+      if (ph && i >= h_lo && i < h_hi) {   // fp16 shadow of the BERT range (chunk-uniform branch)
+        bf16x4 oh;
+        oh[0] = to16<true>(pp[r].x); oh[1] = to16<true>(pp[r].y); oh[2] = to16<true>(pp[r].z); oh[3] = to16<true>(pp[r].w);
+        *reinterpret_cast<bf16x4*>(ph + (i - h_lo)) = oh;
+      }
+      q += pp[r].x * pp[r].x + pp[r].y * pp[r].y + pp[r].z * pp[r].z + pp[r].w * pp[r].w;
     }
-    q += pp.x * pp.x + pp.y * pp.y + pp.z * pp.z + pp.w * pp.w;
-    if (chunk_sq) chunk_flush(c);
+    if (sumsq_next) {
+      q = wave_sum(q);
+      if (lane == 0) {
+        if (chunk_sq) chunk_sq[c] = q;
+        else atomicAdd(sumsq_next + t, q);
+      }
+    }
   }
-  if (!chunk_sq) flush();
 }
 
 }  // namespace
@@ -164,7 +156,7 @@ extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, con
   if (p_f16 && (f16_lo % 1024 || f16_hi % 1024 || f16_lo < 0 || f16_hi < f16_lo))
     return lrce_fail(LRCE_E_ARG, "adamw_step: f16 shadow range [%lld, %lld) not chunk aligned", (long long)f16_lo, (long long)f16_hi);
   if (n_chunks > 0)
-    adamw_kernel<<<(n_chunks + ADAMW_CH - 1) / ADAMW_CH, 256, 0, static_cast<hipStream_t>(stream)>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq,
+    adamw_kernel<<<(n_chunks + 4 * ADAMW_CPW - 1) / (4 * ADAMW_CPW), 256, 0, static_cast<hipStream_t>(stream)>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq,
                                                                          reinterpret_cast<bf16*>(p_bf16), n_chunks, beta1, beta2, eps,
                                                                          weight_decay, grad_scale, reg, bc1, bc2, step, sumsq_next,
                                                                          reinterpret_cast<bf16*>(p_f16), f16_lo, f16_hi,

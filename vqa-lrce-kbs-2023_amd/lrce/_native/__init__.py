@@ -71,6 +71,16 @@ class MhaDesc(ctypes.Structure):
     ]
 
 
+class LnPrologue(ctypes.Structure):
+    _fields_ = [
+        ("mode", ctypes.c_int32), ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("eps", ctypes.c_float),
+        ("x", ctypes.c_void_p), ("ld_x", ctypes.c_int64), ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p),
+        ("y_out", ctypes.c_void_p), ("ld_y", ctypes.c_int64), ("y2_out", ctypes.c_void_p), ("ld_y2", ctypes.c_int64),
+        ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
+        ("drop_p", ctypes.c_float), ("drop_group", ctypes.c_int32), ("drop_seed", ctypes.c_uint64),
+    ]
+
+
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = 1, 2, 4, 8
 EPI_OUT_F32, EPI_ATOMIC, EPI_ACCUM, EPI_AUX_OUT, EPI_OUT_BOTH = 16, 32, 64, 128, 256
 EPI_BIAS_GRAD = 512
@@ -83,6 +93,7 @@ _U64 = ctypes.c_uint64
 
 _SIGS = {
     "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
+    "lrce_gemm_ln": [ctypes.POINTER(GemmDesc), ctypes.POINTER(LnPrologue), _P],
     "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _I64,
                            _P],

@@ -100,10 +100,11 @@ def _chk(t, dtype=None, name="tensor"):
 def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, flags=0, bias=None,
          aux=None, ld_aux=0, aux_out=None, ld_aux_out=0, a_map=None, c_map=None, alpha=1.0, split_k=1,
          scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, a_row_scale=None, a_rows_per_scale=1,
-         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None, f16=False):
+         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None, f16=False, ln=None):
     """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc.  drop = (p, seed, group):
     nn.Dropout fused into the epilogue (exact-f32 skinny path; same mask as dropout()).  f16: every
-    16-bit tensor (A, B, 16-bit C, aux_out) is torch.float16 (the BERT forward)."""
+    16-bit tensor (A, B, 16-bit C, aux_out) is torch.float16 (the BERT forward).  ln: a LayerNorm
+    prologue on A (ln_fwd_prologue / ln_bwd_prologue -> lrce_gemm_ln)."""
     _chk(a, None, "A"); _chk(b, None, "B"); _chk(c, None, "C")
     a_f32 = a.dtype == F32
     b_f32 = b.dtype == F32
@@ -135,10 +136,42 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         d.workspace, d.workspace_elems = ptr(workspace), workspace.numel()
     if drop is not None and drop[0] > 0:
         d.drop_p, d.drop_seed, d.drop_group = float(drop[0]), drop[1] & (2 ** 64 - 1), int(drop[2])
+    if ln is not None:
+        _timed("gemm_f32", c, lambda: call("lrce_gemm_ln", ctypes.byref(d), ctypes.byref(ln), stream_of(c)),
+               flops=2.0 * m * n * k, key=(m, n, k, 1, "AK", "BK" if b_kmajor else "BN", f"ln{ln.mode}", 1, flags))
+        return
     _timed("gemm_f32" if b_f32 else "gemm", c, lambda: call("lrce_gemm", ctypes.byref(d), stream_of(c)),
            flops=2.0 * m * n * k * batch,
            key=(m, n, k, batch, "AK" if a_kmajor else "AM", "BK" if b_kmajor else "BN", "a32" if a_f32 else "a16",
                 split_k, flags))
+
+
+def ln_fwd_prologue(gamma, beta, eps, *, mean=None, rstd=None, y_out=None):
+    """LayerNorm of the GEMM's A rows inside lrce_gemm_ln (mode 1): the GEMM consumes LN(A); mean /
+    rstd [m] and the normalised rows (y_out, f32) are written when given."""
+    pro = N.LnPrologue()
+    pro.mode, pro.gamma, pro.beta, pro.eps = 1, ptr(gamma), ptr(beta), float(eps)
+    pro.mean, pro.rstd = ptr(mean), ptr(rstd)
+    if y_out is not None:
+        pro.y_out, pro.ld_y = ptr(y_out), y_out.shape[-1]
+    return pro
+
+
+def ln_bwd_prologue(x, mean, rstd, gamma, *, dgamma=None, dbeta=None, y_out=None, y2_out=None, drop=None):
+    """LayerNorm backward of the GEMM's A rows (= dy) inside lrce_gemm_ln (mode 2): the GEMM consumes
+    dropout_bwd(LN_bwd(dy)) (drop = (p, seed, group)); dx -> y_out, dropped dx -> y2_out, dgamma /
+    dbeta accumulated (all optional)."""
+    pro = N.LnPrologue()
+    pro.mode, pro.gamma = 2, ptr(gamma)
+    pro.x, pro.ld_x, pro.mean, pro.rstd = ptr(x), x.shape[-1], ptr(mean), ptr(rstd)
+    pro.dgamma, pro.dbeta = ptr(dgamma), ptr(dbeta)
+    if y_out is not None:
+        pro.y_out, pro.ld_y = ptr(y_out), y_out.shape[-1]
+    if y2_out is not None:
+        pro.y2_out, pro.ld_y2 = ptr(y2_out), y2_out.shape[-1]
+    if drop is not None and drop[0] > 0:
+        pro.drop_p, pro.drop_seed, pro.drop_group = float(drop[0]), drop[1] & (2 ** 64 - 1), int(drop[2])
+    return pro
 
 
 def _split_for(m_out, n_out, k_red):
@@ -157,12 +190,12 @@ def _skinny_drop_ok(x, w, M, a_map=None):
 
 def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None, resid=None, c_map=None,
            a_map=None, rows=None, scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, bf16_shadow=None,
-           drop=None):
+           drop=None, ln=None):
     f16 = x.dtype == F16
     """y = x W^T (+b) [gelu] [*row_scale] [dropout] [+resid]; x [M,K] bf16/f32, W [N,K] bf16 (or f32:
     exact path).  drop = (p, seed, group): fused into the skinny epilogue, else a dropout launch."""
     M = rows if rows is not None else x.shape[0]
-    if drop is not None and drop[0] > 0 and not (_skinny_drop_ok(x, w, M, a_map) and c_map is None):
+    if drop is not None and drop[0] > 0 and ln is None and not (_skinny_drop_ok(x, w, M, a_map) and c_map is None):
         y = linear(x, w, bias, out=out if resid is None else None, out_f32=out_f32, gelu=gelu, pre_out=pre_out,
                    c_map=c_map, a_map=a_map, rows=rows, scale_cols=scale_cols, scale_val=scale_val,
                    row_scale=row_scale, rows_per_scale=rows_per_scale)
@@ -189,17 +222,17 @@ def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None
     aux_out = pre_out if gelu else bf16_shadow
     gemm(x, w, out, M, Nn, K, flags=flags, bias=bias, aux=aux, ld_aux=Nn, aux_out=aux_out, ld_aux_out=Nn,
          a_map=a_map, c_map=c_map, scale_cols=scale_cols, scale_val=scale_val, row_scale=row_scale,
-         rows_per_scale=rows_per_scale, drop=drop, f16=f16)
+         rows_per_scale=rows_per_scale, drop=drop, f16=f16, ln=ln)
     return out
 
 
 def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows=None, a_row_scale=None,
-              a_rows_per_scale=1, accumulate=False, resid=None, drop=None):
+              a_rows_per_scale=1, accumulate=False, resid=None, drop=None, ln=None):
     """dX = dY W (+ resid) ; dY [M,N] (bf16/f32), W [N,K] bf16 -> [M,K]; optional *gelu'(pre), and
     drop = (p, seed, group): the dropout backward mask (fused on the skinny path, else a launch)."""
     M = rows if rows is not None else dy.shape[0]
-    if drop is not None and drop[0] > 0 and not (_skinny_drop_ok(dy, w, M, a_map) and not accumulate
-                                                 and resid is None and a_row_scale is None):
+    if drop is not None and drop[0] > 0 and ln is None and not (_skinny_drop_ok(dy, w, M, a_map) and not accumulate
+                                                                and resid is None and a_row_scale is None):
         y = linear_dx(dy, w, out=out, out_f32=out_f32, dgelu_pre=dgelu_pre, a_map=a_map, rows=rows,
                       a_row_scale=a_row_scale, a_rows_per_scale=a_rows_per_scale, accumulate=accumulate, resid=resid)
         return dropout_bwd(y, drop[0], drop[1], out=y, group=drop[2])
@@ -216,7 +249,7 @@ def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows
         flags |= N.EPI_ACCUM if accumulate else N.EPI_OUT_F32
     gemm(dy, w, out, M, K, Nn, a_kmajor=True, b_kmajor=False, lda=dy.shape[-1], ldb=K, flags=flags,
          aux=dgelu_pre if dgelu_pre is not None else resid, ld_aux=K, a_map=a_map, a_row_scale=a_row_scale,
-         a_rows_per_scale=a_rows_per_scale, drop=drop)
+         a_rows_per_scale=a_rows_per_scale, drop=drop, ln=ln)
     return out
 
 

@@ -97,9 +97,9 @@ class TransformerDecoder(nn.Module):
 
 # ----------------------------------------------------------------------------------- decoder
 class _Step:
-    """Saved activations of one (step, layer)."""
-    __slots__ = ("x0", "sad", "x1p", "m1", "r1", "x1", "q", "ctx", "lse", "desc", "x2p", "m2", "r2", "x2", "pre",
-                 "gd", "x3p", "m3", "r3")
+    """Saved activations of one (step, layer).  m3 / r3 (the stats of this layer's norm3) are written
+    by the launch that consumes LN3's output: the next layer's first GEMM, or the step tail."""
+    __slots__ = ("x1p", "m1", "r1", "q", "ctx", "lse", "desc", "x2p", "m2", "r2", "pre", "x3p", "m3", "r3")
 
 
 class _LayerActs:
@@ -122,71 +122,83 @@ class _LayerGrads:
             setattr(self, name, torch.empty(S, Bq, FF if name == "dgp" else E, device=dev))
 
 
-def _layer_fwd(lay, flat, x0, kvv, kvt, step, S, Lt, nmc, p, seed, save, acts, x3_out=None):
-    """One TransformerDecoderLayer (post-norm) on the summary-token rows x0 (Bq, E) f32 (= acts.x0[step]).
-    Query-side linears run on the exact-f32 MFMA path with the f32 master weights (M = Bq is tiny,
-    the recurrence is precision-critical); only the memory K/V (big-M GEMMs) are bf16."""
+def _layer_fwd(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_prev):
+    """One TransformerDecoderLayer (post-norm) of recurrent step `step`.  The post-norm LayerNorms are
+    folded into the GEMM that consumes their output (lrce_gemm_ln): norm1 into the cross-attention q
+    projection, norm2 into linear1, and this layer's INPUT LayerNorm (the previous layer's norm3,
+    `prev`) into the self-attention v projection (x_in is then the previous layer's pre-norm x3p and
+    its stats go to st_prev.m3 / r3).  Each such GEMM also materialises the normalised rows, which
+    the next residual add and the weight gradients read.  Query-side linears run on the exact-f32
+    MFMA path with the f32 master weights (M = Bq is tiny, the recurrence is precision-critical);
+    only the memory K/V (big-M GEMMs) are bf16.  Every dropout rides in the epilogue of the GEMM
+    producing its input."""
     sa, ca = lay.self_attn, lay.multihead_attn
-    # self-attention over one token: out_proj(dropout_head(v_proj(x)))
-    # (every dropout of the layer rides in the epilogue of the GEMM producing its input)
-    sad = K.linear(x0, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step],
-                   drop=(p, seed, E // NHEAD))
-    x1p = K.linear(sad, sa.out_proj.weight, sa.out_proj.bias, out_f32=True, resid=x0, drop=(p, seed + 1, 1))
-    x1, m1, r1 = K.layernorm(x1p, lay.norm1.weight, lay.norm1.bias, EPS, out=acts.x1[step])
-    # cross-attention to [video tokens of this step ; question tokens]
-    q = K.linear(x1, ca.in_proj_weight[:E], ca.in_proj_bias[:E], out_f32=True)
-    Bq = x0.shape[0]
-    ctx = acts.ctx[step]
-    lse = torch.empty(Bq, NHEAD, 1, device=x0.device)
+    Bq = x_in.shape[0]
+    dev = x_in.device
+    st = _Step()
+    x0 = acts.x0[step]
+    # self-attention over one token: out_proj(dropout_head(v_proj(x0)))
+    if prev is None:
+        sad = K.linear(x_in, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step],
+                       drop=(p, seed, E // NHEAD))
+    else:
+        st_prev.m3 = torch.empty(Bq, device=dev)
+        st_prev.r3 = torch.empty(Bq, device=dev)
+        pro = K.ln_fwd_prologue(prev.norm3.weight, prev.norm3.bias, EPS, mean=st_prev.m3, rstd=st_prev.r3, y_out=x0)
+        sad = K.linear(x_in, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step],
+                       drop=(p, seed, E // NHEAD), ln=pro)
+    st.x1p = K.linear(sad, sa.out_proj.weight, sa.out_proj.bias, out_f32=True, resid=x0, drop=(p, seed + 1, 1))
+    # cross-attention to [video tokens of this step ; question tokens]; norm1 in the q projection
+    st.m1, st.r1 = torch.empty(Bq, device=dev), torch.empty(Bq, device=dev)
+    x1 = acts.x1[step]
+    pro = K.ln_fwd_prologue(lay.norm1.weight, lay.norm1.bias, EPS, mean=st.m1, rstd=st.r1, y_out=x1)
+    st.q = K.linear(st.x1p, ca.in_proj_weight[:E], ca.in_proj_bias[:E], out_f32=True, ln=pro)
+    st.ctx = acts.ctx[step]
+    st.lse = torch.empty(Bq, NHEAD, 1, device=dev)
     lv = 150
     kv1 = kvv[step * lv * 2 * E:]
-    desc = K.mha_desc(q, 1, k1=kv1, v1=kv1[E:], lk1=lv, ld_kv1=2 * E, stride_kv1_b=S * lv * 2 * E, kv1_bdiv=nmc,
-                      k2=kvt if Lt else None, v2=kvt[E:] if Lt else None, lk2=Lt, ld_kv2=2 * E,
-                      stride_kv2_b=Lt * 2 * E, kv2_bdiv=1, out=ctx, lse=lse,
-                      B=Bq, H=NHEAD, scale=(E // NHEAD) ** -0.5, drop_p=p, seed=seed + 2)
-    K.mha_fwd(desc, ctx)
-    x2p = K.linear(ctx, ca.out_proj.weight, ca.out_proj.bias, out_f32=True, resid=x1, drop=(p, seed + 3, 1))
-    x2, m2, r2 = K.layernorm(x2p, lay.norm2.weight, lay.norm2.bias, EPS, out=acts.x2[step])
-    # FFN: linear2(dropout(gelu(linear1(x))))
-    pre = torch.empty(Bq, FF, dtype=torch.bfloat16, device=x0.device)
-    gd = K.linear(x2, lay.linear1.weight, lay.linear1.bias, gelu=True, pre_out=pre, out=acts.gd[step],
-                  drop=(p, seed + 4, 1))
-    x3p = K.linear(gd, lay.linear2.weight, lay.linear2.bias, out_f32=True, resid=x2, drop=(p, seed + 5, 1))
-    x3, m3, r3 = K.layernorm(x3p, lay.norm3.weight, lay.norm3.bias, EPS, out=x3_out, out_f32=True)
-    if save is not None:
-        st = _Step()
-        st.x0, st.sad, st.x1p, st.m1, st.r1, st.x1, st.q, st.ctx, st.lse, st.desc = \
-            x0, sad, x1p, m1, r1, x1, q, ctx, lse, desc
-        st.x2p, st.m2, st.r2, st.x2, st.pre, st.gd, st.x3p, st.m3, st.r3 = x2p, m2, r2, x2, pre, gd, x3p, m3, r3
-        save.append(st)
-    return x3
+    st.desc = K.mha_desc(st.q, 1, k1=kv1, v1=kv1[E:], lk1=lv, ld_kv1=2 * E, stride_kv1_b=S * lv * 2 * E, kv1_bdiv=nmc,
+                         k2=kvt if Lt else None, v2=kvt[E:] if Lt else None, lk2=Lt, ld_kv2=2 * E,
+                         stride_kv2_b=Lt * 2 * E, kv2_bdiv=1, out=st.ctx, lse=st.lse,
+                         B=Bq, H=NHEAD, scale=(E // NHEAD) ** -0.5, drop_p=p, seed=seed + 2)
+    K.mha_fwd(st.desc, st.ctx)
+    st.x2p = K.linear(st.ctx, ca.out_proj.weight, ca.out_proj.bias, out_f32=True, resid=x1, drop=(p, seed + 3, 1))
+    # FFN: linear2(dropout(gelu(linear1(norm2(x2p))))); norm2 in linear1
+    st.m2, st.r2 = torch.empty(Bq, device=dev), torch.empty(Bq, device=dev)
+    x2 = acts.x2[step]
+    pro = K.ln_fwd_prologue(lay.norm2.weight, lay.norm2.bias, EPS, mean=st.m2, rstd=st.r2, y_out=x2)
+    st.pre = torch.empty(Bq, FF, dtype=torch.bfloat16, device=dev)
+    gd = K.linear(st.x2p, lay.linear1.weight, lay.linear1.bias, gelu=True, pre_out=st.pre, out=acts.gd[step],
+                  drop=(p, seed + 4, 1), ln=pro)
+    st.x3p = K.linear(gd, lay.linear2.weight, lay.linear2.bias, out_f32=True, resid=x2, drop=(p, seed + 5, 1))
+    return st
 
 
 def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step):
-    """Backward of _layer_fwd; accumulates into the layer's dK/dV buffers and leaves the dY of its
-    six query-side GEMMs in grads[.][step] (weight gradients: _layer_wgrads), returns d(x0)."""
+    """Backward of _layer_fwd from dx3 = d(norm3 output).  Each LayerNorm backward (+ the dropout
+    backward in front of it) is folded into the GEMM that consumes its result (lrce_gemm_ln mode 2),
+    which also materialises dx (the next residual) and the dropped dx (the weight-gradient dY) and
+    accumulates the LN weight / bias gradients.  Accumulates into the layer's dK/dV buffers, leaves
+    the dY of its six query-side GEMMs in grads[.][step], returns d(x0)."""
     sa, ca = lay.self_attn, lay.multihead_attn
     dx3p = torch.empty_like(st.x3p)
-    K.layernorm_bwd(dx3, st.x3p, st.m3, st.r3, lay.norm3.weight, dx3p, dw=_g(flat, lay.norm3.weight),
-                    db=_g(flat, lay.norm3.bias))
-    df = K.dropout_bwd(dx3p, p, seed + 5, out=grads.df[step])
-    dgp = K.linear_dx(df, lay.linear2.weight, dgelu_pre=st.pre, out=grads.dgp[step], drop=(p, seed + 4, 1))
+    pro = K.ln_bwd_prologue(st.x3p, st.m3, st.r3, lay.norm3.weight, dgamma=_g(flat, lay.norm3.weight),
+                            dbeta=_g(flat, lay.norm3.bias), y_out=dx3p, y2_out=grads.df[step], drop=(p, seed + 5, 1))
+    dgp = K.linear_dx(dx3, lay.linear2.weight, dgelu_pre=st.pre, out=grads.dgp[step], drop=(p, seed + 4, 1), ln=pro)
     dx2 = K.linear_dx(dgp, lay.linear1.weight, resid=dx3p)
     dx2p = torch.empty_like(st.x2p)
-    K.layernorm_bwd(dx2, st.x2p, st.m2, st.r2, lay.norm2.weight, dx2p, dw=_g(flat, lay.norm2.weight),
-                    db=_g(flat, lay.norm2.bias))
-    dcao = K.dropout_bwd(dx2p, p, seed + 3, out=grads.dcao[step])
-    dctx = K.linear_dx(dcao, ca.out_proj.weight)
+    pro = K.ln_bwd_prologue(st.x2p, st.m2, st.r2, lay.norm2.weight, dgamma=_g(flat, lay.norm2.weight),
+                            dbeta=_g(flat, lay.norm2.bias), y_out=dx2p, y2_out=grads.dcao[step], drop=(p, seed + 3, 1))
+    dctx = K.linear_dx(dx2, ca.out_proj.weight, ln=pro)
     dq = grads.dq[step]
     K.mha_bwd(st.desc, dout=dctx, dq=dq, dk1=dkvv_step, dv1=dkvv_step[E:], ld_dkv1=2 * E,
               stride_dkv1_b=S * 150 * 2 * E, dk2=dkvt if Lt else None, dv2=dkvt[E:] if Lt else None,
               ld_dkv2=2 * E, stride_dkv2_b=Lt * 2 * E)
     dx1 = K.linear_dx(dq, ca.in_proj_weight[:E], resid=dx2p)
     dx1p = torch.empty_like(st.x1p)
-    K.layernorm_bwd(dx1, st.x1p, st.m1, st.r1, lay.norm1.weight, dx1p, dw=_g(flat, lay.norm1.weight),
-                    db=_g(flat, lay.norm1.bias))
-    dsao = K.dropout_bwd(dx1p, p, seed + 1, out=grads.dsao[step])
-    dsav = K.linear_dx(dsao, sa.out_proj.weight, out=grads.dsav[step], drop=(p, seed, E // NHEAD))
+    pro = K.ln_bwd_prologue(st.x1p, st.m1, st.r1, lay.norm1.weight, dgamma=_g(flat, lay.norm1.weight),
+                            dbeta=_g(flat, lay.norm1.bias), y_out=dx1p, y2_out=grads.dsao[step], drop=(p, seed + 1, 1))
+    dsav = K.linear_dx(dx1, sa.out_proj.weight, out=grads.dsav[step], drop=(p, seed, E // NHEAD), ln=pro)
     return K.linear_dx(dsav, sa.in_proj_weight[2 * E:], resid=dx1p)
 
 
@@ -230,13 +242,17 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         saves = []
         fused = []
         for i in range(S):
-            x = s
             step_saves = []
+            x_in, prev = s, None
             for l, lay in enumerate(layers):
-                x = _layer_fwd(lay, flat, x, kvv[l].view(-1), kvt[l].view(-1) if Lt else None, i, S, Lt, nmc, p,
-                               seed + 64 * (i * nL + l), step_saves, acts[l],
-                               x3_out=acts[l + 1].x0[i] if l + 1 < nL else None)
-            tsum = K.dropout(x, 0.0, 0, res=s)
+                st = _layer_fwd(lay, prev, x_in, kvv[l].view(-1), kvt[l].view(-1) if Lt else None, i, S, Lt, nmc, p,
+                                seed + 64 * (i * nL + l), acts[l], step_saves[-1] if step_saves else None)
+                step_saves.append(st)
+                x_in, prev = st.x3p, lay
+            # step tail: x3 = norm3(x3p) of the last layer, s <- dropout(LN_f(x3 + s))
+            last = step_saves[-1]
+            x3, last.m3, last.r3 = K.layernorm(last.x3p, prev.norm3.weight, prev.norm3.bias, EPS, out_f32=True)
+            tsum = K.dropout(x3, 0.0, 0, res=s)
             u, mu, ru = K.layernorm(tsum, ft.fusion_layer_norm.weight, ft.fusion_layer_norm.bias, EPS, out_f32=True)
             s = K.dropout(u, p, seed + 7 + 64 * 1000 * (i + 1), out=acts[0].x0[i + 1] if i + 1 < S else None)
             saves.append(step_saves)
@@ -262,7 +278,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             dt = torch.empty_like(tsum)
             K.layernorm_bwd(du, tsum, mu, ru, ft.fusion_layer_norm.weight, dt, dw=_g(flat, ft.fusion_layer_norm.weight),
                             db=_g(flat, ft.fusion_layer_norm.bias))
-            dx = dt
+            dx = dt   # d(norm3 output of the last layer)
             for l in reversed(range(len(layers))):
                 dx = _layer_bwd(layers[l], flat, saves[i][l], dx, dkvv[l].view(-1)[i * 150 * 2 * E:],
                                 dkvt[l].view(-1) if Lt else None, S, Lt, p, seed + 64 * (i * len(layers) + l),
