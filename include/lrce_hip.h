@@ -256,6 +256,10 @@ typedef struct LrceMhaDesc {
   /* forward only: 1 = q, k, v and out are IEEE fp16 (BERT self-attention under the reference's
    * fp16 autocast); f16 MFMA forms.  The backward reads bf16. */
   int32_t f16;
+  /* single-query backward only: 1 = the first key segment's dK / dV rows are STORED, not accumulated
+   * (every row has one writer in this launch and no earlier contribution: kv1_bdiv == 1 and a memory
+   * that is distinct per call, e.g. the video tokens of one recurrent step) — no zero fill, no read. */
+  int32_t dkv1_store;
 } LrceMhaDesc;
 
 int lrce_mha_fwd(const LrceMhaDesc* desc, void* stream);

@@ -335,8 +335,9 @@ __global__ void __launch_bounds__(256) mha1_bwd_kernel(MhaP P) {
         const long long o = (long long)(b / d.kv2_bdiv) * d.stride_dkv2_b + (long long)(j - d.lk1) * d.ld_dkv2 + h * D + lane;
         pk[u] = d.dk2 + o; pv[u] = d.dv2 + o; at[u] = at2;
       }
-      okk[u] = at[u] ? 0.f : *pk[u];
-      ovv[u] = at[u] ? 0.f : *pv[u];
+      const bool fresh = d.dkv1_store && j < d.lk1;   // stored, not accumulated
+      okk[u] = (at[u] || fresh) ? 0.f : *pk[u];
+      ovv[u] = (at[u] || fresh) ? 0.f : *pv[u];
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
@@ -711,6 +712,8 @@ extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
 extern "C" int lrce_mha_bwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, true)) return rc;
   if (d->f16) return lrce_fail(LRCE_E_ARG, "mha_bwd: the backward reads bf16 (cast the fp16 forward tensors)");
+  if (d->dkv1_store && (d->Lq != 1 || d->kv1_bdiv != 1 || !aligned_rows(d)))
+    return lrce_fail(LRCE_E_ARG, "mha_bwd: dkv1_store needs the single-query path with kv1_bdiv == 1");
   MhaP p{*d, lrce_rng_offset()};
   if (short_self(d)) {
     const unsigned nb = (d->B * d->H + 1) / 2;

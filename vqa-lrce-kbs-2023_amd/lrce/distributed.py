@@ -68,6 +68,7 @@ class GradReducer:
         self.done = set()
         self.launched = [False] * len(self.buckets)
         self.handles = []
+        self.streams = [set() for _ in self.buckets]   # streams whose kernels wrote each bucket
 
     def reduced_grad(self):
         """The tensor the optimizer reads as the (summed) gradient: flat.grad, or its bf16 mirror."""
@@ -82,6 +83,13 @@ class GradReducer:
             return
         self.launched[bi] = True
         s, e, _ = self.buckets[bi]
+        # a bucket straddling the text (side stream) and video / fusion branches: the stream that
+        # completes it waits for the other writers before the cast / all-reduce reads it
+        if self.flat.grad.is_cuda:
+            cur = torch.cuda.current_stream(self.flat.grad.device)
+            for st in self.streams[bi]:
+                if st != cur:
+                    cur.wait_stream(st)
         if self.grad16 is not None:
             K.cast_bf16(self.flat.grad[s:e], self.grad16[s:e])
         if self.capturing:
@@ -90,12 +98,15 @@ class GradReducer:
             self.handles.append(dist.all_reduce(self._buf(bi), group=self.group, async_op=True))
 
     def notify(self, params):
+        cur = torch.cuda.current_stream(self.flat.grad.device) if self.flat.grad.is_cuda else None
         for p in params:
             k = id(p)
             if k in self.done or k not in self.param_bucket:
                 continue
             self.done.add(k)
             bi = self.param_bucket[k]
+            if cur is not None:
+                self.streams[bi].add(cur)
             self.pending[bi] -= 1
             if self.pending[bi] == 0:
                 self._launch(bi)

@@ -93,7 +93,7 @@ class BertPooler(nn.Module):
 # ----------------------------------------------------------------------------------- autograd
 class _EmbedFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, types, emb, flat, p, seed, *params):
+    def forward(ctx, ids, types, emb, flat, p, seed, join_token, *params):
         B, L = ids.shape
         rows = B * L
         dev = ids.device
@@ -121,7 +121,10 @@ class _EmbedFn(torch.autograd.Function):
             K.bert_embed_bwd(ds, ids, types, gw, gp, gt, s.shape[0], ctx.L, HIDDEN)
         ctx.save = None
         flat.notify(emb.parameters())
-        return (None,) * (6 + len(ctx.needs_input_grad[6:]))
+        # join_token (a leaf): its gradient makes autograd join this stream into the caller's at the
+        # end of backward (the text branch may run on a side stream, E2EBase.forward)
+        dtok = torch.zeros(1, device=dy.device) if ctx.needs_input_grad[6] else None
+        return (None,) * 6 + (dtok,) + (None,) * len(ctx.needs_input_grad[7:])
 
 
 class _LayerFn(torch.autograd.Function):
@@ -244,7 +247,7 @@ class BertModel(nn.Module):
         """Parameters whose fp16 shadow the forward reads (the encoder linears; runtime.bind)."""
         return list(self.encoder.parameters())
 
-    def forward(self, input_ids, attention_mask=None, token_type_ids=None):
+    def forward(self, input_ids, attention_mask=None, token_type_ids=None, join_token=None):
         flat = ensure(self)
         B, L = input_ids.shape
         dev = input_ids.device
@@ -254,7 +257,7 @@ class BertModel(nn.Module):
         p = self.hidden_dropout if self.training else 0.0
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
         anchor = [t for t in self.embeddings.parameters()]
-        x = _EmbedFn.apply(ids, types, self.embeddings, flat, p, seed, *anchor)
+        x = _EmbedFn.apply(ids, types, self.embeddings, flat, p, seed, join_token, *anchor)
         for i, layer in enumerate(self.encoder.layer):
             x = _LayerFn.apply(x, mask, layer, flat, p, seed + 16 * (i + 1), B, L, *layer.parameters())
         return x.view(B, L, HIDDEN)
@@ -315,5 +318,5 @@ class TextExtractor(nn.Module):
                 warnings.warn(f"BERT weights {bert_dir} not found: the text encoder keeps its random "
                               "initialisation", stacklevel=2)
 
-    def forward(self, input_ids, attention_mask, token_type_ids):
-        return self.bert(input_ids, attention_mask, token_type_ids)
+    def forward(self, input_ids, attention_mask, token_type_ids, join_token=None):
+        return self.bert(input_ids, attention_mask, token_type_ids, join_token=join_token)

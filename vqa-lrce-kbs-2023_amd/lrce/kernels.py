@@ -466,7 +466,9 @@ def mha_rebind(desc, *, q, k1, v1, out):
 
 
 def mha_bwd(desc, *, dout, dq, dk1, dv1, ld_dkv1, stride_dkv1_b, dk2=None, dv2=None, ld_dkv2=0, stride_dkv2_b=0,
-            ld_dq=None):
+            ld_dq=None, dkv1_store=False):
+    """dkv1_store: the first segment's dK / dV rows are written, not accumulated (LrceMhaDesc)."""
+    desc.dkv1_store = int(dkv1_store)
     desc.dout, desc.dq = ptr(dout), ptr(dq)
     desc.ld_dq = ld_dq if ld_dq is not None else desc.H * desc.d
     desc.dk1, desc.dv1, desc.ld_dkv1, desc.stride_dkv1_b = ptr(dk1), ptr(dv1), ld_dkv1, stride_dkv1_b

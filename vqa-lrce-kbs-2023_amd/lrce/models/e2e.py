@@ -18,7 +18,7 @@ import torch.nn as nn
 from ..feature_extractor.text import TextExtractor, BERT_DIR
 from ..feature_extractor.video import VideoExtractor, SWIN_B_CKPT
 from .. import kernels as K
-from ..runtime import prepare
+from ..runtime import prepare, side_stream
 from .fusionv3 import LRCEOpenEnded, LRCEMultipleChoice, LRCECount
 
 
@@ -41,8 +41,8 @@ class E2EBase(nn.Module):
         if self.HEAD is not None:
             self.fusion_model = self.HEAD(*_head_args(*head_args))
 
-    def extract_text_features(self, texts, attention_mask, texts_type_ids):
-        return self.text_extractor(texts, attention_mask, texts_type_ids)
+    def extract_text_features(self, texts, attention_mask, texts_type_ids, join_token=None):
+        return self.text_extractor(texts, attention_mask, texts_type_ids, join_token=join_token)
 
     @property
     def pretrained_loaded(self):
@@ -63,12 +63,28 @@ class E2EBase(nn.Module):
         return self.video_extractor(video_clips)
 
     def forward(self, video_clips, texts, texts_attention_mask, texts_type_ids):
+        """The two extractors are independent until the fusion head: BERT runs on a side stream
+        while Swin runs on the current one (forward and, through autograd's stream semantics,
+        backward); a leaf join token consumed by the text branch makes autograd join the side stream
+        back at the end of backward, and the fusion head waits for the text features."""
         flat = prepare(self)
         if self.training:
             K.rng_advance(flat.device)   # fresh dropout masks per step, also under HIP-graph replay
-        return self.fusion_model(self.extract_video_features(video_clips),
-                                 self.extract_text_features(texts, texts_attention_mask, texts_type_ids),
-                                 texts_attention_mask)
+        main = torch.cuda.current_stream(flat.device)
+        side = side_stream(flat.device)
+        tok = None
+        if torch.is_grad_enabled():
+            tok = getattr(self, "_join_token", None)
+            if tok is None or tok.device != flat.device:
+                tok = torch.zeros(1, device=flat.device, requires_grad=True)
+                object.__setattr__(self, "_join_token", tok)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            t = self.extract_text_features(texts, texts_attention_mask, texts_type_ids, join_token=tok)
+        v = self.extract_video_features(video_clips)
+        main.wait_stream(side)
+        t.record_stream(main)
+        return self.fusion_model(v, t, texts_attention_mask)
 
 
 # Constructor defaults differ per task (question length 30 vs 40, one output for counting), so each
@@ -92,10 +108,11 @@ class E2EMultipleChoice(E2EBase):
         super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
                          frame_sample_size, temporal_scale, text_seq_len, **pretrained)
 
-    def extract_text_features(self, texts, attention_mask, texts_type_ids):
+    def extract_text_features(self, texts, attention_mask, texts_type_ids, join_token=None):
         """e2e.py:77-81: the 5 question+answer sequences go through BERT as B*5 rows."""
         b, n_choice, seq = texts.shape
-        feats = self.text_extractor(texts.flatten(0, 1), attention_mask.flatten(0, 1), texts_type_ids.flatten(0, 1))
+        feats = self.text_extractor(texts.flatten(0, 1), attention_mask.flatten(0, 1), texts_type_ids.flatten(0, 1),
+                                    join_token=join_token)
         return feats.view(b, n_choice, seq, -1)
 
 

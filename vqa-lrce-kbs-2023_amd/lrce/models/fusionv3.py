@@ -191,9 +191,10 @@ def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step)
                             dbeta=_g(flat, lay.norm2.bias), y_out=dx2p, y2_out=grads.dcao[step], drop=(p, seed + 3, 1))
     dctx = K.linear_dx(dx2, ca.out_proj.weight, ln=pro)
     dq = grads.dq[step]
+    # the video rows of one step have one writer (nmc == 1: no answer choices share them)
     K.mha_bwd(st.desc, dout=dctx, dq=dq, dk1=dkvv_step, dv1=dkvv_step[E:], ld_dkv1=2 * E,
               stride_dkv1_b=S * 150 * 2 * E, dk2=dkvt if Lt else None, dv2=dkvt[E:] if Lt else None,
-              ld_dkv2=2 * E, stride_dkv2_b=Lt * 2 * E)
+              ld_dkv2=2 * E, stride_dkv2_b=Lt * 2 * E, dkv1_store=st.desc.kv1_bdiv == 1)
     dx1 = K.linear_dx(dq, ca.in_proj_weight[:E], resid=dx2p)
     dx1p = torch.empty_like(st.x1p)
     pro = K.ln_bwd_prologue(st.x1p, st.m1, st.r1, lay.norm1.weight, dgamma=_g(flat, lay.norm1.weight),
@@ -268,7 +269,10 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         B, S, nmc, Bq, Lt = ctx.dims
         layers = ft.transformer.layers
         dev = ds.device
-        dkvv = [torch.zeros(B * S * 150, 2 * E, device=dev) for _ in layers]
+        # video K/V gradients: written once per row by the step's attention backward (OE / Count), or
+        # accumulated by the answer choices sharing the row (MC: atomics onto zeros)
+        alloc = torch.zeros if nmc > 1 else torch.empty
+        dkvv = [alloc(B * S * 150, 2 * E, device=dev) for _ in layers]
         dkvt = [torch.zeros(Bq * Lt, 2 * E, device=dev) if Lt else None for _ in layers]
         ds = ds.contiguous()
         grads = [_LayerGrads(S, Bq, dev) for _ in layers]

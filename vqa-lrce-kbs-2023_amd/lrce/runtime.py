@@ -73,3 +73,17 @@ def ensure(module):
 
 def needs_grad(*tensors):
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
+
+
+_SIDE_STREAMS = {}
+
+
+def side_stream(device):
+    """The second HIP stream of `device` that the text branch (BERT) runs on while the video branch
+    (Swin) runs on the current stream: the two extractors are independent until the fusion head, and
+    BERT's small latency-bound launches fill the gaps of Swin's large ones."""
+    key = torch.device(device).index
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return s
