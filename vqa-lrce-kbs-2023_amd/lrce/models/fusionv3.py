@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from .. import kernels as K
-from ..runtime import ensure
+from ..runtime import ensure, aux_stream, stream_anchor
 from .embedding import TextPosEmbed, VideoPosEmbed, VideoEmbedFn, TextEmbedFn, init_weight
 
 EPS = 1e-12
@@ -222,7 +222,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
     is the video tokens alone (FusionVideo.forward, fusionv3.py:70-88)."""
 
     @staticmethod
-    def forward(ctx, v, v16, t, t16, ft, flat, p, seed, B, S, nmc, *params):
+    def forward(ctx, v, v16, t, t16, ft, flat, p, seed, B, S, nmc, anchor, *params):
         dev = v.device
         layers = ft.transformer.layers
         Lt = t.shape[1] if t is not None else 0
@@ -289,32 +289,49 @@ class _RecurrentDecoderFn(torch.autograd.Function):
                                 grads[l], i)
             ds = K.dropout(dx, 0.0, 0, res=dt)   # s fed both the residual and the decoder
             saves[i] = None
-        for l, lay in enumerate(layers):
-            _layer_wgrads(lay, flat, acts[l], grads[l])
-        del grads, acts
-        gt = _g(flat, ft.summarization_token)
-        if gt is not None:
-            K.colsum(ds, gt.view(E))
+        main = torch.cuda.current_stream(dev)
         dv = torch.zeros(B * S * 150, E, device=dev)
         dtt = torch.zeros(Bq * Lt, E, device=dev) if Lt else None
-        dk16 = torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev)
-        dt16 = torch.empty(Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None
-        for l, lay in enumerate(layers):
-            ca = lay.multihead_attn
-            # the memory-side K/V gradients (accumulated in f32 over steps / answer choices) enter
-            # their big-M GEMMs as bf16, like every other activation gradient
-            K.cast_bf16(dkvv[l], dk16)
-            _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16, v16, rows=(E, 3 * E))
-            w = flat.w16(ca.in_proj_weight)[E:]
-            K.linear_dx(dk16, w, out=dv, accumulate=True)
+        # the memory-side K/V gradients (accumulated in f32 over steps / answer choices) enter their
+        # big-M GEMMs as bf16, like every other activation gradient
+        dk16 = [torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev) for _ in layers]
+        dt16 = [torch.empty(Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None for _ in layers]
+        for l in range(len(layers)):
+            K.cast_bf16(dkvv[l], dk16[l])
             if Lt:
-                K.cast_bf16(dkvt[l], dt16)
-                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16, t16, rows=(E, 3 * E))
-                K.linear_dx(dt16, w, out=dtt, accumulate=True)
+                K.cast_bf16(dkvt[l], dt16[l])
+        # The weight gradients (query-side outer products over all steps, memory K/V projections,
+        # the summary token) feed nothing downstream: a second stream runs them while the
+        # extractors' backward, which needs only dv / dt, proceeds on this one.  The forward's
+        # stream anchor joins that stream back at the end of backward.
+        wg = aux_stream(dev, "decoder_wgrad")
+        wg.wait_stream(main)
+        with torch.cuda.stream(wg):
+            for l, lay in enumerate(layers):
+                ca = lay.multihead_attn
+                _layer_wgrads(lay, flat, acts[l], grads[l])
+                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16[l], v16, rows=(E, 3 * E))
+                if Lt:
+                    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[l], t16, rows=(E, 3 * E))
+            gt = _g(flat, ft.summarization_token)
+            if gt is not None:
+                K.colsum(ds, gt.view(E))
+            flat.notify(ft.parameters())
+        used = [ds, v16] + ([t16] if Lt else []) + dk16 + [x for x in dt16 if x is not None]
+        for a_, g_ in zip(acts, grads):
+            used += [getattr(a_, n) for n in a_.__slots__] + [getattr(g_, n) for n in g_.__slots__]
+        for x in used:
+            x.record_stream(wg)
+        del grads, acts
+        for l, lay in enumerate(layers):
+            w = flat.w16(lay.multihead_attn.in_proj_weight)[E:]
+            K.linear_dx(dk16[l], w, out=dv, accumulate=True)
+            if Lt:
+                K.linear_dx(dt16[l], w, out=dtt, accumulate=True)
         ctx.save = None
-        flat.notify(ft.parameters())
-        return (dv.view(B, S, 150, E), None, dtt.view(Bq, Lt, E) if Lt else None) + \
-            (None,) * (8 + len(ctx.needs_input_grad[11:]))
+        danchor = torch.zeros(1, device=dev) if ctx.needs_input_grad[11] else None
+        return (dv.view(B, S, 150, E), None, dtt.view(Bq, Lt, E) if Lt else None) + (None,) * 8 + (danchor,) + \
+            (None,) * len(ctx.needs_input_grad[12:])
 
 
 class _LinearFn(torch.autograd.Function):
@@ -360,7 +377,8 @@ class FusionTransformer(nn.Module):
         S = v.shape[1]
         p = self.drop_out_rate if self.training else 0.0
         seed = int(torch.randint(0, 2 ** 40, (1,)).item())
-        return _RecurrentDecoderFn.apply(v, v16, t, t16, self, flat, p, seed, B, S, nmc, *self.parameters())
+        anchor = stream_anchor(self, aux_stream(v.device, "decoder_wgrad"))
+        return _RecurrentDecoderFn.apply(v, v16, t, t16, self, flat, p, seed, B, S, nmc, anchor, *self.parameters())
 
 
 class FusionVideo(FusionTransformer):

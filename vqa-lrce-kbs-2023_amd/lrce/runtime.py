@@ -78,12 +78,47 @@ def needs_grad(*tensors):
 _SIDE_STREAMS = {}
 
 
-def side_stream(device):
-    """The second HIP stream of `device` that the text branch (BERT) runs on while the video branch
-    (Swin) runs on the current stream: the two extractors are independent until the fusion head, and
-    BERT's small latency-bound launches fill the gaps of Swin's large ones."""
-    key = torch.device(device).index
+def aux_stream(device, name="text"):
+    """A named extra HIP stream of `device`.  "text": the text branch (BERT) runs on it while the
+    video branch (Swin) runs on the current stream — the extractors are independent until the fusion
+    head, and BERT's small latency-bound launches fill the gaps of Swin's large ones.
+    "decoder_wgrad": the recurrent decoder's weight gradients, which feed nothing downstream."""
+    key = (torch.device(device).index, name)
     s = _SIDE_STREAMS.get(key)
     if s is None:
         s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
     return s
+
+
+def side_stream(device):
+    return aux_stream(device, "text")
+
+
+class _StreamAnchor(torch.autograd.Function):
+    """Identity on a one-element leaf token, run on an aux stream: the autograd node inherits that
+    stream, so the token's gradient accumulates there and autograd makes the caller's stream wait
+    for it at the end of backward (its leaf-stream join) — after everything a backward enqueued on
+    the aux stream before this node's turn (it is the earliest node of the forward, hence last)."""
+
+    @staticmethod
+    def forward(ctx, token):
+        return token.detach().clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+def stream_anchor(module, stream):
+    """A tensor to pass into an autograd Function whose backward forks work onto `stream`; the
+    Function returns zeros for it.  None when no backward will run."""
+    if not torch.is_grad_enabled():
+        return None
+    dev = stream.device
+    tok = getattr(module, "_lrce_join_token", None)
+    if tok is None or tok.device != dev:
+        tok = torch.zeros(1, device=dev, requires_grad=True)
+        object.__setattr__(module, "_lrce_join_token", tok)
+    stream.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(stream):
+        return _StreamAnchor.apply(tok)
