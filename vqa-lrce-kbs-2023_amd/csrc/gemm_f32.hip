@@ -167,23 +167,42 @@ struct SkinnyP {
   const uint64_t* rng_off;
 };
 
-__device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, int n) {
+// The epilogue's global operands of one output element (bias, dGELU pre-activation, residual, the
+// accumulated C), loaded at kernel start so they ride the same memory round trip as the weights
+// instead of a second one after the reduction.
+struct SkPre {
+  float bias, dg, res, acc;
+};
+
+__device__ __forceinline__ SkPre sk_prefetch(const SkinnyP& p, int m, int n) {
+  SkPre e{0.f, 1.f, 0.f, 0.f};
+  if (m >= p.m || n >= p.n) return e;
   const int fl = p.flags;
   const long long row = m;
-  x = x * p.alpha + ((fl & LRCE_EPI_BIAS) ? p.bias[n] : 0.f);
+  if (fl & LRCE_EPI_BIAS) e.bias = p.bias[n];
+  if (fl & LRCE_EPI_DGELU) e.dg = bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]);
+  if (fl & LRCE_EPI_RESID) e.res = static_cast<const float*>(p.aux)[row * p.ld_aux + n];
+  if (fl & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) e.acc = static_cast<const float*>(p.c)[row * p.ldc + n];
+  return e;
+}
+
+__device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, int n, const SkPre& e) {
+  const int fl = p.flags;
+  const long long row = m;
+  x = x * p.alpha + e.bias;
   x *= (n < p.scale_cols) ? p.scale_val : 1.f;
   if (fl & LRCE_EPI_GELU) {
     if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + n] = f2bf(x);
     x = gelu_f(x);
   }
-  if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]));
+  if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(e.dg);
   if (p.row_scale) x *= p.row_scale[m / p.rows_per_scale];
   if (p.drop_p > 0.f)   // same mask as lrce_dropout on the contiguous [m][n] result
     x = lrce_uniform(lrce_seed(p.drop_seed, p.rng_off), ((long long)m * p.n + n) / p.drop_group) >= p.drop_p
             ? x / (1.0f - p.drop_p) : 0.f;
-  if (fl & LRCE_EPI_RESID) x += static_cast<const float*>(p.aux)[row * p.ld_aux + n];
+  x += e.res;
   if (fl & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) {
-    static_cast<float*>(p.c)[row * p.ldc + n] += x;   // one owner per element: a plain RMW suffices
+    static_cast<float*>(p.c)[row * p.ldc + n] = e.acc + x;   // one owner per element: a plain RMW suffices
   } else if (fl & LRCE_EPI_OUT_F32) {
     static_cast<float*>(p.c)[row * p.ldc + n] = x;
     if (fl & LRCE_EPI_OUT_BOTH) p.aux_out[row * p.ld_aux_out + n] = f2bf(x);
@@ -220,6 +239,11 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p, float*
   int kchunk = (kend - kbase + SK_WAVES - 1) / SK_WAVES;
   kchunk = (kchunk + 15) & ~15;
   const int kb = kbase + wave * kchunk, ke = min(kend, kb + kchunk);
+  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, grp256 = threadIdx.x >> 8;
+  SkPre pre[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+    pre[t] = (t % NPART == grp256) ? sk_prefetch(p, t * 16 + ml, n0 + nl) : SkPre{0.f, 1.f, 0.f, 0.f};
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -260,7 +284,6 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p, float*
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][t][grp * 4 + r][col] = acc[t][r];
   __syncthreads();
-  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, grp256 = threadIdx.x >> 8;
   if (KS == 1) {
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
@@ -270,7 +293,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p, float*
         float x = 0.f;
 #pragma unroll
         for (int w = 0; w < SK_WAVES; ++w) x += red[w][t][ml][nl];
-        sk_epilogue(p, x, m, nn);
+        sk_epilogue(p, x, m, nn, pre[t]);
       }
     }
     return;
@@ -308,7 +331,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p, float*
     float x = 0.f;
     float* src = part + (long long)blockIdx.x * KS * (MT * 256) + t * 256 + ml * 16 + nl;
     for (int j = 0; j < KS; ++j) x += __hip_atomic_load(src + j * (MT * 256), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (m < p.m && nn < p.n) sk_epilogue(p, x, m, nn);
+    if (m < p.m && nn < p.n) sk_epilogue(p, x, m, nn, pre[t]);
   }
   if (threadIdx.x == 0)   // ready for the next launch / graph replay
     __hip_atomic_store(&counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -409,6 +432,11 @@ __global__ void __launch_bounds__(LN_W * 64) skinny_ln_kernel(SkinnyP p, LnP q) 
   const int kw = p.k / LN_W, nu = kw >> 4;
   const int kb = wave * kw;
   const float inv_k = 1.0f / (float)p.k;
+  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, grp256 = threadIdx.x >> 8;
+  SkPre pre[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+    pre[t] = (t % 2 == grp256) ? sk_prefetch(p, t * 16 + ml, n0 + nl) : SkPre{0.f, 1.f, 0.f, 0.f};
   // every global load up front: the weight slab, the A rows, gamma / beta, (PRO 2) x rows + stats
   float4 bv[LN_US], av[LN_US][MT], gv[LN_US], ev[LN_US];
   float4 xv[PRO == 2 ? LN_US : 1][MT];
@@ -624,7 +652,6 @@ __global__ void __launch_bounds__(LN_W * 64) skinny_ln_kernel(SkinnyP p, LnP q) 
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][t][grp * 4 + r][col] = acc[t][r];
   __syncthreads();
-  const int ml = (threadIdx.x >> 4) & 15, nl = threadIdx.x & 15, grp256 = threadIdx.x >> 8;
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
     if (t % 2 != grp256) continue;
@@ -633,7 +660,7 @@ __global__ void __launch_bounds__(LN_W * 64) skinny_ln_kernel(SkinnyP p, LnP q) 
       float x = 0.f;
 #pragma unroll
       for (int w = 0; w < LN_W; ++w) x += red[w][t][ml][nl];
-      sk_epilogue(p, x, m, nn);
+      sk_epilogue(p, x, m, nn, pre[t]);
     }
   }
 }
