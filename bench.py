@@ -91,6 +91,9 @@ def build(batch, device, grad_dtype, seed=0):
                              {"params": model.text_extractor.parameters(), "lr": lr},
                              {"params": model.video_extractor.parameters(), "lr": lr}],
                      lr=lr, betas=(0.9, 0.999), reg_strength=0.001)
+    if reducer is None and os.environ.get("LRCE_EARLY_UPDATES", "1") != "0":
+        # single process: the decoder / BERT updates overlap the Swin backward (env 0: A/B switch)
+        opt.enable_early_updates(model.optimizer_groups())
     rank = dist.get_rank() if dist.is_initialized() else 0
     batch_dev = tuple(t.to(device) for t in synthetic_batch(batch, 1000 + rank))
     return model, opt, reducer, batch_dev

@@ -328,9 +328,12 @@ int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t*
  * BERT weights the fp16 forward reads — written in the same pass.  g_bf16 (optional): read the
  * gradient from this bf16 buffer (the all-reduced bf16 gradient buckets) instead of g (g may be NULL).
  * tensor_chunk_off int32 [n_tensors+1] (first chunk of each tensor) + chunk_sq f32 [n_chunks] scratch
- * (both or neither, here and in lrce_l2norm_multi): the per-tensor norms are summed per chunk with
- * plain stores and then per tensor in a fixed order — bitwise reproducible, so data-parallel replicas
- * (whose L2-term gradient reg * p / ||p|| depends on them) stay identical; without them, float atomics. */
+ * (both or neither in lrce_l2norm_multi): the per-tensor norms are summed per chunk with plain stores
+ * and then per tensor in a fixed order — bitwise reproducible, so data-parallel replicas (whose
+ * L2-term gradient reg * p / ||p|| depends on them) stay identical; without them, float atomics.
+ * Sub-range updates (p, g, m, v, p_bf16, chunk_tensor, chunk_sq, g_bf16 offset to a chunk range, the
+ * f16 range relative to p): chunk_sq without tensor_chunk_off only writes the range's chunk sums;
+ * the launch that passes tensor_chunk_off (after all ranges) sums every tensor. */
 
 /* BERT embeddings before their LayerNorm (HF BertEmbeddings): out[r] = word[ids[r]] + pos[r % L] +
  * type[types[r]] (f32 tables, int64 ids), and the scatter-add backward into the three tables. */

@@ -126,3 +126,37 @@ def test_train_ddp_then_eval_scripts(tmp_path):
                         "--synthetic", "2"] + common, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "Accuracy:" in r.stderr + r.stdout
+
+
+def test_early_group_updates_match_one_update():
+    """FusedAdamW.enable_early_updates: the decoder and BERT groups are updated inside the backward
+    (on the streams that finish their gradients) and the rest by step().  On the same gradients, from
+    the same optimizer state, that gives the parameters of ONE update over the whole flat store, bit
+    for bit."""
+    from lrce.optim import FusedAdamW
+    b = [t.cuda() for t in _batch("oe", 32)]
+    model = _model("oe", 50, 32).cuda().train()
+    opt = FusedAdamW(model, [model.parameters()], lr=1e-4, reg_strength=0.001)
+    flat = opt.flat
+    for _ in range(2):   # a plain first step: moments and norms become non-trivial
+        opt.zero_grad()
+        F.cross_entropy(model(*b[:4]).float(), b[4]).backward()
+        opt.step()
+    state = [t.clone() for t in (flat.f32, opt.exp_avg, opt.exp_avg_sq, opt.sumsq, opt.step_t)]
+    count = opt.step_count
+    opt.enable_early_updates(model.optimizer_groups())
+    opt.zero_grad()
+    F.cross_entropy(model(*b[:4]).float(), b[4]).backward()
+    assert opt.early_updates == 2                 # decoder + text, inside the backward
+    opt.step()
+    torch.cuda.synchronize()
+    early = flat.f32.clone()
+    # the same gradients through one whole-store update from the saved state
+    for dst, src in zip((flat.f32, opt.exp_avg, opt.exp_avg_sq, opt.sumsq, opt.step_t), state):
+        dst.copy_(src)
+    opt.step_count = count
+    opt._norm_version = flat.master_version()   # the restored norms belong to the restored weights
+    opt.enable_early_updates({})
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.equal(early, flat.f32)

@@ -151,9 +151,10 @@ extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, con
                                float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
                                float* sumsq_next, uint16_t* p_f16, int64_t f16_lo, int64_t f16_hi, const uint16_t* g_bf16,
                                const int32_t* tensor_chunk_off, float* chunk_sq, int n_tensors, void* stream) {
-  if (!tensor_chunk_off != !chunk_sq) return lrce_fail(LRCE_E_ARG, "adamw_step: tensor_chunk_off and chunk_sq go together");
+  if (tensor_chunk_off && !chunk_sq) return lrce_fail(LRCE_E_ARG, "adamw_step: tensor_chunk_off needs chunk_sq");
   if (!p || (!g && !g_bf16) || !m || !v || !chunk_tensor || !tensor_lr) return lrce_fail(LRCE_E_ARG, "adamw_step: null pointer");
-  if (p_f16 && (f16_lo % 1024 || f16_hi % 1024 || f16_lo < 0 || f16_hi < f16_lo))
+  // the f16 range is relative to p (it may start before this call's first chunk: a sub-range update)
+  if (p_f16 && (f16_lo % 1024 || f16_hi % 1024 || f16_hi < f16_lo))
     return lrce_fail(LRCE_E_ARG, "adamw_step: f16 shadow range [%lld, %lld) not chunk aligned", (long long)f16_lo, (long long)f16_hi);
   if (n_chunks > 0)
     adamw_kernel<<<(n_chunks + 4 * ADAMW_CPW - 1) / (4 * ADAMW_CPW), 256, 0, static_cast<hipStream_t>(stream)>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq,
@@ -162,7 +163,7 @@ extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, con
                                                                          reinterpret_cast<bf16*>(p_f16), f16_lo, f16_hi,
                                                                          reinterpret_cast<const bf16*>(g_bf16),
                                                                          sumsq_next ? chunk_sq : nullptr);
-  if (sumsq_next && chunk_sq && n_tensors > 0)
+  if (sumsq_next && chunk_sq && tensor_chunk_off && n_tensors > 0)
     segsum_kernel<<<n_tensors, 256, 0, static_cast<hipStream_t>(stream)>>>(chunk_sq, tensor_chunk_off, n_tensors, sumsq_next);
   return lrce_check_launch("adamw_step");
 }

@@ -118,6 +118,9 @@ class AgentBase:
                  {"params": model.text_extractor.parameters(), "lr": lrs[1]},
                  {"params": model.video_extractor.parameters(), "lr": lrs[2]}],
                 lr=lrs[0], betas=(0.9, 0.999), reg_strength=self.reg_strength)
+            if self.model.reducer is None and hasattr(model, "optimizer_groups"):
+                # single process: decoder / BERT updates overlap the Swin backward
+                self.optim.enable_early_updates(model.optimizer_groups())
             if getattr(args, "use_cosine_scheduler", False):
                 self.scheduler = CosineAnnealingWarmupRestarts(
                     self.optim, first_cycle_steps=args.lr_restart_epoch, cycle_mult=args.lr_restart_mul,

@@ -121,6 +121,7 @@ class _EmbedFn(torch.autograd.Function):
             K.bert_embed_bwd(ds, ids, types, gw, gp, gt, s.shape[0], ctx.L, HIDDEN)
         ctx.save = None
         flat.notify(emb.parameters())
+        flat.group_done("text")   # every BERT gradient is final: the optimizer may update BERT now
         # join_token (a leaf): its gradient makes autograd join this stream into the caller's at the
         # end of backward (the text branch may run on a side stream, E2EBase.forward)
         dtok = torch.zeros(1, device=dy.device) if ctx.needs_input_grad[6] else None

@@ -24,6 +24,8 @@ class FlatParams:
             assert len(order) == len(self.params) and {id(p) for p in order} == ids, "order must permute parameters"
             self.params = list(order)
         self.reducer = None          # notify target during a backward (lrce/distributed.py)
+        self.early_update = None     # optimizer hook: a parameter group's gradients are final (optim.py)
+        self.step_begin_hook = None  # optimizer hook: a training forward starts (optim.py)
         self.grad_reducer = None     # its GradReducer, whose reduced gradient the optimizer reads
         self.names = {id(p): n for n, p in module.named_parameters()}
         offs, o = [], 0
@@ -84,6 +86,25 @@ class FlatParams:
         """Called by native autograd Functions when their parameters' gradients are final."""
         if self.reducer is not None:
             self.reducer.notify(params)
+
+    def step_begin(self):
+        """A training forward starts (on the stream the step's other streams fork from)."""
+        if self.step_begin_hook is not None:
+            self.step_begin_hook()
+
+    def group_done(self, name):
+        """A whole parameter group's gradients are final (on the current stream): the optimizer may
+        update that group now, off the critical path (FusedAdamW.enable_early_updates)."""
+        if self.early_update is not None:
+            self.early_update(name)
+
+    def chunk_range(self, params):
+        """[c0, c1) in 1024-element chunks covering exactly `params` (they must be contiguous in the
+        layout: no other parameter inside)."""
+        idx = sorted(self._index[id(p)] for p in params)
+        if not idx or idx != list(range(idx[0], idx[-1] + 1)):
+            raise ValueError("parameters are not contiguous in the flat layout")
+        return self.offsets[idx[0]] // ALIGN, self.range_of(self.params[idx[-1]])[1] // ALIGN
 
     # ------------------------------------------------------------------ views
     def _slice(self, buf, p):

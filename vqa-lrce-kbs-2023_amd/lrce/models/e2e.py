@@ -59,6 +59,14 @@ class E2EBase(nn.Module):
         video = list(self.video_extractor.parameters())[::-1]
         return fusion + text + video + list(bert.pooler.parameters())
 
+    def optimizer_groups(self):
+        """Parameter groups whose gradients are final before the whole backward is (FusedAdamW
+        .enable_early_updates): the recurrent decoder (its backward ends before the extractors')
+        and the BERT encoder (its backward runs on the side stream beside Swin's)."""
+        pool = {id(p) for p in self.text_extractor.bert.pooler.parameters()}
+        return {"decoder": list(self.fusion_model.fusion_transformer.parameters()),
+                "text": [p for p in self.text_extractor.parameters() if id(p) not in pool]}
+
     def extract_video_features(self, video_clips):
         return self.video_extractor(video_clips)
 
@@ -70,6 +78,8 @@ class E2EBase(nn.Module):
         flat = prepare(self)
         if self.training:
             K.rng_advance(flat.device)   # fresh dropout masks per step, also under HIP-graph replay
+            if torch.is_grad_enabled():
+                flat.step_begin()        # optimizer step bookkeeping, before any stream forks
         main = torch.cuda.current_stream(flat.device)
         side = side_stream(flat.device)
         tok = None

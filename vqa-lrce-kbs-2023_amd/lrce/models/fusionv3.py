@@ -300,10 +300,16 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             K.cast_bf16(dkvv[l], dk16[l])
             if Lt:
                 K.cast_bf16(dkvt[l], dt16[l])
+        for l, lay in enumerate(layers):
+            w = flat.w16(lay.multihead_attn.in_proj_weight)[E:]
+            K.linear_dx(dk16[l], w, out=dv, accumulate=True)
+            if Lt:
+                K.linear_dx(dt16[l], w, out=dtt, accumulate=True)
         # The weight gradients (query-side outer products over all steps, memory K/V projections,
-        # the summary token) feed nothing downstream: a second stream runs them while the
-        # extractors' backward, which needs only dv / dt, proceeds on this one.  The forward's
-        # stream anchor joins that stream back at the end of backward.
+        # the summary token) feed nothing downstream: a second stream runs them — and then the
+        # decoder's optimizer update, which rewrites the weights dv / dt were just computed with —
+        # while the extractors' backward, which needs only dv / dt, proceeds on this one.  The
+        # forward's stream anchor joins that stream back at the end of backward.
         wg = aux_stream(dev, "decoder_wgrad")
         wg.wait_stream(main)
         with torch.cuda.stream(wg):
@@ -317,17 +323,13 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             if gt is not None:
                 K.colsum(ds, gt.view(E))
             flat.notify(ft.parameters())
+            flat.group_done("decoder")   # the optimizer may update the decoder now (FusedAdamW)
         used = [ds, v16] + ([t16] if Lt else []) + dk16 + [x for x in dt16 if x is not None]
         for a_, g_ in zip(acts, grads):
             used += [getattr(a_, n) for n in a_.__slots__] + [getattr(g_, n) for n in g_.__slots__]
         for x in used:
             x.record_stream(wg)
         del grads, acts
-        for l, lay in enumerate(layers):
-            w = flat.w16(lay.multihead_attn.in_proj_weight)[E:]
-            K.linear_dx(dk16[l], w, out=dv, accumulate=True)
-            if Lt:
-                K.linear_dx(dt16[l], w, out=dtt, accumulate=True)
         ctx.save = None
         danchor = torch.zeros(1, device=dev) if ctx.needs_input_grad[11] else None
         return (dv.view(B, S, 150, E), None, dtt.view(Bq, Lt, E) if Lt else None) + (None,) * 8 + (danchor,) + \

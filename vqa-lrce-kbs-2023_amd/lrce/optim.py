@@ -43,6 +43,65 @@ class FusedAdamW(torch.optim.Optimizer):
         self.step_count = 0
         self.step_t = torch.zeros(1, device=dev)   # device step count t (graph-safe bias corrections)
         self.last_l2 = None
+        self._early = {}        # group name -> chunk range updated as soon as its gradients are final
+        self._begun = False     # this step's counters / norms are set up (_begin)
+        self._done = []         # chunk ranges already updated this step
+        self.early_updates = 0  # group updates issued from inside a backward (statistics)
+
+    def enable_early_updates(self, groups):
+        """groups: {name: parameters}.  When the backward reports a group final (flat.group_done,
+        called on the stream that produced its last gradient) that group is updated right there, so
+        e.g. the decoder's and BERT's updates overlap the Swin backward instead of following it.
+        Single process only: with a gradient reducer the update must wait for the all-reduce."""
+        self._early = {name: self.flat.chunk_range(list(ps)) for name, ps in groups.items()}
+        self.flat.early_update = self._early_update if self._early else None
+        # the step's device bookkeeping (step counter, norms) runs when the training forward starts,
+        # on the stream every later stream forks from (E2EBase.forward -> flat.step_begin)
+        self.flat.step_begin_hook = self._begin if self._early else None
+
+    def _begin(self):
+        if self._begun:
+            return
+        flat = self.flat
+        self._sync_lrs()
+        self.step_count += 1
+        self.step_t.add_(1.0)
+        if self._norm_version != flat.master_version():
+            # parameters changed outside the optimizer (init / load): one norm pass; afterwards the
+            # update kernel itself produces the next step's norms
+            self._norms()
+        self.sumsq_next.zero_()
+        self._begun = True
+
+    def _update(self, c0, c1, grad_scale, last):
+        """AdamW over chunks [c0, c1); last: then sum the per-chunk norms of ALL tensors (after every
+        range of the step has written its chunk sums)."""
+        flat = self.flat
+        b1, b2 = self.defaults["betas"]
+        t = self.step_count
+        red = getattr(flat, "grad_reducer", None)
+        g16 = red.grad16 if red is not None else None    # all-reduced bf16 gradient buckets
+        e0, e1 = c0 * 1024, c1 * 1024
+        hyper = (b1, b2, self.defaults["eps"], self.defaults["weight_decay"], float(grad_scale), self.reg_strength,
+                 1.0 - b1 ** t, 1.0 - b2 ** t)
+        if c1 > c0:
+            K.adamw_step(flat.f32[e0:e1], flat.grad[e0:e1] if g16 is None else None, self.exp_avg[e0:e1],
+                         self.exp_avg_sq[e0:e1], flat.chunk_tensor[c0:c1], self.tensor_lr, self.sumsq, flat.bf16[e0:e1],
+                         c1 - c0, *hyper, step=self.step_t, sumsq_next=self.sumsq_next, p_f16=flat.f16,
+                         f16_range=(flat.f16_lo - e0, flat.f16_hi - e0) if flat.f16 is not None else (0, 0),
+                         g_bf16=None if g16 is None else g16[e0:e1], chunk_sq=self.chunk_sq[c0:c1], n_tensors=0)
+        if last:   # no update: the fixed-order per-tensor sums over the whole chunk_sq
+            K.adamw_step(flat.f32, flat.grad, self.exp_avg, self.exp_avg_sq, flat.chunk_tensor, self.tensor_lr,
+                         self.sumsq, None, 0, *hyper, step=self.step_t, sumsq_next=self.sumsq_next,
+                         tensor_chunk_off=flat.tensor_chunk_off, chunk_sq=self.chunk_sq)
+
+    def _early_update(self, name):
+        rng = self._early.get(name)
+        if rng is None or rng in self._done or not self._begun or getattr(self.flat, "grad_reducer", None) is not None:
+            return
+        self._update(rng[0], rng[1], 1.0, last=False)
+        self._done.append(rng)
+        self.early_updates += 1
 
     def _sync_lrs(self):
         key = tuple(g["lr"] for g in self.param_groups)
@@ -60,26 +119,24 @@ class FusedAdamW(torch.optim.Optimizer):
     def step(self, closure=None, grad_scale=1.0):
         loss = closure() if closure is not None else None
         flat = self.flat
-        self._sync_lrs()
-        self.step_count += 1
-        self.step_t.add_(1.0)
-        b1, b2 = self.defaults["betas"]
-        t = self.step_count
-        if self._norm_version != flat.master_version():
-            # parameters changed outside the optimizer (init / load): one norm pass; afterwards the
-            # update kernel itself produces the next step's norms
-            self._norms()
-        self.sumsq_next.zero_()
-        red = getattr(flat, "grad_reducer", None)
-        g16 = red.grad16 if red is not None else None    # all-reduced bf16 gradient buckets
-        K.adamw_step(flat.f32, flat.grad if g16 is None else None, self.exp_avg, self.exp_avg_sq, flat.chunk_tensor, self.tensor_lr, self.sumsq,
-                     flat.bf16, flat.n_chunks, b1, b2, self.defaults["eps"], self.defaults["weight_decay"],
-                     float(grad_scale), self.reg_strength, 1.0 - b1 ** t, 1.0 - b2 ** t, step=self.step_t,
-                     sumsq_next=self.sumsq_next, p_f16=flat.f16, f16_range=(flat.f16_lo, flat.f16_hi), g_bf16=g16,
-                     tensor_chunk_off=flat.tensor_chunk_off, chunk_sq=self.chunk_sq)
+        self._begin()
+        # the chunk ranges not updated early, in order; the last launch also sums the next norms
+        segs, c = [], 0
+        for c0, c1 in sorted(self._done):
+            if c0 > c:
+                segs.append((c, c0))
+            c = max(c, c1)
+        if c < flat.n_chunks:
+            segs.append((c, flat.n_chunks))
+        # (early updates ran on the streams that finished those groups' gradients; autograd's
+        # end-of-backward join makes this stream wait for them, so their chunk sums are in place)
+        for i, (c0, c1) in enumerate(segs):
+            self._update(c0, c1, grad_scale, last=i == len(segs) - 1)
         self.sumsq.copy_(self.sumsq_next)
         self._norm_version = flat.master_version()
         flat.mark_bf16_fresh()
+        self._begun = False
+        self._done = []
         return loss
 
     def l2_term(self):
