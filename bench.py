@@ -291,7 +291,10 @@ def main():
     if agent is not None:
         out["agent_path"] = agent
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or len(os.sched_getaffinity(0))
+        # the GPU box's CPU share is OMP_NUM_THREADS (16): more threads than that oversubscribe the
+        # shared host (256 threads measured 2.4x slower than 16)
+        share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16
+        threads = args.cpu_threads or min(len(os.sched_getaffinity(0)), share)
         log(f"cpu baseline (oracle, fp32, {threads} threads) ...")
         try:
             v, dt, ve, dte = cpu_baseline(threads, args.batch_size)

@@ -7,7 +7,9 @@ Columns match `rocprofv3 --stats` (calls, total / average / min / max duration i
 share of total kernel time).  --last N keeps only the dispatches of the last N training steps (the
 timed graph replays of `bench.py --roofline-steps 0 --agent-steps 0`): everything after the optimizer
 launch that precedes them, up to the last optimizer launch, so warm-up / capture / eager steps and
-one-off work are excluded.  Kernel names are shortened (template args kept)."""
+one-off work are excluded.  Steps are delimited by the patch-embedding im2col launch that opens
+every forward (the optimizer now runs as several sub-range launches per step); the window is the
+N steps before the last im2col.  Kernel names are shortened (template args kept)."""
 import argparse
 import re
 import sqlite3
@@ -41,13 +43,13 @@ def main():
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
     rows = load(a.db)
-    adam = [i for i, r in enumerate(rows) if "adamw_kernel" in r[0]]
-    steps = len(adam) or 1
+    opens = [i for i, r in enumerate(rows) if "im2col_kernel" in r[0]]
+    steps = len(opens) or 1
     window = "all dispatches"
-    if a.last and len(adam) > a.last:
-        rows = rows[adam[-a.last - 1] + 1:adam[-1] + 1]
+    if a.last and len(opens) > a.last:
+        rows = rows[opens[-a.last - 1]:opens[-1]]
         steps = a.last
-        window = f"the last {a.last} training steps (dispatches after optimizer launch #{len(adam) - a.last})"
+        window = f"{a.last} training steps (from forward #{len(opens) - a.last} to the last forward's start)"
     agg = defaultdict(lambda: [0, 0.0, 0.0, float("inf"), 0.0])
     for name, _, d in rows:
         e = agg[name]
