@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 typedef __bf16 bf16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
@@ -120,3 +122,14 @@ __device__ __forceinline__ float4 lrce_uniform4(uint64_t seed, uint64_t idx4) {
                      (float)((h >> 48) & 0xFFFFu) * s);
 }
 __device__ __forceinline__ uint64_t lrce_seed(uint64_t seed, const uint64_t* off) { return off ? seed + *off : seed; }
+
+// compile-time loop: f(integral_constant<int, I>) for I = 0..N-1 (keeps accumulator indices static)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_impl(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_impl<I + 1, N>(f);
+  }
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_impl<0, N>(f); }

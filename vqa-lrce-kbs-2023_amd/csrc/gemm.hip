@@ -142,17 +142,6 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16* lds, int r0, int ks, int
   }
 }
 
-// compile-time loop: f(integral_constant<int, I>) for I = 0..N-1 (keeps accumulator indices static)
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for_impl(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for_impl<I + 1, N>(f);
-  }
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) { static_for_impl<0, N>(f); }
-
 constexpr int EP = 68;  // padded fp32 row of the epilogue staging tile (conflict-free writes)
 
 __device__ __forceinline__ void wave_lds_fence() {
@@ -185,26 +174,34 @@ __device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row
   }
 }
 
-// Fused epilogue for 8 consecutive columns n..n+7 of output row m (see LrceGemmDesc flags).
+// Fused epilogue for 8 consecutive columns n..n+7 of output row m (see LrceGemmDesc flags).  The
+// 16-bit format is a template parameter and every optional factor sits behind a wave-uniform branch
+// (alpha, the q-scale columns — host guarantees scale_cols % 8 == 0 on the vector path — and the row
+// scale), so a plain epilogue is a conversion and a 16-B store per 8 outputs.
+template <bool F16>
 __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int n, int sk, char* cbase) {
   if (m >= p.m || n >= p.n) return;
   const int fl = p.flags;
   const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
   const bool first = sk == 0;
-  const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
   if (p.vec && n + 8 <= p.n) {
-    float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (p.alpha != 1.f) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+    }
     if ((fl & LRCE_EPI_BIAS) && first) {
       const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n), b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
-      bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w; bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
     }
+    if (n < p.scale_cols) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (v[e] * p.alpha + bias[e]) * ((n + e < p.scale_cols) ? p.scale_val : 1.f);
+      for (int e = 0; e < 8; ++e) v[e] *= p.scale_val;
+    }
     if (fl & LRCE_EPI_GELU) {
       if (fl & LRCE_EPI_AUX_OUT) {
         bf16x8 pre;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) pre[e] = to16r(v[e], p.f16);
+        for (int e = 0; e < 8; ++e) pre[e] = to16<F16>(v[e]);
         *reinterpret_cast<bf16x8*>(p.aux_out + row * p.ld_aux_out + n) = pre;
       }
 #pragma unroll
@@ -213,10 +210,13 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
     if (fl & LRCE_EPI_DGELU) {
       const bf16x8 pre = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(p.aux) + row * p.ld_aux + n);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(from16r(pre[e], p.f16));
+      for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(from16<F16>(pre[e]));
     }
+    if (p.row_scale) {
+      const float rs = p.row_scale[m / p.rows_per_scale];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] *= rs;
+      for (int e = 0; e < 8; ++e) v[e] *= rs;
+    }
     if ((fl & LRCE_EPI_RESID) && first) {
       const float* ap = static_cast<const float*>(p.aux) + row * p.ld_aux + n;
       const float4 r0 = *reinterpret_cast<const float4*>(ap), r1 = *reinterpret_cast<const float4*>(ap + 4);
@@ -237,17 +237,18 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
       if ((fl & LRCE_EPI_OUT_BOTH) && !(fl & LRCE_EPI_ACCUM)) {
         bf16x8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = to16r(v[e], p.f16);
+        for (int e = 0; e < 8; ++e) o[e] = to16<F16>(v[e]);
         *reinterpret_cast<bf16x8*>(p.aux_out + row * p.ld_aux_out + n) = o;
       }
     } else {
       bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = to16r(v[e], p.f16);
+      for (int e = 0; e < 8; ++e) o[e] = to16<F16>(v[e]);
       *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(cbase) + row * p.ldc + n) = o;
     }
     return;
   }
+  const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
   // ragged / unaligned edge: element by element
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -353,7 +354,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
         const float4 x0 = *reinterpret_cast<const float4*>(E + rr * EP + cc);
         const float4 x1 = *reinterpret_cast<const float4*>(E + rr * EP + cc + 4);
         float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        epilogue8(p, v, m0 + wm * 64 + h * 32 + rr, n0 + wn * 64 + cc, sk, cbase);
+        epilogue8<false>(p, v, m0 + wm * 64 + h * 32 + rr, n0 + wn * 64 + cc, sk, cbase);   // f16 is LDS-DMA only
       }
     }
     wave_lds_fence();
@@ -496,12 +497,12 @@ struct GldsOperand {
   __device__ __forceinline__ void advance() { base += step; }
 };
 
-template <int TBM, int TBN, bool A_KM, bool B_KM, bool F16 = false>
+template <int TBM, int TBN, bool A_KM, bool B_KM, bool F16 = false, int NS = 2>
 __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   constexpr int WM = TBM / 2, WN = TBN / 2;      // per-wave tile
   constexpr int IM = WM / 16, JN = WN / 16;      // 16x16 accumulator blocks per wave
   constexpr int A_EL = TBM * BK, B_EL = TBN * BK;
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * (A_EL + B_EL)];  // [stage][A | B]
+  __shared__ __attribute__((aligned(16))) bf16 lds[NS * (A_EL + B_EL)];  // [stage][A | B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles = p.tiles_m * p.tiles_n;
@@ -556,6 +557,9 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   };
 
   if (nfull > 0) {
+    // NS-stage ring, one barrier per K tile: at the top of iteration kt this wave waits for its part
+    // of tile kt (tiles kt+1 .. kt+NS-2 stay in flight), the barrier makes every wave's part visible
+    // AND proves every wave finished tile kt-1, whose stage then receives tile kt+NS-1.
     constexpr int INFLIGHT = (TBM + TBN) / 32;   // glds per wave per K tile
     GldsOperand<A_KM, TBM> ga;
     GldsOperand<B_KM, TBN> gb;
@@ -565,29 +569,45 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     gb.init(bbase, p.ldb, p.n, n0, kb, wave, lane);
     ga.issue(la0, wave_u);
     gb.issue(lb0, wave_u);
-    for (int kt = 0; kt < nfull; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nfull) {
+#pragma unroll
+    for (int i = 1; i < NS - 1; ++i)
+      if (i < nfull) {
         ga.advance(); gb.advance();
-        ga.issue(la0 + (uint32_t)((cur ^ 1) * STG * 2), wave_u);
-        gb.issue(lb0 + (uint32_t)((cur ^ 1) * STG * 2), wave_u);
-        // this wave's tile kt landed, kt+1 in flight
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
+        ga.issue(la0 + (uint32_t)(i * STG * 2), wave_u);
+        gb.issue(lb0 + (uint32_t)(i * STG * 2), wave_u);
+      }
+    int cur = 0;
+    for (int kt = 0; kt < nfull; ++kt) {
+      const int ahead = min(NS - 2, nfull - 1 - kt);   // tiles issued after tile kt
+      if constexpr (NS >= 4) {
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * INFLIGHT) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if constexpr (NS == 3) {
+        if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      __builtin_amdgcn_s_barrier();                          // ... and every other wave's part of it
+      __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      if (kt + NS - 1 < nfull) {
+        const int nxt = cur == 0 ? NS - 1 : cur - 1;   // (kt + NS - 1) % NS
+        ga.advance(); gb.advance();
+        ga.issue(la0 + (uint32_t)(nxt * STG * 2), wave_u);
+        gb.issue(lb0 + (uint32_t)(nxt * STG * 2), wave_u);
+      }
       compute(sa0 + cur * STG, sb0 + cur * STG);
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();                          // stage `cur` free for tile kt+2
-      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of stage `cur` are done
+      cur = cur + 1 == NS ? 0 : cur + 1;
     }
+    __builtin_amdgcn_s_barrier();   // every wave is done with every stage (tail / LDS epilogue reuse)
+    __builtin_amdgcn_sched_barrier(0);
   }
   if (tail) {
     const int k0 = kb + nfull * BK;
-    const int st = nfull & 1;
+    const int st = nfull % NS;
     tail_tile<A_KM, TBM>(sa0 + st * STG, abase, p.lda, p.m, ke, m0, k0, p.a_map);
     tail_tile<B_KM, TBN>(sb0 + st * STG, bbase, p.ldb, p.n, ke, n0, k0, nullptr);
     __syncthreads();
@@ -711,7 +731,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(u[2 * h + (e >> 2)][e & 3]);
-      epilogue8(p, v, m, ncol + 8 * h, sk, cbase);
+      epilogue8<F16>(p, v, m, ncol + 8 * h, sk, cbase);
     }
   });
 }
@@ -812,7 +832,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   p.tiles_m = (d->m + BM - 1) / BM; p.tiles_n = (d->n + BN - 1) / BN;
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   const bool out32 = d->flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM);
-  p.vec = (d->n % 8 == 0) && (d->ldc % 8 == 0) && al16(d->c) && (d->stride_c % 8 == 0) &&
+  p.vec = (d->n % 8 == 0) && (d->ldc % 8 == 0) && al16(d->c) && (d->stride_c % 8 == 0) && (d->scale_cols % 8 == 0) &&
           (!d->bias || al16(d->bias)) && (!d->aux || (al16(d->aux) && d->ld_aux % 8 == 0)) &&
           (!d->aux_out || (al16(d->aux_out) && d->ld_aux_out % 8 == 0));
   (void)out32;
@@ -857,24 +877,29 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     }
     const int gk = (d->a_kmajor ? 2 : 0) | (d->b_kmajor ? 1 : 0) | (small ? 4 : 0) | (tall_m == 192 ? 8 : 0) |
                    (tall_m == 160 ? 16 : 0) | (p.f16 ? 32 : 0);
-    switch (gk) {
-      case 32 + 11: gemm_glds_kernel<192, 128, true, true, true><<<grid, NT, 0, s>>>(p); break;
-      case 32 + 19: gemm_glds_kernel<160, 128, true, true, true><<<grid, NT, 0, s>>>(p); break;
-      case 32 + 3: gemm_glds_kernel<128, 128, true, true, true><<<grid, NT, 0, s>>>(p); break;
-      case 32 + 7: gemm_glds_kernel<64, 64, true, true, true><<<grid, NT, 0, s>>>(p); break;
-      case 11: gemm_glds_kernel<192, 128, true, true><<<grid, NT, 0, s>>>(p); break;
-      case 10: gemm_glds_kernel<192, 128, true, false><<<grid, NT, 0, s>>>(p); break;
-      case 19: gemm_glds_kernel<160, 128, true, true><<<grid, NT, 0, s>>>(p); break;
-      case 18: gemm_glds_kernel<160, 128, true, false><<<grid, NT, 0, s>>>(p); break;
-      case 3: gemm_glds_kernel<128, 128, true, true><<<grid, NT, 0, s>>>(p); break;
-      case 2: gemm_glds_kernel<128, 128, true, false><<<grid, NT, 0, s>>>(p); break;
-      case 1: gemm_glds_kernel<128, 128, false, true><<<grid, NT, 0, s>>>(p); break;
-      case 0: gemm_glds_kernel<128, 128, false, false><<<grid, NT, 0, s>>>(p); break;
-      case 7: gemm_glds_kernel<64, 64, true, true><<<grid, NT, 0, s>>>(p); break;
-      case 6: gemm_glds_kernel<64, 64, true, false><<<grid, NT, 0, s>>>(p); break;
-      case 5: gemm_glds_kernel<64, 64, false, true><<<grid, NT, 0, s>>>(p); break;
-      case 4: gemm_glds_kernel<64, 64, false, false><<<grid, NT, 0, s>>>(p); break;
-    }
+    auto launch = [&](auto nsc) {
+      constexpr int S = decltype(nsc)::value;
+      switch (gk) {
+        case 32 + 11: gemm_glds_kernel<192, 128, true, true, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 19: gemm_glds_kernel<160, 128, true, true, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 3: gemm_glds_kernel<128, 128, true, true, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 7: gemm_glds_kernel<64, 64, true, true, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 11: gemm_glds_kernel<192, 128, true, true, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 10: gemm_glds_kernel<192, 128, true, false, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 19: gemm_glds_kernel<160, 128, true, true, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 18: gemm_glds_kernel<160, 128, true, false, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 3: gemm_glds_kernel<128, 128, true, true, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 2: gemm_glds_kernel<128, 128, true, false, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 1: gemm_glds_kernel<128, 128, false, true, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 0: gemm_glds_kernel<128, 128, false, false, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 7: gemm_glds_kernel<64, 64, true, true, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 6: gemm_glds_kernel<64, 64, true, false, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 5: gemm_glds_kernel<64, 64, false, true, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 4: gemm_glds_kernel<64, 64, false, false, false, S><<<grid, NT, 0, s>>>(p); break;
+      }
+    };
+    // two stages: a third (one resident workgroup per CU) measured 1.3-1.5x slower on every step shape
+    launch(std::integral_constant<int, 2>{});
     if (p.ws) {
       const long long q4 = (long long)d->m * d->n / 4;
       splitk_reduce_kernel<<<(unsigned)((q4 + 255) / 256), 256, 0, s>>>(p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
