@@ -34,7 +34,8 @@ enum {
  *   B(n,k) = b_kmajor ? B[n*ldb + k] : B[k*ldb + n]      (bf16, or f32 with b_f32)
  *   a_map (optional int32): gathers A rows — replaces m (a_kmajor) or k (!a_kmajor) by a_map[.]
  *   c_map (optional int32): scatters output rows — row m is written to c_map[m] (also the row of
- *                           the RESID / DGELU aux read).
+ *                           the RESID / DGELU aux read); c_map[m] < 0 drops row m (a padded window
+ *                           position, cropped by the reference at video_swin_ori.py:292-293).
  * Replaces: nn.Linear forward/backward (addmm/mm) at video_swin_ori.py:46-57,150,152,318;
  * fusionv3.py:154,160; the decoder/BERT linears; conv3d patch-embed as a K=96 GEMM (:458).
  */
@@ -139,7 +140,10 @@ int lrce_gemm_ln(const LrceGemmDesc* desc, const LrceLnPrologue* prologue, void*
 /* ---------------------------------------------------------------- LayerNorm
  * Row r of the (rows x cols) LN input is the concatenation of nseg segments of cols/nseg
  * channels, segment s read from source row in_map[r*nseg+s] of x (identity if in_map == NULL;
- * a negative index reads zeros = padding).  Output row r goes to out_map[r] (identity if NULL).
+ * a negative index reads zeros = padding before the norm, PatchMerging :328-331).  With nseg == 1 a
+ * negative index marks padding AFTER the norm (the block's F.pad of norm1's output, :253-258): the
+ * output row is zero, its stats 0, and the backward skips the row (no dx, no dw/db).  Output row r
+ * goes to out_map[r] (identity if NULL).
  * Saves per-row mean and rstd (f32) for the backward.  y_bf16_copy (optional): a bf16 copy of y (f32 y
  * for the residual stream + bf16 operand for the next GEMM / weight gradient, one pass).
  * Replaces: nn.LayerNorm at video_swin_ori.py:252,285,339,476-480,684; PatchMerging gather

@@ -68,3 +68,34 @@ def test_kinetics_backbone_checkpoint_loads(tmp_path):
     for k in ("patch_embed.proj.weight", "layers.2.blocks.17.attn.relative_position_bias_table",
               "layers.3.blocks.1.mlp.fc2.bias", "norm.weight"):
         assert torch.equal(got[k], filled["video_extractor.swin." + k]), k
+
+
+@pytest.mark.parametrize("D,H,W", [(3, 25, 25), (3, 13, 13), (3, 14, 14), (3, 7, 7)])
+def test_padded_window_maps_match_pad_roll_partition(D, H, W):
+    """StageGeometry's window-order maps equal the reference's index movement on the padded volume:
+    F.pad up to whole windows (video_swin_ori.py:253-258, padded positions = -1 here), torch.roll by
+    -shift (:262), window_partition (:60-72); the inverse maps every real token to its one window row;
+    the PatchMerging map pads an odd H / W (:328-331) with -1."""
+    import torch.nn.functional as F
+    from lrce.feature_extractor.video_swin import StageGeometry
+    nc, window = 2, (8, 7, 7)
+    g = StageGeometry(nc, D, H, W, window, "cpu")
+    wd, wh, ww = g.ws
+    idx = torch.arange(nc * D * H * W).view(nc, D, H, W)
+    padded = F.pad(idx, (0, g.Wp - W, 0, g.Hp - H, 0, g.Dp - D), value=-1)
+
+    def partition(v):
+        v = v.view(nc, g.Dp // wd, wd, g.Hp // wh, wh, g.Wp // ww, ww).permute(0, 1, 3, 5, 2, 4, 6)
+        return v.reshape(-1)
+
+    assert torch.equal(g.win2sp.long(), partition(padded))
+    assert g.M_win == g.win2sp.numel() and int((g.win2sp < 0).sum()) == g.M_win - g.M
+    live = g.win2sp >= 0
+    assert torch.equal(g.sp2win[g.win2sp[live].long()].long(), torch.nonzero(live).flatten())
+    if g.shifted:
+        rolled = torch.roll(padded, shifts=tuple(-s for s in g.ss), dims=(1, 2, 3))
+        assert torch.equal(g.win2sp_shift.long(), partition(rolled))
+    m = F.pad(idx, (0, W % 2, 0, H % 2), value=-1)
+    ref = torch.stack([m[:, :, 0::2, 0::2], m[:, :, 1::2, 0::2], m[:, :, 0::2, 1::2], m[:, :, 1::2, 1::2]], -1)
+    assert torch.equal(g.merge_map.long(), ref.reshape(-1))
+    assert g.M_merged == nc * D * ((H + 1) // 2) * ((W + 1) // 2)

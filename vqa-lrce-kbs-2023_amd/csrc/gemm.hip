@@ -183,6 +183,7 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
   if (m >= p.m || n >= p.n) return;
   const int fl = p.flags;
   const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
+  if (row < 0) return;   // c_map -1: a padded window position (no output row)
   const bool first = sk == 0;
   if (p.vec && n + 8 <= p.n) {
     if (p.alpha != 1.f) {
@@ -343,6 +344,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
           const int m = m0 + wm * 64 + h * 32 + rr;
           if (m >= p.m) break;
           const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
+          if (row < 0) continue;
           const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
           epilogue1(p, E[rr * EP + lane], row, m, n, sk == 0, rs, cbase);
         }
@@ -647,6 +649,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
           const int m = m0 + wm * WM + h * 32 + rr;
           if (m >= p.m) break;
           const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
+          if (row < 0) continue;
           const float rs = p.row_scale ? p.row_scale[m / p.rows_per_scale] : 1.f;
           epilogue1(p, E[rr * EPW + col], row, m, n, sk == 0, rs, cbase);
         }

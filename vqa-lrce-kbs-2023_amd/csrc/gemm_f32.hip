@@ -115,6 +115,7 @@ __global__ void __launch_bounds__(NT) gemm_f32_kernel(GemmF32P p) {
         const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
         if (m >= p.m) continue;
         const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
+        if (row < 0) continue;   // c_map -1: padded position, no output row
         float v = acc[i][j][r] * p.alpha + bias;
         if (fl & LRCE_EPI_GELU) {
           if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + n] = f2bf(v);

@@ -4,6 +4,10 @@
 // read: torch.roll + window_partition before the attention (video_swin_ori.py:262,268), the 2x2
 // PatchMerging concat (:333-337), and identity for plain LNs.  HBM-bound: one read of x, one write
 // of y, 8 B of stats per row.
+// A missing source (in_map entry < 0) means zero padding: inside a multi-segment row (PatchMerging,
+// which pads BEFORE its norm, :328-331) the segment reads as zeros; a whole missing row of a
+// one-segment gather is a window position past the volume (the block pads AFTER norm1, :253-258):
+// its output row is zero and it takes no part in the backward.
 #include "common.h"
 #include "lrce_capi.h"
 
@@ -65,6 +69,22 @@ __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, in
   const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
   if (r >= rows) return;
   const int nch = cols >> 2, seg = cols / nseg;
+  if (in_map && nseg == 1 && in_map[r] < 0) {   // padded window position: zero row
+    const long long orow = out_map ? (long long)out_map[r] : (long long)r;
+#pragma unroll
+    for (int t = 0; t < CH; ++t) {
+      const int c = sl + LPR * t;
+      if (c < nch) {
+        st4<TY>(y + orow * cols + 4 * c, make_float4(0.f, 0.f, 0.f, 0.f));
+        if (y2) st4_16(y2 + orow * cols + 4 * c, make_float4(0.f, 0.f, 0.f, 0.f), y2_f16 != 0);
+      }
+    }
+    if (sl == 0) {
+      if (mean_o) mean_o[r] = 0.f;
+      if (rstd_o) rstd_o[r] = 0.f;
+    }
+    return;
+  }
   float4 v[CH], ww[CH], bb[CH];
   float s = 0.f;
 #pragma unroll
@@ -134,9 +154,11 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
   // run >= 8 rows per wave: without it each row is a full memory round trip).
   const int stride = gridDim.x * 4 * RPW;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  // rows of a one-segment gather whose source is missing are padding (no output, no dw / db)
+  auto row_live = [&](int r) { return r < rows && !(in_map && nseg == 1 && in_map[r] < 0); };
   auto fetch = [&](int rb, float4 (&xv)[CH], float4 (&dv)[CH], float4 (&rv)[CH], float& mu, float& rs) {
     const int r = rb + lane / LPR;
-    const bool live = r < rows;
+    const bool live = row_live(r);
     mu = live ? mean_i[r] : 0.f;
     rs = live ? rstd_i[r] : 0.f;
     const long long dyr = !live ? 0 : (dy_map ? (long long)dy_map[r] : (long long)r);
@@ -171,7 +193,7 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
     const bool more = r0 + stride < rows;
     if (more) fetch(r0 + stride, xnx, dnx, rnx, mnx, snx);
     const int r = r0 + lane / LPR;
-    const bool live = r < rows;
+    const bool live = row_live(r);
     const float mean = mcur, rstd = scur;
     float4 xh[CH], g[CH];
     float s1 = 0.f, s2 = 0.f;

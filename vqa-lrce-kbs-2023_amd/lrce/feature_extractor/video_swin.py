@@ -49,20 +49,28 @@ def relative_position_index(window):
 
 # ----------------------------------------------------------------------------------- geometry
 class StageGeometry:
-    """Index maps for one stage at a given input size (cached per device)."""
+    """Index maps for one stage at a given input size (cached per device).
+
+    Windows tile the volume padded up to whole windows (video_swin_ori.py:253-258 pads norm1's output
+    with zeros, :346 builds the mask over the padded volume): the window-order maps run over the
+    padded volume and mark padded positions -1 (the LN1 gather writes zero rows there, the proj GEMM
+    drops them, the LN1 backward skips them).  Spatial tensors keep the unpadded M rows; window-order
+    tensors (LN1 output, qkv, attention output) have M_win = n_win * n rows."""
 
     def __init__(self, nc, D, H, W, window, device):
         half = tuple(i // 2 for i in window)
         ws, ss = get_window_size((D, H, W), window, half)
-        if D % ws[0] or H % ws[1] or W % ws[2]:
-            raise ValueError(f"Swin stage {D}x{H}x{W} needs window padding (unsupported; 224x224x(5|16) inputs never do)")
         self.nc, self.D, self.H, self.W = nc, D, H, W
         self.ws, self.ss = ws, ss
+        self.Dp, self.Hp, self.Wp = (-(-D // ws[0]) * ws[0], -(-H // ws[1]) * ws[1], -(-W // ws[2]) * ws[2])
+        self.padded = (self.Dp, self.Hp, self.Wp) != (D, H, W)
         self.n = ws[0] * ws[1] * ws[2]
-        self.nW = (D // ws[0]) * (H // ws[1]) * (W // ws[2])
+        self.nW = (self.Dp // ws[0]) * (self.Hp // ws[1]) * (self.Wp // ws[2])
         self.n_win = nc * self.nW
         self.M = nc * D * H * W
+        self.M_win = self.n_win * self.n
         self.rows_per_clip = D * H * W
+        self.win_rows_per_clip = self.nW * self.n
         self.win2sp = self._win_map((0, 0, 0), device)
         self.sp2win = self._inverse(self.win2sp)
         self.shifted = any(s > 0 for s in ss)
@@ -72,30 +80,37 @@ class StageGeometry:
             self.region, self.win_pat, self.n_pat = self._mask_patterns(device)
             self.groups_shift = K.wattn_groups(self.win_pat, self.n_win, device)
         self.groups = K.wattn_groups(None, self.n_win, device)
-        self.merge_map = self._merge_map(device) if (H % 2 == 0 and W % 2 == 0) else None
+        # PatchMerging pads odd H / W with zeros before its 2x2 gather (video_swin_ori.py:328-331)
+        self.Hm, self.Wm = -(-H // 2), -(-W // 2)
+        self.M_merged = nc * D * self.Hm * self.Wm
+        self.merge_map = self._merge_map(device)
 
     def _win_map(self, shift, device):
         D, H, W = self.D, self.H, self.W
+        Dp, Hp, Wp = self.Dp, self.Hp, self.Wp
         wd, wh, ww = self.ws
         ar = lambda n: torch.arange(n, device=device)
-        b, iwd, iwh, iww, td, th, tw = torch.meshgrid(ar(self.nc), ar(D // wd), ar(H // wh), ar(W // ww), ar(wd), ar(wh),
-                                                      ar(ww), indexing="ij")
-        d = (iwd * wd + td + shift[0]) % D
-        h = (iwh * wh + th + shift[1]) % H
-        w = (iww * ww + tw + shift[2]) % W
-        return (((b * D + d) * H + h) * W + w).reshape(-1).to(torch.int32).contiguous()
+        b, iwd, iwh, iww, td, th, tw = torch.meshgrid(ar(self.nc), ar(Dp // wd), ar(Hp // wh), ar(Wp // ww), ar(wd),
+                                                      ar(wh), ar(ww), indexing="ij")
+        d = (iwd * wd + td + shift[0]) % Dp
+        h = (iwh * wh + th + shift[1]) % Hp
+        w = (iww * ww + tw + shift[2]) % Wp
+        row = ((b * D + d) * H + h) * W + w
+        row = torch.where((d < D) & (h < H) & (w < W), row, torch.full_like(row, -1))
+        return row.reshape(-1).to(torch.int32).contiguous()
 
-    @staticmethod
-    def _inverse(perm):
-        inv = torch.empty_like(perm)
-        inv[perm.long()] = torch.arange(perm.numel(), device=perm.device, dtype=perm.dtype)
+    def _inverse(self, perm):
+        """spatial row -> window-order row (every real token sits in exactly one window)"""
+        inv = torch.empty(self.M, dtype=perm.dtype, device=perm.device)
+        live = perm >= 0
+        inv[perm[live].long()] = torch.arange(perm.numel(), device=perm.device, dtype=perm.dtype)[live]
         return inv
 
     def _mask_patterns(self, device):
-        """Region labels of compute_mask (video_swin_ori.py:346-359) over the rolled volume, as
-        per-window region-id rows, de-duplicated into patterns (windows away from the rolled
+        """Region labels of compute_mask (video_swin_ori.py:346-359) over the padded, rolled volume,
+        as per-window region-id rows, de-duplicated into patterns (windows away from the rolled
         border all share the all-zero pattern)."""
-        D, H, W = self.D, self.H, self.W
+        D, H, W = self.Dp, self.Hp, self.Wp
         ws, ss = self.ws, self.ss
         lab = torch.zeros(D, H, W, dtype=torch.int32)
         cnt = 0
@@ -111,13 +126,16 @@ class StageGeometry:
         return patterns.to(torch.int32).contiguous().to(device), win_pat.contiguous().to(device), patterns.shape[0]
 
     def _merge_map(self, device):
-        """PatchMerging concat order x0..x3 = (h,w) offsets (0,0),(1,0),(0,1),(1,1) (:333-337)."""
+        """PatchMerging concat order x0..x3 = (h,w) offsets (0,0),(1,0),(0,1),(1,1) (:333-337); sources
+        past an odd H / W are the zero padding (-1)."""
         nc, D, H, W = self.nc, self.D, self.H, self.W
         ar = lambda n: torch.arange(n, device=device)
-        b, d, i, j, s = torch.meshgrid(ar(nc), ar(D), ar(H // 2), ar(W // 2), ar(4), indexing="ij")
-        dh = torch.tensor([0, 1, 0, 1], device=device)[s]
-        dw = torch.tensor([0, 0, 1, 1], device=device)[s]
-        return (((b * D + d) * H + 2 * i + dh) * W + 2 * j + dw).reshape(-1).to(torch.int32).contiguous()
+        b, d, i, j, s = torch.meshgrid(ar(nc), ar(D), ar(self.Hm), ar(self.Wm), ar(4), indexing="ij")
+        h = 2 * i + torch.tensor([0, 1, 0, 1], device=device)[s]
+        w = 2 * j + torch.tensor([0, 0, 1, 1], device=device)[s]
+        row = ((b * D + d) * H + h) * W + w
+        row = torch.where((h < H) & (w < W), row, torch.full_like(row, -1))
+        return row.reshape(-1).to(torch.int32).contiguous()
 
 
 _GEO_CACHE = {}
@@ -211,6 +229,10 @@ class _PatchEmbedFn(torch.autograd.Function):
         else:
             B, _, T, H, W = clips.shape
             nc = B
+        if H % 4 or W % 4:
+            # the reference zero-pads H / W up to the 4x4 patch (video_swin_ori.py:466-470); the fused
+            # im2col reads whole patches only
+            raise ValueError(f"PatchEmbed3D: frame size {H}x{W} is not a multiple of the 4x4 patch (unsupported)")
         clips = clips.contiguous()
         Dp, Hp, Wp = (T + 1) // 2, H // 4, W // 4
         M = nc * Dp * Hp * Wp
@@ -302,14 +324,15 @@ class _SwinBlockFn(torch.autograd.Function):
         bias_b = torch.empty_like(bias_f)
         K.wattn_bias_build(at.relative_position_bias_table, at.relative_position_index, n, nH, region, n_pat,
                            bias_f, bias_b)
-        xw, m1, r1 = K.layernorm(x, blk.norm1.weight, blk.norm1.bias, 1e-5, in_map=wmap, rows=M)
+        Mw = geo.M_win   # window-order rows (incl. the padded positions of a partial window)
+        xw, m1, r1 = K.layernorm(x, blk.norm1.weight, blk.norm1.bias, 1e-5, in_map=wmap, rows=Mw)
         c = (C // nH) ** -0.5 * LOG2E
-        o = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+        o = torch.empty(Mw, C, dtype=torch.bfloat16, device=dev)
         lse = torch.empty(geo.n_win, nH, 160, device=dev)
         if nH % 4 == 0 and C % 64 == 0:
             # QKV projection fused with the attention (csrc/window_fused.hip); qkv is still written
             # for the backward
-            qkv = torch.empty(M, 3 * C, dtype=torch.bfloat16, device=dev)
+            qkv = torch.empty(Mw, 3 * C, dtype=torch.bfloat16, device=dev)
             K.wattn_qkv_fwd(xw, flat.w16(at.qkv.weight), at.qkv.bias, c, bias_f, win_pat, qkv, o, lse, geo.n_win, n,
                             nH)
         else:   # head counts the fused kernel's 4-head groups do not divide (not Swin-B)
@@ -317,7 +340,7 @@ class _SwinBlockFn(torch.autograd.Function):
             K.wattn_fwd_grouped(qkv, bias_f, geo.groups_shift if shifted else geo.groups, o, lse, geo.n_win, n, nH)
         x_mid = torch.empty(M, C, device=dev)
         K.linear(o, flat.w16(at.proj.weight), at.proj.bias, out=x_mid, resid=x, c_map=wmap, row_scale=dp1,
-                 rows_per_scale=geo.rows_per_clip)
+                 rows_per_scale=geo.win_rows_per_clip)
         h2, m2, r2 = K.layernorm(x_mid, blk.norm2.weight, blk.norm2.bias, 1e-5)
         pre = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=dev)
         g = K.linear(h2, flat.w16(blk.mlp.fc1.weight), blk.mlp.fc1.bias, gelu=True, pre_out=pre)
@@ -350,7 +373,8 @@ class _SwinBlockFn(torch.autograd.Function):
         del dpre, h2
         dx_mid = torch.empty_like(x_mid)
         # attention branch input gradient s1 * dx_mid, as bf16 in window order (rows of o / qkv)
-        dmid16 = torch.empty(M, C, dtype=torch.bfloat16, device=dout.device)
+        # (window order; padded positions carry no gradient: the reference crops them, :292-293)
+        dmid16 = (torch.zeros if geo.padded else torch.empty)(geo.M_win, C, dtype=torch.bfloat16, device=dout.device)
         K.layernorm_bwd(dh2, x_mid, m2, r2, blk.norm2.weight, dx_mid, dres=dout,
                         dw=_g(flat, blk.norm2.weight), db=_g(flat, blk.norm2.bias),
                         dx16=dmid16, dx16_map=ctx.sp2win, dx_scale=dp1, dx_scale_rps=rpc)
@@ -384,7 +408,7 @@ class _PatchMergeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, pm, geo, flat, *params):
         C = pm.dim
-        Mo = geo.M // 4
+        Mo = geo.M_merged
         xl, mean, rstd = K.layernorm(x, pm.norm.weight, pm.norm.bias, 1e-5, in_map=geo.merge_map, nseg=4, rows=Mo,
                                      cols=4 * C)
         y = K.linear(xl, flat.w16(pm.reduction.weight), out_f32=True)
@@ -402,7 +426,7 @@ class _PatchMergeFn(torch.autograd.Function):
             K.linear_dw(dy16, xl, gw)
         dxl = K.linear_dx(dy16, flat.w16(pm.reduction.weight))
         dx = torch.empty_like(x)
-        K.layernorm_bwd(dxl, x, mean, rstd, pm.norm.weight, dx, in_map=geo.merge_map, nseg=4, rows=geo.M // 4,
+        K.layernorm_bwd(dxl, x, mean, rstd, pm.norm.weight, dx, in_map=geo.merge_map, nseg=4, rows=geo.M_merged,
                         cols=4 * pm.dim, dw=_g(flat, pm.norm.weight), db=_g(flat, pm.norm.bias))
         ctx.save = None
         flat.notify(pm.parameters())
@@ -471,7 +495,7 @@ class SwinTransformer3D(nn.Module):
                 x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, *blk.parameters())
             if layer.downsample is not None:
                 x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())
-                H, W = H // 2, W // 2
+                H, W = (H + 1) // 2, (W + 1) // 2
         x = _LayerNormFn.apply(x, self.norm, flat, 1e-5, *self.norm.parameters())
         return x, (nc, D, H, W)
 
@@ -490,7 +514,7 @@ class SwinTransformer3D(nn.Module):
             x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, *blk.parameters())
         if layer.downsample is not None:
             x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())
-            H, W = H // 2, W // 2
+            H, W = (H + 1) // 2, (W + 1) // 2
         return x.view(nc, D, H, W, -1)
 
     def forward(self, x):
