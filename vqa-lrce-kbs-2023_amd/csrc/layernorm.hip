@@ -154,11 +154,12 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
   // run >= 8 rows per wave: without it each row is a full memory round trip).
   const int stride = gridDim.x * 4 * RPW;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  // rows of a one-segment gather whose source is missing are padding (no output, no dw / db)
-  auto row_live = [&](int r) { return r < rows && !(in_map && nseg == 1 && in_map[r] < 0); };
-  auto fetch = [&](int rb, float4 (&xv)[CH], float4 (&dv)[CH], float4 (&rv)[CH], float& mu, float& rs) {
+  // rows of a one-segment gather whose source is missing are padding (no output, no dw / db); the
+  // flag comes from the gather's own source lookup, so it does not delay the row's other loads
+  auto fetch = [&](int rb, float4 (&xv)[CH], float4 (&dv)[CH], float4 (&rv)[CH], float& mu, float& rs, bool& pad) {
     const int r = rb + lane / LPR;
-    const bool live = row_live(r);
+    const bool live = r < rows;
+    pad = false;
     mu = live ? mean_i[r] : 0.f;
     rs = live ? rstd_i[r] : 0.f;
     const long long dyr = !live ? 0 : (dy_map ? (long long)dy_map[r] : (long long)r);
@@ -172,6 +173,8 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
         if (ok) {
           xv[t] = ld4<TX>(x + o);
           if (dres) rv[t] = *reinterpret_cast<const float4*>(dres + o);
+        } else if (nseg == 1) {
+          pad = true;
         }
         dv[t] = ld4<TD>(dy + dyr * cols + 4 * c);
       }
@@ -186,14 +189,16 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
   }
   float4 xcur[CH], dcur[CH], rcur[CH];
   float mcur = 0.f, scur = 0.f;
-  if (r0 < rows) fetch(r0, xcur, dcur, rcur, mcur, scur);
+  bool pcur = false;
+  if (r0 < rows) fetch(r0, xcur, dcur, rcur, mcur, scur, pcur);
   for (; r0 < rows; r0 += stride) {
     float4 xnx[CH], dnx[CH], rnx[CH];
     float mnx = 0.f, snx = 0.f;
+    bool pnx = false;
     const bool more = r0 + stride < rows;
-    if (more) fetch(r0 + stride, xnx, dnx, rnx, mnx, snx);
+    if (more) fetch(r0 + stride, xnx, dnx, rnx, mnx, snx, pnx);
     const int r = r0 + lane / LPR;
-    const bool live = row_live(r);
+    const bool live = r < rows && !pcur;
     const float mean = mcur, rstd = scur;
     float4 xh[CH], g[CH];
     float s1 = 0.f, s2 = 0.f;
@@ -244,6 +249,7 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
       for (int t = 0; t < CH; ++t) { xcur[t] = xnx[t]; dcur[t] = dnx[t]; rcur[t] = rnx[t]; }
       mcur = mnx;
       scur = snx;
+      pcur = pnx;
     }
   }
   if (!dw && !db) return;
