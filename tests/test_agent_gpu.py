@@ -129,8 +129,9 @@ def test_train_ddp_then_eval_scripts(tmp_path):
 
 
 def test_early_group_updates_match_one_update():
-    """FusedAdamW.enable_early_updates: the decoder and BERT groups are updated inside the backward
-    (on the streams that finish their gradients) and the rest by step().  On the same gradients, from
+    """FusedAdamW.enable_early_updates: the decoder, BERT and Swin stage 4/3/2 groups are updated inside
+    the backward (on the streams that finish their gradients / the decoder's weight-gradient stream)
+    and the rest by step().  On the same gradients, from
     the same optimizer state, that gives the parameters of ONE update over the whole flat store, bit
     for bit."""
     from lrce.optim import FusedAdamW
@@ -147,7 +148,7 @@ def test_early_group_updates_match_one_update():
     opt.enable_early_updates(model.optimizer_groups())
     opt.zero_grad()
     F.cross_entropy(model(*b[:4]).float(), b[4]).backward()
-    assert opt.early_updates == 2                 # decoder + text, inside the backward
+    assert opt.early_updates == 5                 # decoder, text, swin3, swin2, swin1 inside the backward
     opt.step()
     torch.cuda.synchronize()
     early = flat.f32.clone()

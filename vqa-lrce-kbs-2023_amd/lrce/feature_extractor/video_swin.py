@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from .. import kernels as K
-from ..runtime import ensure
+from ..runtime import aux_stream, ensure
 
 LOG2E = 1.4426950408889634
 
@@ -399,6 +399,16 @@ class _SwinBlockFn(torch.autograd.Function):
                         dw=_g(flat, blk.norm1.weight), db=_g(flat, blk.norm1.bias))
         ctx.save = None
         flat.notify(blk.parameters())
+        group = getattr(blk, "_lrce_group", None)
+        if group is not None and flat.early_update is not None:
+            # this stage's gradients are final: its optimizer update runs on the decoder's weight-
+            # gradient stream (joined at the end of backward by the decoder's stream anchor) while
+            # the earlier stages' backward continues here; it touches only this stage's weights
+            main = torch.cuda.current_stream(dout.device)
+            s = aux_stream(dout.device, "decoder_wgrad")
+            s.wait_stream(main)
+            with torch.cuda.stream(s):
+                flat.group_done(group)
         return (dx, None, None, None, None, None) + (None,) * len(ctx.needs_input_grad[6:])
 
 
@@ -471,6 +481,10 @@ class SwinTransformer3D(nn.Module):
                                           dpr[sum(depths[:i]):sum(depths[:i + 1])], i < len(depths) - 1))
         self.num_features = embed_dim * 2 ** (len(depths) - 1)
         self.norm = nn.LayerNorm(self.num_features)
+        # stage i > 0 is final once its first block's backward is done (the backward runs the last
+        # stage first): that block reports the stage's optimizer group (E2EBase.optimizer_groups)
+        for i, layer in enumerate(self.layers):
+            object.__setattr__(layer.blocks[0], "_lrce_group", f"swin{i}" if i > 0 else None)
 
     def forward_tokens(self, clips, layout="BSTCHW", normalize=True):
         """clips (B,S,T,3,H,W) f32 in [0,1] (normalised in-kernel) or (B,3,T,H,W) already normalised.

@@ -61,11 +61,19 @@ class E2EBase(nn.Module):
 
     def optimizer_groups(self):
         """Parameter groups whose gradients are final before the whole backward is (FusedAdamW
-        .enable_early_updates): the recurrent decoder (its backward ends before the extractors')
-        and the BERT encoder (its backward runs on the side stream beside Swin's)."""
+        .enable_early_updates): the recurrent decoder (its backward ends before the extractors'),
+        the BERT encoder (its backward runs on the side stream beside Swin's), and Swin stages 4, 3,
+        2 (the backward runs stage 4 -> 1; stage 4's group carries the final LayerNorm)."""
         pool = {id(p) for p in self.text_extractor.bert.pooler.parameters()}
-        return {"decoder": list(self.fusion_model.fusion_transformer.parameters()),
-                "text": [p for p in self.text_extractor.parameters() if id(p) not in pool]}
+        swin = self.video_extractor.swin
+        groups = {"decoder": list(self.fusion_model.fusion_transformer.parameters()),
+                  "text": [p for p in self.text_extractor.parameters() if id(p) not in pool]}
+        for i in range(len(swin.layers) - 1, 0, -1):
+            ps = list(swin.layers[i].parameters())
+            if i == len(swin.layers) - 1:
+                ps += list(swin.norm.parameters())
+            groups[swin.layers[i].blocks[0]._lrce_group] = ps
+        return groups
 
     def extract_video_features(self, video_clips):
         return self.video_extractor(video_clips)
