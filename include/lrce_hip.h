@@ -159,7 +159,8 @@ int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_map, int nseg
  * to row in_map[r*nseg+s] of dx (f32): dx = LN_bwd + (dres ? dres[same row] : 0).  dw/db (f32,
  * may be NULL) are accumulated with atomics.  Optional dx_bf16: a bf16 copy of LN row r's dx,
  * times dx_scale[r / dx_scale_rps] (DropPath of the branch the copy feeds), stored row-major at row
- * dx_bf16_map[r] (e.g. window order) — the A operand of the following weight/input-gradient GEMMs. */
+ * dx_bf16_map[r] (e.g. window order) — the A operand of the following weight/input-gradient GEMMs.
+ * dx may be NULL when dx_bf16 is given (the bf16 copy is then the only output). */
 int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map,
                        const void* x, int x_f32, const int32_t* in_map, int nseg,
                        const float* mean, const float* rstd, const float* w,
@@ -348,8 +349,10 @@ int lrce_bert_embed_bwd(const float* dout, const int64_t* ids, const int64_t* ty
 /* LRCE positional embeddings before their LayerNorm (embedding.py:47-63, 17-23). */
 int lrce_video_posembed_fwd(const float* x, const float* cls, const float* pos, const float* len, const float* clip, float* out,
                             int B, int S, int Tg, int P, int C, void* stream);
-int lrce_video_posembed_bwd(const float* dout, float* dx, float* dcls, float* dpos, float* dlen, float* dclip, int B, int S,
-                            int Tg, int P, int C, void* stream);
+/* Backward: dx (f32) and / or dx_bf16 (either may be NULL, not both) get the token rows, the four
+ * tables' gradients are ADDED (f32 atomics) into dcls / dpos / dlen / dclip.  C % 4 == 0. */
+int lrce_video_posembed_bwd(const float* dout, float* dx, uint16_t* dx_bf16, float* dcls, float* dpos, float* dlen,
+                            float* dclip, int B, int S, int Tg, int P, int C, void* stream);
 int lrce_text_posembed_fwd(const float* x, const float* cls, const float* pos, float* out, int B, int L, int C, void* stream);
 int lrce_text_posembed_bwd(const float* dout, float* dx, float* dcls, float* dpos, int B, int L, int C, void* stream);
 

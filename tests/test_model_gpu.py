@@ -189,7 +189,8 @@ def test_e2e_train_step_grads_match_oracle():
     F.cross_entropy(y, label.cuda()).backward()
     named = dict(m.named_parameters())
     worst = {}
-    for k in ("video_extractor.swin.patch_embed.proj.weight", "video_extractor.swin.layers.0.blocks.1.attn.qkv.weight",
+    for k in ("video_extractor.swin.patch_embed.proj.weight", "video_extractor.swin.patch_embed.proj.bias",
+              "video_extractor.swin.patch_embed.norm.weight", "video_extractor.swin.layers.0.blocks.1.attn.qkv.weight",
               "video_extractor.swin.layers.2.blocks.17.mlp.fc2.weight",
               "video_extractor.swin.layers.1.blocks.0.attn.relative_position_bias_table",
               "video_extractor.swin.layers.3.blocks.1.norm2.weight", "video_extractor.swin.norm.weight",

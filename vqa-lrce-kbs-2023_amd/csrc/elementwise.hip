@@ -207,31 +207,55 @@ __global__ void video_pos_kernel(const float* __restrict__ x, const float* __res
   const float4 k = *reinterpret_cast<const float4*>(clip + (long long)s * C + c);
   *reinterpret_cast<float4*>(out + e) = make_float4(v.x + a.x + l.x + k.x, v.y + a.y + l.y + k.y, v.z + a.z + l.z + k.z, v.w + a.w + l.w + k.w);
 }
-__global__ void video_pos_bwd_kernel(const float* __restrict__ d, float* __restrict__ dx, float* __restrict__ dcls, float* __restrict__ dpos,
-                                     float* __restrict__ dlen, float* __restrict__ dclip, int B, int S, int Tg, int P, int C) {
-  // one thread per (p, c): loop over (b, s, t); len/clip/cls through atomics of per-thread sums
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  const int p = blockIdx.y;
-  if (c >= C) return;
-  float sp = 0.f;
-  for (int s = 0; s < S; ++s) {
-    float ss = 0.f;
-    for (int tg = 0; tg < Tg; ++tg) {
-      float st = 0.f;
-      for (int b = 0; b < B; ++b) {
-        const long long bst = ((long long)b * S + s) * Tg + tg;
-        const float g = d[(bst * (P + 1) + p) * C + c];
-        st += g;
-        if (p > 0) dx[(bst * P + (p - 1)) * C + c] = g;
+// Backward of the above: one block per (clip s, frame group tg) x VP_PPB positions p, one lane per
+// float4 column.  The B rows of a (s, tg, p) are loaded 8 at a time (independent loads in flight),
+// summed in registers and copied out to dx (f32) and / or dx16 (bf16: the projection GEMMs' operand);
+// the table gradients take the per-lane partial sums by atomics (dpos / dcls: S*Tg adds per element,
+// dlen / dclip: one per block).
+constexpr int VP_PPB = 2;
+__global__ void __launch_bounds__(256) video_pos_bwd_kernel(const float* __restrict__ d, float* __restrict__ dx, bf16* __restrict__ dx16,
+                                                            float* __restrict__ dcls, float* __restrict__ dpos, float* __restrict__ dlen,
+                                                            float* __restrict__ dclip, int B, int S, int Tg, int P, int C) {
+  const int s = blockIdx.x / Tg, tg = blockIdx.x % Tg;
+  const int p0 = blockIdx.y * VP_PPB;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add4 = [](float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; };
+  auto atom4 = [](float* dst, const float4& v) {
+    atomicAdd(dst, v.x); atomicAdd(dst + 1, v.y); atomicAdd(dst + 2, v.z); atomicAdd(dst + 3, v.w);
+  };
+  for (int c = 4 * threadIdx.x; c < C; c += 4 * blockDim.x) {
+    float4 acc = z4;
+    for (int p = p0; p < p0 + VP_PPB && p <= P; ++p) {
+      float4 sp = z4;
+      for (int b0 = 0; b0 < B; b0 += 8) {
+        float4 g[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const long long bst = ((long long)(b0 + u) * S + s) * Tg + tg;
+          g[u] = b0 + u < B ? *reinterpret_cast<const float4*>(d + (bst * (P + 1) + p) * C + c) : z4;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (b0 + u >= B) break;
+          add4(sp, g[u]);
+          if (p > 0) {
+            const long long o = ((((long long)(b0 + u) * S + s) * Tg + tg) * P + (p - 1)) * C + c;
+            if (dx) *reinterpret_cast<float4*>(dx + o) = g[u];
+            if (dx16) {
+              bf16x4 h;
+              h[0] = f2bf(g[u].x); h[1] = f2bf(g[u].y); h[2] = f2bf(g[u].z); h[3] = f2bf(g[u].w);
+              *reinterpret_cast<bf16x4*>(dx16 + o) = h;
+            }
+          }
+        }
       }
-      ss += st;
-      atomicAdd(dlen + (long long)tg * C + c, st);
+      atom4(dpos + (long long)p * C + c, sp);
+      if (p == 0) atom4(dcls + c, sp);
+      add4(acc, sp);
     }
-    sp += ss;
-    atomicAdd(dclip + (long long)s * C + c, ss);
+    atom4(dlen + (long long)tg * C + c, acc);
+    atom4(dclip + (long long)s * C + c, acc);
   }
-  dpos[(long long)p * C + c] += sp;
-  if (p == 0) dcls[c] += sp;
 }
 
 // TextPosEmbed (embedding.py:17-23): out[b,l,c] = (l == 0 ? cls[c] : x[b,l-1,c]) + pos[l,c]
@@ -379,11 +403,14 @@ extern "C" int lrce_video_posembed_fwd(const float* x, const float* cls, const f
   return lrce_check_launch("video_posembed_fwd");
 }
 
-extern "C" int lrce_video_posembed_bwd(const float* dout, float* dx, float* dcls, float* dpos, float* dlen, float* dclip, int B, int S,
-                                       int Tg, int P, int C, void* stream) {
-  if (!dout || !dx || !dcls || !dpos || !dlen || !dclip) return lrce_fail(LRCE_E_ARG, "video_posembed_bwd: null pointer");
-  dim3 grid((C + 255) / 256, P + 1);
-  video_pos_bwd_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(dout, dx, dcls, dpos, dlen, dclip, B, S, Tg, P, C);
+extern "C" int lrce_video_posembed_bwd(const float* dout, float* dx, uint16_t* dx_bf16, float* dcls, float* dpos, float* dlen,
+                                       float* dclip, int B, int S, int Tg, int P, int C, void* stream) {
+  if (!dout || (!dx && !dx_bf16) || !dcls || !dpos || !dlen || !dclip) return lrce_fail(LRCE_E_ARG, "video_posembed_bwd: null pointer");
+  if (C % 4 || B < 1 || S < 1 || Tg < 1 || P < 0) return lrce_fail(LRCE_E_ARG, "video_posembed_bwd: bad shape");
+  const int threads = std::min(256, (C / 4 + 63) / 64 * 64);
+  dim3 grid(S * Tg, (P + 1 + VP_PPB - 1) / VP_PPB);
+  video_pos_bwd_kernel<<<grid, threads, 0, static_cast<hipStream_t>(stream)>>>(dout, dx, reinterpret_cast<bf16*>(dx_bf16), dcls, dpos,
+                                                                               dlen, dclip, B, S, Tg, P, C);
   return lrce_check_launch("video_posembed_bwd");
 }
 

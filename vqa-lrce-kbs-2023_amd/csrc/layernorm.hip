@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
           const float4 rr = rcur[t];
           out.x += rr.x; out.y += rr.y; out.z += rr.z; out.w += rr.w;
         }
-        *reinterpret_cast<float4*>(dx + o) = out;
+        if (dx) *reinterpret_cast<float4*>(dx + o) = out;
         if (dx16) {   // bf16 copy (optionally row-scaled / row-permuted) for the next GEMMs' A operand
           const float f = dsc ? dsc[r / dsc_rps] : 1.f;
           const long long orow = dx16_map ? (long long)dx16_map[r] : (long long)r;
@@ -355,7 +355,7 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
                                   float* dx, const float* dres, float* dw, float* db, int rows, int cols, uint16_t* dx_bf16,
                                   const int32_t* dx_bf16_map, const float* dx_scale, int dx_scale_rps, float* workspace,
                                   int64_t workspace_elems, void* stream) {
-  if (!dy || !x || !mean || !rstd || !w || !dx) return lrce_fail(LRCE_E_ARG, "layernorm_bwd: null pointer");
+  if (!dy || !x || !mean || !rstd || !w || (!dx && !dx_bf16)) return lrce_fail(LRCE_E_ARG, "layernorm_bwd: null pointer");
   if (dx_scale_rps < 1) dx_scale_rps = 1;
   if (nseg < 1) nseg = 1;
   if (cols % 4 || (cols / nseg) % 4 || cols % nseg || cols > 64 * 4 * MAXC)

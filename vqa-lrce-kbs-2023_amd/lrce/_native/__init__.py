@@ -116,7 +116,7 @@ _SIGS = {
     "lrce_bert_embed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_bert_embed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I64, _P],
     "lrce_video_posembed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "lrce_video_posembed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lrce_video_posembed_bwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lrce_text_posembed_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_text_posembed_bwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_l2norm_multi": [_P, _P, _I, _P, _I, _P, _P, _P],

@@ -249,15 +249,16 @@ class _PatchEmbedFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dx):
         pe, flat = ctx.pe, ctx.flat
-        dy = torch.empty_like(ctx.y)
-        K.layernorm_bwd(dx.contiguous(), ctx.y, ctx.mean, ctx.rstd, pe.norm.weight, dy,
+        # the LN backward writes dy only as the bf16 operand of the conv-weight gradient GEMM, whose
+        # epilogue also sums the bias gradient (no f32 dy round trip, no separate column sum)
+        dy16 = torch.empty(ctx.y.shape, dtype=torch.bfloat16, device=dx.device)
+        K.layernorm_bwd(dx.contiguous(), ctx.y, ctx.mean, ctx.rstd, pe.norm.weight, None, dx16=dy16,
                         dw=_g(flat, pe.norm.weight), db=_g(flat, pe.norm.bias))
-        gw = _g(flat, pe.proj.weight)
+        gw, gb = _g(flat, pe.proj.weight), _g(flat, pe.proj.bias)
         if gw is not None:
-            K.linear_dw(dy, ctx.patches, gw.view(pe.embed_dim, 96))
-        gb = _g(flat, pe.proj.bias)
-        if gb is not None:
-            K.colsum(dy, gb)
+            K.linear_dw(dy16, ctx.patches, gw.view(pe.embed_dim, 96), bias_grad=gb)
+        elif gb is not None:
+            K.colsum(dy16, gb)
         flat.notify(pe.parameters())
         return (None,) * (5 + len(list(pe.parameters())))
 

@@ -295,17 +295,19 @@ def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out
 def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1, dres=None, dw=None, db=None,
                   rows=None, cols=None, dx16=None, dx16_map=None, dx_scale=None, dx_scale_rps=1, workspace=True):
     """dx16: optional bf16 copy of dx (times dx_scale[r / dx_scale_rps], at row dx16_map[r]).
-    workspace=False: dw/db by per-block atomics instead of the two-pass partials sum."""
+    workspace=False: dw/db by per-block atomics instead of the two-pass partials sum.
+    dx may be None when dx16 is given (returns dx16 then)."""
     R = rows if rows is not None else mean.shape[0]
     Cc = cols if cols is not None else w.shape[0]
+    out = dx if dx is not None else dx16
     ws, nws = None, 0
     if workspace and (dw is not None or db is not None):
         nws = N.lib().lrce_layernorm_bwd_workspace(R, Cc)
-        ws = torch.empty(nws, dtype=F32, device=dx.device) if nws > 0 else None
+        ws = torch.empty(nws, dtype=F32, device=out.device) if nws > 0 else None
     call("lrce_layernorm_bwd", ptr(dy), int(dy.dtype == F32), ptr(dy_map), ptr(x), int(x.dtype == F32), ptr(in_map),
          nseg, ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dres), ptr(dw), ptr(db), R, Cc, ptr(dx16), ptr(dx16_map),
-         ptr(dx_scale), dx_scale_rps, ptr(ws), nws, stream_of(dx))
-    return dx
+         ptr(dx_scale), dx_scale_rps, ptr(ws), nws, stream_of(out))
+    return out
 
 
 def scale_cast_bf16(x, row_scale=None, rows_per_scale=1, out=None):
@@ -537,9 +539,10 @@ def video_posembed_fwd(x, cls, pos, len_, clip, out, B, S, Tg, P, C):
          stream_of(out))
 
 
-def video_posembed_bwd(dout, dx, dcls, dpos, dlen, dclip, B, S, Tg, P, C):
-    call("lrce_video_posembed_bwd", ptr(dout), ptr(dx), ptr(dcls), ptr(dpos), ptr(dlen), ptr(dclip), B, S, Tg, P, C,
-         stream_of(dout))
+def video_posembed_bwd(dout, dx, dcls, dpos, dlen, dclip, B, S, Tg, P, C, *, dx16=None):
+    """dx (f32) and / or dx16 (bf16) may be None, not both; the table gradients are accumulated."""
+    call("lrce_video_posembed_bwd", ptr(dout), ptr(dx), ptr(dx16), ptr(dcls), ptr(dpos), ptr(dlen), ptr(dclip), B, S, Tg,
+         P, C, stream_of(dout))
 
 
 def text_posembed_fwd(x, cls, pos, out, B, L, C):

@@ -83,15 +83,14 @@ class VideoEmbedFn(torch.autograd.Function):
         dz = torch.empty_like(z)
         K.layernorm_bwd(dv, z, mean, rstd, pe.layer_norm.weight, dz, dw=_g(flat, pe.layer_norm.weight),
                         db=_g(flat, pe.layer_norm.bias))
-        dy = torch.empty(B * S * Tg * P, C, device=dz.device)
         gs = [_g(flat, t) for t in (pe.emb_cls, pe.emb_pos, pe.emb_len, pe.emb_clip)]
         tmp = [g if g is not None else torch.zeros(t.shape, device=dz.device)
                for g, t in zip(gs, (pe.emb_cls, pe.emb_pos, pe.emb_len, pe.emb_clip))]
-        K.video_posembed_bwd(dz, dy, tmp[0], tmp[1], tmp[2], tmp[3], B, S, Tg, P, C)
         if proj is not None:
-            # the projection's backward GEMMs read a bf16 copy of dy (LDS-DMA MFMA path); the bias
-            # gradient rides in the weight-gradient GEMM
-            dy16 = K.scale_cast_bf16(dy)
+            # the projection's backward GEMMs read dy as bf16 (LDS-DMA MFMA path), written directly by
+            # the positional-embedding backward; the bias gradient rides in the weight-gradient GEMM
+            dy16 = torch.empty(B * S * Tg * P, C, dtype=torch.bfloat16, device=dz.device)
+            K.video_posembed_bwd(dz, None, tmp[0], tmp[1], tmp[2], tmp[3], B, S, Tg, P, C, dx16=dy16)
             gw, gb = _g(flat, proj.weight), _g(flat, proj.bias)
             if gw is not None:
                 K.linear_dw(dy16, vf16, gw, bias_grad=gb)
@@ -99,7 +98,8 @@ class VideoEmbedFn(torch.autograd.Function):
                 K.colsum(dy16, gb)
             dvf = K.linear_dx(dy16, flat.w16(proj.weight))
         else:
-            dvf = dy
+            dvf = torch.empty(B * S * Tg * P, C, device=dz.device)
+            K.video_posembed_bwd(dz, dvf, tmp[0], tmp[1], tmp[2], tmp[3], B, S, Tg, P, C)
         ctx.save = None
         flat.notify(list(pe.parameters()) + (list(proj.parameters()) if proj is not None else []))
         return (dvf.view(B, S, Tg, P, Cin),) + (None,) * (5 + len(ctx.needs_input_grad[6:]))
