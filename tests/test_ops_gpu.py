@@ -254,14 +254,15 @@ def test_gemm_epilogues_and_maps():
     k.linear_dw(dy, xb, dw, a_map=gat)
     ref_dw = bf(dy[gat.long()]).float().t() @ xb.float()
     assert rel(dw, ref_dw) < 1e-2
-    # dW + fused bias gradient (bf16 dY: LDS-DMA kernel, ones-operand MFMA), split-K and not
-    for rows in (M, 4096 + 64):
+    # dW + fused bias gradient (bf16 dY: LDS-DMA kernel, ones-operand MFMA), split-K and not; 9 and 40
+    # slices take the slice-parallel reduce (remainder slices included)
+    for rows in (M, 4096 + 64, 9 * 1024 + 40, 40 * 1024 + 8):
         dyb = bf(torch.randn(rows, N, device=dev))
         xb2 = bf(torch.randn(rows, Kd, device=dev))
-        dw2 = torch.zeros(N, Kd, device=dev)
+        dw2 = torch.full((N, Kd), 0.25, device=dev)
         db2 = torch.full((N,), 0.5, device=dev)
         k.linear_dw(dyb, xb2, dw2, bias_grad=db2)
-        assert rel(dw2, dyb.float().t() @ xb2.float()) < 1e-3
+        assert rel(dw2, dyb.float().t() @ xb2.float() + 0.25) < 1e-3
         assert rel(db2, dyb.float().sum(0) + 0.5) < 1e-3
     # colsum
     cs = torch.zeros(N, device=dev)

@@ -755,6 +755,41 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, in
   *cp = o;
 }
 
+// Deep splits (small weight gradients over many rows: 100+ slices of a 384 x 128 tile) would leave
+// the one-thread-per-float4 reduce above with a few waves each walking every slab serially; here a
+// block is 64 float4 columns x 4 slice groups, each thread keeps 4 slab loads in flight, and the
+// groups meet in LDS.
+__global__ void __launch_bounds__(256) splitk_reduce_deep_kernel(const float* __restrict__ ws, int split, int m, int n,
+                                                                 float* __restrict__ c, long long ldc) {
+  const long long mn = (long long)m * n;
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long long e = ((long long)blockIdx.x * 64 + lane) * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [&](const float4& t) { s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w; };
+  if (e < mn) {
+    int k = g;
+    for (; k + 12 < split; k += 16) {
+      const float4 t0 = *reinterpret_cast<const float4*>(ws + k * mn + e);
+      const float4 t1 = *reinterpret_cast<const float4*>(ws + (k + 4) * mn + e);
+      const float4 t2 = *reinterpret_cast<const float4*>(ws + (k + 8) * mn + e);
+      const float4 t3 = *reinterpret_cast<const float4*>(ws + (k + 12) * mn + e);
+      add(t0); add(t1); add(t2); add(t3);
+    }
+    for (; k < split; k += 4) add(*reinterpret_cast<const float4*>(ws + k * mn + e));
+  }
+  __shared__ float4 red[4][64];
+  red[g][lane] = s;
+  __syncthreads();
+  if (g == 0 && e < mn) {
+    const float4 a = red[1][lane], b = red[2][lane], d = red[3][lane];
+    float4* cp = reinterpret_cast<float4*>(c + (e / n) * ldc + (e % n));
+    float4 o = *cp;
+    o.x += s.x + a.x + b.x + d.x; o.y += s.y + a.y + b.y + d.y;
+    o.z += s.z + a.z + b.z + d.z; o.w += s.w + a.w + b.w + d.w;
+    *cp = o;
+  }
+}
+
 }  // namespace
 
 int lrce_gemm_f32(const LrceGemmDesc* d, void* stream);
@@ -905,7 +940,10 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     launch(std::integral_constant<int, 2>{});
     if (p.ws) {
       const long long q4 = (long long)d->m * d->n / 4;
-      splitk_reduce_kernel<<<(unsigned)((q4 + 255) / 256), 256, 0, s>>>(p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
+      if (split >= 8)
+        splitk_reduce_deep_kernel<<<(unsigned)((q4 + 63) / 64), 256, 0, s>>>(p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
+      else
+        splitk_reduce_kernel<<<(unsigned)((q4 + 255) / 256), 256, 0, s>>>(p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
     }
     return lrce_check_launch("gemm(glds)");
   }

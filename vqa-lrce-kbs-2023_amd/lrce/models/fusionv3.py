@@ -290,8 +290,8 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             ds = K.dropout(dx, 0.0, 0, res=dt)   # s fed both the residual and the decoder
             saves[i] = None
         main = torch.cuda.current_stream(dev)
-        dv = torch.zeros(B * S * 150, E, device=dev)
-        dtt = torch.zeros(Bq * Lt, E, device=dev) if Lt else None
+        dv = torch.empty(B * S * 150, E, device=dev)     # the first layer's GEMM writes, the rest add
+        dtt = torch.empty(Bq * Lt, E, device=dev) if Lt else None
         # the memory-side K/V gradients (accumulated in f32 over steps / answer choices) enter their
         # big-M GEMMs as bf16, like every other activation gradient
         dk16 = [torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev) for _ in layers]
@@ -302,9 +302,9 @@ class _RecurrentDecoderFn(torch.autograd.Function):
                 K.cast_bf16(dkvt[l], dt16[l])
         for l, lay in enumerate(layers):
             w = flat.w16(lay.multihead_attn.in_proj_weight)[E:]
-            K.linear_dx(dk16[l], w, out=dv, accumulate=True)
+            K.linear_dx(dk16[l], w, out=dv, accumulate=l > 0)
             if Lt:
-                K.linear_dx(dt16[l], w, out=dtt, accumulate=True)
+                K.linear_dx(dt16[l], w, out=dtt, accumulate=l > 0)
         # The weight gradients (query-side outer products over all steps, memory K/V projections,
         # the summary token) feed nothing downstream: a second stream runs them — and then the
         # decoder's optimizer update, which rewrites the weights dv / dt were just computed with —
