@@ -6,6 +6,7 @@ Conventions: activations are 2-D row-major [rows, features]; weights are nn.Line
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -16,6 +17,7 @@ BF16 = torch.bfloat16
 F16 = torch.float16
 F32 = torch.float32
 NUM_CU = 256
+_SPLIT_PER_CU = float(os.environ.get("LRCE_SPLITK_PER_CU", "2"))   # A/B knob: split-K blocks per CU
 
 
 class KernelTimer:
@@ -177,7 +179,7 @@ def ln_bwd_prologue(x, mean, rstd, gamma, *, dgamma=None, dbeta=None, y_out=None
 def _split_for(m_out, n_out, k_red):
     """Split-K factor of a weight-gradient GEMM: ~2 blocks of 128x128 per CU, K slices >= 1024 deep."""
     tiles = math.ceil(m_out / 128) * math.ceil(n_out / 128)
-    want = max(1, math.ceil(2 * NUM_CU / tiles))
+    want = max(1, math.ceil(_SPLIT_PER_CU * NUM_CU / tiles))
     return int(max(1, min(want, k_red // 1024)))
 
 
