@@ -111,3 +111,39 @@ def test_video_extractor_matches_golden_slice(swin):
     with torch.no_grad():
         f = v(clips.cuda())
     assert rel(f[..., :64], torch.from_numpy(g["video_features_slice"])) < 2e-2
+
+
+@pytest.mark.parametrize("hw", [14, 13])
+def test_block_gradient_handoff_is_bit_exact(swin, hw):
+    """Consecutive blocks of a stage hand the earlier block's bf16, DropPath-scaled output gradient
+    over from the later block's LN1 backward (video_swin._Handoff) instead of a separate scale-cast
+    launch.  Train mode (per-clip DropPath scales, stage 3: rates > 0), whole-window and padded
+    volumes: every gradient equal bit for bit to the path without the handoff where that path is
+    itself run-to-run deterministic (the input gradient, the GEMM weight gradients), within 1e-6
+    where it is not (LN γ/β partials and bias sums are added by atomics in arrival order)."""
+    from lrce.feature_extractor import video_swin as vs
+    v, _ = swin
+    v.train()
+    try:
+        torch.manual_seed(3)
+        x = torch.randn(3, 3, hw, hw, 512, device="cuda")
+        R = torch.randn(3, 3, (hw + 1) // 2, (hw + 1) // 2, 1024, device="cuda")
+        grads = []
+        for handoff in (True, False, False):
+            vs._HANDOFF = handoff
+            v.zero_grad(set_to_none=True)
+            torch.manual_seed(4)
+            xg = x.clone().requires_grad_(True)
+            (v.swin.forward_stage(2, xg, depth=4) * R).sum().backward()
+            named = dict(v.named_parameters())
+            grads.append([xg.grad] + [named[f"swin.layers.2.blocks.{b}.{k}"].grad.clone() for b in range(4)
+                                      for k in ("mlp.fc2.weight", "mlp.fc1.bias", "norm2.weight", "attn.qkv.weight")])
+        names = ["x"] + [f"{b}.{k}" for b in range(4) for k in ("fc2.w", "fc1.b", "norm2.w", "qkv.w")]
+        for name, a, b, c in zip(names, *grads):
+            if torch.equal(b, c):
+                assert torch.equal(a, b), name
+            else:
+                assert rel(a, b) < 1e-6, (name, rel(a, b), rel(b, c))
+    finally:
+        vs._HANDOFF = True
+        v.eval()

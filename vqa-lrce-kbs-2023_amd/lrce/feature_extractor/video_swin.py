@@ -310,11 +310,49 @@ def _bin_rows(at, window):
     return hit[1]
 
 
+_HANDOFF = True   # tests switch it off to compare against the separate scale-cast launch
+
+
+class _Handoff:
+    """Backward link between two consecutive blocks of a stage.  The later block's LN1 backward (which
+    writes dx, the earlier block's output gradient) also writes it as bf16 scaled by the earlier
+    block's DropPath dp2 — the A operand of that block's MLP GEMMs — instead of a separate f32 read +
+    cast launch.  The earlier block takes the copy only if its dout IS that dx (same storage, shape,
+    strides, version: the handoff holds dx, so its memory cannot have been reused)."""
+    __slots__ = ("scale", "dx", "dx16", "ver")
+
+    def __init__(self, scale):
+        self.scale, self.dx, self.dx16, self.ver = scale, None, None, -1
+
+    def put(self, dx, dx16):
+        self.dx, self.dx16, self.ver = dx, dx16, dx._version
+
+    def take(self, dout):
+        dx, dx16 = self.dx, self.dx16
+        self.dx = self.dx16 = None
+        if (dx is None or dout.data_ptr() != dx.data_ptr() or dout.shape != dx.shape or dout.stride() != dx.stride()
+                or dout._version != self.ver):
+            return None
+        return dx16
+
+
+def _run_blocks(blocks, x, geo, flat, scales):
+    """The blocks of one stage in order; scales [(dp1, dp2)] per block (None entries in eval)."""
+    links = [None] + [_Handoff(scales[j - 1][1]) if _HANDOFF else None for j in range(1, len(blocks))]
+    for j, blk in enumerate(blocks):
+        dp1, dp2 = scales[j]
+        x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, links[j], links[j + 1] if j + 1 < len(blocks) else None,
+                               *blk.parameters())
+    return x
+
+
 class _SwinBlockFn(torch.autograd.Function):
     """One SwinTransformerBlock3D (video_swin_ori.py:248-306) forward / backward."""
 
     @staticmethod
-    def forward(ctx, x, blk, geo, flat, dp1, dp2, *params):
+    def forward(ctx, x, blk, geo, flat, dp1, dp2, up, down, *params):
+        """up: the _Handoff this block's backward fills for the block before it; down: the one the
+        block after it fills for this block (either None)."""
         C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
         at = blk.attn
         shifted = geo.shifted and any(s > 0 for s in blk.shift_size)
@@ -351,7 +389,7 @@ class _SwinBlockFn(torch.autograd.Function):
         if any(t.requires_grad for t in (x,) + params):
             ctx.save = (x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_b)
             ctx.blk, ctx.geo, ctx.flat, ctx.dp1, ctx.dp2 = blk, geo, flat, dp1, dp2
-            ctx.wmap, ctx.win_pat = wmap, win_pat
+            ctx.wmap, ctx.win_pat, ctx.up, ctx.down = wmap, win_pat, up, down
             ctx.sp2win = geo.sp2win_shift if shifted else geo.sp2win
         return out
 
@@ -362,10 +400,13 @@ class _SwinBlockFn(torch.autograd.Function):
         at = blk.attn
         C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
         rpc = geo.rows_per_clip
+        dout16 = ctx.down.take(dout) if ctx.down is not None else None
         dout = dout.contiguous()
         # MLP branch: y = x_mid + s2 * fc2(gelu(fc1(LN2(x_mid)))).  The branch's GEMMs read the
-        # DropPath-scaled gradient as one bf16 copy (the A operand of both dW and dX).
-        dout16 = K.scale_cast_bf16(dout, dp2, rpc)
+        # DropPath-scaled gradient as one bf16 copy (the A operand of both dW and dX), written by the
+        # next block's LN1 backward when there is one
+        if dout16 is None:
+            dout16 = K.scale_cast_bf16(dout, dp2, rpc)
         _wgrad(flat, blk.mlp.fc2, dout16, g)
         dpre = K.linear_dx(dout16, flat.w16(blk.mlp.fc2.weight), out_f32=False, dgelu_pre=pre)
         del g, pre, dout16
@@ -396,9 +437,17 @@ class _SwinBlockFn(torch.autograd.Function):
         dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight))
         del dqkv, qkv, xw
         dx = torch.empty_like(x)
+        up = ctx.up
+        # for the previous block: dx as bf16 times its dp2, in token order (rows r of this LN are in
+        # window order, clip-major: the scale index is r / rows-per-clip in window order)
+        dx16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if up is not None else None
         K.layernorm_bwd(dxw, x, m1, r1, blk.norm1.weight, dx, in_map=wmap, dres=dx_mid,
-                        dw=_g(flat, blk.norm1.weight), db=_g(flat, blk.norm1.bias))
-        ctx.save = None
+                        dw=_g(flat, blk.norm1.weight), db=_g(flat, blk.norm1.bias), dx16=dx16,
+                        dx16_map=wmap if up is not None else None, dx_scale=up.scale if up is not None else None,
+                        dx_scale_rps=geo.win_rows_per_clip)
+        if up is not None:
+            up.put(dx, dx16)
+        ctx.save = ctx.up = ctx.down = None
         flat.notify(blk.parameters())
         group = getattr(blk, "_lrce_group", None)
         if group is not None and flat.early_update is not None:
@@ -410,7 +459,7 @@ class _SwinBlockFn(torch.autograd.Function):
             s.wait_stream(main)
             with torch.cuda.stream(s):
                 flat.group_done(group)
-        return (dx, None, None, None, None, None) + (None,) * len(ctx.needs_input_grad[6:])
+        return (dx, None, None, None, None, None, None, None) + (None,) * len(ctx.needs_input_grad[8:])
 
 
 class _PatchMergeFn(torch.autograd.Function):
@@ -504,10 +553,10 @@ class SwinTransformer3D(nn.Module):
         bi = 0
         for layer in self.layers:
             geo = stage_geometry(nc, D, H, W, self.window_size, dev)
-            for blk in layer.blocks:
-                dp1, dp2 = scales[bi] if scales is not None else (None, None)
-                bi += 1
-                x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, *blk.parameters())
+            nb = len(layer.blocks)
+            x = _run_blocks(list(layer.blocks), x, geo, flat,
+                            scales[bi:bi + nb] if scales is not None else [(None, None)] * nb)
+            bi += nb
             if layer.downsample is not None:
                 x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())
                 H, W = (H + 1) // 2, (W + 1) // 2
@@ -523,10 +572,10 @@ class SwinTransformer3D(nn.Module):
         geo = stage_geometry(nc, D, H, W, self.window_size, x_cl.device)
         x = x_cl.reshape(-1, C).contiguous()
         layer = self.layers[i]
-        for blk in list(layer.blocks)[:depth]:
-            dp1 = _drop_path_scale(blk.drop_path, nc, x.device, self.training)
-            dp2 = _drop_path_scale(blk.drop_path, nc, x.device, self.training)
-            x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, *blk.parameters())
+        blocks = list(layer.blocks)[:depth]
+        scales = [(_drop_path_scale(blk.drop_path, nc, x.device, self.training),
+                   _drop_path_scale(blk.drop_path, nc, x.device, self.training)) for blk in blocks]
+        x = _run_blocks(blocks, x, geo, flat, scales)
         if layer.downsample is not None:
             x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())
             H, W = (H + 1) // 2, (W + 1) // 2
