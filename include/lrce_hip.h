@@ -288,6 +288,10 @@ int lrce_frames_resize(const uint8_t* frames, int n_frames, int H, int W, const 
  * scale optional): bias gradients (nn.Linear bias, incl. DropPath-scaled branches) */
 int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int64_t ld, int m, int n, const float* row_scale,
                 int rows_per_scale, float* out, void* stream);
+/* dst[i] = bf16(sum over r < nshard of src[r * len + i]), summed in f32 in rank order (len % 8 == 0,
+ * 16-B aligned): the local reduce of the data-parallel gradient exchange (bf16 all-to-all -> this ->
+ * bf16 all-gather), replacing the f32 sum of the reference's DDP all-reduce (agent_base.py:76). */
+int lrce_sum_shards_bf16(const uint16_t* src, int nshard, int64_t len, uint16_t* dst, void* stream);
 /* f32 -> bf16 cast (n elements) */
 int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
 /* f32 -> IEEE fp16 cast (n elements): the BERT forward's GEMM operands */

@@ -49,12 +49,20 @@ def _worker(rank, world, port, mode, q):
         torch.manual_seed(0)
         model = _Toy()
         flat = FlatParams(model, "cpu", order=list(model.parameters())[::-1])
-        red = GradReducer(flat, bucket_mb=1)
+        if mode == "bf16":
+            # the exchange's two native kernels, restated in torch for CPU tensors (test stand-ins:
+            # the product raises on CPU tensors)
+            from lrce import kernels as K
+            K.cast_bf16 = lambda x, y: y.copy_(x.to(torch.bfloat16))
+            K.sum_shards_bf16 = lambda src, n, dst: dst.copy_(src.view(n, -1).float().sum(0).to(torch.bfloat16))
+            red = GradReducer(flat, bucket_mb=1, grad_dtype=torch.bfloat16)
+        else:
+            red = GradReducer(flat, bucket_mb=1)
         out = {"n_buckets": len(red.buckets)}
         # rank-specific gradients: g_r = (r + 1) * base
         base = torch.arange(flat.total, dtype=torch.float32) % 97
         flat.grad.copy_(base * (rank + 1))
-        if mode == "notify":
+        if mode in ("notify", "bf16"):
             # report parameters in backward order; buckets launch as they complete
             for p in reversed(list(model.parameters())):
                 red.notify([p])
@@ -63,8 +71,13 @@ def _worker(rank, world, port, mode, q):
         else:
             scale = red.reduce_all()
         out["scale"] = scale
-        out["grad_sum"] = flat.grad.double().sum().item()
-        out["grad_head"] = flat.grad[:8].tolist()   # plain data: no shared-memory handle outlives the child
+        g = red.reduced_grad().float()
+        out["grad_sum"] = g.double().sum().item()
+        out["grad_head"] = g[:8].tolist()   # plain data: no shared-memory handle outlives the child
+        if mode == "bf16":
+            # the f32 sum of the ranks' bf16 copies, rounded once: here exact (small integers)
+            ref = ((base * (rank + 1)).to(torch.bfloat16).float() + (base * (2 - rank)).to(torch.bfloat16).float())
+            out["bf16_exact"] = bool(torch.equal(g, ref.to(torch.bfloat16).float()))
         out["param_view_is_flat"] = all(p.grad.data_ptr() == flat.g32(p).data_ptr() for p in model.parameters())
         q.put((rank, out))
     finally:
@@ -85,7 +98,7 @@ def _run(mode, world=2):
     return res
 
 
-@pytest.mark.parametrize("mode", ["notify", "reduce_all"])
+@pytest.mark.parametrize("mode", ["notify", "reduce_all", "bf16"])
 def test_grad_reducer_sums_over_ranks_gloo(mode):
     res = _run(mode)
     r0, r1 = res[0], res[1]
@@ -97,8 +110,11 @@ def test_grad_reducer_sums_over_ranks_gloo(mode):
     assert r0["grad_head"] == (3 * base_head).tolist()
     assert r0["grad_sum"] == pytest.approx(r1["grad_sum"])
     assert r0["param_view_is_flat"] and r1["param_view_is_flat"]
-    if mode == "notify":
+    if mode in ("notify", "bf16"):
         assert r0["launched_before_finish"] == r0["n_buckets"]   # every bucket launched from notify()
+    if mode == "bf16":
+        # bf16 transport (all-to-all, f32 shard sum, all-gather): same sums on every rank
+        assert r0["bf16_exact"] and r1["bf16_exact"]
 
 
 def test_flat_layout_alignment_cpu():

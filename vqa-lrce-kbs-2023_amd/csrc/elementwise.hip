@@ -330,6 +330,35 @@ extern "C" int lrce_scale_cast_bf16(const float* x, int64_t rows, int cols, cons
   return lrce_check_launch("scale_cast_bf16");
 }
 
+// dst[i] = bf16(sum_r src[r * len + i]) with the sum in f32, r in ascending order (deterministic):
+// the reduce step of the data-parallel gradient exchange (all-to-all of bf16 shards, this sum, then an
+// all-gather), so the cross-rank sum is f32 with one bf16 rounding of the result.  8 elements / thread.
+__global__ void sum_shards_kernel(const bf16* __restrict__ src, int nshard, long long len, bf16* __restrict__ dst) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= len) return;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = 0; r < nshard; ++r) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + (long long)r * len + i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+  *reinterpret_cast<bf16x8*>(dst + i) = o;
+}
+
+extern "C" int lrce_sum_shards_bf16(const uint16_t* src, int nshard, int64_t len, uint16_t* dst, void* stream) {
+  if (!src || !dst) return lrce_fail(LRCE_E_ARG, "sum_shards_bf16: null pointer");
+  if (nshard < 1 || len % 8 || ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15))
+    return lrce_fail(LRCE_E_ARG, "sum_shards_bf16: nshard=%d, len %% 8 == 0 and 16-B aligned buffers needed", nshard);
+  if (len <= 0) return LRCE_OK;
+  const long long thr = len / 8;
+  sum_shards_kernel<<<(unsigned)((thr + 255) / 256), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      reinterpret_cast<const bf16*>(src), nshard, len, reinterpret_cast<bf16*>(dst));
+  return lrce_check_launch("sum_shards_bf16");
+}
+
 extern "C" int lrce_cast_bf16(const float* x, uint16_t* y, int64_t n, void* stream) {
   if (!x || !y) return lrce_fail(LRCE_E_ARG, "cast_bf16: null pointer");
   if (n <= 0) return LRCE_OK;

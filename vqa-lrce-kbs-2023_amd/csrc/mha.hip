@@ -551,24 +551,66 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
   stage64<LP>(S.q, qb, d.ld_q, L, lane);
   stage64<LP>(S.k, kb, d.ld_kv1, L, lane);
   stage64<LP>(S.dout, gb, d.ld_o, L, lane);
-  for (int i = lane; i < LP; i += 64) {
-    float dl = 0.f, l2 = 0.f;
-    if (i < L) {
-#pragma unroll
-      for (int part = 0; part < 8; ++part) {
-        const bf16x8 a = ldrow16(ob + i * d.ld_o + part * 8), g = ldrow16(gb + i * d.ld_o + part * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dl += bf2f(a[j]) * bf2f(g[j]);
-      }
-      l2 = d.lse[((long long)b * d.H + h) * L + i] * LOG2E_F;
-    }
-    S.delta[i] = dl;
-    S.lse2[i] = l2;
-  }
+  (void)ob;
   wave_lds_fence_m();
   const int hh = lane >> 5, r32 = lane & 31;
   const int* km = d.key_mask ? d.key_mask + (long long)b * L : nullptr;
   const float c2 = d.scale * LOG2E_F;
+  // Pass 1: this kernel's own softmax statistics.  The forward ran on fp16 operands; its lse and O
+  // do not match the scores recomputed here from bf16 Q / K, and a normalisation that does not sum
+  // to one over the recomputed scores (or delta = dO.O from another P) leaves sum_j dS_ij != 0,
+  // which swamps the small true dS of near-uniform attention rows.  So: per query row, max and sum
+  // of the recomputed scores (whole row: L <= 64 keys) and delta_i = sum_j P_ij f_ij dP_ij from the
+  // same P and dP — the row sums of dS are then zero up to f32 rounding.  Scores / dP transposed
+  // (key rows, query on the lane) so the row reductions stay in registers + one cross-half swap.
+#pragma unroll
+  for (int qt = 0; qt < NTL; ++qt) {
+    const int qi = qt * 32 + r32;
+    f32x16 st[NTL], dpt[NTL];
+#pragma unroll
+    for (int kt = 0; kt < NTL; ++kt) {
+      st[kt] = dpt[kt] = f32x16{};
+      const int key = kt * 32 + r32;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(S.q + qi * D + 16 * s + 8 * hh);
+        const bf16x8 ga = *reinterpret_cast<const bf16x8*>(S.dout + qi * D + 16 * s + 8 * hh);
+        const bf16x8 kk = *reinterpret_cast<const bf16x8*>(S.k + key * D + 16 * s + 8 * hh);
+        const bf16x8 vv = key < L ? ldrow16(vb + key * d.ld_kv1 + 16 * s + 8 * hh) : bf16x8{};
+        st[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qa, st[kt], 0, 0, 0);
+        dpt[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, ga, dpt[kt], 0, 0, 0);
+      }
+    }
+    float m = -1.0e30f;
+#pragma unroll
+    for (int kt = 0; kt < NTL; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + crow32(r, hh);
+        if (key < L && (!km || km[key] != 0)) m = fmaxf(m, st[kt][r]);
+      }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f, dl = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NTL; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + crow32(r, hh);
+        if (key < L && (!km || km[key] != 0)) {
+          const float p = __builtin_amdgcn_exp2f((st[kt][r] - m) * c2);
+          const float f = d.drop_p > 0.f ? drop_factor(d, P.off, b, h, qi, key, L) : 1.f;
+          sum += p;
+          dl += p * f * dpt[kt][r];
+        }
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    if (hh == 0) {
+      S.lse2[qi] = sum > 0.f ? m * c2 + __log2f(sum) : 0.f;
+      S.delta[qi] = sum > 0.f ? dl / sum : 0.f;
+    }
+  }
+  wave_lds_fence_m();
   f32x16 dq[NTL][2];
 #pragma unroll
   for (int qt = 0; qt < NTL; ++qt) dq[qt][0] = dq[qt][1] = f32x16{};

@@ -109,6 +109,7 @@ _SIGS = {
     "lrce_patch_im2col": [_P, _I, _I, _I, _I, _I64, _I64, _I64, _I, _P, _P],
     "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _I, _P, _P],
     "lrce_cast_bf16": [_P, _P, _I64, _P],
+    "lrce_sum_shards_bf16": [_P, _I, _I64, _P, _P],
     "lrce_cast_f16": [_P, _P, _I64, _P],
     "lrce_cast_f16_bf16": [_P, _P, _I64, _P],
     "lrce_dropout": [_P, _P, _P, _P, _I64, _F, _U64, _I64, _P],

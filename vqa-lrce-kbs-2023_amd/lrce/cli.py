@@ -45,6 +45,13 @@ def _additive(p):
     p.add_argument("--seed", type=int, default=0, help="synthetic data seed")
     p.add_argument("--allow-random-init", action="store_true",
                    help="train from random backbones when the pretrained Swin / BERT weights are missing")
+    p.add_argument("--eager", action="store_true",
+                   help="launch every training step from Python instead of replaying it from HIP graphs")
+    p.add_argument("--log-interval", type=int, default=50,
+                   help="steps between reads of the device-side loss / metric sums")
+    p.add_argument("--grad-reduce-dtype", choices=["bf16", "f32"], default="bf16",
+                   help="data-parallel gradient exchange: bf16 on the wire with the cross-rank sum in f32 "
+                        "(default), or f32 all-reduce")
 
 
 def _merge_config(result):

@@ -6,9 +6,13 @@ GPU, same model replica, rank-strided batches, gradients averaged every step.  D
   ~bucket_mb contiguous buckets; each native autograd Function reports the parameters it finished,
   and a bucket's all-reduce is started the moment its last parameter is done — so the reduction of
   the fusion / BERT / late-Swin buckets overlaps the rest of the backward;
-* optional bf16 buckets (grad_dtype=torch.bfloat16): the finished bucket is cast once into a bf16
-  mirror of the gradient buffer and THAT is all-reduced (half the xGMI bytes: 0.62 GB instead of
-  1.25 GB per step); the fused AdamW kernel then reads the bf16 gradient directly;
+* optional bf16 transport (grad_dtype=torch.bfloat16): the finished bucket is cast once into a bf16
+  mirror of the gradient buffer and exchanged as an all-to-all of bf16 shards -> a native f32 sum of
+  the world's copies of this rank's shard (lrce_sum_shards_bf16) -> an all-gather of the bf16 sums:
+  the same bytes on the xGMI links as a bf16 ring all-reduce (2 (N-1)/N of 0.62 GB instead of 1.25
+  GB per step), but the cross-rank sum is f32 (the reference's DDP sums f32), rounded to bf16 once;
+  the fused AdamW kernel then reads the bf16 sum directly.  The three steps of a bucket run on a
+  communication stream, so the backward on the compute stream never waits for them;
 * HIP-graph mode: when the backward is captured into a graph, a finished bucket's bf16 cast is
   captured with it and the bucket is remembered in completion order; after each replay
   `replay_allreduce()` issues the bucket all-reduces in that order, asynchronously on RCCL's stream,
@@ -23,10 +27,16 @@ Parameters no Function reports (the unused BERT pooler) sit in the last bucket, 
 Collectives are issued in bucket-completion order, which is the same on every rank (the backward
 is deterministic), as RCCL requires.
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
 
 from . import kernels as K
+
+
+def _nullctx():
+    return contextlib.nullcontext()
 
 
 class GradReducer:
@@ -40,6 +50,7 @@ class GradReducer:
         # the reduced gradient the optimizer reads (f32: flat.grad itself)
         self.grad16 = torch.zeros(flat.total, dtype=torch.bfloat16, device=flat.device) \
             if grad_dtype == torch.bfloat16 else None
+        self.comm = torch.cuda.Stream(device=flat.device) if flat.device.type == "cuda" else None
         lim = int(bucket_mb * (1 << 20) // 4)
         self.buckets = []          # (start, end, [param ids])
         self.param_bucket = {}
@@ -58,6 +69,13 @@ class GradReducer:
         for bi, (_, _, ids) in enumerate(self.buckets):
             for i in ids:
                 self.param_bucket[i] = bi
+        # bf16 exchange scratch: the all-to-all receive buffer (world shards of the largest bucket) and
+        # this rank's summed shard; one each, the buckets' exchanges are ordered on the comm stream
+        self.recv = self.shard = None
+        if self.grad16 is not None and self.world > 1:
+            big = max(e - s for s, e, _ in self.buckets)
+            self.recv = torch.empty(big, dtype=torch.bfloat16, device=flat.device)
+            self.shard = torch.empty(-(-big // self.world), dtype=torch.bfloat16, device=flat.device)
         self.capturing = False
         self.captured = None       # buckets in completion order (graph mode)
         self.begin()
@@ -95,7 +113,41 @@ class GradReducer:
         if self.capturing:
             self.captured.append(bi)
         elif self.world > 1:
-            self.handles.append(dist.all_reduce(self._buf(bi), group=self.group, async_op=True))
+            self._exchange(bi)
+
+    def _exchange(self, bi):
+        """Sum bucket bi over the ranks, asynchronously w.r.t. the current (compute) stream.  f32: one
+        all-reduce.  bf16: all-to-all of bf16 shards, f32 sum of this rank's shard, all-gather — on the
+        comm stream (after the current stream's work so far), which finish() joins."""
+        s, e, _ = self.buckets[bi]
+        if self.grad16 is None:
+            self.handles.append(dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True))
+            return
+        n, w = e - s, self.world
+        if n % (8 * w):
+            # a bucket that does not split into 16-B-aligned shards (only with an odd world size):
+            # plain bf16 all-reduce of that bucket
+            self.handles.append(dist.all_reduce(self.grad16[s:e], group=self.group, async_op=True))
+            return
+        sh = n // w
+        if self.comm is not None:
+            self.comm.wait_stream(torch.cuda.current_stream(self.flat.device))
+            ctx = torch.cuda.stream(self.comm)
+        else:
+            ctx = _nullctx()
+        with ctx:
+            recv = self.recv[:n]
+            dist.all_to_all_single(recv, self.grad16[s:e], group=self.group)
+            K.sum_shards_bf16(recv, w, self.shard[:sh])
+            dist.all_gather_into_tensor(self.grad16[s:e], self.shard[:sh], group=self.group)
+
+    def _join(self):
+        """The current stream waits for every exchange issued so far."""
+        for h in self.handles:
+            h.wait()
+        self.handles = []
+        if self.comm is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.comm)
 
     def notify(self, params):
         cur = torch.cuda.current_stream(self.flat.grad.device) if self.flat.grad.is_cuda else None
@@ -118,8 +170,7 @@ class GradReducer:
             self._launch(bi)
         if self.capturing:
             return 1.0 / self.world
-        for h in self.handles:
-            h.wait()
+        self._join()
         self.begin()
         return 1.0 / self.world
 
@@ -149,9 +200,10 @@ class GradReducer:
         if order is None:
             raise RuntimeError("replay_allreduce: no captured backward")
         if self.world > 1:
-            handles = [dist.all_reduce(self._buf(bi), group=self.group, async_op=True) for bi in order]
-            for h in handles:
-                h.wait()
+            self.handles = []
+            for bi in order:
+                self._exchange(bi)
+            self._join()
         return 1.0 / self.world
 
 

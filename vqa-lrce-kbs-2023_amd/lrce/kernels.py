@@ -496,6 +496,14 @@ def cast_bf16(x, y):
     call("lrce_cast_bf16", ptr(x), ptr(y), x.numel(), stream_of(y))
 
 
+def sum_shards_bf16(src, nshard, dst):
+    """dst = bf16(sum of the nshard equal bf16 slices of src, in f32, in slice order)."""
+    _chk(src, BF16, "src"); _chk(dst, BF16, "dst")
+    if src.numel() != nshard * dst.numel():
+        raise N.NativeError(f"sum_shards_bf16: {src.numel()} elements != {nshard} x {dst.numel()}")
+    call("lrce_sum_shards_bf16", ptr(src), nshard, dst.numel(), ptr(dst), stream_of(dst))
+
+
 def cast_f16(x, y):
     call("lrce_cast_f16", ptr(x), ptr(y), x.numel(), stream_of(y))
 
