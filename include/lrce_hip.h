@@ -182,10 +182,12 @@ int64_t lrce_layernorm_bwd_workspace(int rows, int cols);
  * (relative_position_bias_table) and the int64 relative_position_index (ld = index_ld), with the
  * shift mask of each window pattern given as per-token region ids region[n_pat][n] (-100 between
  * different regions, video_swin_ori.py:346-359); bias_fwd holds the S^T-oriented tiles (forward),
- * bias_bwd the S-oriented ones (backward). */
+ * bias_bwd the S-oriented ones (backward).  fwd_f16: bias_fwd as IEEE fp16 (what lrce_wattn_qkv_fwd
+ * reads; padded keys -30000) instead of f32 (lrce_wattn_fwd_grouped). */
 int64_t lrce_wattn_bias_elems(int n_pat, int nH);
 int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
-                          const int32_t* region, int n_pat, float* bias_fwd, float* bias_bwd, void* stream);
+                          const int32_t* region, int n_pat, void* bias_fwd, int fwd_f16, float* bias_bwd,
+                          void* stream);
 /* Forward with windows grouped by mask pattern, GW = 4 windows per group: win_list int32
  * [n_groups*4] (window ids, -1 = empty slot; NULL = identity 0,1,2,...), grp_pat int32 [n_groups]
  * (the group's mask pattern; NULL = pattern 0).  The bias row of a query tile is staged once per
@@ -196,10 +198,13 @@ int lrce_wattn_fwd_grouped(const uint16_t* qkv, const float* bias_fwd, const int
  * including the qkv Linear :150,165): x bf16 [n_win*n][C] (LN1 output in window order), w_qkv bf16
  * [3C][C], b_qkv f32 [3C]; q is scaled by qscale (= head_dim^-0.5 * log2(e)) after the bias.  Writes
  * qkv bf16 [n_win*n][3C] (the backward's input, same layout as above), out and lse as
- * lrce_wattn_fwd_grouped.  One workgroup per (window, 4 heads); nH % 4 == 0, C % 64 == 0. */
+ * lrce_wattn_fwd_grouped.  bias_fwd16: the fp16 forward tiles (lrce_wattn_bias_build with fwd_f16).
+ * win_order int32 [n_win]: the order the windows are visited in (NULL = identity; sorted by mask
+ * pattern, so one XCD's workgroups share few bias tiles).  One workgroup per (window, 2 heads);
+ * nH % 2 == 0. */
 int lrce_wattn_qkv_fwd(const uint16_t* x, const uint16_t* w_qkv, const float* b_qkv, float qscale,
-                       const float* bias_fwd, const int32_t* win_pat, uint16_t* qkv, uint16_t* out, float* lse,
-                       int n_win, int n, int nH, void* stream);
+                       const uint16_t* bias_fwd16, const int32_t* win_pat, const int32_t* win_order, uint16_t* qkv,
+                       uint16_t* out, float* lse, int n_win, int n, int nH, void* stream);
 /* Backward (one kernel): dqkv bf16 [n_win*n][3C] (d/dq, d/dk, d/dv w.r.t. the UNSCALED q).  win_pat
  * int32 [n_win] (the window's mask pattern, NULL = 0).  The window is wd x wh x ww tokens (n = wd*wh*ww,
  * token order (t, h, w)); dbias_part: f32, lrce_wattn_dbias_part_elems(n_win, nH, n_bins) elements with

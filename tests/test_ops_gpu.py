@@ -416,7 +416,8 @@ def test_window_attention_fwd_bwd(nH, n_win):
         assert rel(got, want) < 1.5e-2
 
 
-@pytest.mark.parametrize("nH,n_win,shifted", [(4, 9, True), (8, 4, False), (16, 5, True), (32, 2, False)])
+@pytest.mark.parametrize("nH,n_win,shifted", [(4, 9, True), (8, 4, False), (16, 5, True), (32, 2, False), (2, 3, True),
+                                             (6, 7, True)])
 def test_window_attention_fused_qkv_forward(nH, n_win, shifted):
     """lrce_wattn_qkv_fwd (QKV projection + attention in one kernel) vs the two-kernel path (QKV GEMM
     with the q-scale epilogue, then the grouped attention forward) and vs an fp32 reference."""
@@ -438,10 +439,14 @@ def test_window_attention_fused_qkv_forward(nH, n_win, shifted):
     bf_ = torch.empty(k.wattn_bias_elems(n_pat, nH), device=dev)
     bb_ = torch.empty_like(bf_)
     k.wattn_bias_build(table, index, n, nH, region if shifted else None, n_pat, bf_, bb_)
+    bfh = torch.empty(k.wattn_bias_elems(n_pat, nH), device=dev, dtype=torch.float16)   # the fused kernel's fp16 tiles
+    k.wattn_bias_build(table, index, n, nH, region if shifted else None, n_pat, bfh, bb_)
     qkv = torch.full((n_win * n, 3 * C), float("nan"), device=dev, dtype=torch.bfloat16)
     out = torch.full((n_win * n, C), float("nan"), device=dev, dtype=torch.bfloat16)
     lse = torch.zeros(n_win, nH, 160, device=dev)
-    k.wattn_qkv_fwd(x, w, bias, c, bf_, win_pat, qkv, out, lse, n_win, n, nH)
+    # windows visited in mask-pattern order (the product path's win_order), or identity
+    order = torch.argsort(win_pat.long(), stable=True).int() if shifted else None
+    k.wattn_qkv_fwd(x, w, bias, c, bfh, win_pat, qkv, out, lse, n_win, n, nH, win_order=order)
     qkv2 = k.linear(x, w, bias, scale_cols=C, scale_val=c)
     assert rel(qkv, qkv2) < 1e-2                        # same products, bf16 rounding of the outputs
     out2 = torch.empty_like(out)

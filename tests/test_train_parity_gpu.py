@@ -11,8 +11,8 @@ term: it is folded into the AdamW kernel and checked against torch there (test_o
 Every floating-point parameter is compared (783 tensors); tensors whose oracle gradient is exactly
 zero (BERT pooler, decoder self-attention q/k: softmax over one key) must be zero here too, and the
 analytically-zero BERT key biases (rounding noise on both sides) small against the query biases.
-Tolerance per tensor, as max|d| / max|ref| against the fp32 oracle: TOL[family] (3e-2 for the bf16
-backward of Swin and BERT, 2e-2 for the exact-f32 decoder query side), or — for the
+Tolerance per tensor, as max|d| / max|ref| against the fp32 oracle: TOL[family] (3e-2: bf16
+GEMM operands and backward), or — for the
 tensors whose gradient the reference's own training numerics cannot resolve to that — the error the
 reference's fp16 autocast (agent_oe.py:28) makes on the same batch, from the committed fixture
 tests/golden/train_grad_yardstick.json (make_train_yardstick.py), or half the error of its bf16
@@ -39,9 +39,9 @@ CFG = {"msvd-qa-oe": ("oe", 1000, 32), "tgif-transition": ("mc", 1, 40)}
 WORKLOADS = [("msvd-qa-oe", 10), ("tgif-transition", 9)]
 SEED = 31
 
-# max|d| / max|ref| per tensor family: bf16 GEMM operands and bf16 backward (Swin, BERT), exact-f32
-# decoder query side (fusion)
-TOL = {"swin": 3e-2, "bert": 3e-2, "fusion": 2e-2}
+# max|d| / max|ref| per tensor family: bf16 GEMM operands and bf16 backward (Swin, BERT); the fusion
+# gradients inherit the bf16 features (the MC head's single logit is a cancellation-heavy sum)
+TOL = {"swin": 3e-2, "bert": 3e-2, "fusion": 3e-2}
 YARD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_grad_yardstick.json")
 
 

@@ -47,6 +47,9 @@ def main():
         be = K.wattn_bias_elems(n_pat, nH)
         bf_, bb_ = torch.empty(be, device=dev), torch.empty(be, device=dev)
         K.wattn_bias_build(table, idx, n, nH, region, n_pat, bf_, bb_)
+        bfh = torch.empty(be, device=dev, dtype=torch.float16)
+        K.wattn_bias_build(table, idx, n, nH, region, n_pat, bfh, bb_)
+        order = torch.argsort(win_pat.long(), stable=True).int()
         out = torch.empty(n_win * n, C, device=dev, dtype=torch.bfloat16)
         lse = torch.empty(n_win * nH * 160, device=dev)
         dout = (torch.randn(n_win * n, C, device=dev, generator=g) * 0.5).to(torch.bfloat16)
@@ -58,7 +61,7 @@ def main():
         x = (torch.randn(n_win * n, C, device=dev, generator=g) * 0.5).to(torch.bfloat16)
         wq = (torch.randn(3 * C, C, device=dev, generator=g) / C ** 0.5).to(torch.bfloat16)
         bq = torch.zeros(3 * C, device=dev)
-        tq = timeit(lambda: K.wattn_qkv_fwd(x, wq, bq, 0.25, bf_, win_pat, qkv, out, lse, n_win, n, nH))
+        tq = timeit(lambda: K.wattn_qkv_fwd(x, wq, bq, 0.25, bfh, win_pat, qkv, out, lse, n_win, n, nH, win_order=order))
         tg = timeit(lambda: K.linear(x, wq, bq, out=qkv, scale_cols=C, scale_val=0.25))
         fq = 2.0 * n_win * n * C * 3 * C + 4.0 * n * n * hd * n_win * nH
         print(f"win {n_win:5d} heads {nH:3d}: fused qkv+attn {tq * 1e3:7.1f} us {fq / tq / 1e9:6.1f} TF/s   "

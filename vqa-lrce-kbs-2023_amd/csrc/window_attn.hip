@@ -78,8 +78,10 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int s) {
 }
 
 // ------------------------------------------------------------------------------ bias tiles
+// forward tiles f32 (bf) or fp16 (bfh, the fused QKV + attention forward: half the bytes; padded keys
+// at -30000, still exp2 -> 0), backward tiles f32 (bb)
 __global__ void bias_build_kernel(const float* table, const int64_t* index, int ld, int n, int nH,
-                                  const int* region, int n_pat, float* bf, float* bb) {
+                                  const int* region, int n_pat, float* bf, f16* bfh, float* bb) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long total = (long long)n_pat * nH * PH_ELEMS;
   if (e >= total) return;
@@ -99,7 +101,9 @@ __global__ void bias_build_kernel(const float* table, const int64_t* index, int 
     return v * LOG2E;
   };
   // forward: S^T tile (rows = keys, cols = queries)
-  bf[e] = val(qt * TQ + (lane_f & 31), kt * TQ + crow(reg_f, lane_f >> 5));
+  const float vf = val(qt * TQ + (lane_f & 31), kt * TQ + crow(reg_f, lane_f >> 5));
+  if (bfh) bfh[e] = f2h(vf < -30000.f ? -30000.f : vf);
+  else bf[e] = vf;
   const int hh = lane >> 5, col = lane & 31;
   // backward: S tile (rows = queries, cols = keys)
   bb[e] = val(qt * TQ + crow(reg, hh), kt * TQ + col);
@@ -534,12 +538,14 @@ extern "C" int64_t lrce_wattn_dbias_part_elems(int n_win, int nH, int n_bins) {
 }
 
 extern "C" int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
-                                     const int32_t* region, int n_pat, float* bias_fwd, float* bias_bwd, void* stream) {
+                                     const int32_t* region, int n_pat, void* bias_fwd, int fwd_f16, float* bias_bwd,
+                                     void* stream) {
   if (!table || !index || !bias_fwd || !bias_bwd) return lrce_fail(LRCE_E_ARG, "wattn_bias_build: null pointer");
   if (n <= 0 || n > NPAD || n_pat < 1 || nH < 1) return lrce_fail(LRCE_E_ARG, "wattn_bias_build: n=%d", n);
   const long long total = (long long)n_pat * nH * PH_ELEMS;
-  bias_build_kernel<<<(total + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(table, index, index_ld, n, nH, region,
-                                                                                    n_pat, bias_fwd, bias_bwd);
+  bias_build_kernel<<<(total + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(
+      table, index, index_ld, n, nH, region, n_pat, fwd_f16 ? nullptr : static_cast<float*>(bias_fwd),
+      fwd_f16 ? static_cast<f16*>(bias_fwd) : nullptr, bias_bwd);
   return lrce_check_launch("wattn_bias_build");
 }
 

@@ -98,9 +98,9 @@ _SIGS = {
     "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _I64,
                            _P],
     "lrce_scale_cast_bf16": [_P, _I64, _I, _P, _I, _P, _P],
-    "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _P, _P],
+    "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P],
     "lrce_wattn_fwd_grouped": [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P],
-    "lrce_wattn_qkv_fwd": [_P, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lrce_wattn_qkv_fwd": [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lrce_wattn_dbias": [_P, _I, _I, _I, _P, _P, _P],
     "lrce_mha_fwd": [ctypes.POINTER(MhaDesc), _P],

@@ -79,6 +79,9 @@ class StageGeometry:
             self.sp2win_shift = self._inverse(self.win2sp_shift)
             self.region, self.win_pat, self.n_pat = self._mask_patterns(device)
             self.groups_shift = K.wattn_groups(self.win_pat, self.n_win, device)
+            # the fused forward visits windows grouped by mask pattern (stable): the workgroups one XCD
+            # runs then share few patterns' bias tiles in its L2
+            self.win_order = torch.argsort(self.win_pat.long(), stable=True).to(torch.int32).contiguous()
         self.groups = K.wattn_groups(None, self.n_win, device)
         # PatchMerging pads odd H / W with zeros before its 2x2 gather (video_swin_ori.py:328-331)
         self.Hm, self.Wm = -(-H // 2), -(-W // 2)
@@ -359,8 +362,9 @@ class _SwinBlockFn(torch.autograd.Function):
         wmap = geo.win2sp_shift if shifted else geo.win2sp
         region, win_pat, n_pat = (geo.region, geo.win_pat, geo.n_pat) if shifted else (None, None, 1)
         dev = x.device
-        bias_f = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev)
-        bias_b = torch.empty_like(bias_f)
+        fused = nH % 2 == 0
+        bias_f = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev, dtype=torch.float16 if fused else torch.float32)
+        bias_b = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev)
         K.wattn_bias_build(at.relative_position_bias_table, at.relative_position_index, n, nH, region, n_pat,
                            bias_f, bias_b)
         Mw = geo.M_win   # window-order rows (incl. the padded positions of a partial window)
@@ -368,13 +372,13 @@ class _SwinBlockFn(torch.autograd.Function):
         c = (C // nH) ** -0.5 * LOG2E
         o = torch.empty(Mw, C, dtype=torch.bfloat16, device=dev)
         lse = torch.empty(geo.n_win, nH, 160, device=dev)
-        if nH % 4 == 0 and C % 64 == 0:
+        if fused:
             # QKV projection fused with the attention (csrc/window_fused.hip); qkv is still written
             # for the backward
             qkv = torch.empty(Mw, 3 * C, dtype=torch.bfloat16, device=dev)
             K.wattn_qkv_fwd(xw, flat.w16(at.qkv.weight), at.qkv.bias, c, bias_f, win_pat, qkv, o, lse, geo.n_win, n,
-                            nH)
-        else:   # head counts the fused kernel's 4-head groups do not divide (not Swin-B)
+                            nH, win_order=geo.win_order if shifted else None)
+        else:   # odd head counts (the fused kernel takes heads in pairs; not Swin-B)
             qkv = K.linear(xw, flat.w16(at.qkv.weight), at.qkv.bias, scale_cols=C, scale_val=c)
             K.wattn_fwd_grouped(qkv, bias_f, geo.groups_shift if shifted else geo.groups, o, lse, geo.n_win, n, nH)
         x_mid = torch.empty(M, C, device=dev)

@@ -326,8 +326,11 @@ def wattn_bias_elems(n_pat, nH):
 
 
 def wattn_bias_build(table, index, n, nH, region, n_pat, bias_fwd, bias_bwd):
+    """bias_fwd f32 (lrce_wattn_fwd_grouped) or fp16 (lrce_wattn_qkv_fwd); bias_bwd f32."""
+    if bias_fwd.dtype not in (torch.float32, F16):
+        raise N.NativeError("wattn_bias_build: bias_fwd must be f32 or fp16")
     call("lrce_wattn_bias_build", ptr(table), ptr(index), index.shape[-1], n, nH, ptr(region), n_pat,
-         ptr(bias_fwd), ptr(bias_bwd), stream_of(bias_fwd))
+         ptr(bias_fwd), int(bias_fwd.dtype == F16), ptr(bias_bwd), stream_of(bias_fwd))
 
 
 WATTN_GROUP = 4   # windows per workgroup of lrce_wattn_fwd_grouped
@@ -360,16 +363,17 @@ def wattn_fwd_grouped(qkv, bias_fwd, groups, out, lse, n_win, n, nH):
            flops=4.0 * n * n * 32 * n_win * nH, nbytes=8.0 * n * 32 * n_win * nH, key=(n_win, nH))
 
 
-def wattn_qkv_fwd(x, w_qkv, b_qkv, qscale, bias_fwd, win_pat, qkv, out, lse, n_win, n, nH):
+def wattn_qkv_fwd(x, w_qkv, b_qkv, qscale, bias_fwd, win_pat, qkv, out, lse, n_win, n, nH, win_order=None):
     """Fused QKV projection + window attention forward (csrc/window_fused.hip).  Algorithmic work per
     launch: the QKV GEMM 2 * (n_win n) * C * 3C + attention 4 n^2 d per (window, head); bytes: x read,
     W_qkv read, qkv + out written (bf16)."""
     C = x.shape[-1]
     M = n_win * n
     _chk(x, BF16, "x"); _chk(w_qkv, BF16, "w_qkv"); _chk(qkv, BF16, "qkv"); _chk(out, BF16, "out")
+    _chk(bias_fwd, F16, "bias_fwd")
     _timed("wattn_qkv_fwd", out, lambda: call("lrce_wattn_qkv_fwd", ptr(x), ptr(w_qkv), ptr(b_qkv), float(qscale),
-                                               ptr(bias_fwd), ptr(win_pat), ptr(qkv), ptr(out), ptr(lse), n_win, n, nH,
-                                               stream_of(out)),
+                                               ptr(bias_fwd), ptr(win_pat), ptr(win_order), ptr(qkv), ptr(out),
+                                               ptr(lse), n_win, n, nH, stream_of(out)),
            flops=2.0 * M * C * 3 * C + 4.0 * n * n * 32 * n_win * nH,
            nbytes=2.0 * (M * C + 3 * C * C + M * 3 * C + M * C), key=(n_win, nH))
 
