@@ -116,11 +116,18 @@ def make_step(model, opt, reducer, batch, mode, world):
         return lambda: train_step(model, opt, reducer, batch)
 
     def body(clips, ids, mask, types, labels):
-        opt.zero_grad()
+        opt.zero_grad(overlap=True)      # the gradient clear runs beside the forward
         loss = F.cross_entropy(model(clips, ids, mask, types), labels, ignore_index=-100)
+        opt.grad_ready()
         loss.backward()
         return loss.detach()
-    step = TrainStepGraph(body, opt, reducer, world)
+    tail = None
+    if reducer is not None:
+        # data parallel: split backward — the fusion head's buckets are exchanged while the extractors'
+        # backward graph replays
+        model.split_backward = True
+        tail = model.backward_extractors
+    step = TrainStepGraph(body, opt, reducer, world, tail=tail)
     return lambda: step(*batch)
 
 

@@ -81,7 +81,9 @@ typedef struct LrceGemmDesc {
   const float* a_row_scale;
   int32_t a_rows_per_scale;
   /* b_f32 = 1: B is f32 (then A must be f32): exact-f32 MFMA path (v_mfma_f32_16x16x4_f32) for the
-   * small-M recurrent-decoder linears that read the f32 master weights directly. */
+   * small-M recurrent-decoder linears.  b_f32 = 2: B is IEEE fp16 (the weights' fp16 shadow, as under
+   * the reference's fp16 autocast, agent_oe.py:28), converted exactly to f32 on load, A and the
+   * arithmetic f32: half the weight bytes of the latency-bound decoder GEMVs (skinny path only). */
   int32_t b_f32;
   /* Split-K workspace (optional, f32, >= split_k * m * n elements, batch 1, flags = ATOMIC [+ BIAS_GRAD]
    * with no other epilogue): each K slice stores its partial tile with plain vector stores and a
@@ -182,12 +184,13 @@ int64_t lrce_layernorm_bwd_workspace(int rows, int cols);
  * (relative_position_bias_table) and the int64 relative_position_index (ld = index_ld), with the
  * shift mask of each window pattern given as per-token region ids region[n_pat][n] (-100 between
  * different regions, video_swin_ori.py:346-359); bias_fwd holds the S^T-oriented tiles (forward),
- * bias_bwd the S-oriented ones (backward).  fwd_f16: bias_fwd as IEEE fp16 (what lrce_wattn_qkv_fwd
- * reads; padded keys -30000) instead of f32 (lrce_wattn_fwd_grouped). */
+ * bias_bwd the S-oriented ones (backward).  fwd_f16 / bwd_f16: that set as IEEE fp16 (padded keys
+ * -30000) instead of f32 — lrce_wattn_qkv_fwd reads fp16 forward tiles, lrce_wattn_fwd_grouped f32;
+ * lrce_wattn_bwd either (bias_f16); a layer's forward and backward should use the same precision. */
 int64_t lrce_wattn_bias_elems(int n_pat, int nH);
 int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
-                          const int32_t* region, int n_pat, void* bias_fwd, int fwd_f16, float* bias_bwd,
-                          void* stream);
+                          const int32_t* region, int n_pat, void* bias_fwd, int fwd_f16, void* bias_bwd,
+                          int bwd_f16, void* stream);
 /* Forward with windows grouped by mask pattern, GW = 4 windows per group: win_list int32
  * [n_groups*4] (window ids, -1 = empty slot; NULL = identity 0,1,2,...), grp_pat int32 [n_groups]
  * (the group's mask pattern; NULL = pattern 0).  The bias row of a query tile is staged once per
@@ -212,8 +215,8 @@ int lrce_wattn_qkv_fwd(const uint16_t* x, const uint16_t* w_qkv, const float* b_
  * position, reduced by lrce_wattn_dbias (NULL: no bias-table gradient, e.g. a frozen table). */
 int64_t lrce_wattn_dbias_part_elems(int n_win, int nH, int n_bins);
 int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                   const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv, float* dbias_part, int n_win,
-                   int n, int nH, int wh, int ww, void* stream);
+                   const void* bias_bwd, int bias_f16, const int32_t* win_pat, uint16_t* dqkv, float* dbias_part,
+                   int n_win, int n, int nH, int wh, int ww, void* stream);
 /* Bias-table gradient (relative_position_bias_table, f32 [table_rows][nH], accumulated) from
  * lrce_wattn_bwd's bins: bin_row int32 [n_bins] = the table row of each relative-position bin (the
  * relative_position_index entry of any (query, key) pair in that bin; -1 = unused), built once per stage

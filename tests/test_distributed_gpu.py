@@ -66,7 +66,7 @@ def _worker(rank, world, port, mode, q):
     out = {}
     try:
         from lrce.agent.agent_base import DataParallel
-        gdt = torch.bfloat16 if mode in ("bf16", "graph") else torch.float32
+        gdt = torch.bfloat16 if mode in ("bf16", "graph", "graph_split") else torch.float32
         model = _model(seed=100 + rank)                 # different init per rank: the broadcast must fix it
         dp = DataParallel(model, bucket_mb=32, grad_dtype=gdt)
         flat = dp.reducer.flat
@@ -102,7 +102,11 @@ def _worker(rank, world, port, mode, q):
                 loss = F.cross_entropy(y.float(), g)
                 loss.backward()
                 return loss.detach()
-            step = TrainStepGraph(body, opt, dp.reducer, world)
+            tail = None
+            if mode == "graph_split":   # head backward graph, exchange overlapping the extractors' graph
+                model.split_backward = True
+                tail = model.backward_extractors
+            step = TrainStepGraph(body, opt, dp.reducer, world, tail=tail)
             batch = (clips[half], ids[half], mask[half], types[half], labels[half])
             for _ in range(3):
                 step(*batch)
@@ -112,6 +116,7 @@ def _worker(rank, world, port, mode, q):
             out["before"] = {k: sd0[k].cpu() for k in KEYS}
             if rank == 0:   # single-process reference: same init, full batch, eager steps
                 dist.barrier()
+                model.split_backward = False
                 flat.reducer = None
                 flat.grad_reducer = None
                 model.load_state_dict(sd0)
@@ -177,8 +182,11 @@ def test_dp_gradients_equal_full_batch(mode, tol):
         assert _rel(res[0]["dp"][k], res[0]["ref"][k]) < tol, (k, _rel(res[0]["dp"][k], res[0]["ref"][k]))
 
 
-def test_dp_graph_training_steps_match_single_process():
-    res = _run("graph")
+@pytest.mark.parametrize("mode", ["graph", "graph_split"])
+def test_dp_graph_training_steps_match_single_process(mode):
+    """graph: graph(fwd + bwd) -> exchange -> graph(optimizer); graph_split: the head's backward and
+    the extractors' backward as two graphs with the head's buckets exchanged between them."""
+    res = _run(mode)
     for k in KEYS:
         a0, a1 = res[0]["after"][k], res[1]["after"][k]
         assert torch.equal(a0, a1), k                            # replicas stay identical

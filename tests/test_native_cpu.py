@@ -5,6 +5,7 @@ import os
 import re
 
 import pytest
+import torch
 
 from conftest import REPO
 
@@ -74,3 +75,22 @@ def test_bias_gradient_bins_map_to_relative_position_index():
     bad[0, 1], bad[1, 2] = bad[1, 2], bad[0, 1] + 1
     with pytest.raises(ValueError):
         K.wattn_bin_rows(bad, (3, 7, 7))
+
+
+def test_torch_library_ops_registered_with_fake_shapes():
+    """lrce/ops.py registers torch.ops.lrce.* with schemas and fake (shape-only) implementations;
+    shape propagation runs on meta tensors without a GPU (no compute)."""
+    from lrce import ops
+    for name in ops.registered():
+        assert hasattr(torch.ops.lrce, name), name
+    bf = torch.bfloat16
+    y = torch.ops.lrce.linear(torch.empty(4, 8, device="meta", dtype=bf), torch.empty(6, 8, device="meta", dtype=bf),
+                              None, False, True)
+    assert y.shape == (4, 6) and y.dtype == torch.float32
+    dx = torch.ops.lrce.linear_dx(torch.empty(4, 6, device="meta", dtype=bf), torch.empty(6, 8, device="meta", dtype=bf))
+    assert dx.shape == (4, 8)
+    out, qkv, lse = torch.ops.lrce.window_attention(
+        torch.empty(2 * 147, 256, device="meta", dtype=bf), torch.empty(768, 256, device="meta", dtype=bf),
+        torch.empty(768, device="meta"), torch.empty(2535, 8, device="meta"),
+        torch.empty(392, 392, device="meta", dtype=torch.int64), 2, 8)
+    assert out.shape == (294, 256) and qkv.shape == (294, 768) and lse.shape == (2, 8, 160)

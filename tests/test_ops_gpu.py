@@ -366,8 +366,10 @@ def _wattn_reference(qkv, table, index, region, win_pat, nH, n, c):
     return o.transpose(1, 2).reshape(nw * n, C), (q, kk, v, tab)
 
 
-@pytest.mark.parametrize("nH,n_win", [(4, 9), (16, 5), (32, 2)])
-def test_window_attention_fwd_bwd(nH, n_win):
+@pytest.mark.parametrize("nH,n_win,bias16", [(4, 9, False), (16, 5, False), (32, 2, False), (4, 9, True), (16, 5, True)])
+def test_window_attention_fwd_bwd(nH, n_win, bias16):
+    """bias16: the backward reads fp16 bias tiles (the Swin-B product path, same rounding as the fused
+    forward's); else f32."""
     k = K()
     n, hd = 147, 32
     C = nH * hd
@@ -385,6 +387,9 @@ def test_window_attention_fwd_bwd(nH, n_win):
     bf_ = torch.empty(k.wattn_bias_elems(n_pat, nH), device=dev)
     bb_ = torch.empty_like(bf_)
     k.wattn_bias_build(table, index, n, nH, region, n_pat, bf_, bb_)
+    if bias16:
+        bb_ = torch.empty(bf_.numel(), device=dev, dtype=torch.float16)
+        k.wattn_bias_build(table, index, n, nH, region, n_pat, torch.empty_like(bf_), bb_)
     lse = torch.zeros(n_win, nH, 160, device=dev)
     ref, (q, kk, v, tab) = _wattn_reference(qkv, table, index, region, win_pat, nH, n, c)
     # grouped-by-pattern forward (the product path)
@@ -706,3 +711,41 @@ def test_gemm_ln_prologue_forward_and_backward(M):
         dx2 = torch.empty_like(dx)
         g2 = k.linear_dx(dy, w2, ln=k.ln_bwd_prologue(x, mean, rstd, gam, y_out=dx2, drop=(p, 91, 1)))
         assert torch.equal(g2, g) and torch.equal(dx2, dx)
+
+
+def test_torch_library_ops():
+    """torch.ops.lrce.* (lrce/ops.py): the same kernels through the dispatcher, vs fp32 torch."""
+    K()
+    from lrce import ops  # noqa: F401  (registers the ops)
+    torch.manual_seed(3)
+    x = bf(torch.randn(300, 256, device=dev))
+    w = bf(torch.randn(512, 256, device=dev) / 16)
+    b = torch.randn(512, device=dev)
+    y = torch.ops.lrce.linear(x, w, b, False, True)
+    assert rel(y, x.float() @ w.float().t() + b) < 1e-2
+    yg = torch.ops.lrce.linear(x, w, b, True, False)
+    assert yg.dtype == torch.bfloat16 and rel(yg, F.gelu(x.float() @ w.float().t() + b)) < 2e-2
+    dy = bf(torch.randn(300, 512, device=dev))
+    assert rel(torch.ops.lrce.linear_dx(dy, w), dy.float() @ w.float()) < 1e-2
+    dw = torch.zeros(512, 256, device=dev)
+    torch.ops.lrce.linear_dw_(dw, dy, x)
+    assert rel(dw, dy.float().t() @ x.float()) < 1e-2
+    xf = torch.randn(300, 256, device=dev)
+    g, be = torch.rand(256, device=dev) + 0.5, torch.randn(256, device=dev)
+    yl, mean, rstd = torch.ops.lrce.layer_norm(xf, g, be, 1e-5)
+    assert rel(yl, F.layer_norm(xf, (256,), g, be, 1e-5)) < 1e-5 and mean.shape == (300,)
+    # fused window attention vs the fp32 reference on the same bf16 qkv
+    nH, n_win, n = 8, 3, 147
+    C = nH * 32
+    c = 32 ** -0.5 * math.log2(math.e)
+    xw = bf(torch.randn(n_win * n, C, device=dev))
+    wq = bf(torch.randn(3 * C, C, device=dev) / math.sqrt(C))
+    bq = torch.randn(3 * C, device=dev) * 0.1
+    table = torch.randn(2535, nH, device=dev) * 0.1
+    index = O.relative_position_index((8, 7, 7)).to(dev)
+    region = torch.zeros(2, n, dtype=torch.int32, device=dev)
+    region[1, 70:] = 1
+    win_pat = torch.tensor([1, 0, 1], dtype=torch.int32, device=dev)
+    out, qkv, lse = torch.ops.lrce.window_attention(xw, wq, bq, table, index, n_win, nH, region, win_pat)
+    ref, _ = _wattn_reference(qkv, table, index, region, win_pat, nH, n, c)
+    assert rel(out, ref) < 2e-2 and lse.shape == (n_win, nH, 160)

@@ -62,6 +62,27 @@ def main():
     res.append(("dropout 10x768", graph_time(lambda: K.dropout(y, 0.1, 5, out=y))))
     ln_w, ln_b = torch.ones(E, device=dev), torch.zeros(E, device=dev)
     res.append(("layernorm 10x768", graph_time(lambda: K.layernorm(y, ln_w, ln_b, 1e-12, out_f32=True))))
+    # rotating weights (36 distinct copies, as the 12 layers x 3 steps of one decoder pass): cold in L2
+    nrot = 36
+    ws32 = [torch.randn(E, E, device=dev) * 0.02 for _ in range(nrot)]
+    ws16 = [t.half() for t in ws32]
+    w1s16 = [(torch.randn(FF, E, device=dev) * 0.02).half() for _ in range(nrot)]
+    ctr = [0]
+
+    def rot(ws, fn):
+        def f():
+            ctr[0] = (ctr[0] + 1) % nrot
+            fn(ws[ctr[0]])
+        return f
+    res.append(("rot skinny fwd 768x768 f32 W", graph_time(rot(ws32, lambda wt: K.linear(x, wt, b, out=y, out_f32=True)), reps=36)))
+    res.append(("rot skinny fwd 768x768 fp16 W", graph_time(rot(ws16, lambda wt: K.linear(x, wt, b, out=y, out_f32=True)), reps=36)))
+    res.append(("L2 skinny fwd 768x768 fp16 W", graph_time(lambda: K.linear(x, ws16[0], b, out=y, out_f32=True))))
+    res.append(("rot skinny fwd 3072x768 fp16 W gelu", graph_time(rot(w1s16, lambda wt: K.linear(x, wt, b1, out=g, gelu=True, pre_out=pre, out_f32=True)), reps=36)))
+    pro_m, pro_r = torch.empty(B, device=dev), torch.empty(B, device=dev)
+    yo = torch.empty(B, E, device=dev)
+    res.append(("rot skinny_ln fwd 768x768 fp16 W", graph_time(rot(ws16, lambda wt: K.linear(
+        x, wt, b, out=y, out_f32=True, ln=K.ln_fwd_prologue(ln_w, ln_b, 1e-12, mean=pro_m, rstd=pro_r, y_out=yo))), reps=36)))
+    res.append(("empty-ish: dropout p=0 10x768", graph_time(lambda: K.dropout(y, 0.0, 5, out=y))))
     for name, us in res:
         print(f"{name:32s} {us:7.2f} us/launch", flush=True)
 

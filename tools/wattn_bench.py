@@ -48,7 +48,8 @@ def main():
         bf_, bb_ = torch.empty(be, device=dev), torch.empty(be, device=dev)
         K.wattn_bias_build(table, idx, n, nH, region, n_pat, bf_, bb_)
         bfh = torch.empty(be, device=dev, dtype=torch.float16)
-        K.wattn_bias_build(table, idx, n, nH, region, n_pat, bfh, bb_)
+        bbh = torch.empty(be, device=dev, dtype=torch.float16)
+        K.wattn_bias_build(table, idx, n, nH, region, n_pat, bfh, bbh)   # the product's fp16 tiles
         order = torch.argsort(win_pat.long(), stable=True).int()
         out = torch.empty(n_win * n, C, device=dev, dtype=torch.bfloat16)
         lse = torch.empty(n_win * nH * 160, device=dev)
@@ -67,9 +68,11 @@ def main():
         print(f"win {n_win:5d} heads {nH:3d}: fused qkv+attn {tq * 1e3:7.1f} us {fq / tq / 1e9:6.1f} TF/s   "
               f"(unfused: qkv GEMM {tg * 1e3:6.1f} us + attn {tf * 1e3:6.1f} us)", flush=True)
         tb = 1e-9 if os.environ.get("WATTN_FWD_ONLY") else \
-            timeit(lambda: K.wattn_bwd(qkv, out, dout, lse, bb_, win_pat, dqkv, dbp, n_win, n, nH, win))
+            timeit(lambda: K.wattn_bwd(qkv, out, dout, lse, bbh, win_pat, dqkv, dbp, n_win, n, nH, win))
         if os.environ.get("WATTN_NOBINS"):
-            tnb = timeit(lambda: K.wattn_bwd(qkv, out, dout, lse, bb_, win_pat, dqkv, None, n_win, n, nH, win))
+            tnb = timeit(lambda: K.wattn_bwd(qkv, out, dout, lse, bbh, win_pat, dqkv, None, n_win, n, nH, win))
+            tf32 = timeit(lambda: K.wattn_bwd(qkv, out, dout, lse, bb_, win_pat, dqkv, dbp, n_win, n, nH, win))
+            print(f"  bwd with f32 bias tiles {tf32 * 1e3:7.1f} us", flush=True)
             print(f"  bwd without the bias-gradient bins {tnb * 1e3:7.1f} us", flush=True)
         ff, fb = 4.0 * n * n * hd * n_win * nH, 8.0 * n * n * hd * n_win * nH
         tot_f += tf; tot_b += tb; fl_f += ff; fl_b += fb

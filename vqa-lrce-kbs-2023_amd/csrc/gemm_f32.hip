@@ -146,7 +146,7 @@ constexpr int SK_NT = 256;
 
 struct SkinnyP {
   const float* a;
-  const float* b;
+  const void* b;        // f32, or IEEE fp16 (BH: the decoder's fp16 weight shadow, f32 compute)
   void* c;
   long long lda, ldb, ldc;
   int m, n, k;
@@ -174,6 +174,31 @@ struct SkinnyP {
 struct SkPre {
   float bias, dg, res, acc;
 };
+
+// four consecutive-k elements of B(n, k..k+3) as f32: B_KM -> B[n][k..k+3] (one 16-B f32 / 8-B fp16
+// load), else B[k..k+3][n] (strided); BH: B holds IEEE fp16 (converted exactly to f32)
+template <bool B_KM, bool BH>
+__device__ __forceinline__ float4 ld_b4(const void* b, long long ldb, int n, int k) {
+  if constexpr (BH) {
+    const f16* bp = static_cast<const f16*>(b);
+    if constexpr (B_KM) {
+      const uint2 u = *reinterpret_cast<const uint2*>(bp + (long long)n * ldb + k);
+      const auto lo = [](unsigned x) { return (float)__builtin_bit_cast(f16, (unsigned short)(x & 0xFFFFu)); };
+      const auto hi = [](unsigned x) { return (float)__builtin_bit_cast(f16, (unsigned short)(x >> 16)); };
+      return make_float4(lo(u.x), hi(u.x), lo(u.y), hi(u.y));
+    } else {
+      const f16* q = bp + (long long)k * ldb + n;
+      return make_float4((float)q[0], (float)q[ldb], (float)q[2 * ldb], (float)q[3 * ldb]);
+    }
+  } else {
+    const float* bp = static_cast<const float*>(b);
+    if constexpr (B_KM) return *reinterpret_cast<const float4*>(bp + (long long)n * ldb + k);
+    else {
+      const float* q = bp + (long long)k * ldb + n;
+      return make_float4(q[0], q[ldb], q[2 * ldb], q[3 * ldb]);
+    }
+  }
+}
 
 __device__ __forceinline__ SkPre sk_prefetch(const SkinnyP& p, int m, int n) {
   SkPre e{0.f, 1.f, 0.f, 0.f};
@@ -222,7 +247,7 @@ __device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, in
 // the epilogue — so nonlinear epilogues (GELU, dGELU, residual) still see the full sum, and the
 // result does not depend on arrival order.  Narrow-N decoder linears (N = 768 -> 48 tiles) get
 // 3-4x the workgroups, deep ones (K = 3072) a quarter of the reduction per workgroup.
-template <int MT, bool B_KM, int SK_WAVES>
+template <int MT, bool B_KM, int SK_WAVES, bool BH>
 __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p, float* __restrict__ part,
                                                                unsigned* __restrict__ counters, int kspan) {
   constexpr int TS = MT <= 2 ? 8 : 4;
@@ -255,12 +280,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_kernel(SkinnyP p, float*
       const int kk = k + 16 * u + 4 * grp;
       const bool k_ok = kk < ke;           // k % 4 == 0: a float4 is all in or all out
       const int kc = k_ok ? kk : 0;
-      if (B_KM) {
-        bv[u] = *reinterpret_cast<const float4*>(p.b + (long long)nc * p.ldb + kc);
-      } else {
-        const float* bp = p.b + (long long)kc * p.ldb + nc;
-        bv[u] = make_float4(bp[0], bp[p.ldb], bp[2 * p.ldb], bp[3 * p.ldb]);
-      }
+      bv[u] = ld_b4<B_KM, BH>(p.b, p.ldb, nc, kc);
       if (!(k_ok && n_ok)) bv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
@@ -354,7 +374,7 @@ __global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   float asum = 0.f;
   const float* ap = p.a + m;
-  const float* bp = p.b + n;
+  const float* bp = static_cast<const float*>(p.b) + n;
   int r = 0;
   for (; r + U <= p.k; r += U) {
     float av[U];
@@ -420,7 +440,7 @@ struct LnP {
 
 constexpr int LN_W = 8, LN_US = 8;
 
-template <int MT, bool B_KM, int PRO>
+template <int MT, bool B_KM, int PRO, bool BH>
 __global__ void __launch_bounds__(LN_W * 64) skinny_ln_kernel(SkinnyP p, LnP q) {
   __shared__ float red[LN_W][MT][16][17];
   __shared__ float rsum[2][LN_W][MT * 16];
@@ -446,12 +466,7 @@ __global__ void __launch_bounds__(LN_W * 64) skinny_ln_kernel(SkinnyP p, LnP q) 
   for (int u = 0; u < LN_US; ++u) {
     if (u >= nu) break;
     const int k = kb + 16 * u + 4 * grp;
-    if (B_KM) {
-      bv[u] = *reinterpret_cast<const float4*>(p.b + (long long)nc * p.ldb + k);
-    } else {
-      const float* bp = p.b + (long long)k * p.ldb + nc;
-      bv[u] = make_float4(bp[0], bp[p.ldb], bp[2 * p.ldb], bp[3 * p.ldb]);
-    }
+    bv[u] = ld_b4<B_KM, BH>(p.b, p.ldb, nc, k);
     if (!n_ok) bv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     gv[u] = *reinterpret_cast<const float4*>(q.gamma + k);
     if (PRO == 1) ev[u] = *reinterpret_cast<const float4*>(q.beta + k);
@@ -712,7 +727,7 @@ SkinnySplitWs* skinny_split_ws(hipStream_t st, int tiles, int ks, int mt) {
 
 // the dW shape the outer-product kernel takes: A M-major, B N-major, reduction <= 256 rows
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d) {
-  return d->b_f32 && d->a_f32 && !d->a_kmajor && !d->b_kmajor && d->k <= 256 && (d->n % 4) == 0 && (d->ldc % 4) == 0 &&
+  return d->b_f32 == 1 && d->a_f32 && !d->a_kmajor && !d->b_kmajor && d->k <= 256 && (d->n % 4) == 0 && (d->ldc % 4) == 0 &&
          (d->ldb % 4) == 0 && d->batch == 1 && !d->a_map && !d->c_map && !d->a_row_scale && d->split_k <= 1 &&
          (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32 | LRCE_EPI_BIAS_GRAD)) == 0 &&
          (d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32)) && !d->row_scale && d->scale_cols == 0 &&
@@ -722,6 +737,7 @@ bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d) {
 int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
   if (!d->a_f32) return lrce_fail(LRCE_E_ARG, "gemm(f32 B): A must be f32 too");
   if (d->batch != 1) return lrce_fail(LRCE_E_ARG, "gemm(f32 B): batch must be 1");
+  const bool bh = d->b_f32 == 2;   // fp16 B (weights), f32 A and compute: skinny path only
   if (d->a_kmajor ? (d->k % 4) : (d->m % 4)) return lrce_fail(LRCE_E_ARG, "gemm(f32): A contiguous dim %% 4 != 0");
   if (d->b_kmajor ? (d->k % 4) : (d->n % 4)) return lrce_fail(LRCE_E_ARG, "gemm(f32): B contiguous dim %% 4 != 0");
   if ((d->lda % 4) || (d->ldb % 4)) return lrce_fail(LRCE_E_ARG, "gemm(f32): lda/ldb %% 4 != 0");
@@ -729,7 +745,7 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (plain) {
     SkinnyP q;
-    q.a = static_cast<const float*>(d->a); q.b = static_cast<const float*>(d->b); q.c = d->c;
+    q.a = static_cast<const float*>(d->a); q.b = d->b; q.c = d->c;
     q.lda = d->lda; q.ldb = d->ldb; q.ldc = d->ldc;
     q.m = d->m; q.n = d->n; q.k = d->k; q.flags = d->flags; q.bias = d->bias;
     q.aux = d->aux; q.ld_aux = d->ld_aux; q.aux_out = static_cast<bf16*>(d->aux_out); q.ld_aux_out = d->ld_aux_out;
@@ -738,7 +754,7 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
     q.bias_grad = const_cast<float*>(d->bias);
     q.drop_p = d->drop_p; q.drop_group = d->drop_group > 0 ? d->drop_group : 1; q.drop_seed = d->drop_seed;
     q.rng_off = lrce_rng_offset();
-    const bool outer_ok = lrce_gemm_f32_outer_ok(d) && d->drop_p <= 0.f;
+    const bool outer_ok = !bh && lrce_gemm_f32_outer_ok(d) && d->drop_p <= 0.f;
     if (outer_ok) {
       const long long work = (long long)d->m * (d->n / 4);
       outer_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(q);
@@ -746,7 +762,7 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
     }
     if (d->flags & LRCE_EPI_BIAS_GRAD) return lrce_fail(LRCE_E_ARG, "gemm(f32): internal: bias grad on a fused path");
     if (d->a_kmajor && d->m <= 64 && (reinterpret_cast<uintptr_t>(d->a) & 15) == 0 &&
-        (!d->b_kmajor || (reinterpret_cast<uintptr_t>(d->b) & 15) == 0)) {
+        (!d->b_kmajor || (reinterpret_cast<uintptr_t>(d->b) & (bh ? 7 : 15)) == 0)) {
       const int mt = (d->m + 15) / 16;
       const int tiles = (d->n + 15) / 16;
       // split K for deep reductions (K >= 2048: the decoder FFN linear2 / linear1-dX) while the grid is under
@@ -763,9 +779,14 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
       dim3 grid(tiles, ks);
       float* part = ws ? ws->part : nullptr;
       unsigned* ctr = ws ? ws->counters : nullptr;
-#define LRCE_SK(MT)                                                                                   \
-  if (d->b_kmajor) skinny_kernel<MT, true, 8><<<grid, 8 * 64, 0, st>>>(q, part, ctr, kspan);          \
-  else skinny_kernel<MT, false, 8><<<grid, 8 * 64, 0, st>>>(q, part, ctr, kspan);
+#define LRCE_SK(MT)                                                                                       \
+  if (bh) {                                                                                               \
+    if (d->b_kmajor) skinny_kernel<MT, true, 8, true><<<grid, 8 * 64, 0, st>>>(q, part, ctr, kspan);      \
+    else skinny_kernel<MT, false, 8, true><<<grid, 8 * 64, 0, st>>>(q, part, ctr, kspan);                 \
+  } else {                                                                                                \
+    if (d->b_kmajor) skinny_kernel<MT, true, 8, false><<<grid, 8 * 64, 0, st>>>(q, part, ctr, kspan);     \
+    else skinny_kernel<MT, false, 8, false><<<grid, 8 * 64, 0, st>>>(q, part, ctr, kspan);                \
+  }
       switch (mt) {
         case 1: LRCE_SK(1) break;
         case 2: LRCE_SK(2) break;
@@ -777,6 +798,7 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
     }
   }
   if (d->drop_p > 0.f) return lrce_fail(LRCE_E_ARG, "gemm(f32): fused dropout needs the skinny path (K-major A, M <= 64)");
+  if (bh) return lrce_fail(LRCE_E_ARG, "gemm(f32): fp16 B needs the skinny path (K-major 16-B aligned A, M <= 64)");
   GemmF32P p;
   p.a = static_cast<const float*>(d->a); p.b = static_cast<const float*>(d->b); p.c = d->c;
   p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc;
@@ -803,13 +825,15 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
 int lrce_gemm_ln(const LrceGemmDesc* d, const LrceLnPrologue* pro, void* stream) {
   if (!d || !pro) return lrce_fail(LRCE_E_ARG, "gemm_ln: null descriptor");
   if (pro->mode != 1 && pro->mode != 2) return lrce_fail(LRCE_E_ARG, "gemm_ln: mode %d", pro->mode);
+  const bool bh = d->b_f32 == 2;
   if (!d->b_f32 || !d->a_f32 || !d->a_kmajor || d->batch != 1 || d->a_map || d->c_map || d->a_row_scale ||
       d->split_k > 1 || d->row_scale || (d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)))
     return lrce_fail(LRCE_E_ARG, "gemm_ln: f32 K-major A, f32 B, no maps / split / atomics");
   if (d->m < 1 || d->m > 64) return lrce_fail(LRCE_E_ARG, "gemm_ln: m=%d outside [1, 64]", d->m);
   if (d->k % (LN_W * 16) || d->k > LN_W * 16 * LN_US) return lrce_fail(LRCE_E_ARG, "gemm_ln: k=%d (multiple of 128, <= 1024)", d->k);
-  if ((d->lda % 4) || (d->ldb % 4) || (reinterpret_cast<uintptr_t>(d->a) & 15) || (reinterpret_cast<uintptr_t>(d->b) & 15))
-    return lrce_fail(LRCE_E_ARG, "gemm_ln: A / B need 16-B alignment");
+  if ((d->lda % 4) || (d->ldb % 4) || (reinterpret_cast<uintptr_t>(d->a) & 15) ||
+      (reinterpret_cast<uintptr_t>(d->b) & (bh ? 7 : 15)))
+    return lrce_fail(LRCE_E_ARG, "gemm_ln: A / B need 16-B (fp16 B: 8-B) alignment");
   if (!pro->gamma || (pro->mode == 1 && !pro->beta)) return lrce_fail(LRCE_E_ARG, "gemm_ln: gamma / beta");
   if (pro->mode == 2 && (!pro->x || !pro->mean || !pro->rstd || (pro->ld_x % 4) || (!pro->dgamma != !pro->dbeta)))
     return lrce_fail(LRCE_E_ARG, "gemm_ln: backward needs x (ld %% 4 == 0), mean, rstd; dgamma with dbeta");
@@ -817,7 +841,7 @@ int lrce_gemm_ln(const LrceGemmDesc* d, const LrceLnPrologue* pro, void* stream)
     return lrce_fail(LRCE_E_ARG, "gemm_ln: materialised outputs need ld %% 4 == 0");
   const int tiles = (d->n + 15) / 16;
   SkinnyP q;
-  q.a = static_cast<const float*>(d->a); q.b = static_cast<const float*>(d->b); q.c = d->c;
+  q.a = static_cast<const float*>(d->a); q.b = d->b; q.c = d->c;
   q.lda = d->lda; q.ldb = d->ldb; q.ldc = d->ldc;
   q.m = d->m; q.n = d->n; q.k = d->k; q.flags = d->flags; q.bias = d->bias;
   q.aux = d->aux; q.ld_aux = d->ld_aux; q.aux_out = static_cast<bf16*>(d->aux_out); q.ld_aux_out = d->ld_aux_out;
@@ -833,8 +857,13 @@ int lrce_gemm_ln(const LrceGemmDesc* d, const LrceLnPrologue* pro, void* stream)
   const int mt = (d->m + 15) / 16;
   hipStream_t st = static_cast<hipStream_t>(stream);
 #define LRCE_SKLN(MT, PRO)                                                                         \
-  if (d->b_kmajor) skinny_ln_kernel<MT, true, PRO><<<tiles, LN_W * 64, 0, st>>>(q, l);             \
-  else skinny_ln_kernel<MT, false, PRO><<<tiles, LN_W * 64, 0, st>>>(q, l);
+  if (bh) {                                                                                        \
+    if (d->b_kmajor) skinny_ln_kernel<MT, true, PRO, true><<<tiles, LN_W * 64, 0, st>>>(q, l);     \
+    else skinny_ln_kernel<MT, false, PRO, true><<<tiles, LN_W * 64, 0, st>>>(q, l);                \
+  } else {                                                                                         \
+    if (d->b_kmajor) skinny_ln_kernel<MT, true, PRO, false><<<tiles, LN_W * 64, 0, st>>>(q, l);    \
+    else skinny_ln_kernel<MT, false, PRO, false><<<tiles, LN_W * 64, 0, st>>>(q, l);               \
+  }
 #define LRCE_SKLN_MT(PRO)                    \
   switch (mt) {                              \
     case 1: LRCE_SKLN(1, PRO) break;         \

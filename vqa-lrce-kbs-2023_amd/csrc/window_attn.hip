@@ -78,10 +78,12 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int s) {
 }
 
 // ------------------------------------------------------------------------------ bias tiles
-// forward tiles f32 (bf) or fp16 (bfh, the fused QKV + attention forward: half the bytes; padded keys
-// at -30000, still exp2 -> 0), backward tiles f32 (bb)
+// forward tiles f32 (bf) or fp16 (bfh: the fused QKV + attention forward), backward tiles f32 (bb) or
+// fp16 (bbh) — fp16 halves the bytes every (window, head) reads; padded keys at -30000 (exp2 -> 0 all
+// the same).  The forward and backward of one layer use the same rounding, so the probabilities the
+// backward recomputes are the forward's.
 __global__ void bias_build_kernel(const float* table, const int64_t* index, int ld, int n, int nH,
-                                  const int* region, int n_pat, float* bf, f16* bfh, float* bb) {
+                                  const int* region, int n_pat, float* bf, f16* bfh, float* bb, f16* bbh) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long total = (long long)n_pat * nH * PH_ELEMS;
   if (e >= total) return;
@@ -106,7 +108,9 @@ __global__ void bias_build_kernel(const float* table, const int64_t* index, int 
   else bf[e] = vf;
   const int hh = lane >> 5, col = lane & 31;
   // backward: S tile (rows = queries, cols = keys)
-  bb[e] = val(qt * TQ + crow(reg, hh), kt * TQ + col);
+  const float vb = val(qt * TQ + crow(reg, hh), kt * TQ + col);
+  if (bbh) bbh[e] = f2h(vb < -30000.f ? -30000.f : vb);
+  else bb[e] = vb;
 }
 
 // K rows XOR-swizzled by 16-B chunk (conflict-free row reads of the grouped forward's Q tiles)
@@ -333,9 +337,10 @@ struct BwdLds {
   float4 qinfo[NPAD];   // per query: lse, delta, token code (as bits), -
 };
 
+template <bool BH>
 __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
                                                               const bf16* __restrict__ dout, const float* __restrict__ lse_g,
-                                                              const float* __restrict__ biasb, const int* __restrict__ win_pat,
+                                                              const void* __restrict__ biasb, const int* __restrict__ win_pat,
                                                               bf16* __restrict__ dqkv, float* __restrict__ dbias_part, int n_win,
                                                               int n, int nH, int wh, int ww, int nb, int boff, float qscale) {
   __shared__ __attribute__((aligned(16))) BwdLds L;
@@ -397,7 +402,7 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
 #pragma unroll
   for (int s = 0; s < 2; ++s) kf[s] = *reinterpret_cast<const bf16x8*>(L.k + key * HD + 16 * s + 8 * hh);
   const int pat = win_pat ? win_pat[w] : 0;
-  const float* bp = biasb + (long long)(pat * nH + h) * PH_ELEMS + lane * 16;
+  const long long bofs = (long long)(pat * nH + h) * PH_ELEMS + lane * 16;   // this lane's 16 values per tile
   const bool key_live = key < n;
   const int kbin = boff - (key_live ? __float_as_int(L.qinfo[key].z) : 0);
   const bool want_bins = dbias_part != nullptr;
@@ -405,8 +410,20 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
   for (int s = 0; s < NTILE; ++s) {
     const int qt = t + s < NTILE ? t + s : t + s - NTILE;
     f32x16 sacc;
-    {
-      const float4* src = reinterpret_cast<const float4*>(bp + (qt * NTILE + t) * TILE_ELEMS);
+    if constexpr (BH) {
+      const uint4* src = reinterpret_cast<const uint4*>(static_cast<const f16*>(biasb) + bofs + (qt * NTILE + t) * TILE_ELEMS);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint4 b = src[u];
+        const unsigned w4[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sacc[8 * u + 2 * e] = (float)__builtin_bit_cast(f16, (unsigned short)(w4[e] & 0xFFFFu));
+          sacc[8 * u + 2 * e + 1] = (float)__builtin_bit_cast(f16, (unsigned short)(w4[e] >> 16));
+        }
+      }
+    } else {
+      const float4* src = reinterpret_cast<const float4*>(static_cast<const float*>(biasb) + bofs + (qt * NTILE + t) * TILE_ELEMS);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const float4 b = src[u];
@@ -538,14 +555,15 @@ extern "C" int64_t lrce_wattn_dbias_part_elems(int n_win, int nH, int n_bins) {
 }
 
 extern "C" int lrce_wattn_bias_build(const float* table, const int64_t* index, int index_ld, int n, int nH,
-                                     const int32_t* region, int n_pat, void* bias_fwd, int fwd_f16, float* bias_bwd,
-                                     void* stream) {
+                                     const int32_t* region, int n_pat, void* bias_fwd, int fwd_f16, void* bias_bwd,
+                                     int bwd_f16, void* stream) {
   if (!table || !index || !bias_fwd || !bias_bwd) return lrce_fail(LRCE_E_ARG, "wattn_bias_build: null pointer");
   if (n <= 0 || n > NPAD || n_pat < 1 || nH < 1) return lrce_fail(LRCE_E_ARG, "wattn_bias_build: n=%d", n);
   const long long total = (long long)n_pat * nH * PH_ELEMS;
   bias_build_kernel<<<(total + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(
       table, index, index_ld, n, nH, region, n_pat, fwd_f16 ? nullptr : static_cast<float*>(bias_fwd),
-      fwd_f16 ? static_cast<f16*>(bias_fwd) : nullptr, bias_bwd);
+      fwd_f16 ? static_cast<f16*>(bias_fwd) : nullptr, bwd_f16 ? nullptr : static_cast<float*>(bias_bwd),
+      bwd_f16 ? static_cast<f16*>(bias_bwd) : nullptr);
   return lrce_check_launch("wattn_bias_build");
 }
 
@@ -562,8 +580,8 @@ extern "C" int lrce_wattn_fwd_grouped(const uint16_t* qkv, const float* bias_fwd
 }
 
 extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                              const float* bias_bwd, const int32_t* win_pat, uint16_t* dqkv, float* dbias_part, int n_win,
-                              int n, int nH, int wh, int ww, void* stream) {
+                              const void* bias_bwd, int bias_f16, const int32_t* win_pat, uint16_t* dqkv, float* dbias_part,
+                              int n_win, int n, int nH, int wh, int ww, void* stream) {
   if (!qkv || !out || !dout || !lse || !bias_bwd || !dqkv) return lrce_fail(LRCE_E_ARG, "wattn_bwd: null pointer");
   if (n <= 4 * TQ || n > NPAD) return lrce_fail(LRCE_E_ARG, "wattn_bwd: n=%d outside (128,160]", n);
   if (wh < 1 || ww < 1 || n % (wh * ww)) return lrce_fail(LRCE_E_ARG, "wattn_bwd: n=%d is not a wd x %d x %d window", n, wh, ww);
@@ -572,7 +590,7 @@ extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const ui
   if (nb > NBMAX) return lrce_fail(LRCE_E_ARG, "wattn_bwd: %d relative-position bins > %d", nb, NBMAX);
   if (n_win <= 0) return LRCE_OK;
   const int boff = ((wd - 1) * (2 * wh - 1) + (wh - 1)) * (2 * ww - 1) + (ww - 1);
-  wattn_bwd_kernel<<<(unsigned)(n_win * nH), BW * 64, 0, static_cast<hipStream_t>(stream)>>>(
+  (bias_f16 ? wattn_bwd_kernel<true> : wattn_bwd_kernel<false>)<<<(unsigned)(n_win * nH), BW * 64, 0, static_cast<hipStream_t>(stream)>>>(
       reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const bf16*>(out), reinterpret_cast<const bf16*>(dout), lse, bias_bwd,
       win_pat, reinterpret_cast<bf16*>(dqkv), dbias_part, n_win, n, nH, wh, ww, nb, boff, 1.0f / sqrtf((float)HD));
   return lrce_check_launch("wattn_bwd");

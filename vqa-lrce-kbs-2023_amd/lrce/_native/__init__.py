@@ -98,10 +98,10 @@ _SIGS = {
     "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _I64,
                            _P],
     "lrce_scale_cast_bf16": [_P, _I64, _I, _P, _I, _P, _P],
-    "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P],
+    "lrce_wattn_bias_build": [_P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _I, _P],
     "lrce_wattn_fwd_grouped": [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_qkv_fwd": [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
-    "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lrce_wattn_dbias": [_P, _I, _I, _I, _P, _P, _P],
     "lrce_mha_fwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_mha_bwd": [ctypes.POINTER(MhaDesc), _P],
@@ -154,6 +154,11 @@ def stream_of(t):
 
 
 def call(name, *args):
-    rc = getattr(lib(), name)(*args)
+    if torch._C._autograd._profiler_enabled():
+        # visible in torch.profiler traces as lrce::<entry point> (the launch itself is async)
+        with torch.profiler.record_function("lrce::" + name[5:]):
+            rc = getattr(lib(), name)(*args)
+    else:
+        rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise NativeError(f"{name} failed ({rc}): {lib().lrce_last_error().decode()}")

@@ -189,11 +189,12 @@ class AgentBase:
     def _train_body(self, video_clips, texts, texts_attention_mask, texts_type_ids, gt):
         """Forward, task loss, L2 value of the current weights, backward (no optimizer step): the
         part of agent_oe.py:27-40 a HIP graph captures.  Returns device tensors."""
-        self.optim.zero_grad()
+        self.optim.zero_grad(overlap=True)   # the gradient clear runs beside the forward
         out = self.model(video_clips, texts, texts_attention_mask, texts_type_ids)
         terms = self.task_loss(out.float(), gt)
         task = terms.mean() if terms.dim() else terms
         l2 = self.calculate_l2_reg() if self.reg_strength != 0.0 else None
+        self.optim.grad_ready()
         task.backward()
         return out.detach(), terms.detach(), task.detach(), l2
 
@@ -208,7 +209,14 @@ class AgentBase:
             if self.use_graph:
                 if self._graph is None:
                     red = self.model.reducer
-                    self._graph = TrainStepGraph(self._train_body, self.optim, red, red.world if red else 1)
+                    tail = None
+                    mod = self.model.module
+                    if red is not None and hasattr(mod, "backward_extractors"):
+                        # data parallel: the head's gradient buckets are exchanged while the
+                        # extractors' backward replays (TrainStepGraph tail)
+                        mod.split_backward = True
+                        tail = mod.backward_extractors
+                    self._graph = TrainStepGraph(self._train_body, self.optim, red, red.world if red else 1, tail=tail)
                 out, terms, task, l2 = self._graph(*inputs)
                 gt = self._graph.static[4]
             else:

@@ -14,12 +14,14 @@ GPU, same model replica, rank-strided batches, gradients averaged every step.  D
   the fused AdamW kernel then reads the bf16 sum directly.  The three steps of a bucket run on a
   communication stream, so the backward on the compute stream never waits for them;
 * HIP-graph mode: when the backward is captured into a graph, a finished bucket's bf16 cast is
-  captured with it and the bucket is remembered in completion order; after each replay
-  `replay_allreduce()` issues the bucket all-reduces in that order, asynchronously on RCCL's stream,
-  and the optimizer graph waits for them.  (Overlapping them with the replayed backward needs an
-  event recorded inside the graph; torch on ROCm refuses external events — "External events are
-  disallowed in rocm", measured on the MI355X box — so in graph mode the exchange follows the
-  backward; eager mode overlaps.);
+  captured with it and the bucket is remembered in completion order; after a replay `exchange()`
+  issues those buckets' exchanges in that order on the comm stream and the optimizer graph waits
+  for them (join()).  torch on ROCm refuses events recorded inside a graph for use outside it
+  ("External events are disallowed in rocm", measured on the MI355X box), so the overlap with the
+  backward comes from splitting it: TrainStepGraph(tail=model.backward_extractors) captures the
+  fusion head's backward and the extractors' backward as two graphs, and the head's buckets (the
+  decoder + heads: 115 M of the 312 M parameters) are exchanged while the second graph replays;
+  eager mode overlaps every bucket;
 * no per-forward buffer broadcast (DDP's broadcast_buffers): the only buffers are constant index
   tables;
 * the 1/world average is folded into the optimizer kernel's grad_scale (no extra pass).
@@ -192,6 +194,24 @@ class GradReducer:
         self.capturing = False
         self.begin()
 
+    def capture_mark(self):
+        """Number of buckets whose completion (bf16 cast) has been captured so far: the split point
+        between two captured backward segments (TrainStepGraph with a tail)."""
+        return len(self.captured)
+
+    def exchange(self, order):
+        """Replay mode: start the exchange of `order`'s buckets (identical on every rank), after the
+        current stream's work so far; asynchronous w.r.t. it until join()."""
+        if self.world > 1:
+            for bi in order:
+                self._exchange(bi)
+
+    def join(self):
+        """The current stream waits for every exchange started so far.  Returns the grad_scale."""
+        if self.world > 1:
+            self._join()
+        return 1.0 / self.world
+
     def replay_allreduce(self, order=None):
         """After replaying the captured backward: one async all-reduce per bucket in capture order
         (identical on every rank), then the current stream waits for all of them (the optimizer
@@ -199,12 +219,8 @@ class GradReducer:
         order = self.captured if order is None else order
         if order is None:
             raise RuntimeError("replay_allreduce: no captured backward")
-        if self.world > 1:
-            self.handles = []
-            for bi in order:
-                self._exchange(bi)
-            self._join()
-        return 1.0 / self.world
+        self.exchange(order)
+        return self.join()
 
 
 def broadcast_parameters(flat, src=0, group=None):

@@ -364,7 +364,7 @@ class _SwinBlockFn(torch.autograd.Function):
         dev = x.device
         fused = nH % 2 == 0
         bias_f = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev, dtype=torch.float16 if fused else torch.float32)
-        bias_b = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev)
+        bias_b = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev, dtype=torch.float16 if fused else torch.float32)
         K.wattn_bias_build(at.relative_position_bias_table, at.relative_position_index, n, nH, region, n_pat,
                            bias_f, bias_b)
         Mw = geo.M_win   # window-order rows (incl. the padded positions of a partial window)

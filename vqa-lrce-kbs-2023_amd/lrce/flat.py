@@ -74,6 +74,13 @@ class FlatParams:
     def f16_src(self):
         return self.f32[self.f16_lo:self.f16_hi]
 
+    def has_f16(self, p):
+        """Does the fp16 shadow cover p?"""
+        if self.f16 is None or id(p) not in self._index:
+            return False
+        off = self.offsets[self._index[id(p)]]
+        return self.f16_lo <= off and off + p.numel() <= self.f16_hi
+
     def w16h(self, p):
         """fp16 shadow of p (enable_f16 must cover it)."""
         i = self._index[id(p)]

@@ -33,11 +33,11 @@ class CapturedStep:
 
 
 class _Captured:
-    __slots__ = ("static", "out", "g_step", "g_opt", "warm", "order", "stage", "turn", "free")
+    __slots__ = ("static", "out", "g_step", "g_tail", "g_opt", "warm", "order", "order_tail", "stage", "turn", "free")
 
     def __init__(self, inputs, device):
         self.static = [torch.empty_like(t, device=device) for t in inputs]
-        self.out = self.g_step = self.g_opt = self.order = None
+        self.out = self.g_step = self.g_tail = self.g_opt = self.order = self.order_tail = None
         self.warm = False
         # two device staging sets for host batches: the H2D copy of batch i+1 runs on a side stream
         # while step i is still replaying, and never overwrites a set the main stream still reads
@@ -57,10 +57,16 @@ class TrainStepGraph:
     casts) -> the bucket all-reduces in capture order -> graph(optimizer).  The first call with a
     new input signature (shapes / dtypes) runs the step eagerly (allocator / kernel warm-up, a real
     training step) and captures on the next one; graphs are kept per signature (a short last batch
-    gets its own).  Every call is exactly one training step."""
+    gets its own).  Every call is exactly one training step.
 
-    def __init__(self, body, optim, reducer=None, world=1):
+    tail (optional, with a reducer): the second half of a split backward (E2EBase.split_backward /
+    backward_extractors): body then ends with the fusion head's backward, and the step is
+    graph(forward + head backward) -> exchange of the head's buckets, overlapping ->
+    graph(extractors' backward) -> exchange of the rest -> graph(optimizer)."""
+
+    def __init__(self, body, optim, reducer=None, world=1, tail=None):
         self.body, self.optim, self.reducer, self.world = body, optim, reducer, world
+        self.tail = tail if reducer is not None else None
         self.states = {}
         self.static = None   # static inputs of the last call (the agent reads the labels from it)
         self.copy_stream = None
@@ -96,6 +102,8 @@ class TrainStepGraph:
 
     def _eager(self, st):
         st.out = self.body(*st.static)
+        if self.tail is not None:
+            self.tail()
         scale = self.reducer.finish() if self.reducer is not None else 1.0
         self.optim.step(grad_scale=scale)
         return st.out
@@ -113,10 +121,21 @@ class TrainStepGraph:
         else:
             self.reducer.capture_begin()
             try:
-                with torch.cuda.graph(st.g_step, pool=pool):
-                    st.out = self.body(*st.static)
-                    self.reducer.finish()            # captures the remaining buckets' bf16 casts
-                st.order = list(self.reducer.captured)
+                if self.tail is None:
+                    with torch.cuda.graph(st.g_step, pool=pool):
+                        st.out = self.body(*st.static)
+                        self.reducer.finish()            # captures the remaining buckets' bf16 casts
+                    st.order = list(self.reducer.captured)
+                else:
+                    with torch.cuda.graph(st.g_step, pool=pool):
+                        st.out = self.body(*st.static)
+                    mark = self.reducer.capture_mark()
+                    st.g_tail = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(st.g_tail, pool=pool):
+                        self.tail()
+                        self.reducer.finish()
+                    st.order = list(self.reducer.captured[:mark])
+                    st.order_tail = list(self.reducer.captured[mark:])
             finally:
                 self.reducer.capture_end()
             st.g_opt = torch.cuda.CUDAGraph()
@@ -140,7 +159,13 @@ class TrainStepGraph:
             self._capture(st)
         self.optim._sync_lrs()
         st.g_step.replay()
-        if st.g_opt is not None:
+        if st.g_tail is not None:
+            self.reducer.exchange(st.order)        # the head's buckets, beside the extractors' backward
+            st.g_tail.replay()
+            self.reducer.exchange(st.order_tail)
+            self.reducer.join()
+            st.g_opt.replay()
+        elif st.g_opt is not None:
             self.reducer.replay_allreduce(st.order)
             st.g_opt.replay()
         self.optim.step_count += 1      # host bookkeeping the captured optimizer step cannot do

@@ -110,8 +110,9 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     _chk(a, None, "A"); _chk(b, None, "B"); _chk(c, None, "C")
     a_f32 = a.dtype == F32
     b_f32 = b.dtype == F32
+    b_half = a_f32 and b.dtype == F16 and not f16   # fp16 weights, f32 activations and arithmetic
     h = F16 if f16 else BF16
-    if (not a_f32 and a.dtype != h) or (not b_f32 and b.dtype != h):
+    if (not a_f32 and a.dtype != h) or (not b_f32 and not b_half and b.dtype != h):
         raise N.NativeError(f"gemm: operands must be {h} or f32")
     if lda is None:
         lda = k if a_kmajor else m
@@ -132,7 +133,7 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.alpha, d.scale_cols, d.scale_val = alpha, scale_cols, scale_val
     d.row_scale, d.rows_per_scale = ptr(row_scale), rows_per_scale
     d.a_row_scale, d.a_rows_per_scale = ptr(a_row_scale), a_rows_per_scale
-    d.b_f32 = int(b_f32)
+    d.b_f32 = 2 if b_half else int(b_f32)
     d.f16 = int(f16)
     if workspace is not None:
         d.workspace, d.workspace_elems = ptr(workspace), workspace.numel()
@@ -142,7 +143,7 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         _timed("gemm_f32", c, lambda: call("lrce_gemm_ln", ctypes.byref(d), ctypes.byref(ln), stream_of(c)),
                flops=2.0 * m * n * k, key=(m, n, k, 1, "AK", "BK" if b_kmajor else "BN", f"ln{ln.mode}", 1, flags))
         return
-    _timed("gemm_f32" if b_f32 else "gemm", c, lambda: call("lrce_gemm", ctypes.byref(d), stream_of(c)),
+    _timed("gemm_f32" if (b_f32 or b_half) else "gemm", c, lambda: call("lrce_gemm", ctypes.byref(d), stream_of(c)),
            flops=2.0 * m * n * k * batch,
            key=(m, n, k, batch, "AK" if a_kmajor else "AM", "BK" if b_kmajor else "BN", "a32" if a_f32 else "a16",
                 split_k, flags))
@@ -186,8 +187,8 @@ def _split_for(m_out, n_out, k_red):
 def _skinny_drop_ok(x, w, M, a_map=None):
     """Does lrce_gemm route this linear to the exact-f32 skinny kernel (the only one with the fused
     dropout epilogue)?  Mirrors the launcher's test: f32 A and W, K-major A, M <= 64, 16-B aligned."""
-    return (x.dtype == F32 and w.dtype == F32 and M <= 64 and a_map is None and x.data_ptr() % 16 == 0
-            and w.data_ptr() % 16 == 0)
+    return (x.dtype == F32 and w.dtype in (F32, F16) and M <= 64 and a_map is None and x.data_ptr() % 16 == 0
+            and w.data_ptr() % (16 if w.dtype == F32 else 8) == 0)
 
 
 def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None, resid=None, c_map=None,
@@ -326,11 +327,11 @@ def wattn_bias_elems(n_pat, nH):
 
 
 def wattn_bias_build(table, index, n, nH, region, n_pat, bias_fwd, bias_bwd):
-    """bias_fwd f32 (lrce_wattn_fwd_grouped) or fp16 (lrce_wattn_qkv_fwd); bias_bwd f32."""
-    if bias_fwd.dtype not in (torch.float32, F16):
-        raise N.NativeError("wattn_bias_build: bias_fwd must be f32 or fp16")
+    """bias_fwd f32 (lrce_wattn_fwd_grouped) or fp16 (lrce_wattn_qkv_fwd); bias_bwd f32 or fp16."""
+    if bias_fwd.dtype not in (torch.float32, F16) or bias_bwd.dtype not in (torch.float32, F16):
+        raise N.NativeError("wattn_bias_build: bias tiles must be f32 or fp16")
     call("lrce_wattn_bias_build", ptr(table), ptr(index), index.shape[-1], n, nH, ptr(region), n_pat,
-         ptr(bias_fwd), int(bias_fwd.dtype == F16), ptr(bias_bwd), stream_of(bias_fwd))
+         ptr(bias_fwd), int(bias_fwd.dtype == F16), ptr(bias_bwd), int(bias_bwd.dtype == F16), stream_of(bias_fwd))
 
 
 WATTN_GROUP = 4   # windows per workgroup of lrce_wattn_fwd_grouped
@@ -383,9 +384,11 @@ def wattn_bwd(qkv, out, dout, lse, bias_bwd, win_pat, dqkv, dbias_part, n_win, n
     wattn_dbias_part_elems) receives the bias-table gradient binned by relative position (wattn_dbias)."""
     _, wh, ww = window
     # algorithmic work: dV, dP, dQ, dK = 8 n^2 d per (window, head)
+    if bias_bwd.dtype not in (torch.float32, F16):
+        raise N.NativeError("wattn_bwd: bias tiles must be f32 or fp16")
     _timed("wattn_bwd", dqkv, lambda: call("lrce_wattn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(bias_bwd),
-                                            ptr(win_pat), ptr(dqkv), ptr(dbias_part), n_win, n, nH, wh, ww,
-                                            stream_of(dqkv)),
+                                            int(bias_bwd.dtype == F16), ptr(win_pat), ptr(dqkv), ptr(dbias_part),
+                                            n_win, n, nH, wh, ww, stream_of(dqkv)),
            flops=8.0 * n * n * 32 * n_win * nH,
            nbytes=2.0 * n * 32 * n_win * nH * 8, key=(n_win, nH))
 

@@ -36,6 +36,12 @@ class E2EBase(nn.Module):
 
     def __init__(self, *head_args, swin_ckpt=SWIN_B_CKPT, bert_dir=BERT_DIR) -> None:
         super().__init__()
+        # split backward (data-parallel graph mode, lrce/graph.TrainStepGraph(tail=...)): the fusion
+        # head runs on leaf copies of the extractor features, so loss.backward() stops at them and
+        # backward_extractors() continues from their gradients — the gradient exchange of the head's
+        # buckets overlaps the extractors' backward between the two captured graphs
+        self.split_backward = False
+        self._split = None
         self.text_extractor = TextExtractor(bert_dir=bert_dir)
         self.video_extractor = VideoExtractor(swin_ckpt)
         if self.HEAD is not None:
@@ -102,7 +108,18 @@ class E2EBase(nn.Module):
         v = self.extract_video_features(video_clips)
         main.wait_stream(side)
         t.record_stream(main)
+        if self.split_backward and torch.is_grad_enabled():
+            v_in, t_in = v.detach().requires_grad_(True), t.detach().requires_grad_(True)
+            self._split = (v, t, v_in, t_in)
+            return self.fusion_model(v_in, t_in, texts_attention_mask)
         return self.fusion_model(v, t, texts_attention_mask)
+
+    def backward_extractors(self):
+        """Second half of a split backward: the extractors' backward (Swin on this stream, BERT on its
+        side stream, joined at the end) from the feature gradients loss.backward() left."""
+        v, t, v_in, t_in = self._split
+        self._split = None
+        torch.autograd.backward([v, t], [v_in.grad, t_in.grad])
 
 
 # Constructor defaults differ per task (question length 30 vs 40, one output for counting), so each

@@ -94,6 +94,24 @@ class TransformerDecoder(nn.Module):
         self.layers = nn.ModuleList([TransformerDecoderLayer(dropout=dropout) for _ in range(num_layers)])
         self.num_layers = num_layers
 
+    def lrce_f16_params(self):
+        """The query-side weights, read by the recurrent step's skinny GEMMs from their fp16 shadow
+        (runtime.bind): fp16 weights with f32 activations and arithmetic — the reference runs these
+        linears under fp16 autocast (agent_oe.py:28) — halve the 85 M-parameter weight stream every
+        recurrent step re-reads (170 MB: it stays in the 256 MB Infinity Cache across steps)."""
+        ps = []
+        for lay in self.layers:
+            ps += [lay.self_attn.in_proj_weight, lay.self_attn.out_proj.weight, lay.multihead_attn.in_proj_weight,
+                   lay.multihead_attn.out_proj.weight, lay.linear1.weight, lay.linear2.weight]
+        return ps
+
+
+def _wq(lay, w):
+    """The weight a query-side GEMM reads: its fp16 shadow when the flat store keeps one (see
+    TransformerDecoder.lrce_f16_params), else the f32 master."""
+    flat = getattr(lay, "_lrce_flat", None)
+    return flat.w16h(w) if flat is not None and flat.has_f16(w) else w
+
 
 # ----------------------------------------------------------------------------------- decoder
 class _Step:
@@ -128,9 +146,10 @@ def _layer_fwd(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_pr
     projection, norm2 into linear1, and this layer's INPUT LayerNorm (the previous layer's norm3,
     `prev`) into the self-attention v projection (x_in is then the previous layer's pre-norm x3p and
     its stats go to st_prev.m3 / r3).  Each such GEMM also materialises the normalised rows, which
-    the next residual add and the weight gradients read.  Query-side linears run on the exact-f32
-    MFMA path with the f32 master weights (M = Bq is tiny, the recurrence is precision-critical);
-    only the memory K/V (big-M GEMMs) are bf16.  Every dropout rides in the epilogue of the GEMM
+    the next residual add and the weight gradients read.  Query-side linears run on the f32 MFMA
+    path with f32 activations and the weights' fp16 shadow (M = Bq is tiny: the launches stream
+    weights; fp16 rounds them 8x finer than bf16, as the reference's fp16 autocast does); only the
+    memory K/V (big-M GEMMs) are bf16.  Every dropout rides in the epilogue of the GEMM
     producing its input."""
     sa, ca = lay.self_attn, lay.multihead_attn
     Bq = x_in.shape[0]
@@ -139,20 +158,20 @@ def _layer_fwd(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_pr
     x0 = acts.x0[step]
     # self-attention over one token: out_proj(dropout_head(v_proj(x0)))
     if prev is None:
-        sad = K.linear(x_in, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step],
+        sad = K.linear(x_in, _wq(lay, sa.in_proj_weight)[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step],
                        drop=(p, seed, E // NHEAD))
     else:
         st_prev.m3 = torch.empty(Bq, device=dev)
         st_prev.r3 = torch.empty(Bq, device=dev)
         pro = K.ln_fwd_prologue(prev.norm3.weight, prev.norm3.bias, EPS, mean=st_prev.m3, rstd=st_prev.r3, y_out=x0)
-        sad = K.linear(x_in, sa.in_proj_weight[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step],
+        sad = K.linear(x_in, _wq(lay, sa.in_proj_weight)[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step],
                        drop=(p, seed, E // NHEAD), ln=pro)
-    st.x1p = K.linear(sad, sa.out_proj.weight, sa.out_proj.bias, out_f32=True, resid=x0, drop=(p, seed + 1, 1))
+    st.x1p = K.linear(sad, _wq(lay, sa.out_proj.weight), sa.out_proj.bias, out_f32=True, resid=x0, drop=(p, seed + 1, 1))
     # cross-attention to [video tokens of this step ; question tokens]; norm1 in the q projection
     st.m1, st.r1 = torch.empty(Bq, device=dev), torch.empty(Bq, device=dev)
     x1 = acts.x1[step]
     pro = K.ln_fwd_prologue(lay.norm1.weight, lay.norm1.bias, EPS, mean=st.m1, rstd=st.r1, y_out=x1)
-    st.q = K.linear(st.x1p, ca.in_proj_weight[:E], ca.in_proj_bias[:E], out_f32=True, ln=pro)
+    st.q = K.linear(st.x1p, _wq(lay, ca.in_proj_weight)[:E], ca.in_proj_bias[:E], out_f32=True, ln=pro)
     st.ctx = acts.ctx[step]
     st.lse = torch.empty(Bq, NHEAD, 1, device=dev)
     lv = 150
@@ -162,15 +181,15 @@ def _layer_fwd(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_pr
                          stride_kv2_b=Lt * 2 * E, kv2_bdiv=1, out=st.ctx, lse=st.lse,
                          B=Bq, H=NHEAD, scale=(E // NHEAD) ** -0.5, drop_p=p, seed=seed + 2)
     K.mha_fwd(st.desc, st.ctx)
-    st.x2p = K.linear(st.ctx, ca.out_proj.weight, ca.out_proj.bias, out_f32=True, resid=x1, drop=(p, seed + 3, 1))
+    st.x2p = K.linear(st.ctx, _wq(lay, ca.out_proj.weight), ca.out_proj.bias, out_f32=True, resid=x1, drop=(p, seed + 3, 1))
     # FFN: linear2(dropout(gelu(linear1(norm2(x2p))))); norm2 in linear1
     st.m2, st.r2 = torch.empty(Bq, device=dev), torch.empty(Bq, device=dev)
     x2 = acts.x2[step]
     pro = K.ln_fwd_prologue(lay.norm2.weight, lay.norm2.bias, EPS, mean=st.m2, rstd=st.r2, y_out=x2)
     st.pre = torch.empty(Bq, FF, dtype=torch.bfloat16, device=dev)
-    gd = K.linear(st.x2p, lay.linear1.weight, lay.linear1.bias, gelu=True, pre_out=st.pre, out=acts.gd[step],
+    gd = K.linear(st.x2p, _wq(lay, lay.linear1.weight), lay.linear1.bias, gelu=True, pre_out=st.pre, out=acts.gd[step],
                   drop=(p, seed + 4, 1), ln=pro)
-    st.x3p = K.linear(gd, lay.linear2.weight, lay.linear2.bias, out_f32=True, resid=x2, drop=(p, seed + 5, 1))
+    st.x3p = K.linear(gd, _wq(lay, lay.linear2.weight), lay.linear2.bias, out_f32=True, resid=x2, drop=(p, seed + 5, 1))
     return st
 
 
@@ -184,23 +203,23 @@ def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step)
     dx3p = torch.empty_like(st.x3p)
     pro = K.ln_bwd_prologue(st.x3p, st.m3, st.r3, lay.norm3.weight, dgamma=_g(flat, lay.norm3.weight),
                             dbeta=_g(flat, lay.norm3.bias), y_out=dx3p, y2_out=grads.df[step], drop=(p, seed + 5, 1))
-    dgp = K.linear_dx(dx3, lay.linear2.weight, dgelu_pre=st.pre, out=grads.dgp[step], drop=(p, seed + 4, 1), ln=pro)
-    dx2 = K.linear_dx(dgp, lay.linear1.weight, resid=dx3p)
+    dgp = K.linear_dx(dx3, _wq(lay, lay.linear2.weight), dgelu_pre=st.pre, out=grads.dgp[step], drop=(p, seed + 4, 1), ln=pro)
+    dx2 = K.linear_dx(dgp, _wq(lay, lay.linear1.weight), resid=dx3p)
     dx2p = torch.empty_like(st.x2p)
     pro = K.ln_bwd_prologue(st.x2p, st.m2, st.r2, lay.norm2.weight, dgamma=_g(flat, lay.norm2.weight),
                             dbeta=_g(flat, lay.norm2.bias), y_out=dx2p, y2_out=grads.dcao[step], drop=(p, seed + 3, 1))
-    dctx = K.linear_dx(dx2, ca.out_proj.weight, ln=pro)
+    dctx = K.linear_dx(dx2, _wq(lay, ca.out_proj.weight), ln=pro)
     dq = grads.dq[step]
     # the video rows of one step have one writer (nmc == 1: no answer choices share them)
     K.mha_bwd(st.desc, dout=dctx, dq=dq, dk1=dkvv_step, dv1=dkvv_step[E:], ld_dkv1=2 * E,
               stride_dkv1_b=S * 150 * 2 * E, dk2=dkvt if Lt else None, dv2=dkvt[E:] if Lt else None,
               ld_dkv2=2 * E, stride_dkv2_b=Lt * 2 * E, dkv1_store=st.desc.kv1_bdiv == 1)
-    dx1 = K.linear_dx(dq, ca.in_proj_weight[:E], resid=dx2p)
+    dx1 = K.linear_dx(dq, _wq(lay, ca.in_proj_weight)[:E], resid=dx2p)
     dx1p = torch.empty_like(st.x1p)
     pro = K.ln_bwd_prologue(st.x1p, st.m1, st.r1, lay.norm1.weight, dgamma=_g(flat, lay.norm1.weight),
                             dbeta=_g(flat, lay.norm1.bias), y_out=dx1p, y2_out=grads.dsao[step], drop=(p, seed + 1, 1))
-    dsav = K.linear_dx(dx1, sa.out_proj.weight, out=grads.dsav[step], drop=(p, seed, E // NHEAD), ln=pro)
-    return K.linear_dx(dsav, sa.in_proj_weight[2 * E:], resid=dx1p)
+    dsav = K.linear_dx(dx1, _wq(lay, sa.out_proj.weight), out=grads.dsav[step], drop=(p, seed, E // NHEAD), ln=pro)
+    return K.linear_dx(dsav, _wq(lay, sa.in_proj_weight)[2 * E:], resid=dx1p)
 
 
 def _layer_wgrads(lay, flat, acts, grads):

@@ -13,7 +13,7 @@ import math
 import torch
 
 from . import kernels as K
-from .runtime import flat_of, ensure
+from .runtime import aux_stream, flat_of, ensure
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -158,8 +158,26 @@ class FusedAdamW(torch.optim.Optimizer):
         K.l2norm_multi(flat.f32, flat.chunk_tensor, flat.n_chunks, self.sumsq, len(flat.params),
                        tensor_chunk_off=flat.tensor_chunk_off, chunk_sq=self.chunk_sq)
 
-    def zero_grad(self, set_to_none=False):
-        self.flat.grad.zero_()
+    def zero_grad(self, set_to_none=False, overlap=False):
+        """flat.grad = 0 (the backward kernels accumulate into it).  overlap=True: the 1.25 GB clear runs
+        on an aux stream beside the forward (which never touches gradients); grad_ready() must then
+        be called before the backward (it makes the current stream wait for the clear)."""
+        if not overlap or not self.flat.grad.is_cuda:
+            self.flat.grad.zero_()
+            return
+        dev = self.flat.device
+        s = aux_stream(dev, "grad_zero")
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            self.flat.grad.zero_()
+        self._zero_stream = s
+
+    def grad_ready(self):
+        """Join an overlapped zero_grad (no-op otherwise): call between the forward and the backward."""
+        s = getattr(self, "_zero_stream", None)
+        if s is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(s)
+            self._zero_stream = None
 
     # ------------------------------------------------------------------ checkpoints
     # torch.optim.AdamW's format: state[i] = {'step', 'exp_avg', 'exp_avg_sq'} per parameter index.
