@@ -1,3 +1,5 @@
 mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_swin_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_sw.log 2>&1; rc=$?; tail -2 gpurun_out/t_sw.log; [ $rc -eq 0 ] || exit $rc
-for v in 0 512 1024 dbias 0 512; do LRCE_SWIN_WGRAD_STREAM=$v timeout -k 10 200 python bench.py --no-cpu-baseline --agent-steps 0 --steps 20 > gpurun_out/ab_w$v.log 2>&1 || exit 1; echo "w=$v $(tail -1 gpurun_out/ab_w$v.log | cut -c100-140)"; done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3_gputest.log 2>&1; rc=$?; tail -3 gpurun_out/r3_gputest.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py > gpurun_out/r3_bench.log 2>&1 || exit 1; tail -1 gpurun_out/r3_bench.log | cut -c1-300
+bash tools/prof_bench.sh gpurun_out/r3prof || exit 1
+python tools/rocprof_summary.py $(python -c "import glob;print(glob.glob('gpurun_out/r3prof/**/*results.db',recursive=True)[0])") --last 5 > gpurun_out/r3_stats.md 2>&1; head -40 gpurun_out/r3_stats.md
