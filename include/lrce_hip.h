@@ -278,6 +278,140 @@ typedef struct LrceMhaDesc {
 int lrce_mha_fwd(const LrceMhaDesc* desc, void* stream);
 int lrce_mha_bwd(const LrceMhaDesc* desc, void* stream);
 
+/* ---------------------------------------------------------------- recurrent decoder attention blocks
+ * One nn.TransformerDecoderLayer (fusionv3.py:8-17: d_model 768, 12 heads x 64, post-norm, one query
+ * token per row) has two attention blocks that factor by head; each is ONE launch of B x 12
+ * workgroups (csrc/decoder.hip), replacing three launches of the unfused path (lrce_gemm_ln ->
+ * lrce_gemm for the self-attention: v projection -> out_proj; lrce_gemm_ln -> lrce_mha_fwd ->
+ * lrce_gemm for the cross-attention: q projection -> attention -> out_proj; and the same three of
+ * each backward).  Rows are f32 [B][768] (row stride 768), weights the IEEE fp16 shadow [768][768]
+ * (row = output feature), biases / LayerNorm parameters f32.  Dropout (drop_p > 0, train mode) uses
+ * the masks of lrce_dropout / lrce_mha_* for the same seeds (seed = the layer's base seed as the
+ * unfused path passes it: self-attention head mask `seed`, its out dropout seed + 1; cross-attention
+ * probabilities seed + 2, out dropout seed + 3).  slab: f32 workspace of lrce_dec_slab_elems(B)
+ * elements; counters: B zero-initialised uint32 (left zero after every launch).  One stream at a time
+ * may use a slab / counters pair.  B <= LRCE_DEC_MAX_ROWS. */
+#define LRCE_DEC_MAX_ROWS 64
+int64_t lrce_dec_slab_elems(int B);
+typedef struct LrceDecKv {   /* memory K/V (bf16): key j < lk1 of row b at k1[(b/bdiv1)*stride1 + j*ld1 + h*64],
+                                 j >= lk1 at k2[(b/bdiv2)*stride2 + (j-lk1)*ld2 + h*64]; V at K + v_off */
+  const uint16_t* k1;
+  int64_t stride1, ld1;
+  int32_t bdiv1, lk1;
+  const uint16_t* k2;
+  int64_t stride2, ld2;
+  int32_t bdiv2, lk2;
+  int64_t v_off;
+} LrceDecKv;
+/* x1p = x0 + drop(out_proj(drop_head(v_proj(x0)))), x0 = LN(x_in) with (ln_gamma, ln_beta, eps)
+ * (the previous layer's norm3; ln_gamma NULL: x0 = x_in) -> x0_out / mean_out / rstd_out;
+ * sad = the dropped v projection (the out_proj's input). */
+typedef struct LrceDecSa {
+  int32_t B;
+  const float* x_in;
+  const float* ln_gamma;
+  const float* ln_beta;
+  float eps;
+  float* x0_out;
+  float* mean_out;
+  float* rstd_out;
+  const uint16_t* wv;   /* self_attn.in_proj_weight rows 2E..3E */
+  const float* bv;
+  const uint16_t* wo;   /* self_attn.out_proj.weight */
+  const float* bo;
+  float* sad;
+  float* x1p;
+  float drop_p;
+  uint64_t seed;
+  float* slab;
+  uint32_t* counters;
+} LrceDecSa;
+int lrce_dec_sa_fwd(const LrceDecSa* args, void* stream);
+/* x1 = LN1(x1p) -> x1_out, mean_out, rstd_out; q = W_q x1 + b_q -> q_out; ctx = attention(q, memory)
+ * -> ctx_out, lse_out [B][12] (natural log); x2p = x1 + drop(out_proj(ctx)).  seed: the layer's seed
+ * + 2 (attention probabilities; the out dropout uses seed + 1 of this value). */
+typedef struct LrceDecCa {
+  int32_t B;
+  const float* x1p;
+  const float* g1;
+  const float* b1;
+  float eps;
+  float* x1_out;
+  float* mean_out;
+  float* rstd_out;
+  const uint16_t* wq;   /* multihead_attn.in_proj_weight rows 0..E */
+  const float* bq;
+  LrceDecKv kv;
+  float* q_out;
+  float* ctx_out;
+  float* lse_out;
+  const uint16_t* wo;   /* multihead_attn.out_proj.weight */
+  const float* bo;
+  float* x2p;
+  float drop_p;
+  uint64_t seed;
+  float* slab;
+  uint32_t* counters;
+} LrceDecCa;
+int lrce_dec_ca_fwd(const LrceDecCa* args, void* stream);
+/* Backward of the cross-attention block from dx2 = d LN2(x2p): dx2p = LN2 backward (mean2 / rstd2 /
+ * g2), dcao = its out-dropout backward -> dcao_out (the out_proj's output gradient); dctx = W_o^T dcao;
+ * attention backward -> dq_out, dK / dV of the memory (video rows dk1 (+ dv_off for dV) with their
+ * own dstride1 / dld1: STORED when bdiv1 == 1, atomically added otherwise; text rows dk2 accumulated);
+ * dx1_out = dx2p + W_q^T dq.  LayerNorm parameter gradients: lrce_dec_ln_grads. */
+typedef struct LrceDecCaBwd {
+  int32_t B;
+  const float* dx2;
+  const float* x2p;
+  const float* mean2;
+  const float* rstd2;
+  const float* g2;
+  float* dcao_out;
+  const uint16_t* wo;
+  LrceDecKv kv;
+  const float* q;
+  const float* ctx;
+  const float* lse;
+  float* dq_out;
+  float* dk1;
+  int64_t dstride1, dld1;
+  float* dk2;
+  int64_t dstride2, dld2;
+  int64_t dv_off;
+  const uint16_t* wq;
+  float* dx1_out;
+  float drop_p;
+  uint64_t seed;   /* as lrce_dec_ca_fwd */
+  float* slab;
+  uint32_t* counters;
+} LrceDecCaBwd;
+int lrce_dec_ca_bwd(const LrceDecCaBwd* args, void* stream);
+/* Backward of the self-attention block from dx1 = d LN1(x1p): dx1p = LN1 backward, dsao = its out-
+ * dropout backward -> dsao_out; dsav = head-mask backward of W_o^T dsao -> dsav_out; dx0_out = dx1p +
+ * W_v^T dsav. */
+typedef struct LrceDecSaBwd {
+  int32_t B;
+  const float* dx1;
+  const float* x1p;
+  const float* mean1;
+  const float* rstd1;
+  const float* g1;
+  float* dsao_out;
+  const uint16_t* wo;
+  float* dsav_out;
+  const uint16_t* wv;
+  float* dx0_out;
+  float drop_p;
+  uint64_t seed;   /* as lrce_dec_sa_fwd */
+  float* slab;
+  uint32_t* counters;
+} LrceDecSaBwd;
+int lrce_dec_sa_bwd(const LrceDecSaBwd* args, void* stream);
+/* LayerNorm parameter gradients over rows [rows][768] of every recurrent step at once (n_ln <= 3
+ * LayerNorms): dgamma[c] += sum_r dy (x - mean) rstd, dbeta[c] += sum_r dy, rows in order. */
+int lrce_dec_ln_grads(const float* const* dy, const float* const* x, const float* const* mean, const float* const* rstd,
+                      float* const* dgamma, float* const* dbeta, int n_ln, int rows, void* stream);
+
 /* ---------------------------------------------------------------- elementwise / data movement */
 /* Patch-embed input stage: [ImageNet Normalize (video.py:35)] + zero-pad T to a multiple of 2
  * (video_swin_ori.py:472-473) + im2col of the non-overlapping (2,4,4) patches of conv3d (:458,475).

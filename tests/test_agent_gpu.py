@@ -161,3 +161,64 @@ def test_early_group_updates_match_one_update():
     opt.step()
     torch.cuda.synchronize()
     assert torch.equal(early, flat.f32)
+
+
+def test_early_updates_do_not_race_the_backward():
+    """The same training step run twice from identical weights and optimizer state — once with the
+    in-backward group updates, once with one update after the backward — with every stochastic element
+    off (train mode, dropout / DropPath 0, so both runs must produce the same gradients): flat.grad and
+    the updated masters must agree bit for bit.  An early update that overlapped a backward kernel still
+    reading its group's weights (the decoder's and Swin stages' updates run on the weight-gradient
+    stream, BERT's on the text stream), or that read a gradient before its last writer, changes one of
+    them; the test above cannot see that, because it reuses the racing run's gradients."""
+    from lrce.optim import FusedAdamW
+    b = [t.cuda() for t in _batch("oe", 32)]
+    model = _model("oe", 50, 32)
+    model.fusion_model.drop_out_rate = 0.0
+    model.fusion_model.fusion_transformer.drop_out_rate = 0.0
+    for layer in model.video_extractor.swin.layers:
+        for blk in layer.blocks:
+            blk.drop_path = 0.0
+    model.text_extractor.bert.hidden_dropout = model.text_extractor.bert.attention_dropout = 0.0
+    model = model.cuda().train()
+    opt = FusedAdamW(model, [model.parameters()], lr=1e-4, reg_strength=0.001)
+    flat = opt.flat
+    for _ in range(2):
+        opt.zero_grad()
+        F.cross_entropy(model(*b[:4]).float(), b[4]).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    bufs = (flat.f32, opt.exp_avg, opt.exp_avg_sq, opt.sumsq, opt.step_t)
+    state = [t.clone() for t in bufs]
+    count = opt.step_count
+
+    def run(groups):
+        for dst, src in zip(bufs, state):
+            dst.copy_(src)
+        opt.step_count = count
+        flat.masters_written()                       # re-cast the bf16 / fp16 shadows of the restored masters
+        opt._norm_version = flat.master_version()    # the restored norms belong to the restored weights
+        opt.enable_early_updates(groups)
+        n0 = opt.early_updates
+        opt.zero_grad()
+        F.cross_entropy(model(*b[:4]).float(), b[4]).backward()
+        opt.step()
+        torch.cuda.synchronize()
+        return flat.grad.clone(), flat.f32.clone(), opt.early_updates - n0
+
+    def diff(a, b):
+        bad = []
+        for name, p in model.named_parameters():
+            sl = flat._slice(a, p)
+            sb = flat._slice(b, p)
+            if not torch.equal(sl, sb):
+                bad.append(f"{name}: max|d| {float((sl - sb).abs().max()):.3e} of {float(sb.abs().max()):.3e}")
+        return bad
+
+    g_plain, w_plain, n_plain = run({})
+    g_plain2, w_plain2, _ = run({})
+    assert not diff(g_plain, g_plain2), "the backward itself is not bitwise repeatable:\n" + "\n".join(diff(g_plain, g_plain2)[:20])
+    g_early, w_early, n_early = run(model.optimizer_groups())
+    assert n_early == 5 and n_plain == 0
+    assert not diff(g_early, g_plain), "gradients differ with early updates:\n" + "\n".join(diff(g_early, g_plain)[:20])
+    assert torch.equal(w_early, w_plain)

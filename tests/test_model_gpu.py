@@ -123,6 +123,39 @@ def test_fusion_backward_matches_oracle(task, L, ncls, B):
         assert rel(named[k].grad, sd["fusion_model." + k].grad) < 3e-2, k
 
 
+@pytest.mark.parametrize("task,L,ncls,B,drop", [("oe", 32, 1000, 3, 0.1), ("oe", 32, 1000, 2, 0.0), ("mc", 40, 1, 2, 0.1),
+                                                 ("mcsim", 40, 1, 2, 0.1)])
+def test_fused_decoder_blocks_match_unfused(task, L, ncls, B, drop, monkeypatch):
+    """The per-head fused attention blocks of the recurrent decoder (csrc/decoder.hip: one launch per
+    block, forward and backward) against the unfused launches (lrce_gemm_ln / lrce_mha / lrce_gemm) on
+    the same inputs, in train mode with dropout on: both draw the same masks, so logits and every
+    parameter / input gradient must agree to f32 rounding (different summation order only)."""
+    from lrce.models.fusionv3 import LRCEOpenEnded, LRCEMultipleChoice, LRCEMultipleChoiceSim
+    cls = {"oe": LRCEOpenEnded, "mc": LRCEMultipleChoice, "mcsim": LRCEMultipleChoiceSim}[task]
+    torch.manual_seed(3)
+    m = cls(768, ncls, drop, (7, 7), 1024, 5, [3], L).cuda().train()
+    vf = torch.randn(B, 3, 3, 49, 1024, device="cuda")
+    tf = torch.randn(B, 5, L, 768, device="cuda") if task != "oe" else torch.randn(B, L, 768, device="cuda")
+    runs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("LRCE_DEC_FUSED", fused)
+        m.zero_grad(set_to_none=True)
+        vg, tg = vf.clone().requires_grad_(True), tf.clone().requires_grad_(True)
+        torch.manual_seed(11)   # the dropout seeds the model draws
+        y = m(vg, tg, None)
+        R = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).cuda()
+        (y.float() * R).sum().backward()
+        torch.cuda.synchronize()
+        runs.append((y.detach().float().clone(), vg.grad.clone(), tg.grad.clone(),
+                     {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}))
+    (y0, v0, t0, g0), (y1, v1, t1, g1) = runs
+    assert rel(y1, y0) < 1e-4
+    assert rel(v1, v0) < 1e-4 and rel(t1, t0) < 1e-4
+    assert g0.keys() == g1.keys()
+    bad = {k: rel(g1[k], g0[k]) for k in g0 if rel(g1[k], g0[k]) > 2e-4}
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]
+
+
 def _e2e(name, ts=(3,)):
     from lrce.models import e2e
     task, ncls, L = CFG[name]

@@ -27,7 +27,7 @@ def K():
 
 def rel(a, b):
     a = a.float(); b = b.float()
-    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
 
 
 def bf(t):
@@ -366,10 +366,14 @@ def _wattn_reference(qkv, table, index, region, win_pat, nH, n, c):
     return o.transpose(1, 2).reshape(nw * n, C), (q, kk, v, tab)
 
 
-@pytest.mark.parametrize("nH,n_win,bias16", [(4, 9, False), (16, 5, False), (32, 2, False), (4, 9, True), (16, 5, True)])
-def test_window_attention_fwd_bwd(nH, n_win, bias16):
+@pytest.mark.parametrize("nH,n_win,bias16,gscale", [(4, 9, False, 1.0), (16, 5, False, 1.0), (32, 2, False, 1.0),
+                                                   (4, 9, True, 1.0), (16, 5, True, 1.0), (4, 9, True, 1e-12),
+                                                   (16, 5, True, 1e6)])
+def test_window_attention_fwd_bwd(nH, n_win, bias16, gscale):
     """bias16: the backward reads fp16 bias tiles (the Swin-B product path, same rounding as the fused
-    forward's); else f32."""
+    forward's); else f32.  gscale: the upstream gradient's magnitude — a batch-mean cross-entropy over
+    ~10^5 tokens hands the attention ~1e-6..1e-12-sized gradients; the bias-table bins' fixed point is
+    scaled per (window, head), so the relative error must not depend on it."""
     k = K()
     n, hd = 147, 32
     C = nH * hd
@@ -401,7 +405,7 @@ def test_window_attention_fwd_bwd(nH, n_win, bias16):
     k.wattn_fwd_grouped(qkv, bf_, k.wattn_groups(None, n_win, dev), out_i, lse_i, n_win, n, nH)   # identity grouping
     ref_i, _ = _wattn_reference(qkv, table, index, region, torch.zeros_like(win_pat), nH, n, c)
     assert rel(out_i, ref_i) < 1e-2
-    dout = bf(torch.randn(n_win * n, C, device=dev))
+    dout = bf(torch.randn(n_win * n, C, device=dev) * gscale)
     ref.backward(dout.float())
     dqkv = torch.full((n_win * n, 3 * C), float("nan"), device=dev, dtype=torch.bfloat16)
     win = (3, 7, 7)

@@ -1,5 +1,4 @@
 mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3_gputest.log 2>&1; rc=$?; tail -3 gpurun_out/r3_gputest.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python bench.py > gpurun_out/r3_bench.log 2>&1 || exit 1; tail -1 gpurun_out/r3_bench.log | cut -c1-300
-bash tools/prof_bench.sh gpurun_out/r3prof || exit 1
-python tools/rocprof_summary.py $(python -c "import glob;print(glob.glob('gpurun_out/r3prof/**/*results.db',recursive=True)[0])") --last 5 > gpurun_out/r3_stats.md 2>&1; head -40 gpurun_out/r3_stats.md
+timeout -k 10 300 python -u -m pytest tests/test_model_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k "fused_decoder" > gpurun_out/t3.log 2>&1; rc=$?; grep -E "^E  |passed|failed|Error" gpurun_out/t3.log | head -30; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u -m pytest tests/test_agent_gpu.py tests/test_ops_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k "early or window_attention_fwd_bwd" > gpurun_out/t2.log 2>&1; rc=$?; grep -E "^E  |passed|failed" gpurun_out/t2.log | head -30
+timeout -k 10 300 python bench.py --no-cpu-baseline --agent-steps 0 --steps 20 > gpurun_out/b3.log 2>&1; tail -1 gpurun_out/b3.log | cut -c1-400

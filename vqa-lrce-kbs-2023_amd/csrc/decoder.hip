@@ -1,0 +1,922 @@
+// Recurrent LRCE decoder, per-head fused attention blocks (nn.TransformerDecoderLayer, post-norm,
+// 768 wide, 12 heads x 64, one query token per batch row: fusionv3.py:8-17,44-49) on gfx950.
+//
+// The recurrent step is a chain of M = B (10..45) row linears: every launch boundary on it costs a
+// dependent round trip (~2 us measured, tools/decoder_probe.hip) on top of the ~1.9 us launch, and the
+// GPU is otherwise idle there.  Both attention blocks of a layer factor by head, so each becomes ONE
+// launch of B x 12 workgroups, workgroup (b, h) doing the head's share of every linear:
+//
+//   self-attention (one key: softmax == 1, so out_proj(drop_head(v_proj(x0)))):
+//     x0 = [LN3 of the previous layer](x_in)                  (row b, recomputed by every head)
+//     v_h = W_v[h] x0 + b_v[h]    (64 x 768 slice, weight rows in registers)
+//     sad_h = drop_head(v_h)      (mask per (b, h): the group-64 dropout of lrce_dropout)
+//     part_h = W_o[:, h] sad_h    (768 x 64 slice, staged in LDS by LDS-DMA at kernel start)
+//     x1p = x0 + drop(sum_h part_h + b_o)          (the last of the 12 heads to arrive sums in h order)
+//   cross-attention:
+//     x1 = LN1(x1p); q_h = W_q[h] x1 + b_q[h]; ctx_h = attn(q_h, memory K/V of head h) (dropout on P)
+//     x2p = x1 + drop(sum_h W_oc[:, h] ctx_h + b_oc)
+// and the backward of each block is one launch the same way (LN backward of the block's output
+// gradient recomputed per head; dctx_h / dsav_h from the W_o slice; mha backward; the dX partials
+// W_q[h]^T dq_h / W_v[h]^T dsav_h summed by the last head).  The FFN keeps its two lrce_gemm_ln /
+// lrce_gemm launches (its 3072-wide hidden layer does not factor by head).
+//
+// Cross-workgroup hand-off: MI355X_MICROARCH.md "splitk-seam" / the skinny split-K of gemm_f32.hip:
+// partial rows by agent-scope relaxed stores, s_waitcnt vmcnt(0), barrier, one agent-scope atomic add
+// per workgroup on a per-row counter; the workgroup whose add returns 11 reads the 12 partials with
+// agent-scope loads in head order (deterministic) and resets the counter (graph-replay safe).
+// Weights are the decoder's IEEE fp16 shadow (the reference's fp16 autocast), arithmetic f32.
+// Dropout masks are the ones the unfused path draws (lrce_dropout hash over the same [B][768] index,
+// mha dropout over ((b*12 + h) * Lk + j)), so forward and backward agree with each other and with it.
+#include "common.h"
+#include "lrce_capi.h"
+
+namespace {
+
+constexpr int E = 768, H = 12, D = 64, NT = 256, MAXK = 192;
+constexpr int WROWS = 16;            // rows of a head's 64-row weight slice per wave
+constexpr int NRI = 24;              // 16-B register loads per lane for 16 rows x 768 (fp16)
+
+__device__ __forceinline__ void dec_glds(const void* sbase, uint32_t voff, uint32_t lds_dst) {
+  unsigned keep;
+  const uint64_t a = reinterpret_cast<uintptr_t>(sbase);
+  const uint64_t su = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a) |
+                      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32);
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(su), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+}
+__device__ __forceinline__ uint32_t dec_lds_addr(const void* p) { return (uint32_t)(uintptr_t)((LRCE_LDS const void*)p); }
+// the same with a per-lane 64-bit source address (rows from two key segments in one instruction)
+__device__ __forceinline__ void dec_glds_p(const void* src, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+}
+
+__device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = (float)__builtin_bit_cast(f16, (unsigned short)(w[e] & 0xFFFFu));
+    f[2 * e + 1] = (float)__builtin_bit_cast(f16, (unsigned short)(w[e] >> 16));
+  }
+}
+
+// The [768][64] slice W[:, h*64 .. h*64+63] of a row-major [768][768] fp16 matrix -> LDS image
+// [n][64] (128-B rows), 8 rows per 1-KB DMA instruction, 24 per wave.  Issued at kernel start.
+__device__ __forceinline__ void slice_dma(const f16* w, int h, void* lds, int wave, int lane) {
+  const uint32_t base = dec_lds_addr(lds);
+#pragma unroll 4
+  for (int i = 0; i < 24; ++i) {
+    const int ins = wave * 24 + i;
+    const int row = ins * 8 + (lane >> 3);
+    dec_glds(w, (uint32_t)((row * E + h * D + (lane & 7) * 8) * 2), base + (uint32_t)ins * 1024u);
+  }
+}
+
+// Rows r0 .. r0+15 of a row-major [.][768] fp16 matrix into registers, 24 x 16 B per lane:
+// ins r (< 16): row r0 + r, 8-element chunk `lane` (elements 8*lane .. 8*lane+7);
+// ins 16 + s:   row r0 + 2s + (lane >= 32), chunk 64 + (lane & 31).
+__device__ __forceinline__ void rows_load(const f16* w, int r0, int lane, uint4 (&reg)[NRI]) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) reg[r] = *reinterpret_cast<const uint4*>(w + (long long)(r0 + r) * E + lane * 8);
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    reg[16 + s] = *reinterpret_cast<const uint4*>(w + (long long)(r0 + 2 * s + (lane >> 5)) * E + (64 + (lane & 31)) * 8);
+}
+
+__device__ __forceinline__ float dot8(const float (&a)[8], const float* x) {
+  const float4 x0 = *reinterpret_cast<const float4*>(x), x1 = *reinterpret_cast<const float4*>(x + 4);
+  return ((a[0] * x0.x + a[1] * x0.y) + (a[2] * x0.z + a[3] * x0.w)) + ((a[4] * x1.x + a[5] * x1.y) + (a[6] * x1.z + a[7] * x1.w));
+}
+
+// out[r] = W[r0 + r] . x for the wave's 16 rows (x in LDS, 768 f32); result written to o[16] in LDS
+// through a [16][64] partial image (each lane's per-row dot, then 4 lanes per row).
+__device__ __forceinline__ void rows_gemv(const uint4 (&reg)[NRI], const float* x, float* pp, float* o, int lane) {
+  float u[16];
+  float wf[8];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    unpack8(reg[r], wf);
+    u[r] = dot8(wf, x + lane * 8);
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    unpack8(reg[16 + s], wf);
+    const float v = dot8(wf, x + (64 + (lane & 31)) * 8);
+    if (lane < 32) u[2 * s] += v;
+    else u[2 * s + 1] += v;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) pp[r * 64 + lane] = u[r];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int r = lane >> 2, q = lane & 3;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += pp[r * 64 + q * 16 + i];
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  if (q == 0) o[r] = s;
+}
+
+// acc[768] (LDS, per wave) = sum_r v[r] W[r0 + r][:] for the wave's 16 rows (the transposed product
+// W^T v of a dX): lane l owns columns 8l..8l+7 and 512 + 8(l&31).. (the latter split by lane half)
+__device__ __forceinline__ void rows_gemv_t(const uint4 (&reg)[NRI], const float* v, float* acc, int lane) {
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, c[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float wf[8];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    unpack8(reg[r], wf);
+    const float vr = v[r];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = fmaf(vr, wf[e], a[e]);
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    unpack8(reg[16 + s], wf);
+    const float vr = v[2 * s + (lane >> 5)];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) c[e] = fmaf(vr, wf[e], c[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) c[e] += __shfl_xor(c[e], 32, 64);
+  *reinterpret_cast<float4*>(acc + lane * 8) = make_float4(a[0], a[1], a[2], a[3]);
+  *reinterpret_cast<float4*>(acc + lane * 8 + 4) = make_float4(a[4], a[5], a[6], a[7]);
+  if (lane < 32) {
+    *reinterpret_cast<float4*>(acc + 512 + lane * 8) = make_float4(c[0], c[1], c[2], c[3]);
+    *reinterpret_cast<float4*>(acc + 512 + lane * 8 + 4) = make_float4(c[4], c[5], c[6], c[7]);
+  }
+}
+
+// out[n] = sum_d S[n][d] v[d] over the LDS head slice S [768][64] (fp16), the wave's rows
+// n = wave*192 .. +191: lane (g = lane/8, c = lane%8) takes row 8i+g, chunk c; 8-lane reduction.
+__device__ __forceinline__ void slice_gemv(const f16* S, const float* v, float* out, int wave, int lane) {
+  const int g = lane >> 3, c = lane & 7;
+  float vv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) vv[e] = v[c * 8 + e];
+#pragma unroll 4
+  for (int i = 0; i < 24; ++i) {
+    const int n = wave * 192 + i * 8 + g;
+    float wf[8];
+    unpack8(*reinterpret_cast<const uint4*>(S + n * D + c * 8), wf);
+    float s = ((wf[0] * vv[0] + wf[1] * vv[1]) + (wf[2] * vv[2] + wf[3] * vv[3])) +
+              ((wf[4] * vv[4] + wf[5] * vv[5]) + (wf[6] * vv[6] + wf[7] * vv[7]));
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (c == 0) out[n] = s;
+  }
+}
+
+// out[d] (d < 64) = sum_n S[n][d] u[n] (u: 768 in LDS); per-wave partials into red[wave][64]
+__device__ __forceinline__ void slice_gemv_t(const f16* S, const float* u, float* red, int wave, int lane) {
+  const int g = lane >> 3, c = lane & 7;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int i = 0; i < 24; ++i) {
+    const int n = wave * 192 + i * 8 + g;
+    float wf[8];
+    unpack8(*reinterpret_cast<const uint4*>(S + n * D + c * 8), wf);
+    const float un = u[n];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = fmaf(un, wf[e], a[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a[e] += __shfl_xor(a[e], 8, 64);
+    a[e] += __shfl_xor(a[e], 16, 64);
+    a[e] += __shfl_xor(a[e], 32, 64);
+  }
+  if (g == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wave * 64 + c * 8 + e] = a[e];
+  }
+}
+
+__device__ __forceinline__ float block_sum4(float v, float* red2, int lane, int wave) {
+  v = wave_sum(v);
+  if (lane == 0) red2[wave] = v;
+  __syncthreads();
+  const float r = (red2[0] + red2[1]) + (red2[2] + red2[3]);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ float block_max4(float v, float* red2, int lane, int wave) {
+  v = wave_max(v);
+  if (lane == 0) red2[wave] = v;
+  __syncthreads();
+  const float r = fmaxf(fmaxf(red2[0], red2[1]), fmaxf(red2[2], red2[3]));
+  __syncthreads();
+  return r;
+}
+
+// LayerNorm forward of one 768 row held as float4 by threads t < 192 (two-pass statistics, the
+// order of lrce_gemm_ln mode 1): y = (x - mu) rstd g + b into ys (LDS)
+__device__ __forceinline__ void ln_row_fwd(float4 x, const float* g, const float* bb, float eps, float* ys, float* red2,
+                                           int t, int lane, int wave, float& mu, float& rs) {
+  const bool live = t < E / 4;
+  const float s1 = block_sum4(live ? (x.x + x.y) + (x.z + x.w) : 0.f, red2, lane, wave);
+  mu = s1 * (1.0f / E);
+  float4 d = make_float4(x.x - mu, x.y - mu, x.z - mu, x.w - mu);
+  const float s2 = block_sum4(live ? (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w) : 0.f, red2, lane, wave);
+  rs = rsqrtf(s2 * (1.0f / E) + eps);
+  if (live) {
+    const float4 gg = *reinterpret_cast<const float4*>(g + 4 * t), be = *reinterpret_cast<const float4*>(bb + 4 * t);
+    *reinterpret_cast<float4*>(ys + 4 * t) =
+        make_float4(d.x * rs * gg.x + be.x, d.y * rs * gg.y + be.y, d.z * rs * gg.z + be.z, d.w * rs * gg.w + be.w);
+  }
+}
+
+// LayerNorm backward of one row: dy (float4, t < 192), x, mean, rstd, gamma -> dx (float4), the
+// formula of lrce_gemm_ln mode 2: dx = rstd (g - mean(g) - xh mean(g xh)), g = dy gamma
+__device__ __forceinline__ float4 ln_row_bwd(float4 dy, float4 x, float mu, float rs, const float* gamma, float* red2, int t,
+                                             int lane, int wave) {
+  const bool live = t < E / 4;
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f), xh = g;
+  if (live) {
+    const float4 gm = *reinterpret_cast<const float4*>(gamma + 4 * t);
+    g = make_float4(dy.x * gm.x, dy.y * gm.y, dy.z * gm.z, dy.w * gm.w);
+    xh = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+  }
+  const float s1 = block_sum4((g.x + g.y) + (g.z + g.w), red2, lane, wave);
+  const float s2 = block_sum4((g.x * xh.x + g.y * xh.y) + (g.z * xh.z + g.w * xh.w), red2, lane, wave);
+  const float mg = s1 * (1.0f / E), mgx = s2 * (1.0f / E);
+  return make_float4(rs * (g.x - mg - xh.x * mgx), rs * (g.y - mg - xh.y * mgx), rs * (g.z - mg - xh.z * mgx),
+                     rs * (g.w - mg - xh.w * mgx));
+}
+
+__device__ __forceinline__ float drop1(float v, float p, uint64_t seed, long long idx) {
+  return lrce_uniform(seed, (uint64_t)idx) >= p ? v / (1.0f - p) : 0.f;
+}
+
+// publish this head's partial row (768 f32) and return true in the last of the 12 heads to arrive
+__device__ __forceinline__ bool publish_partial(const float* part_lds, float* slab, unsigned* ctr, int b, int h, int t,
+                                                unsigned* last_flag) {
+  float* mine = slab + ((long long)b * H + h) * E;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) __hip_atomic_store(mine + t + 256 * i, part_lds[t + 256 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) *last_flag = __hip_atomic_fetch_add(&ctr[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(H - 1);
+  __syncthreads();
+  return *last_flag != 0;
+}
+// the 12 partials of element n of row b, summed in head order
+__device__ __forceinline__ float gather_partials(const float* slab, int b, int n) {
+  float s = 0.f;
+  const float* src = slab + (long long)b * H * E + n;
+#pragma unroll
+  for (int j = 0; j < H; ++j) s += __hip_atomic_load(src + j * E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return s;
+}
+
+// ------------------------------------------------------------------ self-attention block forward
+struct SaFwdP {
+  int B;
+  const float* x_in;              // [B][768]: s or the previous layer's pre-norm x3p
+  const float* ln_g;              // previous layer's norm3 (NULL: x0 = x_in)
+  const float* ln_b;
+  float eps;
+  float* x0_out;                  // LN output (when ln_g), [B][768]
+  float* mean_out;
+  float* rstd_out;
+  const f16* wv;                  // W_v rows [768][768] (in_proj rows 2E..3E)
+  const float* bv;
+  const f16* wo;                  // out_proj [768][768]
+  const float* bo;
+  float* sad;                     // [B][768] dropped v (the out_proj's input, for its weight gradient)
+  float* x1p;                     // [B][768]
+  float p;
+  uint64_t seed;                  // layer seed: head mask seed, out dropout seed + 1
+  const uint64_t* rng_off;
+  float* slab;
+  unsigned* ctr;
+};
+
+struct SaFwdLds {
+  f16 wo[E * D];                  // 96 KB
+  float x0[E];
+  float pp[4][16 * 64];
+  float v[D];
+  float part[E];
+  float red2[4];
+  unsigned last;
+};
+
+__global__ void __launch_bounds__(NT, 1) dec_sa_fwd_kernel(SaFwdP p) {
+  __shared__ __attribute__((aligned(16))) SaFwdLds L;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  // everything that depends on nothing: the row, the W_v rows, the W_o slice (DMA)
+  float4 xr = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < E / 4) xr = *reinterpret_cast<const float4*>(p.x_in + (long long)b * E + 4 * t);
+  uint4 wr[NRI];
+  rows_load(p.wv, h * D + wave * WROWS, lane, wr);
+  const float bvv = t < D ? p.bv[h * D + t] : 0.f;
+  slice_dma(p.wo, h, L.wo, wave, lane);   // last: the compiler's vmcnt waits do not count these
+  if (p.ln_g) {
+    float mu, rs;
+    ln_row_fwd(xr, p.ln_g, p.ln_b, p.eps, L.x0, L.red2, t, lane, wave, mu, rs);
+    if (h == 0) {
+      if (t < E / 4) *reinterpret_cast<float4*>(p.x0_out + (long long)b * E + 4 * t) = *reinterpret_cast<const float4*>(L.x0 + 4 * t);
+      if (t == 0) {
+        p.mean_out[b] = mu;
+        p.rstd_out[b] = rs;
+      }
+    }
+  } else if (t < E / 4) {
+    *reinterpret_cast<float4*>(L.x0 + 4 * t) = xr;
+  }
+  __syncthreads();
+  // v = W_v[h] x0 + b_v ; head dropout
+  rows_gemv(wr, L.x0, L.pp[wave], L.v + wave * WROWS, lane);
+  __syncthreads();
+  const uint64_t seed0 = lrce_seed(p.seed, p.rng_off);
+  if (t < D) {
+    float v = L.v[t] + bvv;
+    if (p.p > 0.f) v = drop1(v, p.p, seed0, ((long long)b * E + h * D + t) / D);
+    L.v[t] = v;
+    p.sad[(long long)b * E + h * D + t] = v;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slice DMA has landed
+  __syncthreads();                                    // ... and every wave's; L.v complete
+  slice_gemv(L.wo, L.v, L.part, wave, lane);
+  __syncthreads();
+  if (!publish_partial(L.part, p.slab, p.ctr, b, h, t, &L.last)) return;
+  const uint64_t seed1 = lrce_seed(p.seed + 1, p.rng_off);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    float y = gather_partials(p.slab, b, n) + p.bo[n];
+    if (p.p > 0.f) y = drop1(y, p.p, seed1, (long long)b * E + n);
+    p.x1p[(long long)b * E + n] = L.x0[n] + y;
+  }
+  if (t == 0) __hip_atomic_store(&p.ctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------ cross-attention block forward
+struct KvP {
+  const bf16* k1;   // video segment: row (b / bdiv1) * stride1 + j * ld (K at +0, V at +v_off)
+  long long stride1, ld1;
+  int bdiv1, lk1;
+  const bf16* k2;   // text segment (NULL: none)
+  long long stride2, ld2;
+  int bdiv2, lk2;
+  long long v_off;  // V = K + v_off (elements)
+};
+__device__ __forceinline__ const bf16* kv_row(const KvP& kv, int b, int j, int h) {
+  if (j < kv.lk1) return kv.k1 + (long long)(b / kv.bdiv1) * kv.stride1 + (long long)j * kv.ld1 + h * D;
+  return kv.k2 + (long long)(b / kv.bdiv2) * kv.stride2 + (long long)(j - kv.lk1) * kv.ld2 + h * D;
+}
+
+struct CaFwdP {
+  int B;
+  const float* x1p;               // [B][768]
+  const float* g1;                // norm1
+  const float* b1;
+  float eps;
+  float* x1_out;                  // [B][768] (h == 0)
+  float* mean_out;
+  float* rstd_out;
+  const f16* wq;                  // in_proj rows 0..E
+  const float* bq;
+  KvP kv;
+  float* q_out;                   // [B][768] f32 (the backward's q)
+  float* ctx_out;                 // [B][768]
+  float* lse_out;                 // [B][12]
+  const f16* wo;                  // out_proj [768][768]
+  const float* bo;
+  float* x2p;                     // [B][768]
+  float p;
+  uint64_t seed;                  // attention dropout seed (seed + 2 of the layer); out dropout seed + 1
+  const uint64_t* rng_off;
+  float* slab;
+  unsigned* ctr;
+};
+
+struct CaFwdLds {
+  f16 wo[E * D];
+  bf16 vimg[MAXK * D];            // V rows of the head (24 KB)
+  float x1[E];
+  float pp[4][16 * 64];
+  float q[D];
+  float ps[MAXK + 64];
+  float opart[4][D];
+  float ctx[D];
+  float part[E];
+  float red2[4];
+  unsigned last;
+};
+
+__global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
+  __shared__ __attribute__((aligned(16))) CaFwdLds L;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int Lk = p.kv.lk1 + p.kv.lk2;
+  float4 xr = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < E / 4) xr = *reinterpret_cast<const float4*>(p.x1p + (long long)b * E + 4 * t);
+  uint4 wr[NRI];
+  rows_load(p.wq, h * D + wave * WROWS, lane, wr);
+  // key row of thread t (registers) and the head's V rows (LDS, 8 rows per DMA instruction)
+  const bool live = t < Lk;
+  uint4 kr[8];
+  {
+    const bf16* kp = kv_row(p.kv, b, live ? t : 0, h);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) kr[c] = *reinterpret_cast<const uint4*>(kp + 8 * c);
+  }
+  const float bqv = t < D ? p.bq[h * D + t] : 0.f;
+  {
+    const uint32_t vb = dec_lds_addr(L.vimg);
+    for (int ins = wave; ins * 8 < Lk; ins += 4) {
+      const int j = min(ins * 8 + (lane >> 3), Lk - 1);
+      const bf16* vp = kv_row(p.kv, b, j, h) + p.kv.v_off + (lane & 7) * 8;
+      dec_glds_p(vp, vb + (uint32_t)ins * 1024u);
+    }
+  }
+  slice_dma(p.wo, h, L.wo, wave, lane);
+  float mu, rs;
+  ln_row_fwd(xr, p.g1, p.b1, p.eps, L.x1, L.red2, t, lane, wave, mu, rs);
+  if (h == 0) {
+    if (t < E / 4) *reinterpret_cast<float4*>(p.x1_out + (long long)b * E + 4 * t) = *reinterpret_cast<const float4*>(L.x1 + 4 * t);
+    if (t == 0) {
+      p.mean_out[b] = mu;
+      p.rstd_out[b] = rs;
+    }
+  }
+  __syncthreads();
+  rows_gemv(wr, L.x1, L.pp[wave], L.q + wave * WROWS, lane);
+  __syncthreads();
+  if (t < D) {
+    const float q = L.q[t] + bqv;
+    p.q_out[(long long)b * E + h * D + t] = q;
+    L.q[t] = q * 0.125f;   // head_dim^-0.5
+  }
+  __syncthreads();
+  // scores, softmax (natural log), dropout on the probabilities
+  float sc = 0.f;
+  if (live) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const unsigned w4[4] = {kr[c].x, kr[c].y, kr[c].z, kr[c].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sc += bfbits2f((unsigned short)(w4[e] & 0xFFFFu)) * L.q[8 * c + 2 * e];
+        sc += bfbits2f((unsigned short)(w4[e] >> 16)) * L.q[8 * c + 2 * e + 1];
+      }
+    }
+  }
+  const float m = block_max4(live ? sc : -1.0e30f, L.red2, lane, wave);
+  const float pe = live ? __expf(sc - m) : 0.f;
+  const float s = block_sum4(pe, L.red2, lane, wave);
+  const uint64_t seed2 = lrce_seed(p.seed, p.rng_off);
+  float pf = pe;
+  if (live && p.p > 0.f) pf = drop1(pe, p.p, seed2, ((long long)b * H + h) * Lk + t);
+  L.ps[t] = live ? pf : 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // V rows and the W_o slice have landed
+  __syncthreads();
+  // ctx = sum_j p_j V_j / s: lane = head dim, wave w takes keys w, w+4, ...
+  {
+    float o0 = 0.f, o1 = 0.f;
+    int j = wave;
+    for (; j + 4 < Lk; j += 8) {
+      o0 += L.ps[j] * bf2f(L.vimg[j * D + lane]);
+      o1 += L.ps[j + 4] * bf2f(L.vimg[(j + 4) * D + lane]);
+    }
+    if (j < Lk) o0 += L.ps[j] * bf2f(L.vimg[j * D + lane]);
+    L.opart[wave][lane] = o0 + o1;
+  }
+  __syncthreads();
+  if (t < D) {
+    const float c = ((L.opart[0][t] + L.opart[1][t]) + (L.opart[2][t] + L.opart[3][t])) / s;
+    L.ctx[t] = c;
+    p.ctx_out[(long long)b * E + h * D + t] = c;
+    if (t == 0) p.lse_out[(long long)b * H + h] = m + __logf(s);
+  }
+  __syncthreads();
+  slice_gemv(L.wo, L.ctx, L.part, wave, lane);
+  __syncthreads();
+  if (!publish_partial(L.part, p.slab, p.ctr, b, h, t, &L.last)) return;
+  const uint64_t seed3 = lrce_seed(p.seed + 1, p.rng_off);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    float y = gather_partials(p.slab, b, n) + p.bo[n];
+    if (p.p > 0.f) y = drop1(y, p.p, seed3, (long long)b * E + n);
+    p.x2p[(long long)b * E + n] = L.x1[n] + y;
+  }
+  if (t == 0) __hip_atomic_store(&p.ctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------ cross-attention block backward
+struct CaBwdP {
+  int B;
+  const float* dx2;               // [B][768] gradient of x2 = LN2(x2p)
+  const float* x2p;
+  const float* mean2;
+  const float* rstd2;
+  const float* g2;
+  float* dcao_out;                // [B][768] dropout_bwd(dx2p): the out_proj's output gradient (h == 0)
+  const f16* wo;                  // out_proj [768][768]
+  KvP kv;
+  const float* q;                 // [B][768] (unscaled)
+  const float* ctx;               // [B][768]
+  const float* lse;               // [B][12]
+  float* dq_out;                  // [B][768]
+  float* dk1;                     // video dK (dV at + dv_off): row (b/bdiv1)*dstride1 + j*dld1
+  long long dstride1, dld1;
+  int dkv1_atomic;                // rows shared by bdiv1 > 1 query rows: atomics, else stores
+  float* dk2;                     // text dK, accumulated (one writer per row)
+  long long dstride2, dld2;
+  long long dv_off;
+  const f16* wq;                  // in_proj rows 0..E
+  float* dx1_out;                 // [B][768] = dx2p + W_q^T dq
+  float p;
+  uint64_t seed;                  // layer seed + 2 (attention dropout); + 1 = the out dropout (seed + 3)
+  const uint64_t* rng_off;
+  float* slab;
+  unsigned* ctr;
+};
+
+struct CaBwdLds {
+  f16 wo[E * D];
+  union {
+    bf16 kimg[MAXK * D];          // K rows of the head (dead once dq / dK / dV are done)
+    float acc[4][E];              // then: per-wave dX partials
+  };
+  bf16 vimg[MAXK * D];
+  float dx2p[E];
+  float dcao[E];
+  float red64[4][D];
+  float dctx[D];
+  float q[D];
+  float dq[D];
+  float ps[MAXK + 64];
+  float dss[MAXK + 64];
+  float red2[4];
+  unsigned last;
+};
+
+__global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
+  __shared__ __attribute__((aligned(16))) CaBwdLds L;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int Lk = p.kv.lk1 + p.kv.lk2;
+  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy;
+  if (t < E / 4) {
+    dy = *reinterpret_cast<const float4*>(p.dx2 + (long long)b * E + 4 * t);
+    xr = *reinterpret_cast<const float4*>(p.x2p + (long long)b * E + 4 * t);
+  }
+  const float mu = p.mean2[b], rs = p.rstd2[b];
+  uint4 wr[NRI];
+  rows_load(p.wq, h * D + wave * WROWS, lane, wr);
+  float qd = 0.f, od = 0.f;
+  if (t < D) {
+    qd = p.q[(long long)b * E + h * D + t];
+    od = p.ctx[(long long)b * E + h * D + t];
+  }
+  const float lse = p.lse[(long long)b * H + h];
+  {
+    const uint32_t kb = dec_lds_addr(L.kimg), vb = dec_lds_addr(L.vimg);
+    for (int ins = wave; ins * 8 < Lk; ins += 4) {
+      const int j = min(ins * 8 + (lane >> 3), Lk - 1);
+      const bf16* kp = kv_row(p.kv, b, j, h) + (lane & 7) * 8;
+      dec_glds_p(kp, kb + (uint32_t)ins * 1024u);
+      dec_glds_p(kp + p.kv.v_off, vb + (uint32_t)ins * 1024u);
+    }
+  }
+  slice_dma(p.wo, h, L.wo, wave, lane);
+  // LN2 backward, then the out dropout's backward (seed + 3 of the layer = p.seed + 1)
+  const float4 dx = ln_row_bwd(dy, xr, mu, rs, p.g2, L.red2, t, lane, wave);
+  const uint64_t seed3 = lrce_seed(p.seed + 1, p.rng_off);
+  if (t < E / 4) {
+    *reinterpret_cast<float4*>(L.dx2p + 4 * t) = dx;
+    float4 d = dx;
+    if (p.p > 0.f) {
+      const long long e = (long long)b * E + 4 * t;
+      d = make_float4(drop1(dx.x, p.p, seed3, e), drop1(dx.y, p.p, seed3, e + 1), drop1(dx.z, p.p, seed3, e + 2),
+                      drop1(dx.w, p.p, seed3, e + 3));
+    }
+    *reinterpret_cast<float4*>(L.dcao + 4 * t) = d;
+    if (h == 0) *reinterpret_cast<float4*>(p.dcao_out + (long long)b * E + 4 * t) = d;
+  }
+  if (t < D) L.q[t] = qd * 0.125f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // dctx = W_o[:, h]^T dcao
+  slice_gemv_t(L.wo, L.dcao, &L.red64[0][0], wave, lane);
+  __syncthreads();
+  float dod = 0.f;
+  if (t < D) {
+    dod = (L.red64[0][t] + L.red64[1][t]) + (L.red64[2][t] + L.red64[3][t]);
+    L.dctx[t] = dod;
+  }
+  const float delta = block_sum4(dod * od, L.red2, lane, wave);   // also publishes L.q / L.dctx
+  // per key: P, dropout factor, dP, dS
+  const bool live = t < Lk;
+  float pf = 0.f, ds = 0.f;
+  if (live) {
+    float sc = 0.f, dp = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint4 ku = *reinterpret_cast<const uint4*>(L.kimg + t * D + 8 * c);
+      const uint4 vu = *reinterpret_cast<const uint4*>(L.vimg + t * D + 8 * c);
+      const unsigned k4[4] = {ku.x, ku.y, ku.z, ku.w}, v4[4] = {vu.x, vu.y, vu.z, vu.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sc += bfbits2f((unsigned short)(k4[e] & 0xFFFFu)) * L.q[8 * c + 2 * e] +
+              bfbits2f((unsigned short)(k4[e] >> 16)) * L.q[8 * c + 2 * e + 1];
+        dp += bfbits2f((unsigned short)(v4[e] & 0xFFFFu)) * L.dctx[8 * c + 2 * e] +
+              bfbits2f((unsigned short)(v4[e] >> 16)) * L.dctx[8 * c + 2 * e + 1];
+      }
+    }
+    const float pr = __expf(sc - lse);
+    float f = 1.f;
+    if (p.p > 0.f) f = lrce_uniform(lrce_seed(p.seed, p.rng_off), (uint64_t)(((long long)b * H + h) * Lk + t)) >= p.p
+                           ? 1.0f / (1.0f - p.p) : 0.f;
+    pf = pr * f;
+    ds = pr * (f * dp - delta);
+  }
+  L.ps[t] = pf;
+  L.dss[t] = ds;
+  __syncthreads();
+  // dq (lane = dim), dK / dV rows: wave w takes keys w, w+4, ...
+  {
+    const float qs = L.q[lane], g = L.dctx[lane];
+    float dq0 = 0.f;
+    for (int j = wave; j < Lk; j += 4) {
+      const float dsj = L.dss[j], pj = L.ps[j];
+      dq0 += dsj * bf2f(L.kimg[j * D + lane]);
+      float* dk;
+      long long o;
+      bool atom;
+      if (j < p.kv.lk1) {
+        o = (long long)(b / p.kv.bdiv1) * p.dstride1 + (long long)j * p.dld1 + h * D + lane;
+        dk = p.dk1;
+        atom = p.dkv1_atomic;
+      } else {
+        o = (long long)(b / p.kv.bdiv2) * p.dstride2 + (long long)(j - p.kv.lk1) * p.dld2 + h * D + lane;
+        dk = p.dk2;
+        atom = false;
+      }
+      if (atom) {
+        __hip_atomic_fetch_add(dk + o, dsj * qs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(dk + o + p.dv_off, pj * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (j < p.kv.lk1) {   // one writer, first contribution: store
+        dk[o] = dsj * qs;
+        dk[o + p.dv_off] = pj * g;
+      } else {                      // text rows accumulate over the recurrent steps
+        dk[o] += dsj * qs;
+        dk[o + p.dv_off] += pj * g;
+      }
+    }
+    L.red64[wave][lane] = dq0;
+  }
+  __syncthreads();
+  if (t < D) {
+    const float dq = ((L.red64[0][t] + L.red64[1][t]) + (L.red64[2][t] + L.red64[3][t])) * 0.125f;
+    L.dq[t] = dq;
+    p.dq_out[(long long)b * E + h * D + t] = dq;
+  }
+  __syncthreads();
+  // dx1 partial = W_q[h]^T dq
+  rows_gemv_t(wr, L.dq + wave * WROWS, L.acc[wave], lane);
+  __syncthreads();
+  float* part = &L.acc[0][0];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    part[n] = (L.acc[0][n] + L.acc[1][n]) + (L.acc[2][n] + L.acc[3][n]);
+  }
+  __syncthreads();
+  if (!publish_partial(part, p.slab, p.ctr, b, h, t, &L.last)) return;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    p.dx1_out[(long long)b * E + n] = L.dx2p[n] + gather_partials(p.slab, b, n);
+  }
+  if (t == 0) __hip_atomic_store(&p.ctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------ self-attention block backward
+struct SaBwdP {
+  int B;
+  const float* dx1;               // [B][768] gradient of x1 = LN1(x1p)
+  const float* x1p;
+  const float* mean1;
+  const float* rstd1;
+  const float* g1;
+  float* dsao_out;                // [B][768] out_proj output gradient (h == 0)
+  const f16* wo;                  // out_proj
+  float* dsav_out;                // [B][768] v_proj output gradient (after the head mask)
+  const f16* wv;                  // in_proj rows 2E..3E
+  float* dx0_out;                 // [B][768] = dx1p + W_v^T dsav
+  float p;
+  uint64_t seed;                  // layer seed (head mask); + 1 = out dropout
+  const uint64_t* rng_off;
+  float* slab;
+  unsigned* ctr;
+};
+
+struct SaBwdLds {
+  f16 wo[E * D];
+  float dx1p[E];
+  float dsao[E];
+  float red64[4][D];
+  float dsav[D];
+  float acc[4][E];
+  float red2[4];
+  unsigned last;
+};
+
+__global__ void __launch_bounds__(NT, 1) dec_sa_bwd_kernel(SaBwdP p) {
+  __shared__ __attribute__((aligned(16))) SaBwdLds L;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy;
+  if (t < E / 4) {
+    dy = *reinterpret_cast<const float4*>(p.dx1 + (long long)b * E + 4 * t);
+    xr = *reinterpret_cast<const float4*>(p.x1p + (long long)b * E + 4 * t);
+  }
+  const float mu = p.mean1[b], rs = p.rstd1[b];
+  uint4 wr[NRI];
+  rows_load(p.wv, h * D + wave * WROWS, lane, wr);
+  slice_dma(p.wo, h, L.wo, wave, lane);
+  const float4 dx = ln_row_bwd(dy, xr, mu, rs, p.g1, L.red2, t, lane, wave);
+  const uint64_t seed1 = lrce_seed(p.seed + 1, p.rng_off);
+  if (t < E / 4) {
+    *reinterpret_cast<float4*>(L.dx1p + 4 * t) = dx;
+    float4 d = dx;
+    if (p.p > 0.f) {
+      const long long e = (long long)b * E + 4 * t;
+      d = make_float4(drop1(dx.x, p.p, seed1, e), drop1(dx.y, p.p, seed1, e + 1), drop1(dx.z, p.p, seed1, e + 2),
+                      drop1(dx.w, p.p, seed1, e + 3));
+    }
+    *reinterpret_cast<float4*>(L.dsao + 4 * t) = d;
+    if (h == 0) *reinterpret_cast<float4*>(p.dsao_out + (long long)b * E + 4 * t) = d;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  slice_gemv_t(L.wo, L.dsao, &L.red64[0][0], wave, lane);
+  __syncthreads();
+  if (t < D) {
+    float v = (L.red64[0][t] + L.red64[1][t]) + (L.red64[2][t] + L.red64[3][t]);
+    if (p.p > 0.f) v = drop1(v, p.p, lrce_seed(p.seed, p.rng_off), ((long long)b * E + h * D + t) / D);
+    L.dsav[t] = v;
+    p.dsav_out[(long long)b * E + h * D + t] = v;
+  }
+  __syncthreads();
+  rows_gemv_t(wr, L.dsav + wave * WROWS, L.acc[wave], lane);
+  __syncthreads();
+  float* part = &L.acc[0][0];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    part[n] = (L.acc[0][n] + L.acc[1][n]) + (L.acc[2][n] + L.acc[3][n]);
+  }
+  __syncthreads();
+  if (!publish_partial(part, p.slab, p.ctr, b, h, t, &L.last)) return;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    p.dx0_out[(long long)b * E + n] = L.dx1p[n] + gather_partials(p.slab, b, n);
+  }
+  if (t == 0) __hip_atomic_store(&p.ctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------ deferred LayerNorm parameter grads
+// dgamma[c] += sum_r dy[r][c] (x[r][c] - mean[r]) rstd[r],  dbeta[c] += sum_r dy[r][c]  over the R = S*B
+// rows of every recurrent step (one owner per column, rows in order: deterministic).  blockIdx.y picks
+// one of up to 3 LayerNorms.
+struct LnGradP {
+  const float* dy[3];
+  const float* x[3];
+  const float* mean[3];
+  const float* rstd[3];
+  float* dgamma[3];
+  float* dbeta[3];
+  int rows;
+};
+__global__ void __launch_bounds__(256) dec_ln_grads_kernel(LnGradP p) {
+  const int c = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y;
+  if (c >= E || !p.dy[k]) return;
+  float sg = 0.f, sb = 0.f;
+  for (int r = 0; r < p.rows; ++r) {
+    const float d = p.dy[k][(long long)r * E + c];
+    sg += d * (p.x[k][(long long)r * E + c] - p.mean[k][r]) * p.rstd[k][r];
+    sb += d;
+  }
+  p.dgamma[k][c] += sg;
+  p.dbeta[k][c] += sb;
+}
+
+template <typename P>
+int launch(void (*kern)(P), const P& prm, int B, hipStream_t st, const char* what) {
+  kern<<<(unsigned)(B * H), NT, 0, st>>>(prm);
+  return lrce_check_launch(what);
+}
+
+bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int64_t lrce_dec_slab_elems(int B) { return (int64_t)B * H * E; }
+
+extern "C" int lrce_dec_sa_fwd(const LrceDecSa* a, void* stream) {
+  if (!a || !a->x_in || !a->wv || !a->bv || !a->wo || !a->bo || !a->sad || !a->x1p || !a->slab || !a->counters)
+    return lrce_fail(LRCE_E_ARG, "dec_sa_fwd: null pointer");
+  if (a->B < 1 || a->B > LRCE_DEC_MAX_ROWS) return lrce_fail(LRCE_E_ARG, "dec_sa_fwd: B=%d outside [1, %d]", a->B, LRCE_DEC_MAX_ROWS);
+  if (a->ln_gamma && (!a->ln_beta || !a->x0_out || !a->mean_out || !a->rstd_out))
+    return lrce_fail(LRCE_E_ARG, "dec_sa_fwd: the input LayerNorm needs beta, x0_out, mean_out, rstd_out");
+  if (!al16(a->x_in) || !al16(a->wv) || !al16(a->wo) || (a->x0_out && !al16(a->x0_out)) || !al16(a->x1p))
+    return lrce_fail(LRCE_E_ARG, "dec_sa_fwd: rows and weights need 16-B alignment");
+  SaFwdP p;
+  p.B = a->B; p.x_in = a->x_in; p.ln_g = a->ln_gamma; p.ln_b = a->ln_beta; p.eps = a->eps;
+  p.x0_out = a->x0_out; p.mean_out = a->mean_out; p.rstd_out = a->rstd_out;
+  p.wv = reinterpret_cast<const f16*>(a->wv); p.bv = a->bv; p.wo = reinterpret_cast<const f16*>(a->wo); p.bo = a->bo;
+  p.sad = a->sad; p.x1p = a->x1p; p.p = a->drop_p; p.seed = a->seed; p.rng_off = lrce_rng_offset();
+  p.slab = a->slab; p.ctr = a->counters;
+  return launch(dec_sa_fwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_sa_fwd");
+}
+
+static int kv_check(const LrceDecKv& kv, const char* what) {
+  if (!kv.k1 || kv.lk1 < 1 || kv.bdiv1 < 1 || (kv.lk2 > 0 && (!kv.k2 || kv.bdiv2 < 1)) || kv.lk1 + kv.lk2 > MAXK)
+    return lrce_fail(LRCE_E_ARG, "%s: memory segments (lk1=%d, lk2=%d, max %d keys)", what, kv.lk1, kv.lk2, MAXK);
+  if (!al16(kv.k1) || (kv.k2 && !al16(kv.k2)) || (kv.ld1 % 8) || (kv.stride1 % 8) || (kv.lk2 > 0 && ((kv.ld2 % 8) || (kv.stride2 % 8))) ||
+      (kv.v_off % 8))
+    return lrce_fail(LRCE_E_ARG, "%s: K/V rows need 16-B alignment", what);
+  return LRCE_OK;
+}
+static KvP kv_conv(const LrceDecKv& a) {
+  KvP k;
+  k.k1 = reinterpret_cast<const bf16*>(a.k1); k.stride1 = a.stride1; k.ld1 = a.ld1; k.bdiv1 = a.bdiv1; k.lk1 = a.lk1;
+  k.k2 = reinterpret_cast<const bf16*>(a.k2); k.stride2 = a.stride2; k.ld2 = a.ld2; k.bdiv2 = a.bdiv2 > 0 ? a.bdiv2 : 1;
+  k.lk2 = a.lk2 > 0 ? a.lk2 : 0; k.v_off = a.v_off;
+  return k;
+}
+
+extern "C" int lrce_dec_ca_fwd(const LrceDecCa* a, void* stream) {
+  if (!a || !a->x1p || !a->g1 || !a->b1 || !a->x1_out || !a->mean_out || !a->rstd_out || !a->wq || !a->bq || !a->q_out ||
+      !a->ctx_out || !a->lse_out || !a->wo || !a->bo || !a->x2p || !a->slab || !a->counters)
+    return lrce_fail(LRCE_E_ARG, "dec_ca_fwd: null pointer");
+  if (a->B < 1 || a->B > LRCE_DEC_MAX_ROWS) return lrce_fail(LRCE_E_ARG, "dec_ca_fwd: B=%d", a->B);
+  if (int rc = kv_check(a->kv, "dec_ca_fwd")) return rc;
+  if (!al16(a->x1p) || !al16(a->x1_out) || !al16(a->wq) || !al16(a->wo)) return lrce_fail(LRCE_E_ARG, "dec_ca_fwd: 16-B alignment");
+  CaFwdP p;
+  p.B = a->B; p.x1p = a->x1p; p.g1 = a->g1; p.b1 = a->b1; p.eps = a->eps; p.x1_out = a->x1_out;
+  p.mean_out = a->mean_out; p.rstd_out = a->rstd_out; p.wq = reinterpret_cast<const f16*>(a->wq); p.bq = a->bq;
+  p.kv = kv_conv(a->kv); p.q_out = a->q_out; p.ctx_out = a->ctx_out; p.lse_out = a->lse_out;
+  p.wo = reinterpret_cast<const f16*>(a->wo); p.bo = a->bo; p.x2p = a->x2p; p.p = a->drop_p; p.seed = a->seed;
+  p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters;
+  return launch(dec_ca_fwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_ca_fwd");
+}
+
+extern "C" int lrce_dec_ca_bwd(const LrceDecCaBwd* a, void* stream) {
+  if (!a || !a->dx2 || !a->x2p || !a->mean2 || !a->rstd2 || !a->g2 || !a->dcao_out || !a->wo || !a->q || !a->ctx || !a->lse ||
+      !a->dq_out || !a->dk1 || !a->wq || !a->dx1_out || !a->slab || !a->counters)
+    return lrce_fail(LRCE_E_ARG, "dec_ca_bwd: null pointer");
+  if (a->B < 1 || a->B > LRCE_DEC_MAX_ROWS) return lrce_fail(LRCE_E_ARG, "dec_ca_bwd: B=%d", a->B);
+  if (int rc = kv_check(a->kv, "dec_ca_bwd")) return rc;
+  if (a->kv.lk2 > 0 && !a->dk2) return lrce_fail(LRCE_E_ARG, "dec_ca_bwd: text segment without dk2");
+  if (!al16(a->dx2) || !al16(a->x2p) || !al16(a->wq) || !al16(a->wo) || !al16(a->dcao_out))
+    return lrce_fail(LRCE_E_ARG, "dec_ca_bwd: 16-B alignment");
+  CaBwdP p;
+  p.B = a->B; p.dx2 = a->dx2; p.x2p = a->x2p; p.mean2 = a->mean2; p.rstd2 = a->rstd2; p.g2 = a->g2;
+  p.dcao_out = a->dcao_out; p.wo = reinterpret_cast<const f16*>(a->wo); p.kv = kv_conv(a->kv); p.q = a->q; p.ctx = a->ctx;
+  p.lse = a->lse; p.dq_out = a->dq_out; p.dk1 = a->dk1; p.dstride1 = a->dstride1; p.dld1 = a->dld1;
+  p.dkv1_atomic = a->kv.bdiv1 > 1; p.dk2 = a->dk2; p.dstride2 = a->dstride2; p.dld2 = a->dld2; p.dv_off = a->dv_off;
+  p.wq = reinterpret_cast<const f16*>(a->wq); p.dx1_out = a->dx1_out; p.p = a->drop_p; p.seed = a->seed;
+  p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters;
+  return launch(dec_ca_bwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_ca_bwd");
+}
+
+extern "C" int lrce_dec_sa_bwd(const LrceDecSaBwd* a, void* stream) {
+  if (!a || !a->dx1 || !a->x1p || !a->mean1 || !a->rstd1 || !a->g1 || !a->dsao_out || !a->wo || !a->dsav_out || !a->wv ||
+      !a->dx0_out || !a->slab || !a->counters)
+    return lrce_fail(LRCE_E_ARG, "dec_sa_bwd: null pointer");
+  if (a->B < 1 || a->B > LRCE_DEC_MAX_ROWS) return lrce_fail(LRCE_E_ARG, "dec_sa_bwd: B=%d", a->B);
+  if (!al16(a->dx1) || !al16(a->x1p) || !al16(a->wv) || !al16(a->wo) || !al16(a->dsao_out))
+    return lrce_fail(LRCE_E_ARG, "dec_sa_bwd: 16-B alignment");
+  SaBwdP p;
+  p.B = a->B; p.dx1 = a->dx1; p.x1p = a->x1p; p.mean1 = a->mean1; p.rstd1 = a->rstd1; p.g1 = a->g1;
+  p.dsao_out = a->dsao_out; p.wo = reinterpret_cast<const f16*>(a->wo); p.dsav_out = a->dsav_out;
+  p.wv = reinterpret_cast<const f16*>(a->wv); p.dx0_out = a->dx0_out; p.p = a->drop_p; p.seed = a->seed;
+  p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters;
+  return launch(dec_sa_bwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_sa_bwd");
+}
+
+extern "C" int lrce_dec_ln_grads(const float* const* dy, const float* const* x, const float* const* mean,
+                                 const float* const* rstd, float* const* dgamma, float* const* dbeta, int n_ln, int rows,
+                                 void* stream) {
+  if (n_ln < 1 || n_ln > 3 || rows < 1) return lrce_fail(LRCE_E_ARG, "dec_ln_grads: n_ln=%d rows=%d", n_ln, rows);
+  LnGradP p{};
+  for (int k = 0; k < n_ln; ++k) {
+    if (!dy[k] || !x[k] || !mean[k] || !rstd[k] || !dgamma[k] || !dbeta[k]) return lrce_fail(LRCE_E_ARG, "dec_ln_grads: null pointer");
+    p.dy[k] = dy[k]; p.x[k] = x[k]; p.mean[k] = mean[k]; p.rstd[k] = rstd[k]; p.dgamma[k] = dgamma[k]; p.dbeta[k] = dbeta[k];
+  }
+  p.rows = rows;
+  dec_ln_grads_kernel<<<dim3((E + 255) / 256, n_ln), 256, 0, static_cast<hipStream_t>(stream)>>>(p);
+  return lrce_check_launch("dec_ln_grads");
+}

@@ -320,10 +320,13 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restri
 // Relative-position-bias gradient: the table row of (query i, key j) is a linear function of the
 // token codes, code(i) - code(j) + off (video_swin_ori.py:133-148 with window (wd, wh, ww)), so dS is
 // binned in LDS by that difference and each (window, head) writes n_bins floats (3.4 KB at 3x7x7)
-// instead of its 160^2 dS image.  The bins are 2^-40 fixed-point int64 (ds_add_u64): integer adds
-// make the sum independent of wave timing, and measured on gfx950 (tools/lds_atomic_bench.hip) an LDS
-// u64 add costs ~9 cycles per wave instruction against ~230 for ds_add_f32.  lrce_wattn_dbias sums
-// the windows in a fixed order and scatters bins to table rows.
+// instead of its 160^2 dS image.  The bins are fixed-point int64 (ds_add_u64): integer adds make the
+// sum independent of wave timing, and measured on gfx950 (tools/lds_atomic_bench.hip) an LDS u64 add
+// costs ~9 cycles per wave instruction against ~230 for ds_add_f32.  The fixed point is scaled per
+// (window, head) by 2^s from a bound on |dS| (|dS_ij| = P_ij |dP_ij - delta_i| <= 2 max|dP| <=
+// 2 max_i |dO_i| max_j |V_j|, so |dS| 2^s < 2^50 and a bin of <= 160 terms stays below 2^58): the
+// quantum follows the gradient's magnitude (an absolute 2^-40 lost batch-mean-sized gradients).
+// lrce_wattn_dbias sums the windows in a fixed order and scatters bins to table rows.
 constexpr int BW = 5;        // waves per backward workgroup (= tiles of 32 rows)
 constexpr int NBMAX = 1024;  // relative-position bins per head held in LDS
 constexpr int WCH = 32;      // window chunks of the deterministic bias-gradient reduction
@@ -333,8 +336,9 @@ struct BwdLds {
   bf16 dout[NPAD * HD];
   bf16 k[NPAD * HD];
   bf16 ds[2][BW][TQ * TQ];
-  unsigned long long bins[NBMAX];   // 2^-40 fixed point
+  unsigned long long bins[NBMAX];   // 2^s fixed point
   float4 qinfo[NPAD];   // per query: lse, delta, token code (as bits), -
+  float nmax[BW][2];    // per wave: max |dO_q|^2, max |V_q|^2 over its rows (the bins' scale)
 };
 
 template <bool BH>
@@ -378,7 +382,9 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
   bf16x8 vf[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) vf[s] = key < n ? ld_row16(base + key * ld + 2 * C + h * HD + 16 * s + 8 * hh) : bf16x8{};
-  // delta[q] = dO[q] . O[q], lse[q] (0 past n: padded queries contribute nothing), token codes
+  // delta[q] = dO[q] . O[q], lse[q] (0 past n: padded queries contribute nothing), token codes;
+  // |dO_q|^2 and |V_q|^2 for the bins' scale
+  float dn2 = 0.f, vn2 = 0.f;
   if (threadIdx.x < NPAD) {
     const int q = threadIdx.x;
     float d = 0.f, l = 0.f;
@@ -388,16 +394,42 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
       for (int part = 0; part < 4; ++part) {
         const bf16x8 a = ld_row16(obase + (long long)q * C + part * 8);
         const bf16x8 b = ld_row16(dobase + (long long)q * C + part * 8);
+        const bf16x8 v = ld_row16(base + q * ld + 2 * C + h * HD + part * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
+        for (int j = 0; j < 8; ++j) {
+          d += bf2f(a[j]) * bf2f(b[j]);
+          dn2 += bf2f(b[j]) * bf2f(b[j]);
+          vn2 += bf2f(v[j]) * bf2f(v[j]);
+        }
       }
       l = lse_g[((long long)w * nH + h) * NPAD + q];
       code = ((q / (wh * ww)) * (2 * wh - 1) + (q / ww) % wh) * (2 * ww - 1) + q % ww;
     }
     L.qinfo[q] = make_float4(l, d, __int_as_float(code), 0.f);
   }
+  dn2 = wave_max(dn2);
+  vn2 = wave_max(vn2);
+  if (lane == 0) {
+    L.nmax[t][0] = dn2;
+    L.nmax[t][1] = vn2;
+  }
   for (int i = threadIdx.x; i < NBMAX; i += BW * 64) L.bins[i] = 0ull;
   __syncthreads();
+  // bins' scale 2^s: |dS| <= 2 max|dO| max|V| = bound < 2^e -> |dS| 2^s < 2^50 with s = 50 - e
+  double bscale, binv;
+  {
+    float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < BW; ++i) {
+      m0 = fmaxf(m0, L.nmax[i][0]);
+      m1 = fmaxf(m1, L.nmax[i][1]);
+    }
+    int e = 0;
+    (void)frexpf(2.0f * sqrtf(m0) * sqrtf(m1) * 1.0001f, &e);   // margin for the norms' own rounding
+    const int sh = 50 - e;
+    bscale = ldexp(1.0, sh);
+    binv = ldexp(1.0, -sh);
+  }
   bf16x8 kf[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) kf[s] = *reinterpret_cast<const bf16x8*>(L.k + key * HD + 16 * s + 8 * hh);
@@ -453,9 +485,9 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
     if (want_bins) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        // round(dS * 2^40) to int64: one f64 fma onto 1.5 * 2^52 leaves the integer in the low
-        // mantissa bits (exact for |dS| < 2^11)
-        const double m = __builtin_fma((double)dp[r], 0x1p40, 0x1.8p52);
+        // round(dS * 2^s) to int64: one f64 fma onto 1.5 * 2^52 leaves the integer in the low
+        // mantissa bits (exact for |dS 2^s| < 2^51)
+        const double m = __builtin_fma((double)dp[r], bscale, 0x1.8p52);
         const unsigned long long v =
             (unsigned long long)(__double_as_longlong(m) - __double_as_longlong(0x1.8p52));
         atomicAdd(&L.bins[__float_as_int(qi4[r].z) + kbin], v);
@@ -518,7 +550,7 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
   __syncthreads();   // every wave's bin adds are done
   float* dst = dbias_part + ((long long)w * nH + h) * nb;
   for (int b = threadIdx.x; b < nb; b += BW * 64)
-    dst[b] = (float)((double)(long long)L.bins[b] * 0x1p-40);
+    dst[b] = (float)((double)(long long)L.bins[b] * binv);
 }
 
 // Bias-table gradient from the per-(window, head) bin rows, no atomics: (1) WCH chunks of windows

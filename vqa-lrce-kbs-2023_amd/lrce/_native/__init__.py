@@ -81,6 +81,56 @@ class LnPrologue(ctypes.Structure):
     ]
 
 
+class DecKv(ctypes.Structure):
+    _fields_ = [
+        ("k1", ctypes.c_void_p), ("stride1", ctypes.c_int64), ("ld1", ctypes.c_int64),
+        ("bdiv1", ctypes.c_int32), ("lk1", ctypes.c_int32),
+        ("k2", ctypes.c_void_p), ("stride2", ctypes.c_int64), ("ld2", ctypes.c_int64),
+        ("bdiv2", ctypes.c_int32), ("lk2", ctypes.c_int32), ("v_off", ctypes.c_int64),
+    ]
+
+
+_WS = [("drop_p", ctypes.c_float), ("seed", ctypes.c_uint64), ("slab", ctypes.c_void_p), ("counters", ctypes.c_void_p)]
+
+
+class DecSa(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("x_in", ctypes.c_void_p), ("ln_gamma", ctypes.c_void_p), ("ln_beta", ctypes.c_void_p),
+        ("eps", ctypes.c_float), ("x0_out", ctypes.c_void_p), ("mean_out", ctypes.c_void_p), ("rstd_out", ctypes.c_void_p),
+        ("wv", ctypes.c_void_p), ("bv", ctypes.c_void_p), ("wo", ctypes.c_void_p), ("bo", ctypes.c_void_p),
+        ("sad", ctypes.c_void_p), ("x1p", ctypes.c_void_p),
+    ] + _WS
+
+
+class DecCa(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("x1p", ctypes.c_void_p), ("g1", ctypes.c_void_p), ("b1", ctypes.c_void_p),
+        ("eps", ctypes.c_float), ("x1_out", ctypes.c_void_p), ("mean_out", ctypes.c_void_p), ("rstd_out", ctypes.c_void_p),
+        ("wq", ctypes.c_void_p), ("bq", ctypes.c_void_p), ("kv", DecKv), ("q_out", ctypes.c_void_p),
+        ("ctx_out", ctypes.c_void_p), ("lse_out", ctypes.c_void_p), ("wo", ctypes.c_void_p), ("bo", ctypes.c_void_p),
+        ("x2p", ctypes.c_void_p),
+    ] + _WS
+
+
+class DecCaBwd(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("dx2", ctypes.c_void_p), ("x2p", ctypes.c_void_p), ("mean2", ctypes.c_void_p),
+        ("rstd2", ctypes.c_void_p), ("g2", ctypes.c_void_p), ("dcao_out", ctypes.c_void_p), ("wo", ctypes.c_void_p),
+        ("kv", DecKv), ("q", ctypes.c_void_p), ("ctx", ctypes.c_void_p), ("lse", ctypes.c_void_p),
+        ("dq_out", ctypes.c_void_p), ("dk1", ctypes.c_void_p), ("dstride1", ctypes.c_int64), ("dld1", ctypes.c_int64),
+        ("dk2", ctypes.c_void_p), ("dstride2", ctypes.c_int64), ("dld2", ctypes.c_int64), ("dv_off", ctypes.c_int64),
+        ("wq", ctypes.c_void_p), ("dx1_out", ctypes.c_void_p),
+    ] + _WS
+
+
+class DecSaBwd(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("dx1", ctypes.c_void_p), ("x1p", ctypes.c_void_p), ("mean1", ctypes.c_void_p),
+        ("rstd1", ctypes.c_void_p), ("g1", ctypes.c_void_p), ("dsao_out", ctypes.c_void_p), ("wo", ctypes.c_void_p),
+        ("dsav_out", ctypes.c_void_p), ("wv", ctypes.c_void_p), ("dx0_out", ctypes.c_void_p),
+    ] + _WS
+
+
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = 1, 2, 4, 8
 EPI_OUT_F32, EPI_ATOMIC, EPI_ACCUM, EPI_AUX_OUT, EPI_OUT_BOTH = 16, 32, 64, 128, 256
 EPI_BIAS_GRAD = 512
@@ -105,6 +155,11 @@ _SIGS = {
     "lrce_wattn_dbias": [_P, _I, _I, _I, _P, _P, _P],
     "lrce_mha_fwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_mha_bwd": [ctypes.POINTER(MhaDesc), _P],
+    "lrce_dec_sa_fwd": [ctypes.POINTER(DecSa), _P],
+    "lrce_dec_ca_fwd": [ctypes.POINTER(DecCa), _P],
+    "lrce_dec_ca_bwd": [ctypes.POINTER(DecCaBwd), _P],
+    "lrce_dec_sa_bwd": [ctypes.POINTER(DecSaBwd), _P],
+    "lrce_dec_ln_grads": [_P, _P, _P, _P, _P, _P, _I, _I, _P],
     "lrce_frames_resize": [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P],
     "lrce_patch_im2col": [_P, _I, _I, _I, _I, _I64, _I64, _I64, _I, _P, _P],
     "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _I, _P, _P],
@@ -130,6 +185,8 @@ _SIGS = {
 _RET = {"lrce_last_error": ctypes.c_char_p, "lrce_wattn_bias_elems": _I64, "lrce_wattn_dbias_part_elems": _I64,
         "lrce_layernorm_bwd_workspace": _I64}
 _SIGS["lrce_wattn_bias_elems"] = [_I, _I]
+_SIGS["lrce_dec_slab_elems"] = [_I]
+_RET["lrce_dec_slab_elems"] = _I64
 _SIGS["lrce_wattn_dbias_part_elems"] = [_I, _I, _I]
 _SIGS["lrce_layernorm_bwd_workspace"] = [_I, _I]
 

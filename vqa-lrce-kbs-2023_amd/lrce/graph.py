@@ -70,6 +70,11 @@ class TrainStepGraph:
         self.states = {}
         self.static = None   # static inputs of the last call (the agent reads the labels from it)
         self.copy_stream = None
+        # ONE private memory pool for every signature's graphs: a short last batch captured into a pool
+        # of its own would keep a second step's activations resident.  Sharing is safe here because
+        # no two graphs ever replay concurrently and a graph's outputs are read only right after its
+        # own replay (the blocks another signature's capture reused hold only that graph's temporaries).
+        self.pool = None
 
     def _load(self, st, inputs):
         """Batch -> the static input buffers.  Host tensors (pinned by the DataLoader) go H2D on a
@@ -112,7 +117,9 @@ class TrainStepGraph:
         torch.cuda.synchronize()
         self.optim._sync_lrs()          # no host->device copy may land inside the capture
         steps = self.optim.step_count   # the host-side count of a captured step() is not a real step
-        pool = torch.cuda.graph_pool_handle()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        pool = self.pool
         st.g_step = torch.cuda.CUDAGraph()
         if self.reducer is None:
             with torch.cuda.graph(st.g_step, pool=pool):

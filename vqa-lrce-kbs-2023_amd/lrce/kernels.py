@@ -464,6 +464,94 @@ def mha_desc(q, Lq, *, k1, v1, lk1, ld_kv1, stride_kv1_b, kv1_bdiv=1, k2=None, v
     return m
 
 
+# ---- recurrent decoder: per-head fused attention blocks (csrc/decoder.hip) -------------------------
+DEC_MAX_ROWS = 64
+_DEC_WS = {}
+
+
+def dec_workspace(device):
+    """The hand-off slab + per-row arrival counters of the fused decoder blocks (one per device; the
+    decoder runs on one stream at a time).  Allocated on first use (the eager warm-up step)."""
+    key = torch.device(device)
+    ws = _DEC_WS.get(key)
+    if ws is None:
+        slab = torch.empty(int(N.lib().lrce_dec_slab_elems(DEC_MAX_ROWS)), dtype=F32, device=key)
+        ctr = torch.zeros(DEC_MAX_ROWS, dtype=torch.int32, device=key)
+        _DEC_WS[key] = ws = (slab, ctr)
+    return ws
+
+
+def dec_kv(k1, *, stride1, ld1, bdiv1, lk1, k2=None, stride2=0, ld2=0, bdiv2=1, lk2=0, v_off):
+    """Memory K/V of one recurrent step (bf16; V at K + v_off elements): key j < lk1 of query row b
+    at k1[(b // bdiv1) * stride1 + j * ld1], the rest from k2 likewise."""
+    kv = N.DecKv()
+    kv.k1, kv.stride1, kv.ld1, kv.bdiv1, kv.lk1 = ptr(k1), stride1, ld1, bdiv1, lk1
+    kv.k2, kv.stride2, kv.ld2, kv.bdiv2, kv.lk2 = ptr(k2), stride2, ld2, bdiv2, lk2 if k2 is not None else 0
+    kv.v_off = v_off
+    kv._keep = (k1, k2)
+    return kv
+
+
+def _dec_ws(a, device, p, seed):
+    a.drop_p, a.seed = float(p), seed & (2 ** 64 - 1)
+    slab, ctr = dec_workspace(device)
+    a.slab, a.counters = ptr(slab), ptr(ctr)
+
+
+def dec_sa_fwd(x_in, wv, bv, wo, bo, *, sad, x1p, p, seed, ln=None, eps=1e-12, x0_out=None, mean_out=None, rstd_out=None):
+    """x1p = x0 + drop(out_proj(drop_head(v_proj(x0)))), x0 = LN(x_in) (ln = (gamma, beta)) or x_in."""
+    a = N.DecSa()
+    a.B, a.x_in = x_in.shape[0], ptr(x_in)
+    if ln is not None:
+        a.ln_gamma, a.ln_beta, a.eps = ptr(ln[0]), ptr(ln[1]), float(eps)
+        a.x0_out, a.mean_out, a.rstd_out = ptr(x0_out), ptr(mean_out), ptr(rstd_out)
+    a.wv, a.bv, a.wo, a.bo, a.sad, a.x1p = ptr(wv), ptr(bv), ptr(wo), ptr(bo), ptr(sad), ptr(x1p)
+    _dec_ws(a, x_in.device, p, seed)
+    _timed("decoder", x1p, lambda: call("lrce_dec_sa_fwd", ctypes.byref(a), stream_of(x1p)))
+
+
+def dec_ca_fwd(x1p, g1, b1, wq, bq, kv, wo, bo, *, x1_out, mean_out, rstd_out, q_out, ctx_out, lse_out, x2p, p, seed,
+               eps=1e-12):
+    """x1 = LN1(x1p); ctx = attention(W_q x1 + b_q, memory); x2p = x1 + drop(out_proj(ctx)).  seed: the
+    attention-dropout seed (the layer's seed + 2)."""
+    a = N.DecCa()
+    a.B, a.x1p, a.g1, a.b1, a.eps = x1p.shape[0], ptr(x1p), ptr(g1), ptr(b1), float(eps)
+    a.x1_out, a.mean_out, a.rstd_out = ptr(x1_out), ptr(mean_out), ptr(rstd_out)
+    a.wq, a.bq, a.kv = ptr(wq), ptr(bq), kv
+    a.q_out, a.ctx_out, a.lse_out = ptr(q_out), ptr(ctx_out), ptr(lse_out)
+    a.wo, a.bo, a.x2p = ptr(wo), ptr(bo), ptr(x2p)
+    _dec_ws(a, x1p.device, p, seed)
+    _timed("decoder", x2p, lambda: call("lrce_dec_ca_fwd", ctypes.byref(a), stream_of(x2p)))
+
+
+def dec_ca_bwd(dx2, x2p, mean2, rstd2, g2, wo, kv, q, ctx, lse, wq, *, dcao_out, dq_out, dk1, dstride1, dld1, dx1_out, p,
+               seed, dk2=None, dstride2=0, dld2=0, dv_off):
+    a = N.DecCaBwd()
+    a.B, a.dx2, a.x2p, a.mean2, a.rstd2, a.g2 = dx2.shape[0], ptr(dx2), ptr(x2p), ptr(mean2), ptr(rstd2), ptr(g2)
+    a.dcao_out, a.wo, a.kv, a.q, a.ctx, a.lse = ptr(dcao_out), ptr(wo), kv, ptr(q), ptr(ctx), ptr(lse)
+    a.dq_out, a.dk1, a.dstride1, a.dld1 = ptr(dq_out), ptr(dk1), dstride1, dld1
+    a.dk2, a.dstride2, a.dld2, a.dv_off = ptr(dk2), dstride2, dld2, dv_off
+    a.wq, a.dx1_out = ptr(wq), ptr(dx1_out)
+    _dec_ws(a, dx2.device, p, seed)
+    _timed("decoder", dx1_out, lambda: call("lrce_dec_ca_bwd", ctypes.byref(a), stream_of(dx1_out)))
+
+
+def dec_sa_bwd(dx1, x1p, mean1, rstd1, g1, wo, wv, *, dsao_out, dsav_out, dx0_out, p, seed):
+    a = N.DecSaBwd()
+    a.B, a.dx1, a.x1p, a.mean1, a.rstd1, a.g1 = dx1.shape[0], ptr(dx1), ptr(x1p), ptr(mean1), ptr(rstd1), ptr(g1)
+    a.dsao_out, a.wo, a.dsav_out, a.wv, a.dx0_out = ptr(dsao_out), ptr(wo), ptr(dsav_out), ptr(wv), ptr(dx0_out)
+    _dec_ws(a, dx1.device, p, seed)
+    _timed("decoder", dx0_out, lambda: call("lrce_dec_sa_bwd", ctypes.byref(a), stream_of(dx0_out)))
+
+
+def dec_ln_grads(items, rows):
+    """items: up to 3 (dy, x, mean, rstd, dgamma, dbeta) over `rows` rows of 768: dgamma += sum dy xhat,
+    dbeta += sum dy (LayerNorm parameter gradients of every recurrent step at once)."""
+    n = len(items)
+    arr = [(ctypes.c_void_p * 3)(*([ptr(it[k]) for it in items] + [None] * (3 - n))) for k in range(6)]
+    call("lrce_dec_ln_grads", *[ctypes.cast(a, ctypes.c_void_p) for a in arr], n, rows, stream_of(items[0][4]))
+
+
 def mha_fwd(desc, stream_tensor):
     call("lrce_mha_fwd", ctypes.byref(desc), stream_of(stream_tensor))
 

@@ -16,6 +16,7 @@ Execution re-design (same math):
   backward and the projection weight gradients are taken once per layer.
 `texts_attention_mask` is accepted and ignored exactly like the reference (no key-padding mask).
 """
+import os
 from typing import Iterable, List
 
 import torch
@@ -117,27 +118,41 @@ def _wq(lay, w):
 class _Step:
     """Saved activations of one (step, layer).  m3 / r3 (the stats of this layer's norm3) are written
     by the launch that consumes LN3's output: the next layer's first GEMM, or the step tail."""
-    __slots__ = ("x1p", "m1", "r1", "q", "ctx", "lse", "desc", "x2p", "m2", "r2", "pre", "x3p", "m3", "r3")
+    __slots__ = ("x1p", "m1", "r1", "q", "ctx", "lse", "desc", "kv", "x2p", "m2", "r2", "pre", "x3p", "m3", "r3")
 
 
 class _LayerActs:
     """Per-layer [S, Bq, .] buffers of the query-side GEMM inputs of every recurrent step: the
     forward writes step i's activations into row block i, so the weight gradients of all S steps
-    are ONE GEMM per weight after the backward sweep (K = S*Bq) instead of S small ones."""
-    __slots__ = ("x0", "sad", "x1", "ctx", "x2", "gd")
+    are ONE GEMM per weight after the backward sweep (K = S*Bq) instead of S small ones.  x1p / x2p and
+    their LayerNorm statistics likewise feed the norm1 / norm2 parameter gradients of all steps at once
+    (the fused attention blocks)."""
+    __slots__ = ("x0", "sad", "x1", "ctx", "x2", "gd", "x1p", "x2p", "m1", "r1", "m2", "r2")
 
     def __init__(self, S, Bq, dev):
         for name in self.__slots__:
-            setattr(self, name, torch.empty(S, Bq, FF if name == "gd" else E, device=dev))
+            shape = (S, Bq) if name in ("m1", "r1", "m2", "r2") else (S, Bq, FF if name == "gd" else E)
+            setattr(self, name, torch.empty(*shape, device=dev))
 
 
 class _LayerGrads:
-    """Per-layer [S, Bq, .] buffers of the matching output gradients (dY of each query-side GEMM)."""
-    __slots__ = ("df", "dgp", "dcao", "dq", "dsao", "dsav")
+    """Per-layer [S, Bq, .] buffers of the matching output gradients (dY of each query-side GEMM), and
+    (fused blocks) the norm1 / norm2 output gradients."""
+    __slots__ = ("df", "dgp", "dcao", "dq", "dsao", "dsav", "dln1", "dln2")
 
     def __init__(self, S, Bq, dev):
         for name in self.__slots__:
             setattr(self, name, torch.empty(S, Bq, FF if name == "dgp" else E, device=dev))
+
+
+def _fused_ok(lay, Bq, Lt):
+    """The per-head fused attention blocks (csrc/decoder.hip) need the fp16 weight shadow, <= 64 query
+    rows and <= 192 memory keys; LRCE_DEC_FUSED=0 selects the unfused launches (A/B, tests)."""
+    if os.environ.get("LRCE_DEC_FUSED", "1") == "0":
+        return False
+    flat = getattr(lay, "_lrce_flat", None)
+    return (flat is not None and flat.has_f16(lay.self_attn.in_proj_weight) and flat.has_f16(lay.multihead_attn.in_proj_weight)
+            and Bq <= K.DEC_MAX_ROWS and 150 + Lt <= 192)
 
 
 def _layer_fwd(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_prev):
@@ -155,7 +170,10 @@ def _layer_fwd(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_pr
     Bq = x_in.shape[0]
     dev = x_in.device
     st = _Step()
+    st.kv = None
     x0 = acts.x0[step]
+    if _fused_ok(lay, Bq, Lt):
+        return _layer_fwd_fused(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_prev, st)
     # self-attention over one token: out_proj(dropout_head(v_proj(x0)))
     if prev is None:
         sad = K.linear(x_in, _wq(lay, sa.in_proj_weight)[2 * E:], sa.in_proj_bias[2 * E:], out=acts.sad[step],
@@ -193,12 +211,71 @@ def _layer_fwd(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_pr
     return st
 
 
+def _layer_fwd_fused(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_prev, st):
+    """_layer_fwd with each attention block as ONE launch of Bq x 12 workgroups (csrc/decoder.hip):
+    [prev norm3 ->] v_proj -> head dropout -> out_proj (+ dropout, residual), then norm1 -> q_proj ->
+    cross-attention -> out_proj (+ dropout, residual); the FFN as before."""
+    sa, ca = lay.self_attn, lay.multihead_attn
+    Bq = x_in.shape[0]
+    wsa, wca = _wq(lay, sa.in_proj_weight), _wq(lay, ca.in_proj_weight)
+    if prev is None:
+        K.dec_sa_fwd(x_in, wsa[2 * E:], sa.in_proj_bias[2 * E:], _wq(lay, sa.out_proj.weight), sa.out_proj.bias,
+                     sad=acts.sad[step], x1p=acts.x1p[step], p=p, seed=seed)
+    else:
+        st_prev.m3 = torch.empty(Bq, device=x_in.device)
+        st_prev.r3 = torch.empty(Bq, device=x_in.device)
+        K.dec_sa_fwd(x_in, wsa[2 * E:], sa.in_proj_bias[2 * E:], _wq(lay, sa.out_proj.weight), sa.out_proj.bias,
+                     sad=acts.sad[step], x1p=acts.x1p[step], p=p, seed=seed, ln=(prev.norm3.weight, prev.norm3.bias), eps=EPS,
+                     x0_out=acts.x0[step], mean_out=st_prev.m3, rstd_out=st_prev.r3)
+    st.x1p, st.m1, st.r1 = acts.x1p[step], acts.m1[step], acts.r1[step]
+    lv = 150
+    st.kv = K.dec_kv(kvv[step * lv * 2 * E:], stride1=S * lv * 2 * E, ld1=2 * E, bdiv1=nmc, lk1=lv,
+                     k2=kvt if Lt else None, stride2=Lt * 2 * E, ld2=2 * E, bdiv2=1, lk2=Lt, v_off=E)
+    st.q = torch.empty(Bq, E, device=x_in.device)
+    st.ctx = acts.ctx[step]
+    st.lse = torch.empty(Bq, NHEAD, 1, device=x_in.device)
+    K.dec_ca_fwd(st.x1p, lay.norm1.weight, lay.norm1.bias, wca[:E], ca.in_proj_bias[:E], st.kv, _wq(lay, ca.out_proj.weight),
+                 ca.out_proj.bias, x1_out=acts.x1[step], mean_out=st.m1, rstd_out=st.r1, q_out=st.q, ctx_out=st.ctx,
+                 lse_out=st.lse, x2p=acts.x2p[step], p=p, seed=seed + 2, eps=EPS)
+    st.x2p, st.m2, st.r2 = acts.x2p[step], acts.m2[step], acts.r2[step]
+    x2 = acts.x2[step]
+    pro = K.ln_fwd_prologue(lay.norm2.weight, lay.norm2.bias, EPS, mean=st.m2, rstd=st.r2, y_out=x2)
+    st.pre = torch.empty(Bq, FF, dtype=torch.bfloat16, device=x_in.device)
+    gd = K.linear(st.x2p, _wq(lay, lay.linear1.weight), lay.linear1.bias, gelu=True, pre_out=st.pre, out=acts.gd[step],
+                  drop=(p, seed + 4, 1), ln=pro)
+    st.x3p = K.linear(gd, _wq(lay, lay.linear2.weight), lay.linear2.bias, out_f32=True, resid=x2, drop=(p, seed + 5, 1))
+    return st
+
+
+def _layer_bwd_fused(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step):
+    """_layer_bwd for a step whose forward ran the fused blocks: FFN backward as before (norm3 backward
+    in linear2's dX), then the cross-attention block and the self-attention block backward as one
+    launch each.  norm1 / norm2 parameter gradients are deferred to _layer_wgrads."""
+    sa, ca = lay.self_attn, lay.multihead_attn
+    dx3p = torch.empty_like(st.x3p)
+    pro = K.ln_bwd_prologue(st.x3p, st.m3, st.r3, lay.norm3.weight, dgamma=_g(flat, lay.norm3.weight),
+                            dbeta=_g(flat, lay.norm3.bias), y_out=dx3p, y2_out=grads.df[step], drop=(p, seed + 5, 1))
+    dgp = K.linear_dx(dx3, _wq(lay, lay.linear2.weight), dgelu_pre=st.pre, out=grads.dgp[step], drop=(p, seed + 4, 1), ln=pro)
+    dx2 = K.linear_dx(dgp, _wq(lay, lay.linear1.weight), resid=dx3p, out=grads.dln2[step])
+    wsa, wca = _wq(lay, sa.in_proj_weight), _wq(lay, ca.in_proj_weight)
+    K.dec_ca_bwd(dx2, st.x2p, st.m2, st.r2, lay.norm2.weight, _wq(lay, ca.out_proj.weight), st.kv, st.q, st.ctx, st.lse,
+                 wca[:E], dcao_out=grads.dcao[step], dq_out=grads.dq[step], dk1=dkvv_step, dstride1=S * 150 * 2 * E,
+                 dld1=2 * E, dk2=dkvt if Lt else None, dstride2=Lt * 2 * E, dld2=2 * E, dv_off=E,
+                 dx1_out=grads.dln1[step], p=p, seed=seed + 2)
+    dx0 = torch.empty_like(st.x1p)
+    K.dec_sa_bwd(grads.dln1[step], st.x1p, st.m1, st.r1, lay.norm1.weight, _wq(lay, sa.out_proj.weight), wsa[2 * E:],
+                 dsao_out=grads.dsao[step], dsav_out=grads.dsav[step], dx0_out=dx0, p=p, seed=seed)
+    return dx0
+
+
 def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step):
     """Backward of _layer_fwd from dx3 = d(norm3 output).  Each LayerNorm backward (+ the dropout
     backward in front of it) is folded into the GEMM that consumes its result (lrce_gemm_ln mode 2),
     which also materialises dx (the next residual) and the dropped dx (the weight-gradient dY) and
     accumulates the LN weight / bias gradients.  Accumulates into the layer's dK/dV buffers, leaves
     the dY of its six query-side GEMMs in grads[.][step], returns d(x0)."""
+    if st.kv is not None:
+        return _layer_bwd_fused(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step)
     sa, ca = lay.self_attn, lay.multihead_attn
     dx3p = torch.empty_like(st.x3p)
     pro = K.ln_bwd_prologue(st.x3p, st.m3, st.r3, lay.norm3.weight, dgamma=_g(flat, lay.norm3.weight),
@@ -222,12 +299,19 @@ def _layer_bwd(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads, step)
     return K.linear_dx(dsav, _wq(lay, sa.in_proj_weight)[2 * E:], resid=dx1p)
 
 
-def _layer_wgrads(lay, flat, acts, grads):
+def _layer_wgrads(lay, flat, acts, grads, fused=False):
     """The six query-side weight (+bias) gradients of one layer over all S recurrent steps at once:
-    dW += dY[S*Bq, out]^T X[S*Bq, in] (one exact-f32 outer-product launch each)."""
+    dW += dY[S*Bq, out]^T X[S*Bq, in] (one exact-f32 outer-product launch each); with the fused
+    attention blocks also the norm1 / norm2 parameter gradients of all steps (one launch)."""
     sa, ca = lay.self_attn, lay.multihead_attn
     R = acts.x0.shape[0] * acts.x0.shape[1]
     v = lambda t: t.view(R, t.shape[-1])  # noqa: E731
+    if fused:
+        items = [(grads.dln1, acts.x1p, acts.m1, acts.r1, _g(flat, lay.norm1.weight), _g(flat, lay.norm1.bias)),
+                 (grads.dln2, acts.x2p, acts.m2, acts.r2, _g(flat, lay.norm2.weight), _g(flat, lay.norm2.bias))]
+        items = [it for it in items if it[4] is not None and it[5] is not None]
+        if items:
+            K.dec_ln_grads(items, R)
     _wgrad(flat, lay.linear2.weight, lay.linear2.bias, v(grads.df), v(acts.gd))
     _wgrad(flat, lay.linear1.weight, lay.linear1.bias, v(grads.dgp), v(acts.x2))
     _wgrad(flat, ca.out_proj.weight, ca.out_proj.bias, v(grads.dcao), v(acts.ctx))
@@ -295,6 +379,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         dkvt = [torch.zeros(Bq * Lt, 2 * E, device=dev) if Lt else None for _ in layers]
         ds = ds.contiguous()
         grads = [_LayerGrads(S, Bq, dev) for _ in layers]
+        fused_layers = [st.kv is not None for st in saves[S - 1]]
         for i in reversed(range(S)):
             tsum, mu, ru = fused[i]
             du = K.dropout_bwd(ds, p, seed + 7 + 64 * 1000 * (i + 1)) if p > 0 else ds
@@ -334,7 +419,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         with torch.cuda.stream(wg):
             for l, lay in enumerate(layers):
                 ca = lay.multihead_attn
-                _layer_wgrads(lay, flat, acts[l], grads[l])
+                _layer_wgrads(lay, flat, acts[l], grads[l], fused=fused_layers[l])
                 _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16[l], v16, rows=(E, 3 * E))
                 if Lt:
                     _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[l], t16, rows=(E, 3 * E))
