@@ -170,9 +170,10 @@ int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map,
                        int rows, int cols, uint16_t* dx_bf16, const int32_t* dx_bf16_map,
                        const float* dx_scale, int dx_scale_rps, float* workspace,
                        int64_t workspace_elems, void* stream);
-/* f32 elements of the dw/db partials workspace lrce_layernorm_bwd uses for (rows, cols): with it
- * the weight/bias gradients are a deterministic two-pass sum instead of same-address atomics from
- * every block (a NULL or smaller workspace falls back to the atomics). */
+/* f32 elements of the dw/db partials workspace lrce_layernorm_bwd uses for (rows, cols) (0: one block
+ * suffices): with it the weight/bias gradients are a deterministic sum in block order (per-block
+ * partials, then a reduce whose last-arriving block per column adds the chunk sums in order) instead
+ * of same-address atomics from every block (a NULL or smaller workspace falls back to the atomics). */
 int64_t lrce_layernorm_bwd_workspace(int rows, int cols);
 
 /* ---------------------------------------------------------------- Swin 3D window attention
@@ -411,6 +412,10 @@ int lrce_dec_sa_bwd(const LrceDecSaBwd* args, void* stream);
  * LayerNorms): dgamma[c] += sum_r dy (x - mean) rstd, dbeta[c] += sum_r dy, rows in order. */
 int lrce_dec_ln_grads(const float* const* dy, const float* const* x, const float* const* mean, const float* const* rstd,
                       float* const* dgamma, float* const* dbeta, int n_ln, int rows, void* stream);
+/* Debug: phase timestamps (s_memrealtime, 100 MHz) of the four fused block kernels (k = sa_fwd, ca_fwd,
+ * ca_bwd, sa_bwd) into buf[(k * 1024 + workgroup) * 16 + mark] (device memory, 4 * 1024 * 16 uint64);
+ * NULL turns it off (the default).  tools/decoder_trace.py reads it. */
+int lrce_dec_set_trace(uint64_t* buf);
 
 /* ---------------------------------------------------------------- elementwise / data movement */
 /* Patch-embed input stage: [ImageNet Normalize (video.py:35)] + zero-pad T to a multiple of 2

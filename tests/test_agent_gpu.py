@@ -164,13 +164,16 @@ def test_early_group_updates_match_one_update():
 
 
 def test_early_updates_do_not_race_the_backward():
-    """The same training step run twice from identical weights and optimizer state — once with the
+    """The same training step run from identical weights and optimizer state — once with the
     in-backward group updates, once with one update after the backward — with every stochastic element
-    off (train mode, dropout / DropPath 0, so both runs must produce the same gradients): flat.grad and
-    the updated masters must agree bit for bit.  An early update that overlapped a backward kernel still
-    reading its group's weights (the decoder's and Swin stages' updates run on the weight-gradient
-    stream, BERT's on the text stream), or that read a gradient before its last writer, changes one of
-    them; the test above cannot see that, because it reuses the racing run's gradients."""
+    off (train mode, dropout / DropPath 0, so both runs see the same gradients): flat.grad and the
+    updated masters must agree.  An early update that overlapped a backward kernel still reading its
+    group's weights (the decoder's and Swin stages' updates run on the weight-gradient stream, BERT's
+    on the text stream), or that read a gradient before its last writer, shifts that gradient by a
+    whole update step (relative ~1e-3 at lr 1e-4); the backward's own run-to-run noise (a few float
+    atomics: embedding rows, bias sums of split-K weight gradients) is ~1e-7, measured here as the
+    difference between two plain runs.  The test above cannot see a race: it reuses the racing run's
+    gradients."""
     from lrce.optim import FusedAdamW
     b = [t.cuda() for t in _batch("oe", 32)]
     model = _model("oe", 50, 32)
@@ -191,6 +194,7 @@ def test_early_updates_do_not_race_the_backward():
     bufs = (flat.f32, opt.exp_avg, opt.exp_avg_sq, opt.sumsq, opt.step_t)
     state = [t.clone() for t in bufs]
     count = opt.step_count
+    w0 = flat.f32.clone()
 
     def run(groups):
         for dst, src in zip(bufs, state):
@@ -206,19 +210,25 @@ def test_early_updates_do_not_race_the_backward():
         torch.cuda.synchronize()
         return flat.grad.clone(), flat.f32.clone(), opt.early_updates - n0
 
-    def diff(a, b):
-        bad = []
+    def worst(a, b_, ref):
+        """max over tensors of max|a - b| / max|ref| (ref: the gradient, or the update w - w0)"""
+        out = []
         for name, p in model.named_parameters():
-            sl = flat._slice(a, p)
-            sb = flat._slice(b, p)
-            if not torch.equal(sl, sb):
-                bad.append(f"{name}: max|d| {float((sl - sb).abs().max()):.3e} of {float(sb.abs().max()):.3e}")
-        return bad
+            if not p.requires_grad:
+                continue
+            da = (flat._slice(a, p) - flat._slice(b_, p)).abs().max().item()
+            out.append((da / (flat._slice(ref, p).abs().max().item() + 1e-30), name))
+        return max(out)
 
     g_plain, w_plain, n_plain = run({})
     g_plain2, w_plain2, _ = run({})
-    assert not diff(g_plain, g_plain2), "the backward itself is not bitwise repeatable:\n" + "\n".join(diff(g_plain, g_plain2)[:20])
     g_early, w_early, n_early = run(model.optimizer_groups())
     assert n_early == 5 and n_plain == 0
-    assert not diff(g_early, g_plain), "gradients differ with early updates:\n" + "\n".join(diff(g_early, g_plain)[:20])
-    assert torch.equal(w_early, w_plain)
+    noise = worst(g_plain2, g_plain, g_plain)
+    err = worst(g_early, g_plain, g_plain)
+    assert noise[0] < 1e-4, f"plain runs differ: {noise}"
+    assert err[0] < max(1e-4, 4 * noise[0]), f"gradients with early updates: {err} (plain-run noise {noise})"
+    upd = w_plain - w0
+    werr = worst(w_early, w_plain, upd)
+    wnoise = worst(w_plain2, w_plain, upd)
+    assert werr[0] < max(1e-3, 4 * wnoise[0]), f"updates with early updates: {werr} (noise {wnoise})"

@@ -150,9 +150,18 @@ def test_fused_decoder_blocks_match_unfused(task, L, ncls, B, drop, monkeypatch)
                      {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}))
     (y0, v0, t0, g0), (y1, v1, t1, g1) = runs
     assert rel(y1, y0) < 1e-4
-    assert rel(v1, v0) < 1e-4 and rel(t1, t0) < 1e-4
+    # the memory side (dK / dV -> bf16 -> the K/V projection's dX and dW, the embeddings) and linear1
+    # (its saved pre-activation is bf16, so dGELU sees it rounded) pass through one bf16 rounding: f32
+    # differences in the last bits flip single bf16 roundings (2^-8 relative)
+    assert rel(v1, v0) < 5e-3 and rel(t1, t0) < 5e-3
     assert g0.keys() == g1.keys()
-    bad = {k: rel(g1[k], g0[k]) for k in g0 if rel(g1[k], g0[k]) > 2e-4}
+    query_side = ("self_attn.", "multihead_attn.out_proj", "linear2", "norm1", "norm2", "norm3",
+                  "fusion_layer_norm", "summarization_token")
+    bad = {}
+    for k in g0:
+        err = rel(g1[k], g0[k])
+        if err > (2e-4 if any(q in k for q in query_side) else 5e-3):
+            bad[k] = err
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]
 
 

@@ -35,6 +35,18 @@ namespace {
 constexpr int E = 768, H = 12, D = 64, NT = 256, MAXK = 192;
 constexpr int WROWS = 16;            // rows of a head's 64-row weight slice per wave
 constexpr int NRI = 24;              // 16-B register loads per lane for 16 rows x 768 (fp16)
+constexpr int MAXTXT = 48;           // text-segment keys (question tokens + 1)
+constexpr int TXU = MAXTXT / 4;      // text keys per wave in the attention backward
+
+// Debug phase timestamps (lrce_dec_set_trace; NULL in production): wave 0 of every workgroup stores
+// s_memrealtime (100 MHz) at the marks of kernel k into p.trace[(k * 1024 + wg) * 16 + i] (the pointer
+// rides in the kernel arguments: a scalar load, no vector-memory wait).
+unsigned long long* g_dec_trace_host = nullptr;
+#define DEC_MARK(K, I)                                                                                     \
+  do {                                                                                                   \
+    if (p.trace && threadIdx.x == 0 && blockIdx.x < 1024)                                                \
+      p.trace[((K) * 1024 + blockIdx.x) * 16 + (I)] = __builtin_amdgcn_s_memrealtime();                  \
+  } while (0)
 
 __device__ __forceinline__ void dec_glds(const void* sbase, uint32_t voff, uint32_t lds_dst) {
   unsigned keep;
@@ -50,6 +62,42 @@ __device__ __forceinline__ void dec_glds_p(const void* src, uint32_t lds_dst) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+}
+
+// Workgroup barrier for LDS hand-offs only: __syncthreads() would also drain vmcnt(0), i.e. wait for
+// every bulk load and LDS-DMA still in flight (the weight slices), serialising the loads with the
+// LayerNorm / reduction phases they are meant to overlap.  Global-memory ordering is explicit where
+// needed (s_waitcnt vmcnt(0) before reading DMA'd LDS, and in publish_partial).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Keep a loaded value in registers: hipcc may otherwise re-load a read-only operand at its later
+// uses (to save VGPRs), and such a re-load behind the bulk loads waits for all of them.
+__device__ __forceinline__ void pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+// the device RNG offset (lrce_rng_offset), read once at kernel start
+__device__ __forceinline__ uint64_t rng_off_now(const uint64_t* off) {
+  uint64_t o = off ? *off : 0ull;
+  asm volatile("" : "+v"(o));
+  return o;
+}
+
+// cross-lane moves inside a row of 16 lanes (DPP: a VALU operand modifier, no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum4(float v) {   // every lane: the sum of its aligned group of 4
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  return v;
+}
+__device__ __forceinline__ float sum8(float v) {   // ... of 8
+  v = sum4(v);
+  v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the 8
+  return v;
 }
 
 __device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
@@ -115,8 +163,7 @@ __device__ __forceinline__ void rows_gemv(const uint4 (&reg)[NRI], const float* 
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) s += pp[r * 64 + q * 16 + i];
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
+  s = sum4(s);
   if (q == 0) o[r] = s;
 }
 
@@ -163,9 +210,7 @@ __device__ __forceinline__ void slice_gemv(const f16* S, const float* v, float* 
     unpack8(*reinterpret_cast<const uint4*>(S + n * D + c * 8), wf);
     float s = ((wf[0] * vv[0] + wf[1] * vv[1]) + (wf[2] * vv[2] + wf[3] * vv[3])) +
               ((wf[4] * vv[4] + wf[5] * vv[5]) + (wf[6] * vv[6] + wf[7] * vv[7]));
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
+    s = sum8(s);
     if (c == 0) out[n] = s;
   }
 }
@@ -185,7 +230,7 @@ __device__ __forceinline__ void slice_gemv_t(const f16* S, const float* u, float
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    a[e] += __shfl_xor(a[e], 8, 64);
+    a[e] += dpp_f<0x128>(a[e]);   // row_ror:8 (lanes g, g^1 of a row)
     a[e] += __shfl_xor(a[e], 16, 64);
     a[e] += __shfl_xor(a[e], 32, 64);
   }
@@ -198,51 +243,63 @@ __device__ __forceinline__ void slice_gemv_t(const f16* S, const float* u, float
 __device__ __forceinline__ float block_sum4(float v, float* red2, int lane, int wave) {
   v = wave_sum(v);
   if (lane == 0) red2[wave] = v;
-  __syncthreads();
+  lds_barrier();
   const float r = (red2[0] + red2[1]) + (red2[2] + red2[3]);
-  __syncthreads();
+  lds_barrier();
   return r;
 }
 __device__ __forceinline__ float block_max4(float v, float* red2, int lane, int wave) {
   v = wave_max(v);
   if (lane == 0) red2[wave] = v;
-  __syncthreads();
+  lds_barrier();
   const float r = fmaxf(fmaxf(red2[0], red2[1]), fmaxf(red2[2], red2[3]));
-  __syncthreads();
+  lds_barrier();
   return r;
 }
 
 // LayerNorm forward of one 768 row held as float4 by threads t < 192 (two-pass statistics, the
-// order of lrce_gemm_ln mode 1): y = (x - mu) rstd g + b into ys (LDS)
-__device__ __forceinline__ void ln_row_fwd(float4 x, const float* g, const float* bb, float eps, float* ys, float* red2,
-                                           int t, int lane, int wave, float& mu, float& rs) {
+// order of lrce_gemm_ln mode 1): y = (x - mu) rstd g + b into ys (LDS).  s1_local: this thread's
+// (x.x + x.y) + (x.z + x.w) (0 past the row), computed by the caller before it issues its bulk loads
+// (the compiler's in-order vmcnt waits would otherwise hold the statistics until they land).
+__device__ __forceinline__ float row_sum_local(float4 x, int t) { return t < E / 4 ? (x.x + x.y) + (x.z + x.w) : 0.f; }
+__device__ __forceinline__ void ln_row_fwd(float4 x, float s1_local, float4 gg, float4 be, float eps, float* ys,
+                                           float* red2, int t, int lane, int wave, float& mu, float& rs) {
   const bool live = t < E / 4;
-  const float s1 = block_sum4(live ? (x.x + x.y) + (x.z + x.w) : 0.f, red2, lane, wave);
+  const float s1 = block_sum4(s1_local, red2, lane, wave);
   mu = s1 * (1.0f / E);
   float4 d = make_float4(x.x - mu, x.y - mu, x.z - mu, x.w - mu);
   const float s2 = block_sum4(live ? (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w) : 0.f, red2, lane, wave);
   rs = rsqrtf(s2 * (1.0f / E) + eps);
   if (live) {
-    const float4 gg = *reinterpret_cast<const float4*>(g + 4 * t), be = *reinterpret_cast<const float4*>(bb + 4 * t);
     *reinterpret_cast<float4*>(ys + 4 * t) =
         make_float4(d.x * rs * gg.x + be.x, d.y * rs * gg.y + be.y, d.z * rs * gg.z + be.z, d.w * rs * gg.w + be.w);
   }
 }
 
 // LayerNorm backward of one row: dy (float4, t < 192), x, mean, rstd, gamma -> dx (float4), the
-// formula of lrce_gemm_ln mode 2: dx = rstd (g - mean(g) - xh mean(g xh)), g = dy gamma
-__device__ __forceinline__ float4 ln_row_bwd(float4 dy, float4 x, float mu, float rs, const float* gamma, float* red2, int t,
-                                             int lane, int wave) {
-  const bool live = t < E / 4;
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f), xh = g;
-  if (live) {
-    const float4 gm = *reinterpret_cast<const float4*>(gamma + 4 * t);
-    g = make_float4(dy.x * gm.x, dy.y * gm.y, dy.z * gm.z, dy.w * gm.w);
-    xh = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+// formula of lrce_gemm_ln mode 2: dx = rstd (g - mean(g) - xh mean(g xh)), g = dy gamma.  Local
+// part (g, xh and this thread's two sums) first, the block reductions after the caller's bulk loads.
+struct LnBwdLocal {
+  float4 g, xh;
+  float s1, s2;
+};
+__device__ __forceinline__ LnBwdLocal ln_row_bwd_local(float4 dy, float4 x, float4 gm, float mu, float rs, int t) {
+  LnBwdLocal l;
+  l.g = make_float4(0.f, 0.f, 0.f, 0.f);
+  l.xh = l.g;
+  if (t < E / 4) {
+    l.g = make_float4(dy.x * gm.x, dy.y * gm.y, dy.z * gm.z, dy.w * gm.w);
+    l.xh = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
   }
-  const float s1 = block_sum4((g.x + g.y) + (g.z + g.w), red2, lane, wave);
-  const float s2 = block_sum4((g.x * xh.x + g.y * xh.y) + (g.z * xh.z + g.w * xh.w), red2, lane, wave);
+  l.s1 = (l.g.x + l.g.y) + (l.g.z + l.g.w);
+  l.s2 = (l.g.x * l.xh.x + l.g.y * l.xh.y) + (l.g.z * l.xh.z + l.g.w * l.xh.w);
+  return l;
+}
+__device__ __forceinline__ float4 ln_row_bwd(const LnBwdLocal& l, float rs, float* red2, int lane, int wave) {
+  const float s1 = block_sum4(l.s1, red2, lane, wave);
+  const float s2 = block_sum4(l.s2, red2, lane, wave);
   const float mg = s1 * (1.0f / E), mgx = s2 * (1.0f / E);
+  const float4 g = l.g, xh = l.xh;
   return make_float4(rs * (g.x - mg - xh.x * mgx), rs * (g.y - mg - xh.y * mgx), rs * (g.z - mg - xh.z * mgx),
                      rs * (g.w - mg - xh.w * mgx));
 }
@@ -293,6 +350,7 @@ struct SaFwdP {
   const uint64_t* rng_off;
   float* slab;
   unsigned* ctr;
+  unsigned long long* trace;
 };
 
 struct SaFwdLds {
@@ -309,16 +367,34 @@ __global__ void __launch_bounds__(NT, 1) dec_sa_fwd_kernel(SaFwdP p) {
   __shared__ __attribute__((aligned(16))) SaFwdLds L;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int b = blockIdx.x / H, h = blockIdx.x % H;
+  DEC_MARK(0, 0);
   // everything that depends on nothing: the row, the W_v rows, the W_o slice (DMA)
-  float4 xr = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (t < E / 4) xr = *reinterpret_cast<const float4*>(p.x_in + (long long)b * E + 4 * t);
+  float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
+  if (t < E / 4) {
+    xr = *reinterpret_cast<const float4*>(p.x_in + (long long)b * E + 4 * t);
+    if (p.ln_g) {
+      gg = *reinterpret_cast<const float4*>(p.ln_g + 4 * t);
+      be = *reinterpret_cast<const float4*>(p.ln_b + 4 * t);
+    }
+  }
+  // the row first (its statistics start right away: the asm pins the sum, and so the wait for the
+  // row, here), then the bulk loads: W_v rows into registers, the W_o slice by DMA (last: the
+  // compiler's in-order vmcnt waits do not count the DMAs)
+  const uint64_t roff = rng_off_now(p.rng_off);
+  pin(xr);
+  pin(gg);
+  pin(be);
+  const float s1l = row_sum_local(xr, t);
+  asm volatile("" ::"v"(s1l));
+  __builtin_amdgcn_sched_barrier(0);
   uint4 wr[NRI];
   rows_load(p.wv, h * D + wave * WROWS, lane, wr);
   const float bvv = t < D ? p.bv[h * D + t] : 0.f;
-  slice_dma(p.wo, h, L.wo, wave, lane);   // last: the compiler's vmcnt waits do not count these
+  slice_dma(p.wo, h, L.wo, wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
   if (p.ln_g) {
     float mu, rs;
-    ln_row_fwd(xr, p.ln_g, p.ln_b, p.eps, L.x0, L.red2, t, lane, wave, mu, rs);
+    ln_row_fwd(xr, s1l, gg, be, p.eps, L.x0, L.red2, t, lane, wave, mu, rs);
     if (h == 0) {
       if (t < E / 4) *reinterpret_cast<float4*>(p.x0_out + (long long)b * E + 4 * t) = *reinterpret_cast<const float4*>(L.x0 + 4 * t);
       if (t == 0) {
@@ -329,11 +405,13 @@ __global__ void __launch_bounds__(NT, 1) dec_sa_fwd_kernel(SaFwdP p) {
   } else if (t < E / 4) {
     *reinterpret_cast<float4*>(L.x0 + 4 * t) = xr;
   }
-  __syncthreads();
+  lds_barrier();
+  DEC_MARK(0, 1);
   // v = W_v[h] x0 + b_v ; head dropout
   rows_gemv(wr, L.x0, L.pp[wave], L.v + wave * WROWS, lane);
-  __syncthreads();
-  const uint64_t seed0 = lrce_seed(p.seed, p.rng_off);
+  lds_barrier();
+  DEC_MARK(0, 2);
+  const uint64_t seed0 = p.seed + roff;
   if (t < D) {
     float v = L.v[t] + bvv;
     if (p.p > 0.f) v = drop1(v, p.p, seed0, ((long long)b * E + h * D + t) / D);
@@ -341,11 +419,15 @@ __global__ void __launch_bounds__(NT, 1) dec_sa_fwd_kernel(SaFwdP p) {
     p.sad[(long long)b * E + h * D + t] = v;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slice DMA has landed
-  __syncthreads();                                    // ... and every wave's; L.v complete
+  lds_barrier();                                    // ... and every wave's; L.v complete
+  DEC_MARK(0, 3);
   slice_gemv(L.wo, L.v, L.part, wave, lane);
-  __syncthreads();
-  if (!publish_partial(L.part, p.slab, p.ctr, b, h, t, &L.last)) return;
-  const uint64_t seed1 = lrce_seed(p.seed + 1, p.rng_off);
+  lds_barrier();
+  DEC_MARK(0, 4);
+  const bool last_sa = publish_partial(L.part, p.slab, p.ctr, b, h, t, &L.last);
+  DEC_MARK(0, 5);
+  if (!last_sa) return;
+  const uint64_t seed1 = p.seed + 1 + roff;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int n = t + 256 * i;
@@ -354,6 +436,7 @@ __global__ void __launch_bounds__(NT, 1) dec_sa_fwd_kernel(SaFwdP p) {
     p.x1p[(long long)b * E + n] = L.x0[n] + y;
   }
   if (t == 0) __hip_atomic_store(&p.ctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  DEC_MARK(0, 6);
 }
 
 // ------------------------------------------------------------------ cross-attention block forward
@@ -366,9 +449,26 @@ struct KvP {
   int bdiv2, lk2;
   long long v_off;  // V = K + v_off (elements)
 };
-__device__ __forceinline__ const bf16* kv_row(const KvP& kv, int b, int j, int h) {
-  if (j < kv.lk1) return kv.k1 + (long long)(b / kv.bdiv1) * kv.stride1 + (long long)j * kv.ld1 + h * D;
-  return kv.k2 + (long long)(b / kv.bdiv2) * kv.stride2 + (long long)(j - kv.lk1) * kv.ld2 + h * D;
+// the memory rows of one (b, h): two uniform segment bases (scalar registers), then a per-lane select
+// — a per-lane choice between the parameter struct's fields would make hipcc fetch them with vector
+// loads and drain vmcnt(0) (every bulk load in flight) before each use
+struct KvRows {
+  const bf16* base1;
+  const bf16* base2;
+  long long ld1, ld2;
+  int lk1;
+};
+__device__ __forceinline__ KvRows kv_rows(const KvP& kv, int b, int h) {
+  KvRows r;
+  r.base1 = kv.k1 + (long long)(b / kv.bdiv1) * kv.stride1 + h * D;
+  r.base2 = kv.k2 ? kv.k2 + (long long)(b / kv.bdiv2) * kv.stride2 + h * D : r.base1;
+  r.ld1 = kv.ld1;
+  r.ld2 = kv.ld2;
+  r.lk1 = kv.lk1;
+  return r;
+}
+__device__ __forceinline__ const bf16* kv_row(const KvRows& r, int j) {
+  return j < r.lk1 ? r.base1 + (long long)j * r.ld1 : r.base2 + (long long)(j - r.lk1) * r.ld2;
 }
 
 struct CaFwdP {
@@ -394,6 +494,7 @@ struct CaFwdP {
   const uint64_t* rng_off;
   float* slab;
   unsigned* ctr;
+  unsigned long long* trace;
 };
 
 struct CaFwdLds {
@@ -415,30 +516,45 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const int Lk = p.kv.lk1 + p.kv.lk2;
-  float4 xr = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (t < E / 4) xr = *reinterpret_cast<const float4*>(p.x1p + (long long)b * E + 4 * t);
-  uint4 wr[NRI];
-  rows_load(p.wq, h * D + wave * WROWS, lane, wr);
-  // key row of thread t (registers) and the head's V rows (LDS, 8 rows per DMA instruction)
+  DEC_MARK(1, 0);
+  float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
+  if (t < E / 4) {
+    xr = *reinterpret_cast<const float4*>(p.x1p + (long long)b * E + 4 * t);
+    gg = *reinterpret_cast<const float4*>(p.g1 + 4 * t);
+    be = *reinterpret_cast<const float4*>(p.b1 + 4 * t);
+  }
+  const uint64_t roff = rng_off_now(p.rng_off);
+  pin(xr);
+  pin(gg);
+  pin(be);
+  const float s1l = row_sum_local(xr, t);
+  asm volatile("" ::"v"(s1l));
+  __builtin_amdgcn_sched_barrier(0);
+  // key row of thread t (registers; needed first, after q), the W_q rows, then the DMAs: the head's V
+  // rows (LDS, 8 rows per instruction) and the W_o slice
   const bool live = t < Lk;
+  const KvRows kvr = kv_rows(p.kv, b, h);
   uint4 kr[8];
   {
-    const bf16* kp = kv_row(p.kv, b, live ? t : 0, h);
+    const bf16* kp = kv_row(kvr, live ? t : 0);
 #pragma unroll
     for (int c = 0; c < 8; ++c) kr[c] = *reinterpret_cast<const uint4*>(kp + 8 * c);
   }
+  uint4 wr[NRI];
+  rows_load(p.wq, h * D + wave * WROWS, lane, wr);
   const float bqv = t < D ? p.bq[h * D + t] : 0.f;
   {
     const uint32_t vb = dec_lds_addr(L.vimg);
     for (int ins = wave; ins * 8 < Lk; ins += 4) {
       const int j = min(ins * 8 + (lane >> 3), Lk - 1);
-      const bf16* vp = kv_row(p.kv, b, j, h) + p.kv.v_off + (lane & 7) * 8;
+      const bf16* vp = kv_row(kvr, j) + p.kv.v_off + (lane & 7) * 8;
       dec_glds_p(vp, vb + (uint32_t)ins * 1024u);
     }
   }
   slice_dma(p.wo, h, L.wo, wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
   float mu, rs;
-  ln_row_fwd(xr, p.g1, p.b1, p.eps, L.x1, L.red2, t, lane, wave, mu, rs);
+  ln_row_fwd(xr, s1l, gg, be, p.eps, L.x1, L.red2, t, lane, wave, mu, rs);
   if (h == 0) {
     if (t < E / 4) *reinterpret_cast<float4*>(p.x1_out + (long long)b * E + 4 * t) = *reinterpret_cast<const float4*>(L.x1 + 4 * t);
     if (t == 0) {
@@ -446,15 +562,17 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
       p.rstd_out[b] = rs;
     }
   }
-  __syncthreads();
+  lds_barrier();
+  DEC_MARK(1, 1);
   rows_gemv(wr, L.x1, L.pp[wave], L.q + wave * WROWS, lane);
-  __syncthreads();
+  lds_barrier();
+  DEC_MARK(1, 2);
   if (t < D) {
     const float q = L.q[t] + bqv;
     p.q_out[(long long)b * E + h * D + t] = q;
     L.q[t] = q * 0.125f;   // head_dim^-0.5
   }
-  __syncthreads();
+  lds_barrier();
   // scores, softmax (natural log), dropout on the probabilities
   float sc = 0.f;
   if (live) {
@@ -471,12 +589,14 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
   const float m = block_max4(live ? sc : -1.0e30f, L.red2, lane, wave);
   const float pe = live ? __expf(sc - m) : 0.f;
   const float s = block_sum4(pe, L.red2, lane, wave);
-  const uint64_t seed2 = lrce_seed(p.seed, p.rng_off);
+  const uint64_t seed2 = p.seed + roff;
   float pf = pe;
   if (live && p.p > 0.f) pf = drop1(pe, p.p, seed2, ((long long)b * H + h) * Lk + t);
   L.ps[t] = live ? pf : 0.f;
+  DEC_MARK(1, 3);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // V rows and the W_o slice have landed
-  __syncthreads();
+  lds_barrier();
+  DEC_MARK(1, 4);
   // ctx = sum_j p_j V_j / s: lane = head dim, wave w takes keys w, w+4, ...
   {
     float o0 = 0.f, o1 = 0.f;
@@ -488,18 +608,22 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
     if (j < Lk) o0 += L.ps[j] * bf2f(L.vimg[j * D + lane]);
     L.opart[wave][lane] = o0 + o1;
   }
-  __syncthreads();
+  lds_barrier();
   if (t < D) {
     const float c = ((L.opart[0][t] + L.opart[1][t]) + (L.opart[2][t] + L.opart[3][t])) / s;
     L.ctx[t] = c;
     p.ctx_out[(long long)b * E + h * D + t] = c;
     if (t == 0) p.lse_out[(long long)b * H + h] = m + __logf(s);
   }
-  __syncthreads();
+  lds_barrier();
+  DEC_MARK(1, 5);
   slice_gemv(L.wo, L.ctx, L.part, wave, lane);
-  __syncthreads();
-  if (!publish_partial(L.part, p.slab, p.ctr, b, h, t, &L.last)) return;
-  const uint64_t seed3 = lrce_seed(p.seed + 1, p.rng_off);
+  lds_barrier();
+  DEC_MARK(1, 6);
+  const bool last_ca = publish_partial(L.part, p.slab, p.ctr, b, h, t, &L.last);
+  DEC_MARK(1, 7);
+  if (!last_ca) return;
+  const uint64_t seed3 = p.seed + 1 + roff;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int n = t + 256 * i;
@@ -508,6 +632,7 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
     p.x2p[(long long)b * E + n] = L.x1[n] + y;
   }
   if (t == 0) __hip_atomic_store(&p.ctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  DEC_MARK(1, 8);
 }
 
 // ------------------------------------------------------------------ cross-attention block backward
@@ -538,6 +663,7 @@ struct CaBwdP {
   const uint64_t* rng_off;
   float* slab;
   unsigned* ctr;
+  unsigned long long* trace;
 };
 
 struct CaBwdLds {
@@ -564,12 +690,20 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const int Lk = p.kv.lk1 + p.kv.lk2;
-  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy;
+  DEC_MARK(2, 0);
+  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
   if (t < E / 4) {
     dy = *reinterpret_cast<const float4*>(p.dx2 + (long long)b * E + 4 * t);
     xr = *reinterpret_cast<const float4*>(p.x2p + (long long)b * E + 4 * t);
+    gm = *reinterpret_cast<const float4*>(p.g2 + 4 * t);
   }
   const float mu = p.mean2[b], rs = p.rstd2[b];
+  const uint64_t roff = rng_off_now(p.rng_off);
+  LnBwdLocal lnl = ln_row_bwd_local(dy, xr, gm, mu, rs, t);
+  pin(lnl.g);
+  pin(lnl.xh);
+  asm volatile("" : "+v"(lnl.s1), "+v"(lnl.s2));
+  __builtin_amdgcn_sched_barrier(0);
   uint4 wr[NRI];
   rows_load(p.wq, h * D + wave * WROWS, lane, wr);
   float qd = 0.f, od = 0.f;
@@ -578,19 +712,33 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
     od = p.ctx[(long long)b * E + h * D + t];
   }
   const float lse = p.lse[(long long)b * H + h];
+  const KvRows kvr = kv_rows(p.kv, b, h);
+  // the text rows' running dK / dV (accumulated over the recurrent steps): read now, added at the end
+  const long long trow = (long long)(b / p.kv.bdiv2) * p.dstride2 + h * D + lane;
+  float told[TXU][2];
+#pragma unroll
+  for (int u = 0; u < TXU; ++u) {
+    const int tj = wave + 4 * u;
+    told[u][0] = told[u][1] = 0.f;
+    if (tj < p.kv.lk2) {
+      told[u][0] = p.dk2[trow + (long long)tj * p.dld2];
+      told[u][1] = p.dk2[trow + (long long)tj * p.dld2 + p.dv_off];
+    }
+  }
   {
     const uint32_t kb = dec_lds_addr(L.kimg), vb = dec_lds_addr(L.vimg);
     for (int ins = wave; ins * 8 < Lk; ins += 4) {
       const int j = min(ins * 8 + (lane >> 3), Lk - 1);
-      const bf16* kp = kv_row(p.kv, b, j, h) + (lane & 7) * 8;
+      const bf16* kp = kv_row(kvr, j) + (lane & 7) * 8;
       dec_glds_p(kp, kb + (uint32_t)ins * 1024u);
       dec_glds_p(kp + p.kv.v_off, vb + (uint32_t)ins * 1024u);
     }
   }
   slice_dma(p.wo, h, L.wo, wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
   // LN2 backward, then the out dropout's backward (seed + 3 of the layer = p.seed + 1)
-  const float4 dx = ln_row_bwd(dy, xr, mu, rs, p.g2, L.red2, t, lane, wave);
-  const uint64_t seed3 = lrce_seed(p.seed + 1, p.rng_off);
+  const float4 dx = ln_row_bwd(lnl, rs, L.red2, lane, wave);
+  const uint64_t seed3 = p.seed + 1 + roff;
   if (t < E / 4) {
     *reinterpret_cast<float4*>(L.dx2p + 4 * t) = dx;
     float4 d = dx;
@@ -603,11 +751,14 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
     if (h == 0) *reinterpret_cast<float4*>(p.dcao_out + (long long)b * E + 4 * t) = d;
   }
   if (t < D) L.q[t] = qd * 0.125f;
+  DEC_MARK(2, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  lds_barrier();
+  DEC_MARK(2, 2);
   // dctx = W_o[:, h]^T dcao
   slice_gemv_t(L.wo, L.dcao, &L.red64[0][0], wave, lane);
-  __syncthreads();
+  lds_barrier();
+  DEC_MARK(2, 3);
   float dod = 0.f;
   if (t < D) {
     dod = (L.red64[0][t] + L.red64[1][t]) + (L.red64[2][t] + L.red64[3][t]);
@@ -634,70 +785,75 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
     }
     const float pr = __expf(sc - lse);
     float f = 1.f;
-    if (p.p > 0.f) f = lrce_uniform(lrce_seed(p.seed, p.rng_off), (uint64_t)(((long long)b * H + h) * Lk + t)) >= p.p
+    if (p.p > 0.f) f = lrce_uniform(p.seed + roff, (uint64_t)(((long long)b * H + h) * Lk + t)) >= p.p
                            ? 1.0f / (1.0f - p.p) : 0.f;
     pf = pr * f;
     ds = pr * (f * dp - delta);
   }
   L.ps[t] = pf;
   L.dss[t] = ds;
-  __syncthreads();
-  // dq (lane = dim), dK / dV rows: wave w takes keys w, w+4, ...
+  lds_barrier();
+  DEC_MARK(2, 4);
+  // dq (lane = dim), dK / dV rows: wave w takes video keys j = w mod 4 and text keys j - lk1 = w mod 4
   {
     const float qs = L.q[lane], g = L.dctx[lane];
-    float dq0 = 0.f;
-    for (int j = wave; j < Lk; j += 4) {
+    float dq0 = 0.f, dq1 = 0.f;
+    const long long vrow = (long long)(b / p.kv.bdiv1) * p.dstride1 + h * D + lane;
+    for (int j = wave; j < p.kv.lk1; j += 4) {
       const float dsj = L.dss[j], pj = L.ps[j];
       dq0 += dsj * bf2f(L.kimg[j * D + lane]);
-      float* dk;
-      long long o;
-      bool atom;
-      if (j < p.kv.lk1) {
-        o = (long long)(b / p.kv.bdiv1) * p.dstride1 + (long long)j * p.dld1 + h * D + lane;
-        dk = p.dk1;
-        atom = p.dkv1_atomic;
-      } else {
-        o = (long long)(b / p.kv.bdiv2) * p.dstride2 + (long long)(j - p.kv.lk1) * p.dld2 + h * D + lane;
-        dk = p.dk2;
-        atom = false;
-      }
-      if (atom) {
-        __hip_atomic_fetch_add(dk + o, dsj * qs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(dk + o + p.dv_off, pj * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else if (j < p.kv.lk1) {   // one writer, first contribution: store
-        dk[o] = dsj * qs;
-        dk[o + p.dv_off] = pj * g;
-      } else {                      // text rows accumulate over the recurrent steps
-        dk[o] += dsj * qs;
-        dk[o + p.dv_off] += pj * g;
+      float* dk = p.dk1 + vrow + (long long)j * p.dld1;
+      if (p.dkv1_atomic) {   // rows shared by bdiv1 query rows (the MC choices)
+        __hip_atomic_fetch_add(dk, dsj * qs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(dk + p.dv_off, pj * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {                // one writer, first contribution: store
+        dk[0] = dsj * qs;
+        dk[p.dv_off] = pj * g;
       }
     }
-    L.red64[wave][lane] = dq0;
+#pragma unroll
+    for (int u = 0; u < TXU; ++u) {   // text rows accumulate over the recurrent steps (prefetched)
+      const int tj = wave + 4 * u;
+      if (tj < p.kv.lk2) {
+        const int j = p.kv.lk1 + tj;
+        const float dsj = L.dss[j], pj = L.ps[j];
+        dq1 += dsj * bf2f(L.kimg[j * D + lane]);
+        float* dk = p.dk2 + trow + (long long)tj * p.dld2;
+        dk[0] = told[u][0] + dsj * qs;
+        dk[p.dv_off] = told[u][1] + pj * g;
+      }
+    }
+    L.red64[wave][lane] = dq0 + dq1;
   }
-  __syncthreads();
+  lds_barrier();
   if (t < D) {
     const float dq = ((L.red64[0][t] + L.red64[1][t]) + (L.red64[2][t] + L.red64[3][t])) * 0.125f;
     L.dq[t] = dq;
     p.dq_out[(long long)b * E + h * D + t] = dq;
   }
-  __syncthreads();
+  lds_barrier();
+  DEC_MARK(2, 5);
   // dx1 partial = W_q[h]^T dq
   rows_gemv_t(wr, L.dq + wave * WROWS, L.acc[wave], lane);
-  __syncthreads();
+  lds_barrier();
   float* part = &L.acc[0][0];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int n = t + 256 * i;
     part[n] = (L.acc[0][n] + L.acc[1][n]) + (L.acc[2][n] + L.acc[3][n]);
   }
-  __syncthreads();
-  if (!publish_partial(part, p.slab, p.ctr, b, h, t, &L.last)) return;
+  lds_barrier();
+  DEC_MARK(2, 6);
+  const bool last_cb = publish_partial(part, p.slab, p.ctr, b, h, t, &L.last);
+  DEC_MARK(2, 7);
+  if (!last_cb) return;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int n = t + 256 * i;
     p.dx1_out[(long long)b * E + n] = L.dx2p[n] + gather_partials(p.slab, b, n);
   }
   if (t == 0) __hip_atomic_store(&p.ctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  DEC_MARK(2, 8);
 }
 
 // ------------------------------------------------------------------ self-attention block backward
@@ -718,6 +874,7 @@ struct SaBwdP {
   const uint64_t* rng_off;
   float* slab;
   unsigned* ctr;
+  unsigned long long* trace;
 };
 
 struct SaBwdLds {
@@ -735,17 +892,26 @@ __global__ void __launch_bounds__(NT, 1) dec_sa_bwd_kernel(SaBwdP p) {
   __shared__ __attribute__((aligned(16))) SaBwdLds L;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int b = blockIdx.x / H, h = blockIdx.x % H;
-  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy;
+  DEC_MARK(3, 0);
+  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
   if (t < E / 4) {
     dy = *reinterpret_cast<const float4*>(p.dx1 + (long long)b * E + 4 * t);
     xr = *reinterpret_cast<const float4*>(p.x1p + (long long)b * E + 4 * t);
+    gm = *reinterpret_cast<const float4*>(p.g1 + 4 * t);
   }
   const float mu = p.mean1[b], rs = p.rstd1[b];
+  const uint64_t roff = rng_off_now(p.rng_off);
+  LnBwdLocal lnl = ln_row_bwd_local(dy, xr, gm, mu, rs, t);
+  pin(lnl.g);
+  pin(lnl.xh);
+  asm volatile("" : "+v"(lnl.s1), "+v"(lnl.s2));
+  __builtin_amdgcn_sched_barrier(0);
   uint4 wr[NRI];
   rows_load(p.wv, h * D + wave * WROWS, lane, wr);
   slice_dma(p.wo, h, L.wo, wave, lane);
-  const float4 dx = ln_row_bwd(dy, xr, mu, rs, p.g1, L.red2, t, lane, wave);
-  const uint64_t seed1 = lrce_seed(p.seed + 1, p.rng_off);
+  __builtin_amdgcn_sched_barrier(0);
+  const float4 dx = ln_row_bwd(lnl, rs, L.red2, lane, wave);
+  const uint64_t seed1 = p.seed + 1 + roff;
   if (t < E / 4) {
     *reinterpret_cast<float4*>(L.dx1p + 4 * t) = dx;
     float4 d = dx;
@@ -757,33 +923,39 @@ __global__ void __launch_bounds__(NT, 1) dec_sa_bwd_kernel(SaBwdP p) {
     *reinterpret_cast<float4*>(L.dsao + 4 * t) = d;
     if (h == 0) *reinterpret_cast<float4*>(p.dsao_out + (long long)b * E + 4 * t) = d;
   }
+  DEC_MARK(3, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  lds_barrier();
+  DEC_MARK(3, 2);
   slice_gemv_t(L.wo, L.dsao, &L.red64[0][0], wave, lane);
-  __syncthreads();
+  lds_barrier();
   if (t < D) {
     float v = (L.red64[0][t] + L.red64[1][t]) + (L.red64[2][t] + L.red64[3][t]);
-    if (p.p > 0.f) v = drop1(v, p.p, lrce_seed(p.seed, p.rng_off), ((long long)b * E + h * D + t) / D);
+    if (p.p > 0.f) v = drop1(v, p.p, p.seed + roff, ((long long)b * E + h * D + t) / D);
     L.dsav[t] = v;
     p.dsav_out[(long long)b * E + h * D + t] = v;
   }
-  __syncthreads();
+  lds_barrier();
   rows_gemv_t(wr, L.dsav + wave * WROWS, L.acc[wave], lane);
-  __syncthreads();
+  lds_barrier();
   float* part = &L.acc[0][0];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int n = t + 256 * i;
     part[n] = (L.acc[0][n] + L.acc[1][n]) + (L.acc[2][n] + L.acc[3][n]);
   }
-  __syncthreads();
-  if (!publish_partial(part, p.slab, p.ctr, b, h, t, &L.last)) return;
+  lds_barrier();
+  DEC_MARK(3, 3);
+  const bool last_sb = publish_partial(part, p.slab, p.ctr, b, h, t, &L.last);
+  DEC_MARK(3, 4);
+  if (!last_sb) return;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int n = t + 256 * i;
     p.dx0_out[(long long)b * E + n] = L.dx1p[n] + gather_partials(p.slab, b, n);
   }
   if (t == 0) __hip_atomic_store(&p.ctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  DEC_MARK(3, 5);
 }
 
 // ------------------------------------------------------------------ deferred LayerNorm parameter grads
@@ -837,13 +1009,14 @@ extern "C" int lrce_dec_sa_fwd(const LrceDecSa* a, void* stream) {
   p.x0_out = a->x0_out; p.mean_out = a->mean_out; p.rstd_out = a->rstd_out;
   p.wv = reinterpret_cast<const f16*>(a->wv); p.bv = a->bv; p.wo = reinterpret_cast<const f16*>(a->wo); p.bo = a->bo;
   p.sad = a->sad; p.x1p = a->x1p; p.p = a->drop_p; p.seed = a->seed; p.rng_off = lrce_rng_offset();
-  p.slab = a->slab; p.ctr = a->counters;
+  p.slab = a->slab; p.ctr = a->counters; p.trace = g_dec_trace_host;
   return launch(dec_sa_fwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_sa_fwd");
 }
 
 static int kv_check(const LrceDecKv& kv, const char* what) {
-  if (!kv.k1 || kv.lk1 < 1 || kv.bdiv1 < 1 || (kv.lk2 > 0 && (!kv.k2 || kv.bdiv2 < 1)) || kv.lk1 + kv.lk2 > MAXK)
-    return lrce_fail(LRCE_E_ARG, "%s: memory segments (lk1=%d, lk2=%d, max %d keys)", what, kv.lk1, kv.lk2, MAXK);
+  if (!kv.k1 || kv.lk1 < 1 || kv.bdiv1 < 1 || (kv.lk2 > 0 && (!kv.k2 || kv.bdiv2 < 1)) || kv.lk1 + kv.lk2 > MAXK ||
+      kv.lk2 > MAXTXT)
+    return lrce_fail(LRCE_E_ARG, "%s: memory segments (lk1=%d, lk2=%d <= %d, max %d keys)", what, kv.lk1, kv.lk2, MAXTXT, MAXK);
   if (!al16(kv.k1) || (kv.k2 && !al16(kv.k2)) || (kv.ld1 % 8) || (kv.stride1 % 8) || (kv.lk2 > 0 && ((kv.ld2 % 8) || (kv.stride2 % 8))) ||
       (kv.v_off % 8))
     return lrce_fail(LRCE_E_ARG, "%s: K/V rows need 16-B alignment", what);
@@ -869,7 +1042,7 @@ extern "C" int lrce_dec_ca_fwd(const LrceDecCa* a, void* stream) {
   p.mean_out = a->mean_out; p.rstd_out = a->rstd_out; p.wq = reinterpret_cast<const f16*>(a->wq); p.bq = a->bq;
   p.kv = kv_conv(a->kv); p.q_out = a->q_out; p.ctx_out = a->ctx_out; p.lse_out = a->lse_out;
   p.wo = reinterpret_cast<const f16*>(a->wo); p.bo = a->bo; p.x2p = a->x2p; p.p = a->drop_p; p.seed = a->seed;
-  p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters;
+  p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters; p.trace = g_dec_trace_host;
   return launch(dec_ca_fwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_ca_fwd");
 }
 
@@ -888,7 +1061,7 @@ extern "C" int lrce_dec_ca_bwd(const LrceDecCaBwd* a, void* stream) {
   p.lse = a->lse; p.dq_out = a->dq_out; p.dk1 = a->dk1; p.dstride1 = a->dstride1; p.dld1 = a->dld1;
   p.dkv1_atomic = a->kv.bdiv1 > 1; p.dk2 = a->dk2; p.dstride2 = a->dstride2; p.dld2 = a->dld2; p.dv_off = a->dv_off;
   p.wq = reinterpret_cast<const f16*>(a->wq); p.dx1_out = a->dx1_out; p.p = a->drop_p; p.seed = a->seed;
-  p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters;
+  p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters; p.trace = g_dec_trace_host;
   return launch(dec_ca_bwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_ca_bwd");
 }
 
@@ -903,7 +1076,7 @@ extern "C" int lrce_dec_sa_bwd(const LrceDecSaBwd* a, void* stream) {
   p.B = a->B; p.dx1 = a->dx1; p.x1p = a->x1p; p.mean1 = a->mean1; p.rstd1 = a->rstd1; p.g1 = a->g1;
   p.dsao_out = a->dsao_out; p.wo = reinterpret_cast<const f16*>(a->wo); p.dsav_out = a->dsav_out;
   p.wv = reinterpret_cast<const f16*>(a->wv); p.dx0_out = a->dx0_out; p.p = a->drop_p; p.seed = a->seed;
-  p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters;
+  p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters; p.trace = g_dec_trace_host;
   return launch(dec_sa_bwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_sa_bwd");
 }
 
@@ -919,4 +1092,10 @@ extern "C" int lrce_dec_ln_grads(const float* const* dy, const float* const* x, 
   p.rows = rows;
   dec_ln_grads_kernel<<<dim3((E + 255) / 256, n_ln), 256, 0, static_cast<hipStream_t>(stream)>>>(p);
   return lrce_check_launch("dec_ln_grads");
+}
+
+// debug: phase timestamps of the fused decoder kernels into buf (device, >= 4 * 1024 * 16 uint64), NULL = off
+extern "C" int lrce_dec_set_trace(uint64_t* buf) {
+  g_dec_trace_host = reinterpret_cast<unsigned long long*>(buf);
+  return LRCE_OK;
 }

@@ -14,6 +14,9 @@
 namespace {
 
 constexpr int MAXC = 8;  // float4 chunks per lane -> cols <= 2048
+constexpr int LN_RED_CTRS = 64;   // ln_bwd_reduce column blocks: (2 * 2048) / 64
+constexpr int LN_RED_ROWS = 128;  // partial rows per ln_bwd_reduce block
+constexpr int LN_RED_MAXY = 16;   // 2048 blocks / LN_RED_ROWS
 
 template <typename T>
 __device__ __forceinline__ float4 ld4(const T* p);
@@ -275,36 +278,63 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
   for (int e = threadIdx.x; e < cols; e += 256) {
     const float sw = red[0][0][e] + red[0][1][e] + red[0][2][e] + red[0][3][e];
     const float sb = red[1][0][e] + red[1][1][e] + red[1][2][e] + red[1][3][e];
-    if (pb) {            // per-block partials, summed by ln_bwd_reduce (no same-address atomics here)
+    if (pb) {            // per-block partials, summed in block order by ln_bwd_reduce
       pb[e] = sw;
       pb[cols + e] = sb;
-    } else {
+    } else if (gridDim.x == 1) {   // the only block: one writer per element (deterministic)
+      if (dw) dw[e] += sw;
+      if (db) db[e] += sb;
+    } else {             // no workspace: same-address atomics (order-dependent rounding)
       if (dw) atomicAdd(dw + e, sw);
       if (db) atomicAdd(db + e, sb);
     }
   }
+  // arrival counters of ln_bwd_reduce (after the partials: the next launch reads them zeroed)
+  if (part && blockIdx.x == 0 && threadIdx.x < LN_RED_CTRS)
+    reinterpret_cast<unsigned*>(part + ((long long)gridDim.x + (gridDim.x + LN_RED_ROWS - 1) / LN_RED_ROWS) * 2 * cols)[threadIdx.x] = 0u;
 }
 
-// dw[e] += sum_b part[b][e], db[e] += sum_b part[b][cols + e]: block (x, y) sums 32 partial rows of
-// 64 columns (8 per wave, loads in flight together) and adds once, so an address sees nb/32 adds.
-__global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ part, int nb, int cols, float* dw, float* db) {
+// dw[e] += sum_b part[b][e], db[e] += sum_b part[b][cols + e], deterministically: block (x, y) sums
+// LN_RED_ROWS partial rows of 64 columns (32 per wave, 8 loads in flight) into chunk row y; the last
+// of the column block's ny (<= 16) blocks to arrive (agent-scope stores / counter, as the skinny
+// split-K of gemm_f32.hip) adds the ny chunk rows in order — one writer per element, a fixed order.
+__global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ part, int nb, int cols, float* dw, float* db,
+                                                     float* chunk, unsigned* counters) {
   __shared__ float red[4][64];
+  __shared__ unsigned last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + lane;
-  const int b0 = blockIdx.y * 32 + wave * 8;
-  float v[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) v[u] = (e < 2 * cols && b0 + u < nb) ? part[(long long)(b0 + u) * 2 * cols + e] : 0.f;
+  const int ny = gridDim.y;
   float t = 0.f;
 #pragma unroll
-  for (int u = 0; u < 8; ++u) t += v[u];
+  for (int q = 0; q < LN_RED_ROWS / 32; ++q) {
+    const int b0 = blockIdx.y * LN_RED_ROWS + q * 32 + wave * 8;
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (e < 2 * cols && b0 + u < nb) ? part[(long long)(b0 + u) * 2 * cols + e] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t += v[u];
+  }
   red[wave][lane] = t;
   __syncthreads();
-  if (wave == 0 && e < 2 * cols) {
-    t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    float* dst = e < cols ? (dw ? dw + e : nullptr) : (db ? db + (e - cols) : nullptr);
-    if (dst) atomicAdd(dst, t);
-  }
+  if (wave == 0 && e < 2 * cols)
+    __hip_atomic_store(chunk + (long long)blockIdx.y * 2 * cols + e, (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(ny - 1);
+  __syncthreads();
+  if (!last || wave != 0 || e >= 2 * cols) return;
+  float cv[LN_RED_MAXY];
+#pragma unroll
+  for (int y = 0; y < LN_RED_MAXY; ++y)
+    cv[y] = y < ny ? __hip_atomic_load(chunk + (long long)y * 2 * cols + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+  float s = 0.f;
+#pragma unroll
+  for (int y = 0; y < LN_RED_MAXY; ++y) s += cv[y];
+  float* dst = e < cols ? (dw ? dw + e : nullptr) : (db ? db + (e - cols) : nullptr);
+  if (dst) *dst += s;
 }
 
 // rows per wave of ln_bwd: small inputs (the decoder / BERT rows) one row per wave (latency-bound:
@@ -366,9 +396,12 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
   const int lpr = ln_bwd_lpr(cols);
   const bool want = dw || db;
   const int nb_ws = ln_bwd_blocks(rows, lpr, true);
-  // (a few blocks -- the decoder / BERT rows -- add directly: a second launch would cost more)
-  float* part = want && nb_ws > 64 && workspace && workspace_elems >= (int64_t)nb_ws * 2 * cols ? workspace : nullptr;
-  const int nb = part ? nb_ws : ln_bwd_blocks(rows, lpr, false);
+  const int ny = (nb_ws + LN_RED_ROWS - 1) / LN_RED_ROWS;
+  // dw / db partials per block + a deterministic reduce launch; a one-block problem (rows <= 4-8, the
+  // decoder's rows) or no workspace: one block adds its sums directly
+  float* part = want && nb_ws > 1 && workspace && workspace_elems >= (int64_t)(nb_ws + ny) * 2 * cols + LN_RED_CTRS
+                    ? workspace : nullptr;
+  const int nb = (part || !want) ? nb_ws : ln_bwd_blocks(rows, lpr, false);
 #define LNB3(TD, TX, CH, LPR)                                                                                          \
   ln_bwd<TD, TX, CH, LPR><<<nb, 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, \
                                                      nseg, mean, rstd, w, dx, dres, dw, db, rows, cols,      \
@@ -387,12 +420,14 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
   else { LNB(bf16, bf16) }
 #undef LNB
 #undef LNB3
-  if (part) ln_bwd_reduce<<<dim3((2 * cols + 63) / 64, (nb + 31) / 32), 256, 0, s>>>(part, nb, cols, dw, db);
+  if (part)
+    ln_bwd_reduce<<<dim3((2 * cols + 63) / 64, ny), 256, 0, s>>>(
+        part, nb, cols, dw, db, part + (long long)nb * 2 * cols, reinterpret_cast<unsigned*>(part + (long long)(nb + ny) * 2 * cols));
   return lrce_check_launch("layernorm_bwd");
 }
 
 extern "C" int64_t lrce_layernorm_bwd_workspace(int rows, int cols) {
   if (rows <= 0 || cols <= 0) return 0;
   const int nb = ln_bwd_blocks(rows, ln_bwd_lpr(cols), true);
-  return nb > 64 ? (int64_t)nb * 2 * cols : 0;
+  return nb > 1 ? (int64_t)(nb + (nb + LN_RED_ROWS - 1) / LN_RED_ROWS) * 2 * cols + LN_RED_CTRS : 0;
 }

@@ -147,12 +147,12 @@ class _LayerGrads:
 
 def _fused_ok(lay, Bq, Lt):
     """The per-head fused attention blocks (csrc/decoder.hip) need the fp16 weight shadow, <= 64 query
-    rows and <= 192 memory keys; LRCE_DEC_FUSED=0 selects the unfused launches (A/B, tests)."""
+    rows and <= 150 + 42 memory keys; LRCE_DEC_FUSED=0 selects the unfused launches (A/B, tests)."""
     if os.environ.get("LRCE_DEC_FUSED", "1") == "0":
         return False
     flat = getattr(lay, "_lrce_flat", None)
     return (flat is not None and flat.has_f16(lay.self_attn.in_proj_weight) and flat.has_f16(lay.multihead_attn.in_proj_weight)
-            and Bq <= K.DEC_MAX_ROWS and 150 + Lt <= 192)
+            and Bq <= K.DEC_MAX_ROWS and Lt <= 42)
 
 
 def _layer_fwd(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_prev):
