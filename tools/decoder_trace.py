@@ -19,8 +19,10 @@ from lrce.models.fusionv3 import LRCEOpenEnded  # noqa: E402
 
 MARKS = {
     "sa_fwd": ["start", "x0 ready", "v proj", "slice landed", "out partial", "published", "last done"],
-    "ca_fwd": ["start", "x1 ready", "q proj", "softmax", "V/slice landed", "ctx", "out partial", "published", "last done"],
-    "ca_bwd": ["start", "LN2 bwd", "K/V/slice landed", "dctx", "P/dS", "dq, dK/dV", "dx1 partial", "published", "last done"],
+    "ca_fwd": ["start", "x1 ready", "q proj", "softmax", "V/slice landed", "ctx", "out partial", "published", "last done",
+               "(row loaded)", "(bulk issued)"],
+    "ca_bwd": ["start", "LN2 bwd", "K/V/slice landed", "dctx", "P/dS", "dq, dK/dV", "dx1 partial", "published", "last done",
+               "(rows loaded)", "(bulk issued)", "(LN reduced)"],
     "sa_bwd": ["start", "LN1 bwd", "slice landed", "dx0 partial", "published", "last done"],
 }
 

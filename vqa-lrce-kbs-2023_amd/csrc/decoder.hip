@@ -36,7 +36,7 @@ constexpr int E = 768, H = 12, D = 64, NT = 256, MAXK = 192;
 constexpr int WROWS = 16;            // rows of a head's 64-row weight slice per wave
 constexpr int NRI = 24;              // 16-B register loads per lane for 16 rows x 768 (fp16)
 constexpr int MAXTXT = 48;           // text-segment keys (question tokens + 1)
-constexpr int TXU = MAXTXT / 4;      // text keys per wave in the attention backward
+constexpr int TXI = (MAXTXT * 8 + NT - 1) / NT;   // text (key, 8-dim chunk) items per thread
 
 // Debug phase timestamps (lrce_dec_set_trace; NULL in production): wave 0 of every workgroup stores
 // s_memrealtime (100 MHz) at the marks of kernel k into p.trace[(k * 1024 + wg) * 16 + i] (the pointer
@@ -98,6 +98,15 @@ __device__ __forceinline__ float sum8(float v) {   // ... of 8
   v = sum4(v);
   v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the 8
   return v;
+}
+
+__device__ __forceinline__ void unpack8bf(const uint4 u, float (&f)[8]) {
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = bfbits2f((unsigned short)(w[e] & 0xFFFFu));
+    f[2 * e + 1] = bfbits2f((unsigned short)(w[e] >> 16));
+  }
 }
 
 __device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
@@ -452,6 +461,12 @@ struct KvP {
 // the memory rows of one (b, h): two uniform segment bases (scalar registers), then a per-lane select
 // — a per-lane choice between the parameter struct's fields would make hipcc fetch them with vector
 // loads and drain vmcnt(0) (every bulk load in flight) before each use
+// K / V images in LDS: row j (64 bf16 = 8 chunks of 16 B) with chunk c stored at chunk c ^ (j & 7),
+// so a wave reading one 16-B chunk of 64 different rows spreads over every bank (the rows are 128 B
+// apart: unswizzled, all 64 lanes hit the same two bank groups)
+__device__ __forceinline__ int kv_swz(int j, int c) { return j * D + ((c ^ (j & 7)) << 3); }
+__device__ __forceinline__ float kv_at(const bf16* img, int j, int d) { return bf2f(img[kv_swz(j, d >> 3) + (d & 7)]); }
+
 struct KvRows {
   const bf16* base1;
   const bf16* base2;
@@ -530,6 +545,7 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
   const float s1l = row_sum_local(xr, t);
   asm volatile("" ::"v"(s1l));
   __builtin_amdgcn_sched_barrier(0);
+  DEC_MARK(1, 9);
   // key row of thread t (registers; needed first, after q), the W_q rows, then the DMAs: the head's V
   // rows (LDS, 8 rows per instruction) and the W_o slice
   const bool live = t < Lk;
@@ -543,18 +559,23 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
   uint4 wr[NRI];
   rows_load(p.wq, h * D + wave * WROWS, lane, wr);
   const float bqv = t < D ? p.bq[h * D + t] : 0.f;
+  __builtin_amdgcn_sched_barrier(0);
+  DEC_MARK(1, 10);
+  // LN1 while those land; the DMAs (needed last) are issued after it: a wave holds at most 63
+  // vector-memory operations in flight, and issuing all of them first stalled the LN behind them
+  float mu, rs;
+  ln_row_fwd(xr, s1l, gg, be, p.eps, L.x1, L.red2, t, lane, wave, mu, rs);
+  __builtin_amdgcn_sched_barrier(0);
   {
     const uint32_t vb = dec_lds_addr(L.vimg);
     for (int ins = wave; ins * 8 < Lk; ins += 4) {
-      const int j = min(ins * 8 + (lane >> 3), Lk - 1);
-      const bf16* vp = kv_row(kvr, j) + p.kv.v_off + (lane & 7) * 8;
+      const int r = ins * 8 + (lane >> 3), j = min(r, Lk - 1);
+      const bf16* vp = kv_row(kvr, j) + p.kv.v_off + (((lane & 7) ^ (r & 7)) << 3);
       dec_glds_p(vp, vb + (uint32_t)ins * 1024u);
     }
   }
   slice_dma(p.wo, h, L.wo, wave, lane);
   __builtin_amdgcn_sched_barrier(0);
-  float mu, rs;
-  ln_row_fwd(xr, s1l, gg, be, p.eps, L.x1, L.red2, t, lane, wave, mu, rs);
   if (h == 0) {
     if (t < E / 4) *reinterpret_cast<float4*>(p.x1_out + (long long)b * E + 4 * t) = *reinterpret_cast<const float4*>(L.x1 + 4 * t);
     if (t == 0) {
@@ -597,16 +618,30 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // V rows and the W_o slice have landed
   lds_barrier();
   DEC_MARK(1, 4);
-  // ctx = sum_j p_j V_j / s: lane = head dim, wave w takes keys w, w+4, ...
+  // ctx = sum_j p_j V_j / s: thread (key group kg = t / 8 of 32, 8-dim chunk c = t % 8) sums keys
+  // j = kg, kg + 32, ... with 16-B row reads, then the 8 key groups of a wave (DPP / shuffles) and the
+  // 4 waves (LDS)
   {
-    float o0 = 0.f, o1 = 0.f;
-    int j = wave;
-    for (; j + 4 < Lk; j += 8) {
-      o0 += L.ps[j] * bf2f(L.vimg[j * D + lane]);
-      o1 += L.ps[j + 4] * bf2f(L.vimg[(j + 4) * D + lane]);
+    const int c = t & 7, kg = t >> 3;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int j = kg; j < Lk; j += 32) {
+      float vf[8];
+      unpack8bf(*reinterpret_cast<const uint4*>(L.vimg + kv_swz(j, c)), vf);
+      const float pj = L.ps[j];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = fmaf(pj, vf[e], a[e]);
     }
-    if (j < Lk) o0 += L.ps[j] * bf2f(L.vimg[j * D + lane]);
-    L.opart[wave][lane] = o0 + o1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] += dpp_f<0x128>(a[e]);   // row_ror:8 -> key groups g, g^1
+      a[e] += __shfl_xor(a[e], 16, 64);
+      a[e] += __shfl_xor(a[e], 32, 64);
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) L.opart[wave][c * 8 + e] = a[e];
+    }
   }
   lds_barrier();
   if (t < D) {
@@ -704,6 +739,7 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
   pin(lnl.xh);
   asm volatile("" : "+v"(lnl.s1), "+v"(lnl.s2));
   __builtin_amdgcn_sched_barrier(0);
+  DEC_MARK(2, 9);
   uint4 wr[NRI];
   rows_load(p.wq, h * D + wave * WROWS, lane, wr);
   float qd = 0.f, od = 0.f;
@@ -713,31 +749,41 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
   }
   const float lse = p.lse[(long long)b * H + h];
   const KvRows kvr = kv_rows(p.kv, b, h);
-  // the text rows' running dK / dV (accumulated over the recurrent steps): read now, added at the end
-  const long long trow = (long long)(b / p.kv.bdiv2) * p.dstride2 + h * D + lane;
-  float told[TXU][2];
+  // the text rows' running dK / dV (accumulated over the recurrent steps), read now as (key, 8-dim
+  // chunk) items and added at the end
+  const long long tbase = (long long)(b / p.kv.bdiv2) * p.dstride2 + h * D;
+  float4 told[TXI][4];
 #pragma unroll
-  for (int u = 0; u < TXU; ++u) {
-    const int tj = wave + 4 * u;
-    told[u][0] = told[u][1] = 0.f;
+  for (int i = 0; i < TXI; ++i) {
+    const int e = t + 256 * i, tj = e >> 3, c = e & 7;
+    told[i][0] = told[i][1] = told[i][2] = told[i][3] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (tj < p.kv.lk2) {
-      told[u][0] = p.dk2[trow + (long long)tj * p.dld2];
-      told[u][1] = p.dk2[trow + (long long)tj * p.dld2 + p.dv_off];
+      const float* src = p.dk2 + tbase + (long long)tj * p.dld2 + c * 8;
+      told[i][0] = *reinterpret_cast<const float4*>(src);
+      told[i][1] = *reinterpret_cast<const float4*>(src + 4);
+      told[i][2] = *reinterpret_cast<const float4*>(src + p.dv_off);
+      told[i][3] = *reinterpret_cast<const float4*>(src + p.dv_off + 4);
     }
   }
+  __builtin_amdgcn_sched_barrier(0);
+  DEC_MARK(2, 10);
+  // LN2 backward while those land; the DMAs (needed after it) are issued next: a wave holds at most
+  // 63 vector-memory operations in flight
+  const float4 dx = ln_row_bwd(lnl, rs, L.red2, lane, wave);
+  __builtin_amdgcn_sched_barrier(0);
+  DEC_MARK(2, 11);
   {
     const uint32_t kb = dec_lds_addr(L.kimg), vb = dec_lds_addr(L.vimg);
     for (int ins = wave; ins * 8 < Lk; ins += 4) {
-      const int j = min(ins * 8 + (lane >> 3), Lk - 1);
-      const bf16* kp = kv_row(kvr, j) + (lane & 7) * 8;
+      const int r = ins * 8 + (lane >> 3), j = min(r, Lk - 1);
+      const bf16* kp = kv_row(kvr, j) + (((lane & 7) ^ (r & 7)) << 3);
       dec_glds_p(kp, kb + (uint32_t)ins * 1024u);
       dec_glds_p(kp + p.kv.v_off, vb + (uint32_t)ins * 1024u);
     }
   }
   slice_dma(p.wo, h, L.wo, wave, lane);
   __builtin_amdgcn_sched_barrier(0);
-  // LN2 backward, then the out dropout's backward (seed + 3 of the layer = p.seed + 1)
-  const float4 dx = ln_row_bwd(lnl, rs, L.red2, lane, wave);
+  // the out dropout's backward (seed + 3 of the layer = p.seed + 1)
   const uint64_t seed3 = p.seed + 1 + roff;
   if (t < E / 4) {
     *reinterpret_cast<float4*>(L.dx2p + 4 * t) = dx;
@@ -772,8 +818,8 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
     float sc = 0.f, dp = 0.f;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      const uint4 ku = *reinterpret_cast<const uint4*>(L.kimg + t * D + 8 * c);
-      const uint4 vu = *reinterpret_cast<const uint4*>(L.vimg + t * D + 8 * c);
+      const uint4 ku = *reinterpret_cast<const uint4*>(L.kimg + kv_swz(t, c));
+      const uint4 vu = *reinterpret_cast<const uint4*>(L.vimg + kv_swz(t, c));
       const unsigned k4[4] = {ku.x, ku.y, ku.z, ku.w}, v4[4] = {vu.x, vu.y, vu.z, vu.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -794,36 +840,64 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
   L.dss[t] = ds;
   lds_barrier();
   DEC_MARK(2, 4);
-  // dq (lane = dim), dK / dV rows: wave w takes video keys j = w mod 4 and text keys j - lk1 = w mod 4
+  // dq: lane = head dim, wave w sums keys j = w, w + 4, ...
   {
-    const float qs = L.q[lane], g = L.dctx[lane];
     float dq0 = 0.f, dq1 = 0.f;
-    const long long vrow = (long long)(b / p.kv.bdiv1) * p.dstride1 + h * D + lane;
-    for (int j = wave; j < p.kv.lk1; j += 4) {
+    int j = wave;
+    for (; j + 4 < Lk; j += 8) {
+      dq0 += L.dss[j] * kv_at(L.kimg, j, lane);
+      dq1 += L.dss[j + 4] * kv_at(L.kimg, j + 4, lane);
+    }
+    if (j < Lk) dq0 += L.dss[j] * kv_at(L.kimg, j, lane);
+    L.red64[wave][lane] = dq0 + dq1;
+  }
+  // dK = dS q~, dV = (P * dropout) dO as (key, 8-dim chunk) items: 16-B stores (video rows: one writer,
+  // stored; shared by bdiv1 > 1 MC choices: atomics), text rows: the prefetched sums + this step's
+  {
+    const long long vbase = (long long)(b / p.kv.bdiv1) * p.dstride1 + h * D;
+    for (int e = t; e < p.kv.lk1 * 8; e += 256) {
+      const int j = e >> 3, c = e & 7;
       const float dsj = L.dss[j], pj = L.ps[j];
-      dq0 += dsj * bf2f(L.kimg[j * D + lane]);
-      float* dk = p.dk1 + vrow + (long long)j * p.dld1;
-      if (p.dkv1_atomic) {   // rows shared by bdiv1 query rows (the MC choices)
-        __hip_atomic_fetch_add(dk, dsj * qs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(dk + p.dv_off, pj * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {                // one writer, first contribution: store
-        dk[0] = dsj * qs;
-        dk[p.dv_off] = pj * g;
+      float kv8[16];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        kv8[i] = dsj * L.q[c * 8 + i];
+        kv8[8 + i] = pj * L.dctx[c * 8 + i];
+      }
+      float* dst = p.dk1 + vbase + (long long)j * p.dld1 + c * 8;
+      if (p.dkv1_atomic) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __hip_atomic_fetch_add(dst + i, kv8[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(dst + p.dv_off + i, kv8[8 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        *reinterpret_cast<float4*>(dst) = make_float4(kv8[0], kv8[1], kv8[2], kv8[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(kv8[4], kv8[5], kv8[6], kv8[7]);
+        *reinterpret_cast<float4*>(dst + p.dv_off) = make_float4(kv8[8], kv8[9], kv8[10], kv8[11]);
+        *reinterpret_cast<float4*>(dst + p.dv_off + 4) = make_float4(kv8[12], kv8[13], kv8[14], kv8[15]);
       }
     }
 #pragma unroll
-    for (int u = 0; u < TXU; ++u) {   // text rows accumulate over the recurrent steps (prefetched)
-      const int tj = wave + 4 * u;
+    for (int i = 0; i < TXI; ++i) {
+      const int e = t + 256 * i, tj = e >> 3, c = e & 7;
       if (tj < p.kv.lk2) {
         const int j = p.kv.lk1 + tj;
         const float dsj = L.dss[j], pj = L.ps[j];
-        dq1 += dsj * bf2f(L.kimg[j * D + lane]);
-        float* dk = p.dk2 + trow + (long long)tj * p.dld2;
-        dk[0] = told[u][0] + dsj * qs;
-        dk[p.dv_off] = told[u][1] + pj * g;
+        const float* qv = L.q + c * 8;
+        const float* gv = L.dctx + c * 8;
+        float* dst = p.dk2 + tbase + (long long)tj * p.dld2 + c * 8;
+        const float4 a0 = told[i][0], a1 = told[i][1], a2 = told[i][2], a3 = told[i][3];
+        *reinterpret_cast<float4*>(dst) =
+            make_float4(a0.x + dsj * qv[0], a0.y + dsj * qv[1], a0.z + dsj * qv[2], a0.w + dsj * qv[3]);
+        *reinterpret_cast<float4*>(dst + 4) =
+            make_float4(a1.x + dsj * qv[4], a1.y + dsj * qv[5], a1.z + dsj * qv[6], a1.w + dsj * qv[7]);
+        *reinterpret_cast<float4*>(dst + p.dv_off) =
+            make_float4(a2.x + pj * gv[0], a2.y + pj * gv[1], a2.z + pj * gv[2], a2.w + pj * gv[3]);
+        *reinterpret_cast<float4*>(dst + p.dv_off + 4) =
+            make_float4(a3.x + pj * gv[4], a3.y + pj * gv[5], a3.z + pj * gv[6], a3.w + pj * gv[7]);
       }
     }
-    L.red64[wave][lane] = dq0 + dq1;
   }
   lds_barrier();
   if (t < D) {
