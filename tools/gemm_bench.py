@@ -29,6 +29,7 @@ SHAPES = [
     (17640, 1536, 512, "fwd", "bias"),
     (17640, 512, 512, "fwd", "bias_resid"),
     (17640, 2048, 512, "dx", "dgelu"),
+    (17640, 512, 512, "dx", ""),
     (17640, 512, 2048, "dx", ""),
     (17640, 512, 1536, "dx", ""),
     (512, 2048, 17640, "dw", ""),

@@ -394,12 +394,10 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
       for (int part = 0; part < 4; ++part) {
         const bf16x8 a = ld_row16(obase + (long long)q * C + part * 8);
         const bf16x8 b = ld_row16(dobase + (long long)q * C + part * 8);
-        const bf16x8 v = ld_row16(base + q * ld + 2 * C + h * HD + part * 8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           d += bf2f(a[j]) * bf2f(b[j]);
           dn2 += bf2f(b[j]) * bf2f(b[j]);
-          vn2 += bf2f(v[j]) * bf2f(v[j]);
         }
       }
       l = lse_g[((long long)w * nH + h) * NPAD + q];
@@ -407,6 +405,12 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
     }
     L.qinfo[q] = make_float4(l, d, __int_as_float(code), 0.f);
   }
+  // |V_key|^2 from the wave's own V fragments (lanes l and l + 32 hold the two halves of a key row)
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vn2 += bf2f(vf[s][j]) * bf2f(vf[s][j]);
+  vn2 += __shfl_xor(vn2, 32, 64);
   dn2 = wave_max(dn2);
   vn2 = wave_max(vn2);
   if (lane == 0) {
