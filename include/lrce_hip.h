@@ -416,6 +416,10 @@ int lrce_dec_ln_grads(const float* const* dy, const float* const* x, const float
  * ca_bwd, sa_bwd) into buf[(k * 1024 + workgroup) * 16 + mark] (device memory, 4 * 1024 * 16 uint64);
  * NULL turns it off (the default).  tools/decoder_trace.py reads it. */
 int lrce_dec_set_trace(uint64_t* buf);
+/* Debug: phase timestamps (s_memrealtime) of lrce_wattn_bwd into buf[workgroup * 16 + mark] (marks: start,
+ * prologue done, steps 0-4 done, stores done, bins written; [10] HW_ID, [11] XCC_ID); NULL turns it off (the
+ * default).  Recorded only by a library built with -DLRCE_WATTN_TRACE (tools/wattn_trace.py). */
+int lrce_wattn_set_trace(uint64_t* buf);
 
 /* ---------------------------------------------------------------- elementwise / data movement */
 /* Patch-embed input stage: [ImageNet Normalize (video.py:35)] + zero-pad T to a multiple of 2

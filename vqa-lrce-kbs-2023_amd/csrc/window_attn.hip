@@ -320,12 +320,15 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restri
 // Relative-position-bias gradient: the table row of (query i, key j) is a linear function of the
 // token codes, code(i) - code(j) + off (video_swin_ori.py:133-148 with window (wd, wh, ww)), so dS is
 // binned in LDS by that difference and each (window, head) writes n_bins floats (3.4 KB at 3x7x7)
-// instead of its 160^2 dS image.  The bins are fixed-point int64 (ds_add_u64): integer adds make the
-// sum independent of wave timing, and measured on gfx950 (tools/lds_atomic_bench.hip) an LDS u64 add
-// costs ~9 cycles per wave instruction against ~230 for ds_add_f32.  The fixed point is scaled per
-// (window, head) by 2^s from a bound on |dS| (|dS_ij| = P_ij |dP_ij - delta_i| <= 2 max|dP| <=
-// 2 max_i |dO_i| max_j |V_j|, so |dS| 2^s < 2^50 and a bin of <= 160 terms stays below 2^58): the
-// quantum follows the gradient's magnitude (an absolute 2^-40 lost batch-mean-sized gradients).
+// instead of its 160^2 dS image.  The bins are fixed-point int32 (ds_add_u32): integer adds make the
+// sum independent of wave timing (an LDS integer add is a few cycles per wave instruction against
+// ~230 for ds_add_f32, tools/lds_atomic_bench.hip).  The fixed point is scaled per (window, head) by
+// 2^s from a bound on |dS| (|dS_ij| = P_ij |dP_ij - delta_i| <= 2 max|dP| <= 2 max_i |dO_i| max_j |V_j|,
+// so |dS| 2^s < 2^22 and a bin of <= 160 terms stays below 2^30): the quantum follows the gradient's
+// magnitude (an absolute quantum lost batch-mean-sized gradients) and is 2^-22 of the bound — finer
+// than the bf16 dS the dQ / dK products use.  Conversion: one f32 fma onto 1.5 * 2^23 leaves
+// round(dS 2^s) in the low mantissa bits, one integer subtract extracts it (the f64 / int64 form of
+// round 2 spent ~7 VALU per element on the conversion and twice the LDS atomic bandwidth).
 // lrce_wattn_dbias sums the windows in a fixed order and scatters bins to table rows.
 constexpr int BW = 5;        // waves per backward workgroup (= tiles of 32 rows)
 constexpr int NBMAX = 1024;  // relative-position bins per head held in LDS
@@ -336,26 +339,53 @@ struct BwdLds {
   bf16 dout[NPAD * HD];
   bf16 k[NPAD * HD];
   bf16 ds[2][BW][TQ * TQ];
-  unsigned long long bins[NBMAX];   // 2^s fixed point
+  unsigned bins[NBMAX];   // 2^s fixed point (two's complement int32)
   float4 qinfo[NPAD];   // per query: lse, delta, token code (as bits), -
   float nmax[BW][2];    // per wave: max |dO_q|^2, max |V_q|^2 over its rows (the bins' scale)
 };
 
-template <bool BH>
-__global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
+// HPW heads per workgroup (2 when nH is even): the hardware keeps only ONE 5-wave workgroup per CU at
+// this kernel's ~160 VGPRs (tools/occupancy_probe.hip: 320-thread workgroups at 136-168 VGPRs are
+// admitted one per CU, 256-thread ones three), so pairing two heads' independent 5-wave halves in one
+// workgroup doubles the waves per CU.
+template <bool BH, int HPW>
+__global__ void __launch_bounds__(BW * 64 * HPW, 3) wattn_bwd_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ outp,
                                                               const bf16* __restrict__ dout, const float* __restrict__ lse_g,
                                                               const void* __restrict__ biasb, const int* __restrict__ win_pat,
                                                               bf16* __restrict__ dqkv, float* __restrict__ dbias_part, int n_win,
-                                                              int n, int nH, int wh, int ww, int nb, int boff, float qscale) {
-  __shared__ __attribute__((aligned(16))) BwdLds L;
-  const int lane = threadIdx.x & 63, t = threadIdx.x >> 6;
+                                                              int n, int nH, int wh, int ww, int nb, int boff, float qscale,
+                                                              unsigned long long* __restrict__ trace) {
+  __shared__ __attribute__((aligned(16))) BwdLds LL[HPW];
+  // debug phase timestamps, compiled in only with -DLRCE_WATTN_TRACE (tools/wattn_trace.py builds that
+  // variant: the marks cost registers this kernel does not have to spare): thread 0 of each workgroup
+#ifdef LRCE_WATTN_TRACE
+#define WB_MARK(I)                                                                    \
+  if (trace && threadIdx.x == 0) trace[(long long)blockIdx.x * 16 + (I)] = __builtin_amdgcn_s_memrealtime();
+  WB_MARK(0)
+  if (trace && threadIdx.x == 0) {   // placement: HW_ID (cu / sh / se) and XCC_ID
+    trace[(long long)blockIdx.x * 16 + 10] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    trace[(long long)blockIdx.x * 16 + 11] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+  }
+#else
+#define WB_MARK(I)
+#endif
+  const int hs = HPW == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / (BW * 64));   // head of the workgroup
+  const int lt = (int)threadIdx.x - hs * BW * 64;   // thread index within that head's half
+  BwdLds& L = LL[hs];
+  const int lane = lt & 63, t = lt >> 6;
   // logical order (head pair, window, head of the pair): the two heads sharing 128-B qkv / dO lines
-  // run next to each other and one XCD's contiguous range covers few heads (their bias tiles stay in
-  // that XCD's L2)
+  // run in one workgroup (HPW = 2) or next to each other, and one XCD's contiguous range covers few
+  // heads (their bias tiles stay in that XCD's L2)
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int hp = (nH & 1) ? 1 : 2;
-  const int h = (lin / hp / n_win) * hp + lin % hp;
-  const int w = (lin / hp) % n_win;
+  int h, w;
+  if constexpr (HPW == 2) {
+    h = (lin / n_win) * 2 + hs;
+    w = lin % n_win;
+  } else {
+    const int hp = (nH & 1) ? 1 : 2;
+    h = (lin / hp / n_win) * hp + lin % hp;
+    w = (lin / hp) % n_win;
+  }
   const int C = nH * HD;
   const long long ld = 3LL * C;
   const bf16* base = qkv + (long long)w * n * ld;
@@ -366,7 +396,7 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
   // Q~, K and dO images [160][32] (rows >= n zero): 3 x 640 16-B chunks over 320 threads
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int c = threadIdx.x + BW * 64 * i;
+    const int c = lt + BW * 64 * i;
     const int row = c >> 2, part = c & 3;
     uint4 qv = make_uint4(0, 0, 0, 0), kv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
     if (row < n) {
@@ -385,8 +415,8 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
   // delta[q] = dO[q] . O[q], lse[q] (0 past n: padded queries contribute nothing), token codes;
   // |dO_q|^2 and |V_q|^2 for the bins' scale
   float dn2 = 0.f, vn2 = 0.f;
-  if (threadIdx.x < NPAD) {
-    const int q = threadIdx.x;
+  if (lt < NPAD) {
+    const int q = lt;
     float d = 0.f, l = 0.f;
     int code = 0;
     if (q < n) {
@@ -417,10 +447,11 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
     L.nmax[t][0] = dn2;
     L.nmax[t][1] = vn2;
   }
-  for (int i = threadIdx.x; i < NBMAX; i += BW * 64) L.bins[i] = 0ull;
+  for (int i = lt; i < NBMAX; i += BW * 64) L.bins[i] = 0u;
   __syncthreads();
-  // bins' scale 2^s: |dS| <= 2 max|dO| max|V| = bound < 2^e -> |dS| 2^s < 2^50 with s = 50 - e
-  double bscale, binv;
+  WB_MARK(1)
+  // bins' scale 2^s: |dS| <= 2 max|dO| max|V| = bound < 2^e -> |dS| 2^s < 2^22 with s = 22 - e
+  float bscale, binv;
   {
     float m0 = 0.f, m1 = 0.f;
 #pragma unroll
@@ -430,9 +461,9 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
     }
     int e = 0;
     (void)frexpf(2.0f * sqrtf(m0) * sqrtf(m1) * 1.0001f, &e);   // margin for the norms' own rounding
-    const int sh = 50 - e;
-    bscale = ldexp(1.0, sh);
-    binv = ldexp(1.0, -sh);
+    const int sh = max(-126, min(126, 22 - e));   // (clamp: both powers stay normal f32)
+    bscale = ldexpf(1.0f, sh);
+    binv = ldexpf(1.0f, -sh);
   }
   bf16x8 kf[2];
 #pragma unroll
@@ -489,12 +520,9 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
     if (want_bins) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        // round(dS * 2^s) to int64: one f64 fma onto 1.5 * 2^52 leaves the integer in the low
-        // mantissa bits (exact for |dS 2^s| < 2^51)
-        const double m = __builtin_fma((double)dp[r], bscale, 0x1.8p52);
-        const unsigned long long v =
-            (unsigned long long)(__double_as_longlong(m) - __double_as_longlong(0x1.8p52));
-        atomicAdd(&L.bins[__float_as_int(qi4[r].z) + kbin], v);
+        // round(dS * 2^s) to int32: the fma result lies in [2^23, 2^24) (ulp 1) for |dS 2^s| < 2^22
+        const float m = __builtin_fmaf(dp[r], bscale, 0x1.8p23f);
+        atomicAdd(&L.bins[__float_as_int(qi4[r].z) + kbin], (unsigned)(__float_as_int(m) - 0x4B400000));
       }
     }
     // dV^T += dO^T P ; dK^T += Q~^T dS  (the accumulators as B operands, permuted k order)
@@ -514,6 +542,7 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
       *reinterpret_cast<bf16x4*>(slot + swz8(r32, 2 * g + hh)) = v;
     }
     __syncthreads();
+    WB_MARK(2 + s)
     // dQ^T(t) += K(kt2)^T dS(t, kt2)^T with the tile wave kt2 = t - s parked this step
     const int kt2 = t - s >= 0 ? t - s : t - s + NTILE;
     const bf16* src = L.ds[s & 1][kt2];
@@ -550,11 +579,14 @@ __global__ void __launch_bounds__(BW * 64, 3) wattn_bwd_kernel(const bf16* __res
       *reinterpret_cast<bf16x4*>(row + 8 * g) = a;
     }
   }
+  WB_MARK(7)
   if (!want_bins) return;
   __syncthreads();   // every wave's bin adds are done
   float* dst = dbias_part + ((long long)w * nH + h) * nb;
-  for (int b = threadIdx.x; b < nb; b += BW * 64)
-    dst[b] = (float)((double)(long long)L.bins[b] * binv);
+  for (int b = lt; b < nb; b += BW * 64)
+    dst[b] = (float)(int)L.bins[b] * binv;
+  WB_MARK(8)
+#undef WB_MARK
 }
 
 // Bias-table gradient from the per-(window, head) bin rows, no atomics: (1) WCH chunks of windows
@@ -583,6 +615,8 @@ __global__ void dbias_scatter_kernel(const float* __restrict__ red, int hb, int 
 }
 
 }  // namespace
+
+static unsigned long long* g_wb_trace = nullptr;   // lrce_wattn_set_trace
 
 extern "C" int64_t lrce_wattn_bias_elems(int n_pat, int nH) { return (int64_t)n_pat * nH * PH_ELEMS; }
 // bias-gradient scratch (f32): one bin row per (window, head) + the WCH chunk sums
@@ -626,10 +660,22 @@ extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const ui
   if (nb > NBMAX) return lrce_fail(LRCE_E_ARG, "wattn_bwd: %d relative-position bins > %d", nb, NBMAX);
   if (n_win <= 0) return LRCE_OK;
   const int boff = ((wd - 1) * (2 * wh - 1) + (wh - 1)) * (2 * ww - 1) + (ww - 1);
-  (bias_f16 ? wattn_bwd_kernel<true> : wattn_bwd_kernel<false>)<<<(unsigned)(n_win * nH), BW * 64, 0, static_cast<hipStream_t>(stream)>>>(
+  static const bool one_head = getenv("LRCE_WATTN_HPW1") != nullptr;   // A/B: one head per workgroup
+  const int hpw = (nH & 1) || one_head ? 1 : 2;
+  const auto kern = bias_f16 ? (hpw == 2 ? wattn_bwd_kernel<true, 2> : wattn_bwd_kernel<true, 1>)
+                             : (hpw == 2 ? wattn_bwd_kernel<false, 2> : wattn_bwd_kernel<false, 1>);
+  kern<<<(unsigned)(n_win * nH / hpw), BW * 64 * hpw, 0, static_cast<hipStream_t>(stream)>>>(
       reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const bf16*>(out), reinterpret_cast<const bf16*>(dout), lse, bias_bwd,
-      win_pat, reinterpret_cast<bf16*>(dqkv), dbias_part, n_win, n, nH, wh, ww, nb, boff, 1.0f / sqrtf((float)HD));
+      win_pat, reinterpret_cast<bf16*>(dqkv), dbias_part, n_win, n, nH, wh, ww, nb, boff, 1.0f / sqrtf((float)HD),
+      g_wb_trace);
   return lrce_check_launch("wattn_bwd");
+}
+
+// debug: phase timestamps of wattn_bwd into buf (device, >= workgroups * 16 uint64), NULL = off; recorded
+// only by a build with -DLRCE_WATTN_TRACE
+extern "C" int lrce_wattn_set_trace(uint64_t* buf) {
+  g_wb_trace = reinterpret_cast<unsigned long long*>(buf);
+  return LRCE_OK;
 }
 
 extern "C" int lrce_wattn_dbias(float* dbias_part, int n_win, int nH, int n_bins, const int32_t* bin_row, float* table_grad,

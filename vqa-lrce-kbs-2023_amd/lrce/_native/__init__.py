@@ -161,6 +161,7 @@ _SIGS = {
     "lrce_dec_sa_bwd": [ctypes.POINTER(DecSaBwd), _P],
     "lrce_dec_ln_grads": [_P, _P, _P, _P, _P, _P, _I, _I, _P],
     "lrce_dec_set_trace": [_P],
+    "lrce_wattn_set_trace": [_P],
     "lrce_frames_resize": [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P],
     "lrce_patch_im2col": [_P, _I, _I, _I, _I, _I64, _I64, _I64, _I, _P, _P],
     "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _I, _P, _P],
