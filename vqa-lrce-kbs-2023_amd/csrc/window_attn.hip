@@ -330,6 +330,14 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restri
 // round(dS 2^s) in the low mantissa bits, one integer subtract extracts it (the f64 / int64 form of
 // round 2 spent ~7 VALU per element on the conversion and twice the LDS atomic bandwidth).
 // lrce_wattn_dbias sums the windows in a fixed order and scatters bins to table rows.
+// Workgroup barrier for LDS hand-offs only: __syncthreads() would also drain vmcnt(0), i.e. wait for
+// the bias-tile loads of later steps and the dK / dV / dQ stores in flight.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 constexpr int BW = 5;        // waves per backward workgroup (= tiles of 32 rows)
 constexpr int NBMAX = 1024;  // relative-position bins per head held in LDS
 constexpr int WCH = 32;      // window chunks of the deterministic bias-gradient reduction
@@ -541,7 +549,7 @@ __global__ void __launch_bounds__(BW * 64 * HPW, 3) wattn_bwd_kernel(const bf16*
       for (int e = 0; e < 4; ++e) v[e] = f2bf(dp[4 * g + e]);
       *reinterpret_cast<bf16x4*>(slot + swz8(r32, 2 * g + hh)) = v;
     }
-    __syncthreads();
+    lds_barrier();
     WB_MARK(2 + s)
     // dQ^T(t) += K(kt2)^T dS(t, kt2)^T with the tile wave kt2 = t - s parked this step
     const int kt2 = t - s >= 0 ? t - s : t - s + NTILE;
@@ -581,7 +589,7 @@ __global__ void __launch_bounds__(BW * 64 * HPW, 3) wattn_bwd_kernel(const bf16*
   }
   WB_MARK(7)
   if (!want_bins) return;
-  __syncthreads();   // every wave's bin adds are done
+  lds_barrier();   // every wave's bin adds are done (the row stores above stay in flight)
   float* dst = dbias_part + ((long long)w * nH + h) * nb;
   for (int b = lt; b < nb; b += BW * 64)
     dst[b] = (float)(int)L.bins[b] * binv;
