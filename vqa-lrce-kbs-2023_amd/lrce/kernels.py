@@ -18,6 +18,7 @@ F16 = torch.float16
 F32 = torch.float32
 NUM_CU = 256
 _SPLIT_PER_CU = float(os.environ.get("LRCE_SPLITK_PER_CU", "2"))   # A/B knob: split-K blocks per CU
+_SPLIT_MIN_DEPTH = int(os.environ.get("LRCE_SPLITK_MIN_DEPTH", "1024"))   # A/B knob: shallowest K slice
 
 
 class KernelTimer:
@@ -181,7 +182,7 @@ def _split_for(m_out, n_out, k_red):
     """Split-K factor of a weight-gradient GEMM: ~2 blocks of 128x128 per CU, K slices >= 1024 deep."""
     tiles = math.ceil(m_out / 128) * math.ceil(n_out / 128)
     want = max(1, math.ceil(_SPLIT_PER_CU * NUM_CU / tiles))
-    return int(max(1, min(want, k_red // 1024)))
+    return int(max(1, min(want, k_red // _SPLIT_MIN_DEPTH)))
 
 
 def _skinny_drop_ok(x, w, M, a_map=None):
