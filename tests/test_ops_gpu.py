@@ -368,12 +368,13 @@ def _wattn_reference(qkv, table, index, region, win_pat, nH, n, c):
 
 @pytest.mark.parametrize("nH,n_win,bias16,gscale", [(4, 9, False, 1.0), (16, 5, False, 1.0), (32, 2, False, 1.0),
                                                    (4, 9, True, 1.0), (16, 5, True, 1.0), (4, 9, True, 1e-12),
-                                                   (16, 5, True, 1e6)])
+                                                   (16, 5, True, 1e6), (3, 4, True, 1.0), (5, 3, False, 1.0)])
 def test_window_attention_fwd_bwd(nH, n_win, bias16, gscale):
     """bias16: the backward reads fp16 bias tiles (the Swin-B product path, same rounding as the fused
     forward's); else f32.  gscale: the upstream gradient's magnitude — a batch-mean cross-entropy over
     ~10^5 tokens hands the attention ~1e-6..1e-12-sized gradients; the bias-table bins' fixed point is
-    scaled per (window, head), so the relative error must not depend on it."""
+    scaled per (window, head), so the relative error must not depend on it.  Odd nH runs the backward's
+    one-head-per-workgroup variant (even nH pairs two heads per workgroup)."""
     k = K()
     n, hd = 147, 32
     C = nH * hd

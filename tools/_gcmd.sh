@@ -1,2 +1,2 @@
 mkdir -p gpurun_out && export TMPDIR=/tmp
-for v in aux defer main aux defer main; do LRCE_DEC_WGRAD_STREAM=$v timeout -k 10 300 python bench.py --no-cpu-baseline --agent-steps 0 --steps 20 > gpurun_out/b7_$v.log 2>&1 || exit 1; echo "wgrad stream $v: $(tail -1 gpurun_out/b7_$v.log | cut -c100-190)"; done
+timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k "window_attention_fwd_bwd" > gpurun_out/t6.log 2>&1; rc=$?; grep -E "^E  |passed|failed|Error" gpurun_out/t6.log | head -20; [ $rc -eq 0 ] || exit $rc
