@@ -101,8 +101,12 @@ typedef struct LrceGemmDesc {
   uint64_t drop_seed;
   /* f16 = 1: every 16-bit tensor of the call (A, B, a 16-bit C, aux_out, the DGELU aux) is IEEE
    * fp16 instead of bf16 and the MFMAs are the f16 forms (v_mfma_f32_*_f16): the BERT forward runs
-   * in fp16 like the reference's fp16 autocast (agent_oe.py:28).  bf16 x bf16 LDS-DMA path only. */
+   * in fp16 like the reference's fp16 autocast (agent_oe.py:28), and its backward in fp16 on scaled
+   * gradients like the reference's GradScaler (agent_oe.py:40-42).  bf16 x bf16 LDS-DMA path only. */
   int32_t f16;
+  /* Non-NULL: alpha is read from this device float instead of `alpha` (the inverse of a gradient
+   * scale lrce_grad_scale computed on the GPU).  LDS-DMA and register-staged bf16/fp16 paths. */
+  const float* alpha_dev;
 } LrceGemmDesc;
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);
@@ -267,10 +271,11 @@ typedef struct LrceMhaDesc {
   float* dk2;
   float* dv2;
   int64_t ld_dkv2, stride_dkv2_b;
-  /* forward only: 1 = q, k, v and out are IEEE fp16 (BERT self-attention under the reference's
-   * fp16 autocast); f16 MFMA forms.  The backward reads bf16. */
+  /* 1 = q, k, v, out (and, in the backward, dout) are IEEE fp16 (BERT self-attention under the
+   * reference's fp16 autocast; the backward's dout a scaled fp16 gradient, its f32 dq / dk / dv carry
+   * the same scale); f16 MFMA forms.  Short self-attention path only (Lq = Lk <= 64). */
   int32_t f16;
-  /* single-query backward only: 1 = the first key segment's dK / dV rows are STORED, not accumulated
+  /* single-query or short self-attention backward: 1 = the first key segment's dK / dV rows are STORED, not accumulated
    * (every row has one writer in this launch and no earlier contribution: kv1_bdiv == 1 and a memory
    * that is distinct per call, e.g. the video tokens of one recurrent step) — no zero fill, no read. */
   int32_t dkv1_store;
@@ -409,7 +414,8 @@ typedef struct LrceDecSaBwd {
 } LrceDecSaBwd;
 int lrce_dec_sa_bwd(const LrceDecSaBwd* args, void* stream);
 /* LayerNorm parameter gradients over rows [rows][768] of every recurrent step at once (n_ln <= 3
- * LayerNorms): dgamma[c] += sum_r dy (x - mean) rstd, dbeta[c] += sum_r dy, rows in order. */
+ * LayerNorms): dgamma[c] += sum_r dy (x - mean) rstd, dbeta[c] += sum_r dy, rows in order; one of
+ * dgamma[k] / dbeta[k] may be NULL (frozen parameter). */
 int lrce_dec_ln_grads(const float* const* dy, const float* const* x, const float* const* mean, const float* const* rstd,
                       float* const* dgamma, float* const* dbeta, int n_ln, int rows, void* stream);
 /* Debug: phase timestamps (s_memrealtime, 100 MHz) of the four fused block kernels (k = sa_fwd, ca_fwd,
@@ -462,6 +468,16 @@ int lrce_dropout(const float* x, const float* res, float* y, uint16_t* y_bf16, i
                  int64_t group, void* stream);
 int lrce_dropout_bwd(const float* dy, float* dx, uint16_t* dx_bf16, int64_t n, float p, uint64_t seed, int64_t group,
                      void* stream);  /* dx and/or its bf16 copy dx_bf16 (either may be NULL) */
+/* GradScaler for the fp16 backward (the reference's torch.cuda.amp.GradScaler, agent_oe.py:40-42,
+ * per tensor instead of per step): scale[0] = S = 2^(7 - floor(log2(max|x|))) (max|x| * S in
+ * [128, 256); S = 1 for an all-zero or non-finite x), scale[1] = 1/S.  scale[2..3] are the kernel's
+ * arrival words: zero them once when allocating (the kernel leaves them zero).  n % 4 == 0, x 16-B
+ * aligned. */
+int lrce_grad_scale(const float* x, int64_t n, float* scale, void* stream);
+/* dx_f16 = fp16(scale[0] * dropout_bwd(dy)) (p = 0: a scaled cast): the fp16 operand of the BERT
+ * backward GEMMs from an f32 residual-stream gradient. */
+int lrce_dropout_bwd_f16(const float* dy, uint16_t* dx_f16, int64_t n, float p, uint64_t seed, int64_t group,
+                         const float* scale, void* stream);
 /* Device-side RNG offset for graph replay: every hash-based mask (lrce_dropout*, lrce_mha_* dropout)
  * uses seed + *offset when a device pointer is registered (NULL = 0, the default).  A captured
  * HIP graph bakes the host seeds; advancing *offset (one device add per training step) gives each

@@ -122,6 +122,85 @@ def test_mha_self_f16_forward(L):
     assert rel(out, ref.float()) < 2e-3
 
 
+def test_grad_scale_and_f16_operand():
+    """lrce_grad_scale: S = 2^(7 - floor(log2 max|x|)) (1 for zeros / non-finite), 1/S, arrival words
+    left zero (replayable); dropout_bwd_f16 = fp16(S * dropout_bwd)."""
+    k = K()
+    sc = torch.zeros(4, device=dev)
+    for amax in (3.0e-6, 0.75, 1.0, 5.0e3):
+        x = torch.randn(320 * 768, device=dev)
+        x = x / x.abs().max() * amax
+        k.grad_scale(x, sc)
+        torch.cuda.synchronize()
+        S = 2.0 ** (7 - math.floor(math.log2(amax)))
+        assert float(sc[0]) == S and float(sc[1]) == 1.0 / S, (amax, sc)
+        assert float(sc[2]) == 0.0 and float(sc[3]) == 0.0
+        assert 128.0 <= amax * S < 256.0
+        h = k.dropout_bwd_f16(x, 0.0, 0, sc)
+        assert torch.equal(h, (x * S).to(torch.float16))
+        hd = k.dropout_bwd_f16(x, 0.1, 7, sc)
+        ref = k.dropout_bwd(x, 0.1, 7)
+        assert rel(hd.float(), ref * S) < 1e-3
+    for bad in (torch.zeros(4096, device=dev), torch.full((4096,), float("nan"), device=dev)):
+        k.grad_scale(bad, sc)
+        torch.cuda.synchronize()
+        assert float(sc[0]) == 1.0 and float(sc[3]) == 0.0
+
+
+@pytest.mark.parametrize("M,N,Kd", [(320, 768, 768), (320, 3072, 768), (2000, 768, 3072)])
+def test_gemm_f16_backward_layouts(M, N, Kd):
+    """The fp16 BERT backward GEMMs: dX = dY W (B N-major) with dGELU or residual epilogues, dW = dY^T X
+    (both M/N-major) with the fused bias gradient, alpha read from device memory."""
+    k = K()
+    h = torch.float16
+    dy = (torch.randn(M, N, device=dev) * 100).to(h)          # a scaled gradient
+    W = (torch.randn(N, Kd, device=dev) / math.sqrt(Kd)).to(h)
+    X = torch.randn(M, Kd, device=dev).to(h)
+    inv = torch.tensor([1.0 / 128], device=dev)
+    res = torch.randn(M, Kd, device=dev)
+    dx = k.linear_dx(dy, W, resid=res, alpha_dev=inv)
+    ref = (dy.double() @ W.double()) / 128 + res.double()
+    assert rel(dx, ref.float()) < 1e-5
+    pre = torch.randn(M, Kd, device=dev).to(h)
+    dg = k.linear_dx(dy, W, out_f32=False, dgelu_pre=pre)
+    x = pre.double().requires_grad_(True)
+    gg = torch.autograd.grad((F.gelu(x) * (dy.double() @ W.double())).sum(), x)[0]
+    assert dg.dtype == h and rel(dg, gg.float()) < 2e-3
+    dw = torch.zeros(N, Kd, device=dev)
+    db = torch.zeros(N, device=dev)
+    k.linear_dw(dy, X, dw, bias_grad=db, alpha_dev=inv)
+    assert rel(dw, ((dy.double().t() @ X.double()) / 128).float()) < 1e-5
+    assert rel(db, (dy.double().sum(0) / 128).float()) < 1e-5
+
+
+@pytest.mark.parametrize("L", [32, 40])
+def test_mha_self_f16_backward(L):
+    """BERT self-attention backward with fp16 q/k/v/out and a scaled fp16 dout (the fp16 BERT
+    backward): vs fp64 autograd of masked SDPA; dK / dV stored (dkv1_store) into NaN-filled buffers."""
+    k = K()
+    B, H, D = 6, 12, 64
+    q, kk, v = (torch.randn(B * L, H * D, device=dev).to(torch.float16) for _ in range(3))
+    mask = torch.ones(B, L, dtype=torch.int32, device=dev)
+    mask[:, 20:] = 0
+    out = torch.empty(B * L, H * D, device=dev, dtype=torch.float16)
+    lse = torch.empty(B, H, L, device=dev)
+    desc = k.mha_desc(q, L, k1=kk, v1=v, lk1=L, ld_kv1=H * D, stride_kv1_b=L * H * D, key_mask=mask, out=out, lse=lse,
+                      B=B, H=H, scale=0.125)
+    k.mha_fwd(desc, out)
+    do = torch.randn(B * L, H * D, device=dev)
+    S = 256.0
+    dq, dk_, dv = (torch.full((B * L, H * D), float("nan"), device=dev) for _ in range(3))
+    k.mha_bwd(desc, dout=(do * S).to(torch.float16), dq=dq, dk1=dk_, dv1=dv, ld_dkv1=H * D, stride_dkv1_b=L * H * D,
+              dkv1_store=True)
+    qh, kh, vh = (t.double().view(B, L, H, D).transpose(1, 2).requires_grad_(True) for t in (q, kk, v))
+    s = qh @ kh.transpose(-1, -2) * 0.125 + (1 - mask.double())[:, None, None, :] * -1e30
+    o = (s.softmax(-1) @ vh).transpose(1, 2).reshape(B * L, H * D)
+    gq, gk, gv = torch.autograd.grad(o, (qh, kh, vh), do.double() * S)
+    for got, ref in ((dq, gq), (dk_, gk), (dv, gv)):
+        ref = ref.transpose(1, 2).reshape(B * L, H * D).float()
+        assert torch.isfinite(got).all() and rel(got, ref) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,Kd", [(10, 768, 768), (50, 3072, 768), (45, 768, 3072), (128, 200, 96)])
 @pytest.mark.parametrize("a_km,b_km", [(1, 1), (1, 0), (0, 0)])
 def test_gemm_exact_f32_path(M, N, Kd, a_km, b_km):

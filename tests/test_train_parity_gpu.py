@@ -4,23 +4,25 @@ parameter gradients on the HIP path vs the CPU oracle's autograd on the same bat
 Workloads (dropout / DropPath off, train mode, so every tile / split-K depth the bench runs at
 these batch sizes is exercised — the split depth of a weight gradient depends on M = tokens):
   * msvd-qa-oe, bs 10, temporal scale 3, cross-entropy (agent_oe.py:35-36);
-  * tgif-transition 5-way MC, bs 9, multi-class hinge loss (agent_mc.py:20-41, margin 1).
+  * msrvtt-qa-oe, bs 10, L = 37, 1500 answers, cross-entropy (configs/msrvtt-qa-oe.json);
+  * tgif-transition 5-way MC, bs 9, multi-class hinge loss (agent_mc.py:20-41, margin 1);
+  * tgif-count, bs 10, L = 30, mean-squared error on the ReLU count (agent_count.py:35-44).
 The L2 regulariser's gradient reg * p / ||p|| (agent_base.py:103-108) is not a model-backward
 term: it is folded into the AdamW kernel and checked against torch there (test_ops_gpu.py).
 
 Every floating-point parameter is compared (783 tensors); tensors whose oracle gradient is exactly
 zero (BERT pooler, decoder self-attention q/k: softmax over one key) must be zero here too, and the
 analytically-zero BERT key biases (rounding noise on both sides) small against the query biases.
-Tolerance per tensor, as max|d| / max|ref| against the fp32 oracle: TOL[family] (3e-2: bf16
-GEMM operands and backward), or — for the
-tensors whose gradient the reference's own training numerics cannot resolve to that — the error the
-reference's fp16 autocast (agent_oe.py:28) makes on the same batch, from the committed fixture
-tests/golden/train_grad_yardstick.json (make_train_yardstick.py), or half the error of its bf16
-autocast (the dtype this path computes in) when that is larger.  Those are the LayerNorm and
-relative-position-bias gradients of the early Swin stages (sums over ~10^5 tokens with cancellation)
-and the top BERT layers' query / key gradients (near-uniform attention rows: the true dS is a small
-difference of large dP terms).  The oracle runs on the GPU box's host cores as the checker (about
-25 s / batch)."""
+
+Bar per tensor, as max|d| / max|ref| against the fp32 oracle: 3e-2, or twice the error the
+reference's own training numerics make on that tensor (fp16 autocast + GradScaler, restated on the
+CPU in tests/golden/make_train_yardstick.py; at most 0.028 on any tensor of these batches), or — for
+the Swin and fusion tensors, which this path computes with bf16 operands — the error of the same
+numerics in bf16; and NEVER above CAP = 0.1.  The BERT encoder runs fp16 forward and backward, like
+the reference, so its bar is the fp16 one (<= 0.056): its bf16 error would be up to 0.28 on the top
+layers' query / key gradients (near-uniform attention rows make them small differences of large
+terms), which the cap rejects.  The measured errors are written to $LRCE_PARITY_OUT (JSON) when set.
+The oracle runs on the GPU box's host cores as the checker (about 25 s / batch)."""
 import json
 import os
 
@@ -35,8 +37,9 @@ from oracle import weights as W
 
 pytestmark = pytest.mark.gpu
 
-CFG = {"msvd-qa-oe": ("oe", 1000, 32), "tgif-transition": ("mc", 1, 40)}
-WORKLOADS = [("msvd-qa-oe", 10), ("tgif-transition", 9)]
+CFG = {"msvd-qa-oe": ("oe", 1000, 32), "msrvtt-qa-oe": ("oe", 1500, 37), "tgif-transition": ("mc", 1, 40),
+       "tgif-count": ("count", 1, 30)}
+WORKLOADS = [("msvd-qa-oe", 10), ("msrvtt-qa-oe", 10), ("tgif-transition", 9), ("tgif-count", 10)]
 SEED = 31
 
 # max|d| / max|ref| per tensor family: bf16 GEMM operands and bf16 backward (Swin, BERT); the fusion
@@ -53,11 +56,23 @@ def _family(name):
     return "fusion"
 
 
-def _model(name):
+def _build(name):
     from lrce.models import e2e
     task, ncls, L = CFG[name]
-    cls = {"oe": e2e.E2EOpenEnded, "mc": e2e.E2EMultipleChoice}[task]
-    m = cls(768, ncls, 0.0, (7, 7), 1024, 5, [3], L)
+    cls = {"oe": e2e.E2EOpenEnded, "mc": e2e.E2EMultipleChoice, "count": e2e.E2ECount}[task]
+    return cls(768, ncls, 0.0, (7, 7), 1024, 5, [3], L)
+
+
+def recipe(name):
+    """(recipe state dict, task, text length) of a workload, without a GPU (the yardstick script)."""
+    m = _build(name)
+    filled = W.fill_state_dict({k: v for k, v in m.state_dict().items()}, 0)
+    return filled, CFG[name][0], CFG[name][2]
+
+
+def _model(name):
+    task = CFG[name][0]
+    m = _build(name)
     # train mode with every stochastic element off: DropPath (video_swin_ori.py:546), BERT dropout
     for layer in m.video_extractor.swin.layers:
         for blk in layer.blocks:
@@ -67,28 +82,49 @@ def _model(name):
     return m.cuda().train(), filled, task
 
 
-def _inputs(task, batch, L, seed):
+def _inputs(name, batch, seed):
+    task, ncls, L = CFG[name]
     clips = W.synthetic_clips(batch, 3, seed=seed)
     if task == "mc":
         ids, mask, types = W.synthetic_question(batch, L, seed=seed, n_choice=5, ans_tokens=8)
         label = torch.from_numpy(np.random.default_rng(seed).integers(0, 5, size=batch))
+    elif task == "count":
+        ids, mask, types = W.synthetic_question(batch, L, seed=seed)
+        label = torch.from_numpy(np.random.default_rng(seed).integers(1, 8, size=batch).astype(np.float32))
     else:
         ids, mask, types = W.synthetic_question(batch, L, seed=seed)
-        label = torch.from_numpy(np.random.default_rng(seed).integers(0, CFG["msvd-qa-oe"][1], size=batch))
+        label = torch.from_numpy(np.random.default_rng(seed).integers(0, ncls, size=batch))
     return clips, ids, mask, types, label
 
 
 def _loss(task, out, label):
+    """The agents' task losses: hinge (agent_mc.py:20-41, margin 1), mean MSE (agent_count.py:35-44),
+    cross-entropy (agent_oe.py:35-36)."""
     if task == "mc":
         from lrce.agent.agent_mc import hinge_loss
         return hinge_loss(out, label, 1.0)
+    if task == "count":
+        return F.mse_loss(out.float(), label.float())
     return F.cross_entropy(out.float(), label, ignore_index=-100)
 
 
-def _allow(tol, y):
-    """The bar of one tensor: its family tolerance, the reference's own fp16-autocast error, or half
-    its bf16-autocast error (we compute in bf16), whichever is largest."""
-    return max(tol, y.get("fp16", 0.0), 0.5 * y.get("bf16", 0.0))
+def oracle_loss(task, y, label):
+    if task == "mc":
+        return O.hinge_loss(y, label, 1.0)
+    if task == "count":
+        return F.mse_loss(y, label.float())
+    return F.cross_entropy(y, label, ignore_index=-100)
+
+
+CAP = 0.1
+
+
+def _allow(tol, y, fam):
+    """The bar of one tensor (module docstring): never above CAP."""
+    b = max(tol, 2.0 * y.get("fp16", 0.0))
+    if fam in ("swin", "fusion"):
+        b = max(b, y.get("bf16", 0.0))
+    return min(CAP, b)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -101,7 +137,7 @@ def _gpu():
 def test_baseline_train_step_grads_match_oracle(name, batch):
     m, filled, task = _model(name)
     L = CFG[name][2]
-    clips, ids, mask, types, label = _inputs(task, batch, L, seed=SEED)
+    clips, ids, mask, types, label = _inputs(name, batch, seed=SEED)
     m.zero_grad(set_to_none=True)
     y = m(clips.cuda(), ids.cuda(), mask.cuda(), types.cuda())
     loss = _loss(task, y, label.cuda())
@@ -116,11 +152,10 @@ def test_baseline_train_step_grads_match_oracle(name, batch):
     torch.set_num_threads(min(16, torch.get_num_threads()))
     sd = oracle_sd(filled, requires_grad=True)
     yr = O.e2e_forward(sd, clips, ids, mask, types, task)
-    if task == "mc":
-        lr_ = O.hinge_loss(yr, label, 1.0)
-    else:
-        lr_ = F.cross_entropy(yr, label, ignore_index=-100)
+    lr_ = oracle_loss(task, yr, label)
     lr_.backward()
+    if task == "count":
+        assert int((yr > 0).sum()) >= batch // 2, "count head: too few positive outputs for a gradient test"
     assert rel(y, yr) < 1e-2
     lr_v = float(lr_.detach())
     assert abs(loss - lr_v) < 1e-2 * max(1.0, abs(lr_v))
@@ -129,6 +164,7 @@ def test_baseline_train_step_grads_match_oracle(name, batch):
         yard = json.load(f)[f"{name}_b{batch}"]
     worst = {f: (0.0, "") for f in TOL}
     errs, bad = [], []
+    record = {}
     checked = 0
     for k, t in sd.items():
         if not t.is_floating_point():
@@ -144,13 +180,16 @@ def test_baseline_train_step_grads_match_oracle(name, batch):
             # both sides are rounding noise; bound ours by the query-bias gradient's scale
             qb = sd[k.replace("key.bias", "query.bias")].grad
             kb = float(g.abs().max()) / float(qb.abs().max())
-            if kb > _allow(2e-2, yard.get(k, {})):
-                bad.append((kb, k))
+            kbar = _allow(2e-2, yard.get(k, {}), "bert")
+            record[k] = {"err": round(kb, 6), "bar": round(kbar, 6), **yard.get(k, {})}
+            if kb > kbar:
+                bad.append((kb, kbar, k))
             continue
         e = rel(g, gr)
         fam = _family(k)
-        bar = _allow(TOL[fam], yard.get(k, {}))
+        bar = _allow(TOL[fam], yard.get(k, {}), fam)
         errs.append((e, bar, k))
+        record[k] = {"err": round(e, 6), "bar": round(bar, 6), **yard.get(k, {})}
         if e > bar:
             bad.append((e, bar, k))
         if e > worst[fam][0]:
@@ -160,6 +199,12 @@ def test_baseline_train_step_grads_match_oracle(name, batch):
     for e, bar, k in sorted(errs, reverse=True)[:40]:
         print(f"  {e:.3e} (bar {bar:.3e})  {k}")
     n_yard = sum(1 for e, bar, k in errs if e > TOL[_family(k)])
-    print(f"  {n_yard} tensors above the family bar, within the fp16-autocast yardstick")
+    print(f"  {n_yard} tensors above 3e-2, within their yardstick bar (<= {CAP})")
+    out = os.environ.get("LRCE_PARITY_OUT")
+    if out:
+        allrec = json.load(open(out)) if os.path.exists(out) else {}
+        allrec[f"{name}_b{batch}"] = {"loss": loss, "loss_ref": lr_v, "logits_rel": rel(y, yr), "tensors": record}
+        with open(out, "w") as f:
+            json.dump(allrec, f, indent=0, sort_keys=True)
     assert checked > 500
     assert not bad, bad

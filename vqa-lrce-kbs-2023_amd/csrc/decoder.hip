@@ -1035,7 +1035,7 @@ __global__ void __launch_bounds__(NT, 1) dec_sa_bwd_kernel(SaBwdP p) {
 // ------------------------------------------------------------------ deferred LayerNorm parameter grads
 // dgamma[c] += sum_r dy[r][c] (x[r][c] - mean[r]) rstd[r],  dbeta[c] += sum_r dy[r][c]  over the R = S*B
 // rows of every recurrent step (one owner per column, rows in order: deterministic).  blockIdx.y picks
-// one of up to 3 LayerNorms.
+// one of up to 3 LayerNorms; a NULL dgamma or dbeta (frozen parameter) is skipped.
 struct LnGradP {
   const float* dy[3];
   const float* x[3];
@@ -1054,8 +1054,8 @@ __global__ void __launch_bounds__(256) dec_ln_grads_kernel(LnGradP p) {
     sg += d * (p.x[k][(long long)r * E + c] - p.mean[k][r]) * p.rstd[k][r];
     sb += d;
   }
-  p.dgamma[k][c] += sg;
-  p.dbeta[k][c] += sb;
+  if (p.dgamma[k]) p.dgamma[k][c] += sg;
+  if (p.dbeta[k]) p.dbeta[k][c] += sb;
 }
 
 template <typename P>
@@ -1160,7 +1160,8 @@ extern "C" int lrce_dec_ln_grads(const float* const* dy, const float* const* x, 
   if (n_ln < 1 || n_ln > 3 || rows < 1) return lrce_fail(LRCE_E_ARG, "dec_ln_grads: n_ln=%d rows=%d", n_ln, rows);
   LnGradP p{};
   for (int k = 0; k < n_ln; ++k) {
-    if (!dy[k] || !x[k] || !mean[k] || !rstd[k] || !dgamma[k] || !dbeta[k]) return lrce_fail(LRCE_E_ARG, "dec_ln_grads: null pointer");
+    if (!dy[k] || !x[k] || !mean[k] || !rstd[k] || (!dgamma[k] && !dbeta[k]))
+      return lrce_fail(LRCE_E_ARG, "dec_ln_grads: null pointer (one of dgamma / dbeta may be NULL, not both)");
     p.dy[k] = dy[k]; p.x[k] = x[k]; p.mean[k] = mean[k]; p.rstd[k] = rstd[k]; p.dgamma[k] = dgamma[k]; p.dbeta[k] = dbeta[k];
   }
   p.rows = rows;

@@ -161,6 +161,63 @@ __global__ void dropout_bwd_kernel(const float* __restrict__ dy, float* __restri
   if (dx16) dx16[i] = f2bf(v);
 }
 
+// GradScaler restated per tensor for the fp16 backward (agent_oe.py:40-42): max|x| over the grid
+// (NaN-propagating), then the last block to arrive turns it into a power-of-two scale.  The arrival
+// words live in scale[2..3] (agent-scope atomics on both sides; the last block resets them).
+__global__ void __launch_bounds__(256) grad_scale_kernel(const float* __restrict__ x, long long n4, float* scale) {
+  unsigned* words = reinterpret_cast<unsigned*>(scale + 2);
+  __shared__ float red[4];
+  float m = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    const float a[4] = {fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m = (a[e] > m || a[e] != a[e]) ? a[e] : m;   // NaN sticks
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float t = __shfl_xor(m, o, 64);
+    m = (t > m || t != t) ? t : m;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) m = (red[w] > m || red[w] != red[w]) ? red[w] : m;
+    // |x| bit patterns order like the values (NaN above +inf)
+    __hip_atomic_fetch_max(&words[0], __float_as_uint(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (__hip_atomic_fetch_add(&words[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      const unsigned bits = __hip_atomic_fetch_max(&words[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int e = (int)((bits >> 23) & 0xFF) - 127;          // floor(log2(max|x|)) for a normal max
+      float s = 1.f;
+      if (bits != 0 && e < 128 && e > -127) s = ldexpf(1.f, min(100, max(-100, 7 - e)));
+      scale[0] = s;
+      scale[1] = 1.f / s;
+      __hip_atomic_store(&words[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&words[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ void dropout_bwd_f16_kernel(const float* __restrict__ dy, f16* __restrict__ dx, long long n, float p, uint64_t seed,
+                                       long long group, const uint64_t* __restrict__ off, const float* __restrict__ scale) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  const float s = scale[0] / (p > 0.f ? 1.0f - p : 1.0f);
+  const float4 v = *reinterpret_cast<const float4*>(dy + i);
+  float o[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+  if (p > 0.f) {
+    const uint64_t sd = lrce_seed(seed, off);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = lrce_uniform(sd, (i + e) / group) >= p ? o[e] : 0.f;
+  }
+  typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+  f16x4 h;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) h[e] = (f16)o[e];
+  *reinterpret_cast<f16x4*>(dx + i) = h;
+}
+
 // ---------------------------------------------------------------- embeddings
 // BERT: out[r][c] = word[ids[r]][c] + pos[r % L][c] + type[types[r]][c]
 __global__ void bert_embed_kernel(const long long* __restrict__ ids, const long long* __restrict__ types, const float* __restrict__ word,
@@ -404,6 +461,28 @@ extern "C" int lrce_dropout_bwd(const float* dy, float* dx, uint16_t* dx_bf16, i
   dropout_bwd_kernel<<<(n + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(
       dy, dx, reinterpret_cast<bf16*>(dx_bf16), n, p, seed, group, lrce_rng_offset());
   return lrce_check_launch("dropout_bwd");
+}
+
+extern "C" int lrce_grad_scale(const float* x, int64_t n, float* scale, void* stream) {
+  if (!x || !scale) return lrce_fail(LRCE_E_ARG, "grad_scale: null pointer");
+  if ((n & 3) || (reinterpret_cast<uintptr_t>(x) & 15)) return lrce_fail(LRCE_E_ARG, "grad_scale: n %% 4 != 0 or x not 16-B aligned");
+  const long long n4 = n / 4;
+  const unsigned blocks = (unsigned)std::max<long long>(1, std::min<long long>(256, (n4 + 2047) / 2048));
+  grad_scale_kernel<<<blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(x, n4, scale);
+  return lrce_check_launch("grad_scale");
+}
+
+extern "C" int lrce_dropout_bwd_f16(const float* dy, uint16_t* dx_f16, int64_t n, float p, uint64_t seed, int64_t group,
+                                    const float* scale, void* stream) {
+  if (!dy || !dx_f16 || !scale) return lrce_fail(LRCE_E_ARG, "dropout_bwd_f16: null pointer");
+  if ((n & 3) || ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(dx_f16)) & 7))
+    return lrce_fail(LRCE_E_ARG, "dropout_bwd_f16: n %% 4 != 0 or unaligned buffers");
+  if (n <= 0) return LRCE_OK;
+  if (group < 1) group = 1;
+  const long long thr = n / 4;
+  dropout_bwd_f16_kernel<<<(unsigned)((thr + 255) / 256), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      dy, reinterpret_cast<f16*>(dx_f16), n, p, seed, group, lrce_rng_offset(), scale);
+  return lrce_check_launch("dropout_bwd_f16");
 }
 
 extern "C" int lrce_bert_embed_fwd(const int64_t* ids, const int64_t* types, const float* word, const float* pos, const float* typ,

@@ -51,7 +51,10 @@ struct GemmP {
   float* ws; // split-K slabs [split][m][n] (plain stores, reduced by splitk_reduce_kernel), or null
   int f16;   // 16-bit tensors are IEEE fp16 (LrceGemmDesc.f16)
   int group_m;   // tile raster: groups of group_m tile rows, column-major inside a group (1 = row-major)
+  const float* alpha_dev;   // non-null: alpha read from device memory (a gradient scale computed on the GPU)
 };
+
+__device__ __forceinline__ float alpha_of(const GemmP& p) { return p.alpha_dev ? *p.alpha_dev : p.alpha; }
 
 // Tile (tm, tn) of linear index lin (already XCD-remapped: each XCD owns a contiguous lin range).
 // Grouped order: a group is group_m tile rows x all tile columns, walked column by column, so the
@@ -169,7 +172,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 __device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row, int m, int nn, bool first, float rs,
                                           char* cbase) {
   const int fl = p.flags;
-  x = x * p.alpha + (((fl & LRCE_EPI_BIAS) && first) ? p.bias[nn] : 0.f);
+  x = x * alpha_of(p) + (((fl & LRCE_EPI_BIAS) && first) ? p.bias[nn] : 0.f);
   x *= (nn < p.scale_cols) ? p.scale_val : 1.f;
   if (fl & LRCE_EPI_GELU) {
     if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + nn] = to16r(x, p.f16);
@@ -202,9 +205,10 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
   if (row < 0) return;   // c_map -1: a padded window position (no output row)
   const bool first = sk == 0;
   if (p.vec && n + 8 <= p.n) {
-    if (p.alpha != 1.f) {
+    const float al = alpha_of(p);
+    if (al != 1.f) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+      for (int e = 0; e < 8; ++e) v[e] *= al;
     }
     if ((fl & LRCE_EPI_BIAS) && first) {
       const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n), b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
@@ -640,7 +644,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
 #pragma unroll
     for (int i = 0; i < IM; ++i) {
       const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      if (m < p.m) __hip_atomic_fetch_add(db + m, p.alpha * accb[i][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (m < p.m) __hip_atomic_fetch_add(db + m, alpha_of(p) * accb[i][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   char* cbase = static_cast<char*>(p.c) +
@@ -719,6 +723,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     // split-K slab: this slice's alpha * partial tile, plain stores (reduced by splitk_reduce_kernel)
     float* slab = p.ws + (long long)sk * p.m * p.n;
     const bool vec4 = (p.n & 3) == 0;
+    const float al = alpha_of(p);
     static_for<IM>([&](auto ic) {
       uint32_t u[JN][4];
       transpose(ic, u);
@@ -728,8 +733,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
 #pragma unroll
         for (int j = 0; j < JN; ++j) {
           const int n = ncol + 4 * j;
-          const float4 v = make_float4(__uint_as_float(u[j][0]) * p.alpha, __uint_as_float(u[j][1]) * p.alpha,
-                                       __uint_as_float(u[j][2]) * p.alpha, __uint_as_float(u[j][3]) * p.alpha);
+          const float4 v = make_float4(__uint_as_float(u[j][0]) * al, __uint_as_float(u[j][1]) * al,
+                                       __uint_as_float(u[j][2]) * al, __uint_as_float(u[j][3]) * al);
           if (vec4 && n + 4 <= p.n) {
             *reinterpret_cast<float4*>(row + n) = v;
           } else {
@@ -835,7 +840,7 @@ extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
   g.flags &= ~LRCE_EPI_BIAS_GRAD;
   g.bias = nullptr;
   if (int rc = gemm_dispatch(&g, stream)) return rc;
-  if (d->alpha != 1.0f) return lrce_fail(LRCE_E_ARG, "gemm: BIAS_GRAD with alpha != 1");
+  if (d->alpha != 1.0f || d->alpha_dev) return lrce_fail(LRCE_E_ARG, "gemm: BIAS_GRAD with alpha != 1 off the fused paths");
   return lrce_colsum(d->a, d->a_f32, d->a_map, d->lda, d->k, d->m, d->a_row_scale, d->a_rows_per_scale,
                      const_cast<float*>(d->bias), stream);
 }
@@ -856,7 +861,10 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   if ((d->flags & (LRCE_EPI_DGELU | LRCE_EPI_RESID)) && !d->aux) return lrce_fail(LRCE_E_ARG, "gemm: aux missing");
   if ((d->flags & (LRCE_EPI_AUX_OUT | LRCE_EPI_OUT_BOTH)) && !d->aux_out) return lrce_fail(LRCE_E_ARG, "gemm: aux_out missing");
   if ((d->flags & LRCE_EPI_BIAS) && !d->bias) return lrce_fail(LRCE_E_ARG, "gemm: bias missing");
-  if (d->b_f32) return lrce_gemm_f32(d, stream);
+  if (d->b_f32) {
+    if (d->alpha_dev) return lrce_fail(LRCE_E_ARG, "gemm: alpha_dev is not supported on the f32 / fp16-weight skinny path");
+    return lrce_gemm_f32(d, stream);
+  }
   // vector loads need the contiguous dim of every operand to be a multiple of 8 elements
   if (d->a_kmajor ? (d->k % 8) : (d->m % 8)) return lrce_fail(LRCE_E_ARG, "gemm: A contiguous dim %% 8 != 0");
   if (d->b_kmajor ? (d->k % 8) : (d->n % 8)) return lrce_fail(LRCE_E_ARG, "gemm: B contiguous dim %% 8 != 0");
@@ -881,7 +889,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   p.bias = d->bias; p.aux = d->aux; p.ld_aux = d->ld_aux;
   p.aux_out = static_cast<bf16*>(d->aux_out); p.ld_aux_out = d->ld_aux_out;
   p.a_map = d->a_map; p.c_map = d->c_map;
-  p.alpha = d->alpha; p.scale_cols = d->scale_cols; p.scale_val = d->scale_val;
+  p.alpha = d->alpha; p.alpha_dev = d->alpha_dev; p.scale_cols = d->scale_cols; p.scale_val = d->scale_val;
   p.row_scale = d->row_scale; p.rows_per_scale = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
   p.a_row_scale = d->a_row_scale; p.a_rows_per_scale = d->a_rows_per_scale > 0 ? d->a_rows_per_scale : 1;
   if (p.a_row_scale && !d->a_f32) return lrce_fail(LRCE_E_ARG, "gemm: a_row_scale needs f32 A");
@@ -898,8 +906,8 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   (void)out32;
   p.ws = nullptr;
   p.f16 = d->f16 ? 1 : 0;
-  if (p.f16 && !(glds_ok(d) && d->a_kmajor && d->b_kmajor))
-    return lrce_fail(LRCE_E_ARG, "gemm: f16 needs 16-B aligned K-major bf16-layout operands (LDS-DMA path)");
+  if (p.f16 && !glds_ok(d))
+    return lrce_fail(LRCE_E_ARG, "gemm: f16 needs 16-B aligned bf16-layout operands (LDS-DMA path)");
   const bool use_ws = d->workspace && split > 1 && (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)) == 0 &&
                       (d->flags & LRCE_EPI_ATOMIC) && d->batch == 1 && !d->c_map && !d->row_scale && d->scale_cols == 0 &&
                       d->n % 4 == 0 && d->ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(d->c) & 15) == 0 &&
@@ -944,6 +952,14 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
         case 32 + 19: gemm_glds_kernel<160, 128, true, true, true, S><<<grid, NT, 0, s>>>(p); break;
         case 32 + 3: gemm_glds_kernel<128, 128, true, true, true, S><<<grid, NT, 0, s>>>(p); break;
         case 32 + 7: gemm_glds_kernel<64, 64, true, true, true, S><<<grid, NT, 0, s>>>(p); break;
+        // fp16 backward (BERT, scaled gradients): dX = dY W (B N-major) and dW = dY^T X (both M/N-major)
+        case 32 + 10: gemm_glds_kernel<192, 128, true, false, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 18: gemm_glds_kernel<160, 128, true, false, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 2: gemm_glds_kernel<128, 128, true, false, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 6: gemm_glds_kernel<64, 64, true, false, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 0: gemm_glds_kernel<128, 128, false, false, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 4: gemm_glds_kernel<64, 64, false, false, true, S><<<grid, NT, 0, s>>>(p); break;
+        default: return lrce_fail(LRCE_E_ARG, "gemm: no LDS-DMA kernel for operand layout key %d", gk);
         case 11: gemm_glds_kernel<192, 128, true, true, false, S><<<grid, NT, 0, s>>>(p); break;
         case 10: gemm_glds_kernel<192, 128, true, false, false, S><<<grid, NT, 0, s>>>(p); break;
         case 19: gemm_glds_kernel<160, 128, true, true, false, S><<<grid, NT, 0, s>>>(p); break;
@@ -959,7 +975,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
       }
     };
     // two stages: a third (one resident workgroup per CU) measured 1.3-1.5x slower on every step shape
-    launch(std::integral_constant<int, 2>{});
+    if (int rc = launch(std::integral_constant<int, 2>{})) return rc;
     if (p.ws) {
       const long long q4 = (long long)d->m * d->n / 4;
       if (split >= 8)

@@ -532,7 +532,7 @@ struct MhaLBwdLds {
   float delta[LP];
 };
 
-template <int NTL>
+template <int NTL, bool F16>
 __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
   constexpr int LP = 32 * NTL;
   const LrceMhaDesc& d = P.d;
@@ -556,8 +556,8 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
   const int hh = lane >> 5, r32 = lane & 31;
   const int* km = d.key_mask ? d.key_mask + (long long)b * L : nullptr;
   const float c2 = d.scale * LOG2E_F;
-  // Pass 1: this kernel's own softmax statistics.  The forward ran on fp16 operands; its lse and O
-  // do not match the scores recomputed here from bf16 Q / K, and a normalisation that does not sum
+  // Pass 1: this kernel's own softmax statistics.  Its lse and O need not match the scores
+  // recomputed here (a bf16 backward of the fp16 forward; or the forward's dropout-free rounding), and a normalisation that does not sum
   // to one over the recomputed scores (or delta = dO.O from another P) leaves sum_j dS_ij != 0,
   // which swamps the small true dS of near-uniform attention rows.  So: per query row, max and sum
   // of the recomputed scores (whole row: L <= 64 keys) and delta_i = sum_j P_ij f_ij dP_ij from the
@@ -577,8 +577,8 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
         const bf16x8 ga = *reinterpret_cast<const bf16x8*>(S.dout + qi * D + 16 * s + 8 * hh);
         const bf16x8 kk = *reinterpret_cast<const bf16x8*>(S.k + key * D + 16 * s + 8 * hh);
         const bf16x8 vv = key < L ? ldrow16(vb + key * d.ld_kv1 + 16 * s + 8 * hh) : bf16x8{};
-        st[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qa, st[kt], 0, 0, 0);
-        dpt[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, ga, dpt[kt], 0, 0, 0);
+        st[kt] = mfma32x32x16<F16>(kk, qa, st[kt]);
+        dpt[kt] = mfma32x32x16<F16>(vv, ga, dpt[kt]);
       }
     }
     float m = -1.0e30f;
@@ -632,8 +632,8 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
       for (int s = 0; s < 4; ++s) {
         const bf16x8 qa = *reinterpret_cast<const bf16x8*>(S.q + (qt * 32 + r32) * D + 16 * s + 8 * hh);
         const bf16x8 ga = *reinterpret_cast<const bf16x8*>(S.dout + (qt * 32 + r32) * D + 16 * s + 8 * hh);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[s], dp, 0, 0, 0);
+        sacc = mfma32x32x16<F16>(qa, kf[s], sacc);
+        dp = mfma32x32x16<F16>(ga, vf[s], dp);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -645,11 +645,11 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 pa = pack8f(sacc, s), da = pack8f(dp, s);
+        const bf16x8 pa = pack8t<F16>(sacc, s), da = pack8t<F16>(dp, s);
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
-          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, tr_perm64(S.dout, qt * 32 + 16 * s, 32 * dt, lane), dv[dt], 0, 0, 0);
-          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, tr_perm64(S.q, qt * 32 + 16 * s, 32 * dt, lane), dk[dt], 0, 0, 0);
+          dv[dt] = mfma32x32x16<F16>(pa, tr_perm64(S.dout, qt * 32 + 16 * s, 32 * dt, lane), dv[dt]);
+          dk[dt] = mfma32x32x16<F16>(da, tr_perm64(S.q, qt * 32 + 16 * s, 32 * dt, lane), dk[dt]);
         }
       }
       // dS^T -> LDS T[key][query], then dQ[qt] += dS K
@@ -657,7 +657,7 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
       for (int rr = 0; rr < 4; ++rr) {
         bf16x4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = f2bf(dp[4 * rr + e]);
+        for (int e = 0; e < 4; ++e) v[e] = to16<F16>(dp[4 * rr + e]);
         *reinterpret_cast<bf16x4*>(S.t + r32 * 32 + 8 * rr + 4 * hh) = v;
       }
       wave_lds_fence_m();
@@ -666,7 +666,7 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
         const bf16x8 a = tr_nat<32>(S.t, 16 * s, 0, lane);
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
-          dq[qt][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, tr_nat<D>(S.k, kt * 32 + 16 * s, 32 * dt, lane), dq[qt][dt], 0, 0, 0);
+          dq[qt][dt] = mfma32x32x16<F16>(a, tr_nat<D>(S.k, kt * 32 + 16 * s, 32 * dt, lane), dq[qt][dt]);
       }
       wave_lds_fence_m();
     }
@@ -678,8 +678,13 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
         const long long o = (long long)b * d.stride_dkv1_b + (long long)kk * d.ld_dkv1 + h * D + r32;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
-          d.dk1[o + 32 * dt] += dk[dt][r] * d.scale;
-          d.dv1[o + 32 * dt] += dv[dt][r];
+          if (d.dkv1_store) {
+            d.dk1[o + 32 * dt] = dk[dt][r] * d.scale;
+            d.dv1[o + 32 * dt] = dv[dt][r];
+          } else {
+            d.dk1[o + 32 * dt] += dk[dt][r] * d.scale;
+            d.dv1[o + 32 * dt] += dv[dt][r];
+          }
         }
       }
     }
@@ -753,14 +758,20 @@ extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
 
 extern "C" int lrce_mha_bwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, true)) return rc;
-  if (d->f16) return lrce_fail(LRCE_E_ARG, "mha_bwd: the backward reads bf16 (cast the fp16 forward tensors)");
-  if (d->dkv1_store && (d->Lq != 1 || d->kv1_bdiv != 1 || !aligned_rows(d)))
-    return lrce_fail(LRCE_E_ARG, "mha_bwd: dkv1_store needs the single-query path with kv1_bdiv == 1");
+  if (d->f16 && !short_self(d)) return lrce_fail(LRCE_E_ARG, "mha_bwd: f16 io only on the short self-attention path (Lq = Lk <= 64)");
+  if (d->dkv1_store && !short_self(d) && (d->Lq != 1 || d->kv1_bdiv != 1 || !aligned_rows(d)))
+    return lrce_fail(LRCE_E_ARG, "mha_bwd: dkv1_store needs the short self-attention path or the single-query path with kv1_bdiv == 1");
   MhaP p{*d, lrce_rng_offset()};
   if (short_self(d)) {
     const unsigned nb = (d->B * d->H + 1) / 2;
-    if (d->Lq <= 32) mhaL_bwd_kernel<1><<<nb, 128, 0, static_cast<hipStream_t>(stream)>>>(p);
-    else mhaL_bwd_kernel<2><<<nb, 128, 0, static_cast<hipStream_t>(stream)>>>(p);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (d->f16) {
+      if (d->Lq <= 32) mhaL_bwd_kernel<1, true><<<nb, 128, 0, st>>>(p);
+      else mhaL_bwd_kernel<2, true><<<nb, 128, 0, st>>>(p);
+    } else {
+      if (d->Lq <= 32) mhaL_bwd_kernel<1, false><<<nb, 128, 0, st>>>(p);
+      else mhaL_bwd_kernel<2, false><<<nb, 128, 0, st>>>(p);
+    }
     return lrce_check_launch("mha_bwd(mfma)");
   }
   if (d->Lq == 1 && aligned_rows(d)) {

@@ -50,7 +50,7 @@ class GemmDesc(ctypes.Structure):
         ("b_f32", ctypes.c_int32),
         ("workspace", ctypes.c_void_p), ("workspace_elems", ctypes.c_int64),
         ("drop_p", ctypes.c_float), ("drop_group", ctypes.c_int32), ("drop_seed", ctypes.c_uint64),
-        ("f16", ctypes.c_int32),
+        ("f16", ctypes.c_int32), ("alpha_dev", ctypes.c_void_p),
     ]
 
 
@@ -171,6 +171,8 @@ _SIGS = {
     "lrce_cast_f16_bf16": [_P, _P, _I64, _P],
     "lrce_dropout": [_P, _P, _P, _P, _I64, _F, _U64, _I64, _P],
     "lrce_dropout_bwd": [_P, _P, _P, _I64, _F, _U64, _I64, _P],
+    "lrce_grad_scale": [_P, _I64, _P, _P],
+    "lrce_dropout_bwd_f16": [_P, _P, _I64, _F, _U64, _I64, _P, _P],
     "lrce_bert_embed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_bert_embed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I64, _P],
     "lrce_video_posembed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],

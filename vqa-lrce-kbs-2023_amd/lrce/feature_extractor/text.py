@@ -10,7 +10,7 @@ branches in train mode) with the SAME parameter names (`bert.embeddings.*`, `ber
 buffer in 4.20, is accepted and ignored).  The pooler is kept for the schema but, as in the
 reference (its output is never used by the loss), not computed.  No network fetch: weights come
 from a checkpoint or the caller.  The encoder's forward operands are fp16 (the reference runs
-BERT under fp16 autocast), its backward bf16.
+BERT under fp16 autocast), its backward fp16 on scaled gradients (the reference's GradScaler).
 """
 import os
 import warnings
@@ -133,8 +133,8 @@ class _LayerFn(torch.autograd.Function):
 
     Forward GEMM / attention operands are IEEE fp16, as under the reference's fp16 autocast
     (agent_oe.py:28; bf16 here would put BERT's rounding error at ~1e-2 of the MC / Count logits).
-    Every 16-bit activation the backward needs lives in ONE fp16 buffer that the backward casts to
-    bf16 in one pass: the backward GEMMs keep bf16's range for the small gradients."""
+    Every 16-bit activation the backward needs lives in ONE fp16 buffer, read by the fp16 backward
+    as it stands (scaled gradients: backward's docstring)."""
 
     @staticmethod
     def forward(ctx, x, mask, layer, flat, p, seed, B, L, *params):
@@ -167,43 +167,60 @@ class _LayerFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        """fp16 backward on scaled gradients, as the reference trains (fp16 autocast + GradScaler,
+        agent_oe.py:28,40-42): each f32 residual-stream gradient entering a GEMM gets its own power-of-two
+        scale (lrce_grad_scale, on the device), the fp16 operands carry it, and the GEMMs that leave the
+        scaled domain (weight gradients, the dX GEMMs with an f32 residual) multiply by 1/S in their
+        epilogue.  bf16 here left the top layers' query / key gradients ~0.2 off (near-uniform attention
+        rows make them small differences of large terms); fp16 puts them at the reference's own error."""
         buf, mask, lse, a2, m1, r1, o2, m2, r2 = ctx.save
         layer, flat, p, seed, B, L = ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L
         sa, ao, it, oo = layer.attention.self, layer.attention.output, layer.intermediate, layer.output
         rows = B * L
-        b16 = torch.empty(buf.shape, dtype=torch.bfloat16, device=buf.device)
-        K.cast_f16_bf16(buf, b16)
-        del buf
-        xb, q, k, v, ctxt, h1b, g, pre = _views(b16, rows)
+        xb, q, k, v, ctxt, h1b, g, pre = _views(buf, rows)   # fp16, as the forward wrote them
+        sc = _grad_scales(layer, dout.device)                # (S, 1/S) of the FFN and attention gradients
+        inv_f, inv_a = sc[0, 1:2], sc[1, 1:2]
+        w = flat.w16h
         dout = dout.contiguous()
         do2 = torch.empty_like(o2)
         K.layernorm_bwd(dout, o2, m2, r2, oo.LayerNorm.weight, do2, dw=_g(flat, oo.LayerNorm.weight),
                         db=_g(flat, oo.LayerNorm.bias))
-        # the backward GEMMs read bf16 gradients (glds MFMA path); residual sums stay f32
-        do = _grad16(do2, p, seed + 2)
-        _wgrad(flat, oo.dense, do, g)
-        dh1 = K.linear_dx(do, flat.w16(oo.dense.weight), out_f32=False, dgelu_pre=pre)   # d(pre), bf16
-        _wgrad(flat, it.dense, dh1, h1b)
-        dh1x = K.linear_dx(dh1, flat.w16(it.dense.weight), resid=do2)
+        K.grad_scale(do2, sc[0])
+        do = K.dropout_bwd_f16(do2, p, seed + 2, sc[0])                                   # S_f * d(o)
+        _wgrad(flat, oo.dense, do, g, inv_f)
+        dh1 = K.linear_dx(do, w(oo.dense.weight), out_f32=False, dgelu_pre=pre)           # S_f * d(pre)
+        _wgrad(flat, it.dense, dh1, h1b, inv_f)
+        dh1x = K.linear_dx(dh1, w(it.dense.weight), resid=do2, alpha_dev=inv_f)
         da2 = torch.empty_like(a2)
         K.layernorm_bwd(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, dw=_g(flat, ao.LayerNorm.weight),
                         db=_g(flat, ao.LayerNorm.bias))
-        da = _grad16(da2, p, seed + 1)
-        _wgrad(flat, ao.dense, da, ctxt)
-        dctx = K.linear_dx(da, flat.w16(ao.dense.weight), out_f32=False)
-        dqkv = torch.zeros(3, rows, HIDDEN, device=dout.device)
-        desc = K.mha_rebind(ctx.desc, q=q, k1=k, v1=v, out=ctxt)
-        K.mha_bwd(desc, dout=dctx, dq=dqkv[0], dk1=dqkv[1], dv1=dqkv[2], ld_dkv1=HIDDEN, stride_dkv1_b=L * HIDDEN)
-        dqkv16 = torch.empty(3, rows, HIDDEN, dtype=torch.bfloat16, device=dout.device)
-        K.cast_bf16(dqkv, dqkv16)
+        K.grad_scale(da2, sc[1])
+        da = K.dropout_bwd_f16(da2, p, seed + 1, sc[1])                                   # S_a * d(a)
+        _wgrad(flat, ao.dense, da, ctxt, inv_a)
+        dctx = K.linear_dx(da, w(ao.dense.weight), out_f32=False)                         # S_a * d(ctx)
+        dqkv = torch.empty(3, rows, HIDDEN, device=dout.device)
+        K.mha_bwd(ctx.desc, dout=dctx, dq=dqkv[0], dk1=dqkv[1], dv1=dqkv[2], ld_dkv1=HIDDEN, stride_dkv1_b=L * HIDDEN,
+                  dkv1_store=True)
+        dqkv16 = torch.empty(3, rows, HIDDEN, dtype=torch.float16, device=dout.device)
+        K.cast_f16(dqkv, dqkv16)
         for i, lin in enumerate((sa.query, sa.key, sa.value)):
-            _wgrad(flat, lin, dqkv16[i], xb)
-        dx = K.linear_dx(dqkv16[0], flat.w16(sa.query.weight), resid=da2)
-        K.linear_dx(dqkv16[1], flat.w16(sa.key.weight), out=dx, accumulate=True)
-        K.linear_dx(dqkv16[2], flat.w16(sa.value.weight), out=dx, accumulate=True)
+            _wgrad(flat, lin, dqkv16[i], xb, inv_a)
+        dx = K.linear_dx(dqkv16[0], w(sa.query.weight), resid=da2, alpha_dev=inv_a)
+        K.linear_dx(dqkv16[1], w(sa.key.weight), out=dx, accumulate=True, alpha_dev=inv_a)
+        K.linear_dx(dqkv16[2], w(sa.value.weight), out=dx, accumulate=True, alpha_dev=inv_a)
         ctx.save = ctx.desc = None
         flat.notify(layer.parameters())
         return (dx,) + (None,) * (7 + len(ctx.needs_input_grad[8:]))
+
+
+def _grad_scales(layer, dev):
+    """The layer's two gradient-scale slots [2, 4] f32 (S, 1/S, two arrival words zeroed once: the
+    lrce_grad_scale contract), allocated on first use and kept (graph replays reuse them)."""
+    sc = getattr(layer, "_lrce_grad_scales", None)
+    if sc is None or sc.device != dev:
+        sc = torch.zeros(2, 4, device=dev)
+        object.__setattr__(layer, "_lrce_grad_scales", sc)
+    return sc
 
 
 def _views(buf, rows):
@@ -224,14 +241,20 @@ def _grad16(d32, p, seed):
     return out
 
 
-def _wgrad(flat, lin, dy, x16):
-    """dW += dY^T X with the bias gradient (column sums of dY) fused into the same GEMM."""
+def _wgrad(flat, lin, dy, x16, inv_scale=None):
+    """dW += dY^T X with the bias gradient (column sums of dY) fused into the same GEMM; inv_scale (a
+    device f32): dY carries a gradient scale, both sums are multiplied by it."""
     gw = _g(flat, lin.weight)
     gb = _g(flat, lin.bias) if lin.bias is not None else None
     if gw is not None:
-        K.linear_dw(dy, x16, gw, bias_grad=gb)
+        K.linear_dw(dy, x16, gw, bias_grad=gb, alpha_dev=inv_scale)
     elif gb is not None:
-        K.colsum(dy, gb)
+        if inv_scale is None:
+            K.colsum(dy, gb)
+        else:   # frozen weight, trainable bias of a scaled gradient (not on the training path)
+            t = torch.zeros_like(gb)
+            K.colsum(dy, t)
+            gb.add_(t * inv_scale)
 
 
 class BertModel(nn.Module):

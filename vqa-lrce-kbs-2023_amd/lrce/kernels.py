@@ -103,11 +103,12 @@ def _chk(t, dtype=None, name="tensor"):
 def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, flags=0, bias=None,
          aux=None, ld_aux=0, aux_out=None, ld_aux_out=0, a_map=None, c_map=None, alpha=1.0, split_k=1,
          scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, a_row_scale=None, a_rows_per_scale=1,
-         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None, f16=False, ln=None):
+         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None, f16=False, ln=None, alpha_dev=None):
     """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc.  drop = (p, seed, group):
     nn.Dropout fused into the epilogue (exact-f32 skinny path; same mask as dropout()).  f16: every
     16-bit tensor (A, B, 16-bit C, aux_out) is torch.float16 (the BERT forward).  ln: a LayerNorm
-    prologue on A (ln_fwd_prologue / ln_bwd_prologue -> lrce_gemm_ln)."""
+    prologue on A (ln_fwd_prologue / ln_bwd_prologue -> lrce_gemm_ln).  alpha_dev: a device f32 read
+    as alpha (the inverse gradient scale of grad_scale())."""
     _chk(a, None, "A"); _chk(b, None, "B"); _chk(c, None, "C")
     a_f32 = a.dtype == F32
     b_f32 = b.dtype == F32
@@ -136,6 +137,9 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.a_row_scale, d.a_rows_per_scale = ptr(a_row_scale), a_rows_per_scale
     d.b_f32 = 2 if b_half else int(b_f32)
     d.f16 = int(f16)
+    if alpha_dev is not None:
+        _chk(alpha_dev, F32, "alpha_dev")
+        d.alpha_dev = ptr(alpha_dev)
     if workspace is not None:
         d.workspace, d.workspace_elems = ptr(workspace), workspace.numel()
     if drop is not None and drop[0] > 0:
@@ -231,14 +235,17 @@ def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None
 
 
 def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows=None, a_row_scale=None,
-              a_rows_per_scale=1, accumulate=False, resid=None, drop=None, ln=None):
+              a_rows_per_scale=1, accumulate=False, resid=None, drop=None, ln=None, alpha_dev=None):
     """dX = dY W (+ resid) ; dY [M,N] (bf16/f32), W [N,K] bf16 -> [M,K]; optional *gelu'(pre), and
-    drop = (p, seed, group): the dropout backward mask (fused on the skinny path, else a launch)."""
+    drop = (p, seed, group): the dropout backward mask (fused on the skinny path, else a launch).
+    fp16 dY and W (the BERT backward): fp16 MFMAs, a 16-bit output is fp16; alpha_dev scales the
+    product before the residual (the inverse gradient scale)."""
     M = rows if rows is not None else dy.shape[0]
     if drop is not None and drop[0] > 0 and ln is None and not (_skinny_drop_ok(dy, w, M, a_map) and not accumulate
                                                                 and resid is None and a_row_scale is None):
         y = linear_dx(dy, w, out=out, out_f32=out_f32, dgelu_pre=dgelu_pre, a_map=a_map, rows=rows,
-                      a_row_scale=a_row_scale, a_rows_per_scale=a_rows_per_scale, accumulate=accumulate, resid=resid)
+                      a_row_scale=a_row_scale, a_rows_per_scale=a_rows_per_scale, accumulate=accumulate, resid=resid,
+                      alpha_dev=alpha_dev)
         return dropout_bwd(y, drop[0], drop[1], out=y, group=drop[2])
     Nn, K = w.shape
     flags = 0
@@ -247,19 +254,22 @@ def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows
     if resid is not None:
         assert dgelu_pre is None
         flags |= N.EPI_RESID
+    f16 = dy.dtype == F16 and w.dtype == F16
     if out is None:
-        out = torch.empty((M, K), dtype=F32 if out_f32 else BF16, device=dy.device)
+        out = torch.empty((M, K), dtype=F32 if out_f32 else (F16 if f16 else BF16), device=dy.device)
     if out.dtype == F32:
         flags |= N.EPI_ACCUM if accumulate else N.EPI_OUT_F32
     gemm(dy, w, out, M, K, Nn, a_kmajor=True, b_kmajor=False, lda=dy.shape[-1], ldb=K, flags=flags,
          aux=dgelu_pre if dgelu_pre is not None else resid, ld_aux=K, a_map=a_map, a_row_scale=a_row_scale,
-         a_rows_per_scale=a_rows_per_scale, drop=drop, ln=ln)
+         a_rows_per_scale=a_rows_per_scale, drop=drop, ln=ln, f16=f16, alpha_dev=alpha_dev)
     return out
 
 
-def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_scale=1, bias_grad=None):
+def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_scale=1, bias_grad=None,
+              alpha_dev=None):
     """dW[N,K] += dY^T X ; dY [M,N] (bf16/f32, rows optionally gathered by a_map), X [M,K] bf16.
-    bias_grad: also db[N] += colsum(dY) (fused into the skinny f32 path, a column-sum launch otherwise)."""
+    bias_grad: also db[N] += colsum(dY) (fused into the skinny f32 path, a column-sum launch otherwise).
+    fp16 dY and X (the BERT backward): fp16 MFMAs; alpha_dev = the inverse gradient scale (device)."""
     M = rows if rows is not None else x.shape[0]
     Nn = dw.shape[0]
     K = dw.shape[1]
@@ -268,11 +278,12 @@ def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_
     # per-slice f32 slabs in a workspace + one reduce launch (bf16 operands), atomics otherwise
     flags = (N.EPI_ATOMIC if split > 1 else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if bias_grad is not None else 0)
     ws = None
-    if split > 1 and dy.dtype == BF16 and x.dtype == BF16:
+    f16 = dy.dtype == F16 and x.dtype == F16
+    if split > 1 and ((dy.dtype == BF16 and x.dtype == BF16) or f16):
         ws = torch.empty(split * Nn * K, dtype=F32, device=dw.device)
     gemm(dy, x, dw, Nn, K, M, a_kmajor=False, b_kmajor=False, lda=dy.shape[-1], ldb=x.shape[-1], ldc=K,
          flags=flags, bias=bias_grad, a_map=a_map, split_k=split, a_row_scale=a_row_scale,
-         a_rows_per_scale=a_rows_per_scale, workspace=ws)
+         a_rows_per_scale=a_rows_per_scale, workspace=ws, f16=f16, alpha_dev=alpha_dev)
 
 
 def colsum(x, out, *, row_map=None, rows=None, row_scale=None, rows_per_scale=1):
@@ -547,10 +558,12 @@ def dec_sa_bwd(dx1, x1p, mean1, rstd1, g1, wo, wv, *, dsao_out, dsav_out, dx0_ou
 
 def dec_ln_grads(items, rows):
     """items: up to 3 (dy, x, mean, rstd, dgamma, dbeta) over `rows` rows of 768: dgamma += sum dy xhat,
-    dbeta += sum dy (LayerNorm parameter gradients of every recurrent step at once)."""
+    dbeta += sum dy (LayerNorm parameter gradients of every recurrent step at once); either of dgamma /
+    dbeta may be None (frozen), not both."""
     n = len(items)
     arr = [(ctypes.c_void_p * 3)(*([ptr(it[k]) for it in items] + [None] * (3 - n))) for k in range(6)]
-    call("lrce_dec_ln_grads", *[ctypes.cast(a, ctypes.c_void_p) for a in arr], n, rows, stream_of(items[0][4]))
+    st = items[0][4] if items[0][4] is not None else items[0][5]
+    call("lrce_dec_ln_grads", *[ctypes.cast(a, ctypes.c_void_p) for a in arr], n, rows, stream_of(st))
 
 
 def mha_fwd(desc, stream_tensor):
@@ -607,6 +620,22 @@ def cast_f16(x, y):
 def cast_f16_bf16(x, y):
     _chk(x, F16, "x"); _chk(y, BF16, "y")
     call("lrce_cast_f16_bf16", ptr(x), ptr(y), x.numel(), stream_of(y))
+
+
+def grad_scale(x, scale):
+    """scale[0:2] = (S, 1/S), S a power of two with max|x| * S in [128, 256) (lrce_grad_scale);
+    scale is a float32 [4] tensor zeroed once at allocation (scale[2:4] are the kernel's arrival words)."""
+    _chk(x, F32, "x"); _chk(scale, F32, "scale")
+    call("lrce_grad_scale", ptr(x), x.numel(), ptr(scale), stream_of(x))
+
+
+def dropout_bwd_f16(dy, p, seed, scale, group=1, out=None):
+    """fp16(scale[0] * dropout_bwd(dy)): the scaled fp16 GEMM operand of an f32 gradient."""
+    if out is None:
+        out = torch.empty(dy.shape, dtype=F16, device=dy.device)
+    call("lrce_dropout_bwd_f16", ptr(dy), ptr(out), dy.numel(), float(p), seed & (2 ** 64 - 1), group, ptr(scale),
+         stream_of(out))
+    return out
 
 
 def dropout(x, p, seed, out=None, out_bf16=None, res=None, group=1):

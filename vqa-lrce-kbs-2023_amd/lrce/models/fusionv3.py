@@ -309,7 +309,8 @@ def _layer_wgrads(lay, flat, acts, grads, fused=False):
     if fused:
         items = [(grads.dln1, acts.x1p, acts.m1, acts.r1, _g(flat, lay.norm1.weight), _g(flat, lay.norm1.bias)),
                  (grads.dln2, acts.x2p, acts.m2, acts.r2, _g(flat, lay.norm2.weight), _g(flat, lay.norm2.bias))]
-        items = [it for it in items if it[4] is not None and it[5] is not None]
+        # a frozen gamma or beta alone is passed as NULL (the kernel skips it)
+        items = [it for it in items if it[4] is not None or it[5] is not None]
         if items:
             K.dec_ln_grads(items, R)
     _wgrad(flat, lay.linear2.weight, lay.linear2.bias, v(grads.df), v(acts.gd))
