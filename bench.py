@@ -124,9 +124,11 @@ def make_step(model, opt, reducer, batch, mode, world):
     tail = None
     if reducer is not None:
         # data parallel: split backward — the fusion head's buckets are exchanged while the extractors'
-        # backward graph replays
+        # backward replays, BERT's and Swin stages 3-4's while Swin stages 1-2 replay
+        from lrce.agent.agent_base import SPLIT_SWIN_STAGE
         model.split_backward = True
-        tail = model.backward_extractors
+        model.split_swin_stage = SPLIT_SWIN_STAGE
+        tail = model.backward_segments()
     step = TrainStepGraph(body, opt, reducer, world, tail=tail)
     return lambda: step(*batch)
 

@@ -424,7 +424,9 @@ int lrce_dec_ln_grads(const float* const* dy, const float* const* x, const float
 int lrce_dec_set_trace(uint64_t* buf);
 /* Debug: phase timestamps (s_memrealtime) of lrce_wattn_bwd into buf[workgroup * 16 + mark] (marks: start,
  * prologue done, steps 0-4 done, stores done, bins written; [10] HW_ID, [11] XCC_ID); NULL turns it off (the
- * default).  Recorded only by a library built with -DLRCE_WATTN_TRACE (tools/wattn_trace.py). */
+ * default).  Recorded only by a library built with -DLRCE_WATTN_TRACE (tools/wattn_trace.py).  The same
+ * buffer also receives lrce_wattn_qkv_fwd's marks (start, GEMM done, epilogue done, qkv stored, attention
+ * done, O stored; tools/wattn_trace.py WATTN_FWD=1): trace one kernel per launch. */
 int lrce_wattn_set_trace(uint64_t* buf);
 
 /* ---------------------------------------------------------------- elementwise / data movement */

@@ -20,9 +20,19 @@ from conftest import PKG, REPO, gpu_available
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a GPU")]
 
-KEYS = ("video_extractor.swin.patch_embed.proj.weight", "video_extractor.swin.layers.2.blocks.5.attn.qkv.weight",
+KEYS = ("video_extractor.swin.patch_embed.proj.weight", "video_extractor.swin.patch_embed.norm.bias",
+        "video_extractor.swin.layers.0.blocks.1.mlp.fc2.weight", "video_extractor.swin.layers.0.downsample.reduction.weight",
         "video_extractor.swin.layers.1.blocks.1.attn.relative_position_bias_table",
+        "video_extractor.swin.layers.1.blocks.0.norm1.weight",
+        "video_extractor.swin.layers.2.blocks.0.attn.qkv.weight", "video_extractor.swin.layers.2.blocks.5.attn.qkv.weight",
+        "video_extractor.swin.layers.2.blocks.17.mlp.fc1.bias", "video_extractor.swin.layers.3.blocks.1.attn.proj.weight",
+        "video_extractor.swin.norm.weight",
+        "text_extractor.bert.embeddings.word_embeddings.weight",
+        "text_extractor.bert.encoder.layer.0.output.dense.weight",
         "text_extractor.bert.encoder.layer.3.attention.self.query.weight",
+        "text_extractor.bert.encoder.layer.11.attention.output.LayerNorm.bias",
+        "fusion_model.video_pos_embed.emb_pos", "fusion_model.projection_layer.weight",
+        "fusion_model.fusion_transformer.transformer.layers.0.multihead_attn.in_proj_weight",
         "fusion_model.fusion_transformer.transformer.layers.7.linear1.weight", "fusion_model.final_fc.bias")
 
 
@@ -66,7 +76,7 @@ def _worker(rank, world, port, mode, q):
     out = {}
     try:
         from lrce.agent.agent_base import DataParallel
-        gdt = torch.bfloat16 if mode in ("bf16", "graph", "graph_split") else torch.float32
+        gdt = torch.bfloat16 if mode in ("bf16", "graph", "graph_split", "graph_split3") else torch.float32
         model = _model(seed=100 + rank)                 # different init per rank: the broadcast must fix it
         dp = DataParallel(model, bucket_mb=32, grad_dtype=gdt)
         flat = dp.reducer.flat
@@ -103,9 +113,11 @@ def _worker(rank, world, port, mode, q):
                 loss.backward()
                 return loss.detach()
             tail = None
-            if mode == "graph_split":   # head backward graph, exchange overlapping the extractors' graph
+            if mode.startswith("graph_split"):   # head backward graph, exchange overlapping the extractors'
                 model.split_backward = True
-                tail = model.backward_extractors
+                if mode.startswith("graph_split3"):   # ... and BERT / Swin 3-4 buckets beside Swin 1-2
+                    model.split_swin_stage = 2
+                tail = model.backward_segments()
             step = TrainStepGraph(body, opt, dp.reducer, world, tail=tail)
             batch = (clips[half], ids[half], mask[half], types[half], labels[half])
             for _ in range(3):
@@ -117,6 +129,7 @@ def _worker(rank, world, port, mode, q):
             if rank == 0:   # single-process reference: same init, full batch, eager steps
                 dist.barrier()
                 model.split_backward = False
+                model.split_swin_stage = None
                 flat.reducer = None
                 flat.grad_reducer = None
                 model.load_state_dict(sd0)
@@ -182,16 +195,28 @@ def test_dp_gradients_equal_full_batch(mode, tol):
         assert _rel(res[0]["dp"][k], res[0]["ref"][k]) < tol, (k, _rel(res[0]["dp"][k], res[0]["ref"][k]))
 
 
-@pytest.mark.parametrize("mode", ["graph", "graph_split"])
+@pytest.mark.parametrize("mode", ["graph", "graph_split", "graph_split3", "graph_split3_f32"])
 def test_dp_graph_training_steps_match_single_process(mode):
     """graph: graph(fwd + bwd) -> exchange -> graph(optimizer); graph_split: the head's backward and
-    the extractors' backward as two graphs with the head's buckets exchanged between them."""
+    the extractors' backward as two graphs with the head's buckets exchanged between them;
+    graph_split3: three backward graphs (the Swin backward cut before stage 3, E2EBase.split_swin_stage),
+    BERT's and Swin 3-4's buckets exchanged while Swin 1-2 replay.  bf16 buckets: updates compared in
+    aggregate; f32 buckets (graph_split3_f32): per element."""
     res = _run(mode)
+    lr = 1e-4
     for k in KEYS:
         a0, a1 = res[0]["after"][k], res[1]["after"][k]
         assert torch.equal(a0, a1), k                            # replicas stay identical
         upd = a0 - res[0]["before"][k]
         ref = res[0]["ref_after"][k] - res[0]["before"][k]
         assert upd.abs().max() > 0, k
-        # AdamW's first steps are ~lr * sign(g): compare the updates in aggregate
-        assert float((upd - ref).abs().mean() / ref.abs().mean()) < 0.1, k
+        if mode.endswith("f32"):
+            # AdamW's first steps are ~lr * sign(g) per element: every element within 5 % of lr of the
+            # single-process update, except the few whose gradient is at rounding level (a sign flip of
+            # a ~0 gradient moves that element by up to 2 lr per step): at most 0.5 % of them
+            d = (upd - ref).abs()
+            assert float((d > 0.05 * lr).float().mean()) < 5e-3, (k, float((d > 0.05 * lr).float().mean()))
+            assert float(d.max()) <= 6.01 * lr, k
+        else:
+            # bf16 transport: compare the updates in aggregate
+            assert float((upd - ref).abs().mean() / ref.abs().mean()) < 0.1, k

@@ -833,3 +833,54 @@ def test_torch_library_ops():
     out, qkv, lse = torch.ops.lrce.window_attention(xw, wq, bq, table, index, n_win, nH, region, win_pat)
     ref, _ = _wattn_reference(qkv, table, index, region, win_pat, nH, n, c)
     assert rel(out, ref) < 2e-2 and lse.shape == (n_win, nH, 160)
+
+
+def test_torch_library_autograd():
+    """Backprop through torch.ops.lrce.window_attention (window_attention_backward: lrce_wattn_bwd +
+    lrce_wattn_dbias + the qkv Linear's GEMMs), linear (with GELU) and layer_norm, vs fp32 torch autograd
+    of the reference math (video_swin_ori.py:158-189) on the same bf16 values."""
+    K()
+    from lrce import ops  # noqa: F401
+    torch.manual_seed(5)
+    nH, n_win, n, hd = 8, 3, 147, 32
+    C = nH * hd
+    index = O.relative_position_index((8, 7, 7)).to(dev)
+    region = torch.zeros(2, n, dtype=torch.int32, device=dev)
+    region[1, 70:] = 1
+    win_pat = torch.tensor([1, 0, 1], dtype=torch.int32, device=dev)
+    xw = bf(torch.randn(n_win * n, C, device=dev)).requires_grad_(True)
+    wq = bf(torch.randn(3 * C, C, device=dev) / math.sqrt(C)).requires_grad_(True)
+    bq = (torch.randn(3 * C, device=dev) * 0.1).requires_grad_(True)
+    table = (torch.randn(2535, nH, device=dev) * 0.3).requires_grad_(True)
+    out, qkv, lse = torch.ops.lrce.window_attention(xw, wq, bq, table, index, n_win, nH, region, win_pat)
+    gout = torch.randn(out.shape, device=dev)
+    (out.float() * gout).sum().backward()
+    xr, wr, br, tr = (t.detach().float().requires_grad_(True) for t in (xw, wq, bq, table))
+    qkv_r = (xr @ wr.t() + br).view(n_win, n, 3, nH, hd).permute(2, 0, 3, 1, 4)
+    bias = tr[index[:n, :n].reshape(-1)].view(n, n, nH).permute(2, 0, 1)
+    mask = (region[win_pat.long()][:, :, None] != region[win_pat.long()][:, None, :]).float() * -100.0
+    s = (qkv_r[0] * hd ** -0.5) @ qkv_r[1].transpose(-1, -2) + bias[None] + mask[:, None]
+    o = (s.softmax(-1) @ qkv_r[2]).transpose(1, 2).reshape(n_win * n, C)
+    assert rel(out, o) < 2e-2
+    (o * gout).sum().backward()
+    for got, ref in ((xw.grad, xr.grad), (wq.grad, wr.grad), (bq.grad, br.grad), (table.grad, tr.grad)):
+        assert got is not None and rel(got.float(), ref) < 3e-2, (rel(got.float(), ref), ref.shape)
+    # linear (+ GELU) and layer_norm
+    x = bf(torch.randn(300, 256, device=dev)).requires_grad_(True)
+    w = bf(torch.randn(512, 256, device=dev) / 16).requires_grad_(True)
+    b = torch.randn(512, device=dev).requires_grad_(True)
+    g = torch.randn(300, 512, device=dev)
+    (torch.ops.lrce.linear(x, w, b, True, True) * g).sum().backward()
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    (F.gelu(xr @ wr.t() + br) * g).sum().backward()
+    for got, ref in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert rel(got.float(), ref) < 2e-2
+    xf = torch.randn(300, 256, device=dev, requires_grad=True)
+    gm = (torch.rand(256, device=dev) + 0.5).requires_grad_(True)
+    be = torch.randn(256, device=dev, requires_grad=True)
+    gy = torch.randn(300, 256, device=dev)
+    (torch.ops.lrce.layer_norm(xf, gm, be, 1e-5)[0] * gy).sum().backward()
+    xr, gr, br = (t.detach().clone().requires_grad_(True) for t in (xf, gm, be))
+    (F.layer_norm(xr, (256,), gr, br, 1e-5) * gy).sum().backward()
+    for got, ref in ((xf.grad, xr.grad), (gm.grad, gr.grad), (be.grad, br.grad)):
+        assert rel(got, ref) < 1e-4

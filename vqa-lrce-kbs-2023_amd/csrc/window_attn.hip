@@ -625,6 +625,7 @@ __global__ void dbias_scatter_kernel(const float* __restrict__ red, int hb, int 
 }  // namespace
 
 static unsigned long long* g_wb_trace = nullptr;   // lrce_wattn_set_trace
+unsigned long long* g_wattn_trace = nullptr;      // the same buffer, read by lrce_wattn_qkv_fwd (window_fused.hip)
 
 extern "C" int64_t lrce_wattn_bias_elems(int n_pat, int nH) { return (int64_t)n_pat * nH * PH_ELEMS; }
 // bias-gradient scratch (f32): one bin row per (window, head) + the WCH chunk sums
@@ -683,6 +684,7 @@ extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const ui
 // only by a build with -DLRCE_WATTN_TRACE
 extern "C" int lrce_wattn_set_trace(uint64_t* buf) {
   g_wb_trace = reinterpret_cast<unsigned long long*>(buf);
+  g_wattn_trace = g_wb_trace;
   return LRCE_OK;
 }
 

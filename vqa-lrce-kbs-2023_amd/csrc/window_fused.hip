@@ -103,7 +103,16 @@ struct FusedP {
   float* lse;           // [n_win][nH][160], log2 domain
   float qscale;         // head_dim^-0.5 * log2(e)
   int n_win, n, nH, C;
+  unsigned long long* trace;   // phase timestamps (builds with -DLRCE_WATTN_TRACE only; lrce_wattn_set_trace)
 };
+
+// debug phase marks: thread 0 of each workgroup stamps s_memrealtime (100 MHz) into trace[wg * 16 + i]
+#ifdef LRCE_WATTN_TRACE
+#define WF_MARK(I) \
+  if (p.trace && threadIdx.x == 0) p.trace[(long long)blockIdx.x * 16 + (I)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define WF_MARK(I)
+#endif
 
 // the 20 fp16x4 bias loads of one attention unit: bias row of query tile qt, key tiles 0..4
 __device__ __forceinline__ void bias_load(const FusedP& p, int pat, int h, int qt, int lane, uint2 (&bv)[NTILE][4]) {
@@ -128,6 +137,13 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
   const long long ld3 = 3LL * C;
   const bf16* xwin = p.x + (long long)w * n * C;
   const int pat = p.win_pat ? p.win_pat[w] : 0;
+  WF_MARK(0)
+#ifdef LRCE_WATTN_TRACE
+  if (p.trace && threadIdx.x == 0) {   // placement: HW_ID (cu / sh / se) and XCC_ID
+    p.trace[(long long)blockIdx.x * 16 + 10] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    p.trace[(long long)blockIdx.x * 16 + 11] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+  }
+#endif
 
   // ---- 1. GEMM: acc[i][j][r] = Y[tok = wm*80 + i*16 + (lane&15)][col = wn*48 + j*16 + 4*(lane>>4) + r]
   const int wm = wave >> 2, wn = wave & 3;
@@ -207,6 +223,7 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();                                      // ring free: the images alias it
   __builtin_amdgcn_sched_barrier(0);
+  WF_MARK(1)
 
   const int hh = lane >> 5, r32 = lane & 31;
   uint2 bv[NTILE][4];
@@ -235,6 +252,7 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
     }
   }
   __syncthreads();
+  WF_MARK(2)
   // qkv rows for the backward: per token and part, the head pair's 64 columns = 128 contiguous bytes
   for (int it = threadIdx.x; it < n * 3 * 8; it += NW * 64) {
     const int c8 = it & 7, tp = it >> 3;
@@ -246,6 +264,7 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
     *reinterpret_cast<uint4*>(p.qkv + ((long long)w * n + tok) * ld3 + part * C + hg * (HB * HD) + c8 * 8) = v;
   }
   __syncthreads();   // the Q rows are read by the stores above before a unit parks its O in them
+  WF_MARK(3)
 
   // ---- 3. attention: unit u = (head hl, query tile qt), u = wave, wave + 8 (< 10)
   for (int u = wave; u < HB * NTILE; u += NW) {
@@ -307,6 +326,7 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
     if (hh == 0 && qi < n) p.lse[((long long)w * p.nH + h) * NPAD + qi] = m + __log2f(sum);
   }
   __syncthreads();
+  WF_MARK(4)
   // O rows: per token the head pair's 64 columns = 128 contiguous bytes
   for (int it = threadIdx.x; it < n * 8; it += NW * 64) {
     const int c8 = it & 7, tok = it >> 3;
@@ -314,9 +334,15 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
     const uint4 v = *reinterpret_cast<const uint4*>(lds + hl * IMG + qk_off(tok, c4 * 8));
     *reinterpret_cast<uint4*>(p.out + ((long long)w * n + tok) * C + hg * (HB * HD) + c8 * 8) = v;
   }
+#ifdef LRCE_WATTN_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  WF_MARK(5)
+#endif
 }
 
 }  // namespace
+
+extern unsigned long long* g_wattn_trace;   // window_attn.hip, lrce_wattn_set_trace
 
 extern "C" int lrce_wattn_qkv_fwd(const uint16_t* x, const uint16_t* w_qkv, const float* b_qkv, float qscale,
                                   const uint16_t* bias_fwd16, const int32_t* win_pat, const int32_t* win_order,
@@ -343,6 +369,7 @@ extern "C" int lrce_wattn_qkv_fwd(const uint16_t* x, const uint16_t* w_qkv, cons
   p.lse = lse;
   p.qscale = qscale;
   p.n_win = n_win; p.n = n; p.nH = nH; p.C = C;
+  p.trace = g_wattn_trace;
   wattn_qkv_fwd_kernel<<<(unsigned)(n_win * (nH / HB)), NW * 64, 0, static_cast<hipStream_t>(stream)>>>(p);
   return lrce_check_launch("wattn_qkv_fwd");
 }

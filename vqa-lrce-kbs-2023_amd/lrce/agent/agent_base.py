@@ -37,6 +37,9 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..graph import TrainStepGraph
+
+# data-parallel split backward: the Swin backward is cut before this stage (E2EBase.split_swin_stage)
+SPLIT_SWIN_STAGE = 2
 from ..optim import FusedAdamW
 from ..runtime import ensure
 from .schedulers import CosineAnnealingWarmupRestarts, ReduceLROnPlateau
@@ -211,11 +214,13 @@ class AgentBase:
                     red = self.model.reducer
                     tail = None
                     mod = self.model.module
-                    if red is not None and hasattr(mod, "backward_extractors"):
+                    if red is not None and hasattr(mod, "backward_segments"):
                         # data parallel: the head's gradient buckets are exchanged while the
-                        # extractors' backward replays (TrainStepGraph tail)
+                        # extractors' backward replays, and BERT's + Swin stages 3-4's while Swin
+                        # stages 1-2 replay (TrainStepGraph tail segments)
                         mod.split_backward = True
-                        tail = mod.backward_extractors
+                        mod.split_swin_stage = SPLIT_SWIN_STAGE
+                        tail = mod.backward_segments()
                     self._graph = TrainStepGraph(self._train_body, self.optim, red, red.world if red else 1, tail=tail)
                 out, terms, task, l2 = self._graph(*inputs)
                 gt = self._graph.static[4]

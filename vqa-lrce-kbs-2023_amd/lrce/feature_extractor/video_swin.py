@@ -535,6 +535,10 @@ class SwinTransformer3D(nn.Module):
                                           dpr[sum(depths[:i]):sum(depths[:i + 1])], i < len(depths) - 1))
         self.num_features = embed_dim * 2 ** (len(depths) - 1)
         self.norm = nn.LayerNorm(self.num_features)
+        # split backward (data parallel, E2EBase.split_swin_stage): the input of stage split_at enters it
+        # as a detached leaf, so one backward call ends there and backward_below_split() continues
+        self.split_at = None
+        self._split_mid = None
         # stage i > 0 is final once its first block's backward is done (the backward runs the last
         # stage first): that block reports the stage's optimizer group (E2EBase.optimizer_groups)
         for i, layer in enumerate(self.layers):
@@ -555,7 +559,11 @@ class SwinTransformer3D(nn.Module):
         D, H, W = (T + 1) // 2, H // 4, W // 4
         scales = _drop_path_scales(self, nc, dev)
         bi = 0
-        for layer in self.layers:
+        for li, layer in enumerate(self.layers):
+            if li == self.split_at and torch.is_grad_enabled() and x.requires_grad:
+                x_leaf = x.detach().requires_grad_(True)
+                self._split_mid = (x, x_leaf)
+                x = x_leaf
             geo = stage_geometry(nc, D, H, W, self.window_size, dev)
             nb = len(layer.blocks)
             x = _run_blocks(list(layer.blocks), x, geo, flat,
@@ -566,6 +574,13 @@ class SwinTransformer3D(nn.Module):
                 H, W = (H + 1) // 2, (W + 1) // 2
         x = _LayerNormFn.apply(x, self.norm, flat, 1e-5, *self.norm.parameters())
         return x, (nc, D, H, W)
+
+    def backward_below_split(self):
+        """Second part of a split Swin backward: stages below split_at (and the patch embedding) from
+        the gradient the first part left on the stage input."""
+        x, x_leaf = self._split_mid
+        self._split_mid = None
+        torch.autograd.backward([x], [x_leaf.grad])
 
     def forward_stage(self, i, x_cl, depth=None):
         """Run stage i (its first `depth` blocks, all by default, then PatchMerging) on channels-last

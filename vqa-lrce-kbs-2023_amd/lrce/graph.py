@@ -34,6 +34,7 @@ class CapturedStep:
 
 class _Captured:
     __slots__ = ("static", "out", "g_step", "g_tail", "g_opt", "warm", "order", "order_tail", "stage", "turn", "free")
+    # g_tail / order_tail: one captured graph and one bucket-order list per tail segment
 
     def __init__(self, inputs, device):
         self.static = [torch.empty_like(t, device=device) for t in inputs]
@@ -59,14 +60,17 @@ class TrainStepGraph:
     training step) and captures on the next one; graphs are kept per signature (a short last batch
     gets its own).  Every call is exactly one training step.
 
-    tail (optional, with a reducer): the second half of a split backward (E2EBase.split_backward /
-    backward_extractors): body then ends with the fusion head's backward, and the step is
-    graph(forward + head backward) -> exchange of the head's buckets, overlapping ->
-    graph(extractors' backward) -> exchange of the rest -> graph(optimizer)."""
+    tail (optional, with a reducer): the rest of a split backward (E2EBase.split_backward), one callable
+    or a list of segments (E2EBase.backward_segments): body then ends with the fusion head's backward,
+    and the step is graph(forward + head backward) -> exchange of the head's buckets, overlapping ->
+    graph(segment 1) -> exchange of the buckets it completed, overlapping -> graph(segment 2) ... ->
+    exchange of the rest -> graph(optimizer)."""
 
     def __init__(self, body, optim, reducer=None, world=1, tail=None):
         self.body, self.optim, self.reducer, self.world = body, optim, reducer, world
-        self.tail = tail if reducer is not None else None
+        if tail is not None and not isinstance(tail, (list, tuple)):
+            tail = [tail]
+        self.tail = list(tail) if (tail and reducer is not None) else None
         self.states = {}
         self.static = None   # static inputs of the last call (the agent reads the labels from it)
         self.copy_stream = None
@@ -107,8 +111,8 @@ class TrainStepGraph:
 
     def _eager(self, st):
         st.out = self.body(*st.static)
-        if self.tail is not None:
-            self.tail()
+        for seg in self.tail or ():
+            seg()
         scale = self.reducer.finish() if self.reducer is not None else 1.0
         self.optim.step(grad_scale=scale)
         return st.out
@@ -136,13 +140,18 @@ class TrainStepGraph:
                 else:
                     with torch.cuda.graph(st.g_step, pool=pool):
                         st.out = self.body(*st.static)
-                    mark = self.reducer.capture_mark()
-                    st.g_tail = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(st.g_tail, pool=pool):
-                        self.tail()
-                        self.reducer.finish()
-                    st.order = list(self.reducer.captured[:mark])
-                    st.order_tail = list(self.reducer.captured[mark:])
+                    marks = [self.reducer.capture_mark()]
+                    st.g_tail = []
+                    for i, seg in enumerate(self.tail):
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, pool=pool):
+                            seg()
+                            if i == len(self.tail) - 1:
+                                self.reducer.finish()
+                        st.g_tail.append(g)
+                        marks.append(self.reducer.capture_mark())
+                    st.order = list(self.reducer.captured[:marks[0]])
+                    st.order_tail = [list(self.reducer.captured[a:b]) for a, b in zip(marks[:-1], marks[1:])]
             finally:
                 self.reducer.capture_end()
             st.g_opt = torch.cuda.CUDAGraph()
@@ -168,8 +177,9 @@ class TrainStepGraph:
         st.g_step.replay()
         if st.g_tail is not None:
             self.reducer.exchange(st.order)        # the head's buckets, beside the extractors' backward
-            st.g_tail.replay()
-            self.reducer.exchange(st.order_tail)
+            for g, order in zip(st.g_tail, st.order_tail):
+                g.replay()
+                self.reducer.exchange(order)       # this segment's buckets, beside the next segment
             self.reducer.join()
             st.g_opt.replay()
         elif st.g_opt is not None:

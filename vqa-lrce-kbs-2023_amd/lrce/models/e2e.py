@@ -42,6 +42,10 @@ class E2EBase(nn.Module):
         # buckets overlaps the extractors' backward between the two captured graphs
         self.split_backward = False
         self._split = None
+        # with split_backward, also cut the Swin backward before this stage (None: one segment): the
+        # buckets of the stages above it (stages 3-4 of Swin-B: ~82 M of its 87.6 M parameters) and
+        # of BERT are exchanged while the stages below replay (backward_segments)
+        self.split_swin_stage = None
         self.text_extractor = TextExtractor(bert_dir=bert_dir)
         self.video_extractor = VideoExtractor(swin_ckpt)
         if self.HEAD is not None:
@@ -105,6 +109,8 @@ class E2EBase(nn.Module):
         side.wait_stream(main)
         with torch.cuda.stream(side):
             t = self.extract_text_features(texts, texts_attention_mask, texts_type_ids, join_token=tok)
+        swin = self.video_extractor.swin
+        swin.split_at = self.split_swin_stage if self.split_backward else None
         v = self.extract_video_features(video_clips)
         main.wait_stream(side)
         t.record_stream(main)
@@ -117,9 +123,22 @@ class E2EBase(nn.Module):
     def backward_extractors(self):
         """Second half of a split backward: the extractors' backward (Swin on this stream, BERT on its
         side stream, joined at the end) from the feature gradients loss.backward() left."""
+        self._backward_upper()
+        if self.video_extractor.swin._split_mid is not None:
+            self.video_extractor.swin.backward_below_split()
+
+    def _backward_upper(self):
         v, t, v_in, t_in = self._split
         self._split = None
         torch.autograd.backward([v, t], [v_in.grad, t_in.grad])
+
+    def backward_segments(self):
+        """The extractors' backward as TrainStepGraph tail segments: one, or two when split_swin_stage
+        cuts the Swin backward — [BERT + Swin stages >= split_swin_stage, the stages below it + the
+        patch embedding]."""
+        if self.split_swin_stage is None:
+            return [self.backward_extractors]
+        return [self._backward_upper, self.video_extractor.swin.backward_below_split]
 
 
 # Constructor defaults differ per task (question length 30 vs 40, one output for counting), so each
