@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--grad-reduce-dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--agent-steps", type=int, default=6, help="steps of the train_ddp agent path (0: skip)")
     ap.add_argument("--roofline-steps", type=int, default=2)
+    ap.add_argument("--gemm-table", default=None,
+                    help="write the per-shape roofline table of the bf16 GEMMs of the roofline steps (markdown) here")
     return ap.parse_args()
 
 
@@ -267,6 +269,8 @@ def main():
             train_step(model, opt, reducer, batch)
     torch.cuda.synchronize()
     roof = _roofline(timer)
+    if args.gemm_table and rank == 0 and args.roofline_steps > 0:
+        _gemm_table(timer, args.roofline_steps, args.gemm_table)
     del step, model, opt, reducer, batch
     torch.cuda.empty_cache()
     agent = None
@@ -385,6 +389,45 @@ def _roofline(timer):
                                "frac": round(t / MFMA_BF16_PEAK_TFLOPS, 4)}
     roof["others"] = extra
     return roof
+
+
+def _gemm_table(timer, steps, path):
+    """Per-shape roofline of the bf16 / fp16 MFMA GEMMs (lrce_gemm, LDS-DMA / register-staged paths) over
+    the roofline steps: algorithmic flops 2 M N K and bytes (A, B once; C by its epilogue: 16-bit or
+    f32 out, an f32 accumulate read, residual / pre-activation operands), the bound they imply against
+    the bf16 ridge, and the fraction of that bound the launch reaches (HIP events, eager steps)."""
+    from lrce import _native as N
+    rows, tot_us = [], 0.0
+    for name, key, calls, t_ms, tf in timer.breakdown():
+        if name != "gemm":
+            continue
+        m, n, k, batch, al, bl, a32, split, flags = key
+        ab = 4 if a32 == "a32" else 2
+        outb = 4 if flags & (N.EPI_OUT_F32 | N.EPI_ATOMIC | N.EPI_ACCUM) else 2
+        if flags & N.EPI_ACCUM:
+            outb += 4
+        outb += (4 if flags & N.EPI_RESID else 0) + (2 if flags & N.EPI_DGELU else 0) + \
+            (2 if flags & N.EPI_AUX_OUT else 0) + (2 if flags & N.EPI_OUT_BOTH else 0)
+        byts = batch * (ab * m * k + 2 * n * k + outb * m * n)
+        fl = 2.0 * m * n * k * batch
+        us = 1000.0 * t_ms / calls
+        ai = fl / byts
+        bound = "mfma" if ai >= RIDGE else "hbm"
+        ach_tf, ach_gb = fl / us / 1e6, byts / us / 1e3
+        frac = ach_tf / MFMA_BF16_PEAK_TFLOPS if bound == "mfma" else ach_gb / HBM_PEAK_GBS
+        per_step_us = 1000.0 * t_ms / steps
+        tot_us += per_step_us
+        rows.append((per_step_us, f"| {m}x{n}x{k}{'' if batch == 1 else f' x{batch}'} | {al}/{bl}/{a32} | {split} | {flags} | "
+                                  f"{calls / steps:g} | {us:.1f} | {per_step_us:.0f} | {ach_tf:.0f} | {ach_gb:.0f} | {ai:.0f} | "
+                                  f"{bound} | {frac:.3f} |"))
+    rows.sort(key=lambda r: -r[0])
+    with open(path, "w") as f:
+        f.write(f"# bf16/fp16 GEMM launches per training step (bench.py --gemm-table, {steps} eager roofline steps)\n")
+        f.write(f"# total {tot_us / 1000:.2f} ms/step of lrce_gemm launches (HIP events; eager, so launch gaps excluded)\n\n")
+        f.write("| M x N x K | A/B layout | split-K | epilogue flags | launches/step | us/launch | us/step | TFLOP/s | GB/s "
+                "| flop/B | bound | frac of bound |\n|---|---|---|---|---|---|---|---|---|---|---|---|\n")
+        for _, r in rows:
+            f.write(r + "\n")
 
 
 if __name__ == "__main__":

@@ -327,9 +327,17 @@ __global__ void __launch_bounds__(256, 2) wattn_fwd3_kernel(const bf16* __restri
 // so |dS| 2^s < 2^22 and a bin of <= 160 terms stays below 2^30): the quantum follows the gradient's
 // magnitude (an absolute quantum lost batch-mean-sized gradients) and is 2^-22 of the bound — finer
 // than the bf16 dS the dQ / dK products use.  Conversion: one f32 fma onto 1.5 * 2^23 leaves
-// round(dS 2^s) in the low mantissa bits, one integer subtract extracts it (the f64 / int64 form of
-// round 2 spent ~7 VALU per element on the conversion and twice the LDS atomic bandwidth).
+// round(dS 2^s) in the low mantissa bits; the add takes the fma's bit pattern as it is and the
+// epilogue subtracts 0x4B400000 times the bin's (closed-form) number of adds, modulo 2^32 (the f64 /
+// int64 form of round 2 spent ~7 VALU per element on the conversion and twice the LDS atomic bandwidth).
 // lrce_wattn_dbias sums the windows in a fixed order and scatters bins to table rows.
+// Bank-spread bin order: in LDS a relative position (dt, dh, dw) lives at dt A + dh B + dw with B = ww
+// (mod 32), A = wh ww (mod 32) and A, B large enough to keep the map injective (3x7x7: B = 39,
+// A = 497, 2469 slots), so the token code t A + h B + w is congruent to the token index mod 32: the
+// 32 lanes of a half (one query, 32 consecutive keys) add to 32 distinct banks.  The natural radix
+// (2ww-1, 2wh-1) put key rows 7 words apart in 13-word strides — 32 keys spanned ~56 words, so lanes
+// 32 words apart collided (45 % of the LDS cycles were bank conflicts).  The bins leave in natural
+// order (the relative-position index the dbias pass and lrce_wattn_dbias's bin_row use).
 // Workgroup barrier for LDS hand-offs only: __syncthreads() would also drain vmcnt(0), i.e. wait for
 // the bias-tile loads of later steps and the dK / dV / dQ stores in flight.
 __device__ __forceinline__ void lds_barrier() {
@@ -339,7 +347,8 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 constexpr int BW = 5;        // waves per backward workgroup (= tiles of 32 rows)
-constexpr int NBMAX = 1024;  // relative-position bins per head held in LDS
+constexpr int NBMAX = 1024;  // relative-position bins per (window, head) written out (natural order)
+constexpr int NBL = 2560;    // LDS bins per head in the bank-spread order (bin_spread)
 constexpr int WCH = 32;      // window chunks of the deterministic bias-gradient reduction
 
 struct BwdLds {
@@ -347,7 +356,7 @@ struct BwdLds {
   bf16 dout[NPAD * HD];
   bf16 k[NPAD * HD];
   bf16 ds[2][BW][TQ * TQ];
-  unsigned bins[NBMAX];   // 2^s fixed point (two's complement int32)
+  unsigned bins[NBL];      // 2^s fixed point (two's complement int32), bank-spread order
   float4 qinfo[NPAD];   // per query: lse, delta, token code (as bits), -
   float nmax[BW][2];    // per wave: max |dO_q|^2, max |V_q|^2 over its rows (the bins' scale)
 };
@@ -361,8 +370,8 @@ __global__ void __launch_bounds__(BW * 64 * HPW, 3) wattn_bwd_kernel(const bf16*
                                                               const bf16* __restrict__ dout, const float* __restrict__ lse_g,
                                                               const void* __restrict__ biasb, const int* __restrict__ win_pat,
                                                               bf16* __restrict__ dqkv, float* __restrict__ dbias_part, int n_win,
-                                                              int n, int nH, int wh, int ww, int nb, int boff, float qscale,
-                                                              unsigned long long* __restrict__ trace) {
+                                                              int n, int nH, int wh, int ww, int nb, int boff, int ba, int bb,
+                                                              float qscale, unsigned long long* __restrict__ trace) {
   __shared__ __attribute__((aligned(16))) BwdLds LL[HPW];
   // debug phase timestamps, compiled in only with -DLRCE_WATTN_TRACE (tools/wattn_trace.py builds that
   // variant: the marks cost registers this kernel does not have to spare): thread 0 of each workgroup
@@ -439,7 +448,7 @@ __global__ void __launch_bounds__(BW * 64 * HPW, 3) wattn_bwd_kernel(const bf16*
         }
       }
       l = lse_g[((long long)w * nH + h) * NPAD + q];
-      code = ((q / (wh * ww)) * (2 * wh - 1) + (q / ww) % wh) * (2 * ww - 1) + q % ww;
+      code = (q / (wh * ww)) * ba + ((q / ww) % wh) * bb + q % ww;   // bank-spread token code
     }
     L.qinfo[q] = make_float4(l, d, __int_as_float(code), 0.f);
   }
@@ -455,7 +464,7 @@ __global__ void __launch_bounds__(BW * 64 * HPW, 3) wattn_bwd_kernel(const bf16*
     L.nmax[t][0] = dn2;
     L.nmax[t][1] = vn2;
   }
-  for (int i = lt; i < NBMAX; i += BW * 64) L.bins[i] = 0u;
+  for (int i = lt; i < NBL; i += BW * 64) L.bins[i] = 0u;
   __syncthreads();
   WB_MARK(1)
   // bins' scale 2^s: |dS| <= 2 max|dO| max|V| = bound < 2^e -> |dS| 2^s < 2^22 with s = 22 - e
@@ -482,6 +491,7 @@ __global__ void __launch_bounds__(BW * 64 * HPW, 3) wattn_bwd_kernel(const bf16*
   const int kbin = boff - (key_live ? __float_as_int(L.qinfo[key].z) : 0);
   const bool want_bins = dbias_part != nullptr;
   f32x16 dkT = {}, dvT = {}, dqT = {};
+#pragma unroll 1
   for (int s = 0; s < NTILE; ++s) {
     const int qt = t + s < NTILE ? t + s : t + s - NTILE;
     f32x16 sacc;
@@ -523,14 +533,16 @@ __global__ void __launch_bounds__(BW * 64 * HPW, 3) wattn_bwd_kernel(const bf16*
       sacc[r] = p;
       dp[r] = p * (dp[r] - qi4[r].y);
     }
-    // bias-table gradient: no predicates needed: dS is exactly 0 for padded queries (zero dO rows,
-    // delta 0) and padded keys (P = 0), and their bins (code 0) stay inside [0, n_bins)
-    if (want_bins) {
+    // bias-table gradient: dS is exactly 0 for padded queries (zero dO rows, delta 0; their code 0 keeps
+    // the bin inside the array) and padded keys (P = 0); the padded keys' lanes are masked off (they
+    // would all add to one word)
+    if (want_bins && key_live) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         // round(dS * 2^s) to int32: the fma result lies in [2^23, 2^24) (ulp 1) for |dS 2^s| < 2^22
+        // the add carries the bias 0x4B400000 of the fma trick; the epilogue subtracts it once per add
         const float m = __builtin_fmaf(dp[r], bscale, 0x1.8p23f);
-        atomicAdd(&L.bins[__float_as_int(qi4[r].z) + kbin], (unsigned)(__float_as_int(m) - 0x4B400000));
+        atomicAdd(&L.bins[__float_as_int(qi4[r].z) + kbin], (unsigned)__float_as_int(m));
       }
     }
     // dV^T += dO^T P ; dK^T += Q~^T dS  (the accumulators as B operands, permuted k order)
@@ -591,8 +603,16 @@ __global__ void __launch_bounds__(BW * 64 * HPW, 3) wattn_bwd_kernel(const bf16*
   if (!want_bins) return;
   lds_barrier();   // every wave's bin adds are done (the row stores above stay in flight)
   float* dst = dbias_part + ((long long)w * nH + h) * nb;
-  for (int b = lt; b < nb; b += BW * 64)
-    dst[b] = (float)(int)L.bins[b] * binv;
+  const int nw2 = 2 * ww - 1, nh2 = 2 * wh - 1, wd = n / (wh * ww);
+  for (int b = lt; b < nb; b += BW * 64) {   // natural bin b = ((dt + wd-1) nh2 + dh + wh-1) nw2 + dw + ww-1
+    const int dw = b % nw2 - (ww - 1), r = b / nw2;
+    const int dh = r % nh2 - (wh - 1), dt = r / nh2 - (wd - 1);
+    // adds into this slot: the (query, key) pairs at that relative position, plus one per padded query
+    // (code 0) for the relative positions of -(a key's position) — each carried the 0x4B400000 bias
+    const unsigned cnt = (unsigned)((wd - abs(dt)) * (wh - abs(dh)) * (ww - abs(dw)) +
+                                    ((dt <= 0 && dh <= 0 && dw <= 0) ? NPAD - n : 0));
+    dst[b] = (float)(int)(L.bins[dt * ba + dh * bb + dw + boff] - cnt * 0x4B400000u) * binv;
+  }
   WB_MARK(8)
 #undef WB_MARK
 }
@@ -668,14 +688,20 @@ extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const ui
   const int nb = (2 * wd - 1) * (2 * wh - 1) * (2 * ww - 1);
   if (nb > NBMAX) return lrce_fail(LRCE_E_ARG, "wattn_bwd: %d relative-position bins > %d", nb, NBMAX);
   if (n_win <= 0) return LRCE_OK;
-  const int boff = ((wd - 1) * (2 * wh - 1) + (wh - 1)) * (2 * ww - 1) + (ww - 1);
+  // bank-spread LDS bin order (see the kernel's comment): B = ww, A = wh ww (mod 32), injective
+  int bb = 2 * ww - 1;
+  while ((bb - ww) % 32) ++bb;
+  int ba = 2 * ((wh - 1) * bb + (ww - 1)) + 1;
+  while ((ba - wh * ww) % 32) ++ba;
+  const int boff = (wd - 1) * ba + (wh - 1) * bb + (ww - 1);
+  if (2 * boff + 1 > NBL) return lrce_fail(LRCE_E_ARG, "wattn_bwd: %d bank-spread bins > %d", 2 * boff + 1, NBL);
   static const bool one_head = getenv("LRCE_WATTN_HPW1") != nullptr;   // A/B: one head per workgroup
   const int hpw = (nH & 1) || one_head ? 1 : 2;
   const auto kern = bias_f16 ? (hpw == 2 ? wattn_bwd_kernel<true, 2> : wattn_bwd_kernel<true, 1>)
                              : (hpw == 2 ? wattn_bwd_kernel<false, 2> : wattn_bwd_kernel<false, 1>);
   kern<<<(unsigned)(n_win * nH / hpw), BW * 64 * hpw, 0, static_cast<hipStream_t>(stream)>>>(
       reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const bf16*>(out), reinterpret_cast<const bf16*>(dout), lse, bias_bwd,
-      win_pat, reinterpret_cast<bf16*>(dqkv), dbias_part, n_win, n, nH, wh, ww, nb, boff, 1.0f / sqrtf((float)HD),
+      win_pat, reinterpret_cast<bf16*>(dqkv), dbias_part, n_win, n, nH, wh, ww, nb, boff, ba, bb, 1.0f / sqrtf((float)HD),
       g_wb_trace);
   return lrce_check_launch("wattn_bwd");
 }
