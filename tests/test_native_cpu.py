@@ -36,6 +36,22 @@ def test_gemm_rejects_bad_shapes_without_launching():
     assert b"% 8" in _native.lib().lrce_last_error()
 
 
+@pytest.mark.skipif(torch.cuda.is_available(), reason="would launch on the GPU with fake pointers")
+@pytest.mark.parametrize("f16,a_km,b_km", [(0, 1, 1), (1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 0, 0)])
+def test_gemm_dispatch_returns_without_a_device(f16, a_km, b_km):
+    """Every LDS-DMA dispatch branch (bf16 / fp16, the forward, dX and dW layouts) runs its host path to
+    the launch and returns the HIP error as a status code when no device is visible (a host-side fault in
+    the launcher — e.g. a dispatch lambda that falls off its end — would crash this process)."""
+    from lrce import _native
+    d = _native.GemmDesc()
+    d.a = d.b = d.c = 0x7F0000000000
+    d.m, d.n, d.k, d.batch = 320, 768, 768, 1
+    d.lda = d.ldb = d.ldc = 768
+    d.a_kmajor, d.b_kmajor, d.f16, d.alpha = a_km, b_km, f16, 1.0
+    rc = _native.lib().lrce_gemm(ctypes.byref(d), None)
+    assert rc != 0
+
+
 def test_wattn_rejects_unsupported_window():
     from lrce import _native
     rc = _native.lib().lrce_wattn_fwd_grouped(0x1000, 0x1000, None, None, 1, 0x1000, 0x1000, 4, 100, 4, None)

@@ -317,7 +317,17 @@ __device__ __forceinline__ float drop1(float v, float p, uint64_t seed, long lon
   return lrce_uniform(seed, (uint64_t)idx) >= p ? v / (1.0f - p) : 0.f;
 }
 
-// publish this head's partial row (768 f32) and return true in the last of the 12 heads to arrive
+// publish this head's partial row (768 f32) and return true in the last of the 12 heads to arrive.
+// Hand-off protocol: MI355X_MICROARCH.md "Valid forms", first row of the sc1 hand-off table (the
+// same as gemm_f32.hip's skinny split-K), in place of a release/acquire pair — every partial is an
+// agent-scope relaxed store (global_store ... sc1: written through past this XCD's L2), every storing
+// wave drains it with s_waitcnt vmcnt(0), a workgroup barrier follows, ONE lane's agent-scope atomic
+// add signals, the workgroup whose add returns H-1 is told by that value, and it reads EVERY partial
+// with agent-scope relaxed loads (global_load ... sc1, no L1/L2 reuse) after the barrier that
+// publishes last_flag.  All four conditions of that row hold, so no buffer_wbl2 / buffer_inv (~1.7 us
+// each, on a ~10-20 us latency-bound launch) is needed.  This is measured gfx950 behaviour, not a
+// C++ memory-model guarantee: a port to another target must switch to __ATOMIC_RELEASE on the add
+// plus an agent acquire fence in the last arriver.
 __device__ __forceinline__ bool publish_partial(const float* part_lds, float* slab, unsigned* ctr, int b, int h, int t,
                                                 unsigned* last_flag) {
   float* mine = slab + ((long long)b * H + h) * E;

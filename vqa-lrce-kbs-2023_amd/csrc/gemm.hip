@@ -973,6 +973,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
         case 5: gemm_glds_kernel<64, 64, false, true, false, S><<<grid, NT, 0, s>>>(p); break;
         case 4: gemm_glds_kernel<64, 64, false, false, false, S><<<grid, NT, 0, s>>>(p); break;
       }
+      return (int)LRCE_OK;
     };
     // two stages: a third (one resident workgroup per CU) measured 1.3-1.5x slower on every step shape
     if (int rc = launch(std::integral_constant<int, 2>{})) return rc;

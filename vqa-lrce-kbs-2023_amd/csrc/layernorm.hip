@@ -298,6 +298,9 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
 // LN_RED_ROWS partial rows of 64 columns (32 per wave, 8 loads in flight) into chunk row y; the last
 // of the column block's ny (<= 16) blocks to arrive (agent-scope stores / counter, as the skinny
 // split-K of gemm_f32.hip) adds the ny chunk rows in order — one writer per element, a fixed order.
+// The hand-off is MI355X_MICROARCH.md's first-row sc1 form (relaxed agent-scope stores drained by
+// vmcnt(0), a barrier, one agent atomic add, agent-scope relaxed loads in the last arriver): measured
+// gfx950 behaviour, not a C++ memory-model release/acquire pair (see decoder.hip publish_partial).
 __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ part, int nb, int cols, float* dw, float* db,
                                                      float* chunk, unsigned* counters) {
   __shared__ float red[4][64];
