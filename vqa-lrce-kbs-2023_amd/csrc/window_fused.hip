@@ -68,6 +68,14 @@ __device__ __forceinline__ void glds_s(const void* sbase, uint32_t voff, uint32_
 }
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)((LRCE_LDS const void*)p); }
 
+// Workgroup barrier for LDS hand-offs only: __syncthreads() also drains vmcnt(0), i.e. waits for the
+// attention's bias-tile loads and the qkv / O row stores still in flight.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // element j = img[r_base + 8*(j>>2) + 4*hh + (j&3)][lane & 31] of a plain [rows][32] image: the
 // A operand of O^T = V^T P^T in the accumulators' permuted key order (window_attn.hip)
 __device__ __forceinline__ bf16x8 tr_read_perm(const bf16* img, int r_base, int lane) {
@@ -148,6 +156,14 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
   // ---- 1. GEMM: acc[i][j][r] = Y[tok = wm*80 + i*16 + (lane&15)][col = wn*48 + j*16 + 4*(lane>>4) + r]
   const int wm = wave >> 2, wn = wave & 3;
   constexpr int IM = 5, JN = 3;
+  // the qkv bias of this lane's epilogue columns, loaded first: issued after the attention's bias-tile
+  // loads it would wait behind them (in-order vmcnt) — 3.3 us of epilogue per workgroup in the trace
+  float4 bqkv[JN];
+#pragma unroll
+  for (int j = 0; j < JN; ++j) {
+    const int col = wn * 48 + j * 16 + 4 * (lane >> 4);
+    bqkv[j] = *reinterpret_cast<const float4*>(p.b + (col / (HB * HD)) * C + hg * (HB * HD) + (col % (HB * HD)));
+  }
   f32x4 acc[IM][JN];
 #pragma unroll
   for (int i = 0; i < IM; ++i)
@@ -237,8 +253,7 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
   for (int j = 0; j < JN; ++j) {
     const int col = wn * 48 + j * 16 + 4 * (lane >> 4);   // 4 consecutive columns, one head
     const int part = col / (HB * HD), hl = (col % (HB * HD)) / HD, d = col % HD;
-    const int gcol = part * C + hg * (HB * HD) + (col % (HB * HD));
-    const float4 bb = *reinterpret_cast<const float4*>(p.b + gcol);
+    const float4 bb = bqkv[j];
     const float sc = part == 0 ? p.qscale : 1.0f;
     bf16* img = lds + (part * HB + hl) * IMG;
 #pragma unroll
@@ -251,7 +266,7 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
       *reinterpret_cast<bf16x4*>(img + off) = v;
     }
   }
-  __syncthreads();
+  lds_barrier();
   WF_MARK(2)
   // qkv rows for the backward: per token and part, the head pair's 64 columns = 128 contiguous bytes
   for (int it = threadIdx.x; it < n * 3 * 8; it += NW * 64) {
@@ -263,7 +278,7 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
     const uint4 v = *reinterpret_cast<const uint4*>(img + off);
     *reinterpret_cast<uint4*>(p.qkv + ((long long)w * n + tok) * ld3 + part * C + hg * (HB * HD) + c8 * 8) = v;
   }
-  __syncthreads();   // the Q rows are read by the stores above before a unit parks its O in them
+  lds_barrier();   // the Q rows are read by the stores above before a unit parks its O in them
   WF_MARK(3)
 
   // ---- 3. attention: unit u = (head hl, query tile qt), u = wave, wave + 8 (< 10)
@@ -325,7 +340,7 @@ __global__ void __launch_bounds__(NW * 64, 4) wattn_qkv_fwd_kernel(FusedP p) {
     }
     if (hh == 0 && qi < n) p.lse[((long long)w * p.nH + h) * NPAD + qi] = m + __log2f(sum);
   }
-  __syncthreads();
+  lds_barrier();
   WF_MARK(4)
   // O rows: per token the head pair's 64 columns = 128 contiguous bytes
   for (int it = threadIdx.x; it < n * 8; it += NW * 64) {
