@@ -71,6 +71,36 @@ def test_gemm_tall_tiles(M, N, Kd, b_km):
     assert rel(C, ref) < 2e-3
 
 
+@pytest.mark.parametrize("M,N,Kd", [(20000, 512, 128), (5003, 264, 64), (4100, 1024, 96), (3000, 512, 512)])
+def test_gemm_short_k_prefetched_epilogues(M, N, Kd):
+    """Short K (<= 8 full K tiles): every K tile issued up front when it has a stage of its own, and the
+    epilogue's dGELU pre-activation / f32 residual loaded before the tiles.  dX = dY W with dGELU
+    (bf16 out) and Y = X W^T + b + residual (f32 out, through a scatter map with dropped rows);
+    ragged M, a K tail (96) and N % 8 != 0 columns (scalar epilogue) included."""
+    k = K()
+    dy = bf(torch.randn(M, Kd, device=dev))
+    W = bf(torch.randn(Kd, N, device=dev) / math.sqrt(Kd))       # dX [M, N] = dY [M, Kd] W [Kd, N] (B N-major)
+    pre = bf(torch.randn(M, N, device=dev))
+    out = k.linear_dx(dy, W, out_f32=False, dgelu_pre=pre)
+    g = pre.float()
+    phi = 0.5 * (1 + torch.erf(g / math.sqrt(2)))
+    ref = (dy.float() @ W.float()) * (phi + g * torch.exp(-0.5 * g * g) / math.sqrt(2 * math.pi))
+    assert rel(out, ref) < 1e-2
+    x = bf(torch.randn(M, Kd, device=dev))
+    w = bf(torch.randn(N, Kd, device=dev) / math.sqrt(Kd))
+    b = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    perm = torch.randperm(M, device=dev).int()
+    perm[::7] = -1                                               # rows with no output (padded windows)
+    y = torch.full((M, N), 7.0, device=dev)
+    k.linear(x, w, b, out=y, resid=res, c_map=perm)
+    ref = torch.full((M, N), 7.0, device=dev)
+    keep = perm >= 0
+    dst = perm[keep].long()
+    ref[dst] = (x.float() @ w.float().t() + b)[keep] + res[dst]    # the residual is read at the output row
+    assert rel(y, ref) < 2e-3
+
+
 @pytest.mark.parametrize("M,N,Kd", [(320, 768, 768), (1800, 3072, 768), (300, 768, 3072), (17640, 512, 256)])
 def test_gemm_f16_forward(M, N, Kd):
     """fp16 operands (the BERT forward, reference fp16 autocast): f16 MFMA, bias + GELU with the fp16
@@ -222,17 +252,21 @@ def test_gemm_exact_f32_path(M, N, Kd, a_km, b_km):
     assert rel(C2, ref + bias) < 1e-5
 
 
-@pytest.mark.parametrize("M,N,R", [(768, 3072, 10), (3072, 768, 50), (768, 768, 64)])
+@pytest.mark.parametrize("M,N,R", [(768, 3072, 10), (3072, 768, 50), (768, 768, 64), (3072, 768, 30), (772, 100, 7),
+                                   (3076, 776, 9), (36, 68, 9)])
 def test_gemm_f32_outer_accumulate(M, N, R):
-    """dW (+)= dY^T X with a skinny reduction (decoder weight gradients): outer-product kernel."""
+    """dW (+)= dY^T X, db += colsum(dY) with a skinny reduction (decoder weight gradients): the
+    4 x 4 / 2 x 4 per-thread tile kernels, ragged tiles (36 x 68: one partial tile)."""
     k = K()
     dy = torch.randn(R, M, device=dev)
     x = torch.randn(R, N, device=dev)
     dw0 = torch.randn(M, N, device=dev)
-    dw = dw0.clone()
-    k.linear_dw(dy, x, dw)
+    db0 = torch.randn(M, device=dev)
+    dw, db = dw0.clone(), db0.clone()
+    k.linear_dw(dy, x, dw, bias_grad=db)
     ref = dw0.double() + dy.double().t() @ x.double()
     assert rel(dw, ref.float()) < 1e-5
+    assert rel(db, (db0.double() + dy.double().sum(0)).float()) < 1e-5
 
 
 def test_gemm_f32_splitk_repeatable():

@@ -1,9 +1,9 @@
 #!/usr/bin/env python
-"""LayerNorm-backward microbenchmark (dev tool, GPU): the Swin block's norm2 backward shape
-(dy, x f32, + residual gradient, + bf16 copy of dx) per stage, with and without the dw/db
-reductions, against the algorithmic HBM bytes.
+"""LayerNorm microbenchmark (dev tool, GPU): lrce LayerNorm backward / forward at the Swin-B step's
+row x column shapes, isolated (HIP events over back-to-back launches), against torch's native
+layer_norm backward on the same shape.  Bytes are the algorithmic ones of the lrce call.
 
-    python tools/ln_bench.py [--iters 30]
+    python tools/ln_bench.py [--iters 30]      (LRCE_LN_BWD_PERCU=0|k: grid A/B knob of layernorm.hip)
 """
 import argparse
 import os
@@ -16,10 +16,10 @@ import torch  # noqa: E402
 
 from lrce import kernels as K  # noqa: E402
 
-SHAPES = [(282240, 128), (70560, 256), (17640, 512), (4410, 1024), (12000, 768), (320, 768)]
+SHAPES = [(250880, 128), (62720, 256), (15680, 512), (3920, 1024), (62720, 512), (15680, 1024), (3920, 2048), (320, 768)]
 
 
-def timeit(fn, iters):
+def timed(fn, iters):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -29,7 +29,7 @@ def timeit(fn, iters):
         fn()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / iters
+    return e0.elapsed_time(e1) / iters * 1e3
 
 
 def main():
@@ -39,26 +39,32 @@ def main():
     dev = "cuda"
     for R, C in SHAPES:
         x = torch.randn(R, C, device=dev)
-        dy = torch.randn(R, C, device=dev)
-        dres = torch.randn(R, C, device=dev)
         w = torch.rand(C, device=dev) + 0.5
-        b = torch.zeros(C, device=dev)
-        _, mean, rstd = K.layernorm(x, w, b, 1e-5, out_f32=True)
-        dx = torch.empty_like(x)
-        dx16 = torch.empty(R, C, dtype=torch.bfloat16, device=dev)
+        b = torch.randn(C, device=dev)
+        y, mean, rstd = K.layernorm(x, w, b, 1e-5, out_f32=True)
+        dres = torch.randn(R, C, device=dev)
+        dx = torch.empty(R, C, device=dev)
+        dx16 = torch.empty(R, C, device=dev, dtype=torch.bfloat16)
         dw = torch.zeros(C, device=dev)
         db = torch.zeros(C, device=dev)
-        line = f"ln_bwd {R:7d} x {C:5d}:"
-        for name, kw, nbytes in (
-                ("plain", {}, 3 * 4),
-                ("dwdb", dict(dw=dw, db=db), 3 * 4),
-                ("dres+dx16+dwdb", dict(dres=dres, dx16=dx16, dw=dw, db=db), 4 * 4 + 2)):
-            ms = timeit(lambda: K.layernorm_bwd(dy, x, mean, rstd, w, dx, **kw), a.iters)
-            gbs = R * C * nbytes / ms / 1e6
-            line += f"  {name} {ms * 1e3:7.1f} us {gbs:6.0f} GB/s"
-        print(line, flush=True)
-        ms = timeit(lambda: K.layernorm(x, w, b, 1e-5, out=dx), a.iters)
-        print(f"ln_fwd {R:7d} x {C:5d}: {ms * 1e3:7.1f} us {R * C * 8 / ms / 1e6:6.0f} GB/s", flush=True)
+        for dyt in (torch.float32, torch.bfloat16):
+            dy = torch.randn(R, C, device=dev).to(dyt)
+            f = lambda: K.layernorm_bwd(dy, x, mean, rstd, w, dx, dres=dres, dw=dw, db=db, dx16=dx16)  # noqa
+            us = timed(f, a.iters)
+            by = R * C * (4 + dy.element_size() + 4 + 4 + 2) + 8 * R
+            print(f"ln_bwd {R:7d} x {C:5d} dy {str(dyt)[6:]:9s} {us:8.1f} us {by / us / 1e3:7.0f} GB/s", flush=True)
+        xt = x.clone()
+        dyt = torch.randn(R, C, device=dev)
+        tf = lambda: torch.ops.aten.native_layer_norm_backward(dyt, xt, [C], mean.view(R, 1), rstd.view(R, 1), w, b,  # noqa
+                                                               [True, True, True])
+        us = timed(tf, a.iters)
+        by = R * C * (4 + 4 + 4) + 8 * R
+        print(f"torch  {R:7d} x {C:5d} dy f32       {us:8.1f} us {by / us / 1e3:7.0f} GB/s (x, dy read; dx write)", flush=True)
+        y16 = torch.empty(R, C, device=dev, dtype=torch.bfloat16)
+        f = lambda: K.layernorm(x, w, b, 1e-5, out=y16)  # noqa
+        us = timed(f, a.iters)
+        by = R * C * (4 + 2) + 8 * R
+        print(f"ln_fwd {R:7d} x {C:5d} y bf16    {us:8.1f} us {by / us / 1e3:7.0f} GB/s", flush=True)
 
 
 if __name__ == "__main__":

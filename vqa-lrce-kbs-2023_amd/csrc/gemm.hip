@@ -198,7 +198,8 @@ __device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row
 // (alpha, the q-scale columns — host guarantees scale_cols % 8 == 0 on the vector path — and the row
 // scale), so a plain epilogue is a conversion and a 16-B store per 8 outputs.
 template <bool F16>
-__device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int n, int sk, char* cbase) {
+__device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int n, int sk, char* cbase,
+                                          const bf16x8* dg_pf = nullptr, const float4* rs_pf = nullptr) {
   if (m >= p.m || n >= p.n) return;
   const int fl = p.flags;
   const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
@@ -229,7 +230,7 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
       for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
     }
     if (fl & LRCE_EPI_DGELU) {
-      const bf16x8 pre = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(p.aux) + row * p.ld_aux + n);
+      const bf16x8 pre = dg_pf ? *dg_pf : *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(p.aux) + row * p.ld_aux + n);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(from16<F16>(pre[e]));
     }
@@ -240,7 +241,8 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
     }
     if ((fl & LRCE_EPI_RESID) && first) {
       const float* ap = static_cast<const float*>(p.aux) + row * p.ld_aux + n;
-      const float4 r0 = *reinterpret_cast<const float4*>(ap), r1 = *reinterpret_cast<const float4*>(ap + 4);
+      const float4 r0 = rs_pf ? rs_pf[0] : *reinterpret_cast<const float4*>(ap);
+      const float4 r1 = rs_pf ? rs_pf[1] : *reinterpret_cast<const float4*>(ap + 4);
       v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w; v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
     }
     if (fl & LRCE_EPI_ATOMIC) {
@@ -520,6 +522,12 @@ struct GldsOperand {
   __device__ __forceinline__ void advance() { base += step; }
 };
 
+// short-K epilogue-operand prefetch (gemm_glds_kernel): K tiles up to which it is done, and the
+// register slots (accumulator row blocks) it may hold — the f32 residual only up to 4 row blocks
+constexpr int PF_KT = 8;
+constexpr int pf_dg_slots(int im) { return im; }
+constexpr int pf_rs_slots(int im) { return im <= 4 ? im : 1; }
+
 template <int TBM, int TBN, bool A_KM, bool B_KM, bool F16 = false, int NS = 2>
 __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   constexpr int WM = TBM / 2, WN = TBN / 2;      // per-wave tile
@@ -580,7 +588,70 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     }
   };
 
-  if (nfull > 0) {
+  // Short K (<= PF_KT full tiles): the epilogue's global operands (the dGELU pre-activation, the f32
+  // residual) are loaded BEFORE the operand tiles, so they ride the tiles' memory round trip instead
+  // of adding one after the MFMAs (at K = 128 the kernel is a chain of such round trips).  Issued
+  // first, they also complete before the tiles' counted vmcnt waits pass (loads retire in order).
+  constexpr int NH = JN / 2;
+  const int ncol = n0 + wn * WN + (JN * 4) * (lane >> 4);
+  const bool pf_dg = (p.flags & LRCE_EPI_DGELU) && p.vec && nfull <= PF_KT && !p.ws && !(p.flags & LRCE_EPI_ATOMIC);
+  const bool pf_rs = IM <= 4 && (p.flags & LRCE_EPI_RESID) && sk == 0 && p.vec && nfull <= PF_KT && !p.ws &&
+                     !(p.flags & LRCE_EPI_ATOMIC);
+  bf16x8 dgp[pf_dg_slots(IM)][NH];
+  float4 rsp[pf_rs_slots(IM)][NH][2];
+  if (pf_dg || pf_rs) {
+#pragma unroll
+    for (int i = 0; i < IM; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+      const long long row = m < p.m ? (p.c_map ? (long long)p.c_map[m] : (long long)m) : -1;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const int n = ncol + 8 * h;
+        const bool ok = row >= 0 && n + 8 <= p.n;
+        if (pf_dg && i < pf_dg_slots(IM)) {
+          const bf16* src = static_cast<const bf16*>(p.aux) + (ok ? row * p.ld_aux + n : 0);
+          dgp[i][h] = *reinterpret_cast<const bf16x8*>(src);
+        }
+        if (pf_rs && i < pf_rs_slots(IM)) {
+          const float* src = static_cast<const float*>(p.aux) + (ok ? row * p.ld_aux + n : 0);
+          rsp[i][h][0] = *reinterpret_cast<const float4*>(src);
+          rsp[i][h][1] = *reinterpret_cast<const float4*>(src + 4);
+        }
+      }
+    }
+  }
+  if (nfull > 0 && nfull <= NS) {
+    // every K tile has a stage of its own: issue them all now, then consume in order (one
+    // round trip for the whole K instead of one per stage turnover)
+    constexpr int INFLIGHT = (TBM + TBN) / 32;
+    GldsOperand<A_KM, TBM> ga;
+    GldsOperand<B_KM, TBN> gb;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const uint32_t la0 = lds_addr(sa0), lb0 = lds_addr(sb0);
+    ga.init(abase, p.lda, p.m, m0, kb, wave, lane);
+    gb.init(bbase, p.ldb, p.n, n0, kb, wave, lane);
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+      if (i < nfull) {
+        if (i) { ga.advance(); gb.advance(); }
+        ga.issue(la0 + (uint32_t)(i * STG * 2), wave_u);
+        gb.issue(lb0 + (uint32_t)(i * STG * 2), wave_u);
+      }
+    for (int kt = 0; kt < nfull; ++kt) {
+      const int ahead = nfull - 1 - kt;   // tiles issued after tile kt
+      if (NS >= 4 && ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * INFLIGHT) : "memory");
+      else if (NS >= 3 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * INFLIGHT) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      compute(sa0 + kt * STG, sb0 + kt * STG);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // every wave is done with every stage (tail / LDS epilogue reuse)
+    __builtin_amdgcn_sched_barrier(0);
+  } else if (nfull > 0) {
     // NS-stage ring, one barrier per K tile: at the top of iteration kt this wave waits for its part
     // of tile kt (tiles kt+1 .. kt+NS-2 stay in flight), the barrier makes every wave's part visible
     // AND proves every wave finished tile kt-1, whose stage then receives tile kt+NS-1.
@@ -718,7 +789,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       }
     }
   };
-  const int ncol = n0 + wn * WN + (JN * 4) * (lane >> 4);
   if (p.ws) {
     // split-K slab: this slice's alpha * partial tile, plain stores (reduced by splitk_reduce_kernel)
     float* slab = p.ws + (long long)sk * p.m * p.n;
@@ -757,7 +827,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(u[2 * h + (e >> 2)][e & 3]);
-      epilogue8<F16>(p, v, m, ncol + 8 * h, sk, cbase);
+      constexpr int i = decltype(ic)::value;
+      const bf16x8* dg = (pf_dg && i < pf_dg_slots(IM)) ? &dgp[i < pf_dg_slots(IM) ? i : 0][h] : nullptr;
+      const float4* rs = (pf_rs && i < pf_rs_slots(IM)) ? rsp[i < pf_rs_slots(IM) ? i : 0][h] : nullptr;
+      epilogue8<F16>(p, v, m, ncol + 8 * h, sk, cbase, dg, rs);
     }
   });
 }

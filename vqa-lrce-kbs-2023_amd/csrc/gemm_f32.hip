@@ -403,6 +403,77 @@ __global__ void __launch_bounds__(256) outer_kernel(SkinnyP p) {
   if ((p.flags & LRCE_EPI_BIAS_GRAD) && n == 0) p.bias_grad[m] += p.alpha * asum;   // db (one owner per m)
 }
 
+// The same outer-product sum with an MR x 4 block of C per thread (MR consecutive rows m, 4 columns
+// n): per reduction step one A vector (MR rows) and one B float4 feed 4 MR FMAs, so the X rows,
+// which every output row shares, are pulled from L2 MR times less often than by outer_kernel (one
+// float4 of B per 4 outputs: at 3072 x 768 x R=30 that re-read, not the 9.4 MB read-modify-write of
+// C, set the time).  Workgroup = 16 x 16 threads over a (16 MR) x 64 tile; lanes run along n, so a
+// wave instruction touches MR x 4 rows of 256 contiguous bytes.  All U steps of a batch are issued
+// before any is consumed.
+template <int MR>
+__global__ void __launch_bounds__(256) outer_tile_kernel(SkinnyP p) {
+  constexpr int U = 8;
+  const int tn = threadIdx.x & 15, tm = threadIdx.x >> 4;
+  const int n = blockIdx.x * 64 + tn * 4;
+  const int m = (blockIdx.y * 16 + tm) * MR;
+  if (n >= p.n || m >= p.m) return;
+  const bool acc_c = p.flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM);
+  float* cbase = static_cast<float*>(p.c) + (long long)m * p.ldc + n;
+  float4 o[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+    o[i] = acc_c ? *reinterpret_cast<const float4*>(cbase + (long long)i * p.ldc) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 acc[MR];
+  float asum[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) { acc[i] = make_float4(0.f, 0.f, 0.f, 0.f); asum[i] = 0.f; }
+  const float* ap = p.a + m;
+  const float* bp = static_cast<const float*>(p.b) + n;
+  auto lda_vec = [&](int r, float (&av)[MR]) {
+    if constexpr (MR == 4) {
+      const float4 t = *reinterpret_cast<const float4*>(ap + (long long)r * p.lda);
+      av[0] = t.x; av[1] = t.y; av[2] = t.z; av[3] = t.w;
+    } else {
+      const float2 t = *reinterpret_cast<const float2*>(ap + (long long)r * p.lda);
+      av[0] = t.x; av[1] = t.y;
+    }
+  };
+  auto step = [&](const float (&av)[MR], const float4& bv) {
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      asum[i] += av[i];
+      acc[i].x = fmaf(av[i], bv.x, acc[i].x); acc[i].y = fmaf(av[i], bv.y, acc[i].y);
+      acc[i].z = fmaf(av[i], bv.z, acc[i].z); acc[i].w = fmaf(av[i], bv.w, acc[i].w);
+    }
+  };
+  int r = 0;
+  for (; r + U <= p.k; r += U) {
+    float av[U][MR];
+    float4 bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      lda_vec(r + u, av[u]);
+      bv[u] = *reinterpret_cast<const float4*>(bp + (long long)(r + u) * p.ldb);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) step(av[u], bv[u]);
+  }
+  for (; r < p.k; ++r) {
+    float av[MR];
+    lda_vec(r, av);
+    step(av, *reinterpret_cast<const float4*>(bp + (long long)r * p.ldb));
+  }
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    if (m + i >= p.m) break;
+    float4 w;
+    w.x = fmaf(acc[i].x, p.alpha, o[i].x); w.y = fmaf(acc[i].y, p.alpha, o[i].y);
+    w.z = fmaf(acc[i].z, p.alpha, o[i].z); w.w = fmaf(acc[i].w, p.alpha, o[i].w);
+    *reinterpret_cast<float4*>(cbase + (long long)i * p.ldc) = w;
+    if ((p.flags & LRCE_EPI_BIAS_GRAD) && n == 0) p.bias_grad[m + i] += p.alpha * asum[i];   // db (one owner per m)
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Skinny exact-f32 linear with a LayerNorm prologue on A (lrce_gemm_ln).  The recurrent decoder's
 // post-norm LayerNorms (nn.TransformerDecoderLayer norm1..3, fusionv3.py:8-17) are folded into the
@@ -756,8 +827,18 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
     q.rng_off = lrce_rng_offset();
     const bool outer_ok = !bh && lrce_gemm_f32_outer_ok(d) && d->drop_p <= 0.f;
     if (outer_ok) {
-      const long long work = (long long)d->m * (d->n / 4);
-      outer_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(q);
+      // MR x 4 per thread when the A rows allow vector loads: 4 while that still gives >= 512
+      // workgroups, else 2 (a 768 x 768 dW: 288 workgroups)
+      const bool avec = (reinterpret_cast<uintptr_t>(d->a) & 15) == 0 && d->lda % 4 == 0;
+      const long long tiles64 = (long long)((d->n + 63) / 64) * ((d->m + 63) / 64);
+      if (avec && d->m % 4 == 0 && tiles64 >= 512) {
+        outer_tile_kernel<4><<<dim3((unsigned)((d->n + 63) / 64), (unsigned)((d->m + 63) / 64)), 256, 0, st>>>(q);
+      } else if (avec && d->m % 2 == 0) {
+        outer_tile_kernel<2><<<dim3((unsigned)((d->n + 63) / 64), (unsigned)((d->m + 31) / 32)), 256, 0, st>>>(q);
+      } else {
+        const long long work = (long long)d->m * (d->n / 4);
+        outer_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(q);
+      }
       return lrce_check_launch("gemm_f32(outer)");
     }
     if (d->flags & LRCE_EPI_BIAS_GRAD) return lrce_fail(LRCE_E_ARG, "gemm(f32): internal: bias grad on a fused path");

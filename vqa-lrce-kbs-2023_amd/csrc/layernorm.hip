@@ -10,6 +10,7 @@
 // its output row is zero and it takes no part in the backward.
 #include "common.h"
 #include "lrce_capi.h"
+#include <cstdlib>
 
 namespace {
 
@@ -340,14 +341,32 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ p
   if (dst) *dst += s;
 }
 
-// rows per wave of ln_bwd: small inputs (the decoder / BERT rows) one row per wave (latency-bound:
-// as many waves as rows); larger ones 4-8 with the next row prefetched.  Without a partials
-// workspace every block adds its dw/db into the SAME 2 x cols addresses, so blocks are capped.
-int ln_bwd_blocks(int rows, int lpr, bool ws) {
+// ln_bwd grid.  With a partials workspace: one row per wave while the whole grid fits on the chip
+// at once, else exactly one chip-full of blocks looping over the rows (a balanced grid-stride with
+// the next row prefetched): the wave count, not rows per wave, is what keeps enough loads in flight
+// (a fixed 8 rows per wave left the 17,640 x 512 stage-3 rows on 2 waves per SIMD at 4 TB/s).
+// Resident blocks per CU follow the register budget of the CH instantiation (one wave per SIMD
+// per block).  Without a workspace every block adds its dw/db into the SAME 2 x cols addresses, so
+// blocks are capped.
+int ln_bwd_blocks(int rows, int lpr, bool ws, int cols) {
   const int rpb = 4 * (64 / lpr);                 // rows per block per pass
-  const int per_wave = ws ? (rows <= 2048 ? 1 : rows <= 8192 ? 4 : 8) : (rows <= 8192 ? 1 : 8);
-  const int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
-  return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+  const int nb1 = (rows + rpb - 1) / rpb;         // one row per wave
+  if (!ws) {
+    const int per_wave = rows <= 8192 ? 1 : 8;
+    const int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
+    return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+  }
+  static const int knob = getenv("LRCE_LN_BWD_PERCU") ? atoi(getenv("LRCE_LN_BWD_PERCU")) : -1;   // A/B: 0 = fixed rows per wave
+  if (knob == 0) {
+    const int per_wave = rows <= 2048 ? 1 : rows <= 8192 ? 4 : 8;
+    const int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
+    return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+  }
+  const int nch = cols / 4;
+  const int per_cu = knob > 0 ? knob : nch <= 64 ? 8 : nch <= 128 ? 6 : nch <= 256 ? 3 : 2;   // VGPRs: <=64, 80, 108-136, 240
+  int cap = 256 * per_cu;
+  if (cap > 2048) cap = 2048;                     // ln_bwd_reduce: <= LN_RED_MAXY * LN_RED_ROWS partial rows
+  return nb1 < 1 ? 1 : (nb1 > cap ? cap : nb1);
 }
 int ln_bwd_lpr(int cols) { return cols / 4 <= 32 ? 32 : 64; }
 
@@ -398,13 +417,13 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
   const int nch = cols / 4;
   const int lpr = ln_bwd_lpr(cols);
   const bool want = dw || db;
-  const int nb_ws = ln_bwd_blocks(rows, lpr, true);
+  const int nb_ws = ln_bwd_blocks(rows, lpr, true, cols);
   const int ny = (nb_ws + LN_RED_ROWS - 1) / LN_RED_ROWS;
   // dw / db partials per block + a deterministic reduce launch; a one-block problem (rows <= 4-8, the
   // decoder's rows) or no workspace: one block adds its sums directly
   float* part = want && nb_ws > 1 && workspace && workspace_elems >= (int64_t)(nb_ws + ny) * 2 * cols + LN_RED_CTRS
                     ? workspace : nullptr;
-  const int nb = (part || !want) ? nb_ws : ln_bwd_blocks(rows, lpr, false);
+  const int nb = (part || !want) ? nb_ws : ln_bwd_blocks(rows, lpr, false, cols);
 #define LNB3(TD, TX, CH, LPR)                                                                                          \
   ln_bwd<TD, TX, CH, LPR><<<nb, 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, \
                                                      nseg, mean, rstd, w, dx, dres, dw, db, rows, cols,      \
@@ -431,6 +450,6 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
 
 extern "C" int64_t lrce_layernorm_bwd_workspace(int rows, int cols) {
   if (rows <= 0 || cols <= 0) return 0;
-  const int nb = ln_bwd_blocks(rows, ln_bwd_lpr(cols), true);
+  const int nb = ln_bwd_blocks(rows, ln_bwd_lpr(cols), true, cols);
   return nb > 1 ? (int64_t)(nb + (nb + LN_RED_ROWS - 1) / LN_RED_ROWS) * 2 * cols + LN_RED_CTRS : 0;
 }

@@ -415,7 +415,9 @@ class _SwinBlockFn(torch.autograd.Function):
         dpre = K.linear_dx(dout16, flat.w16(blk.mlp.fc2.weight), out_f32=False, dgelu_pre=pre)
         del g, pre, dout16
         _wgrad(flat, blk.mlp.fc1, dpre, h2)
-        dh2 = K.linear_dx(dpre, flat.w16(blk.mlp.fc1.weight))
+        # the LayerNorms' input gradients arrive as bf16 GEMM outputs (as under the reference's
+        # autocast, where a bf16 linear's grad_input is bf16): half the bytes of the LN backward's dy
+        dh2 = K.linear_dx(dpre, flat.w16(blk.mlp.fc1.weight), out_f32=False)
         del dpre, h2
         dx_mid = torch.empty_like(x_mid)
         # attention branch input gradient s1 * dx_mid, as bf16 in window order (rows of o / qkv)
@@ -438,7 +440,7 @@ class _SwinBlockFn(torch.autograd.Function):
             K.wattn_dbias(dbp, geo.n_win, nH, geo.ws, _bin_rows(at, geo.ws), gt)
         del dbp
         _wgrad(flat, at.qkv, dqkv, xw)
-        dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight))
+        dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight), out_f32=False)
         del dqkv, qkv, xw
         dx = torch.empty_like(x)
         up = ctx.up
@@ -488,7 +490,7 @@ class _PatchMergeFn(torch.autograd.Function):
         gw = _g(flat, pm.reduction.weight)
         if gw is not None:
             K.linear_dw(dy16, xl, gw)
-        dxl = K.linear_dx(dy16, flat.w16(pm.reduction.weight))
+        dxl = K.linear_dx(dy16, flat.w16(pm.reduction.weight), out_f32=False)
         dx = torch.empty_like(x)
         K.layernorm_bwd(dxl, x, mean, rstd, pm.norm.weight, dx, in_map=geo.merge_map, nseg=4, rows=geo.M_merged,
                         cols=4 * pm.dim, dw=_g(flat, pm.norm.weight), db=_g(flat, pm.norm.bias))
