@@ -363,7 +363,8 @@ int lrce_dec_ca_fwd(const LrceDecCa* args, void* stream);
 /* Backward of the cross-attention block from dx2 = d LN2(x2p): dx2p = LN2 backward (mean2 / rstd2 /
  * g2), dcao = its out-dropout backward -> dcao_out (the out_proj's output gradient); dctx = W_o^T dcao;
  * attention backward -> dq_out, dK / dV of the memory (video rows dk1 (+ dv_off for dV) with their
- * own dstride1 / dld1: STORED when bdiv1 == 1, atomically added otherwise; text rows dk2 accumulated);
+ * own dstride1 / dld1: STORED when bdiv1 == 1, atomically added otherwise; text rows dk2 accumulated,
+ * or stored when dk2_store);
  * dx1_out = dx2p + W_q^T dq.  LayerNorm parameter gradients: lrce_dec_ln_grads. */
 typedef struct LrceDecCaBwd {
   int32_t B;
@@ -390,6 +391,7 @@ typedef struct LrceDecCaBwd {
   uint64_t seed;   /* as lrce_dec_ca_fwd */
   float* slab;
   uint32_t* counters;
+  int32_t dk2_store;   /* 1: the text rows' dK / dV are STORED (the first recurrent step of the backward; no zeroed buffer needed), 0: added */
 } LrceDecCaBwd;
 int lrce_dec_ca_bwd(const LrceDecCaBwd* args, void* stream);
 /* Backward of the self-attention block from dx1 = d LN1(x1p): dx1p = LN1 backward, dsao = its out-
@@ -428,6 +430,12 @@ int lrce_dec_set_trace(uint64_t* buf);
  * buffer also receives lrce_wattn_qkv_fwd's marks (start, GEMM done, epilogue done, qkv stored, attention
  * done, O stored; tools/wattn_trace.py WATTN_FWD=1): trace one kernel per launch. */
 int lrce_wattn_set_trace(uint64_t* buf);
+
+/* Debug: phase timestamps of the LDS-DMA GEMM kernel into buf[workgroup * 8 + mark] (marks: start, first K tile
+ * landed, K loop done, epilogue stores issued and drained; [6] HW_ID, [7] XCC_ID), workgroups of split 0 only;
+ * NULL turns it off (the default).  Recorded only by a library built with -DLRCE_GEMM_TRACE
+ * (tools/gemm_trace.py). */
+int lrce_gemm_set_trace(uint64_t* buf);
 
 /* ---------------------------------------------------------------- elementwise / data movement */
 /* Patch-embed input stage: [ImageNet Normalize (video.py:35)] + zero-pad T to a multiple of 2

@@ -698,7 +698,8 @@ struct CaBwdP {
   float* dk1;                     // video dK (dV at + dv_off): row (b/bdiv1)*dstride1 + j*dld1
   long long dstride1, dld1;
   int dkv1_atomic;                // rows shared by bdiv1 > 1 query rows: atomics, else stores
-  float* dk2;                     // text dK, accumulated (one writer per row)
+  float* dk2;                     // text dK, accumulated (one writer per row), or stored (dk2_store)
+  int dk2_store;
   long long dstride2, dld2;
   long long dv_off;
   const f16* wq;                  // in_proj rows 0..E
@@ -767,7 +768,7 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
   for (int i = 0; i < TXI; ++i) {
     const int e = t + 256 * i, tj = e >> 3, c = e & 7;
     told[i][0] = told[i][1] = told[i][2] = told[i][3] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tj < p.kv.lk2) {
+    if (tj < p.kv.lk2 && !p.dk2_store) {
       const float* src = p.dk2 + tbase + (long long)tj * p.dld2 + c * 8;
       told[i][0] = *reinterpret_cast<const float4*>(src);
       told[i][1] = *reinterpret_cast<const float4*>(src + 4);
@@ -1176,7 +1177,7 @@ extern "C" int lrce_dec_ca_bwd(const LrceDecCaBwd* a, void* stream) {
   p.B = a->B; p.dx2 = a->dx2; p.x2p = a->x2p; p.mean2 = a->mean2; p.rstd2 = a->rstd2; p.g2 = a->g2;
   p.dcao_out = a->dcao_out; p.wo = reinterpret_cast<const f16*>(a->wo); p.kv = kv_conv(a->kv); p.q = a->q; p.ctx = a->ctx;
   p.lse = a->lse; p.dq_out = a->dq_out; p.dk1 = a->dk1; p.dstride1 = a->dstride1; p.dld1 = a->dld1;
-  p.dkv1_atomic = a->kv.bdiv1 > 1; p.dk2 = a->dk2; p.dstride2 = a->dstride2; p.dld2 = a->dld2; p.dv_off = a->dv_off;
+  p.dkv1_atomic = a->kv.bdiv1 > 1; p.dk2 = a->dk2; p.dk2_store = a->dk2_store; p.dstride2 = a->dstride2; p.dld2 = a->dld2; p.dv_off = a->dv_off;
   p.wq = reinterpret_cast<const f16*>(a->wq); p.dx1_out = a->dx1_out; p.p = a->drop_p; p.seed = a->seed;
   p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters; p.trace = g_dec_trace_host;
   return launch(dec_ca_bwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_ca_bwd");

@@ -52,7 +52,21 @@ struct GemmP {
   int f16;   // 16-bit tensors are IEEE fp16 (LrceGemmDesc.f16)
   int group_m;   // tile raster: groups of group_m tile rows, column-major inside a group (1 = row-major)
   const float* alpha_dev;   // non-null: alpha read from device memory (a gradient scale computed on the GPU)
+  unsigned long long* trace;   // phase timestamps (builds with -DLRCE_GEMM_TRACE only; lrce_gemm_set_trace)
 };
+
+// Debug phase marks of gemm_glds_kernel (tools/gemm_trace.py): wave 0 of every workgroup stores
+// s_memrealtime (100 MHz) at mark i into trace[blockIdx.x * 8 + i]; slot 6/7 = HW_ID / XCC_ID.
+#ifdef LRCE_GEMM_TRACE
+#define GT_MARK(I)                                                                                   \
+  do {                                                                                               \
+    if (p.trace && threadIdx.x == 0 && blockIdx.y == 0)                                              \
+      p.trace[(long long)blockIdx.x * 8 + (I)] = __builtin_amdgcn_s_memrealtime();                   \
+  } while (0)
+#else
+#define GT_MARK(I) do {} while (0)
+#endif
+static unsigned long long* g_gemm_trace = nullptr;
 
 __device__ __forceinline__ float alpha_of(const GemmP& p) { return p.alpha_dev ? *p.alpha_dev : p.alpha; }
 
@@ -543,6 +557,13 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   int tm, tn;
   tile_of(p, lin, tm, tn);
   const int m0 = tm * TBM, n0 = tn * TBN;
+  GT_MARK(0);
+#ifdef LRCE_GEMM_TRACE
+  if (p.trace && threadIdx.x == 0 && blockIdx.y == 0) {
+    p.trace[(long long)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    p.trace[(long long)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+  }
+#endif
   const bf16* abase = static_cast<const bf16*>(p.a) + (long long)bz * p.sa;
   const bf16* bbase = p.b + (long long)bz * p.sb;
   const int kb = sk * p.k_chunk;
@@ -645,6 +666,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      if (kt == 0) GT_MARK(1);
       compute(sa0 + kt * STG, sb0 + kt * STG);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -686,6 +708,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      if (kt == 0) GT_MARK(1);
       if (kt + NS - 1 < nfull) {
         const int nxt = cur == 0 ? NS - 1 : cur - 1;   // (kt + NS - 1) % NS
         ga.advance(); gb.advance();
@@ -710,6 +733,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     __syncthreads();
   }
 
+  GT_MARK(2);
   if (bias_block && (lane >> 4) == 0) {   // accb row 0 of each C^T block: sum_k A(m, k), m = lane&15
     float* db = const_cast<float*>(p.bias);
 #pragma unroll
@@ -833,6 +857,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       epilogue8<F16>(p, v, m, ncol + 8 * h, sk, cbase, dg, rs);
     }
   });
+#ifdef LRCE_GEMM_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stores have left this wave
+#endif
+  GT_MARK(3);
 }
 
 // C[m][n] += sum_s ws[s][m][n]  (n % 4 == 0, ldc % 4 == 0)
@@ -963,6 +991,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   p.aux_out = static_cast<bf16*>(d->aux_out); p.ld_aux_out = d->ld_aux_out;
   p.a_map = d->a_map; p.c_map = d->c_map;
   p.alpha = d->alpha; p.alpha_dev = d->alpha_dev; p.scale_cols = d->scale_cols; p.scale_val = d->scale_val;
+  p.trace = g_gemm_trace;
   p.row_scale = d->row_scale; p.rows_per_scale = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
   p.a_row_scale = d->a_row_scale; p.a_rows_per_scale = d->a_rows_per_scale > 0 ? d->a_rows_per_scale : 1;
   if (p.a_row_scale && !d->a_f32) return lrce_fail(LRCE_E_ARG, "gemm: a_row_scale needs f32 A");
@@ -1048,8 +1077,30 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
       }
       return (int)LRCE_OK;
     };
-    // two stages: a third (one resident workgroup per CU) measured 1.3-1.5x slower on every step shape
-    if (int rc = launch(std::integral_constant<int, 2>{})) return rc;
+    // two stages: a third (one resident workgroup per CU) measured 1.3-1.5x slower on every step shape.
+    // 64x64 tiles (small problems: few workgroups, each latency-bound on its operand stream) take a
+    // 4-stage ring in the same 64 KB of LDS as two 128x128 stages, so three K tiles are in flight
+    // per workgroup instead of one
+    static const int g_small_ns = getenv("LRCE_GEMM_SMALL_NS") ? atoi(getenv("LRCE_GEMM_SMALL_NS")) : 4;   // A/B knob
+    auto launch_small = [&](auto nsc) {
+      constexpr int S = decltype(nsc)::value;
+      switch (gk) {
+        case 32 + 7: gemm_glds_kernel<64, 64, true, true, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 6: gemm_glds_kernel<64, 64, true, false, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 32 + 4: gemm_glds_kernel<64, 64, false, false, true, S><<<grid, NT, 0, s>>>(p); break;
+        case 7: gemm_glds_kernel<64, 64, true, true, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 6: gemm_glds_kernel<64, 64, true, false, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 5: gemm_glds_kernel<64, 64, false, true, false, S><<<grid, NT, 0, s>>>(p); break;
+        case 4: gemm_glds_kernel<64, 64, false, false, false, S><<<grid, NT, 0, s>>>(p); break;
+        default: return lrce_fail(LRCE_E_ARG, "gemm: no LDS-DMA kernel for operand layout key %d", gk);
+      }
+      return (int)LRCE_OK;
+    };
+    if (small && g_small_ns == 4) {
+      if (int rc = launch_small(std::integral_constant<int, 4>{})) return rc;
+    } else if (int rc = launch(std::integral_constant<int, 2>{})) {
+      return rc;
+    }
     if (p.ws) {
       const long long q4 = (long long)d->m * d->n / 4;
       if (split >= 8)
@@ -1071,4 +1122,11 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     case 3: gemm_kernel<false, true, true><<<grid, NT, 0, s>>>(p); break;
   }
   return lrce_check_launch("gemm");
+}
+
+// debug: phase timestamps of gemm_glds_kernel into buf (device, >= 8 per workgroup), NULL = off; the
+// marks exist only in a -DLRCE_GEMM_TRACE build (tools/gemm_trace.py)
+extern "C" int lrce_gemm_set_trace(uint64_t* buf) {
+  g_gemm_trace = reinterpret_cast<unsigned long long*>(buf);
+  return LRCE_OK;
 }

@@ -120,7 +120,7 @@ class DecCaBwd(ctypes.Structure):
         ("dq_out", ctypes.c_void_p), ("dk1", ctypes.c_void_p), ("dstride1", ctypes.c_int64), ("dld1", ctypes.c_int64),
         ("dk2", ctypes.c_void_p), ("dstride2", ctypes.c_int64), ("dld2", ctypes.c_int64), ("dv_off", ctypes.c_int64),
         ("wq", ctypes.c_void_p), ("dx1_out", ctypes.c_void_p),
-    ] + _WS
+    ] + _WS + [("dk2_store", ctypes.c_int32)]
 
 
 class DecSaBwd(ctypes.Structure):
@@ -162,6 +162,7 @@ _SIGS = {
     "lrce_dec_ln_grads": [_P, _P, _P, _P, _P, _P, _I, _I, _P],
     "lrce_dec_set_trace": [_P],
     "lrce_wattn_set_trace": [_P],
+    "lrce_gemm_set_trace": [_P],
     "lrce_frames_resize": [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P],
     "lrce_patch_im2col": [_P, _I, _I, _I, _I, _I64, _I64, _I64, _I, _P, _P],
     "lrce_colsum": [_P, _I, _P, _I64, _I, _I, _P, _I, _P, _P],

@@ -206,6 +206,31 @@ class GradReducer:
             for bi in order:
                 self._exchange(bi)
 
+    def chunk_ranges(self, order):
+        """The optimizer chunk ranges (1024 elements each; every tensor starts on a chunk) covered by
+        the buckets of `order`, merged.  A bucket ends inside its last tensor's final chunk, which no
+        other tensor shares, so the ranges of different buckets never overlap."""
+        rs = sorted((s // 1024, -(-e // 1024)) for s, e, _ in (self.buckets[bi] for bi in order))
+        out = []
+        for c0, c1 in rs:
+            if out and c0 <= out[-1][1]:
+                out[-1] = (out[-1][0], max(out[-1][1], c1))
+            else:
+                out.append((c0, c1))
+        return out
+
+    def exchanged_stream(self):
+        """A stream ordered after every exchange started so far (the collective stream; f32 buckets:
+        it also waits for their all-reduce handles), for work that consumes the summed buckets while
+        the compute stream moves on.  None on CPU."""
+        if self.comm is None:
+            return None
+        if self.grad16 is None:
+            with torch.cuda.stream(self.comm):
+                for h in self.handles:
+                    h.wait()
+        return self.comm
+
     def join(self):
         """The current stream waits for every exchange started so far.  Returns the grad_scale."""
         if self.world > 1:

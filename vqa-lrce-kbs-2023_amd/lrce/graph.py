@@ -33,12 +33,14 @@ class CapturedStep:
 
 
 class _Captured:
-    __slots__ = ("static", "out", "g_step", "g_tail", "g_opt", "warm", "order", "order_tail", "stage", "turn", "free")
-    # g_tail / order_tail: one captured graph and one bucket-order list per tail segment
+    __slots__ = ("static", "out", "g_step", "g_tail", "g_opt", "g_early", "warm", "order", "order_tail", "stage", "turn",
+                 "free")
+    # g_tail / order_tail: one captured graph and one bucket-order list per tail segment; g_early: the
+    # optimizer update of the buckets exchanged before each tail segment (None: not split)
 
     def __init__(self, inputs, device):
         self.static = [torch.empty_like(t, device=device) for t in inputs]
-        self.out = self.g_step = self.g_tail = self.g_opt = self.order = self.order_tail = None
+        self.out = self.g_step = self.g_tail = self.g_opt = self.g_early = self.order = self.order_tail = None
         self.warm = False
         # two device staging sets for host batches: the H2D copy of batch i+1 runs on a side stream
         # while step i is still replaying, and never overwrites a set the main stream still reads
@@ -64,10 +66,18 @@ class TrainStepGraph:
     or a list of segments (E2EBase.backward_segments): body then ends with the fusion head's backward,
     and the step is graph(forward + head backward) -> exchange of the head's buckets, overlapping ->
     graph(segment 1) -> exchange of the buckets it completed, overlapping -> graph(segment 2) ... ->
-    exchange of the rest -> graph(optimizer)."""
+    exchange of the rest -> graph(optimizer).
 
-    def __init__(self, body, optim, reducer=None, world=1, tail=None):
+    early_opt (with a tail): the optimizer update of the buckets exchanged before a segment (the head's
+    before segment 1, segment 1's before segment 2, ...) is captured as a graph of its own and replayed
+    on the collective stream right behind that exchange, so it runs beside the next backward segment
+    (which reads none of those parameters) instead of after the whole backward; the final optimizer
+    graph updates the rest and sums the next step's norms (agent_base.py:76's DDP overlap, carried
+    through to the update)."""
+
+    def __init__(self, body, optim, reducer=None, world=1, tail=None, early_opt=True):
         self.body, self.optim, self.reducer, self.world = body, optim, reducer, world
+        self.early_opt = early_opt
         if tail is not None and not isinstance(tail, (list, tuple)):
             tail = [tail]
         self.tail = list(tail) if (tail and reducer is not None) else None
@@ -154,6 +164,16 @@ class TrainStepGraph:
                     st.order_tail = [list(self.reducer.captured[a:b]) for a, b in zip(marks[:-1], marks[1:])]
             finally:
                 self.reducer.capture_end()
+            if self.tail is not None and self.early_opt:
+                # one update graph per exchange that a later segment overlaps; its own memory pool,
+                # since it replays concurrently with a backward segment (it allocates nothing anyway)
+                epool = torch.cuda.graph_pool_handle()
+                st.g_early = []
+                for order in [st.order] + st.order_tail[:-1]:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=epool):
+                        self.optim.update_chunks(self.reducer.chunk_ranges(order), grad_scale=1.0 / self.world)
+                    st.g_early.append(g)
             st.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(st.g_opt, pool=pool):
                 self.optim.step(grad_scale=1.0 / self.world)
@@ -177,7 +197,10 @@ class TrainStepGraph:
         st.g_step.replay()
         if st.g_tail is not None:
             self.reducer.exchange(st.order)        # the head's buckets, beside the extractors' backward
-            for g, order in zip(st.g_tail, st.order_tail):
+            for i, (g, order) in enumerate(zip(st.g_tail, st.order_tail)):
+                if st.g_early is not None:         # their update too, behind the exchange
+                    with torch.cuda.stream(self.reducer.exchanged_stream()):
+                        st.g_early[i].replay()
                 g.replay()
                 self.reducer.exchange(order)       # this segment's buckets, beside the next segment
             self.reducer.join()

@@ -537,13 +537,16 @@ def dec_ca_fwd(x1p, g1, b1, wq, bq, kv, wo, bo, *, x1_out, mean_out, rstd_out, q
 
 
 def dec_ca_bwd(dx2, x2p, mean2, rstd2, g2, wo, kv, q, ctx, lse, wq, *, dcao_out, dq_out, dk1, dstride1, dld1, dx1_out, p,
-               seed, dk2=None, dstride2=0, dld2=0, dv_off):
+               seed, dk2=None, dstride2=0, dld2=0, dv_off, dk2_store=False):
+    """dk2_store: the text rows' dK / dV are written, not added (the backward's first recurrent step:
+    the accumulation buffer needs no zeroing launch)."""
     a = N.DecCaBwd()
     a.B, a.dx2, a.x2p, a.mean2, a.rstd2, a.g2 = dx2.shape[0], ptr(dx2), ptr(x2p), ptr(mean2), ptr(rstd2), ptr(g2)
     a.dcao_out, a.wo, a.kv, a.q, a.ctx, a.lse = ptr(dcao_out), ptr(wo), kv, ptr(q), ptr(ctx), ptr(lse)
     a.dq_out, a.dk1, a.dstride1, a.dld1 = ptr(dq_out), ptr(dk1), dstride1, dld1
     a.dk2, a.dstride2, a.dld2, a.dv_off = ptr(dk2), dstride2, dld2, dv_off
     a.wq, a.dx1_out = ptr(wq), ptr(dx1_out)
+    a.dk2_store = int(bool(dk2_store))
     _dec_ws(a, dx2.device, p, seed)
     _timed("decoder", dx1_out, lambda: call("lrce_dec_ca_bwd", ctypes.byref(a), stream_of(dx1_out)))
 

@@ -261,7 +261,7 @@ def _layer_bwd_fused(lay, flat, st, dx3, dkvv_step, dkvt, S, Lt, p, seed, grads,
     K.dec_ca_bwd(dx2, st.x2p, st.m2, st.r2, lay.norm2.weight, _wq(lay, ca.out_proj.weight), st.kv, st.q, st.ctx, st.lse,
                  wca[:E], dcao_out=grads.dcao[step], dq_out=grads.dq[step], dk1=dkvv_step, dstride1=S * 150 * 2 * E,
                  dld1=2 * E, dk2=dkvt if Lt else None, dstride2=Lt * 2 * E, dld2=2 * E, dv_off=E,
-                 dx1_out=grads.dln1[step], p=p, seed=seed + 2)
+                 dx1_out=grads.dln1[step], p=p, seed=seed + 2, dk2_store=step == S - 1)
     dx0 = torch.empty_like(st.x1p)
     K.dec_sa_bwd(grads.dln1[step], st.x1p, st.m1, st.r1, lay.norm1.weight, _wq(lay, sa.out_proj.weight), wsa[2 * E:],
                  dsao_out=grads.dsao[step], dsav_out=grads.dsav[step], dx0_out=dx0, p=p, seed=seed)
@@ -377,10 +377,13 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         # accumulated by the answer choices sharing the row (MC: atomics onto zeros)
         alloc = torch.zeros if nmc > 1 else torch.empty
         dkvv = [alloc(B * S * 150, 2 * E, device=dev) for _ in layers]
-        dkvt = [torch.zeros(Bq * Lt, 2 * E, device=dev) if Lt else None for _ in layers]
+        fused_layers = [st.kv is not None for st in saves[S - 1]]
+        # question-row K/V gradients, accumulated over the steps: the fused block's first step (S - 1)
+        # stores them (dk2_store), so only the unfused path needs a zeroed buffer
+        dkvt = [(torch.empty if fused_layers[l] else torch.zeros)(Bq * Lt, 2 * E, device=dev) if Lt else None
+                for l in range(len(layers))]
         ds = ds.contiguous()
         grads = [_LayerGrads(S, Bq, dev) for _ in layers]
-        fused_layers = [st.kv is not None for st in saves[S - 1]]
         for i in reversed(range(S)):
             tsum, mu, ru = fused[i]
             du = K.dropout_bwd(ds, p, seed + 7 + 64 * 1000 * (i + 1)) if p > 0 else ds

@@ -103,6 +103,16 @@ class FusedAdamW(torch.optim.Optimizer):
         self._done.append(rng)
         self.early_updates += 1
 
+    def update_chunks(self, ranges, grad_scale=1.0):
+        """Update the chunk ranges [(c0, c1)] now, ahead of step() (whose remaining update then skips
+        them): the data-parallel split step runs this on the collective stream for the buckets whose
+        exchange has finished, beside the backward segments still replaying (lrce/graph.py)."""
+        self._begin()
+        for c0, c1 in ranges:
+            if c1 > c0 and (c0, c1) not in self._done:
+                self._update(c0, c1, grad_scale, last=False)
+                self._done.append((c0, c1))
+
     def _sync_lrs(self):
         key = tuple(g["lr"] for g in self.param_groups)
         if key == self._lr_cache:
