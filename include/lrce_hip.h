@@ -392,6 +392,8 @@ typedef struct LrceDecCaBwd {
   float* slab;
   uint32_t* counters;
   int32_t dk2_store;   /* 1: the text rows' dK / dV are STORED (the first recurrent step of the backward; no zeroed buffer needed), 0: added */
+  uint16_t* dk1_bf16;  /* non-NULL (one writer per video row, kv.bdiv1 == 1 only): the video rows' dK / dV go here as bf16, same
+                          dstride1 / dld1 / dv_off (the operand of the memory-side GEMMs), and dk1 may be NULL */
 } LrceDecCaBwd;
 int lrce_dec_ca_bwd(const LrceDecCaBwd* args, void* stream);
 /* Backward of the self-attention block from dx1 = d LN1(x1p): dx1p = LN1 backward, dsao = its out-

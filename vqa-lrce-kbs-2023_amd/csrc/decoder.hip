@@ -700,6 +700,7 @@ struct CaBwdP {
   int dkv1_atomic;                // rows shared by bdiv1 > 1 query rows: atomics, else stores
   float* dk2;                     // text dK, accumulated (one writer per row), or stored (dk2_store)
   int dk2_store;
+  bf16* dk1_16;                   // non-null: the video rows' dK / dV stored as bf16 here instead of dk1
   long long dstride2, dld2;
   long long dv_off;
   const f16* wq;                  // in_proj rows 0..E
@@ -874,6 +875,15 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_bwd_kernel(CaBwdP p) {
       for (int i = 0; i < 8; ++i) {
         kv8[i] = dsj * L.q[c * 8 + i];
         kv8[8 + i] = pj * L.dctx[c * 8 + i];
+      }
+      if (p.dk1_16) {   // bf16 directly: the memory-side GEMMs' operand (same rounding as a later cast)
+        bf16* d16 = p.dk1_16 + vbase + (long long)j * p.dld1 + c * 8;
+        bf16x8 k16, v16;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { k16[i] = f2bf(kv8[i]); v16[i] = f2bf(kv8[8 + i]); }
+        *reinterpret_cast<bf16x8*>(d16) = k16;
+        *reinterpret_cast<bf16x8*>(d16 + p.dv_off) = v16;
+        continue;
       }
       float* dst = p.dk1 + vbase + (long long)j * p.dld1 + c * 8;
       if (p.dkv1_atomic) {
@@ -1166,8 +1176,11 @@ extern "C" int lrce_dec_ca_fwd(const LrceDecCa* a, void* stream) {
 
 extern "C" int lrce_dec_ca_bwd(const LrceDecCaBwd* a, void* stream) {
   if (!a || !a->dx2 || !a->x2p || !a->mean2 || !a->rstd2 || !a->g2 || !a->dcao_out || !a->wo || !a->q || !a->ctx || !a->lse ||
-      !a->dq_out || !a->dk1 || !a->wq || !a->dx1_out || !a->slab || !a->counters)
+      !a->dq_out || (!a->dk1 && !a->dk1_bf16) || !a->wq || !a->dx1_out || !a->slab || !a->counters)
     return lrce_fail(LRCE_E_ARG, "dec_ca_bwd: null pointer");
+  if (a->dk1_bf16 && (a->kv.bdiv1 > 1 || (reinterpret_cast<uintptr_t>(a->dk1_bf16) & 15) || a->dstride1 % 8 ||
+                      a->dld1 % 8 || a->dv_off % 8))
+    return lrce_fail(LRCE_E_ARG, "dec_ca_bwd: bf16 dK/dV needs one writer per row (bdiv1 == 1) and 16-B aligned rows");
   if (a->B < 1 || a->B > LRCE_DEC_MAX_ROWS) return lrce_fail(LRCE_E_ARG, "dec_ca_bwd: B=%d", a->B);
   if (int rc = kv_check(a->kv, "dec_ca_bwd")) return rc;
   if (a->kv.lk2 > 0 && !a->dk2) return lrce_fail(LRCE_E_ARG, "dec_ca_bwd: text segment without dk2");
@@ -1177,7 +1190,7 @@ extern "C" int lrce_dec_ca_bwd(const LrceDecCaBwd* a, void* stream) {
   p.B = a->B; p.dx2 = a->dx2; p.x2p = a->x2p; p.mean2 = a->mean2; p.rstd2 = a->rstd2; p.g2 = a->g2;
   p.dcao_out = a->dcao_out; p.wo = reinterpret_cast<const f16*>(a->wo); p.kv = kv_conv(a->kv); p.q = a->q; p.ctx = a->ctx;
   p.lse = a->lse; p.dq_out = a->dq_out; p.dk1 = a->dk1; p.dstride1 = a->dstride1; p.dld1 = a->dld1;
-  p.dkv1_atomic = a->kv.bdiv1 > 1; p.dk2 = a->dk2; p.dk2_store = a->dk2_store; p.dstride2 = a->dstride2; p.dld2 = a->dld2; p.dv_off = a->dv_off;
+  p.dkv1_atomic = a->kv.bdiv1 > 1; p.dk2 = a->dk2; p.dk2_store = a->dk2_store; p.dk1_16 = reinterpret_cast<bf16*>(a->dk1_bf16); p.dstride2 = a->dstride2; p.dld2 = a->dld2; p.dv_off = a->dv_off;
   p.wq = reinterpret_cast<const f16*>(a->wq); p.dx1_out = a->dx1_out; p.p = a->drop_p; p.seed = a->seed;
   p.rng_off = lrce_rng_offset(); p.slab = a->slab; p.ctr = a->counters; p.trace = g_dec_trace_host;
   return launch(dec_ca_bwd_kernel, p, a->B, static_cast<hipStream_t>(stream), "dec_ca_bwd");

@@ -120,7 +120,7 @@ class DecCaBwd(ctypes.Structure):
         ("dq_out", ctypes.c_void_p), ("dk1", ctypes.c_void_p), ("dstride1", ctypes.c_int64), ("dld1", ctypes.c_int64),
         ("dk2", ctypes.c_void_p), ("dstride2", ctypes.c_int64), ("dld2", ctypes.c_int64), ("dv_off", ctypes.c_int64),
         ("wq", ctypes.c_void_p), ("dx1_out", ctypes.c_void_p),
-    ] + _WS + [("dk2_store", ctypes.c_int32)]
+    ] + _WS + [("dk2_store", ctypes.c_int32), ("dk1_bf16", ctypes.c_void_p)]
 
 
 class DecSaBwd(ctypes.Structure):

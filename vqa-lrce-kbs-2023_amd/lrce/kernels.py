@@ -539,11 +539,15 @@ def dec_ca_fwd(x1p, g1, b1, wq, bq, kv, wo, bo, *, x1_out, mean_out, rstd_out, q
 def dec_ca_bwd(dx2, x2p, mean2, rstd2, g2, wo, kv, q, ctx, lse, wq, *, dcao_out, dq_out, dk1, dstride1, dld1, dx1_out, p,
                seed, dk2=None, dstride2=0, dld2=0, dv_off, dk2_store=False):
     """dk2_store: the text rows' dK / dV are written, not added (the backward's first recurrent step:
-    the accumulation buffer needs no zeroing launch)."""
+    the accumulation buffer needs no zeroing launch).  A bf16 dk1 (one writer per video row): the
+    video rows' dK / dV are stored as bf16 directly (no f32 buffer + cast)."""
     a = N.DecCaBwd()
     a.B, a.dx2, a.x2p, a.mean2, a.rstd2, a.g2 = dx2.shape[0], ptr(dx2), ptr(x2p), ptr(mean2), ptr(rstd2), ptr(g2)
     a.dcao_out, a.wo, a.kv, a.q, a.ctx, a.lse = ptr(dcao_out), ptr(wo), kv, ptr(q), ptr(ctx), ptr(lse)
-    a.dq_out, a.dk1, a.dstride1, a.dld1 = ptr(dq_out), ptr(dk1), dstride1, dld1
+    if dk1.dtype == BF16:
+        a.dq_out, a.dk1, a.dk1_bf16, a.dstride1, a.dld1 = ptr(dq_out), None, ptr(dk1), dstride1, dld1
+    else:
+        a.dq_out, a.dk1, a.dstride1, a.dld1 = ptr(dq_out), ptr(dk1), dstride1, dld1
     a.dk2, a.dstride2, a.dld2, a.dv_off = ptr(dk2), dstride2, dld2, dv_off
     a.wq, a.dx1_out = ptr(wq), ptr(dx1_out)
     a.dk2_store = int(bool(dk2_store))

@@ -375,9 +375,13 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         dev = ds.device
         # video K/V gradients: written once per row by the step's attention backward (OE / Count), or
         # accumulated by the answer choices sharing the row (MC: atomics onto zeros)
-        alloc = torch.zeros if nmc > 1 else torch.empty
-        dkvv = [alloc(B * S * 150, 2 * E, device=dev) for _ in layers]
         fused_layers = [st.kv is not None for st in saves[S - 1]]
+        # ... and with one writer per row the fused block stores them as bf16 directly: the operand of
+        # the memory-side GEMMs below, no f32 buffer and cast (bit-identical: the same RNE rounding)
+        direct16 = [fused_layers[l] and nmc == 1 for l in range(len(layers))]
+        alloc = torch.zeros if nmc > 1 else torch.empty
+        dkvv = [torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev) if direct16[l] else
+                alloc(B * S * 150, 2 * E, device=dev) for l in range(len(layers))]
         # question-row K/V gradients, accumulated over the steps: the fused block's first step (S - 1)
         # stores them (dk2_store), so only the unfused path needs a zeroed buffer
         dkvt = [(torch.empty if fused_layers[l] else torch.zeros)(Bq * Lt, 2 * E, device=dev) if Lt else None
@@ -402,10 +406,12 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         dtt = torch.empty(Bq * Lt, E, device=dev) if Lt else None
         # the memory-side K/V gradients (accumulated in f32 over steps / answer choices) enter their
         # big-M GEMMs as bf16, like every other activation gradient
-        dk16 = [torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev) for _ in layers]
+        dk16 = [dkvv[l] if direct16[l] else torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev)
+                for l in range(len(layers))]
         dt16 = [torch.empty(Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None for _ in layers]
         for l in range(len(layers)):
-            K.cast_bf16(dkvv[l], dk16[l])
+            if not direct16[l]:
+                K.cast_bf16(dkvv[l], dk16[l])
             if Lt:
                 K.cast_bf16(dkvt[l], dt16[l])
         for l, lay in enumerate(layers):
