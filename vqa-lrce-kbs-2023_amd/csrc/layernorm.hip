@@ -341,32 +341,24 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ p
   if (dst) *dst += s;
 }
 
-// ln_bwd grid.  With a partials workspace: one row per wave while the whole grid fits on the chip
-// at once, else exactly one chip-full of blocks looping over the rows (a balanced grid-stride with
-// the next row prefetched): the wave count, not rows per wave, is what keeps enough loads in flight
-// (a fixed 8 rows per wave left the 17,640 x 512 stage-3 rows on 2 waves per SIMD at 4 TB/s).
-// Resident blocks per CU follow the register budget of the CH instantiation (one wave per SIMD
-// per block).  Without a workspace every block adds its dw/db into the SAME 2 x cols addresses, so
-// blocks are capped.
+// rows per wave of ln_bwd: small inputs (the decoder / BERT rows) one row per wave (latency-bound:
+// as many waves as rows); larger ones 4-8 with the next row prefetched.  (A chip-capacity grid —
+// one row per wave up to 2-8 resident blocks per CU — measured 5-25 % slower on the 15 680 x 512 and
+// 3 920 x 1024 shapes, 4 % faster on 62 720 rows: more blocks mean more dw / db partials to reduce;
+// tools/ln_bench.py, LRCE_LN_BWD_PERCU=k selects it for A/B.)  Without a partials workspace every
+// block adds its dw/db into the SAME 2 x cols addresses, so blocks are capped.
 int ln_bwd_blocks(int rows, int lpr, bool ws, int cols) {
   const int rpb = 4 * (64 / lpr);                 // rows per block per pass
-  const int nb1 = (rows + rpb - 1) / rpb;         // one row per wave
-  if (!ws) {
-    const int per_wave = rows <= 8192 ? 1 : 8;
-    const int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
-    return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+  static const int knob = getenv("LRCE_LN_BWD_PERCU") ? atoi(getenv("LRCE_LN_BWD_PERCU")) : 0;   // A/B knob
+  if (ws && knob > 0) {
+    const int nb1 = (rows + rpb - 1) / rpb;
+    const int cap = 256 * knob > 2048 ? 2048 : 256 * knob;   // ln_bwd_reduce: <= LN_RED_MAXY * LN_RED_ROWS partial rows
+    return nb1 < 1 ? 1 : (nb1 > cap ? cap : nb1);
   }
-  static const int knob = getenv("LRCE_LN_BWD_PERCU") ? atoi(getenv("LRCE_LN_BWD_PERCU")) : -1;   // A/B: 0 = fixed rows per wave
-  if (knob == 0) {
-    const int per_wave = rows <= 2048 ? 1 : rows <= 8192 ? 4 : 8;
-    const int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
-    return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
-  }
-  const int nch = cols / 4;
-  const int per_cu = knob > 0 ? knob : nch <= 64 ? 8 : nch <= 128 ? 6 : nch <= 256 ? 3 : 2;   // VGPRs: <=64, 80, 108-136, 240
-  int cap = 256 * per_cu;
-  if (cap > 2048) cap = 2048;                     // ln_bwd_reduce: <= LN_RED_MAXY * LN_RED_ROWS partial rows
-  return nb1 < 1 ? 1 : (nb1 > cap ? cap : nb1);
+  (void)cols;
+  const int per_wave = ws ? (rows <= 2048 ? 1 : rows <= 8192 ? 4 : 8) : (rows <= 8192 ? 1 : 8);
+  const int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
+  return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
 }
 int ln_bwd_lpr(int cols) { return cols / 4 <= 32 ? 32 : 64; }
 
