@@ -434,7 +434,7 @@ int lrce_dec_set_trace(uint64_t* buf);
 int lrce_wattn_set_trace(uint64_t* buf);
 
 /* Debug: phase timestamps of the LDS-DMA GEMM kernel into buf[workgroup * 8 + mark] (marks: start, first K tile
- * landed, K loop done, epilogue stores issued and drained; [6] HW_ID, [7] XCC_ID), workgroups of split 0 only;
+ * landed, K loop done, epilogue stores issued, stores drained; [6] HW_ID, [7] XCC_ID), workgroups of split 0 only;
  * NULL turns it off (the default).  Recorded only by a library built with -DLRCE_GEMM_TRACE
  * (tools/gemm_trace.py). */
 int lrce_gemm_set_trace(uint64_t* buf);

@@ -19,7 +19,7 @@ from lrce import _native as N  # noqa: E402
 from lrce import kernels as K  # noqa: E402
 import gemm_bench as GB  # noqa: E402
 
-MARKS = ["start", "tile 0 in", "K loop", "stored"]
+MARKS = ["start", "tile 0 in", "K loop", "issued", "drained"]
 
 
 def trace(idx):
@@ -57,14 +57,14 @@ def trace(idx):
     tr = buf.view(nmax, 8)
     nwg = int((tr[:, 0] != 0).sum().item())
     tr = tr[:nwg]
-    t = tr[:, :4].double().cpu() / 100.0
+    t = tr[:, :5].double().cpu() / 100.0
     t0 = t[:, 0]
-    span = (t[:, 3].max() - t0.min()).item()
+    span = (t[:, 4].max() - t0.min()).item()
     print(f"== {M}x{Nn}x{Kk} {lay} {epi}: {nwg} workgroups, launch span {span:.1f} us")
-    st, en = t0.sort().values, t[:, 3].sort().values
+    st, en = t0.sort().values, t[:, 4].sort().values
     alive = torch.arange(1, nwg + 1, dtype=torch.float64) - torch.searchsorted(en, st, right=True).double()
     print(f"resident workgroups at a start: median {alive.median().item():.0f}  max {alive.max().item():.0f}")
-    life = t[:, 3] - t0
+    life = t[:, 4] - t0
     print(f"workgroup lifetime: median {life.median().item():.2f}  p90 {life.quantile(0.9).item():.2f} us")
     rel_start = t0 - t0.min()
     print(f"workgroup starts: p10 {rel_start.quantile(0.1).item():.1f}  median {rel_start.median().item():.1f}  "

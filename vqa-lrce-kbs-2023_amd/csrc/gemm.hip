@@ -857,10 +857,11 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       epilogue8<F16>(p, v, m, ncol + 8 * h, sk, cbase, dg, rs);
     }
   });
+  GT_MARK(3);   // epilogue math done, stores issued
 #ifdef LRCE_GEMM_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stores have left this wave
 #endif
-  GT_MARK(3);
+  GT_MARK(4);
 }
 
 // C[m][n] += sum_s ws[s][m][n]  (n % 4 == 0, ldc % 4 == 0)
