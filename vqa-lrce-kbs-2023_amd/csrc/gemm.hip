@@ -211,22 +211,36 @@ __device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row
 // 16-bit format is a template parameter and every optional factor sits behind a wave-uniform branch
 // (alpha, the q-scale columns — host guarantees scale_cols % 8 == 0 on the vector path — and the row
 // scale), so a plain epilogue is a conversion and a 16-B store per 8 outputs.
+// Epilogue operands loaded ahead of the epilogue's first store (gemm_glds_kernel): vmcnt counts loads
+// and stores in one in-order counter, so a load issued after a store can only be waited for together
+// with that store — per 8-column chunk that was a full store round trip (6.7-13 us of epilogue per
+// workgroup in tools/gemm_trace.py).  `have` = 0: epilogue8 loads them itself (the legacy kernel).
+struct EpiPf {
+  int have;
+  float al;              // alpha_of(p)
+  long long row;         // c_map-resolved output row (-1: none)
+  float rs;              // row scale (1 if none)
+  const float4* bias;    // 2 float4 of bias for this chunk, or null
+};
+
 template <bool F16>
 __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int n, int sk, char* cbase,
-                                          const bf16x8* dg_pf = nullptr, const float4* rs_pf = nullptr) {
+                                          const bf16x8* dg_pf = nullptr, const float4* rs_pf = nullptr,
+                                          const EpiPf* pf = nullptr, const float4* acc_pf = nullptr) {
   if (m >= p.m || n >= p.n) return;
   const int fl = p.flags;
-  const long long row = p.c_map ? (long long)p.c_map[m] : (long long)m;
+  const long long row = pf ? pf->row : (p.c_map ? (long long)p.c_map[m] : (long long)m);
   if (row < 0) return;   // c_map -1: a padded window position (no output row)
   const bool first = sk == 0;
   if (p.vec && n + 8 <= p.n) {
-    const float al = alpha_of(p);
+    const float al = pf ? pf->al : alpha_of(p);
     if (al != 1.f) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= al;
     }
     if ((fl & LRCE_EPI_BIAS) && first) {
-      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n), b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+      const float4 b0 = pf ? pf->bias[0] : *reinterpret_cast<const float4*>(p.bias + n);
+      const float4 b1 = pf ? pf->bias[1] : *reinterpret_cast<const float4*>(p.bias + n + 4);
       v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
     }
     if (n < p.scale_cols) {
@@ -249,7 +263,7 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
       for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(from16<F16>(pre[e]));
     }
     if (p.row_scale) {
-      const float rs = p.row_scale[m / p.rows_per_scale];
+      const float rs = pf ? pf->rs : p.row_scale[m / p.rows_per_scale];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= rs;
     }
@@ -267,7 +281,7 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
       float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(cbase) + row * p.ldc + n);
       float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
       if (fl & LRCE_EPI_ACCUM) {
-        const float4 c0 = cp[0], c1 = cp[1];
+        const float4 c0 = acc_pf ? acc_pf[0] : cp[0], c1 = acc_pf ? acc_pf[1] : cp[1];
         o0.x += c0.x; o0.y += c0.y; o0.z += c0.z; o0.w += c0.w; o1.x += c1.x; o1.y += c1.y; o1.z += c1.z; o1.w += c1.w;
       }
       cp[0] = o0; cp[1] = o1;
@@ -842,20 +856,82 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     });
     return;
   }
-  static_for<IM>([&](auto ic) {
-    uint32_t u[JN][4];
-    transpose(ic, u);
-    const int m = m0 + wm * WM + decltype(ic)::value * 16 + (lane & 15);
+  // every global operand of the epilogue is loaded here, before its first store (EpiPf)
+  const float al_pf = alpha_of(p);
+  float4 bias_pf[NH][2];
+  const bool have_bias = (p.flags & LRCE_EPI_BIAS) && sk == 0 && p.vec;
 #pragma unroll
-    for (int h = 0; h < JN / 2; ++h) {
-      float v[8];
+  for (int h = 0; h < NH; ++h) {
+    const int n = ncol + 8 * h;
+    const bool ok = have_bias && n + 8 <= p.n;
+    bias_pf[h][0] = ok ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bias_pf[h][1] = ok ? *reinterpret_cast<const float4*>(p.bias + n + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  long long row_pf[IM];
+  float rsc_pf[IM];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(u[2 * h + (e >> 2)][e & 3]);
-      constexpr int i = decltype(ic)::value;
-      const bf16x8* dg = (pf_dg && i < pf_dg_slots(IM)) ? &dgp[i < pf_dg_slots(IM) ? i : 0][h] : nullptr;
-      const float4* rs = (pf_rs && i < pf_rs_slots(IM)) ? rsp[i < pf_rs_slots(IM) ? i : 0][h] : nullptr;
-      epilogue8<F16>(p, v, m, ncol + 8 * h, sk, cbase, dg, rs);
+  for (int i = 0; i < IM; ++i) {
+    const int m = m0 + wm * WM + i * 16 + (lane & 15);
+    row_pf[i] = m < p.m ? (p.c_map ? (long long)p.c_map[m] : (long long)m) : -1;
+    rsc_pf[i] = (p.row_scale && m < p.m) ? p.row_scale[m / p.rows_per_scale] : 1.f;
+  }
+  // the dGELU pre-activation of a deeper K (not prefetched before the K loop): all of it now
+  const bool late_dg = (p.flags & LRCE_EPI_DGELU) && p.vec && !pf_dg && !p.ws && !(p.flags & LRCE_EPI_ATOMIC);
+  if (late_dg) {
+#pragma unroll
+    for (int i = 0; i < pf_dg_slots(IM); ++i)
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const int n = ncol + 8 * h;
+        const bool ok = row_pf[i] >= 0 && n + 8 <= p.n;
+        dgp[i][h] = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(p.aux) + (ok ? row_pf[i] * p.ld_aux + n : 0));
+      }
+  }
+  // the f32 residual / accumulated C (read-modify-write) of RC row blocks at a time: one memory round
+  // trip per RC row blocks behind the stores already issued, instead of one per 8-column chunk
+  constexpr int RC = IM >= 5 ? 1 : 2;
+  const bool late_rs = (p.flags & LRCE_EPI_RESID) && sk == 0 && p.vec && !pf_rs && !p.ws && !(p.flags & LRCE_EPI_ATOMIC);
+  const bool late_acc = (p.flags & LRCE_EPI_ACCUM) && !(p.flags & LRCE_EPI_RESID) && p.vec && !p.ws &&
+                        !(p.flags & LRCE_EPI_ATOMIC);
+  static_for<(IM + RC - 1) / RC>([&](auto cc) {
+    constexpr int c0 = decltype(cc)::value * RC;
+    float4 xq[RC][NH][2];
+    if (late_rs || late_acc) {
+#pragma unroll
+      for (int ii = 0; ii < RC; ++ii) {
+        if (c0 + ii >= IM) break;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          const int n = ncol + 8 * h;
+          const long long rw = row_pf[c0 + ii < IM ? c0 + ii : 0];
+          const bool ok = rw >= 0 && n + 8 <= p.n;
+          const float* src = late_rs ? static_cast<const float*>(p.aux) + (ok ? rw * p.ld_aux + n : 0)
+                                     : reinterpret_cast<const float*>(cbase) + (ok ? rw * p.ldc + n : 0);
+          xq[ii][h][0] = *reinterpret_cast<const float4*>(src);
+          xq[ii][h][1] = *reinterpret_cast<const float4*>(src + 4);
+        }
+      }
     }
+    static_for<RC>([&](auto iic) {
+      constexpr int i = c0 + decltype(iic)::value;
+      if constexpr (i < IM) {
+        uint32_t u[JN][4];
+        transpose(std::integral_constant<int, i>{}, u);
+        const int m = m0 + wm * WM + i * 16 + (lane & 15);
+#pragma unroll
+        for (int h = 0; h < JN / 2; ++h) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(u[2 * h + (e >> 2)][e & 3]);
+          const bf16x8* dg = ((pf_dg || late_dg) && i < pf_dg_slots(IM)) ? &dgp[i < pf_dg_slots(IM) ? i : 0][h] : nullptr;
+          const float4* rs = (pf_rs && i < pf_rs_slots(IM)) ? rsp[i < pf_rs_slots(IM) ? i : 0][h]
+                             : late_rs ? xq[decltype(iic)::value][h] : nullptr;
+          const float4* ac = late_acc ? xq[decltype(iic)::value][h] : nullptr;
+          const EpiPf pf{1, al_pf, row_pf[i], rsc_pf[i], have_bias ? bias_pf[h] : nullptr};
+          epilogue8<F16>(p, v, m, ncol + 8 * h, sk, cbase, dg, rs, &pf, ac);
+        }
+      }
+    });
   });
   GT_MARK(3);   // epilogue math done, stores issued
 #ifdef LRCE_GEMM_TRACE
