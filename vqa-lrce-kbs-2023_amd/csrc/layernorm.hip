@@ -355,7 +355,14 @@ int ln_bwd_blocks(int rows, int lpr, bool ws, int cols) {
     const int cap = 256 * knob > 2048 ? 2048 : 256 * knob;   // ln_bwd_reduce: <= LN_RED_MAXY * LN_RED_ROWS partial rows
     return nb1 < 1 ? 1 : (nb1 > cap ? cap : nb1);
   }
-  (void)cols;
+  // measured per row width (tools/ln_bench.py sweep, round 4): rows of <= 512 columns stream best
+  // on a capped chip-wide grid — 1024 blocks at <= 256 columns, 768 at 512 (250 880 x 128: 116.5 ->
+  // 112.6 us, 62 720 x 512: 123 -> 108 us) — wider rows with 4-8 rows per wave
+  const int nch = cols / 4;
+  if (ws && rows > 8192 && nch <= 128 && knob == 0) {   // (knob -1: 4-8 rows per wave everywhere, for A/B)
+    const int nb1 = (rows + rpb - 1) / rpb, cap = nch <= 64 ? 1024 : 768;
+    return nb1 > cap ? cap : nb1;
+  }
   const int per_wave = ws ? (rows <= 2048 ? 1 : rows <= 8192 ? 4 : 8) : (rows <= 8192 ? 1 : 8);
   const int nb = (rows + rpb * per_wave - 1) / (rpb * per_wave);
   return nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);

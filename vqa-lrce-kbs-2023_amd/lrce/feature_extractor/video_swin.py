@@ -16,6 +16,7 @@ execution:
   straight into the flat parameter store (lrce/flat.py).
 """
 import math
+import os
 from functools import lru_cache
 
 import torch
@@ -266,6 +267,11 @@ class _PatchEmbedFn(torch.autograd.Function):
         return (None,) * (5 + len(list(pe.parameters())))
 
 
+# LayerNorm-backward input gradients of rows this wide or wider stay f32 (the LN backward's bf16 loads
+# measured slower there, tools/ln_bench.py); LRCE_LN_F32_WIDE overrides (A/B)
+_LN_F32_WIDE = int(os.environ.get("LRCE_LN_F32_WIDE", "1024"))
+
+
 def _drop_path_scale(rate, nc, device, training):
     """timm DropPath (video_swin_ori.py:243,299): per-sample keep mask / keep_prob, here per clip."""
     if not training or rate <= 0.0:
@@ -416,8 +422,9 @@ class _SwinBlockFn(torch.autograd.Function):
         del g, pre, dout16
         _wgrad(flat, blk.mlp.fc1, dpre, h2)
         # the LayerNorms' input gradients arrive as bf16 GEMM outputs (as under the reference's
-        # autocast, where a bf16 linear's grad_input is bf16): half the bytes of the LN backward's dy
-        dh2 = K.linear_dx(dpre, flat.w16(blk.mlp.fc1.weight), out_f32=False)
+        # autocast, where a bf16 linear's grad_input is bf16): half the bytes of the LN backward's dy;
+        # rows of >= 1024 columns keep f32 (the LN backward's bf16 loads measured slower there)
+        dh2 = K.linear_dx(dpre, flat.w16(blk.mlp.fc1.weight), out_f32=C >= _LN_F32_WIDE)
         del dpre, h2
         dx_mid = torch.empty_like(x_mid)
         # attention branch input gradient s1 * dx_mid, as bf16 in window order (rows of o / qkv)
@@ -440,7 +447,7 @@ class _SwinBlockFn(torch.autograd.Function):
             K.wattn_dbias(dbp, geo.n_win, nH, geo.ws, _bin_rows(at, geo.ws), gt)
         del dbp
         _wgrad(flat, at.qkv, dqkv, xw)
-        dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight), out_f32=False)
+        dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight), out_f32=C >= _LN_F32_WIDE)
         del dqkv, qkv, xw
         dx = torch.empty_like(x)
         up = ctx.up
@@ -490,7 +497,7 @@ class _PatchMergeFn(torch.autograd.Function):
         gw = _g(flat, pm.reduction.weight)
         if gw is not None:
             K.linear_dw(dy16, xl, gw)
-        dxl = K.linear_dx(dy16, flat.w16(pm.reduction.weight), out_f32=False)
+        dxl = K.linear_dx(dy16, flat.w16(pm.reduction.weight), out_f32=4 * pm.dim >= _LN_F32_WIDE)
         dx = torch.empty_like(x)
         K.layernorm_bwd(dxl, x, mean, rstd, pm.norm.weight, dx, in_map=geo.merge_map, nseg=4, rows=geo.M_merged,
                         cols=4 * pm.dim, dw=_g(flat, pm.norm.weight), db=_g(flat, pm.norm.bias))
