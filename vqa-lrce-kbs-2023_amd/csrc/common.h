@@ -62,17 +62,26 @@ __device__ __forceinline__ f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
 // five FMAs — libm erff is a two-range polynomial with branches and dominated the GELU-epilogue GEMMs.
 // The tail is evaluated as 0.5 * erfc(|z|) directly (no 1 - erf cancellation); the derivative reuses
 // exp(-x^2/2) as the normal pdf.  Max abs error vs the exact form: 6e-7 (value), 2.5e-7 (derivative).
+// z = |x|/sqrt2 and the 1/2 are folded into the constants (t = 1 / (1 + 0.3275911 z), the polynomial
+// coefficients halved, exp(-z^2) = exp2(x^2 * -log2(e)/2)), and every step is an explicit fma / mul,
+// so the scalar form and the packed pair form below (v_pk_fma_f32 / v_pk_mul_f32: half the VALU
+// issue of the polynomial in the GEMM epilogues, which the GELU math dominates) give identical bits.
+constexpr float GELU_T = 0.23164189f;          // 0.3275911 / sqrt(2)
+constexpr float GELU_E = -0.72134752044448170f; // -log2(e) / 2
+constexpr float GELU_B1 = 0.127414796f, GELU_B2 = -0.142248368f, GELU_B3 = 0.7107068705f, GELU_B4 = -0.7265760135f,
+                GELU_B5 = 0.5307027145f;        // A&S 7.1.26 a1..a5, halved
+constexpr float GELU_PDF = 0.39894228040143268f;   // 1 / sqrt(2 pi)
 __device__ __forceinline__ float gelu_q(float x, float* e_out) {
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float e = __builtin_amdgcn_exp2f(-(z * z) * 1.4426950408889634f);
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(fabsf(x), GELU_T, 1.0f));
+  const float e = __builtin_amdgcn_exp2f((x * x) * GELU_E);
   *e_out = e;
-  const float q = 0.5f * p * t * e;  // 0.5 erfc(|x|/sqrt2)
-  return x >= 0.f ? 1.0f - q : q;    // Phi(x)
+  float p = __builtin_fmaf(GELU_B5, t, GELU_B4);
+  p = __builtin_fmaf(p, t, GELU_B3);
+  p = __builtin_fmaf(p, t, GELU_B2);
+  p = __builtin_fmaf(p, t, GELU_B1);
+  const float pt = p * t;
+  const float hi = __builtin_fmaf(-pt, e, 1.0f), lo = pt * e;   // 1 - q, q = 0.5 erfc(|x|/sqrt2)
+  return x >= 0.f ? hi : lo;                                    // Phi(x)
 }
 __device__ __forceinline__ float gelu_f(float x) {
   float e;
@@ -81,7 +90,38 @@ __device__ __forceinline__ float gelu_f(float x) {
 __device__ __forceinline__ float gelu_grad_f(float x) {
   float e;
   const float phi = gelu_q(x, &e);
-  return phi + x * 0.39894228040143268f * e;
+  return __builtin_fmaf(x * GELU_PDF, e, phi);
+}
+// the same on a pair (ext vector: the compiler issues the packed FP32 forms)
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2v gelu_q2(f32x2v x, f32x2v& e) {
+  const f32x2v ax = __builtin_elementwise_abs(x);
+  const f32x2v d = __builtin_elementwise_fma(ax, (f32x2v)(GELU_T), (f32x2v)(1.0f));
+  f32x2v t;
+  t.x = __builtin_amdgcn_rcpf(d.x);
+  t.y = __builtin_amdgcn_rcpf(d.y);
+  const f32x2v ee = (x * x) * (f32x2v)(GELU_E);
+  e.x = __builtin_amdgcn_exp2f(ee.x);
+  e.y = __builtin_amdgcn_exp2f(ee.y);
+  f32x2v p = __builtin_elementwise_fma((f32x2v)(GELU_B5), t, (f32x2v)(GELU_B4));
+  p = __builtin_elementwise_fma(p, t, (f32x2v)(GELU_B3));
+  p = __builtin_elementwise_fma(p, t, (f32x2v)(GELU_B2));
+  p = __builtin_elementwise_fma(p, t, (f32x2v)(GELU_B1));
+  const f32x2v pt = p * t;
+  const f32x2v hi = __builtin_elementwise_fma(-pt, e, (f32x2v)(1.0f)), lo = pt * e;
+  f32x2v phi;
+  phi.x = x.x >= 0.f ? hi.x : lo.x;
+  phi.y = x.y >= 0.f ? hi.y : lo.y;
+  return phi;
+}
+__device__ __forceinline__ f32x2v gelu2(f32x2v x) {
+  f32x2v e;
+  return x * gelu_q2(x, e);
+}
+__device__ __forceinline__ f32x2v gelu_grad2(f32x2v x) {
+  f32x2v e;
+  const f32x2v phi = gelu_q2(x, e);
+  return __builtin_elementwise_fma(x * (f32x2v)(GELU_PDF), e, phi);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

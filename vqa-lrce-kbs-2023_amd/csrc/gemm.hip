@@ -255,12 +255,20 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
         *reinterpret_cast<bf16x8*>(p.aux_out + row * p.ld_aux_out + n) = pre;
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2v g = gelu2(f32x2v{v[e], v[e + 1]});
+        v[e] = g.x;
+        v[e + 1] = g.y;
+      }
     }
     if (fl & LRCE_EPI_DGELU) {
       const bf16x8 pre = dg_pf ? *dg_pf : *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(p.aux) + row * p.ld_aux + n);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(from16<F16>(pre[e]));
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2v g = gelu_grad2(f32x2v{from16<F16>(pre[e]), from16<F16>(pre[e + 1])});
+        v[e] *= g.x;
+        v[e + 1] *= g.y;
+      }
     }
     if (p.row_scale) {
       const float rs = pf ? pf->rs : p.row_scale[m / p.rows_per_scale];
