@@ -704,7 +704,8 @@ def adamw_step(p, g, m, v, chunk_tensor, tensor_lr, sumsq, p_bf16, n_chunks, bet
                bc1, bc2, step=None, sumsq_next=None, p_f16=None, f16_range=(0, 0), g_bf16=None, tensor_chunk_off=None,
                chunk_sq=None, n_tensors=None):
     """step: optional f32 device scalar holding t (bias corrections computed on device: graph-safe).
-    sumsq_next: optional zeroed [n_tensors] buffer receiving ||p_t||^2 of the updated parameters."""
+    sumsq_next: optional [n_tensors] buffer receiving ||p_t||^2 of the updated parameters (zeroed first
+    only without chunk_sq / tensor_chunk_off: the per-chunk path stores every entry)."""
     call("lrce_adamw_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(chunk_tensor), ptr(tensor_lr), ptr(sumsq), ptr(p_bf16),
          n_chunks, beta1, beta2, eps, wd, grad_scale, reg, bc1, bc2, ptr(step), ptr(sumsq_next), ptr(p_f16),
          int(f16_range[0]), int(f16_range[1]), ptr(g_bf16), ptr(tensor_chunk_off), ptr(chunk_sq),

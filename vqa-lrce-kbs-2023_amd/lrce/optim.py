@@ -70,7 +70,8 @@ class FusedAdamW(torch.optim.Optimizer):
             # parameters changed outside the optimizer (init / load): one norm pass; afterwards the
             # update kernel itself produces the next step's norms
             self._norms()
-        self.sumsq_next.zero_()
+        # (sumsq_next needs no clearing: the step's last launch writes every tensor's sum of its chunk
+        # sums, segsum_kernel, in a fixed order)
         self._begun = True
 
     def _update(self, c0, c1, grad_scale, last):
