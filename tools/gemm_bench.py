@@ -51,6 +51,11 @@ SHAPES = [
     (4500, 768, 1536, "dx", ""),
     (4500, 1536, 768, "fwd", "bias"),
     (1536, 768, 4500, "dw", ""),
+    (512, 1024, 17640, "dw", ""),     # stage-2 -> 3 patch-merge reduction weight gradient
+    (1024, 2048, 4410, "dw", ""),     # stage-3 -> 4 patch-merge reduction
+    (768, 256, 70560, "dw", ""),      # stage-2 qkv
+    (1024, 256, 70560, "dw", ""),     # stage-2 fc1
+    (768, 768, 330, "dw", ""),
 ]
 
 

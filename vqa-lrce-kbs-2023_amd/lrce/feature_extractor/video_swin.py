@@ -345,34 +345,70 @@ class _Handoff:
         return dx16
 
 
-def _run_blocks(blocks, x, geo, flat, scales):
-    """The blocks of one stage in order; scales [(dp1, dp2)] per block (None entries in eval)."""
+def _run_blocks(blocks, x, geo, flat, scales, tiles=None):
+    """The blocks of one stage in order; scales [(dp1, dp2)] per block (None entries in eval);
+    tiles: per block the (forward, backward) bias tiles built ahead (_prebuild_bias_tiles) or None."""
     links = [None] + [_Handoff(scales[j - 1][1]) if _HANDOFF else None for j in range(1, len(blocks))]
     for j, blk in enumerate(blocks):
         dp1, dp2 = scales[j]
         x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, links[j], links[j + 1] if j + 1 < len(blocks) else None,
-                               *blk.parameters())
+                               tiles[j] if tiles is not None else None, *blk.parameters())
     return x
+
+
+def _bias_tiles(blk, geo):
+    """The block's relative-position bias expanded to per-(mask pattern, head) score tiles
+    (video_swin_ori.py:171-174 gather + the shifted-window mask), forward and backward forms: fp16
+    for the fused head-pair kernels, f32 for odd head counts."""
+    nH = blk.num_heads
+    shifted = geo.shifted and any(s > 0 for s in blk.shift_size)
+    region, n_pat = (geo.region, geo.n_pat) if shifted else (None, 1)
+    dt = torch.float16 if nH % 2 == 0 else torch.float32
+    dev = blk.attn.relative_position_bias_table.device
+    bias_f = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev, dtype=dt)
+    bias_b = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev, dtype=dt)
+    K.wattn_bias_build(blk.attn.relative_position_bias_table, blk.attn.relative_position_index, geo.n, nH, region,
+                       n_pat, bias_f, bias_b)
+    return bias_f, bias_b
+
+
+_PREBUILD_BIAS = os.environ.get("LRCE_SWIN_BIAS_PREBUILD", "1") != "0"   # A/B knob
+
+
+def _prebuild_bias_tiles(stages, dev):
+    """Every block's bias tiles for the whole forward, built in stage order on an aux stream (they
+    depend only on the parameters, which the stream sees after waiting on the current one): the 24
+    small build launches leave the forward's critical path and overlap the patch embedding / earlier
+    stages.  stages: [(blocks, geo)]; returns per stage (tiles per block, event the stage waits on)."""
+    main = torch.cuda.current_stream(dev)
+    s = aux_stream(dev, "swin_bias")
+    s.wait_stream(main)
+    out = []
+    with torch.cuda.stream(s):
+        for blocks, geo in stages:
+            tiles = [_bias_tiles(blk, geo) for blk in blocks]
+            ev = torch.cuda.Event()
+            ev.record(s)
+            out.append((tiles, ev))
+    return out
 
 
 class _SwinBlockFn(torch.autograd.Function):
     """One SwinTransformerBlock3D (video_swin_ori.py:248-306) forward / backward."""
 
     @staticmethod
-    def forward(ctx, x, blk, geo, flat, dp1, dp2, up, down, *params):
+    def forward(ctx, x, blk, geo, flat, dp1, dp2, up, down, tiles, *params):
         """up: the _Handoff this block's backward fills for the block before it; down: the one the
-        block after it fills for this block (either None)."""
+        block after it fills for this block (either None); tiles: prebuilt (forward, backward) bias
+        tiles or None (built here)."""
         C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
         at = blk.attn
         shifted = geo.shifted and any(s > 0 for s in blk.shift_size)
         wmap = geo.win2sp_shift if shifted else geo.win2sp
-        region, win_pat, n_pat = (geo.region, geo.win_pat, geo.n_pat) if shifted else (None, None, 1)
+        win_pat = geo.win_pat if shifted else None
         dev = x.device
         fused = nH % 2 == 0
-        bias_f = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev, dtype=torch.float16 if fused else torch.float32)
-        bias_b = torch.empty(K.wattn_bias_elems(n_pat, nH), device=dev, dtype=torch.float16 if fused else torch.float32)
-        K.wattn_bias_build(at.relative_position_bias_table, at.relative_position_index, n, nH, region, n_pat,
-                           bias_f, bias_b)
+        bias_f, bias_b = tiles if tiles is not None else _bias_tiles(blk, geo)
         Mw = geo.M_win   # window-order rows (incl. the padded positions of a partial window)
         xw, m1, r1 = K.layernorm(x, blk.norm1.weight, blk.norm1.bias, 1e-5, in_map=wmap, rows=Mw)
         c = (C // nH) ** -0.5 * LOG2E
@@ -472,7 +508,7 @@ class _SwinBlockFn(torch.autograd.Function):
             s.wait_stream(main)
             with torch.cuda.stream(s):
                 flat.group_done(group)
-        return (dx, None, None, None, None, None, None, None) + (None,) * len(ctx.needs_input_grad[8:])
+        return (dx, None, None, None, None, None, None, None, None) + (None,) * len(ctx.needs_input_grad[9:])
 
 
 class _PatchMergeFn(torch.autograd.Function):
@@ -567,16 +603,27 @@ class SwinTransformer3D(nn.Module):
             nc = B
         D, H, W = (T + 1) // 2, H // 4, W // 4
         scales = _drop_path_scales(self, nc, dev)
+        geos, (h, w) = [], (H, W)
+        for layer in self.layers:
+            geos.append(stage_geometry(nc, D, h, w, self.window_size, dev))
+            if layer.downsample is not None:
+                h, w = (h + 1) // 2, (w + 1) // 2
+        pre = (_prebuild_bias_tiles([(list(layer.blocks), g) for layer, g in zip(self.layers, geos)], dev)
+               if _PREBUILD_BIAS and dev.type == "cuda" else None)
         bi = 0
         for li, layer in enumerate(self.layers):
             if li == self.split_at and torch.is_grad_enabled() and x.requires_grad:
                 x_leaf = x.detach().requires_grad_(True)
                 self._split_mid = (x, x_leaf)
                 x = x_leaf
-            geo = stage_geometry(nc, D, H, W, self.window_size, dev)
+            geo = geos[li]
             nb = len(layer.blocks)
+            tiles = None
+            if pre is not None:
+                tiles, ev = pre[li]
+                torch.cuda.current_stream(dev).wait_event(ev)
             x = _run_blocks(list(layer.blocks), x, geo, flat,
-                            scales[bi:bi + nb] if scales is not None else [(None, None)] * nb)
+                            scales[bi:bi + nb] if scales is not None else [(None, None)] * nb, tiles)
             bi += nb
             if layer.downsample is not None:
                 x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())
