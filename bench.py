@@ -106,6 +106,8 @@ def train_step(model, opt, reducer, batch):
     out = model(clips, ids, mask, types)
     loss = F.cross_entropy(out, labels, ignore_index=-100)
     loss.backward()
+    if getattr(model, "split_backward", False):   # (set by make_step's graph modes) the extractors' part
+        model.backward_extractors()
     scale = reducer.finish() if reducer is not None else 1.0
     opt.step(grad_scale=scale)
     opt.zero_grad()
