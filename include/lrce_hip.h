@@ -107,6 +107,10 @@ typedef struct LrceGemmDesc {
   /* Non-NULL: alpha is read from this device float instead of `alpha` (the inverse of a gradient
    * scale lrce_grad_scale computed on the GPU).  LDS-DMA and register-staged bf16/fp16 paths. */
   const float* alpha_dev;
+  /* Batch stride of `bias` in elements (batch > 1; 0 = the same bias for every batch): BERT's query /
+   * key / value linears as one batched launch over their weights and biases in the flat parameter
+   * buffers (text.py:11-17 -> HF BertSelfAttention). */
+  int64_t stride_bias;
 } LrceGemmDesc;
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);

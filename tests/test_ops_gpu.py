@@ -122,6 +122,26 @@ def test_gemm_f16_forward(M, N, Kd):
         k.linear(A, B.to(torch.bfloat16), bias)      # mixed encodings are rejected
 
 
+@pytest.mark.parametrize("bf", [False, True])
+def test_gemm_batched_bias_stride(bf):
+    """batch > 1 with a per-batch bias (stride_bias): BERT's query / key / value linears as one launch
+    over weights and biases at one stride in the flat buffers (text.py _qkv); fp16 and bf16 forms."""
+    k = K()
+    h = torch.bfloat16 if bf else torch.float16
+    M, N, Kd, gap = 320, 768, 768, 1024
+    stride = N * Kd + gap
+    wbuf = (torch.randn(3 * stride, device=dev) / math.sqrt(Kd)).to(h)
+    bbuf = torch.randn(3 * stride, device=dev)
+    A = torch.randn(M, Kd, device=dev).to(h)
+    out = torch.empty(3, M, N, device=dev, dtype=h)
+    k.gemm(A, wbuf, out, M, N, Kd, flags=k.N.EPI_BIAS, bias=bbuf, batch=3, stride_b=stride, stride_c=M * N,
+           stride_bias=stride, f16=not bf)
+    for i in range(3):
+        W = wbuf[i * stride:i * stride + N * Kd].view(N, Kd)
+        ref = A.double() @ W.double().t() + bbuf[i * stride:i * stride + N].double()
+        assert rel(out[i], ref.float()) < (8e-3 if bf else 1e-3), i
+
+
 def test_f16_casts():
     k = K()
     x = torch.randn(1000, 768, device=dev) * 3

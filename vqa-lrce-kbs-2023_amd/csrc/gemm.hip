@@ -30,6 +30,7 @@ struct GemmP {
   const bf16* b;
   void* c;
   long long lda, ldb, ldc, sa, sb, sc;
+  long long sbias;   // batch stride of the bias (elements; 0: one bias for every batch)
   int m, n, k, batch, split_k, k_chunk;
   int flags;
   const float* bias;
@@ -325,6 +326,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
   const int tiles = p.tiles_m * p.tiles_n;
   const int z = blockIdx.y;  // batch * split
   const int bz = z / p.split_k, sk = z % p.split_k;
+  p.bias += (long long)bz * p.sbias;
   const int lin = xcd_remap(blockIdx.x, tiles);
   int tm, tn;
   tile_of(p, lin, tm, tn);
@@ -575,6 +577,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   const int tiles = p.tiles_m * p.tiles_n;
   const int z = blockIdx.y;
   const int bz = z / p.split_k, sk = z % p.split_k;
+  p.bias += (long long)bz * p.sbias;
   const int lin = xcd_remap(blockIdx.x, tiles);
   int tm, tn;
   tile_of(p, lin, tm, tn);
@@ -1073,6 +1076,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   p.k_chunk = chunk;
   p.flags = d->flags;
   p.bias = d->bias; p.aux = d->aux; p.ld_aux = d->ld_aux;
+  p.sbias = d->batch > 1 ? d->stride_bias : 0;
   p.aux_out = static_cast<bf16*>(d->aux_out); p.ld_aux_out = d->ld_aux_out;
   p.a_map = d->a_map; p.c_map = d->c_map;
   p.alpha = d->alpha; p.alpha_dev = d->alpha_dev; p.scale_cols = d->scale_cols; p.scale_val = d->scale_val;
@@ -1088,7 +1092,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   const bool out32 = d->flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM);
   p.vec = (d->n % 8 == 0) && (d->ldc % 8 == 0) && al16(d->c) && (d->stride_c % 8 == 0) && (d->scale_cols % 8 == 0) &&
-          (!d->bias || al16(d->bias)) && (!d->aux || (al16(d->aux) && d->ld_aux % 8 == 0)) &&
+          (!d->bias || (al16(d->bias) && p.sbias % 4 == 0)) && (!d->aux || (al16(d->aux) && d->ld_aux % 8 == 0)) &&
           (!d->aux_out || (al16(d->aux_out) && d->ld_aux_out % 8 == 0));
   (void)out32;
   p.ws = nullptr;

@@ -50,7 +50,7 @@ class GemmDesc(ctypes.Structure):
         ("b_f32", ctypes.c_int32),
         ("workspace", ctypes.c_void_p), ("workspace_elems", ctypes.c_int64),
         ("drop_p", ctypes.c_float), ("drop_group", ctypes.c_int32), ("drop_seed", ctypes.c_uint64),
-        ("f16", ctypes.c_int32), ("alpha_dev", ctypes.c_void_p),
+        ("f16", ctypes.c_int32), ("alpha_dev", ctypes.c_void_p), ("stride_bias", ctypes.c_int64),
     ]
 
 

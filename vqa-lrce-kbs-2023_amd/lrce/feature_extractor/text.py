@@ -18,6 +18,7 @@ import warnings
 import torch
 import torch.nn as nn
 
+from .. import _native as N
 from .. import kernels as K
 from ..runtime import ensure
 
@@ -146,9 +147,7 @@ class _LayerFn(torch.autograd.Function):
         xb, q, k, v, ctxt, h1b, g, pre = _views(buf, rows)
         w = flat.w16h
         K.cast_f16(x, xb)
-        K.linear(xb, w(sa.query.weight), sa.query.bias, out=q)
-        K.linear(xb, w(sa.key.weight), sa.key.bias, out=k)
-        K.linear(xb, w(sa.value.weight), sa.value.bias, out=v)
+        _qkv(xb, sa, w, q, k, v, rows)
         lse = torch.empty(B, HEADS, L, device=dev)
         desc = K.mha_desc(q, L, k1=k, v1=v, lk1=L, ld_kv1=HIDDEN, stride_kv1_b=L * HIDDEN, key_mask=mask, out=ctxt,
                           lse=lse, B=B, H=HEADS, scale=0.125, drop_p=p, seed=seed)
@@ -211,6 +210,27 @@ class _LayerFn(torch.autograd.Function):
         ctx.save = ctx.desc = None
         flat.notify(layer.parameters())
         return (dx,) + (None,) * (7 + len(ctx.needs_input_grad[8:]))
+
+
+def _qkv(xb, sa, w, q, k, v, rows):
+    """query / key / value = xb W^T + b (fp16 out): one batched launch when the three weights and
+    biases sit at one stride in the flat buffers and q, k, v at one stride in the layer buffer (3x
+    the workgroups of one 320 x 768 x 768 GEMM, 2 launches fewer per layer); else three."""
+    lins = (sa.query, sa.key, sa.value)
+    ws = [w(l.weight) for l in lins]
+    es = 2   # fp16 shadow / q, k, v element size
+    sw = [(ws[i + 1].data_ptr() - ws[i].data_ptr()) // es for i in range(2)]
+    sb = [(lins[i + 1].bias.data_ptr() - lins[i].bias.data_ptr()) // 4 for i in range(2)]
+    sc = [(o2.data_ptr() - o1.data_ptr()) // es for o1, o2 in ((q, k), (k, v))]
+    if _QKV_BATCHED and sw[0] == sw[1] == sb[0] == sb[1] and sc[0] == sc[1] == rows * HIDDEN and sw[0] > 0:
+        K.gemm(xb, ws[0], q, rows, HIDDEN, HIDDEN, flags=N.EPI_BIAS, bias=lins[0].bias, batch=3, stride_b=sw[0],
+               stride_c=sc[0], stride_bias=sb[0], f16=True)
+        return
+    for lin, wt, o in zip(lins, ws, (q, k, v)):
+        K.linear(xb, wt, lin.bias, out=o)
+
+
+_QKV_BATCHED = os.environ.get("LRCE_BERT_QKV_BATCHED", "1") != "0"   # A/B knob
 
 
 def _grad_scales(layer, dev):

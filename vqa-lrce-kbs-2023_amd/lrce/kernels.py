@@ -103,7 +103,8 @@ def _chk(t, dtype=None, name="tensor"):
 def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, flags=0, bias=None,
          aux=None, ld_aux=0, aux_out=None, ld_aux_out=0, a_map=None, c_map=None, alpha=1.0, split_k=1,
          scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, a_row_scale=None, a_rows_per_scale=1,
-         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None, f16=False, ln=None, alpha_dev=None):
+         batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None, f16=False, ln=None, alpha_dev=None,
+         stride_bias=0):
     """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc.  drop = (p, seed, group):
     nn.Dropout fused into the epilogue (exact-f32 skinny path; same mask as dropout()).  f16: every
     16-bit tensor (A, B, 16-bit C, aux_out) is torch.float16 (the BERT forward).  ln: a LayerNorm
@@ -126,6 +127,7 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.a, d.b, d.c = ptr(a), ptr(b), ptr(c)
     d.lda, d.ldb, d.ldc = lda, ldb, ldc
     d.stride_a, d.stride_b, d.stride_c = stride_a, stride_b, stride_c
+    d.stride_bias = stride_bias
     d.m, d.n, d.k, d.batch = m, n, k, batch
     d.a_kmajor, d.b_kmajor, d.a_f32 = int(a_kmajor), int(b_kmajor), int(a_f32)
     d.flags, d.split_k = flags, split_k
