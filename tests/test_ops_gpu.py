@@ -140,6 +140,20 @@ def test_gemm_batched_bias_stride(bf):
         W = wbuf[i * stride:i * stride + N * Kd].view(N, Kd)
         ref = A.double() @ W.double().t() + bbuf[i * stride:i * stride + N].double()
         assert rel(out[i], ref.float()) < (8e-3 if bf else 1e-3), i
+    # the weight-gradient form: dW_i += dY_i^T X, db_i += colsum(dY_i) (M-major A, one K slice)
+    dy = torch.randn(3, M, N, device=dev).to(h)
+    gw = torch.randn(3 * stride, device=dev)
+    g0 = gw.clone()
+    k.gemm(dy[0], A, gw, N, Kd, M, a_kmajor=False, b_kmajor=False, lda=N, ldb=Kd, ldc=Kd,
+           flags=k.N.EPI_ACCUM | k.N.EPI_BIAS_GRAD, bias=gw[N * Kd:], batch=3, stride_a=M * N, stride_c=stride,
+           stride_bias=stride, f16=not bf)
+    for i in range(3):
+        o = i * stride
+        refw = g0[o:o + N * Kd].view(N, Kd).double() + dy[i].double().t() @ A.double()
+        refb = g0[o + N * Kd:o + N * Kd + N].double() + dy[i].double().sum(0)
+        assert rel(gw[o:o + N * Kd].view(N, Kd), refw.float()) < 1e-5, i
+        assert rel(gw[o + N * Kd:o + N * Kd + N], refb.float()) < 1e-5, i
+        assert torch.equal(gw[o + N * Kd + N:o + stride], g0[o + N * Kd + N:o + stride])   # the gap untouched
 
 
 def test_f16_casts():

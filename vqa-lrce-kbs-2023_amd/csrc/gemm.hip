@@ -1021,8 +1021,11 @@ extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
   if (d->f16 && (d->a_f32 || d->b_f32)) return lrce_fail(LRCE_E_ARG, "gemm: f16 operands cannot be combined with f32 A/B");
   if (!(d->flags & LRCE_EPI_BIAS_GRAD)) return gemm_dispatch(d, stream);
   // bias gradient of a weight-gradient GEMM: db[m] += sum_k A(m, k)
-  if (d->a_kmajor || !d->bias || d->batch != 1) return lrce_fail(LRCE_E_ARG, "gemm: BIAS_GRAD needs M-major A, bias, batch 1");
+  if (d->a_kmajor || !d->bias) return lrce_fail(LRCE_E_ARG, "gemm: BIAS_GRAD needs M-major A and bias");
   if (d->flags & LRCE_EPI_BIAS) return lrce_fail(LRCE_E_ARG, "gemm: BIAS and BIAS_GRAD are exclusive");
+  // batched (BERT's query / key / value weight gradients): LDS-DMA path, one K slice, a bias per batch
+  if (d->batch != 1 && (d->b_f32 || !glds_ok(d) || d->split_k > 1 || d->stride_bias <= 0))
+    return lrce_fail(LRCE_E_ARG, "gemm: batched BIAS_GRAD needs the 16-bit LDS-DMA path, split_k 1 and stride_bias > 0");
   const bool fused = d->b_f32 ? lrce_gemm_f32_outer_ok(d) : glds_ok(d);
   if (fused) return gemm_dispatch(d, stream);   // the skinny outer-product kernel sums A as it goes
   LrceGemmDesc g = *d;
