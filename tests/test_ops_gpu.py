@@ -140,6 +140,11 @@ def test_gemm_batched_bias_stride(bf):
         W = wbuf[i * stride:i * stride + N * Kd].view(N, Kd)
         ref = A.double() @ W.double().t() + bbuf[i * stride:i * stride + N].double()
         assert rel(out[i], ref.float()) < (8e-3 if bf else 1e-3), i
+    # a negative C stride (the reverse parameter layout of training: batch i writes plane 2 - i)
+    out2 = torch.empty(3, M, N, device=dev, dtype=h)
+    k.gemm(A, wbuf, out2[2], M, N, Kd, flags=k.N.EPI_BIAS, bias=bbuf, batch=3, stride_b=stride, stride_c=-M * N,
+           stride_bias=stride, f16=not bf)
+    assert torch.equal(out2.flip(0), out)
     # the weight-gradient form: dW_i += dY_i^T X, db_i += colsum(dY_i) (M-major A, one K slice)
     dy = torch.randn(3, M, N, device=dev).to(h)
     gw = torch.randn(3 * stride, device=dev)

@@ -222,9 +222,13 @@ def _qkv(xb, sa, w, q, k, v, rows):
     sw = [(ws[i + 1].data_ptr() - ws[i].data_ptr()) // es for i in range(2)]
     sb = [(lins[i + 1].bias.data_ptr() - lins[i].bias.data_ptr()) // 4 for i in range(2)]
     sc = [(o2.data_ptr() - o1.data_ptr()) // es for o1, o2 in ((q, k), (k, v))]
-    if _QKV_BATCHED and sw[0] == sw[1] == sb[0] == sb[1] and sc[0] == sc[1] == rows * HIDDEN and sw[0] > 0:
-        K.gemm(xb, ws[0], q, rows, HIDDEN, HIDDEN, flags=N.EPI_BIAS, bias=lins[0].bias, batch=3, stride_b=sw[0],
-               stride_c=sc[0], stride_bias=sb[0], f16=True)
+    if _QKV_BATCHED and sw[0] == sw[1] == sb[0] == sb[1] and sc[0] == sc[1] == rows * HIDDEN and sw[0] != 0:
+        if sw[0] > 0:
+            K.gemm(xb, ws[0], q, rows, HIDDEN, HIDDEN, flags=N.EPI_BIAS, bias=lins[0].bias, batch=3, stride_b=sw[0],
+                   stride_c=sc[0], stride_bias=sb[0], f16=True)
+        else:   # the training layout stores parameters in reverse forward order: batch i = value, key, query
+            K.gemm(xb, ws[2], v, rows, HIDDEN, HIDDEN, flags=N.EPI_BIAS, bias=lins[2].bias, batch=3, stride_b=-sw[0],
+                   stride_c=-sc[0], stride_bias=-sb[0], f16=True)
         return
     for lin, wt, o in zip(lins, ws, (q, k, v)):
         K.linear(xb, wt, lin.bias, out=o)
