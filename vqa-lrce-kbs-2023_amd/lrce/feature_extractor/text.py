@@ -202,8 +202,7 @@ class _LayerFn(torch.autograd.Function):
                   dkv1_store=True)
         dqkv16 = torch.empty(3, rows, HIDDEN, dtype=torch.float16, device=dout.device)
         K.cast_f16(dqkv, dqkv16)
-        for i, lin in enumerate((sa.query, sa.key, sa.value)):
-            _wgrad(flat, lin, dqkv16[i], xb, inv_a)
+        _wgrad_qkv(flat, sa, dqkv16, xb, inv_a, rows)
         dx = K.linear_dx(dqkv16[0], w(sa.query.weight), resid=da2, alpha_dev=inv_a)
         K.linear_dx(dqkv16[1], w(sa.key.weight), out=dx, accumulate=True, alpha_dev=inv_a)
         K.linear_dx(dqkv16[2], w(sa.value.weight), out=dx, accumulate=True, alpha_dev=inv_a)
@@ -279,6 +278,29 @@ def _wgrad(flat, lin, dy, x16, inv_scale=None):
             t = torch.zeros_like(gb)
             K.colsum(dy, t)
             gb.add_(t * inv_scale)
+
+
+def _wgrad_qkv(flat, sa, dqkv16, xb, inv_scale, rows):
+    """_wgrad of query / key / value as one batched launch when their weight and bias gradients sit at
+    one stride in the flat gradient buffer (A/B knob LRCE_BERT_QKV_WGRAD_BATCHED); else three."""
+    lins = (sa.query, sa.key, sa.value)
+    gws = [_g(flat, l.weight) for l in lins]
+    gbs = [_g(flat, l.bias) for l in lins]
+    if _QKV_WGRAD_BATCHED and all(t is not None for t in gws + gbs):
+        sw = [(gws[i + 1].data_ptr() - gws[i].data_ptr()) // 4 for i in range(2)]
+        sb = [(gbs[i + 1].data_ptr() - gbs[i].data_ptr()) // 4 for i in range(2)]
+        if sw[0] == sw[1] == sb[0] == sb[1] and sw[0] != 0:
+            i0, d = (0, 1) if sw[0] > 0 else (2, -1)     # batch order: ascending gradient addresses
+            K.gemm(dqkv16[i0], xb, gws[i0], HIDDEN, HIDDEN, rows, a_kmajor=False, b_kmajor=False, lda=HIDDEN,
+                   ldb=HIDDEN, ldc=HIDDEN, flags=N.EPI_ACCUM | N.EPI_BIAS_GRAD, bias=gbs[i0], batch=3,
+                   stride_a=d * rows * HIDDEN, stride_c=abs(sw[0]), stride_bias=abs(sb[0]), f16=True,
+                   alpha_dev=inv_scale)
+            return
+    for i, lin in enumerate(lins):
+        _wgrad(flat, lin, dqkv16[i], xb, inv_scale)
+
+
+_QKV_WGRAD_BATCHED = os.environ.get("LRCE_BERT_QKV_WGRAD_BATCHED", "1") != "0"   # A/B knob
 
 
 class BertModel(nn.Module):
