@@ -13,12 +13,19 @@ autocast) with f32 master weights / residual stream.  The agent path itself (pin
 process_data) is timed after the main measurement and reported as `agent_path`.
 
     python bench.py [--gpus N --steps K --warmup W]
-N>1: launched by torch.distributed.run (one process per GPU, RCCL); each rank runs bs=10 (weak
-scaling); rank 0 prints ONE JSON line.
+N>1: one process per GPU over RCCL (the reference's train_ddp.py:136-138 spawns world_size =
+device_count processes); each rank runs bs=10 (weak scaling); rank 0 prints ONE JSON line.  Started
+by torch.distributed.run (WORLD_SIZE set) it is one of the ranks; started plainly with --gpus N > 1 it
+first launches the N ranks itself, as children through torch.distributed.run, before anything touches
+the GPU, and exits with their status.  A joined world that differs from --gpus is an error.
+--dry-run: the same launcher and rank/world checks over gloo on the CPU (no model, no GPU) — the
+launcher's test.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -58,7 +65,56 @@ def parse():
     ap.add_argument("--roofline-steps", type=int, default=2)
     ap.add_argument("--gemm-table", default=None,
                     help="write the per-shape roofline table of the bf16 GEMMs of the roofline steps (markdown) here")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check: N gloo ranks on the CPU time an all-reduce 'step'; no GPU, no model")
     return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N > 1 from a plain start: N rank processes through torch.distributed.run, as CHILDREN of
+    this process, which has not touched the GPU (torch.cuda.device_count() does not initialise HIP on
+    this image; nothing else here runs before this point).  Returns their exit status."""
+    if not args.dry_run:
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            log(f"--gpus {args.gpus}: only {ndev} device(s) visible")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # the host driver supports dmabuf IPC only
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """The launcher's check on the CPU: gloo ranks, barrier + max-over-ranks timing of K all-reduce
+    'steps' of a 1 MB gradient stand-in, rank 0 prints the JSON line with the joined world size."""
+    x = torch.ones(1 << 18)
+    for _ in range(args.warmup):
+        dist.all_reduce(x)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dist.all_reduce(x)
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "value": round(world * args.batch_size * args.steps / elapsed, 3),
+                          "unit": "launcher-check steps/s (not a measurement)", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+                          "config": {"parallelism": f"dp{world}", "per_gpu_batch": args.batch_size,
+                                     "grad_reduce": args.grad_reduce_dtype if world > 1 else None}}), flush=True)
 
 
 def synthetic_batch(batch, seed):
@@ -226,12 +282,34 @@ def cpu_baseline(threads, batch=10):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        log("--gpus must be >= 1")
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+            world = dist.get_world_size()
+        if world != args.gpus:
+            log(f"rank {rank}: joined a world of {world} ranks, --gpus {args.gpus}")
+            sys.exit(3)
+        if world > 1:
+            dry_run(args, world, rank)
+            dist.destroy_process_group()
+        elif rank == 0:
+            print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": 1, "config": {"parallelism": "dp1"}}), flush=True)
+        return
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
+    if world != args.gpus:
+        log(f"rank {rank}: joined a world of {world} ranks but --gpus {args.gpus}")
+        sys.exit(3)
     device = torch.device("cuda", local)
     from lrce import kernels as K
     from lrce import _native

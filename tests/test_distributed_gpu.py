@@ -76,9 +76,13 @@ def _worker(rank, world, port, mode, q):
     out = {}
     try:
         from lrce.agent.agent_base import DataParallel
-        gdt = torch.bfloat16 if mode in ("bf16", "graph", "graph_split", "graph_split3") else torch.float32
+        gdt = torch.float32 if mode.endswith("f32") else torch.bfloat16
         model = _model(seed=100 + rank)                 # different init per rank: the broadcast must fix it
         dp = DataParallel(model, bucket_mb=32, grad_dtype=gdt)
+        if mode.endswith("_plain"):
+            # every bf16 bucket through the plain all-reduce fallback (async handles the collective
+            # stream must wait on before the early-update graphs read the sums)
+            dp.reducer.force_plain = True
         flat = dp.reducer.flat
         n = 2 * world
         clips, ids, mask, types, labels = _batch(n)
@@ -195,13 +199,14 @@ def test_dp_gradients_equal_full_batch(mode, tol):
         assert _rel(res[0]["dp"][k], res[0]["ref"][k]) < tol, (k, _rel(res[0]["dp"][k], res[0]["ref"][k]))
 
 
-@pytest.mark.parametrize("mode", ["graph", "graph_split", "graph_split3", "graph_split3_f32"])
+@pytest.mark.parametrize("mode", ["graph", "graph_split", "graph_split3", "graph_split3_f32", "graph_split3_plain"])
 def test_dp_graph_training_steps_match_single_process(mode):
     """graph: graph(fwd + bwd) -> exchange -> graph(optimizer); graph_split: the head's backward and
     the extractors' backward as two graphs with the head's buckets exchanged between them;
     graph_split3: three backward graphs (the Swin backward cut before stage 3, E2EBase.split_swin_stage),
-    BERT's and Swin 3-4's buckets exchanged while Swin 1-2 replay.  bf16 buckets: updates compared in
-    aggregate; f32 buckets (graph_split3_f32): per element."""
+    BERT's and Swin 3-4's buckets exchanged while Swin 1-2 replay, their AdamW updates replayed behind
+    each exchange; graph_split3_plain: the same with every bf16 bucket on the plain all-reduce fallback.
+    Updates compared per element (bf16 buckets with a looser count of rounding-level outliers)."""
     res = _run(mode)
     lr = 1e-4
     for k in KEYS:
@@ -210,13 +215,12 @@ def test_dp_graph_training_steps_match_single_process(mode):
         upd = a0 - res[0]["before"][k]
         ref = res[0]["ref_after"][k] - res[0]["before"][k]
         assert upd.abs().max() > 0, k
-        if mode.endswith("f32"):
-            # AdamW's first steps are ~lr * sign(g) per element: every element within 5 % of lr of the
-            # single-process update, except the few whose gradient is at rounding level (a sign flip of
-            # a ~0 gradient moves that element by up to 2 lr per step): at most 0.5 % of them
-            d = (upd - ref).abs()
-            assert float((d > 0.05 * lr).float().mean()) < 5e-3, (k, float((d > 0.05 * lr).float().mean()))
-            assert float(d.max()) <= 6.01 * lr, k
-        else:
-            # bf16 transport: compare the updates in aggregate
-            assert float((upd - ref).abs().mean() / ref.abs().mean()) < 0.1, k
+        # AdamW's first steps are ~lr * sign(g) per element: every element within 5 % of lr of the
+        # single-process update, except the few whose gradient is at rounding level (a sign flip of a ~0
+        # gradient moves that element by up to 2 lr per step): at most 0.5 % of them with f32 buckets,
+        # 2 % with bf16 ones (the bf16 rounding of each rank's bucket moves more near-zero gradients)
+        d = (upd - ref).abs()
+        frac = float((d > 0.05 * lr).float().mean())
+        assert frac < (5e-3 if mode.endswith("f32") else 2e-2), (k, frac)
+        assert float(d.max()) <= 6.01 * lr, k
+        assert float((upd - ref).abs().mean() / ref.abs().mean()) < 0.05, k

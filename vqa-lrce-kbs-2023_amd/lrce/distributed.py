@@ -80,6 +80,9 @@ class GradReducer:
             self.shard = torch.empty(-(-big // self.world), dtype=torch.bfloat16, device=flat.device)
         self.capturing = False
         self.captured = None       # buckets in completion order (graph mode)
+        # test hook: exchange every bf16 bucket by the plain all-reduce fallback (the path a bucket that
+        # does not split into 16-B-aligned shards takes)
+        self.force_plain = False
         self.begin()
 
     # ------------------------------------------------------------------ bucket state
@@ -126,7 +129,7 @@ class GradReducer:
             self.handles.append(dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True))
             return
         n, w = e - s, self.world
-        if n % (8 * w):
+        if n % (8 * w) or self.force_plain:
             # a bucket that does not split into 16-B-aligned shards (only with an odd world size):
             # plain bf16 all-reduce of that bucket
             self.handles.append(dist.all_reduce(self.grad16[s:e], group=self.group, async_op=True))
@@ -220,15 +223,17 @@ class GradReducer:
         return out
 
     def exchanged_stream(self):
-        """A stream ordered after every exchange started so far (the collective stream; f32 buckets:
-        it also waits for their all-reduce handles), for work that consumes the summed buckets while
-        the compute stream moves on.  None on CPU."""
+        """A stream ordered after every exchange started so far, for work that consumes the summed
+        buckets while the compute stream moves on: the collective stream, made to wait for the compute
+        stream's work so far (the backward that wrote the buckets, whatever path their exchange took)
+        and for every async all-reduce handle (f32 buckets and bf16 buckets on the plain all-reduce
+        fallback, which run on the process group's own stream).  None on CPU."""
         if self.comm is None:
             return None
-        if self.grad16 is None:
-            with torch.cuda.stream(self.comm):
-                for h in self.handles:
-                    h.wait()
+        self.comm.wait_stream(torch.cuda.current_stream(self.flat.device))
+        with torch.cuda.stream(self.comm):
+            for h in self.handles:
+                h.wait()
         return self.comm
 
     def join(self):

@@ -633,9 +633,14 @@ class SwinTransformer3D(nn.Module):
 
     def backward_below_split(self):
         """Second part of a split Swin backward: stages below split_at (and the patch embedding) from
-        the gradient the first part left on the stage input."""
+        the gradient the first part left on the stage input.  No-op when the forward made no split
+        (frozen lower stages / patch embedding, or a forward without gradients)."""
+        if self._split_mid is None:
+            return
         x, x_leaf = self._split_mid
         self._split_mid = None
+        if x_leaf.grad is None:
+            return
         torch.autograd.backward([x], [x_leaf.grad])
 
     def forward_stage(self, i, x_cl, depth=None):

@@ -150,6 +150,11 @@ class TrainStepGraph:
                 else:
                     with torch.cuda.graph(st.g_step, pool=pool):
                         st.out = self.body(*st.static)
+                        if self.early_opt:
+                            # the step's optimizer bookkeeping (device step counter, lr table, a norm
+                            # pass if the masters changed outside the optimizer) on the main stream,
+                            # ahead of every exchange: the early-update graphs then hold only updates
+                            self.optim._begin()
                     marks = [self.reducer.capture_mark()]
                     st.g_tail = []
                     for i, seg in enumerate(self.tail):
@@ -192,7 +197,15 @@ class TrainStepGraph:
             st.warm = True
             return self._eager(st)
         if st.g_step is None:
-            self._capture(st)
+            try:
+                self._capture(st)
+            except BaseException:
+                # a failed capture must not leave the optimizer believing this step has begun (the next
+                # eager step would skip its step-counter increment) or that chunks were updated
+                self.optim._begun = False
+                self.optim._done = []
+                st.g_step = None
+                raise
         self.optim._sync_lrs()
         st.g_step.replay()
         if st.g_tail is not None:
