@@ -111,6 +111,10 @@ typedef struct LrceGemmDesc {
    * key / value linears as one batched launch over their weights and biases in the flat parameter
    * buffers (text.py:11-17 -> HF BertSelfAttention). */
   int64_t stride_bias;
+  /* Batch stride of `alpha_dev` in floats (batch > 1; 0 = one alpha for every batch): the deferred BERT
+   * weight gradients of all layers as one batched launch, each layer's product scaled by the inverse
+   * of that layer's own gradient scale. */
+  int64_t stride_alpha;
 } LrceGemmDesc;
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);
@@ -283,6 +287,10 @@ typedef struct LrceMhaDesc {
    * (every row has one writer in this launch and no earlier contribution: kv1_bdiv == 1 and a memory
    * that is distinct per call, e.g. the video tokens of one recurrent step) — no zero fill, no read. */
   int32_t dkv1_store;
+  /* short self-attention backward with dkv1_store: 1 = dq / dk1 / dv1 point to IEEE fp16 buffers (the
+   * f32 values rounded once), e.g. the three column blocks of one [rows, 3 * H * d] operand of the
+   * fused q/k/v input-gradient GEMM and the deferred weight gradients (BERT, text.py:11-17). */
+  int32_t grad16;
 } LrceMhaDesc;
 
 int lrce_mha_fwd(const LrceMhaDesc* desc, void* stream);

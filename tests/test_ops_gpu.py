@@ -270,6 +270,83 @@ def test_mha_self_f16_backward(L):
         assert torch.isfinite(got).all() and rel(got, ref) < 1e-2
 
 
+@pytest.mark.parametrize("h", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("M,N,Kd", [(320, 768, 768), (320, 768, 3072), (1000, 264, 96), (9000, 512, 128)])
+def test_fused_dropout_lds_dma_epilogue(h, M, N, Kd):
+    """16-bit linears with nn.Dropout + residual fused into the LDS-DMA GEMM epilogue (the BERT
+    residual branches, text.py _LayerFn): the same bits as GEMM + lrce_dropout (mask over the
+    contiguous [M][N] result), 64x64 and 128x128 tile paths."""
+    k = K()
+    k.rng_offset(dev).zero_()
+    x = torch.randn(M, Kd, device=dev).to(h)
+    w = (torch.randn(N, Kd, device=dev) / math.sqrt(Kd)).to(h)
+    b = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    for p in (0.1, 0.5):
+        fused = k.linear(x, w, b, out_f32=True, resid=res, drop=(p, 91, 1))
+        ref = k.dropout(k.linear(x, w, b, out_f32=True), p, 91, res=res)
+        assert torch.equal(fused, ref), p
+    k.rng_offset(dev).add_(12345)          # the device RNG offset moves the mask in both forms
+    fused = k.linear(x, w, b, out_f32=True, resid=res, drop=(0.1, 91, 1))
+    assert torch.equal(fused, k.dropout(k.linear(x, w, b, out_f32=True), 0.1, 91, res=res))
+    k.rng_offset(dev).zero_()
+
+
+def test_gemm_batched_alpha_stride():
+    """Batched weight-gradient GEMMs with a per-batch device alpha (stride_alpha): the deferred BERT
+    weight gradients of all layers in one launch, each scaled by its own layer's 1/S; negative A / alpha
+    strides (batches in ascending gradient address, layers in reverse)."""
+    k = K()
+    h = torch.float16
+    nb, M, N, Kd, gap = 4, 320, 768, 3072, 512
+    sg = N * Kd + N + gap                              # gradient slot per batch: weight, bias, gap
+    dy = (torch.randn(nb, M, N, device=dev) * 64).to(h)
+    X = torch.randn(nb, M, Kd, device=dev).to(h)
+    alpha = torch.zeros(nb, 2, 4, device=dev)
+    alpha[:, 0, 1] = torch.tensor([1 / 64, 1 / 128, 1 / 32, 1 / 256], device=dev)
+    g = torch.randn(nb * sg, device=dev)
+    g0 = g.clone()
+    # batch i <-> operand plane nb-1-i (negative operand / alpha strides)
+    k.gemm(dy[nb - 1], X[nb - 1], g, N, Kd, M, a_kmajor=False, b_kmajor=False, lda=N, ldb=Kd, ldc=Kd,
+           flags=k.N.EPI_ACCUM | k.N.EPI_BIAS_GRAD, bias=g[N * Kd:], batch=nb, stride_a=-M * N, stride_b=-M * Kd,
+           stride_c=sg, stride_bias=sg, f16=True, alpha_dev=alpha[nb - 1, 0, 1:2], stride_alpha=-8)
+    for i in range(nb):
+        j = nb - 1 - i
+        a = float(alpha[j, 0, 1])
+        o = i * sg
+        refw = g0[o:o + N * Kd].view(N, Kd).double() + a * (dy[j].double().t() @ X[j].double())
+        refb = g0[o + N * Kd:o + N * Kd + N].double() + a * dy[j].double().sum(0)
+        assert rel(g[o:o + N * Kd].view(N, Kd), refw.float()) < 1e-5, i
+        assert rel(g[o + N * Kd:o + N * Kd + N], refb.float()) < 1e-5, i
+        assert torch.equal(g[o + N * Kd + N:o + sg], g0[o + N * Kd + N:o + sg])
+
+
+@pytest.mark.parametrize("L", [32, 40])
+def test_mha_self_f16_backward_fp16_gradients(L):
+    """grad16: dq / dk / dv stored as fp16 column blocks of one [rows, 3 * 768] operand (the fused BERT
+    q/k/v input-gradient GEMM): the bits of the f32 outputs cast to fp16."""
+    k = K()
+    B, H, D = 6, 12, 64
+    C = H * D
+    q, kk, v = (torch.randn(B * L, C, device=dev).to(torch.float16) for _ in range(3))
+    mask = torch.ones(B, L, dtype=torch.int32, device=dev)
+    mask[:, 25:] = 0
+    out = torch.empty(B * L, C, device=dev, dtype=torch.float16)
+    lse = torch.empty(B, H, L, device=dev)
+    desc = k.mha_desc(q, L, k1=kk, v1=v, lk1=L, ld_kv1=C, stride_kv1_b=L * C, key_mask=mask, out=out, lse=lse,
+                      B=B, H=H, scale=0.125, drop_p=0.1, seed=5)
+    k.mha_fwd(desc, out)
+    do = (torch.randn(B * L, C, device=dev) * 200).to(torch.float16)
+    f = [torch.empty(B * L, C, device=dev) for _ in range(3)]
+    k.mha_bwd(desc, dout=do, dq=f[0], dk1=f[1], dv1=f[2], ld_dkv1=C, stride_dkv1_b=L * C, dkv1_store=True)
+    g = torch.full((B * L, 3 * C), float("nan"), device=dev, dtype=torch.float16)
+    cols = (2 * C, C, 0)                       # dq, dk, dv blocks in the reverse (value, key, query) order
+    k.mha_bwd(desc, dout=do, dq=g[:, cols[0]:cols[0] + C], dk1=g[:, cols[1]:cols[1] + C], dv1=g[:, cols[2]:cols[2] + C],
+              ld_dq=3 * C, ld_dkv1=3 * C, stride_dkv1_b=L * 3 * C, dkv1_store=True)
+    for t, c in zip(f, cols):
+        assert torch.equal(g[:, c:c + C], t.to(torch.float16)), c
+
+
 @pytest.mark.parametrize("M,N,Kd", [(10, 768, 768), (50, 3072, 768), (45, 768, 3072), (128, 200, 96)])
 @pytest.mark.parametrize("a_km,b_km", [(1, 1), (1, 0), (0, 0)])
 def test_gemm_exact_f32_path(M, N, Kd, a_km, b_km):

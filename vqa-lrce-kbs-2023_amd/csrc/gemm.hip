@@ -53,7 +53,13 @@ struct GemmP {
   int f16;   // 16-bit tensors are IEEE fp16 (LrceGemmDesc.f16)
   int group_m;   // tile raster: groups of group_m tile rows, column-major inside a group (1 = row-major)
   const float* alpha_dev;   // non-null: alpha read from device memory (a gradient scale computed on the GPU)
+  long long salpha;         // batch stride of alpha_dev (floats)
   unsigned long long* trace;   // phase timestamps (builds with -DLRCE_GEMM_TRACE only; lrce_gemm_set_trace)
+  // nn.Dropout in the epilogue (after bias / GELU / row scale, before the RESID add): the mask of
+  // lrce_dropout over the contiguous [m][n] result (element m * n + col), drop_group 1
+  float drop_p;
+  uint64_t drop_seed;
+  const uint64_t* rng_off;
 };
 
 // Debug phase marks of gemm_glds_kernel (tools/gemm_trace.py): wave 0 of every workgroup stores
@@ -195,6 +201,8 @@ __device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row
   }
   if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(from16r(static_cast<const bf16*>(p.aux)[row * p.ld_aux + nn], p.f16));
   x *= rs;
+  if (p.drop_p > 0.f)
+    x = lrce_uniform(lrce_seed(p.drop_seed, p.rng_off), (unsigned long long)m * p.n + nn) >= p.drop_p ? x / (1.0f - p.drop_p) : 0.f;
   if ((fl & LRCE_EPI_RESID) && first) x += static_cast<const float*>(p.aux)[row * p.ld_aux + nn];
   if (fl & LRCE_EPI_ATOMIC) {
     __hip_atomic_fetch_add(reinterpret_cast<float*>(cbase) + row * p.ldc + nn, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -276,6 +284,15 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= rs;
     }
+    if (p.drop_p > 0.f) {   // lrce_dropout's bits: v / (1 - p) where kept (n % 8 == 0 on this path)
+      const uint64_t sd = lrce_seed(p.drop_seed, p.rng_off);
+      const unsigned long long i4 = ((unsigned long long)m * p.n + n) >> 2;
+      const float4 u0 = lrce_uniform4(sd, i4), u1 = lrce_uniform4(sd, i4 + 1);
+      const float u[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      const float kd = 1.0f - p.drop_p;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = u[e] >= p.drop_p ? v[e] / kd : 0.f;
+    }
     if ((fl & LRCE_EPI_RESID) && first) {
       const float* ap = static_cast<const float*>(p.aux) + row * p.ld_aux + n;
       const float4 r0 = rs_pf ? rs_pf[0] : *reinterpret_cast<const float4*>(ap);
@@ -327,6 +344,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
   const int z = blockIdx.y;  // batch * split
   const int bz = z / p.split_k, sk = z % p.split_k;
   p.bias += (long long)bz * p.sbias;
+  if (p.alpha_dev) p.alpha_dev += (long long)bz * p.salpha;
   const int lin = xcd_remap(blockIdx.x, tiles);
   int tm, tn;
   tile_of(p, lin, tm, tn);
@@ -578,6 +596,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   const int z = blockIdx.y;
   const int bz = z / p.split_k, sk = z % p.split_k;
   p.bias += (long long)bz * p.sbias;
+  if (p.alpha_dev) p.alpha_dev += (long long)bz * p.salpha;
   const int lin = xcd_remap(blockIdx.x, tiles);
   int tm, tn;
   tile_of(p, lin, tm, tn);
@@ -1016,7 +1035,11 @@ static int g_gemm_tile = getenv("LRCE_GEMM_TILE") ? atoi(getenv("LRCE_GEMM_TILE"
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
 
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
-  if (d && d->drop_p > 0.f && !d->b_f32) return lrce_fail(LRCE_E_ARG, "gemm: fused dropout is only on the exact-f32 skinny path");
+  if (d && d->drop_p > 0.f && !d->b_f32 &&
+      (!glds_ok(d) || d->drop_group > 1 || d->split_k > 1 || d->batch != 1 || d->c_map ||
+       (d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_BIAS_GRAD))))
+    return lrce_fail(LRCE_E_ARG, "gemm: fused dropout needs the exact-f32 skinny path or the 16-bit LDS-DMA path "
+                                 "(drop_group 1, one K slice, batch 1, no c_map / accumulate)");
   if (!d || !d->a || !d->b || !d->c) return lrce_fail(LRCE_E_ARG, "gemm: null pointer");
   if (d->f16 && (d->a_f32 || d->b_f32)) return lrce_fail(LRCE_E_ARG, "gemm: f16 operands cannot be combined with f32 A/B");
   if (!(d->flags & LRCE_EPI_BIAS_GRAD)) return gemm_dispatch(d, stream);
@@ -1082,7 +1105,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   p.sbias = d->batch > 1 ? d->stride_bias : 0;
   p.aux_out = static_cast<bf16*>(d->aux_out); p.ld_aux_out = d->ld_aux_out;
   p.a_map = d->a_map; p.c_map = d->c_map;
-  p.alpha = d->alpha; p.alpha_dev = d->alpha_dev; p.scale_cols = d->scale_cols; p.scale_val = d->scale_val;
+  p.alpha = d->alpha; p.alpha_dev = d->alpha_dev; p.salpha = d->batch > 1 ? d->stride_alpha : 0; p.scale_cols = d->scale_cols; p.scale_val = d->scale_val;
   p.trace = g_gemm_trace;
   p.row_scale = d->row_scale; p.rows_per_scale = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
   p.a_row_scale = d->a_row_scale; p.a_rows_per_scale = d->a_rows_per_scale > 0 ? d->a_rows_per_scale : 1;
@@ -1100,6 +1123,9 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   (void)out32;
   p.ws = nullptr;
   p.f16 = d->f16 ? 1 : 0;
+  p.drop_p = d->drop_p > 0.f ? d->drop_p : 0.f;
+  p.drop_seed = d->drop_seed;
+  p.rng_off = p.drop_p > 0.f ? lrce_rng_offset() : nullptr;
   if (p.f16 && !glds_ok(d))
     return lrce_fail(LRCE_E_ARG, "gemm: f16 needs 16-B aligned bf16-layout operands (LDS-DMA path)");
   const bool use_ws = d->workspace && split > 1 && (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)) == 0 &&

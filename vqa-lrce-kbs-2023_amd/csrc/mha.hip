@@ -678,7 +678,10 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
         const long long o = (long long)b * d.stride_dkv1_b + (long long)kk * d.ld_dkv1 + h * D + r32;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
-          if (d.dkv1_store) {
+          if (d.grad16) {   // (host: grad16 implies dkv1_store)
+            reinterpret_cast<f16*>(d.dk1)[o + 32 * dt] = f2h(dk[dt][r] * d.scale);
+            reinterpret_cast<f16*>(d.dv1)[o + 32 * dt] = f2h(dv[dt][r]);
+          } else if (d.dkv1_store) {
             d.dk1[o + 32 * dt] = dk[dt][r] * d.scale;
             d.dv1[o + 32 * dt] = dv[dt][r];
           } else {
@@ -695,9 +698,16 @@ __global__ void __launch_bounds__(128) mhaL_bwd_kernel(MhaP P) {
     for (int r = 0; r < 16; ++r) {
       const int qi = qt * 32 + crow32(r, hh);
       if (qi < L) {
-        float* dst = d.dq + ((long long)b * L + qi) * d.ld_dq + h * D + r32;
-        dst[0] = dq[qt][0][r] * d.scale;
-        dst[32] = dq[qt][1][r] * d.scale;
+        const long long o = ((long long)b * L + qi) * d.ld_dq + h * D + r32;
+        if (d.grad16) {
+          f16* dst = reinterpret_cast<f16*>(d.dq) + o;
+          dst[0] = f2h(dq[qt][0][r] * d.scale);
+          dst[32] = f2h(dq[qt][1][r] * d.scale);
+        } else {
+          float* dst = d.dq + o;
+          dst[0] = dq[qt][0][r] * d.scale;
+          dst[32] = dq[qt][1][r] * d.scale;
+        }
       }
     }
 }
@@ -759,6 +769,8 @@ extern "C" int lrce_mha_fwd(const LrceMhaDesc* d, void* stream) {
 extern "C" int lrce_mha_bwd(const LrceMhaDesc* d, void* stream) {
   if (int rc = check(d, true)) return rc;
   if (d->f16 && !short_self(d)) return lrce_fail(LRCE_E_ARG, "mha_bwd: f16 io only on the short self-attention path (Lq = Lk <= 64)");
+  if (d->grad16 && (!short_self(d) || !d->dkv1_store))
+    return lrce_fail(LRCE_E_ARG, "mha_bwd: fp16 gradients need the short self-attention path with dkv1_store");
   if (d->dkv1_store && !short_self(d) && (d->Lq != 1 || d->kv1_bdiv != 1 || !aligned_rows(d)))
     return lrce_fail(LRCE_E_ARG, "mha_bwd: dkv1_store needs the short self-attention path or the single-query path with kv1_bdiv == 1");
   MhaP p{*d, lrce_rng_offset()};

@@ -51,6 +51,7 @@ class GemmDesc(ctypes.Structure):
         ("workspace", ctypes.c_void_p), ("workspace_elems", ctypes.c_int64),
         ("drop_p", ctypes.c_float), ("drop_group", ctypes.c_int32), ("drop_seed", ctypes.c_uint64),
         ("f16", ctypes.c_int32), ("alpha_dev", ctypes.c_void_p), ("stride_bias", ctypes.c_int64),
+        ("stride_alpha", ctypes.c_int64),
     ]
 
 
@@ -67,7 +68,7 @@ class MhaDesc(ctypes.Structure):
         ("dout", ctypes.c_void_p), ("dq", ctypes.c_void_p), ("ld_dq", ctypes.c_int64),
         ("dk1", ctypes.c_void_p), ("dv1", ctypes.c_void_p), ("ld_dkv1", ctypes.c_int64), ("stride_dkv1_b", ctypes.c_int64),
         ("dk2", ctypes.c_void_p), ("dv2", ctypes.c_void_p), ("ld_dkv2", ctypes.c_int64), ("stride_dkv2_b", ctypes.c_int64),
-        ("f16", ctypes.c_int32), ("dkv1_store", ctypes.c_int32),
+        ("f16", ctypes.c_int32), ("dkv1_store", ctypes.c_int32), ("grad16", ctypes.c_int32),
     ]
 
 

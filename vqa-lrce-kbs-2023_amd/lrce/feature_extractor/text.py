@@ -129,39 +129,73 @@ class _EmbedFn(torch.autograd.Function):
         return (None,) * 6 + (dtok,) + (None,) * len(ctx.needs_input_grad[7:])
 
 
+class _Stack:
+    """Per-forward state the BERT layers share (one object per BertModel.forward):
+    fbuf [n_layers, ...] fp16 — each layer's 16-bit activations (xb, q, k, v, ctxt, h1b, g, pre: the
+      forward operands the backward reads), one allocation with a uniform per-layer stride;
+    dbuf [n_layers, ...] fp16 — each layer's scaled output gradients (do, dh1, da, dqkv: the dY operands of
+      its weight gradients), allocated by the first layer backward;
+    scales [n_layers, 2, 4] f32 — the layers' gradient-scale slots (BertModel._grad_scales);
+    flush_at — the index of the last layer whose backward runs (the lowest one with a trainable input or
+      parameter): its backward issues every layer's weight gradients (_flush_wgrads)."""
+
+    def __init__(self, bert, flat, rows, dev):
+        n = len(bert.encoder.layer)
+        self.bert, self.flat, self.rows, self.n = bert, flat, rows, n
+        self.fbuf = torch.empty(n, rows * _FWD_COLS, dtype=torch.float16, device=dev)
+        self.dbuf = None
+        self.scales = bert._grad_scales(dev)
+        self.flush_at = None
+        self.done = []          # layer indices whose backward has run (their dY in dbuf)
+
+    def fviews(self, i):
+        return _views(self.fbuf[i], self.rows, (HIDDEN,) * 6 + (INTER,) * 2)
+
+    def dviews(self, i):
+        if self.dbuf is None:
+            self.dbuf = torch.empty(self.n, self.rows * _BWD_COLS, dtype=torch.float16, device=self.fbuf.device)
+        return _views(self.dbuf[i], self.rows, (HIDDEN, INTER, HIDDEN, 3 * HIDDEN))
+
+
+_FWD_COLS = 6 * HIDDEN + 2 * INTER      # xb, q, k, v, ctxt, h1b | g, pre
+_BWD_COLS = HIDDEN + INTER + HIDDEN + 3 * HIDDEN   # do, dh1, da, dqkv
+
+
 class _LayerFn(torch.autograd.Function):
     """One post-norm BERT layer (HF BertLayer): x -> LN(x + drop(attn_out)) -> LN(. + drop(FFN)).
 
     Forward GEMM / attention operands are IEEE fp16, as under the reference's fp16 autocast
     (agent_oe.py:28; bf16 here would put BERT's rounding error at ~1e-2 of the MC / Count logits).
-    Every 16-bit activation the backward needs lives in ONE fp16 buffer, read by the fp16 backward
-    as it stands (scaled gradients: backward's docstring)."""
+    Every 16-bit activation the backward needs lives in the layer's slice of the stack's fp16 buffer,
+    read by the fp16 backward as it stands (scaled gradients: backward's docstring).  The layer input's
+    fp16 copy is written by the previous layer's last LayerNorm; the two residual-branch dropouts ride
+    the output-projection GEMMs' epilogues."""
 
     @staticmethod
-    def forward(ctx, x, mask, layer, flat, p, seed, B, L, *params):
+    def forward(ctx, x, mask, layer, flat, p, seed, B, L, st, i, *params):
         dev = x.device
         rows = B * L
         sa, ao, it, oo = layer.attention.self, layer.attention.output, layer.intermediate, layer.output
-        sizes = [rows * HIDDEN] * 6 + [rows * INTER] * 2
-        buf = torch.empty(sum(sizes), dtype=torch.float16, device=dev)
-        xb, q, k, v, ctxt, h1b, g, pre = _views(buf, rows)
+        xb, q, k, v, ctxt, h1b, g, pre = st.fviews(i)
         w = flat.w16h
-        K.cast_f16(x, xb)
+        if i == 0:
+            K.cast_f16(x, xb)
         _qkv(xb, sa, w, q, k, v, rows)
         lse = torch.empty(B, HEADS, L, device=dev)
         desc = K.mha_desc(q, L, k1=k, v1=v, lk1=L, ld_kv1=HIDDEN, stride_kv1_b=L * HIDDEN, key_mask=mask, out=ctxt,
                           lse=lse, B=B, H=HEADS, scale=0.125, drop_p=p, seed=seed)
         K.mha_fwd(desc, ctxt)
-        a = K.linear(ctxt, w(ao.dense.weight), ao.dense.bias, out_f32=True)
-        a2 = K.dropout(a, p, seed + 1, res=x)
+        drop1 = (p, seed + 1, 1) if p > 0 else None
+        a2 = K.linear(ctxt, w(ao.dense.weight), ao.dense.bias, out_f32=True, resid=x, drop=drop1)   # x + drop(a)
         h1, m1, r1 = K.layernorm(a2, ao.LayerNorm.weight, ao.LayerNorm.bias, EPS, out_f32=True, bf16_copy=h1b)
         K.linear(h1b, w(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre, out=g)
-        o = K.linear(g, w(oo.dense.weight), oo.dense.bias, out_f32=True)
-        o2 = K.dropout(o, p, seed + 2, res=h1)
-        out, m2, r2 = K.layernorm(o2, oo.LayerNorm.weight, oo.LayerNorm.bias, EPS, out_f32=True)
-        ctx.save = (buf, mask, lse, a2, m1, r1, o2, m2, r2)
+        drop2 = (p, seed + 2, 1) if p > 0 else None
+        o2 = K.linear(g, w(oo.dense.weight), oo.dense.bias, out_f32=True, resid=h1, drop=drop2)
+        nxt = st.fviews(i + 1)[0] if i + 1 < st.n else None   # the next layer's fp16 input
+        out, m2, r2 = K.layernorm(o2, oo.LayerNorm.weight, oo.LayerNorm.bias, EPS, out_f32=True, bf16_copy=nxt)
+        ctx.save = (mask, lse, a2, m1, r1, o2, m2, r2)
         ctx.desc = desc
-        ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L = layer, flat, p, seed, B, L
+        ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L, ctx.st, ctx.i = layer, flat, p, seed, B, L, st, i
         return out
 
     @staticmethod
@@ -171,13 +205,16 @@ class _LayerFn(torch.autograd.Function):
         scale (lrce_grad_scale, on the device), the fp16 operands carry it, and the GEMMs that leave the
         scaled domain (weight gradients, the dX GEMMs with an f32 residual) multiply by 1/S in their
         epilogue.  bf16 here left the top layers' query / key gradients ~0.2 off (near-uniform attention
-        rows make them small differences of large terms); fp16 puts them at the reference's own error."""
-        buf, mask, lse, a2, m1, r1, o2, m2, r2 = ctx.save
-        layer, flat, p, seed, B, L = ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L
+        rows make them small differences of large terms); fp16 puts them at the reference's own error.
+        Weight gradients are deferred: the scaled dY operands stay in the stack's dbuf and the last layer
+        backward issues all layers' weight gradients as six batched launches (_flush_wgrads)."""
+        mask, lse, a2, m1, r1, o2, m2, r2 = ctx.save
+        layer, flat, p, seed, B, L, st, i = ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L, ctx.st, ctx.i
         sa, ao, it, oo = layer.attention.self, layer.attention.output, layer.intermediate, layer.output
         rows = B * L
-        xb, q, k, v, ctxt, h1b, g, pre = _views(buf, rows)   # fp16, as the forward wrote them
-        sc = _grad_scales(layer, dout.device)                # (S, 1/S) of the FFN and attention gradients
+        xb, q, k, v, ctxt, h1b, g, pre = st.fviews(i)      # fp16, as the forward wrote them
+        do, dh1, da, dqkv = st.dviews(i)
+        sc = st.scales[i]                                   # (S, 1/S) of the FFN and attention gradients
         inv_f, inv_a = sc[0, 1:2], sc[1, 1:2]
         w = flat.w16h
         dout = dout.contiguous()
@@ -185,30 +222,61 @@ class _LayerFn(torch.autograd.Function):
         K.layernorm_bwd(dout, o2, m2, r2, oo.LayerNorm.weight, do2, dw=_g(flat, oo.LayerNorm.weight),
                         db=_g(flat, oo.LayerNorm.bias))
         K.grad_scale(do2, sc[0])
-        do = K.dropout_bwd_f16(do2, p, seed + 2, sc[0])                                   # S_f * d(o)
-        _wgrad(flat, oo.dense, do, g, inv_f)
-        dh1 = K.linear_dx(do, w(oo.dense.weight), out_f32=False, dgelu_pre=pre)           # S_f * d(pre)
-        _wgrad(flat, it.dense, dh1, h1b, inv_f)
+        K.dropout_bwd_f16(do2, p, seed + 2, sc[0], out=do)                                # S_f * d(o)
+        K.linear_dx(do, w(oo.dense.weight), out=dh1, out_f32=False, dgelu_pre=pre)        # S_f * d(pre)
         dh1x = K.linear_dx(dh1, w(it.dense.weight), resid=do2, alpha_dev=inv_f)
         da2 = torch.empty_like(a2)
         K.layernorm_bwd(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, dw=_g(flat, ao.LayerNorm.weight),
                         db=_g(flat, ao.LayerNorm.bias))
         K.grad_scale(da2, sc[1])
-        da = K.dropout_bwd_f16(da2, p, seed + 1, sc[1])                                   # S_a * d(a)
-        _wgrad(flat, ao.dense, da, ctxt, inv_a)
+        K.dropout_bwd_f16(da2, p, seed + 1, sc[1], out=da)                                # S_a * d(a)
         dctx = K.linear_dx(da, w(ao.dense.weight), out_f32=False)                         # S_a * d(ctx)
-        dqkv = torch.empty(3, rows, HIDDEN, device=dout.device)
-        K.mha_bwd(ctx.desc, dout=dctx, dq=dqkv[0], dk1=dqkv[1], dv1=dqkv[2], ld_dkv1=HIDDEN, stride_dkv1_b=L * HIDDEN,
+        # dq / dk / dv as fp16 column blocks of ONE [rows, 2304] operand, in the address order of the
+        # three weights (so the input gradient is one K = 2304 GEMM when they are contiguous)
+        cq, ck, cv = _qkv_cols(sa, w)
+        K.mha_bwd(ctx.desc, dout=dctx, dq=dqkv[:, cq:cq + HIDDEN], dk1=dqkv[:, ck:ck + HIDDEN],
+                  dv1=dqkv[:, cv:cv + HIDDEN], ld_dq=3 * HIDDEN, ld_dkv1=3 * HIDDEN, stride_dkv1_b=L * 3 * HIDDEN,
                   dkv1_store=True)
-        dqkv16 = torch.empty(3, rows, HIDDEN, dtype=torch.float16, device=dout.device)
-        K.cast_f16(dqkv, dqkv16)
-        _wgrad_qkv(flat, sa, dqkv16, xb, inv_a, rows)
-        dx = K.linear_dx(dqkv16[0], w(sa.query.weight), resid=da2, alpha_dev=inv_a)
-        K.linear_dx(dqkv16[1], w(sa.key.weight), out=dx, accumulate=True, alpha_dev=inv_a)
-        K.linear_dx(dqkv16[2], w(sa.value.weight), out=dx, accumulate=True, alpha_dev=inv_a)
+        dx = _qkv_dx(dqkv, sa, w, da2, inv_a, rows, (cq, ck, cv))
         ctx.save = ctx.desc = None
-        flat.notify(layer.parameters())
-        return (dx,) + (None,) * (7 + len(ctx.needs_input_grad[8:]))
+        st.done.append(i)
+        if i == st.flush_at:
+            _flush_wgrads(st)
+            for j in st.done:
+                flat.notify(st.bert.encoder.layer[j].parameters())
+        return (dx,) + (None,) * (9 + len(ctx.needs_input_grad[10:]))
+
+
+def _qkv_cols(sa, w):
+    """Column offsets of dq, dk, dv in the [rows, 3 * 768] gradient operand: the rank of each weight's
+    address among the three (the training layout stores them value, key, query)."""
+    ptrs = [w(l.weight).data_ptr() for l in (sa.query, sa.key, sa.value)]
+    order = sorted(range(3), key=lambda j: ptrs[j])
+    cols = [0, 0, 0]
+    for r, j in enumerate(order):
+        cols[j] = r * HIDDEN
+    return cols
+
+
+def _qkv_dx(dqkv, sa, w, resid, inv_scale, rows, cols):
+    """dX = dq Wq + dk Wk + dv Wv + resid (1/S in the epilogue): ONE K = 2304 GEMM over the stacked
+    weights when the three sit back to back in the fp16 shadow, else three accumulating GEMMs."""
+    ws = [w(l.weight) for l in (sa.query, sa.key, sa.value)]
+    lo = min(ws, key=lambda t: t.data_ptr())
+    if _QKV_DX_FUSED and sorted(t.data_ptr() - lo.data_ptr() for t in ws) == [0, 2 * HIDDEN * HIDDEN, 4 * HIDDEN * HIDDEN]:
+        wstack = torch.as_strided(lo, (3 * HIDDEN, HIDDEN), (HIDDEN, 1))
+        return K.linear_dx(dqkv, wstack, resid=resid, alpha_dev=inv_scale)
+    dx = None
+    for wt, c in zip(ws, cols):
+        a = dqkv[:, c:c + HIDDEN]
+        if dx is None:
+            dx = K.linear_dx(a, wt, resid=resid, alpha_dev=inv_scale)
+        else:
+            K.linear_dx(a, wt, out=dx, accumulate=True, alpha_dev=inv_scale)
+    return dx
+
+
+_QKV_DX_FUSED = os.environ.get("LRCE_BERT_QKV_DX_FUSED", "1") != "0"   # A/B knob
 
 
 def _qkv(xb, sa, w, q, k, v, rows):
@@ -236,31 +304,12 @@ def _qkv(xb, sa, w, q, k, v, rows):
 _QKV_BATCHED = os.environ.get("LRCE_BERT_QKV_BATCHED", "1") != "0"   # A/B knob
 
 
-def _grad_scales(layer, dev):
-    """The layer's two gradient-scale slots [2, 4] f32 (S, 1/S, two arrival words zeroed once: the
-    lrce_grad_scale contract), allocated on first use and kept (graph replays reuse them)."""
-    sc = getattr(layer, "_lrce_grad_scales", None)
-    if sc is None or sc.device != dev:
-        sc = torch.zeros(2, 4, device=dev)
-        object.__setattr__(layer, "_lrce_grad_scales", sc)
-    return sc
-
-
-def _views(buf, rows):
-    """xb, q, k, v, ctxt, h1b [rows, 768] and g, pre [rows, 3072] of one layer's 16-bit buffer."""
+def _views(buf, rows, widths):
+    """[rows, width] views of consecutive pieces of a flat 16-bit buffer."""
     out, o = [], 0
-    for cols in (HIDDEN,) * 6 + (INTER,) * 2:
+    for cols in widths:
         out.append(buf[o:o + rows * cols].view(rows, cols))
         o += rows * cols
-    return out
-
-
-def _grad16(d32, p, seed):
-    """bf16 copy of the dropout-backward of an f32 gradient (the operand of the backward GEMMs)."""
-    if p > 0:
-        return K.dropout_bwd(d32, p, seed, f32=False)
-    out = torch.empty(d32.shape, dtype=torch.bfloat16, device=d32.device)
-    K.cast_bf16(d32, out)
     return out
 
 
@@ -280,27 +329,62 @@ def _wgrad(flat, lin, dy, x16, inv_scale=None):
             gb.add_(t * inv_scale)
 
 
-def _wgrad_qkv(flat, sa, dqkv16, xb, inv_scale, rows):
-    """_wgrad of query / key / value as one batched launch when their weight and bias gradients sit at
-    one stride in the flat gradient buffer (A/B knob LRCE_BERT_QKV_WGRAD_BATCHED); else three."""
-    lins = (sa.query, sa.key, sa.value)
-    gws = [_g(flat, l.weight) for l in lins]
-    gbs = [_g(flat, l.bias) for l in lins]
-    if _QKV_WGRAD_BATCHED and all(t is not None for t in gws + gbs):
-        sw = [(gws[i + 1].data_ptr() - gws[i].data_ptr()) // 4 for i in range(2)]
-        sb = [(gbs[i + 1].data_ptr() - gbs[i].data_ptr()) // 4 for i in range(2)]
-        if sw[0] == sw[1] == sb[0] == sb[1] and sw[0] != 0:
-            i0, d = (0, 1) if sw[0] > 0 else (2, -1)     # batch order: ascending gradient addresses
-            K.gemm(dqkv16[i0], xb, gws[i0], HIDDEN, HIDDEN, rows, a_kmajor=False, b_kmajor=False, lda=HIDDEN,
-                   ldb=HIDDEN, ldc=HIDDEN, flags=N.EPI_ACCUM | N.EPI_BIAS_GRAD, bias=gbs[i0], batch=3,
-                   stride_a=d * rows * HIDDEN, stride_c=abs(sw[0]), stride_bias=abs(sb[0]), f16=True,
-                   alpha_dev=inv_scale)
-            return
-    for i, lin in enumerate(lins):
-        _wgrad(flat, lin, dqkv16[i], xb, inv_scale)
+def _wgrad_items(st, i):
+    """The six weight-gradient products of layer i: (linear, dY view, X view, scale slot)."""
+    layer = st.bert.encoder.layer[i]
+    sa, ao, it, oo = layer.attention.self, layer.attention.output, layer.intermediate, layer.output
+    xb, q, k, v, ctxt, h1b, g, pre = st.fviews(i)
+    do, dh1, da, dqkv = st.dviews(i)
+    cq, ck, cv = _qkv_cols(sa, st.flat.w16h)
+    return [(oo.dense, do, g, 0), (it.dense, dh1, h1b, 0), (ao.dense, da, ctxt, 1),
+            (sa.query, dqkv[:, cq:cq + HIDDEN], xb, 1), (sa.key, dqkv[:, ck:ck + HIDDEN], xb, 1),
+            (sa.value, dqkv[:, cv:cv + HIDDEN], xb, 1)]
 
 
-_QKV_WGRAD_BATCHED = os.environ.get("LRCE_BERT_QKV_WGRAD_BATCHED", "1") != "0"   # A/B knob
+def _flush_wgrads(st):
+    """Every layer's deferred weight + bias gradients: for each of the six linears ONE batched launch
+    over the layers (dW_l += (1/S_l) dY_l^T X_l, db_l += (1/S_l) colsum(dY_l), l = the layers whose
+    backward ran), when their gradients, dY / X operands and scale slots sit at uniform strides (the
+    flat store lays every layer out alike); else one launch per layer.  48 launches of 60-432
+    workgroups on the serial text branch become 6 of 1 000+."""
+    flat = st.flat
+    layers = sorted(st.done)
+    items = {i: _wgrad_items(st, i) for i in layers}
+    for j in range(6):
+        per = [(i,) + items[i][j] for i in layers]          # (layer, lin, dy, x, slot)
+        gws = [_g(flat, lin.weight) for _, lin, _, _, _ in per]
+        gbs = [_g(flat, lin.bias) for _, lin, _, _, _ in per]
+        if _WGRAD_BATCHED and len(per) > 1 and all(t is not None for t in gws + gbs):
+            order = sorted(range(len(per)), key=lambda t: gws[t].data_ptr())
+            seq = [per[t] for t in order]
+            gw, gb = [gws[t] for t in order], [gbs[t] for t in order]
+
+            s_w, s_b = _uniform_stride(gw, 4), _uniform_stride(gb, 4)
+            s_a, s_x = _uniform_stride([e[2] for e in seq], 2), _uniform_stride([e[3] for e in seq], 2)
+            slots = [st.scales[e[0], e[4], 1:2] for e in seq]
+            s_al = _uniform_stride(slots, 4)
+            if None not in (s_w, s_b, s_a, s_x, s_al) and s_w > 0 and s_b > 0:
+                _, lin, dy, x, _ = seq[0]
+                Nn, Kk = lin.weight.shape
+                K.gemm(dy, x, gw[0], Nn, Kk, st.rows, a_kmajor=False, b_kmajor=False, lda=dy.stride(0),
+                       ldb=x.stride(0), ldc=Kk, flags=N.EPI_ACCUM | N.EPI_BIAS_GRAD, bias=gb[0], batch=len(seq),
+                       stride_a=s_a, stride_b=s_x, stride_c=s_w, stride_bias=s_b, f16=True, alpha_dev=slots[0],
+                       stride_alpha=s_al)
+                continue
+        for i, lin, dy, x, slot in per:
+            _wgrad(flat, lin, dy, x, st.scales[i, slot, 1:2])
+
+
+_WGRAD_BATCHED = os.environ.get("LRCE_BERT_WGRAD_BATCHED", "1") != "0"   # A/B knob
+
+
+def _uniform_stride(ts, es):
+    """The common address step of consecutive tensors in elements of es bytes (None if not uniform)."""
+    ds = {b.data_ptr() - a.data_ptr() for a, b in zip(ts, ts[1:])}
+    if len(ds) != 1:
+        return None
+    d = ds.pop()
+    return d // es if d % es == 0 else None
 
 
 class BertModel(nn.Module):
@@ -312,6 +396,15 @@ class BertModel(nn.Module):
         self.hidden_dropout, self.attention_dropout = hidden_dropout, attention_dropout
         if hidden_dropout != attention_dropout:
             raise ValueError("bert-base uses one dropout rate (0.1) for hidden states and attention probs")
+
+    def _grad_scales(self, dev):
+        """The layers' gradient-scale slots [n_layers, 2, 4] f32 (S, 1/S, two arrival words zeroed once:
+        the lrce_grad_scale contract), allocated on first use and kept (graph replays reuse them)."""
+        sc = getattr(self, "_lrce_grad_scales", None)
+        if sc is None or sc.device != dev:
+            sc = torch.zeros(len(self.encoder.layer), 2, 4, device=dev)
+            object.__setattr__(self, "_lrce_grad_scales", sc)
+        return sc
 
     def lrce_f16_params(self):
         """Parameters whose fp16 shadow the forward reads (the encoder linears; runtime.bind)."""
@@ -328,8 +421,12 @@ class BertModel(nn.Module):
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
         anchor = [t for t in self.embeddings.parameters()]
         x = _EmbedFn.apply(ids, types, self.embeddings, flat, p, seed, join_token, *anchor)
+        st = _Stack(self, flat, B * L, dev)
         for i, layer in enumerate(self.encoder.layer):
-            x = _LayerFn.apply(x, mask, layer, flat, p, seed + 16 * (i + 1), B, L, *layer.parameters())
+            params = list(layer.parameters())
+            if st.flush_at is None and torch.is_grad_enabled() and (x.requires_grad or any(q.requires_grad for q in params)):
+                st.flush_at = i      # the last layer backward to run issues the deferred weight gradients
+            x = _LayerFn.apply(x, mask, layer, flat, p, seed + 16 * (i + 1), B, L, st, i, *params)
         return x.view(B, L, HIDDEN)
 
 

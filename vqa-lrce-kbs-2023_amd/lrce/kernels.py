@@ -91,6 +91,12 @@ def _timed(name, stream_tensor, fn, flops=0.0, nbytes=0.0, key=None):
     return kt.wrap(name, stream_tensor, fn, flops, nbytes, key)
 
 
+def _ld(t):
+    """Row pitch (elements) of a row-major matrix operand: a column block of a wider matrix has the
+    wider matrix's pitch."""
+    return t.stride(-2) if t.dim() >= 2 else t.shape[-1]
+
+
 def _chk(t, dtype=None, name="tensor"):
     if t is None:
         return
@@ -104,12 +110,12 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
          aux=None, ld_aux=0, aux_out=None, ld_aux_out=0, a_map=None, c_map=None, alpha=1.0, split_k=1,
          scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, a_row_scale=None, a_rows_per_scale=1,
          batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None, drop=None, f16=False, ln=None, alpha_dev=None,
-         stride_bias=0):
+         stride_bias=0, stride_alpha=0):
     """C (+)= epi(alpha * A(m,k) B(n,k)) — see include/lrce_hip.h LrceGemmDesc.  drop = (p, seed, group):
     nn.Dropout fused into the epilogue (exact-f32 skinny path; same mask as dropout()).  f16: every
     16-bit tensor (A, B, 16-bit C, aux_out) is torch.float16 (the BERT forward).  ln: a LayerNorm
     prologue on A (ln_fwd_prologue / ln_bwd_prologue -> lrce_gemm_ln).  alpha_dev: a device f32 read
-    as alpha (the inverse gradient scale of grad_scale())."""
+    as alpha (the inverse gradient scale of grad_scale()); stride_alpha: its batch stride (floats)."""
     _chk(a, None, "A"); _chk(b, None, "B"); _chk(c, None, "C")
     a_f32 = a.dtype == F32
     b_f32 = b.dtype == F32
@@ -128,6 +134,7 @@ def gemm(a, b, c, m, n, k, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     d.lda, d.ldb, d.ldc = lda, ldb, ldc
     d.stride_a, d.stride_b, d.stride_c = stride_a, stride_b, stride_c
     d.stride_bias = stride_bias
+    d.stride_alpha = stride_alpha
     d.m, d.n, d.k, d.batch = m, n, k, batch
     d.a_kmajor, d.b_kmajor, d.a_f32 = int(a_kmajor), int(b_kmajor), int(a_f32)
     d.flags, d.split_k = flags, split_k
@@ -198,14 +205,23 @@ def _skinny_drop_ok(x, w, M, a_map=None):
             and w.data_ptr() % (16 if w.dtype == F32 else 8) == 0)
 
 
+def _glds_drop_ok(x, w, drop, a_map, c_map):
+    """Does lrce_gemm take this 16-bit linear's fused dropout on the LDS-DMA path (element-wise mask,
+    no row maps)?  Mirrors the launcher's test."""
+    return (x.dtype in (F16, BF16) and w.dtype == x.dtype and int(drop[2]) == 1 and a_map is None and c_map is None
+            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and x.shape[-1] % 8 == 0)
+
+
 def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None, resid=None, c_map=None,
            a_map=None, rows=None, scale_cols=0, scale_val=1.0, row_scale=None, rows_per_scale=1, bf16_shadow=None,
            drop=None, ln=None):
-    f16 = x.dtype == F16
     """y = x W^T (+b) [gelu] [*row_scale] [dropout] [+resid]; x [M,K] bf16/f32, W [N,K] bf16 (or f32:
-    exact path).  drop = (p, seed, group): fused into the skinny epilogue, else a dropout launch."""
+    exact path).  drop = (p, seed, group): fused into the epilogue (exact-f32 skinny path, or the 16-bit
+    LDS-DMA path with group 1), else a dropout launch."""
+    f16 = x.dtype == F16
     M = rows if rows is not None else x.shape[0]
-    if drop is not None and drop[0] > 0 and ln is None and not (_skinny_drop_ok(x, w, M, a_map) and c_map is None):
+    if drop is not None and drop[0] > 0 and ln is None and not (_skinny_drop_ok(x, w, M, a_map) and c_map is None) \
+            and not _glds_drop_ok(x, w, drop, a_map, c_map):
         y = linear(x, w, bias, out=out if resid is None else None, out_f32=out_f32, gelu=gelu, pre_out=pre_out,
                    c_map=c_map, a_map=a_map, rows=rows, scale_cols=scale_cols, scale_val=scale_val,
                    row_scale=row_scale, rows_per_scale=rows_per_scale)
@@ -261,7 +277,7 @@ def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows
         out = torch.empty((M, K), dtype=F32 if out_f32 else (F16 if f16 else BF16), device=dy.device)
     if out.dtype == F32:
         flags |= N.EPI_ACCUM if accumulate else N.EPI_OUT_F32
-    gemm(dy, w, out, M, K, Nn, a_kmajor=True, b_kmajor=False, lda=dy.shape[-1], ldb=K, flags=flags,
+    gemm(dy, w, out, M, K, Nn, a_kmajor=True, b_kmajor=False, lda=_ld(dy), ldb=K, flags=flags,
          aux=dgelu_pre if dgelu_pre is not None else resid, ld_aux=K, a_map=a_map, a_row_scale=a_row_scale,
          a_rows_per_scale=a_rows_per_scale, drop=drop, ln=ln, f16=f16, alpha_dev=alpha_dev)
     return out
@@ -283,7 +299,7 @@ def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_
     f16 = dy.dtype == F16 and x.dtype == F16
     if split > 1 and ((dy.dtype == BF16 and x.dtype == BF16) or f16):
         ws = torch.empty(split * Nn * K, dtype=F32, device=dw.device)
-    gemm(dy, x, dw, Nn, K, M, a_kmajor=False, b_kmajor=False, lda=dy.shape[-1], ldb=x.shape[-1], ldc=K,
+    gemm(dy, x, dw, Nn, K, M, a_kmajor=False, b_kmajor=False, lda=_ld(dy), ldb=_ld(x), ldc=K,
          flags=flags, bias=bias_grad, a_map=a_map, split_k=split, a_row_scale=a_row_scale,
          a_rows_per_scale=a_rows_per_scale, workspace=ws, f16=f16, alpha_dev=alpha_dev)
 
@@ -589,8 +605,12 @@ def mha_rebind(desc, *, q, k1, v1, out):
 
 def mha_bwd(desc, *, dout, dq, dk1, dv1, ld_dkv1, stride_dkv1_b, dk2=None, dv2=None, ld_dkv2=0, stride_dkv2_b=0,
             ld_dq=None, dkv1_store=False):
-    """dkv1_store: the first segment's dK / dV rows are written, not accumulated (LrceMhaDesc)."""
+    """dkv1_store: the first segment's dK / dV rows are written, not accumulated (LrceMhaDesc).  fp16
+    dq / dk1 / dv1 (with dkv1_store, the short self-attention path): the gradients are stored as fp16."""
     desc.dkv1_store = int(dkv1_store)
+    desc.grad16 = int(dq.dtype == F16)
+    if desc.grad16 and (dk1.dtype != F16 or dv1.dtype != F16 or not dkv1_store):
+        raise N.NativeError("mha_bwd: fp16 gradients need fp16 dq / dk1 / dv1 and dkv1_store")
     desc.dout, desc.dq = ptr(dout), ptr(dq)
     desc.ld_dq = ld_dq if ld_dq is not None else desc.H * desc.d
     desc.dk1, desc.dv1, desc.ld_dkv1, desc.stride_dkv1_b = ptr(dk1), ptr(dv1), ld_dkv1, stride_dkv1_b
