@@ -1034,3 +1034,58 @@ def test_torch_library_autograd():
     (F.layer_norm(xr, (256,), gr, br, 1e-5) * gy).sum().backward()
     for got, ref in ((xf.grad, xr.grad), (gm.grad, gr.grad), (be.grad, br.grad)):
         assert rel(got, ref) < 1e-4
+
+
+def test_torch_library_patch_embed():
+    """torch.ops.lrce.patch_embed (PatchEmbed3D + Normalize, video_swin_ori.py:464-482, video.py:35)
+    vs the oracle (conv3d + LayerNorm on the normalized, T-padded clip) and its autograd w.r.t. the
+    conv and LayerNorm parameters vs fp32 torch autograd on the same bf16-rounded operands."""
+    K()
+    from lrce import ops  # noqa: F401
+    torch.manual_seed(7)
+    B, T, H, W, E = 2, 5, 32, 48, 128
+    clips = torch.rand(B, 3, T, H, W, device=dev)
+    pw = (torch.randn(E, 3, 2, 4, 4, device=dev) * 0.1).requires_grad_(True)
+    pb = (torch.randn(E, device=dev) * 0.1).requires_grad_(True)
+    lw = (torch.rand(E, device=dev) + 0.5).requires_grad_(True)
+    lb = (torch.randn(E, device=dev) * 0.1).requires_grad_(True)
+    x, patches, y, mean, rstd = torch.ops.lrce.patch_embed(clips, pw, pb, lw, lb, True)
+    D = (T + 1) // 2
+    assert x.shape == (B * D * (H // 4) * (W // 4), E) and patches.dtype == torch.bfloat16
+    sd = {"pe.proj.weight": pw.detach().cpu(), "pe.proj.bias": pb.detach().cpu(), "pe.norm.weight": lw.detach().cpu(),
+          "pe.norm.bias": lb.detach().cpu()}
+    xn = O.normalize_clip(clips.cpu().transpose(1, 2)).transpose(1, 2)
+    ref = O.patch_embed(xn, sd, "pe.").reshape(-1, E)
+    assert rel(x.cpu(), ref) < 1e-2
+    gx = torch.randn(x.shape, device=dev)
+    (x * gx).sum().backward()
+    # the same math in fp32 on the bf16-rounded im2col operands and weight
+    wr, br, lwr, lbr = (t.detach().clone().requires_grad_(True) for t in (pw, pb, lw, lb))
+    yr = patches.float() @ wr.reshape(E, 96).to(torch.bfloat16).float().t() + br
+    (F.layer_norm(yr, (E,), lwr, lbr, 1e-5) * gx).sum().backward()
+    for got, want in ((pw.grad, wr.grad), (pb.grad, br.grad), (lw.grad, lwr.grad), (lb.grad, lbr.grad)):
+        assert got is not None and rel(got, want) < 2e-2, (rel(got, want), want.shape)
+
+
+def test_torch_library_decoder_recurrent():
+    """torch.ops.lrce.decoder_recurrent (FusionTransformer.forward, fusionv3.py:27-51: the recurrent
+    12-layer decoder over S steps through the native decoder kernels) vs the oracle's
+    fusion_transformer on the same weights and memory; text None: FusionVideo (fusionv3.py:70-88)."""
+    K()
+    from lrce import ops  # noqa: F401
+    from lrce.models.fusionv3 import FusionTransformer
+    from oracle import weights as W
+    torch.manual_seed(9)
+    ft = FusionTransformer(768, 0.0)
+    sd = W.fill_state_dict({"fusion_model.fusion_transformer." + k: v for k, v in ft.state_dict().items()}, 0)
+    ft.load_state_dict({k[len("fusion_model.fusion_transformer."):]: v for k, v in sd.items()})
+    params = [p.detach().to(dev) for p in ft.parameters()]
+    B, S, L = 3, 2, 21
+    video = torch.randn(B, S, 150, 768) * 0.5
+    text = torch.randn(B, L, 768) * 0.5
+    s = torch.ops.lrce.decoder_recurrent(video.to(dev), text.to(dev), params)
+    ref = O.fusion_transformer(video, text, sd).reshape(B, 768)
+    assert s.shape == (B, 768) and rel(s.cpu(), ref) < 1e-2, rel(s.cpu(), ref)
+    sv = torch.ops.lrce.decoder_recurrent(video.to(dev), None, params)
+    refv = O.fusion_video(video, sd).reshape(B, 768)
+    assert rel(sv.cpu(), refv) < 1e-2, rel(sv.cpu(), refv)

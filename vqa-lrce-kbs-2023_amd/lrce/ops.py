@@ -23,10 +23,19 @@ Ops (reference modules they replace):
                                                   gradient, lrce_wattn_dbias) and the qkv Linear's
                                                   dX / dW / db GEMMs
 
-Autograd (torch.library.register_autograd): linear, layer_norm and window_attention are
+  patch_embed(clips, proj_w, proj_b, ln_w, ln_b, normalize) -> (x, patches, y, mean, rstd)
+                                                  PatchEmbed3D (+ Normalize)  video_swin_ori.py:464-482,
+                                                  video.py:35: im2col -> K = 96 GEMM -> LayerNorm
+  decoder_recurrent(video, text, params) -> s     FusionTransformer.forward   fusionv3.py:27-51
+                                                  (the recurrent 12-layer decoder over S steps, eval
+                                                  mode; text None: FusionVideo, fusionv3.py:70-88)
+
+Autograd (torch.library.register_autograd): linear, layer_norm, window_attention and patch_embed are
 differentiable through the same native kernels (linear: dX / dW GEMMs + fused bias gradient;
 layer_norm: lrce_layernorm_bwd w.r.t. y; window_attention: window_attention_backward w.r.t. out —
-its qkv / lse outputs are saved activations, marked non-differentiable).
+its qkv / lse outputs are saved activations, marked non-differentiable; patch_embed: w.r.t. the conv
+and LayerNorm parameters, the clips are data).  decoder_recurrent is a forward (inference) op; the
+model's training path differentiates the decoder as one autograd node (lrce/models/fusionv3.py).
 """
 from typing import List, Optional, Tuple
 
@@ -220,6 +229,113 @@ def _wattn_backward(ctx, dout, dqkv, dlse):
 window_attention.register_autograd(_wattn_backward, setup_context=_wattn_setup)
 
 
+@torch.library.custom_op("lrce::patch_embed", mutates_args=())
+def patch_embed(clips: Tensor, proj_w: Tensor, proj_b: Tensor, ln_w: Tensor, ln_b: Tensor,
+                normalize: bool = False) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """PatchEmbed3D (video_swin_ori.py:464-482): clips (B, 3, T, H, W) f32 (normalize=True applies
+    video.py:35's ImageNet Normalize first), T zero-padded to the 2-frame patch, H and W multiples of
+    4; conv3d k = s = (2, 4, 4) as im2col (lrce_patch_im2col, bf16 [M, 96]) -> K = 96 GEMM + bias ->
+    LayerNorm(E, 1e-5).  Returns (x f32 [B * D' * H' * W', E] channels-last tokens, and the saved
+    activations patches bf16 [M, 96], y f32 [M, E] (pre-norm), mean, rstd)."""
+    B, C, T, H, W = clips.shape
+    if C != 3 or H % 4 or W % 4:
+        raise ValueError(f"patch_embed: (B, 3, T, H, W) with H, W multiples of 4, got {tuple(clips.shape)}")
+    E = proj_w.shape[0]
+    M = B * ((T + 1) // 2) * (H // 4) * (W // 4)
+    patches = torch.empty(M, 96, dtype=torch.bfloat16, device=clips.device)
+    K.patch_im2col(clips.contiguous(), patches, layout="BCTHW", normalize=normalize)
+    w16 = proj_w.reshape(E, 96).to(torch.bfloat16).contiguous()
+    y = K.linear(patches, w16, proj_b.float().contiguous(), out_f32=True)
+    x, mean, rstd = K.layernorm(y, ln_w.float().contiguous(), ln_b.float().contiguous(), 1e-5, out_f32=True)
+    return x, patches, y, mean, rstd
+
+
+@patch_embed.register_fake
+def _(clips, proj_w, proj_b, ln_w, ln_b, normalize=False):
+    B, _, T, H, W = clips.shape
+    E = proj_w.shape[0]
+    M = B * ((T + 1) // 2) * (H // 4) * (W // 4)
+    f = torch.float32
+    return (clips.new_empty((M, E), dtype=f), clips.new_empty((M, 96), dtype=torch.bfloat16),
+            clips.new_empty((M, E), dtype=f), clips.new_empty((M,), dtype=f), clips.new_empty((M,), dtype=f))
+
+
+def _pe_setup(ctx, inputs, output):
+    clips, proj_w, proj_b, ln_w, ln_b, normalize = inputs
+    x, patches, y, mean, rstd = output
+    ctx.save_for_backward(patches, y, mean, rstd, proj_w, ln_w)
+    ctx.mark_non_differentiable(patches, y, mean, rstd)
+
+
+def _pe_backward(ctx, dx, dpatches, dy_, dmean, drstd):
+    """w.r.t. x: the LayerNorm backward writes dy only as the bf16 operand of the conv-weight GEMM,
+    whose epilogue sums the bias gradient (as _PatchEmbedFn.backward)."""
+    patches, y, mean, rstd, proj_w, ln_w = ctx.saved_tensors
+    E = proj_w.shape[0]
+    dev = y.device
+    dy16 = torch.empty(y.shape, dtype=torch.bfloat16, device=dev)
+    dlw = torch.zeros(E, dtype=torch.float32, device=dev)
+    dlb = torch.zeros(E, dtype=torch.float32, device=dev)
+    K.layernorm_bwd(dx.float().contiguous(), y, mean, rstd, ln_w.float().contiguous(), None, dx16=dy16, dw=dlw, db=dlb)
+    dw = torch.zeros(E, 96, dtype=torch.float32, device=dev)
+    db = torch.zeros(E, dtype=torch.float32, device=dev)
+    K.linear_dw(dy16, patches, dw, bias_grad=db)
+    return None, dw.view(proj_w.shape).to(proj_w.dtype), db, dlw, dlb, None
+
+
+patch_embed.register_autograd(_pe_backward, setup_context=_pe_setup)
+
+
+_DEC = {}
+
+
+def _decoder_module(device, n_params):
+    """One FusionTransformer per device whose flat store the op's parameters are copied into."""
+    m = _DEC.get(device)
+    if m is None:
+        from .models.fusionv3 import FusionTransformer
+        from .runtime import prepare
+        m = FusionTransformer(768, 0.0).to(device).eval()
+        prepare(m)
+        _DEC[device] = m
+    if len(list(m.parameters())) != n_params:
+        raise ValueError(f"decoder_recurrent: {n_params} parameters given, FusionTransformer has "
+                         f"{len(list(m.parameters()))}")
+    return m
+
+
+@torch.library.custom_op("lrce::decoder_recurrent", mutates_args=())
+def decoder_recurrent(video: Tensor, text: Optional[Tensor], params: List[Tensor]) -> Tensor:
+    """FusionTransformer.forward (fusionv3.py:27-51), eval mode: s <- summarization token; for each of
+    the S steps, memory = [video[:, i] (150 tokens); text (L + 1 tokens)], s <- LN(s + Dec12(s,
+    memory)) through the native recurrent decoder (csrc/decoder.hip fused attention blocks + the
+    exact-f32 FFN GEMMs).  video (B, S, 150, 768) f32, text (B, L + 1, 768) f32 or None (FusionVideo,
+    fusionv3.py:70-88); params: FusionTransformer.parameters() in module order (the 12 decoder layers,
+    fusion_layer_norm, summarization_token).  Returns s (B, 768) f32."""
+    dev = video.device
+    m = _decoder_module(dev, len(params))
+    from .runtime import ensure
+    flat = ensure(m)
+    with torch.no_grad():
+        for dst, src in zip(m.parameters(), params):
+            if dst.shape != src.shape:
+                raise ValueError(f"decoder_recurrent: parameter shape {tuple(src.shape)} != {tuple(dst.shape)}")
+            dst.copy_(src)
+        flat.masters_written()
+        B = video.shape[0]
+        v = video.contiguous().float()
+        v16 = v.to(torch.bfloat16)
+        t = text.contiguous().float() if text is not None else None
+        t16 = t.to(torch.bfloat16) if t is not None else None
+        return m.run(v, v16, t, t16, B, 1).reshape(B, 768).clone()
+
+
+@decoder_recurrent.register_fake
+def _(video, text, params):
+    return video.new_empty((video.shape[0], 768), dtype=torch.float32)
+
+
 def registered() -> List[str]:
     """The lrce operators the dispatcher knows."""
-    return ["linear", "linear_dx", "linear_dw_", "layer_norm", "window_attention", "window_attention_backward"]
+    return ["linear", "linear_dx", "linear_dw_", "layer_norm", "window_attention", "window_attention_backward",
+            "patch_embed", "decoder_recurrent"]
