@@ -218,3 +218,14 @@ def test_config1_cpu_eval_plumbing(monkeypatch):
     assert agent.last_metric_val == pytest.approx(correct / total)
     nz = [x for x in losses if x != 0]
     assert agent.last_loss == pytest.approx(sum(nz) / len(nz), rel=1e-5)
+
+
+def test_graph_capture_refuses_the_crashing_hip_debug_queue_knob(monkeypatch):
+    """DEBUG_HIP_FORCE_GRAPH_QUEUES=8 crashed the HIP runtime at the first captured step (round-4
+    A/B "fq8", reproduced in round 5): the capture refuses it with an explanation."""
+    from lrce import graph
+    monkeypatch.setenv("DEBUG_HIP_FORCE_GRAPH_QUEUES", "8")
+    with pytest.raises(RuntimeError, match="DEBUG_HIP_FORCE_GRAPH_QUEUES"):
+        graph._check_runtime_env()
+    monkeypatch.setenv("DEBUG_HIP_FORCE_GRAPH_QUEUES", "0")
+    graph._check_runtime_env()

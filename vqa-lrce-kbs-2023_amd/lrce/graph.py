@@ -9,12 +9,28 @@ a captured add (kernels.rng_advance), DropPath uses torch's graph-aware Philox, 
 bias corrections read a device step counter and its learning rates a device table refreshed before
 each replay.  Inputs are static buffers: TrainStepGraph copies each batch into them.
 """
+import os
+
 import torch
+
+# HIP runtime debug variable that hands a graph's parallel branches to N extra queues.  With it set to
+# 8 the ROCm 7 runtime crashed in the first captured training step of this model (round-4 A/B variant
+# "fq8": core dump at the capture; reproduced once in round 5: segmentation fault), so the capture
+# refuses it with an explanation instead of reaching that crash.
+_FORCE_GRAPH_QUEUES = "DEBUG_HIP_FORCE_GRAPH_QUEUES"
+
+
+def _check_runtime_env():
+    v = os.environ.get(_FORCE_GRAPH_QUEUES, "")
+    if v not in ("", "0"):
+        raise RuntimeError(f"{_FORCE_GRAPH_QUEUES}={v} is set: the HIP runtime crashes replaying this model's "
+                           f"captured training step under that debug setting (DESIGN.md §8); unset it")
 
 
 class CapturedStep:
     def __init__(self, fn, warmup=2, pool=None):
         """fn(): one training step on the current stream, returning a tensor (e.g. the loss)."""
+        _check_runtime_env()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -128,6 +144,7 @@ class TrainStepGraph:
         return st.out
 
     def _capture(self, st):
+        _check_runtime_env()
         torch.cuda.synchronize()
         self.optim._sync_lrs()          # no host->device copy may land inside the capture
         steps = self.optim.step_count   # the host-side count of a captured step() is not a real step
