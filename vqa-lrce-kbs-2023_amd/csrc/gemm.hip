@@ -190,6 +190,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 }
 
 // Fused epilogue for one element (row = c_map-resolved output row).
+template <bool DROP = false>
 __device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row, int m, int nn, bool first, float rs,
                                           char* cbase) {
   const int fl = p.flags;
@@ -201,7 +202,7 @@ __device__ __forceinline__ void epilogue1(const GemmP& p, float x, long long row
   }
   if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(from16r(static_cast<const bf16*>(p.aux)[row * p.ld_aux + nn], p.f16));
   x *= rs;
-  if (p.drop_p > 0.f)
+  if (DROP)
     x = lrce_uniform(lrce_seed(p.drop_seed, p.rng_off), (unsigned long long)m * p.n + nn) >= p.drop_p ? x / (1.0f - p.drop_p) : 0.f;
   if ((fl & LRCE_EPI_RESID) && first) x += static_cast<const float*>(p.aux)[row * p.ld_aux + nn];
   if (fl & LRCE_EPI_ATOMIC) {
@@ -232,7 +233,7 @@ struct EpiPf {
   const float4* bias;    // 2 float4 of bias for this chunk, or null
 };
 
-template <bool F16>
+template <bool F16, bool DROP = false>
 __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int n, int sk, char* cbase,
                                           const bf16x8* dg_pf = nullptr, const float4* rs_pf = nullptr,
                                           const EpiPf* pf = nullptr, const float4* acc_pf = nullptr) {
@@ -284,7 +285,7 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= rs;
     }
-    if (p.drop_p > 0.f) {   // lrce_dropout's bits: v / (1 - p) where kept (n % 8 == 0 on this path)
+    if (DROP) {   // lrce_dropout's bits: v / (1 - p) where kept (n % 8 == 0 on this path)
       const uint64_t sd = lrce_seed(p.drop_seed, p.rng_off);
       const unsigned long long i4 = ((unsigned long long)m * p.n + n) >> 2;
       const float4 u0 = lrce_uniform4(sd, i4), u1 = lrce_uniform4(sd, i4 + 1);
@@ -330,7 +331,7 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, float v[8], int m, int
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     if (n + e >= p.n) break;
-    epilogue1(p, v[e], row, m, n + e, first, rs, cbase);
+    epilogue1<DROP>(p, v[e], row, m, n + e, first, rs, cbase);
   }
 }
 
@@ -584,7 +585,9 @@ constexpr int PF_KT = 8;
 constexpr int pf_dg_slots(int im) { return im; }
 constexpr int pf_rs_slots(int im) { return im <= 4 ? im : 1; }
 
-template <int TBM, int TBN, bool A_KM, bool B_KM, bool F16 = false, int NS = 2>
+// DROP: the fused-dropout epilogue (a separate instantiation: the branch in every kernel measured
+// 14-17 % slower tall-tile GEMMs through changed code generation)
+template <int TBM, int TBN, bool A_KM, bool B_KM, bool F16 = false, int NS = 2, bool DROP = false>
 __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   constexpr int WM = TBM / 2, WN = TBN / 2;      // per-wave tile
   constexpr int IM = WM / 16, JN = WN / 16;      // 16x16 accumulator blocks per wave
@@ -958,7 +961,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
                              : late_rs ? xq[decltype(iic)::value][h] : nullptr;
           const float4* ac = late_acc ? xq[decltype(iic)::value][h] : nullptr;
           const EpiPf pf{1, al_pf, row_pf[i], rsc_pf[i], have_bias ? bias_pf[h] : nullptr};
-          epilogue8<F16>(p, v, m, ncol + 8 * h, sk, cbase, dg, rs, &pf, ac);
+          epilogue8<F16, DROP>(p, v, m, ncol + 8 * h, sk, cbase, dg, rs, &pf, ac);
         }
       }
     });
@@ -1138,7 +1141,8 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   if (glds_ok(d)) {
     // 128x128 tiles when they give every CU work; 64x64 otherwise (small-M / small-N problems)
     const int t128 = p.tiles_m * p.tiles_n * d->batch * split;
-    const bool small = g_gemm_tile == 64 || (g_gemm_tile == 0 && t128 < 256);
+    // (fused dropout: 64x64 tiles only — the one instantiation family that carries that epilogue)
+    const bool small = g_gemm_tile == 64 || (g_gemm_tile == 0 && t128 < 256) || p.drop_p > 0.f;
     // Taller tiles (K-major A only): 160 or 192 rows x 128 do 1.25x / 1.5x the work of a 128x128
     // tile, so they win when the 128-row tile count overshoots a round of the 2-blocks-per-CU grid.
     // Pick the height minimising rounds x rows (e.g. M 17 640, N 512: 552 -> 444 tiles in ONE round
@@ -1202,6 +1206,14 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     static const int g_small_ns = getenv("LRCE_GEMM_SMALL_NS") ? atoi(getenv("LRCE_GEMM_SMALL_NS")) : 4;   // A/B knob
     auto launch_small = [&](auto nsc) {
       constexpr int S = decltype(nsc)::value;
+      if (p.drop_p > 0.f) {
+        switch (gk) {
+          case 32 + 7: gemm_glds_kernel<64, 64, true, true, true, S, true><<<grid, NT, 0, s>>>(p); break;
+          case 7: gemm_glds_kernel<64, 64, true, true, false, S, true><<<grid, NT, 0, s>>>(p); break;
+          default: return lrce_fail(LRCE_E_ARG, "gemm: fused dropout needs K-major A and B (key %d)", gk);
+        }
+        return (int)LRCE_OK;
+      }
       switch (gk) {
         case 32 + 7: gemm_glds_kernel<64, 64, true, true, true, S><<<grid, NT, 0, s>>>(p); break;
         case 32 + 6: gemm_glds_kernel<64, 64, true, false, true, S><<<grid, NT, 0, s>>>(p); break;
@@ -1214,7 +1226,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
       }
       return (int)LRCE_OK;
     };
-    if (small && g_small_ns == 4) {
+    if (small && (g_small_ns == 4 || p.drop_p > 0.f)) {
       if (int rc = launch_small(std::integral_constant<int, 4>{})) return rc;
     } else if (int rc = launch(std::integral_constant<int, 2>{})) {
       return rc;

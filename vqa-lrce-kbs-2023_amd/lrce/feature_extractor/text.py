@@ -224,7 +224,7 @@ class _LayerFn(torch.autograd.Function):
         K.grad_scale(do2, sc[0])
         K.dropout_bwd_f16(do2, p, seed + 2, sc[0], out=do)                                # S_f * d(o)
         K.linear_dx(do, w(oo.dense.weight), out=dh1, out_f32=False, dgelu_pre=pre)        # S_f * d(pre)
-        dh1x = K.linear_dx(dh1, w(it.dense.weight), resid=do2, alpha_dev=inv_f)
+        dh1x = _dx_resid(dh1, w(it.dense.weight), do2, inv_f)                          # do2 + (1/S_f) dh1 W1
         da2 = torch.empty_like(a2)
         K.layernorm_bwd(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, dw=_g(flat, ao.LayerNorm.weight),
                         db=_g(flat, ao.LayerNorm.bias))
@@ -265,7 +265,7 @@ def _qkv_dx(dqkv, sa, w, resid, inv_scale, rows, cols):
     lo = min(ws, key=lambda t: t.data_ptr())
     if _QKV_DX_FUSED and sorted(t.data_ptr() - lo.data_ptr() for t in ws) == [0, 2 * HIDDEN * HIDDEN, 4 * HIDDEN * HIDDEN]:
         wstack = torch.as_strided(lo, (3 * HIDDEN, HIDDEN), (HIDDEN, 1))
-        return K.linear_dx(dqkv, wstack, resid=resid, alpha_dev=inv_scale)
+        return _dx_resid(dqkv, wstack, resid, inv_scale)
     dx = None
     for wt, c in zip(ws, cols):
         a = dqkv[:, c:c + HIDDEN]
@@ -277,6 +277,26 @@ def _qkv_dx(dqkv, sa, w, resid, inv_scale, rows, cols):
 
 
 _QKV_DX_FUSED = os.environ.get("LRCE_BERT_QKV_DX_FUSED", "1") != "0"   # A/B knob
+
+
+def _dx_resid(dy, w, resid, inv_scale):
+    """resid + inv_scale * (dY W) for a deep-K input gradient of the 320-row text branch (K = 2304 /
+    3072): split-K slices of 768 (12 K tiles each) write f32 slabs and ONE reduce launch adds them INTO
+    resid (an f32 gradient that is dead afterwards: no initialising launch).  A 60-workgroup grid with
+    the whole K per workgroup is bound by each workgroup's serial operand intake (36-48 K tiles); the
+    slices put 180-240 workgroups on the chip."""
+    Kd = w.shape[0]
+    split = Kd // 768 if (_SPLIT_DX and Kd % 768 == 0 and Kd >= 1536) else 1
+    if split == 1:
+        return K.linear_dx(dy, w, resid=resid, alpha_dev=inv_scale)
+    rows, n = dy.shape[0], w.shape[1]
+    ws = torch.empty(split * rows * n, dtype=torch.float32, device=dy.device)
+    K.gemm(dy, w, resid, rows, n, Kd, a_kmajor=True, b_kmajor=False, lda=dy.stride(0), ldb=n, ldc=n,
+           flags=N.EPI_ATOMIC, split_k=split, workspace=ws, f16=True, alpha_dev=inv_scale)
+    return resid
+
+
+_SPLIT_DX = os.environ.get("LRCE_BERT_SPLIT_DX", "1") != "0"   # A/B knob
 
 
 def _qkv(xb, sa, w, q, k, v, rows):
