@@ -292,6 +292,29 @@ def test_fused_dropout_lds_dma_epilogue(h, M, N, Kd):
     k.rng_offset(dev).zero_()
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_splitk_epilogue_reduce(p):
+    """Split-K with the bias / dropout / residual epilogue applied by the reduce launch (the K = 3072
+    BERT output projection): the dropout mask is lrce_dropout's (same zero pattern), values agree with
+    the unsplit fused GEMM to f32 summation-order rounding."""
+    k = K()
+    k.rng_offset(dev).zero_()
+    h = torch.float16
+    M, N, Kd = 320, 768, 3072
+    x = torch.randn(M, Kd, device=dev).to(h)
+    w = (torch.randn(N, Kd, device=dev) / math.sqrt(Kd)).to(h)
+    b = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    drop = (p, 93, 1) if p > 0 else None
+    out = torch.empty(M, N, device=dev)
+    ws = torch.empty(4 * M * N, device=dev)
+    k.gemm(x, w, out, M, N, Kd, flags=k.N.EPI_BIAS | k.N.EPI_RESID | k.N.EPI_OUT_F32, bias=b, aux=res, ld_aux=N,
+           split_k=4, workspace=ws, drop=drop, f16=True)
+    ref = k.dropout(k.linear(x, w, b, out_f32=True), p, 93, res=res) if p > 0 else k.linear(x, w, b, out_f32=True, resid=res)
+    assert torch.equal(out == res, ref == res)            # the same dropped elements
+    assert rel(out - res, ref - res) < 1e-5
+
+
 def test_gemm_batched_alpha_stride():
     """Batched weight-gradient GEMMs with a per-batch device alpha (stride_alpha): the deferred BERT
     weight gradients of all layers in one launch, each scaled by its own layer's 1/S; negative A / alpha

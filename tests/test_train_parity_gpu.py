@@ -14,15 +14,17 @@ Every floating-point parameter is compared (783 tensors); tensors whose oracle g
 zero (BERT pooler, decoder self-attention q/k: softmax over one key) must be zero here too, and the
 analytically-zero BERT key biases (rounding noise on both sides) small against the query biases.
 
-Bar per tensor, as max|d| / max|ref| against the fp32 oracle: 3e-2, or twice the error the
-reference's own training numerics make on that tensor (fp16 autocast + GradScaler, restated on the
-CPU in tests/golden/make_train_yardstick.py; at most 0.028 on any tensor of these batches), or — for
-the Swin and fusion tensors, which this path computes with bf16 operands — 2.5x the error of the same
-numerics in bf16 (one sample of a rounding process: the measured errors sit at 0.7-1.1x it, one
-relative-position table of 72 at 2.06x); and NEVER above CAP = 0.1.  The BERT encoder runs fp16 forward and backward, like
-the reference, so its bar is the fp16 one (<= 0.056): its bf16 error would be up to 0.28 on the top
-layers' query / key gradients (near-uniform attention rows make them small differences of large
-terms), which the cap rejects.  The measured errors are written to $LRCE_PARITY_OUT (JSON) when set.
+Bar per tensor, as max|d| / max|ref| against the fp32 oracle — a RATCHET on the committed
+measurement of this path (tests/golden/train_grad_errors.json, the round-5 GPU run, also in
+profiles/r5_train_parity_errors.json): min(CAP, max(3e-2, 1.5 x the committed error)), CAP = 0.1; the
+kernels are deterministic up to a few f32 atomics, so a 1.5x margin catches regressions.  For scale,
+the reference's own training numerics (fp16 autocast + GradScaler, restated on the CPU in
+tests/golden/make_train_yardstick.py) make at most 0.028 on any tensor of these batches, and the same
+numerics in bf16 up to 0.28 (BERT top-layer query / key) / 0.08 (Swin relative-position tables); the
+committed errors are <= 0.03 except the Swin relative-position tables (bf16 dS summed over ~1e5
+terms; <= 0.052, tgif-transition).  Tensors absent from the committed file fall back to the yardstick
+bar: 3e-2, 2x the fp16 yardstick, 2.5x the bf16 one for Swin / fusion tensors, never above CAP.
+The measured errors are written to $LRCE_PARITY_OUT (JSON) when set.
 The oracle runs on the GPU box's host cores as the checker (about 25 s / batch)."""
 import json
 import os
@@ -47,6 +49,7 @@ SEED = 31
 # gradients inherit the bf16 features (the MC head's single logit is a cancellation-heavy sum)
 TOL = {"swin": 3e-2, "bert": 3e-2, "fusion": 3e-2}
 YARD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_grad_yardstick.json")
+RATCHET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_grad_errors.json")
 
 
 def _family(name):
@@ -124,8 +127,11 @@ CAP = 0.1
 BF16_FACTOR = 2.5
 
 
-def _allow(tol, y, fam):
-    """The bar of one tensor (module docstring): never above CAP."""
+def _allow(tol, y, fam, committed=None):
+    """The bar of one tensor (module docstring): the ratchet on its committed error, else the
+    yardstick bar; never above CAP."""
+    if committed is not None:
+        return min(CAP, max(tol, 1.5 * committed))
     b = max(tol, 2.0 * y.get("fp16", 0.0))
     if fam in ("swin", "fusion"):
         b = max(b, BF16_FACTOR * y.get("bf16", 0.0))
@@ -167,6 +173,8 @@ def test_baseline_train_step_grads_match_oracle(name, batch):
 
     with open(YARD) as f:
         yard = json.load(f)[f"{name}_b{batch}"]
+    with open(RATCHET) as f:
+        ratchet = json.load(f).get(f"{name}_b{batch}", {})
     worst = {f: (0.0, "") for f in TOL}
     errs, bad = [], []
     record = {}
@@ -185,14 +193,14 @@ def test_baseline_train_step_grads_match_oracle(name, batch):
             # both sides are rounding noise; bound ours by the query-bias gradient's scale
             qb = sd[k.replace("key.bias", "query.bias")].grad
             kb = float(g.abs().max()) / float(qb.abs().max())
-            kbar = _allow(2e-2, yard.get(k, {}), "bert")
+            kbar = _allow(2e-2, yard.get(k, {}), "bert", ratchet.get(k))
             record[k] = {"err": round(kb, 6), "bar": round(kbar, 6), **yard.get(k, {})}
             if kb > kbar:
                 bad.append((kb, kbar, k))
             continue
         e = rel(g, gr)
         fam = _family(k)
-        bar = _allow(TOL[fam], yard.get(k, {}), fam)
+        bar = _allow(TOL[fam], yard.get(k, {}), fam, ratchet.get(k))
         errs.append((e, bar, k))
         record[k] = {"err": round(e, 6), "bar": round(bar, 6), **yard.get(k, {})}
         if e > bar:

@@ -80,6 +80,40 @@ def main():
     t2 = timed(capture(both(False)))
     print(f"A alone {ta:.3f} ms, B alone {tb:.3f} ms, A+B {ta + tb:.3f}, max {max(ta, tb):.3f}")
     print(f"A || B, side chain captured first: {t1:.3f} ms; captured second: {t2:.3f} ms")
+    # two latency-bound chains (neither fills the chip): concurrent branches would take ~max
+    sx2 = sx.clone()
+
+    def chain_c():
+        y = sx2
+        for _ in range(150):
+            y = torch.nn.functional.gelu(y @ sw)
+        return y
+
+    def two_small():
+        main = torch.cuda.current_stream()
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            chain_a()
+        chain_c()
+        main.wait_stream(side)
+    tc = timed(capture(chain_c))
+    t3 = timed(capture(two_small))
+    print(f"two latency-bound chains: alone {ta:.3f} / {tc:.3f} ms, sum {ta + tc:.3f}, captured on two streams {t3:.3f} ms")
+    # the same two chains as two graphs replayed on two streams
+    ga, gc = capture(chain_a), capture(chain_c)
+    s2 = torch.cuda.Stream()
+    for _ in range(3):
+        ga.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        s2.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s2):
+            ga.replay()
+        gc.replay()
+        torch.cuda.current_stream().wait_stream(s2)
+    torch.cuda.synchronize()
+    print(f"  as two graphs replayed on two streams: {(time.perf_counter() - t0) / 20 * 1e3:.3f} ms")
 
 
 if __name__ == "__main__":

@@ -989,6 +989,38 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, in
   *cp = o;
 }
 
+// Split-K of a linear with a bias / dropout / residual epilogue (the 320-row BERT output projections,
+// K = 3072): out[m][n] = resid[m][n] + drop(sum_s ws[s][m][n] + bias[n]) (f32 out, n % 4 == 0), the
+// dropout mask of lrce_dropout over the contiguous [m][n] result (element m * n + col, drop_group 1).
+__global__ void splitk_reduce_epi_kernel(const float* __restrict__ ws, int split, int m, int n, const float* __restrict__ bias,
+                                         const float* __restrict__ resid, long long ld_res, float p, uint64_t seed,
+                                         const uint64_t* __restrict__ off, float* __restrict__ c, long long ldc) {
+  const long long mn = (long long)m * n;
+  const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e >= mn) return;
+  float4 s = *reinterpret_cast<const float4*>(ws + e);
+  for (int k = 1; k < split; ++k) {
+    const float4 t = *reinterpret_cast<const float4*>(ws + k * mn + e);
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  }
+  const long long r = e / n, col = e % n;
+  if (bias) {
+    const float4 b = *reinterpret_cast<const float4*>(bias + col);
+    s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+  }
+  if (p > 0.f) {
+    const float4 u = lrce_uniform4(lrce_seed(seed, off), (unsigned long long)e >> 2);
+    const float kd = 1.0f - p;
+    s.x = u.x >= p ? s.x / kd : 0.f; s.y = u.y >= p ? s.y / kd : 0.f;
+    s.z = u.z >= p ? s.z / kd : 0.f; s.w = u.w >= p ? s.w / kd : 0.f;
+  }
+  if (resid) {
+    const float4 q = *reinterpret_cast<const float4*>(resid + r * ld_res + col);
+    s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
+  }
+  *reinterpret_cast<float4*>(c + r * ldc + col) = s;
+}
+
 // Deep splits (small weight gradients over many rows: 100+ slices of a 384 x 128 tile) would leave
 // the one-thread-per-float4 reduce above with a few waves each walking every slab serially; here a
 // block is 64 float4 columns x 4 slice groups, each thread keeps 4 slab loads in flight, and the
@@ -1039,7 +1071,7 @@ bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
 
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
   if (d && d->drop_p > 0.f && !d->b_f32 &&
-      (!glds_ok(d) || d->drop_group > 1 || d->split_k > 1 || d->batch != 1 || d->c_map ||
+      (!glds_ok(d) || d->drop_group > 1 || (d->split_k > 1 && !d->workspace) || d->batch != 1 || d->c_map ||
        (d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM | LRCE_EPI_BIAS_GRAD))))
     return lrce_fail(LRCE_E_ARG, "gemm: fused dropout needs the exact-f32 skinny path or the 16-bit LDS-DMA path "
                                  "(drop_group 1, one K slice, batch 1, no c_map / accumulate)");
@@ -1088,7 +1120,14 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   if (d->b_kmajor ? (d->k % 8) : (d->n % 8)) return lrce_fail(LRCE_E_ARG, "gemm: B contiguous dim %% 8 != 0");
   if ((d->lda % 8) || (d->ldb % 8)) return lrce_fail(LRCE_E_ARG, "gemm: lda/ldb %% 8 != 0");
   const int split = d->split_k > 1 ? d->split_k : 1;
-  if (split > 1 && !(d->flags & LRCE_EPI_ATOMIC)) return lrce_fail(LRCE_E_ARG, "gemm: split_k needs ATOMIC");
+  // split-K with an epilogue (bias / residual / f32 out / dropout): f32 slabs + splitk_reduce_epi_kernel
+  const bool epi_split = split > 1 && !(d->flags & LRCE_EPI_ATOMIC) && d->workspace &&
+                         (d->flags & ~(LRCE_EPI_BIAS | LRCE_EPI_RESID | LRCE_EPI_OUT_F32)) == 0 && (d->flags & LRCE_EPI_OUT_F32) &&
+                         d->batch == 1 && !d->c_map && !d->row_scale && d->scale_cols == 0 && d->n % 4 == 0 &&
+                         d->ldc % 4 == 0 && (!d->aux || d->ld_aux % 4 == 0) && d->drop_group <= 1 &&
+                         d->workspace_elems >= (int64_t)split * d->m * d->n;
+  if (split > 1 && !(d->flags & LRCE_EPI_ATOMIC) && !epi_split)
+    return lrce_fail(LRCE_E_ARG, "gemm: split_k needs ATOMIC, or a workspace and only BIAS / RESID / OUT_F32 epilogues");
   if ((d->flags & (LRCE_EPI_GELU | LRCE_EPI_AUX_OUT)) == LRCE_EPI_AUX_OUT) return lrce_fail(LRCE_E_ARG, "gemm: AUX_OUT needs GELU");
   if ((d->flags & (LRCE_EPI_DGELU | LRCE_EPI_RESID)) && !d->aux) return lrce_fail(LRCE_E_ARG, "gemm: aux missing");
   if ((d->flags & (LRCE_EPI_AUX_OUT | LRCE_EPI_OUT_BOTH)) && !d->aux_out) return lrce_fail(LRCE_E_ARG, "gemm: aux_out missing");
@@ -1131,10 +1170,13 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   p.rng_off = p.drop_p > 0.f ? lrce_rng_offset() : nullptr;
   if (p.f16 && !glds_ok(d))
     return lrce_fail(LRCE_E_ARG, "gemm: f16 needs 16-B aligned bf16-layout operands (LDS-DMA path)");
-  const bool use_ws = d->workspace && split > 1 && (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)) == 0 &&
-                      (d->flags & LRCE_EPI_ATOMIC) && d->batch == 1 && !d->c_map && !d->row_scale && d->scale_cols == 0 &&
-                      d->n % 4 == 0 && d->ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(d->c) & 15) == 0 &&
-                      d->workspace_elems >= (int64_t)split * d->m * d->n && glds_ok(d);
+  const bool use_ws = (epi_split || (d->workspace && split > 1 && (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)) == 0 &&
+                                     (d->flags & LRCE_EPI_ATOMIC) && d->batch == 1 && !d->c_map && !d->row_scale &&
+                                     d->scale_cols == 0 && d->n % 4 == 0 && d->ldc % 4 == 0 &&
+                                     d->workspace_elems >= (int64_t)split * d->m * d->n)) &&
+                      (reinterpret_cast<uintptr_t>(d->c) & 15) == 0 && glds_ok(d);
+  if (epi_split && !use_ws) return lrce_fail(LRCE_E_ARG, "gemm: split-K epilogue needs the 16-bit LDS-DMA path and a 16-B aligned C");
+  if (epi_split) p.drop_p = 0.f;   // the reduce launch applies bias / dropout / residual
   if (use_ws) p.ws = d->workspace;
   dim3 grid(p.tiles_m * p.tiles_n, d->batch * split);
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1231,7 +1273,13 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     } else if (int rc = launch(std::integral_constant<int, 2>{})) {
       return rc;
     }
-    if (p.ws) {
+    if (p.ws && epi_split) {
+      const long long q4 = (long long)d->m * d->n / 4;
+      splitk_reduce_epi_kernel<<<(unsigned)((q4 + 255) / 256), 256, 0, s>>>(
+          p.ws, split, d->m, d->n, (d->flags & LRCE_EPI_BIAS) ? d->bias : nullptr,
+          (d->flags & LRCE_EPI_RESID) ? static_cast<const float*>(d->aux) : nullptr, d->ld_aux, d->drop_p > 0.f ? d->drop_p : 0.f,
+          d->drop_seed, d->drop_p > 0.f ? lrce_rng_offset() : nullptr, static_cast<float*>(d->c), d->ldc);
+    } else if (p.ws) {
       const long long q4 = (long long)d->m * d->n / 4;
       if (split >= 8)
         splitk_reduce_deep_kernel<<<(unsigned)((q4 + 63) / 64), 256, 0, s>>>(p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);

@@ -190,7 +190,7 @@ class _LayerFn(torch.autograd.Function):
         h1, m1, r1 = K.layernorm(a2, ao.LayerNorm.weight, ao.LayerNorm.bias, EPS, out_f32=True, bf16_copy=h1b)
         K.linear(h1b, w(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre, out=g)
         drop2 = (p, seed + 2, 1) if p > 0 else None
-        o2 = K.linear(g, w(oo.dense.weight), oo.dense.bias, out_f32=True, resid=h1, drop=drop2)
+        o2 = _proj_resid(g, w(oo.dense.weight), oo.dense.bias, h1, drop2)                # h1 + drop(g W2^T + b2)
         nxt = st.fviews(i + 1)[0] if i + 1 < st.n else None   # the next layer's fp16 input
         out, m2, r2 = K.layernorm(o2, oo.LayerNorm.weight, oo.LayerNorm.bias, EPS, out_f32=True, bf16_copy=nxt)
         ctx.save = (mask, lse, a2, m1, r1, o2, m2, r2)
@@ -277,6 +277,23 @@ def _qkv_dx(dqkv, sa, w, resid, inv_scale, rows, cols):
 
 
 _QKV_DX_FUSED = os.environ.get("LRCE_BERT_QKV_DX_FUSED", "1") != "0"   # A/B knob
+
+
+def _proj_resid(x, w, bias, resid, drop):
+    """resid + drop(x W^T + bias), f32, for the K = 3072 output projection of the 320-row text branch:
+    split-K slices of 768 into f32 slabs, then ONE reduce launch that adds the bias, draws the dropout
+    mask of lrce_dropout and adds the residual (a 60-workgroup grid with the whole K per workgroup is
+    bound by each workgroup's serial operand intake)."""
+    Kd = x.shape[1]
+    split = Kd // 768 if (_SPLIT_DX and Kd % 768 == 0 and Kd >= 1536) else 1
+    if split == 1:
+        return K.linear(x, w, bias, out_f32=True, resid=resid, drop=drop)
+    rows, n = x.shape[0], w.shape[0]
+    out = torch.empty(rows, n, dtype=torch.float32, device=x.device)
+    ws = torch.empty(split * rows * n, dtype=torch.float32, device=x.device)
+    K.gemm(x, w, out, rows, n, Kd, flags=N.EPI_BIAS | N.EPI_RESID | N.EPI_OUT_F32, bias=bias, aux=resid, ld_aux=n,
+           split_k=split, workspace=ws, drop=drop, f16=True)
+    return out
 
 
 def _dx_resid(dy, w, resid, inv_scale):
