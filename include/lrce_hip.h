@@ -498,6 +498,19 @@ int lrce_dropout_bwd(const float* dy, float* dx, uint16_t* dx_bf16, int64_t n, f
  * arrival words: zero them once when allocating (the kernel leaves them zero).  n % 4 == 0, x 16-B
  * aligned. */
 int lrce_grad_scale(const float* x, int64_t n, float* scale, void* stream);
+/* Delayed scaling of the BERT backward's fp16 operands (the reference's GradScaler keeps one scale for
+ * thousands of steps, agent_oe.py:40-42; here one per tensor, from the previous step): for each of
+ * n_slots scale slots [S, 1/S, amax bits, -] with a recorded max (word 2 != 0): S = 2^(7 - floor(log2
+ * amax)), 1/S, word 2 cleared; slots without one keep their scale.  One launch per step. */
+int lrce_grad_scale_update(float* scale, int n_slots, void* stream);
+/* lrce_layernorm_bwd (identity maps, f32 dy / x, no residual) fused with lrce_dropout_bwd_f16: dx (f32,
+ * optional), dx_f16 = fp16(scale[0] * dropout_bwd(dx)) (mask of lrce_dropout over [rows][cols], p / seed
+ * + the device RNG offset), max|dx| folded into the slot's word 2 (NaN-sticky); dw / db as
+ * lrce_layernorm_bwd (workspace: lrce_layernorm_bwd_workspace).  Replaces BertOutput / BertSelfOutput
+ * LayerNorm backward + the fp16 cast of the reference's autocast backward (text.py:11-17). */
+int lrce_layernorm_bwd_f16s(const float* dy, const float* x, const float* mean, const float* rstd, const float* w,
+                            float* dx, float* dw, float* db, int rows, int cols, uint16_t* dx_f16, float* scale,
+                            float p, uint64_t seed, float* workspace, int64_t workspace_elems, void* stream);
 /* dx_f16 = fp16(scale[0] * dropout_bwd(dy)) (p = 0: a scaled cast): the fp16 operand of the BERT
  * backward GEMMs from an f32 residual-stream gradient. */
 int lrce_dropout_bwd_f16(const float* dy, uint16_t* dx_f16, int64_t n, float p, uint64_t seed, int64_t group,

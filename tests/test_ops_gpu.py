@@ -216,6 +216,42 @@ def test_grad_scale_and_f16_operand():
         assert float(sc[0]) == 1.0 and float(sc[3]) == 0.0
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_layernorm_bwd_f16s_matches_unfused(p):
+    """The BERT backward's fused LN backward + scaled fp16 operand (lrce_layernorm_bwd_f16s, delayed
+    scale): dx, dw, db and the fp16 operand bit-identical to layernorm_bwd + dropout_bwd_f16 with the
+    same scale; the slot records max|dx| and grad_scale_update turns it into the next scale."""
+    k = K()
+    k.rng_offset(dev).zero_()
+    R, C = 320, 768
+    x = torch.randn(R, C, device=dev) * 2 + 0.5
+    g = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev)
+    _, mean, rstd = k.layernorm(x, g, b, 1e-12, out_f32=True)
+    dy = torch.randn(R, C, device=dev) * 1e-3
+    S = 2.0 ** 17
+    dx = torch.empty(R, C, device=dev)
+    dw, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    k.layernorm_bwd(dy, x, mean, rstd, g, dx, dw=dw, db=db)
+    sc = torch.tensor([S, 1.0 / S, 0.0, 0.0], device=dev)
+    ref16 = k.dropout_bwd_f16(dx, p, 41, sc)
+    dx2 = torch.empty(R, C, device=dev)
+    out16 = torch.empty(R, C, device=dev, dtype=torch.float16)
+    dw2, db2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    k.layernorm_bwd_f16s(dy, x, mean, rstd, g, dx2, out16, sc, p, 41, dw=dw2, db=db2)
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, dx) and torch.equal(out16, ref16) and torch.equal(dw2, dw) and torch.equal(db2, db)
+    amax = float(dx.abs().max())
+    assert sc[2:3].view(torch.int32).item() == torch.tensor([amax]).view(torch.int32).item()
+    k.grad_scale_update(sc)
+    torch.cuda.synchronize()
+    S2 = 2.0 ** (7 - math.floor(math.log2(amax)))
+    assert float(sc[0]) == S2 and float(sc[1]) == 1.0 / S2 and float(sc[2]) == 0.0
+    k.grad_scale_update(sc)                      # no recorded max: the scale stays
+    torch.cuda.synchronize()
+    assert float(sc[0]) == S2
+
+
 @pytest.mark.parametrize("M,N,Kd", [(320, 768, 768), (320, 3072, 768), (2000, 768, 3072)])
 def test_gemm_f16_backward_layouts(M, N, Kd):
     """The fp16 BERT backward GEMMs: dX = dY W (B N-major) with dGELU or residual epilogues, dW = dY^T X

@@ -199,6 +199,24 @@ __global__ void __launch_bounds__(256) grad_scale_kernel(const float* __restrict
   }
 }
 
+// Delayed per-tensor scales (lrce_layernorm_bwd_f16s): slot i's max |x| of the last step (word 2,
+// accumulated by the fused LN backward) becomes its scale S = 2^(7 - floor(log2 max)) and 1/S, and the
+// word is cleared for this step; a slot with no recorded max keeps its scale.  One thread per slot.
+__global__ void grad_scale_update_kernel(float* __restrict__ scale, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float* sc = scale + 4 * i;
+  unsigned* words = reinterpret_cast<unsigned*>(sc + 2);
+  const unsigned bits = words[0];
+  if (bits == 0u) return;
+  const int e = (int)((bits >> 23) & 0xFF) - 127;
+  float s = 1.f;
+  if (e < 128 && e > -127) s = ldexpf(1.f, min(100, max(-100, 7 - e)));
+  sc[0] = s;
+  sc[1] = 1.f / s;
+  words[0] = 0u;
+}
+
 __global__ void dropout_bwd_f16_kernel(const float* __restrict__ dy, f16* __restrict__ dx, long long n, float p, uint64_t seed,
                                        long long group, const uint64_t* __restrict__ off, const float* __restrict__ scale) {
   const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
@@ -470,6 +488,13 @@ extern "C" int lrce_grad_scale(const float* x, int64_t n, float* scale, void* st
   const unsigned blocks = (unsigned)std::max<long long>(1, std::min<long long>(256, (n4 + 2047) / 2048));
   grad_scale_kernel<<<blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(x, n4, scale);
   return lrce_check_launch("grad_scale");
+}
+
+extern "C" int lrce_grad_scale_update(float* scale, int n_slots, void* stream) {
+  if (!scale || n_slots < 0) return lrce_fail(LRCE_E_ARG, "grad_scale_update: bad arguments");
+  if (n_slots == 0) return LRCE_OK;
+  grad_scale_update_kernel<<<(n_slots + 255) / 256, 256, 0, static_cast<hipStream_t>(stream)>>>(scale, n_slots);
+  return lrce_check_launch("grad_scale_update");
 }
 
 extern "C" int lrce_dropout_bwd_f16(const float* dy, uint16_t* dx_f16, int64_t n, float p, uint64_t seed, int64_t group,

@@ -141,11 +141,23 @@ __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, in
   }
 }
 
-template <typename TD, typename TX, int CH, int LPR>
+// Scaled fp16 copy of the LN input gradient (F16S: the BERT backward, text.py): dx16[r][c] =
+// fp16(keep ? dx * S / (1 - p) : 0) with S = f16s->scale[0] (a delayed per-tensor gradient scale,
+// lrce_grad_scale_update), the mask of lrce_dropout over the contiguous [rows][cols] tensor, and
+// max|dx| folded into f16s->scale word 2 for the next step's scale.
+struct F16Scaled {
+  float* scale;          // [S, 1/S, amax bits (next step), -]
+  float p;
+  uint64_t seed;
+  const uint64_t* off;
+};
+
+template <typename TD, typename TX, int CH, int LPR, bool F16S = false>
 __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, const TX* x, const int* in_map, int nseg,
                                               const float* mean_i, const float* rstd_i, const float* w, float* dx,
                                               const float* dres, float* dw, float* db, int rows, int cols, bf16* dx16,
-                                              const int* dx16_map, const float* dsc, int dsc_rps, float* part) {
+                                              const int* dx16_map, const float* dsc, int dsc_rps, float* part,
+                                              F16Scaled fs = F16Scaled{}) {
   constexpr int RPW = 64 / LPR;
   __shared__ float red[2][4][4 * CH * LPR + 4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sl = lane % LPR;
@@ -194,6 +206,9 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
   float4 xcur[CH], dcur[CH], rcur[CH];
   float mcur = 0.f, scur = 0.f;
   bool pcur = false;
+  float amax = 0.f;                                    // F16S: max |dx| of this wave's rows
+  const float s16 = F16S ? fs.scale[0] / (fs.p > 0.f ? 1.0f - fs.p : 1.0f) : 0.f;
+  const uint64_t dseed = F16S && fs.p > 0.f ? lrce_seed(fs.seed, fs.off) : 0ull;
   if (r0 < rows) fetch(r0, xcur, dcur, rcur, mcur, scur, pcur);
   for (; r0 < rows; r0 += stride) {
     float4 xnx[CH], dnx[CH], rnx[CH];
@@ -241,7 +256,21 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
           out.x += rr.x; out.y += rr.y; out.z += rr.z; out.w += rr.w;
         }
         if (dx) *reinterpret_cast<float4*>(dx + o) = out;
-        if (dx16) {   // bf16 copy (optionally row-scaled / row-permuted) for the next GEMMs' A operand
+        if constexpr (F16S) {   // (identity maps on this path: the host checks)
+          const float a4[4] = {out.x, out.y, out.z, out.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float ae = fabsf(a4[e]);
+            amax = (ae > amax || ae != ae) ? ae : amax;   // NaN sticks (lrce_grad_scale)
+          }
+          float4 u = make_float4(1.f, 1.f, 1.f, 1.f);
+          if (fs.p > 0.f) u = lrce_uniform4(dseed, ((unsigned long long)r * cols + 4 * c) >> 2);
+          typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+          h4 hv;
+          hv[0] = (f16)(u.x >= fs.p ? out.x * s16 : 0.f); hv[1] = (f16)(u.y >= fs.p ? out.y * s16 : 0.f);
+          hv[2] = (f16)(u.z >= fs.p ? out.z * s16 : 0.f); hv[3] = (f16)(u.w >= fs.p ? out.w * s16 : 0.f);
+          *reinterpret_cast<h4*>(dx16 + (long long)r * cols + 4 * c) = hv;
+        } else if (dx16) {   // bf16 copy (optionally row-scaled / row-permuted) for the next GEMMs' A operand
           const float f = dsc ? dsc[r / dsc_rps] : 1.f;
           const long long orow = dx16_map ? (long long)dx16_map[r] : (long long)r;
           st4<bf16>(dx16 + orow * cols + 4 * c, make_float4(out.x * f, out.y * f, out.z * f, out.w * f));
@@ -255,6 +284,16 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
       scur = snx;
       pcur = pnx;
     }
+  }
+  if constexpr (F16S) {   // the next step's scale: one agent-scope max per wave (|x| bits order like values)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float t = __shfl_xor(amax, o, 64);
+      amax = (t > amax || t != t) ? t : amax;
+    }
+    if (lane == 0 && amax != 0.f)
+      __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(fs.scale + 2), __float_as_uint(amax), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
   }
   if (!dw && !db) return;
   if (LPR == 32) {  // fold the two half-wave row slots onto lanes 0..31
@@ -445,6 +484,40 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
     ln_bwd_reduce<<<dim3((2 * cols + 63) / 64, ny), 256, 0, s>>>(
         part, nb, cols, dw, db, part + (long long)nb * 2 * cols, reinterpret_cast<unsigned*>(part + (long long)(nb + ny) * 2 * cols));
   return lrce_check_launch("layernorm_bwd");
+}
+
+// lrce_layernorm_bwd + the scaled fp16 operand of the next GEMM in one pass (the BERT backward):
+// dx (f32, optional) and dx_f16 = fp16(S * dropout_bwd(dx)), S = scale[0]; max|dx| -> scale word 2
+// (lrce_grad_scale_update turns it into the next step's S).  Identity maps, no residual, f32 dy / x.
+extern "C" int lrce_layernorm_bwd_f16s(const float* dy, const float* x, const float* mean, const float* rstd, const float* w,
+                                       float* dx, float* dw, float* db, int rows, int cols, uint16_t* dx_f16, float* scale,
+                                       float p, uint64_t seed, float* workspace, int64_t workspace_elems, void* stream) {
+  if (!dy || !x || !mean || !rstd || !w || !dx_f16 || !scale) return lrce_fail(LRCE_E_ARG, "layernorm_bwd_f16s: null pointer");
+  if (cols % 4 || cols > 64 * 4 * MAXC || cols / 4 <= 32) return lrce_fail(LRCE_E_ARG, "layernorm_bwd_f16s: cols=%d", cols);
+  if (rows <= 0) return LRCE_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nch = cols / 4;
+  const bool want = dw || db;
+  const int nb_ws = ln_bwd_blocks(rows, 64, true, cols);
+  const int ny = (nb_ws + LN_RED_ROWS - 1) / LN_RED_ROWS;
+  float* part = want && nb_ws > 1 && workspace && workspace_elems >= (int64_t)(nb_ws + ny) * 2 * cols + LN_RED_CTRS
+                    ? workspace : nullptr;
+  const int nb = (part || !want) ? nb_ws : ln_bwd_blocks(rows, 64, false, cols);
+  const F16Scaled fs{scale, p > 0.f ? p : 0.f, seed, p > 0.f ? lrce_rng_offset() : nullptr};
+  bf16* o16 = reinterpret_cast<bf16*>(dx_f16);
+#define LNBS(CH)                                                                                                    \
+  ln_bwd<float, float, CH, 64, true><<<nb, 256, 0, s>>>(dy, nullptr, x, nullptr, 1, mean, rstd, w, dx, nullptr, dw, db, \
+                                                        rows, cols, o16, nullptr, nullptr, 1, part, fs)
+  if (nch <= 64) LNBS(1);
+  else if (nch <= 128) LNBS(2);
+  else if (nch <= 192) LNBS(3);
+  else if (nch <= 256) LNBS(4);
+  else LNBS(8);
+#undef LNBS
+  if (part)
+    ln_bwd_reduce<<<dim3((2 * cols + 63) / 64, ny), 256, 0, s>>>(
+        part, nb, cols, dw, db, part + (long long)nb * 2 * cols, reinterpret_cast<unsigned*>(part + (long long)(nb + ny) * 2 * cols));
+  return lrce_check_launch("layernorm_bwd_f16s");
 }
 
 extern "C" int64_t lrce_layernorm_bwd_workspace(int rows, int cols) {

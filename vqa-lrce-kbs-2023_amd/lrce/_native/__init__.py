@@ -174,6 +174,8 @@ _SIGS = {
     "lrce_dropout": [_P, _P, _P, _P, _I64, _F, _U64, _I64, _P],
     "lrce_dropout_bwd": [_P, _P, _P, _I64, _F, _U64, _I64, _P],
     "lrce_grad_scale": [_P, _I64, _P, _P],
+    "lrce_grad_scale_update": [_P, _I, _P],
+    "lrce_layernorm_bwd_f16s": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _F, _U64, _P, _I64, _P],
     "lrce_dropout_bwd_f16": [_P, _P, _I64, _F, _U64, _I64, _P, _P],
     "lrce_bert_embed_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_bert_embed_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I64, _P],

@@ -146,6 +146,10 @@ class _Stack:
         self.dbuf = None
         self.scales = bert._grad_scales(dev)
         self.flush_at = None
+        # delayed gradient scales (lrce_layernorm_bwd_f16s): once a backward has computed every layer's
+        # scales from its own maxima, each later step uses the previous step's (the reference's
+        # GradScaler likewise keeps one scale across steps); LRCE_BERT_DELAYED_SCALE=0: per-step scales
+        self.delayed = _DELAYED_SCALE and getattr(bert, "_lrce_scales_ready", False)
         self.done = []          # layer indices whose backward has run (their dY in dbuf)
 
     def fviews(self, i):
@@ -219,17 +223,27 @@ class _LayerFn(torch.autograd.Function):
         w = flat.w16h
         dout = dout.contiguous()
         do2 = torch.empty_like(o2)
-        K.layernorm_bwd(dout, o2, m2, r2, oo.LayerNorm.weight, do2, dw=_g(flat, oo.LayerNorm.weight),
-                        db=_g(flat, oo.LayerNorm.bias))
-        K.grad_scale(do2, sc[0])
-        K.dropout_bwd_f16(do2, p, seed + 2, sc[0], out=do)                                # S_f * d(o)
+        if i == st.n - 1 and st.delayed:
+            K.grad_scale_update(st.scales)      # this step's scales from the last step's maxima
+        if st.delayed:   # LN backward + the scaled fp16 operand in one launch (delayed scale)
+            K.layernorm_bwd_f16s(dout, o2, m2, r2, oo.LayerNorm.weight, do2, do, sc[0], p, seed + 2,
+                                 dw=_g(flat, oo.LayerNorm.weight), db=_g(flat, oo.LayerNorm.bias))
+        else:
+            K.layernorm_bwd(dout, o2, m2, r2, oo.LayerNorm.weight, do2, dw=_g(flat, oo.LayerNorm.weight),
+                            db=_g(flat, oo.LayerNorm.bias))
+            K.grad_scale(do2, sc[0])
+            K.dropout_bwd_f16(do2, p, seed + 2, sc[0], out=do)                            # S_f * d(o)
         K.linear_dx(do, w(oo.dense.weight), out=dh1, out_f32=False, dgelu_pre=pre)        # S_f * d(pre)
         dh1x = _dx_resid(dh1, w(it.dense.weight), do2, inv_f)                          # do2 + (1/S_f) dh1 W1
         da2 = torch.empty_like(a2)
-        K.layernorm_bwd(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, dw=_g(flat, ao.LayerNorm.weight),
-                        db=_g(flat, ao.LayerNorm.bias))
-        K.grad_scale(da2, sc[1])
-        K.dropout_bwd_f16(da2, p, seed + 1, sc[1], out=da)                                # S_a * d(a)
+        if st.delayed:
+            K.layernorm_bwd_f16s(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, da, sc[1], p, seed + 1,
+                                 dw=_g(flat, ao.LayerNorm.weight), db=_g(flat, ao.LayerNorm.bias))
+        else:
+            K.layernorm_bwd(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, dw=_g(flat, ao.LayerNorm.weight),
+                            db=_g(flat, ao.LayerNorm.bias))
+            K.grad_scale(da2, sc[1])
+            K.dropout_bwd_f16(da2, p, seed + 1, sc[1], out=da)                            # S_a * d(a)
         dctx = K.linear_dx(da, w(ao.dense.weight), out_f32=False)                         # S_a * d(ctx)
         # dq / dk / dv as fp16 column blocks of ONE [rows, 2304] operand, in the address order of the
         # three weights (so the input gradient is one K = 2304 GEMM when they are contiguous)
@@ -244,6 +258,8 @@ class _LayerFn(torch.autograd.Function):
             _flush_wgrads(st)
             for j in st.done:
                 flat.notify(st.bert.encoder.layer[j].parameters())
+            # a full backward has set every scale: later steps may use delayed scales
+            object.__setattr__(st.bert, "_lrce_scales_ready", True)
         return (dx,) + (None,) * (9 + len(ctx.needs_input_grad[10:]))
 
 
@@ -413,6 +429,7 @@ def _flush_wgrads(st):
 
 
 _WGRAD_BATCHED = os.environ.get("LRCE_BERT_WGRAD_BATCHED", "1") != "0"   # A/B knob
+_DELAYED_SCALE = os.environ.get("LRCE_BERT_DELAYED_SCALE", "1") != "0"   # A/B knob
 
 
 def _uniform_stride(ts, es):

@@ -658,6 +658,27 @@ def grad_scale(x, scale):
     call("lrce_grad_scale", ptr(x), x.numel(), ptr(scale), stream_of(x))
 
 
+def grad_scale_update(scales):
+    """Delayed scales: every [S, 1/S, amax, -] slot of `scales` (f32, [..., 4]) with a recorded max
+    becomes S = 2^(7 - floor(log2 max)), 1/S, the max cleared (lrce_grad_scale_update)."""
+    _chk(scales, F32, "scales")
+    call("lrce_grad_scale_update", ptr(scales), scales.numel() // 4, stream_of(scales))
+
+
+def layernorm_bwd_f16s(dy, x, mean, rstd, w, dx, out16, scale, p, seed, *, dw=None, db=None):
+    """LayerNorm backward (f32 dy / x, identity maps) + out16 = fp16(scale[0] * dropout_bwd(dx)) in one
+    launch, max|dx| recorded into scale[2] for grad_scale_update (lrce_layernorm_bwd_f16s)."""
+    _chk(out16, F16, "out16"); _chk(scale, F32, "scale")
+    R, Cc = mean.shape[0], w.shape[0]
+    ws, nws = None, 0
+    if dw is not None or db is not None:
+        nws = N.lib().lrce_layernorm_bwd_workspace(R, Cc)
+        ws = torch.empty(nws, dtype=F32, device=dy.device) if nws > 0 else None
+    call("lrce_layernorm_bwd_f16s", ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dw), ptr(db), R, Cc,
+         ptr(out16), ptr(scale), float(p), seed & (2 ** 64 - 1), ptr(ws), nws, stream_of(out16))
+    return dx
+
+
 def dropout_bwd_f16(dy, p, seed, scale, group=1, out=None):
     """fp16(scale[0] * dropout_bwd(dy)): the scaled fp16 GEMM operand of an f32 gradient."""
     if out is None:
