@@ -321,6 +321,13 @@ def _layer_wgrads(lay, flat, acts, grads, fused=False):
     _wgrad(flat, sa.in_proj_weight, sa.in_proj_bias, v(grads.dsav), v(acts.x0), rows=(2 * E, 3 * E))
 
 
+def _dev_layers(ft):
+    """The decoder layers a step runs: all 12 (LRCE_DEV_DEC_LAYERS=k keeps the first k — a critical-path
+    sensitivity experiment only, never set in the product)."""
+    k = int(os.environ.get("LRCE_DEV_DEC_LAYERS", "0"))
+    return list(ft.transformer.layers)[:k] if k else ft.transformer.layers
+
+
 class _RecurrentDecoderFn(torch.autograd.Function):
     """FusionTransformer.forward (fusionv3.py:27-51) as one autograd node; with t = None the memory
     is the video tokens alone (FusionVideo.forward, fusionv3.py:70-88)."""
@@ -328,7 +335,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, v, v16, t, t16, ft, flat, p, seed, B, S, nmc, anchor, *params):
         dev = v.device
-        layers = ft.transformer.layers
+        layers = _dev_layers(ft)
         Lt = t.shape[1] if t is not None else 0
         Bq = t.shape[0] if t is not None else B * nmc
         rows_v = B * S * 150
@@ -371,7 +378,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         kvv, kvt, saves, fused, v16, t16, acts = ctx.save
         ft, flat, p, seed = ctx.ft, ctx.flat, ctx.p, ctx.seed
         B, S, nmc, Bq, Lt = ctx.dims
-        layers = ft.transformer.layers
+        layers = _dev_layers(ft)
         dev = ds.device
         # video K/V gradients: written once per row by the step's attention backward (OE / Count), or
         # accumulated by the answer choices sharing the row (MC: atomics onto zeros)
