@@ -120,15 +120,18 @@ __device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
 
 // The [768][64] slice W[:, h*64 .. h*64+63] of a row-major [768][768] fp16 matrix -> LDS image
 // [n][64] (128-B rows), 8 rows per 1-KB DMA instruction, 24 per wave.  Issued at kernel start.
+// 16-B chunk k of row n sits in slot k ^ (n & 7) (slice_at): a thread per row reading chunk k of 8
+// consecutive rows then hits 8 different bank groups instead of one.
 __device__ __forceinline__ void slice_dma(const f16* w, int h, void* lds, int wave, int lane) {
   const uint32_t base = dec_lds_addr(lds);
 #pragma unroll 4
   for (int i = 0; i < 24; ++i) {
     const int ins = wave * 24 + i;
     const int row = ins * 8 + (lane >> 3);
-    dec_glds(w, (uint32_t)((row * E + h * D + (lane & 7) * 8) * 2), base + (uint32_t)ins * 1024u);
+    dec_glds(w, (uint32_t)((row * E + h * D + ((lane & 7) ^ (row & 7)) * 8) * 2), base + (uint32_t)ins * 1024u);
   }
 }
+__device__ __forceinline__ const f16* slice_at(const f16* S, int n, int k) { return S + n * D + ((k ^ (n & 7)) << 3); }
 
 // Rows r0 .. r0+15 of a row-major [.][768] fp16 matrix into registers, 24 x 16 B per lane:
 // ins r (< 16): row r0 + r, 8-element chunk `lane` (elements 8*lane .. 8*lane+7);
@@ -205,22 +208,31 @@ __device__ __forceinline__ void rows_gemv_t(const uint4 (&reg)[NRI], const float
   }
 }
 
-// out[n] = sum_d S[n][d] v[d] over the LDS head slice S [768][64] (fp16), the wave's rows
-// n = wave*192 .. +191: lane (g = lane/8, c = lane%8) takes row 8i+g, chunk c; 8-lane reduction.
-__device__ __forceinline__ void slice_gemv(const f16* S, const float* v, float* out, int wave, int lane) {
-  const int g = lane >> 3, c = lane & 7;
-  float vv[8];
+// out[n] = sum_d S[n][d] v[d] over the LDS head slice S [768][64] (fp16): thread t owns rows t,
+// t + 256, t + 512 and walks each whole row (8 x 16-B reads, swizzled slots), v (64 f32, LDS
+// broadcast reads) in registers — no cross-lane reduction.  (Lane-per-chunk with an 8-lane DPP sum
+// per row measured 2.5 us per launch for this phase: a dependent reduction chain per 8 rows.)
+__device__ __forceinline__ void slice_gemv(const f16* S, const float* v, float* out, int t) {
+  float vv[D];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) vv[e] = v[c * 8 + e];
-#pragma unroll 4
-  for (int i = 0; i < 24; ++i) {
-    const int n = wave * 192 + i * 8 + g;
-    float wf[8];
-    unpack8(*reinterpret_cast<const uint4*>(S + n * D + c * 8), wf);
-    float s = ((wf[0] * vv[0] + wf[1] * vv[1]) + (wf[2] * vv[2] + wf[3] * vv[3])) +
-              ((wf[4] * vv[4] + wf[5] * vv[5]) + (wf[6] * vv[6] + wf[7] * vv[7]));
-    s = sum8(s);
-    if (c == 0) out[n] = s;
+  for (int e = 0; e < D; e += 4) {
+    const float4 q = *reinterpret_cast<const float4*>(v + e);
+    vv[e] = q.x; vv[e + 1] = q.y; vv[e + 2] = q.z; vv[e + 3] = q.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float wf[8];
+      unpack8(*reinterpret_cast<const uint4*>(slice_at(S, n, k)), wf);
+      a0 = fmaf(wf[0], vv[8 * k], a0); a1 = fmaf(wf[1], vv[8 * k + 1], a1);
+      a0 = fmaf(wf[2], vv[8 * k + 2], a0); a1 = fmaf(wf[3], vv[8 * k + 3], a1);
+      a0 = fmaf(wf[4], vv[8 * k + 4], a0); a1 = fmaf(wf[5], vv[8 * k + 5], a1);
+      a0 = fmaf(wf[6], vv[8 * k + 6], a0); a1 = fmaf(wf[7], vv[8 * k + 7], a1);
+    }
+    out[n] = a0 + a1;
   }
 }
 
@@ -232,7 +244,7 @@ __device__ __forceinline__ void slice_gemv_t(const f16* S, const float* u, float
   for (int i = 0; i < 24; ++i) {
     const int n = wave * 192 + i * 8 + g;
     float wf[8];
-    unpack8(*reinterpret_cast<const uint4*>(S + n * D + c * 8), wf);
+    unpack8(*reinterpret_cast<const uint4*>(slice_at(S, n, c)), wf);
     const float un = u[n];
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] = fmaf(un, wf[e], a[e]);
@@ -376,7 +388,7 @@ struct SaFwdLds {
   f16 wo[E * D];                  // 96 KB
   float x0[E];
   float pp[4][16 * 64];
-  float v[D];
+  alignas(16) float v[D];
   float part[E];
   float red2[4];
   unsigned last;
@@ -440,7 +452,7 @@ __global__ void __launch_bounds__(NT, 1) dec_sa_fwd_kernel(SaFwdP p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slice DMA has landed
   lds_barrier();                                    // ... and every wave's; L.v complete
   DEC_MARK(0, 3);
-  slice_gemv(L.wo, L.v, L.part, wave, lane);
+  slice_gemv(L.wo, L.v, L.part, t);
   lds_barrier();
   DEC_MARK(0, 4);
   const bool last_sa = publish_partial(L.part, p.slab, p.ctr, b, h, t, &L.last);
@@ -530,7 +542,7 @@ struct CaFwdLds {
   float q[D];
   float ps[MAXK + 64];
   float opart[4][D];
-  float ctx[D];
+  alignas(16) float ctx[D];
   float part[E];
   float red2[4];
   unsigned last;
@@ -662,7 +674,7 @@ __global__ void __launch_bounds__(NT, 1) dec_ca_fwd_kernel(CaFwdP p) {
   }
   lds_barrier();
   DEC_MARK(1, 5);
-  slice_gemv(L.wo, L.ctx, L.part, wave, lane);
+  slice_gemv(L.wo, L.ctx, L.part, t);
   lds_barrier();
   DEC_MARK(1, 6);
   const bool last_ca = publish_partial(L.part, p.slab, p.ctr, b, h, t, &L.last);

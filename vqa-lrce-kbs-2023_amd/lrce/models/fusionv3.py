@@ -321,6 +321,12 @@ def _layer_wgrads(lay, flat, acts, grads, fused=False):
     _wgrad(flat, sa.in_proj_weight, sa.in_proj_bias, v(grads.dsav), v(acts.x0), rows=(2 * E, 3 * E))
 
 
+# Memory-side K/V projections on their own stream (A/B knob LRCE_DEC_KV_ASYNC=0: in line): the
+# recurrence waits for layer l's K/V only when step 0 reaches layer l, and in the backward each layer's
+# memory-side input-gradient GEMMs start as soon as step 0's sweep has finished that layer.
+_KV_ASYNC = os.environ.get("LRCE_DEC_KV_ASYNC", "1") != "0"
+
+
 def _dev_layers(ft):
     """The decoder layers a step runs: all 12 (LRCE_DEV_DEC_LAYERS=k keeps the first k — a critical-path
     sensitivity experiment only, never set in the product)."""
@@ -341,12 +347,25 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         rows_v = B * S * 150
         v16 = v16.view(rows_v, E)
         t16 = t16.view(Bq * Lt, E) if Lt else None
-        kvv, kvt = [], []
-        for lay in layers:
-            ca = lay.multihead_attn
-            w = flat.w16(ca.in_proj_weight)[E:]
-            kvv.append(K.linear(v16, w, ca.in_proj_bias[E:]))
-            kvt.append(K.linear(t16, w, ca.in_proj_bias[E:]) if Lt else None)
+        kvv, kvt, kv_ready = [], [], []
+        main = torch.cuda.current_stream(dev)
+        ks = aux_stream(dev, "decoder_kv") if _KV_ASYNC else main
+        if ks is not main:
+            ks.wait_stream(main)
+        with torch.cuda.stream(ks):
+            for lay in layers:
+                ca = lay.multihead_attn
+                w = flat.w16(ca.in_proj_weight)[E:]
+                kvv.append(K.linear(v16, w, ca.in_proj_bias[E:]))
+                kvt.append(K.linear(t16, w, ca.in_proj_bias[E:]) if Lt else None)
+                if ks is not main:
+                    kv_ready.append(ks.record_event())
+        if ks is not main:
+            for x in kvv + [x for x in kvt if x is not None]:
+                x.record_stream(main)
+            for x in (v16, t16):
+                if x is not None:
+                    x.record_stream(ks)
         nL = len(layers)
         acts = [_LayerActs(S, Bq, dev) for _ in layers]
         s = acts[0].x0[0]
@@ -357,6 +376,8 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             step_saves = []
             x_in, prev = s, None
             for l, lay in enumerate(layers):
+                if i == 0 and kv_ready:
+                    main.wait_event(kv_ready[l])
                 st = _layer_fwd(lay, prev, x_in, kvv[l].view(-1), kvt[l].view(-1) if Lt else None, i, S, Lt, nmc, p,
                                 seed + 64 * (i * nL + l), acts[l], step_saves[-1] if step_saves else None)
                 step_saves.append(st)
@@ -395,6 +416,33 @@ class _RecurrentDecoderFn(torch.autograd.Function):
                 for l in range(len(layers))]
         ds = ds.contiguous()
         grads = [_LayerGrads(S, Bq, dev) for _ in layers]
+        main = torch.cuda.current_stream(dev)
+        dv = torch.empty(B * S * 150, E, device=dev)
+        dtt = torch.empty(Bq * Lt, E, device=dev) if Lt else None
+        # the memory-side K/V gradients (accumulated in f32 over steps / answer choices) enter their
+        # big-M GEMMs as bf16, like every other activation gradient
+        dk16 = [dkvv[l] if direct16[l] else torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev)
+                for l in range(len(layers))]
+        dt16 = [torch.empty(Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None for _ in layers]
+        ks = aux_stream(dev, "decoder_kv") if _KV_ASYNC else main
+        first = [True]
+
+        def memory_dx(l):
+            """dv (+)= dK/dV_l W_kv,l, dtt likewise: layer l's K/V gradients are complete once step 0's
+            sweep has passed it (the first layer issued writes, the rest add)."""
+            if ks is not main:
+                ks.wait_stream(main)
+            with torch.cuda.stream(ks):
+                if not direct16[l]:
+                    K.cast_bf16(dkvv[l], dk16[l])
+                if Lt:
+                    K.cast_bf16(dkvt[l], dt16[l])
+                w = flat.w16(layers[l].multihead_attn.in_proj_weight)[E:]
+                K.linear_dx(dk16[l], w, out=dv, accumulate=not first[0])
+                if Lt:
+                    K.linear_dx(dt16[l], w, out=dtt, accumulate=not first[0])
+            first[0] = False
+
         for i in reversed(range(S)):
             tsum, mu, ru = fused[i]
             du = K.dropout_bwd(ds, p, seed + 7 + 64 * 1000 * (i + 1)) if p > 0 else ds
@@ -406,26 +454,15 @@ class _RecurrentDecoderFn(torch.autograd.Function):
                 dx = _layer_bwd(layers[l], flat, saves[i][l], dx, dkvv[l].view(-1)[i * 150 * 2 * E:],
                                 dkvt[l].view(-1) if Lt else None, S, Lt, p, seed + 64 * (i * len(layers) + l),
                                 grads[l], i)
+                if i == 0:
+                    memory_dx(l)
             ds = K.dropout(dx, 0.0, 0, res=dt)   # s fed both the residual and the decoder
             saves[i] = None
-        main = torch.cuda.current_stream(dev)
-        dv = torch.empty(B * S * 150, E, device=dev)     # the first layer's GEMM writes, the rest add
-        dtt = torch.empty(Bq * Lt, E, device=dev) if Lt else None
-        # the memory-side K/V gradients (accumulated in f32 over steps / answer choices) enter their
-        # big-M GEMMs as bf16, like every other activation gradient
-        dk16 = [dkvv[l] if direct16[l] else torch.empty(B * S * 150, 2 * E, dtype=torch.bfloat16, device=dev)
-                for l in range(len(layers))]
-        dt16 = [torch.empty(Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None for _ in layers]
-        for l in range(len(layers)):
-            if not direct16[l]:
-                K.cast_bf16(dkvv[l], dk16[l])
-            if Lt:
-                K.cast_bf16(dkvt[l], dt16[l])
-        for l, lay in enumerate(layers):
-            w = flat.w16(lay.multihead_attn.in_proj_weight)[E:]
-            K.linear_dx(dk16[l], w, out=dv, accumulate=l > 0)
-            if Lt:
-                K.linear_dx(dt16[l], w, out=dtt, accumulate=l > 0)
+        if ks is not main:
+            main.wait_stream(ks)
+            for x in [dv, dtt] + dk16 + dt16 + dkvv + dkvt:
+                if x is not None:
+                    x.record_stream(ks)
         # The weight gradients (query-side outer products over all steps, memory K/V projections,
         # the summary token) feed nothing downstream: a second stream runs them — and then the
         # decoder's optimizer update, which rewrites the weights dv / dt were just computed with —
