@@ -165,6 +165,35 @@ def test_fused_decoder_blocks_match_unfused(task, L, ncls, B, drop, monkeypatch)
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]
 
 
+@pytest.mark.parametrize("task", ["oe", "mc"])
+def test_decoder_kv_stream_is_bit_identical(task, monkeypatch):
+    """The memory-side K/V projections and their input-gradient GEMMs on the "decoder_kv" stream
+    (fusionv3._KV_ASYNC) run the same launches in the same order as in line: logits and every gradient
+    bit-identical, in train mode with dropout on."""
+    from lrce.models import fusionv3 as F
+    cls = {"oe": F.LRCEOpenEnded, "mc": F.LRCEMultipleChoice}[task]
+    torch.manual_seed(3)
+    L, B = (32, 3) if task == "oe" else (40, 2)
+    m = cls(768, 1000 if task == "oe" else 1, 0.1, (7, 7), 1024, 5, [3], L).cuda().train()
+    vf = torch.randn(B, 3, 3, 49, 1024, device="cuda")
+    tf = torch.randn(B, L, 768, device="cuda") if task == "oe" else torch.randn(B, 5, L, 768, device="cuda")
+    runs = []
+    for on in (False, True):
+        monkeypatch.setattr(F, "_KV_ASYNC", on)
+        m.zero_grad(set_to_none=True)
+        vg, tg = vf.clone().requires_grad_(True), tf.clone().requires_grad_(True)
+        torch.manual_seed(11)
+        y = m(vg, tg, None)
+        R = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).cuda()
+        (y.float() * R).sum().backward()
+        torch.cuda.synchronize()
+        runs.append([y.detach().float().clone(), vg.grad.clone(), tg.grad.clone()] +
+                    [p.grad.detach().clone() for p in m.parameters() if p.grad is not None])
+    assert len(runs[0]) == len(runs[1])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
 def _e2e(name, ts=(3,)):
     from lrce.models import e2e
     task, ncls, L = CFG[name]

@@ -60,7 +60,6 @@ struct GemmP {
   float drop_p;
   uint64_t drop_seed;
   const uint64_t* rng_off;
-  int stagger;   // (experiment, LRCE_GEMM_STAGGER) s_sleep(127) rounds for the second workgroup slot of a CU in the first round
 };
 
 // Debug phase marks of gemm_glds_kernel (tools/gemm_trace.py): wave 0 of every workgroup stores
@@ -605,8 +604,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   int tm, tn;
   tile_of(p, lin, tm, tn);
   const int m0 = tm * TBM, n0 = tn * TBN;
-  if (p.stagger > 0 && blockIdx.y == 0 && blockIdx.x >= 256 && blockIdx.x < 512)
-    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   GT_MARK(0);
 #ifdef LRCE_GEMM_TRACE
   if (p.trace && threadIdx.x == 0 && blockIdx.y == 0) {
@@ -1170,8 +1167,6 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   p.f16 = d->f16 ? 1 : 0;
   p.drop_p = d->drop_p > 0.f ? d->drop_p : 0.f;
   p.drop_seed = d->drop_seed;
-  static const int g_stagger = getenv("LRCE_GEMM_STAGGER") ? atoi(getenv("LRCE_GEMM_STAGGER")) : 0;   // experiment knob
-  p.stagger = g_stagger;
   p.rng_off = p.drop_p > 0.f ? lrce_rng_offset() : nullptr;
   if (p.f16 && !glds_ok(d))
     return lrce_fail(LRCE_E_ARG, "gemm: f16 needs 16-B aligned bf16-layout operands (LDS-DMA path)");

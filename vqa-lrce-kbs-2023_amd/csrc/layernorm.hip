@@ -152,8 +152,8 @@ struct F16Scaled {
   const uint64_t* off;
 };
 
-template <typename TD, typename TX, int CH, int LPR, bool F16S = false, bool PF2 = false>
-__global__ void __launch_bounds__(256, PF2 ? 3 : 1) ln_bwd(const TD* dy, const int* dy_map, const TX* x, const int* in_map, int nseg,
+template <typename TD, typename TX, int CH, int LPR, bool F16S = false>
+__global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, const TX* x, const int* in_map, int nseg,
                                               const float* mean_i, const float* rstd_i, const float* w, float* dx,
                                               const float* dres, float* dw, float* db, int rows, int cols, bf16* dx16,
                                               const int* dx16_map, const float* dsc, int dsc_rps, float* part,
@@ -210,29 +210,12 @@ __global__ void __launch_bounds__(256, PF2 ? 3 : 1) ln_bwd(const TD* dy, const i
   const float s16 = F16S ? fs.scale[0] / (fs.p > 0.f ? 1.0f - fs.p : 1.0f) : 0.f;
   const uint64_t dseed = F16S && fs.p > 0.f ? lrce_seed(fs.seed, fs.off) : 0ull;
   if (r0 < rows) fetch(r0, xcur, dcur, rcur, mcur, scur, pcur);
-  // PF2: the row after next is in flight too (two rows of loads per wave: a wave walks 5-6 rows, each
-  // otherwise waiting a full memory round trip for the one prefetched row)
-  float4 x2[PF2 ? CH : 1], d2[PF2 ? CH : 1], r2[PF2 ? CH : 1];
-  float m2 = 0.f, s2 = 0.f;
-  bool p2 = false;
-  if constexpr (PF2) {
-    if (r0 + stride < rows) fetch(r0 + stride, x2, d2, r2, m2, s2, p2);
-  }
   for (; r0 < rows; r0 += stride) {
     float4 xnx[CH], dnx[CH], rnx[CH];
     float mnx = 0.f, snx = 0.f;
     bool pnx = false;
     const bool more = r0 + stride < rows;
-    if constexpr (PF2) {
-      if (more) {
-#pragma unroll
-        for (int t = 0; t < CH; ++t) { xnx[t] = x2[t]; dnx[t] = d2[t]; rnx[t] = r2[t]; }
-        mnx = m2; snx = s2; pnx = p2;
-      }
-      if (r0 + 2 * stride < rows) fetch(r0 + 2 * stride, x2, d2, r2, m2, s2, p2);
-    } else {
-      if (more) fetch(r0 + stride, xnx, dnx, rnx, mnx, snx, pnx);
-    }
+    if (more) fetch(r0 + stride, xnx, dnx, rnx, mnx, snx, pnx);
     const int r = r0 + lane / LPR;
     const bool live = r < rows && !pcur;
     const float mean = mcur, rstd = scur;
@@ -479,12 +462,8 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
   float* part = want && nb_ws > 1 && workspace && workspace_elems >= (int64_t)(nb_ws + ny) * 2 * cols + LN_RED_CTRS
                     ? workspace : nullptr;
   const int nb = (part || !want) ? nb_ws : ln_bwd_blocks(rows, lpr, false, cols);
-  static const bool pf2 = getenv("LRCE_LN_PF2") ? atoi(getenv("LRCE_LN_PF2")) != 0 : false;   // A/B knob
 #define LNB3(TD, TX, CH, LPR)                                                                                          \
-  if (pf2) ln_bwd<TD, TX, CH, LPR, false, true><<<nb, 256, 0, s>>>(static_cast<const TD*>(dy), dy_map,            \
-      static_cast<const TX*>(x), in_map, nseg, mean, rstd, w, dx, dres, dw, db, rows, cols,                        \
-      reinterpret_cast<bf16*>(dx_bf16), dx_bf16_map, dx_scale, dx_scale_rps, part);                               \
-  else ln_bwd<TD, TX, CH, LPR><<<nb, 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, \
+  ln_bwd<TD, TX, CH, LPR><<<nb, 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, \
                                                      nseg, mean, rstd, w, dx, dres, dw, db, rows, cols,      \
                                                      reinterpret_cast<bf16*>(dx_bf16), dx_bf16_map, dx_scale, dx_scale_rps, \
                                                      part)

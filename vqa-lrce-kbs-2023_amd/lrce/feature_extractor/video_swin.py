@@ -320,30 +320,6 @@ def _bin_rows(at, window):
 
 
 _HANDOFF = True   # tests switch it off to compare against the separate scale-cast launch
-# A block's four weight-gradient GEMMs feed nothing downstream: they run on the weight-gradient
-# stream (with the stage's early optimizer update behind them) while this stream continues down the
-# input-gradient chain (A/B knob LRCE_SWIN_WGRAD_ASYNC=0: in line)
-_WGRAD_ASYNC = os.environ.get("LRCE_SWIN_WGRAD_ASYNC", "1") != "0"
-
-
-class _WgradIssuer:
-    """_wgrad on the "decoder_wgrad" stream after the current stream's work so far (the operands' and
-    every earlier gradient's producers), the operands kept alive for that stream; in line when off."""
-
-    def __init__(self, flat, dev):
-        self.flat = flat
-        self.main = torch.cuda.current_stream(dev)
-        self.ws = aux_stream(dev, "decoder_wgrad") if _WGRAD_ASYNC else None
-
-    def __call__(self, lin, dy16, x16):
-        if self.ws is None:
-            _wgrad(self.flat, lin, dy16, x16)
-            return
-        self.ws.wait_stream(self.main)
-        with torch.cuda.stream(self.ws):
-            _wgrad(self.flat, lin, dy16, x16)
-        dy16.record_stream(self.ws)
-        x16.record_stream(self.ws)
 
 
 class _Handoff:
@@ -477,11 +453,10 @@ class _SwinBlockFn(torch.autograd.Function):
         # next block's LN1 backward when there is one
         if dout16 is None:
             dout16 = K.scale_cast_bf16(dout, dp2, rpc)
-        wgrad = _WgradIssuer(flat, dout.device)
-        wgrad(blk.mlp.fc2, dout16, g)
+        _wgrad(flat, blk.mlp.fc2, dout16, g)
         dpre = K.linear_dx(dout16, flat.w16(blk.mlp.fc2.weight), out_f32=False, dgelu_pre=pre)
         del g, pre, dout16
-        wgrad(blk.mlp.fc1, dpre, h2)
+        _wgrad(flat, blk.mlp.fc1, dpre, h2)
         # the LayerNorms' input gradients arrive as bf16 GEMM outputs (as under the reference's
         # autocast, where a bf16 linear's grad_input is bf16): half the bytes of the LN backward's dy;
         # rows of >= 1024 columns keep f32 (the LN backward's bf16 loads measured slower there)
@@ -496,7 +471,7 @@ class _SwinBlockFn(torch.autograd.Function):
                         dx16=dmid16, dx16_map=ctx.sp2win, dx_scale=dp1, dx_scale_rps=rpc)
         del dh2
         # attention branch: x_mid = x + s1 * unwindow(proj(attn(qkv(LN1(window(x))))))
-        wgrad(at.proj, dmid16, o)
+        _wgrad(flat, at.proj, dmid16, o)
         do = K.linear_dx(dmid16, flat.w16(at.proj.weight), out_f32=False)
         del dmid16
         dqkv = torch.empty_like(qkv)
@@ -507,7 +482,7 @@ class _SwinBlockFn(torch.autograd.Function):
         if gt is not None:
             K.wattn_dbias(dbp, geo.n_win, nH, geo.ws, _bin_rows(at, geo.ws), gt)
         del dbp
-        wgrad(at.qkv, dqkv, xw)
+        _wgrad(flat, at.qkv, dqkv, xw)
         dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight), out_f32=C >= _LN_F32_WIDE)
         del dqkv, qkv, xw
         dx = torch.empty_like(x)
@@ -522,15 +497,7 @@ class _SwinBlockFn(torch.autograd.Function):
         if up is not None:
             up.put(dx, dx16)
         ctx.save = ctx.up = ctx.down = None
-        if wgrad.ws is not None:
-            # the block's gradients are final on the weight-gradient stream once it has caught up with
-            # this one (the LayerNorm parameter gradients): a gradient bucket completed here is cast /
-            # exchanged from there
-            wgrad.ws.wait_stream(wgrad.main)
-            with torch.cuda.stream(wgrad.ws):
-                flat.notify(blk.parameters())
-        else:
-            flat.notify(blk.parameters())
+        flat.notify(blk.parameters())
         group = getattr(blk, "_lrce_group", None)
         if group is not None and flat.early_update is not None:
             # this stage's gradients are final: its optimizer update runs on the decoder's weight-
