@@ -187,6 +187,21 @@ int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map,
  * partials, then a reduce whose last-arriving block per column adds the chunk sums in order) instead
  * of same-address atomics from every block (a NULL or smaller workspace falls back to the atomics). */
 int64_t lrce_layernorm_bwd_workspace(int rows, int cols);
+/* lrce_layernorm_bwd without its gamma / beta reduction launch: *nb_out = the number of per-block partial
+ * rows left in workspace (0: none were needed — a one-block problem, no dw / db, or no workspace — and
+ * dw / db are already final).  With nb_out > 0 the caller keeps the workspace and later passes
+ * (workspace, nb_out, cols, dw, db) to lrce_layernorm_grad_reduce, which many LayerNorms share: a
+ * stage's LayerNorm parameter gradients then cost one launch instead of one per LayerNorm. */
+int lrce_layernorm_bwd_deferred(const void* dy, int dy_f32, const int32_t* dy_map, const void* x, int x_f32,
+                                const int32_t* in_map, int nseg, const float* mean, const float* rstd, const float* w,
+                                float* dx, const float* dres, float* dw, float* db, int rows, int cols,
+                                uint16_t* dx_bf16, const int32_t* dx_bf16_map, const float* dx_scale, int dx_scale_rps,
+                                float* workspace, int64_t workspace_elems, int* nb_out, void* stream);
+/* dw[i][c] += sum_b part_i[b][c], db[i][c] += sum_b part_i[b][cols_i + c] for n deferred LayerNorm
+ * backwards (parts[i] / nbs[i] / cols[i] as lrce_layernorm_bwd_deferred left them; dw[i] or db[i] may be
+ * NULL): up to 40 per launch, each summed in block order exactly as lrce_layernorm_bwd does (same bits). */
+int lrce_layernorm_grad_reduce(const float* const* parts, const int32_t* nbs, const int32_t* cols, float* const* dw,
+                               float* const* db, int n, void* stream);
 
 /* ---------------------------------------------------------------- Swin 3D window attention
  * Replaces WindowAttention3D.forward video_swin_ori.py:164-186 (QK^T, relative-position bias,
@@ -237,6 +252,11 @@ int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dou
  * entry written by one thread, no atomics. */
 int lrce_wattn_dbias(float* dbias_part, int n_win, int nH, int n_bins, const int32_t* bin_row, float* table_grad,
                      void* stream);
+/* lrce_wattn_dbias for n blocks at once (item i: dbias_part[i], n_win[i], nH[i], n_bins[i], bin_row[i],
+ * table_grad[i]; up to 24 per pair of launches): the same sums in the same order (same bits), two
+ * launches for all of a stage's blocks instead of two per block. */
+int lrce_wattn_dbias_batched(float* const* dbias_part, const int32_t* n_win, const int32_t* nH, const int32_t* n_bins,
+                             const int32_t* const* bin_row, float* const* table_grad, int n, void* stream);
 
 /* ---------------------------------------------------------------- small multi-head attention
  * Masked SDPA, head_dim 64, for BERT self-attention (text.py:12-17 -> HF BertSelfAttention, L<=64)
@@ -511,6 +531,12 @@ int lrce_grad_scale_update(float* scale, int n_slots, void* stream);
 int lrce_layernorm_bwd_f16s(const float* dy, const float* x, const float* mean, const float* rstd, const float* w,
                             float* dx, float* dw, float* db, int rows, int cols, uint16_t* dx_f16, float* scale,
                             float p, uint64_t seed, float* workspace, int64_t workspace_elems, void* stream);
+/* lrce_layernorm_bwd_f16s with its gamma / beta reduction left to lrce_layernorm_grad_reduce (*nb_out as
+ * lrce_layernorm_bwd_deferred): the BERT backward reduces all its LayerNorms in one launch. */
+int lrce_layernorm_bwd_f16s_deferred(const float* dy, const float* x, const float* mean, const float* rstd,
+                                     const float* w, float* dx, float* dw, float* db, int rows, int cols,
+                                     uint16_t* dx_f16, float* scale, float p, uint64_t seed, float* workspace,
+                                     int64_t workspace_elems, int* nb_out, void* stream);
 /* dx_f16 = fp16(scale[0] * dropout_bwd(dy)) (p = 0: a scaled cast): the fp16 operand of the BERT
  * backward GEMMs from an f32 residual-stream gradient. */
 int lrce_dropout_bwd_f16(const float* dy, uint16_t* dx_f16, int64_t n, float p, uint64_t seed, int64_t group,

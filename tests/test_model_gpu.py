@@ -194,6 +194,32 @@ def test_decoder_kv_stream_is_bit_identical(task, monkeypatch):
         assert torch.equal(a, b)
 
 
+def test_swin_deferred_reductions_are_bit_identical(monkeypatch):
+    """A stage's LayerNorm gamma / beta and relative-position bias-table gradient reductions deferred to
+    batched launches at the stage's first block (video_swin._DEFER_REDUCTIONS: lrce_layernorm_grad_reduce,
+    lrce_wattn_dbias_batched) sum the same partials in the same order as one launch per LayerNorm /
+    block: every Swin gradient bit-identical, DropPath on."""
+    from lrce.feature_extractor import video_swin as VS
+    from lrce.feature_extractor.video import VideoExtractor
+    torch.manual_seed(0)
+    ve = VideoExtractor(None).cuda().train()
+    clips = torch.rand(1, 2, 5, 3, 224, 224, device="cuda")   # 3 x 7 x 7 windows (the bench clips)
+    runs = []
+    for on in (False, True):
+        monkeypatch.setattr(VS, "_DEFER_REDUCTIONS", on)
+        ve.zero_grad(set_to_none=True)
+        torch.manual_seed(7)
+        y = ve(clips)
+        R = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).cuda()
+        (y.float() * R).sum().backward()
+        torch.cuda.synchronize()
+        runs.append({k: p.grad.detach().clone() for k, p in ve.named_parameters() if p.grad is not None})
+    assert runs[0].keys() == runs[1].keys() and len(runs[0]) > 0
+    assert any("norm1" in k for k in runs[0]) and any("relative_position_bias_table" in k for k in runs[0])
+    bad = [k for k in runs[0] if not torch.equal(runs[0][k], runs[1][k])]
+    assert not bad, bad[:10]
+
+
 def _e2e(name, ts=(3,)):
     from lrce.models import e2e
     task, ncls, L = CFG[name]

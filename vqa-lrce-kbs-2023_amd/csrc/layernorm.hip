@@ -341,17 +341,16 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
 // The hand-off is MI355X_MICROARCH.md's first-row sc1 form (relaxed agent-scope stores drained by
 // vmcnt(0), a barrier, one agent atomic add, agent-scope relaxed loads in the last arriver): measured
 // gfx950 behaviour, not a C++ memory-model release/acquire pair (see decoder.hip publish_partial).
-__global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ part, int nb, int cols, float* dw, float* db,
-                                                     float* chunk, unsigned* counters) {
+__device__ __forceinline__ void ln_reduce_body(const float* __restrict__ part, int nb, int cols, float* dw, float* db,
+                                               float* chunk, unsigned* counters, int bx, int by, int ny) {
   __shared__ float red[4][64];
   __shared__ unsigned last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + lane;
-  const int ny = gridDim.y;
+  const int e = bx * 64 + lane;
   float t = 0.f;
 #pragma unroll
   for (int q = 0; q < LN_RED_ROWS / 32; ++q) {
-    const int b0 = blockIdx.y * LN_RED_ROWS + q * 32 + wave * 8;
+    const int b0 = by * LN_RED_ROWS + q * 32 + wave * 8;
     float v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = (e < 2 * cols && b0 + u < nb) ? part[(long long)(b0 + u) * 2 * cols + e] : 0.f;
@@ -361,12 +360,12 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ p
   red[wave][lane] = t;
   __syncthreads();
   if (wave == 0 && e < 2 * cols)
-    __hip_atomic_store(chunk + (long long)blockIdx.y * 2 * cols + e, (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]),
+    __hip_atomic_store(chunk + (long long)by * 2 * cols + e, (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(&counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(ny - 1);
+    last = __hip_atomic_fetch_add(&counters[bx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(ny - 1);
   __syncthreads();
   if (!last || wave != 0 || e >= 2 * cols) return;
   float cv[LN_RED_MAXY];
@@ -378,6 +377,31 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ p
   for (int y = 0; y < LN_RED_MAXY; ++y) s += cv[y];
   float* dst = e < cols ? (dw ? dw + e : nullptr) : (db ? db + (e - cols) : nullptr);
   if (dst) *dst += s;
+}
+__global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ part, int nb, int cols, float* dw, float* db,
+                                                     float* chunk, unsigned* counters) {
+  ln_reduce_body(part, nb, cols, dw, db, chunk, counters, blockIdx.x, blockIdx.y, gridDim.y);
+}
+
+// Many LayerNorms' deferred reductions in one launch (lrce_layernorm_grad_reduce): blockIdx.z picks the
+// item, (x, y) as ln_bwd_reduce over that item's partials; blocks past an item's grid return at once.
+struct LnRedItem {
+  const float* part;
+  float* dw;
+  float* db;
+  int nb, cols;
+};
+constexpr int LN_RED_BATCH = 40;
+struct LnRedBatch {
+  LnRedItem it[LN_RED_BATCH];
+};
+__global__ void __launch_bounds__(256) ln_bwd_reduce_batched(LnRedBatch b) {
+  const LnRedItem& it = b.it[blockIdx.z];
+  const int ny = (it.nb + LN_RED_ROWS - 1) / LN_RED_ROWS;
+  if ((int)blockIdx.x * 64 >= 2 * it.cols || (int)blockIdx.y >= ny) return;   // uniform over the block
+  float* chunk = const_cast<float*>(it.part) + (long long)it.nb * 2 * it.cols;
+  unsigned* ctr = reinterpret_cast<unsigned*>(chunk + (long long)ny * 2 * it.cols);
+  ln_reduce_body(it.part, it.nb, it.cols, it.dw, it.db, chunk, ctr, blockIdx.x, blockIdx.y, ny);
 }
 
 // rows per wave of ln_bwd: small inputs (the decoder / BERT rows) one row per wave (latency-bound:
@@ -440,11 +464,12 @@ extern "C" int lrce_layernorm_fwd(const void* x, int x_f32, const int32_t* in_ma
   return lrce_check_launch("layernorm_fwd");
 }
 
-extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map, const void* x, int x_f32,
-                                  const int32_t* in_map, int nseg, const float* mean, const float* rstd, const float* w,
-                                  float* dx, const float* dres, float* dw, float* db, int rows, int cols, uint16_t* dx_bf16,
-                                  const int32_t* dx_bf16_map, const float* dx_scale, int dx_scale_rps, float* workspace,
-                                  int64_t workspace_elems, void* stream) {
+static int layernorm_bwd_impl(const void* dy, int dy_f32, const int32_t* dy_map, const void* x, int x_f32,
+                              const int32_t* in_map, int nseg, const float* mean, const float* rstd, const float* w,
+                              float* dx, const float* dres, float* dw, float* db, int rows, int cols, uint16_t* dx_bf16,
+                              const int32_t* dx_bf16_map, const float* dx_scale, int dx_scale_rps, float* workspace,
+                              int64_t workspace_elems, void* stream, int* defer_nb) {
+  if (defer_nb) *defer_nb = 0;
   if (!dy || !x || !mean || !rstd || !w || (!dx && !dx_bf16)) return lrce_fail(LRCE_E_ARG, "layernorm_bwd: null pointer");
   if (dx_scale_rps < 1) dx_scale_rps = 1;
   if (nseg < 1) nseg = 1;
@@ -480,18 +505,63 @@ extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_
   else { LNB(bf16, bf16) }
 #undef LNB
 #undef LNB3
-  if (part)
+  if (part && defer_nb) *defer_nb = nb;   // the caller reduces later (lrce_layernorm_grad_reduce)
+  else if (part)
     ln_bwd_reduce<<<dim3((2 * cols + 63) / 64, ny), 256, 0, s>>>(
         part, nb, cols, dw, db, part + (long long)nb * 2 * cols, reinterpret_cast<unsigned*>(part + (long long)(nb + ny) * 2 * cols));
   return lrce_check_launch("layernorm_bwd");
 }
 
+extern "C" int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map, const void* x, int x_f32,
+                                  const int32_t* in_map, int nseg, const float* mean, const float* rstd, const float* w,
+                                  float* dx, const float* dres, float* dw, float* db, int rows, int cols, uint16_t* dx_bf16,
+                                  const int32_t* dx_bf16_map, const float* dx_scale, int dx_scale_rps, float* workspace,
+                                  int64_t workspace_elems, void* stream) {
+  return layernorm_bwd_impl(dy, dy_f32, dy_map, x, x_f32, in_map, nseg, mean, rstd, w, dx, dres, dw, db, rows, cols, dx_bf16,
+                            dx_bf16_map, dx_scale, dx_scale_rps, workspace, workspace_elems, stream, nullptr);
+}
+
+extern "C" int lrce_layernorm_bwd_deferred(const void* dy, int dy_f32, const int32_t* dy_map, const void* x, int x_f32,
+                                           const int32_t* in_map, int nseg, const float* mean, const float* rstd,
+                                           const float* w, float* dx, const float* dres, float* dw, float* db, int rows,
+                                           int cols, uint16_t* dx_bf16, const int32_t* dx_bf16_map, const float* dx_scale,
+                                           int dx_scale_rps, float* workspace, int64_t workspace_elems, int* nb_out,
+                                           void* stream) {
+  if (!nb_out) return lrce_fail(LRCE_E_ARG, "layernorm_bwd_deferred: null nb_out");
+  return layernorm_bwd_impl(dy, dy_f32, dy_map, x, x_f32, in_map, nseg, mean, rstd, w, dx, dres, dw, db, rows, cols, dx_bf16,
+                            dx_bf16_map, dx_scale, dx_scale_rps, workspace, workspace_elems, stream, nb_out);
+}
+
+extern "C" int lrce_layernorm_grad_reduce(const float* const* parts, const int32_t* nbs, const int32_t* cols,
+                                          float* const* dw, float* const* db, int n, void* stream) {
+  if (n < 0 || (n > 0 && (!parts || !nbs || !cols || !dw || !db))) return lrce_fail(LRCE_E_ARG, "layernorm_grad_reduce: args");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += LN_RED_BATCH) {
+    LnRedBatch b{};
+    const int m = n - i0 < LN_RED_BATCH ? n - i0 : LN_RED_BATCH;
+    int gx = 1, gy = 1;
+    for (int j = 0; j < m; ++j) {
+      const int i = i0 + j;
+      if (!parts[i] || nbs[i] < 2 || nbs[i] > LN_RED_MAXY * LN_RED_ROWS || cols[i] < 4 || cols[i] % 4 || (!dw[i] && !db[i]))
+        return lrce_fail(LRCE_E_ARG, "layernorm_grad_reduce: item %d (nb=%d cols=%d)", i, nbs[i], cols[i]);
+      b.it[j] = LnRedItem{parts[i], dw[i], db[i], nbs[i], cols[i]};
+      const int bx = (2 * cols[i] + 63) / 64, by = (nbs[i] + LN_RED_ROWS - 1) / LN_RED_ROWS;
+      gx = bx > gx ? bx : gx;
+      gy = by > gy ? by : gy;
+    }
+    ln_bwd_reduce_batched<<<dim3(gx, gy, m), 256, 0, s>>>(b);
+  }
+  return lrce_check_launch("layernorm_grad_reduce");
+}
+
 // lrce_layernorm_bwd + the scaled fp16 operand of the next GEMM in one pass (the BERT backward):
 // dx (f32, optional) and dx_f16 = fp16(S * dropout_bwd(dx)), S = scale[0]; max|dx| -> scale word 2
 // (lrce_grad_scale_update turns it into the next step's S).  Identity maps, no residual, f32 dy / x.
-extern "C" int lrce_layernorm_bwd_f16s(const float* dy, const float* x, const float* mean, const float* rstd, const float* w,
-                                       float* dx, float* dw, float* db, int rows, int cols, uint16_t* dx_f16, float* scale,
-                                       float p, uint64_t seed, float* workspace, int64_t workspace_elems, void* stream) {
+static int layernorm_bwd_f16s_impl(const float* dy, const float* x, const float* mean, const float* rstd, const float* w,
+                                   float* dx, float* dw, float* db, int rows, int cols, uint16_t* dx_f16, float* scale,
+                                   float p, uint64_t seed, float* workspace, int64_t workspace_elems, void* stream,
+                                   int* defer_nb) {
+  if (defer_nb) *defer_nb = 0;
   if (!dy || !x || !mean || !rstd || !w || !dx_f16 || !scale) return lrce_fail(LRCE_E_ARG, "layernorm_bwd_f16s: null pointer");
   if (cols % 4 || cols > 64 * 4 * MAXC || cols / 4 <= 32) return lrce_fail(LRCE_E_ARG, "layernorm_bwd_f16s: cols=%d", cols);
   if (rows <= 0) return LRCE_OK;
@@ -514,10 +584,27 @@ extern "C" int lrce_layernorm_bwd_f16s(const float* dy, const float* x, const fl
   else if (nch <= 256) LNBS(4);
   else LNBS(8);
 #undef LNBS
-  if (part)
+  if (part && defer_nb) *defer_nb = nb;
+  else if (part)
     ln_bwd_reduce<<<dim3((2 * cols + 63) / 64, ny), 256, 0, s>>>(
         part, nb, cols, dw, db, part + (long long)nb * 2 * cols, reinterpret_cast<unsigned*>(part + (long long)(nb + ny) * 2 * cols));
   return lrce_check_launch("layernorm_bwd_f16s");
+}
+
+extern "C" int lrce_layernorm_bwd_f16s(const float* dy, const float* x, const float* mean, const float* rstd, const float* w,
+                                       float* dx, float* dw, float* db, int rows, int cols, uint16_t* dx_f16, float* scale,
+                                       float p, uint64_t seed, float* workspace, int64_t workspace_elems, void* stream) {
+  return layernorm_bwd_f16s_impl(dy, x, mean, rstd, w, dx, dw, db, rows, cols, dx_f16, scale, p, seed, workspace,
+                                 workspace_elems, stream, nullptr);
+}
+
+extern "C" int lrce_layernorm_bwd_f16s_deferred(const float* dy, const float* x, const float* mean, const float* rstd,
+                                                const float* w, float* dx, float* dw, float* db, int rows, int cols,
+                                                uint16_t* dx_f16, float* scale, float p, uint64_t seed, float* workspace,
+                                                int64_t workspace_elems, int* nb_out, void* stream) {
+  if (!nb_out) return lrce_fail(LRCE_E_ARG, "layernorm_bwd_f16s_deferred: null nb_out");
+  return layernorm_bwd_f16s_impl(dy, x, mean, rstd, w, dx, dw, db, rows, cols, dx_f16, scale, p, seed, workspace,
+                                 workspace_elems, stream, nb_out);
 }
 
 extern "C" int64_t lrce_layernorm_bwd_workspace(int rows, int cols) {

@@ -642,6 +642,43 @@ __global__ void dbias_scatter_kernel(const float* __restrict__ red, int hb, int 
   tgrad[(long long)row * nH + h] += s;
 }
 
+// Several blocks' bias-table gradients in two launches (lrce_wattn_dbias_batched): blockIdx.z picks
+// the block (its bins, bin map, table gradient); the same two passes as above.
+struct DbItem {
+  float* part;
+  const int* bin_row;
+  float* tgrad;
+  int n_win, nH, nb;
+};
+constexpr int DB_BATCH = 24;
+struct DbBatch {
+  DbItem it[DB_BATCH];
+};
+__global__ void dbias_chunk_batched(DbBatch b) {
+  const DbItem& it = b.it[blockIdx.z];
+  const int hb = it.nH * it.nb;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= hb) return;
+  const int per = (it.n_win + WCH - 1) / WCH;
+  const int w0 = blockIdx.y * per, w1 = min(it.n_win, w0 + per);
+  float s = 0.f;
+  for (int w = w0; w < w1; ++w) s += it.part[(long long)w * hb + e];
+  it.part[(long long)it.n_win * hb + (long long)blockIdx.y * hb + e] = s;
+}
+__global__ void dbias_scatter_batched(DbBatch b) {
+  const DbItem& it = b.it[blockIdx.z];
+  const int hb = it.nH * it.nb;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= hb) return;
+  const int h = e / it.nb, row = it.bin_row[e % it.nb];
+  if (row < 0) return;
+  const float* red = it.part + (long long)it.n_win * hb;
+  float s = 0.f;
+#pragma unroll 8
+  for (int c = 0; c < WCH; ++c) s += red[(long long)c * hb + e];
+  it.tgrad[(long long)row * it.nH + h] += s;
+}
+
 }  // namespace
 
 static unsigned long long* g_wb_trace = nullptr;   // lrce_wattn_set_trace
@@ -725,4 +762,27 @@ extern "C" int lrce_wattn_dbias(float* dbias_part, int n_win, int nH, int n_bins
   dbias_chunk_kernel<<<dim3((unsigned)((hb + 255) / 256), WCH), 256, 0, st>>>(dbias_part, n_win, hb, red);
   dbias_scatter_kernel<<<(unsigned)((hb + 255) / 256), 256, 0, st>>>(red, hb, n_bins, nH, bin_row, table_grad);
   return lrce_check_launch("wattn_dbias");
+}
+
+extern "C" int lrce_wattn_dbias_batched(float* const* dbias_part, const int32_t* n_win, const int32_t* nH, const int32_t* n_bins,
+                                        const int32_t* const* bin_row, float* const* table_grad, int n, void* stream) {
+  if (n < 0 || (n > 0 && (!dbias_part || !n_win || !nH || !n_bins || !bin_row || !table_grad)))
+    return lrce_fail(LRCE_E_ARG, "wattn_dbias_batched: args");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += DB_BATCH) {
+    DbBatch b{};
+    const int m = n - i0 < DB_BATCH ? n - i0 : DB_BATCH;
+    int gx = 1;
+    for (int j = 0; j < m; ++j) {
+      const int i = i0 + j;
+      if (!dbias_part[i] || !bin_row[i] || !table_grad[i] || n_win[i] <= 0 || nH[i] <= 0 || n_bins[i] <= 0 || n_bins[i] > NBMAX)
+        return lrce_fail(LRCE_E_ARG, "wattn_dbias_batched: item %d (n_win=%d nH=%d n_bins=%d)", i, n_win[i], nH[i], n_bins[i]);
+      b.it[j] = DbItem{dbias_part[i], bin_row[i], table_grad[i], n_win[i], nH[i], n_bins[i]};
+      const int bx = (nH[i] * n_bins[i] + 255) / 256;
+      gx = bx > gx ? bx : gx;
+    }
+    dbias_chunk_batched<<<dim3((unsigned)gx, WCH, (unsigned)m), 256, 0, st>>>(b);
+    dbias_scatter_batched<<<dim3((unsigned)gx, 1, (unsigned)m), 256, 0, st>>>(b);
+  }
+  return lrce_check_launch("wattn_dbias_batched");
 }

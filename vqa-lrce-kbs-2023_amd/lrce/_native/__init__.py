@@ -154,6 +154,11 @@ _SIGS = {
     "lrce_wattn_qkv_fwd": [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_wattn_bwd": [_P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lrce_wattn_dbias": [_P, _I, _I, _I, _P, _P, _P],
+    "lrce_wattn_dbias_batched": [_P, _P, _P, _P, _P, _P, _I, _P],
+    "lrce_layernorm_bwd_deferred": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P,
+                                    _I64, _P, _P],
+    "lrce_layernorm_grad_reduce": [_P, _P, _P, _P, _P, _I, _P],
+    "lrce_layernorm_bwd_f16s_deferred": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _F, _U64, _P, _I64, _P, _P],
     "lrce_mha_fwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_mha_bwd": [ctypes.POINTER(MhaDesc), _P],
     "lrce_dec_sa_fwd": [ctypes.POINTER(DecSa), _P],

@@ -151,6 +151,9 @@ class _Stack:
         # GradScaler likewise keeps one scale across steps); LRCE_BERT_DELAYED_SCALE=0: per-step scales
         self.delayed = _DELAYED_SCALE and getattr(bert, "_lrce_scales_ready", False)
         self.done = []          # layer indices whose backward has run (their dY in dbuf)
+        # the layers' LayerNorm gamma / beta reductions, one batched launch at the flush (LRCE_BERT_LN_DEFER=0:
+        # one launch per LayerNorm); not with a gradient reducer (it would see the layers final too early)
+        self.red = K.DeferredGrads() if _LN_DEFER and getattr(flat, "reducer", None) is None else None
 
     def fviews(self, i):
         return _views(self.fbuf[i], self.rows, (HIDDEN,) * 6 + (INTER,) * 2)
@@ -227,10 +230,10 @@ class _LayerFn(torch.autograd.Function):
             K.grad_scale_update(st.scales)      # this step's scales from the last step's maxima
         if st.delayed:   # LN backward + the scaled fp16 operand in one launch (delayed scale)
             K.layernorm_bwd_f16s(dout, o2, m2, r2, oo.LayerNorm.weight, do2, do, sc[0], p, seed + 2,
-                                 dw=_g(flat, oo.LayerNorm.weight), db=_g(flat, oo.LayerNorm.bias))
+                                 dw=_g(flat, oo.LayerNorm.weight), db=_g(flat, oo.LayerNorm.bias), defer=st.red)
         else:
             K.layernorm_bwd(dout, o2, m2, r2, oo.LayerNorm.weight, do2, dw=_g(flat, oo.LayerNorm.weight),
-                            db=_g(flat, oo.LayerNorm.bias))
+                            db=_g(flat, oo.LayerNorm.bias), defer=st.red)
             K.grad_scale(do2, sc[0])
             K.dropout_bwd_f16(do2, p, seed + 2, sc[0], out=do)                            # S_f * d(o)
         K.linear_dx(do, w(oo.dense.weight), out=dh1, out_f32=False, dgelu_pre=pre)        # S_f * d(pre)
@@ -238,10 +241,10 @@ class _LayerFn(torch.autograd.Function):
         da2 = torch.empty_like(a2)
         if st.delayed:
             K.layernorm_bwd_f16s(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, da, sc[1], p, seed + 1,
-                                 dw=_g(flat, ao.LayerNorm.weight), db=_g(flat, ao.LayerNorm.bias))
+                                 dw=_g(flat, ao.LayerNorm.weight), db=_g(flat, ao.LayerNorm.bias), defer=st.red)
         else:
             K.layernorm_bwd(dh1x, a2, m1, r1, ao.LayerNorm.weight, da2, dw=_g(flat, ao.LayerNorm.weight),
-                            db=_g(flat, ao.LayerNorm.bias))
+                            db=_g(flat, ao.LayerNorm.bias), defer=st.red)
             K.grad_scale(da2, sc[1])
             K.dropout_bwd_f16(da2, p, seed + 1, sc[1], out=da)                            # S_a * d(a)
         dctx = K.linear_dx(da, w(ao.dense.weight), out_f32=False)                         # S_a * d(ctx)
@@ -256,6 +259,8 @@ class _LayerFn(torch.autograd.Function):
         st.done.append(i)
         if i == st.flush_at:
             _flush_wgrads(st)
+            if st.red is not None:
+                st.red.flush(dx)
             for j in st.done:
                 flat.notify(st.bert.encoder.layer[j].parameters())
             # a full backward has set every scale: later steps may use delayed scales
@@ -429,6 +434,7 @@ def _flush_wgrads(st):
 
 
 _WGRAD_BATCHED = os.environ.get("LRCE_BERT_WGRAD_BATCHED", "1") != "0"   # A/B knob
+_LN_DEFER = os.environ.get("LRCE_BERT_LN_DEFER", "1") != "0"             # A/B knob
 _DELAYED_SCALE = os.environ.get("LRCE_BERT_DELAYED_SCALE", "1") != "0"   # A/B knob
 
 

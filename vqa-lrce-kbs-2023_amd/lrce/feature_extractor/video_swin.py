@@ -345,14 +345,32 @@ class _Handoff:
         return dx16
 
 
+_DEFER_REDUCTIONS = os.environ.get("LRCE_SWIN_DEFER_RED", "1") != "0"   # A/B knob
+
+
+def _stage_deferral(blocks, flat):
+    """A DeferredGrads the stage's blocks share, or None: the LayerNorm gamma / beta and bias-table
+    gradient reductions of every block then run as batched launches when the backward reaches the
+    stage's first block (always the last of them, and present in the graph whenever its parameters
+    train).  Not with a gradient reducer: it launches a bucket's exchange as soon as a block reports its
+    parameters final."""
+    if not _DEFER_REDUCTIONS or getattr(flat, "reducer", None) is not None or not torch.is_grad_enabled():
+        return None
+    if not any(p.requires_grad for p in blocks[0].parameters()):
+        return None
+    return K.DeferredGrads()
+
+
 def _run_blocks(blocks, x, geo, flat, scales, tiles=None):
     """The blocks of one stage in order; scales [(dp1, dp2)] per block (None entries in eval);
     tiles: per block the (forward, backward) bias tiles built ahead (_prebuild_bias_tiles) or None."""
     links = [None] + [_Handoff(scales[j - 1][1]) if _HANDOFF else None for j in range(1, len(blocks))]
+    red = _stage_deferral(blocks, flat)
     for j, blk in enumerate(blocks):
         dp1, dp2 = scales[j]
         x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, links[j], links[j + 1] if j + 1 < len(blocks) else None,
-                               tiles[j] if tiles is not None else None, *blk.parameters())
+                               tiles[j] if tiles is not None else None, (red, j == 0) if red is not None else None,
+                               *blk.parameters())
     return x
 
 
@@ -397,10 +415,11 @@ class _SwinBlockFn(torch.autograd.Function):
     """One SwinTransformerBlock3D (video_swin_ori.py:248-306) forward / backward."""
 
     @staticmethod
-    def forward(ctx, x, blk, geo, flat, dp1, dp2, up, down, tiles, *params):
+    def forward(ctx, x, blk, geo, flat, dp1, dp2, up, down, tiles, red, *params):
         """up: the _Handoff this block's backward fills for the block before it; down: the one the
         block after it fills for this block (either None); tiles: prebuilt (forward, backward) bias
-        tiles or None (built here)."""
+        tiles or None (built here); red: (the stage's DeferredGrads, is the stage's first block) or
+        None (reductions launched in place)."""
         C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
         at = blk.attn
         shifted = geo.shifted and any(s > 0 for s in blk.shift_size)
@@ -435,7 +454,7 @@ class _SwinBlockFn(torch.autograd.Function):
         if any(t.requires_grad for t in (x,) + params):
             ctx.save = (x, xw, m1, r1, qkv, o, lse, x_mid, h2, m2, r2, pre, g, bias_b)
             ctx.blk, ctx.geo, ctx.flat, ctx.dp1, ctx.dp2 = blk, geo, flat, dp1, dp2
-            ctx.wmap, ctx.win_pat, ctx.up, ctx.down = wmap, win_pat, up, down
+            ctx.wmap, ctx.win_pat, ctx.up, ctx.down, ctx.red = wmap, win_pat, up, down, red
             ctx.sp2win = geo.sp2win_shift if shifted else geo.sp2win
         return out
 
@@ -446,6 +465,7 @@ class _SwinBlockFn(torch.autograd.Function):
         at = blk.attn
         C, nH, n, M = blk.dim, blk.num_heads, geo.n, geo.M
         rpc = geo.rows_per_clip
+        red, flush = ctx.red if ctx.red is not None else (None, False)
         dout16 = ctx.down.take(dout) if ctx.down is not None else None
         dout = dout.contiguous()
         # MLP branch: y = x_mid + s2 * fc2(gelu(fc1(LN2(x_mid)))).  The branch's GEMMs read the
@@ -468,7 +488,7 @@ class _SwinBlockFn(torch.autograd.Function):
         dmid16 = (torch.zeros if geo.padded else torch.empty)(geo.M_win, C, dtype=torch.bfloat16, device=dout.device)
         K.layernorm_bwd(dh2, x_mid, m2, r2, blk.norm2.weight, dx_mid, dres=dout,
                         dw=_g(flat, blk.norm2.weight), db=_g(flat, blk.norm2.bias),
-                        dx16=dmid16, dx16_map=ctx.sp2win, dx_scale=dp1, dx_scale_rps=rpc)
+                        dx16=dmid16, dx16_map=ctx.sp2win, dx_scale=dp1, dx_scale_rps=rpc, defer=red)
         del dh2
         # attention branch: x_mid = x + s1 * unwindow(proj(attn(qkv(LN1(window(x))))))
         _wgrad(flat, at.proj, dmid16, o)
@@ -480,7 +500,7 @@ class _SwinBlockFn(torch.autograd.Function):
         del do, o
         gt = _g(flat, at.relative_position_bias_table)
         if gt is not None:
-            K.wattn_dbias(dbp, geo.n_win, nH, geo.ws, _bin_rows(at, geo.ws), gt)
+            K.wattn_dbias(dbp, geo.n_win, nH, geo.ws, _bin_rows(at, geo.ws), gt, defer=red)
         del dbp
         _wgrad(flat, at.qkv, dqkv, xw)
         dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight), out_f32=C >= _LN_F32_WIDE)
@@ -493,10 +513,12 @@ class _SwinBlockFn(torch.autograd.Function):
         K.layernorm_bwd(dxw, x, m1, r1, blk.norm1.weight, dx, in_map=wmap, dres=dx_mid,
                         dw=_g(flat, blk.norm1.weight), db=_g(flat, blk.norm1.bias), dx16=dx16,
                         dx16_map=wmap if up is not None else None, dx_scale=up.scale if up is not None else None,
-                        dx_scale_rps=geo.win_rows_per_clip)
+                        dx_scale_rps=geo.win_rows_per_clip, defer=red)
         if up is not None:
             up.put(dx, dx16)
-        ctx.save = ctx.up = ctx.down = None
+        if flush:
+            red.flush(dx)   # the stage's deferred LayerNorm / bias-table gradient sums
+        ctx.save = ctx.up = ctx.down = ctx.red = None
         flat.notify(blk.parameters())
         group = getattr(blk, "_lrce_group", None)
         if group is not None and flat.early_update is not None:
@@ -508,7 +530,7 @@ class _SwinBlockFn(torch.autograd.Function):
             s.wait_stream(main)
             with torch.cuda.stream(s):
                 flat.group_done(group)
-        return (dx, None, None, None, None, None, None, None, None) + (None,) * len(ctx.needs_input_grad[9:])
+        return (dx, None, None, None, None, None, None, None, None, None) + (None,) * len(ctx.needs_input_grad[10:])
 
 
 class _PatchMergeFn(torch.autograd.Function):

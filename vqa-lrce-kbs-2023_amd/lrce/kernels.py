@@ -326,10 +326,12 @@ def layernorm(x, w, b, eps, *, out=None, out_f32=False, in_map=None, nseg=1, out
 
 
 def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1, dres=None, dw=None, db=None,
-                  rows=None, cols=None, dx16=None, dx16_map=None, dx_scale=None, dx_scale_rps=1, workspace=True):
+                  rows=None, cols=None, dx16=None, dx16_map=None, dx_scale=None, dx_scale_rps=1, workspace=True,
+                  defer=None):
     """dx16: optional bf16 copy of dx (times dx_scale[r / dx_scale_rps], at row dx16_map[r]).
     workspace=False: dw/db by per-block atomics instead of the two-pass partials sum.
-    dx may be None when dx16 is given (returns dx16 then)."""
+    defer: a DeferredGrads — the dw / db reduction joins its batch (layernorm_grad_reduce at its flush)
+    instead of a launch of its own.  dx may be None when dx16 is given (returns dx16 then)."""
     R = rows if rows is not None else mean.shape[0]
     Cc = cols if cols is not None else w.shape[0]
     out = dx if dx is not None else dx16
@@ -337,10 +339,46 @@ def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1,
     if workspace and (dw is not None or db is not None):
         nws = N.lib().lrce_layernorm_bwd_workspace(R, Cc)
         ws = torch.empty(nws, dtype=F32, device=out.device) if nws > 0 else None
-    call("lrce_layernorm_bwd", ptr(dy), int(dy.dtype == F32), ptr(dy_map), ptr(x), int(x.dtype == F32), ptr(in_map),
-         nseg, ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dres), ptr(dw), ptr(db), R, Cc, ptr(dx16), ptr(dx16_map),
-         ptr(dx_scale), dx_scale_rps, ptr(ws), nws, stream_of(out))
+    args = (ptr(dy), int(dy.dtype == F32), ptr(dy_map), ptr(x), int(x.dtype == F32), ptr(in_map), nseg, ptr(mean),
+            ptr(rstd), ptr(w), ptr(dx), ptr(dres), ptr(dw), ptr(db), R, Cc, ptr(dx16), ptr(dx16_map), ptr(dx_scale),
+            dx_scale_rps, ptr(ws), nws)
+    if defer is None or ws is None:
+        call("lrce_layernorm_bwd", *args, stream_of(out))
+        return out
+    nb = ctypes.c_int(0)
+    call("lrce_layernorm_bwd_deferred", *args, ctypes.byref(nb), stream_of(out))
+    if nb.value > 0:
+        defer.ln.append((ws, nb.value, Cc, dw, db))
     return out
+
+
+class DeferredGrads:
+    """Parameter-gradient reductions that nothing downstream reads before the optimizer, collected over
+    several blocks and issued as batched launches by flush(): LayerNorm gamma / beta sums
+    (layernorm_bwd(defer=...)) and relative-position bias-table gradients (wattn_dbias(defer=...)).
+    Each sum is the one the immediate launch computes, in the same order (bit-identical)."""
+
+    def __init__(self):
+        self.ln, self.db = [], []
+
+    def flush(self, stream_tensor):
+        if self.ln:
+            n = len(self.ln)
+            arr = lambda vals, t: (t * n)(*vals)  # noqa: E731
+            call("lrce_layernorm_grad_reduce", ctypes.cast(arr([ptr(i[0]) for i in self.ln], ctypes.c_void_p), ctypes.c_void_p),
+                 ctypes.cast(arr([i[1] for i in self.ln], ctypes.c_int32), ctypes.c_void_p),
+                 ctypes.cast(arr([i[2] for i in self.ln], ctypes.c_int32), ctypes.c_void_p),
+                 ctypes.cast(arr([ptr(i[3]) for i in self.ln], ctypes.c_void_p), ctypes.c_void_p),
+                 ctypes.cast(arr([ptr(i[4]) for i in self.ln], ctypes.c_void_p), ctypes.c_void_p), n,
+                 stream_of(stream_tensor))
+        if self.db:
+            n = len(self.db)
+            arr = lambda vals, t: ctypes.cast((t * n)(*vals), ctypes.c_void_p)  # noqa: E731
+            call("lrce_wattn_dbias_batched", arr([ptr(i[0]) for i in self.db], ctypes.c_void_p),
+                 arr([i[1] for i in self.db], ctypes.c_int32), arr([i[2] for i in self.db], ctypes.c_int32),
+                 arr([i[3] for i in self.db], ctypes.c_int32), arr([ptr(i[4]) for i in self.db], ctypes.c_void_p),
+                 arr([ptr(i[5]) for i in self.db], ctypes.c_void_p), n, stream_of(stream_tensor))
+        self.ln, self.db = [], []
 
 
 def scale_cast_bf16(x, row_scale=None, rows_per_scale=1, out=None):
@@ -471,7 +509,11 @@ def wattn_bin_rows(index, window):
     return rows.to(torch.int32).to(index.device)
 
 
-def wattn_dbias(dbias_part, n_win, nH, window, bin_row, table_grad):
+def wattn_dbias(dbias_part, n_win, nH, window, bin_row, table_grad, defer=None):
+    """defer: a DeferredGrads — join its batched launch (the part buffer is kept until its flush)."""
+    if defer is not None:
+        defer.db.append((dbias_part, n_win, nH, wattn_n_bins(window), bin_row, table_grad))
+        return
     call("lrce_wattn_dbias", ptr(dbias_part), n_win, nH, wattn_n_bins(window), ptr(bin_row), ptr(table_grad),
          stream_of(table_grad))
 
@@ -665,17 +707,25 @@ def grad_scale_update(scales):
     call("lrce_grad_scale_update", ptr(scales), scales.numel() // 4, stream_of(scales))
 
 
-def layernorm_bwd_f16s(dy, x, mean, rstd, w, dx, out16, scale, p, seed, *, dw=None, db=None):
+def layernorm_bwd_f16s(dy, x, mean, rstd, w, dx, out16, scale, p, seed, *, dw=None, db=None, defer=None):
     """LayerNorm backward (f32 dy / x, identity maps) + out16 = fp16(scale[0] * dropout_bwd(dx)) in one
-    launch, max|dx| recorded into scale[2] for grad_scale_update (lrce_layernorm_bwd_f16s)."""
+    launch, max|dx| recorded into scale[2] for grad_scale_update (lrce_layernorm_bwd_f16s).  defer: a
+    DeferredGrads that takes the gamma / beta reduction (see layernorm_bwd)."""
     _chk(out16, F16, "out16"); _chk(scale, F32, "scale")
     R, Cc = mean.shape[0], w.shape[0]
     ws, nws = None, 0
     if dw is not None or db is not None:
         nws = N.lib().lrce_layernorm_bwd_workspace(R, Cc)
         ws = torch.empty(nws, dtype=F32, device=dy.device) if nws > 0 else None
-    call("lrce_layernorm_bwd_f16s", ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dw), ptr(db), R, Cc,
-         ptr(out16), ptr(scale), float(p), seed & (2 ** 64 - 1), ptr(ws), nws, stream_of(out16))
+    args = (ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(w), ptr(dx), ptr(dw), ptr(db), R, Cc, ptr(out16), ptr(scale),
+            float(p), seed & (2 ** 64 - 1), ptr(ws), nws)
+    if defer is None or ws is None:
+        call("lrce_layernorm_bwd_f16s", *args, stream_of(out16))
+        return dx
+    nb = ctypes.c_int(0)
+    call("lrce_layernorm_bwd_f16s_deferred", *args, ctypes.byref(nb), stream_of(out16))
+    if nb.value > 0:
+        defer.ln.append((ws, nb.value, Cc, dw, db))
     return dx
 
 

@@ -325,6 +325,12 @@ def _layer_wgrads(lay, flat, acts, grads, fused=False):
 # recurrence waits for layer l's K/V only when step 0 reaches layer l, and in the backward each layer's
 # memory-side input-gradient GEMMs start as soon as step 0's sweep has finished that layer.
 _KV_ASYNC = os.environ.get("LRCE_DEC_KV_ASYNC", "1") != "0"
+# Each layer's deferred weight gradients are issued on the weight-gradient stream as soon as step 0's
+# backward sweep has passed the layer (beside the rest of the latency-bound sweep) instead of all after
+# it (beside the Swin backward's full-chip GEMMs); LRCE_DEC_WGRAD_EARLY=1.  Measured slower than after the
+# sweep (same-box A/B 284.0 vs 286.4 QA-samples/s, profiles/r5_bench_defer_wgrad_early_ab.txt): the
+# weight-gradient kernels slow the latency-bound sweep they share the CUs with.  Off.
+_WGRAD_EARLY = os.environ.get("LRCE_DEC_WGRAD_EARLY", "0") == "1"   # measured slower (285.3 vs 286.4): off
 
 
 def _dev_layers(ft):
@@ -425,23 +431,43 @@ class _RecurrentDecoderFn(torch.autograd.Function):
                 for l in range(len(layers))]
         dt16 = [torch.empty(Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None for _ in layers]
         ks = aux_stream(dev, "decoder_kv") if _KV_ASYNC else main
+        wg = aux_stream(dev, "decoder_wgrad")
         first = [True]
+
+        def layer_wgrads(l, cast_done):
+            """Layer l's query-side weight / LayerNorm gradients over all steps and its K/V projection
+            weight gradients, on the weight-gradient stream (they feed nothing downstream)."""
+            wg.wait_stream(main)
+            if cast_done is not None:
+                wg.wait_event(cast_done)
+            lay = layers[l]
+            ca = lay.multihead_attn
+            with torch.cuda.stream(wg):
+                _layer_wgrads(lay, flat, acts[l], grads[l], fused=fused_layers[l])
+                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16[l], v16, rows=(E, 3 * E))
+                if Lt:
+                    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[l], t16, rows=(E, 3 * E))
 
         def memory_dx(l):
             """dv (+)= dK/dV_l W_kv,l, dtt likewise: layer l's K/V gradients are complete once step 0's
-            sweep has passed it (the first layer issued writes, the rest add)."""
+            sweep has passed it (the first layer issued writes, the rest add).  Returns the event of
+            the bf16 operand casts (None when in line)."""
             if ks is not main:
                 ks.wait_stream(main)
+            cast_done = None
             with torch.cuda.stream(ks):
                 if not direct16[l]:
                     K.cast_bf16(dkvv[l], dk16[l])
                 if Lt:
                     K.cast_bf16(dkvt[l], dt16[l])
+                if ks is not main:
+                    cast_done = ks.record_event()
                 w = flat.w16(layers[l].multihead_attn.in_proj_weight)[E:]
                 K.linear_dx(dk16[l], w, out=dv, accumulate=not first[0])
                 if Lt:
                     K.linear_dx(dt16[l], w, out=dtt, accumulate=not first[0])
             first[0] = False
+            return cast_done
 
         for i in reversed(range(S)):
             tsum, mu, ru = fused[i]
@@ -455,7 +481,9 @@ class _RecurrentDecoderFn(torch.autograd.Function):
                                 dkvt[l].view(-1) if Lt else None, S, Lt, p, seed + 64 * (i * len(layers) + l),
                                 grads[l], i)
                 if i == 0:
-                    memory_dx(l)
+                    cast_done = memory_dx(l)
+                    if _WGRAD_EARLY:
+                        layer_wgrads(l, cast_done)
             ds = K.dropout(dx, 0.0, 0, res=dt)   # s fed both the residual and the decoder
             saves[i] = None
         if ks is not main:
@@ -468,15 +496,11 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         # decoder's optimizer update, which rewrites the weights dv / dt were just computed with —
         # while the extractors' backward, which needs only dv / dt, proceeds on this one.  The
         # forward's stream anchor joins that stream back at the end of backward.
-        wg = aux_stream(dev, "decoder_wgrad")
+        if not _WGRAD_EARLY:
+            for l in range(len(layers)):
+                layer_wgrads(l, None)
         wg.wait_stream(main)
         with torch.cuda.stream(wg):
-            for l, lay in enumerate(layers):
-                ca = lay.multihead_attn
-                _layer_wgrads(lay, flat, acts[l], grads[l], fused=fused_layers[l])
-                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16[l], v16, rows=(E, 3 * E))
-                if Lt:
-                    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[l], t16, rows=(E, 3 * E))
             gt = _g(flat, ft.summarization_token)
             if gt is not None:
                 K.colsum(ds, gt.view(E))
