@@ -191,7 +191,10 @@ def test_early_updates_do_not_race_the_backward():
         F.cross_entropy(model(*b[:4]).float(), b[4]).backward()
         opt.step()
     torch.cuda.synchronize()
-    bufs = (flat.f32, opt.exp_avg, opt.exp_avg_sq, opt.sumsq, opt.step_t)
+    # BERT's delayed per-tensor gradient scales (the previous backward's maxima) are step state too:
+    # restored with the rest, every run scales its fp16 gradients alike
+    bufs = (flat.f32, opt.exp_avg, opt.exp_avg_sq, opt.sumsq, opt.step_t,
+            model.text_extractor.bert._grad_scales(flat.device))
     state = [t.clone() for t in bufs]
     count = opt.step_count
     w0 = flat.f32.clone()

@@ -169,7 +169,9 @@ def test_fused_decoder_blocks_match_unfused(task, L, ncls, B, drop, monkeypatch)
 def test_decoder_kv_stream_is_bit_identical(task, monkeypatch):
     """The memory-side K/V projections and their input-gradient GEMMs on the "decoder_kv" stream
     (fusionv3._KV_ASYNC) run the same launches in the same order as in line: logits and every gradient
-    bit-identical, in train mode with dropout on."""
+    bit-identical, in train mode with dropout on — except the video positional-embedding tables, whose
+    backward adds rows with float atomics (not bit-reproducible even between two identical runs,
+    tools/determinism_probe.py): those to f32 rounding."""
     from lrce.models import fusionv3 as F
     cls = {"oe": F.LRCEOpenEnded, "mc": F.LRCEMultipleChoice}[task]
     torch.manual_seed(3)
@@ -187,37 +189,57 @@ def test_decoder_kv_stream_is_bit_identical(task, monkeypatch):
         R = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).cuda()
         (y.float() * R).sum().backward()
         torch.cuda.synchronize()
-        runs.append([y.detach().float().clone(), vg.grad.clone(), tg.grad.clone()] +
-                    [p.grad.detach().clone() for p in m.parameters() if p.grad is not None])
-    assert len(runs[0]) == len(runs[1])
-    for a, b in zip(*runs):
-        assert torch.equal(a, b)
+        runs.append({"y": y.detach().float().clone(), "dv": vg.grad.clone(), "dt": tg.grad.clone(),
+                     **{k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}})
+    assert runs[0].keys() == runs[1].keys()
+    for k in runs[0]:
+        if k.startswith("video_pos_embed."):
+            assert rel(runs[1][k], runs[0][k]) < 1e-5, k
+        else:
+            assert torch.equal(runs[0][k], runs[1][k]), k
 
 
-def test_swin_deferred_reductions_are_bit_identical(monkeypatch):
+def _swin_grads(ve, clips):
+    ve.zero_grad(set_to_none=True)
+    torch.manual_seed(7)
+    y = ve(clips)
+    R = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).cuda()
+    (y.float() * R).sum().backward()
+    torch.cuda.synchronize()
+    return {k: p.grad.detach().clone() for k, p in ve.named_parameters() if p.grad is not None}
+
+
+def test_swin_deferred_reductions_and_weight_gradients(monkeypatch):
     """A stage's LayerNorm gamma / beta and relative-position bias-table gradient reductions deferred to
     batched launches at the stage's first block (video_swin._DEFER_REDUCTIONS: lrce_layernorm_grad_reduce,
     lrce_wattn_dbias_batched) sum the same partials in the same order as one launch per LayerNorm /
-    block: every Swin gradient bit-identical, DropPath on."""
+    block: every Swin gradient bit-identical, DropPath on.  The stage's weight gradients as one
+    pointer-table batched GEMM per linear (video_swin._DEFER_WGRAD, lrce_gemm_ptr_batched: one K slice
+    per tile instead of split-K slabs) change only the K summation order: f32 rounding."""
     from lrce.feature_extractor import video_swin as VS
     from lrce.feature_extractor.video import VideoExtractor
     torch.manual_seed(0)
     ve = VideoExtractor(None).cuda().train()
     clips = torch.rand(1, 2, 5, 3, 224, 224, device="cuda")   # 3 x 7 x 7 windows (the bench clips)
-    runs = []
-    for on in (False, True):
-        monkeypatch.setattr(VS, "_DEFER_REDUCTIONS", on)
-        ve.zero_grad(set_to_none=True)
-        torch.manual_seed(7)
-        y = ve(clips)
-        R = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).cuda()
-        (y.float() * R).sum().backward()
-        torch.cuda.synchronize()
-        runs.append({k: p.grad.detach().clone() for k, p in ve.named_parameters() if p.grad is not None})
-    assert runs[0].keys() == runs[1].keys() and len(runs[0]) > 0
-    assert any("norm1" in k for k in runs[0]) and any("relative_position_bias_table" in k for k in runs[0])
-    bad = [k for k in runs[0] if not torch.equal(runs[0][k], runs[1][k])]
+    monkeypatch.setattr(VS, "_DEFER_WGRAD", False)
+    monkeypatch.setattr(VS, "_DEFER_REDUCTIONS", False)
+    g0 = _swin_grads(ve, clips)
+    monkeypatch.setattr(VS, "_DEFER_REDUCTIONS", True)
+    g1 = _swin_grads(ve, clips)
+    monkeypatch.setattr(VS, "_DEFER_WGRAD", True)
+    g2 = _swin_grads(ve, clips)
+    assert g0.keys() == g1.keys() == g2.keys() and len(g0) > 0
+    assert any("norm1" in k for k in g0) and any("relative_position_bias_table" in k for k in g0)
+    bad = [k for k in g0 if not torch.equal(g0[k], g1[k])]
     assert not bad, bad[:10]
+    lin = (".qkv.", ".proj.", ".fc1.", ".fc2.")
+    bad = {}
+    for k in g0:
+        err = rel(g2[k], g0[k])
+        ok = err < 1e-5 if any(t in k for t in lin) else torch.equal(g2[k], g0[k])
+        if not ok:
+            bad[k] = err
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]
 
 
 def _e2e(name, ts=(3,)):

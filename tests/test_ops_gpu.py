@@ -1148,3 +1148,25 @@ def test_torch_library_decoder_recurrent():
     sv = torch.ops.lrce.decoder_recurrent(video.to(dev), None, params)
     refv = O.fusion_video(video, sd).reshape(B, 768)
     assert rel(sv.cpu(), refv) < 1e-2, rel(sv.cpu(), refv)
+
+
+def test_linear_dw_batched_matches_per_item():
+    """lrce_gemm_ptr_batched (a Swin stage's same-shape weight gradients as one launch, one K slice per
+    tile) against linear_dw per item (split-K slabs + reduce): dW and the bias gradient to f32 rounding,
+    including a K tail (T % 64 != 0) and entries at unrelated addresses."""
+    torch.manual_seed(0)
+    T, O, I, n = 1000, 256, 384, 5
+    items, ref = [], []
+    for j in range(n):
+        dy = torch.randn(T, O, device="cuda").to(torch.bfloat16)
+        x = torch.randn(T, I, device="cuda").to(torch.bfloat16)
+        dw = torch.randn(O, I, device="cuda")
+        db = torch.randn(O, device="cuda")
+        rw, rb = dw.clone(), db.clone()
+        K.linear_dw(dy, x, rw, bias_grad=rb)
+        items.append((dy, x, dw, db))
+        ref.append((rw, rb))
+    K.linear_dw_batched(items)
+    torch.cuda.synchronize()
+    for (dy, x, dw, db), (rw, rb) in zip(items, ref):
+        assert rel(dw, rw) < 1e-5 and rel(db, rb) < 1e-5

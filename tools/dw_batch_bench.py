@@ -1,0 +1,76 @@
+#!/usr/bin/env python
+"""Weight gradients of a Swin stage's blocks (dev tool, GPU): n_blocks separate split-K launches
+(linear_dw: f32 slabs + reduce, what the block backward issues) against ONE batched launch over the
+blocks (batch = n_blocks, one K slice per tile, ACCUM + BIAS_GRAD with per-batch strides), on the
+stage-3 shapes.  HIP events over back-to-back repetitions.
+
+    python tools/dw_batch_bench.py [--blocks 18] [--iters 5]
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "vqa-lrce-kbs-2023_amd"))
+import torch  # noqa: E402
+
+from lrce import kernels as K  # noqa: E402
+from lrce import _native as N  # noqa: E402
+
+# (name, out, in): dW[out, in] += dY[T, out]^T X[T, in] over T tokens
+SHAPES = [("qkv", 1536, 512), ("proj", 512, 512), ("fc1", 2048, 512), ("fc2", 512, 2048)]
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=18)
+    ap.add_argument("--tokens", type=int, default=17640)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    nb, T = a.blocks, a.tokens
+    bf = torch.bfloat16
+    total_sep = total_bat = 0.0
+    for name, O, I in SHAPES:
+        dy = torch.rand(nb, T, O, device="cuda").sub_(0.5).to(bf)
+        x = torch.rand(nb, T, I, device="cuda").sub_(0.5).to(bf)
+        dw = torch.zeros(nb, O, I, device="cuda")
+        db = torch.zeros(nb, O, device="cuda")
+
+        def sep():
+            for j in range(nb):
+                K.linear_dw(dy[j], x[j], dw[j], bias_grad=db[j])
+
+        def bat():
+            K.gemm(dy, x, dw, O, I, T, a_kmajor=False, b_kmajor=False, lda=O, ldb=I, ldc=I,
+                   flags=N.EPI_ACCUM | N.EPI_BIAS_GRAD, bias=db, batch=nb, stride_a=T * O, stride_b=T * I,
+                   stride_c=O * I, stride_bias=O)
+
+        # agreement: both from zero
+        dw.zero_(); db.zero_(); sep(); ref_w, ref_b = dw.clone(), db.clone()
+        dw.zero_(); db.zero_(); bat()
+        err = ((dw - ref_w).abs().max() / ref_w.abs().max()).item()
+        errb = ((db - ref_b).abs().max() / ref_b.abs().max()).item()
+        ts, tb = timed(sep, a.iters), timed(bat, a.iters)
+        total_sep += ts
+        total_bat += tb
+        fl = 2.0 * nb * T * O * I
+        print(f"{name:5s} {O:5d}x{I:5d}x{T}: {nb} split-K launches {ts:8.1f} us ({fl / ts / 1e6:6.1f} TF/s)   "
+              f"batched {tb:8.1f} us ({fl / tb / 1e6:6.1f} TF/s)   rel diff w {err:.1e} b {errb:.1e}", flush=True)
+    print(f"stage total: separate {total_sep:.1f} us, batched {total_bat:.1f} us")
+
+
+if __name__ == "__main__":
+    main()

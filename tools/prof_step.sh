@@ -10,4 +10,5 @@ db=$(ls /tmp/$tag/*/run_results.db /tmp/$tag/run_results.db 2>/dev/null | head -
 python $GRAFT_REPO_ROOT/tools/rocprof_summary.py $db --last 4 --top 60 > ${out}_stats.md
 (cd $GRAFT_REPO_ROOT/tools && python step_phases.py $db > ${out}_phases.txt && python text_branch.py $db --list > ${out}_text.txt)
 python $GRAFT_REPO_ROOT/tools/timeline_gaps.py $db > ${out}_gaps.txt 2>&1 || true
+(cd $GRAFT_REPO_ROOT/tools && python step_timeline.py $db > ${out}_timeline.txt 2>&1) || true
 rm -rf /tmp/$tag

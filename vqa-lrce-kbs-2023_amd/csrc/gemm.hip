@@ -62,6 +62,19 @@ struct GemmP {
   const uint64_t* rng_off;
 };
 
+// Pointer-table batch (lrce_gemm_ptr_batched): batch entry z reads A / B / C / bias from its own
+// pointers instead of base + z * stride — a Swin stage's per-block weight gradients as one launch
+// without copying the blocks' operands into uniformly strided buffers.
+constexpr int GPT = 24;
+struct GemmPT : GemmP {
+  const void* ta[GPT];
+  const bf16* tb[GPT];
+  void* tc[GPT];
+  const float* tbias[GPT];
+};
+template <bool PT>
+using GemmArg = typename std::conditional<PT, GemmPT, GemmP>::type;
+
 // Debug phase marks of gemm_glds_kernel (tools/gemm_trace.py): wave 0 of every workgroup stores
 // s_memrealtime (100 MHz) at mark i into trace[blockIdx.x * 8 + i]; slot 6/7 = HW_ID / XCC_ID.
 #ifdef LRCE_GEMM_TRACE
@@ -587,8 +600,8 @@ constexpr int pf_rs_slots(int im) { return im <= 4 ? im : 1; }
 
 // DROP: the fused-dropout epilogue (a separate instantiation: the branch in every kernel measured
 // 14-17 % slower tall-tile GEMMs through changed code generation)
-template <int TBM, int TBN, bool A_KM, bool B_KM, bool F16 = false, int NS = 2, bool DROP = false>
-__global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
+template <int TBM, int TBN, bool A_KM, bool B_KM, bool F16 = false, int NS = 2, bool DROP = false, bool PT = false>
+__global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmArg<PT> p) {
   constexpr int WM = TBM / 2, WN = TBN / 2;      // per-wave tile
   constexpr int IM = WM / 16, JN = WN / 16;      // 16x16 accumulator blocks per wave
   constexpr int A_EL = TBM * BK, B_EL = TBN * BK;
@@ -598,7 +611,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
   const int tiles = p.tiles_m * p.tiles_n;
   const int z = blockIdx.y;
   const int bz = z / p.split_k, sk = z % p.split_k;
-  p.bias += (long long)bz * p.sbias;
+  if constexpr (PT) p.bias = p.tbias[bz];
+  else p.bias += (long long)bz * p.sbias;
   if (p.alpha_dev) p.alpha_dev += (long long)bz * p.salpha;
   const int lin = xcd_remap(blockIdx.x, tiles);
   int tm, tn;
@@ -611,8 +625,15 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
     p.trace[(long long)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
   }
 #endif
-  const bf16* abase = static_cast<const bf16*>(p.a) + (long long)bz * p.sa;
-  const bf16* bbase = p.b + (long long)bz * p.sb;
+  const bf16* abase;
+  const bf16* bbase;
+  if constexpr (PT) {
+    abase = static_cast<const bf16*>(p.ta[bz]);
+    bbase = p.tb[bz];
+  } else {
+    abase = static_cast<const bf16*>(p.a) + (long long)bz * p.sa;
+    bbase = p.b + (long long)bz * p.sb;
+  }
   const int kb = sk * p.k_chunk;
   const int ke = min(p.k, kb + p.k_chunk);
   const int nfull = ke > kb ? (ke - kb) / BK : 0;
@@ -789,8 +810,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmP p) {
       if (m < p.m) __hip_atomic_fetch_add(db + m, alpha_of(p) * accb[i][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  char* cbase = static_cast<char*>(p.c) +
-                (long long)bz * p.sc * ((p.flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
+  char* cbase;
+  if constexpr (PT) cbase = static_cast<char*>(p.tc[bz]);
+  else cbase = static_cast<char*>(p.c) +
+               (long long)bz * p.sc * ((p.flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
   if ((p.flags & LRCE_EPI_ATOMIC) && !p.ws) {
     // split-K partials: stage 32-row slabs through LDS (free now) so each atomic instruction covers
     // consecutive columns of a row.  acc[i][j][r] = C[m = i*16 + (lane&15)][n = j*16 + 4*(lane>>4) + r]
@@ -1300,6 +1323,55 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     case 3: gemm_kernel<false, true, true><<<grid, NT, 0, s>>>(p); break;
   }
   return lrce_check_launch("gemm");
+}
+
+// Weight gradients of n same-shape linears in one launch: dW_z[m][n] += sum_k dY_z[k][m] X_z[k][n]
+// (A M-major = dY_z with lda, B N-major = X_z with ldb, C_z f32 with ldc), bias_z[m] += sum_k dY_z[k][m]
+// when d->flags has BIAS_GRAD.  One K slice per tile (no split-K slabs, no reduce launch): the
+// n-fold tile count fills the chip.  d gives the shape / leading dims / flags (ACCUM [| BIAS_GRAD]);
+// its a / b / c / bias / batch / strides are ignored.  Chunks of GPT entries per launch.
+extern "C" int lrce_gemm_ptr_batched(const LrceGemmDesc* d, const void* const* a, const void* const* b, void* const* c,
+                                     const float* const* bias, int n, void* stream) {
+  if (!d || n < 0 || (n > 0 && (!a || !b || !c))) return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: null argument");
+  if (n == 0) return LRCE_OK;
+  const bool bg = d->flags & LRCE_EPI_BIAS_GRAD;
+  if ((d->flags & ~(LRCE_EPI_ACCUM | LRCE_EPI_BIAS_GRAD)) || !(d->flags & LRCE_EPI_ACCUM) || d->a_kmajor || d->b_kmajor ||
+      d->a_f32 || d->b_f32 || d->f16 || d->a_map || d->c_map || d->split_k > 1 || d->alpha_dev || d->row_scale ||
+      d->a_row_scale || d->scale_cols || d->drop_p > 0.f || (bg && !bias))
+    return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: bf16 weight gradients only (M-major dY, N-major X, ACCUM [| BIAS_GRAD])");
+  if (d->m <= 0 || d->n <= 0 || d->k <= 0 || d->m % 8 || d->n % 8 || d->lda % 8 || d->ldb % 8 || d->ldc % 8)
+    return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: m=%d n=%d lda=%lld ldb=%lld ldc=%lld", d->m, d->n, (long long)d->lda,
+                     (long long)d->ldb, (long long)d->ldc);
+  if (((long long)d->k * d->lda + d->m) * 2 >= (1LL << 31) || ((long long)d->k * d->ldb + d->n) * 2 >= (1LL << 31))
+    return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: operand extent over 2 GB");
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  for (int i = 0; i < n; ++i)
+    if (!a[i] || !b[i] || !c[i] || !al16(a[i]) || !al16(b[i]) || !al16(c[i]) || (bg && (!bias[i] || !al16(bias[i]))))
+      return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: entry %d null or not 16-B aligned", i);
+  GemmPT p{};
+  p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc;
+  p.m = d->m; p.n = d->n; p.k = d->k; p.split_k = 1;
+  p.k_chunk = (d->k + BK - 1) / BK * BK;
+  p.flags = d->flags;
+  p.alpha = d->alpha; p.scale_val = 1.f; p.rows_per_scale = 1; p.a_rows_per_scale = 1;
+  p.tiles_m = (d->m + BM - 1) / BM; p.tiles_n = (d->n + BN - 1) / BN;
+  p.group_m = 4;
+  p.vec = 1;
+  p.trace = g_gemm_trace;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += GPT) {
+    const int cnt = n - i0 < GPT ? n - i0 : GPT;
+    for (int j = 0; j < cnt; ++j) {
+      p.ta[j] = a[i0 + j];
+      p.tb[j] = static_cast<const bf16*>(b[i0 + j]);
+      p.tc[j] = c[i0 + j];
+      p.tbias[j] = bg ? bias[i0 + j] : nullptr;
+    }
+    p.batch = cnt;
+    p.a = p.ta[0]; p.b = p.tb[0]; p.c = p.tc[0]; p.bias = p.tbias[0];
+    gemm_glds_kernel<128, 128, false, false, false, 2, false, true><<<dim3(p.tiles_m * p.tiles_n, cnt), NT, 0, s>>>(p);
+  }
+  return lrce_check_launch("gemm_ptr_batched");
 }
 
 // debug: phase timestamps of gemm_glds_kernel into buf (device, >= 8 per workgroup), NULL = off; the

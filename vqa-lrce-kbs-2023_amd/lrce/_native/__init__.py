@@ -145,6 +145,7 @@ _U64 = ctypes.c_uint64
 _SIGS = {
     "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
     "lrce_gemm_ln": [ctypes.POINTER(GemmDesc), ctypes.POINTER(LnPrologue), _P],
+    "lrce_gemm_ptr_batched": [ctypes.POINTER(GemmDesc), _P, _P, _P, _P, _I, _P],
     "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _I64,
                            _P],

@@ -298,12 +298,17 @@ def _drop_path_scales(swin, nc, device):
     return [(s[2 * i], s[2 * i + 1]) if r > 0.0 else (None, None) for i, r in enumerate(rates)]
 
 
-def _wgrad(flat, lin, dy16, x16):
-    """dW += dY^T X and db += colsum(dY) in one GEMM launch (bias sum fused via LRCE_EPI_BIAS_GRAD)."""
+def _wgrad(flat, lin, dy16, x16, defer=None):
+    """dW += dY^T X and db += colsum(dY) in one GEMM launch (bias sum fused via LRCE_EPI_BIAS_GRAD);
+    defer: a DeferredGrads whose flush issues the stage's same-shape weight gradients as one batched
+    launch (no split-K slabs / reduce) — the operands stay alive until then."""
     gw = _g(flat, lin.weight)
     gb = _g(flat, lin.bias) if lin.bias is not None else None
     if gw is not None:
-        K.linear_dw(dy16, x16, gw, bias_grad=gb)
+        if defer is not None and _DEFER_WGRAD and dy16.dtype == torch.bfloat16 and x16.dtype == torch.bfloat16:
+            defer.dw.append((dy16, x16, gw, gb))
+        else:
+            K.linear_dw(dy16, x16, gw, bias_grad=gb)
     elif gb is not None:
         K.colsum(dy16, gb)
 
@@ -346,6 +351,8 @@ class _Handoff:
 
 
 _DEFER_REDUCTIONS = os.environ.get("LRCE_SWIN_DEFER_RED", "1") != "0"   # A/B knob
+# with the reductions deferred, the blocks' weight gradients too: one launch per linear for the stage
+_DEFER_WGRAD = os.environ.get("LRCE_SWIN_DEFER_WGRAD", "1") != "0"      # A/B knob
 
 
 def _stage_deferral(blocks, flat):
@@ -473,10 +480,10 @@ class _SwinBlockFn(torch.autograd.Function):
         # next block's LN1 backward when there is one
         if dout16 is None:
             dout16 = K.scale_cast_bf16(dout, dp2, rpc)
-        _wgrad(flat, blk.mlp.fc2, dout16, g)
+        _wgrad(flat, blk.mlp.fc2, dout16, g, red)
         dpre = K.linear_dx(dout16, flat.w16(blk.mlp.fc2.weight), out_f32=False, dgelu_pre=pre)
         del g, pre, dout16
-        _wgrad(flat, blk.mlp.fc1, dpre, h2)
+        _wgrad(flat, blk.mlp.fc1, dpre, h2, red)
         # the LayerNorms' input gradients arrive as bf16 GEMM outputs (as under the reference's
         # autocast, where a bf16 linear's grad_input is bf16): half the bytes of the LN backward's dy;
         # rows of >= 1024 columns keep f32 (the LN backward's bf16 loads measured slower there)
@@ -491,7 +498,7 @@ class _SwinBlockFn(torch.autograd.Function):
                         dx16=dmid16, dx16_map=ctx.sp2win, dx_scale=dp1, dx_scale_rps=rpc, defer=red)
         del dh2
         # attention branch: x_mid = x + s1 * unwindow(proj(attn(qkv(LN1(window(x))))))
-        _wgrad(flat, at.proj, dmid16, o)
+        _wgrad(flat, at.proj, dmid16, o, red)
         do = K.linear_dx(dmid16, flat.w16(at.proj.weight), out_f32=False)
         del dmid16
         dqkv = torch.empty_like(qkv)
@@ -502,7 +509,7 @@ class _SwinBlockFn(torch.autograd.Function):
         if gt is not None:
             K.wattn_dbias(dbp, geo.n_win, nH, geo.ws, _bin_rows(at, geo.ws), gt, defer=red)
         del dbp
-        _wgrad(flat, at.qkv, dqkv, xw)
+        _wgrad(flat, at.qkv, dqkv, xw, red)
         dxw = K.linear_dx(dqkv, flat.w16(at.qkv.weight), out_f32=C >= _LN_F32_WIDE)
         del dqkv, qkv, xw
         dx = torch.empty_like(x)

@@ -304,6 +304,31 @@ def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_
          a_rows_per_scale=a_rows_per_scale, workspace=ws, f16=f16, alpha_dev=alpha_dev)
 
 
+def linear_dw_batched(items):
+    """dW_i += dY_i^T X_i (+ db_i += colsum(dY_i)) for items [(dy16, x16, dw, db|None)] of one shape
+    (bf16 [T, out] / [T, in], f32 [out, in]) as ONE launch (lrce_gemm_ptr_batched: no split-K)."""
+    dy0, x0, dw0, db0 = items[0]
+    T, O, I = x0.shape[0], dw0.shape[0], dw0.shape[1]
+    bias = db0 is not None
+    for dy, x, dw, db in items:
+        if (dy.dtype != BF16 or x.dtype != BF16 or dw.dtype != F32 or dy.shape != (T, O) or x.shape != (T, I)
+                or dw.shape != (O, I) or (db is not None) != bias or not dw.is_contiguous()
+                or dy.stride(1) != 1 or x.stride(1) != 1):
+            raise N.NativeError("linear_dw_batched: items differ in shape / dtype / layout")
+    d = N.GemmDesc()
+    d.m, d.n, d.k, d.batch = O, I, T, 1
+    d.lda, d.ldb, d.ldc = _ld(dy0), _ld(x0), I
+    d.a_kmajor, d.b_kmajor = 0, 0
+    d.flags = N.EPI_ACCUM | (N.EPI_BIAS_GRAD if bias else 0)
+    d.alpha, d.scale_val, d.rows_per_scale, d.a_rows_per_scale = 1.0, 1.0, 1, 1
+    n = len(items)
+    arr = lambda vals: ctypes.cast((ctypes.c_void_p * n)(*vals), ctypes.c_void_p)  # noqa: E731
+    _timed("gemm", dw0, lambda: call("lrce_gemm_ptr_batched", ctypes.byref(d), arr([ptr(i[0]) for i in items]),
+                                     arr([ptr(i[1]) for i in items]), arr([ptr(i[2]) for i in items]),
+                                     arr([ptr(i[3]) for i in items]), n, stream_of(dw0)),
+           flops=2.0 * O * I * T * n, key=(O, I, T, n, "AM", "BN", "a16", 1, d.flags))
+
+
 def colsum(x, out, *, row_map=None, rows=None, row_scale=None, rows_per_scale=1):
     M = rows if rows is not None else x.shape[0]
     call("lrce_colsum", ptr(x), int(x.dtype == F32), ptr(row_map), x.shape[-1], M, x.shape[-1], ptr(row_scale),
@@ -359,9 +384,16 @@ class DeferredGrads:
     Each sum is the one the immediate launch computes, in the same order (bit-identical)."""
 
     def __init__(self):
-        self.ln, self.db = [], []
+        self.ln, self.db, self.dw = [], [], []
 
     def flush(self, stream_tensor):
+        if self.dw:
+            # same-shape weight gradients (one per block and linear) as one launch per shape
+            groups = {}
+            for it in self.dw:
+                groups.setdefault((tuple(it[0].shape), tuple(it[1].shape), it[3] is not None), []).append(it)
+            for items in groups.values():
+                linear_dw_batched(items)
         if self.ln:
             n = len(self.ln)
             arr = lambda vals, t: (t * n)(*vals)  # noqa: E731
@@ -378,7 +410,7 @@ class DeferredGrads:
                  arr([i[1] for i in self.db], ctypes.c_int32), arr([i[2] for i in self.db], ctypes.c_int32),
                  arr([i[3] for i in self.db], ctypes.c_int32), arr([ptr(i[4]) for i in self.db], ctypes.c_void_p),
                  arr([ptr(i[5]) for i in self.db], ctypes.c_void_p), n, stream_of(stream_tensor))
-        self.ln, self.db = [], []
+        self.ln, self.db, self.dw = [], [], []
 
 
 def scale_cast_bf16(x, row_scale=None, rows_per_scale=1, out=None):
