@@ -529,7 +529,8 @@ int lrce_grad_scale(const float* x, int64_t n, float* scale, void* stream);
 /* Delayed scaling of the BERT backward's fp16 operands (the reference's GradScaler keeps one scale for
  * thousands of steps, agent_oe.py:40-42; here one per tensor, from the previous step): for each of
  * n_slots scale slots [S, 1/S, amax bits, -] with a recorded max (word 2 != 0): S = 2^(7 - floor(log2
- * amax)), 1/S, word 2 cleared; slots without one keep their scale.  One launch per step. */
+ * amax)), 1/S, word 2 cleared; slots without one keep their scale; a non-finite amax (an fp16 operand
+ * overflowed) halves S (GradScaler's backoff).  One launch per step. */
 int lrce_grad_scale_update(float* scale, int n_slots, void* stream);
 /* lrce_layernorm_bwd (identity maps, f32 dy / x, no residual) fused with lrce_dropout_bwd_f16: dx (f32,
  * optional), dx_f16 = fp16(scale[0] * dropout_bwd(dx)) (mask of lrce_dropout over [rows][cols], p / seed
@@ -560,7 +561,9 @@ int lrce_set_rng_offset(const uint64_t* offset);
  * lrce_l2norm_multi: sumsq[t] = ||p_t||^2 (zeroed here).  lrce_adamw_step: torch.optim.AdamW update
  * (decoupled weight decay, bias corrections bc1 = 1-beta1^t, bc2 = 1-beta2^t) on the gradient
  * grad_scale * g + reg * p / ||p|| (the L2-regulariser term), tensor_lr[t] per tensor; also writes
- * the bf16 shadow copy of p (p_bf16, optional) used by the next forward. */
+ * the bf16 shadow copy of p (p_bf16, optional) used by the next forward.  An element whose gradient
+ * term is not finite keeps its parameter and moments (the reference's GradScaler skips the whole
+ * step on an overflow; per element here, so early per-group updates need no global flag). */
 int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks, float* sumsq, int n_tensors,
                       const int32_t* tensor_chunk_off, float* chunk_sq, void* stream);
 int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,

@@ -192,9 +192,16 @@ def test_decoder_kv_stream_is_bit_identical(task, monkeypatch):
         runs.append({"y": y.detach().float().clone(), "dv": vg.grad.clone(), "dt": tg.grad.clone(),
                      **{k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}})
     assert runs[0].keys() == runs[1].keys()
+    # MC: the 5 answer choices share each video row, so its dK / dV (and everything fed by it: dv, the
+    # memory-side projections' gradients) accumulate by float atomics — reproducible to f32 rounding
+    atomic = ("video_pos_embed.", "dv", "projection_layer.", "multihead_attn.in_proj") if task == "mc" else \
+        ("video_pos_embed.",)
+    # (MC: the atomically accumulated f32 dK / dV pass through a bf16 cast — a flipped rounding is 2^-8
+    # of that element)
+    tol = 5e-3 if task == "mc" else 1e-5
     for k in runs[0]:
-        if k.startswith("video_pos_embed."):
-            assert rel(runs[1][k], runs[0][k]) < 1e-5, k
+        if k.startswith(atomic):
+            assert rel(runs[1][k], runs[0][k]) < tol, k
         else:
             assert torch.equal(runs[0][k], runs[1][k]), k
 
@@ -230,13 +237,14 @@ def test_swin_deferred_reductions_and_weight_gradients(monkeypatch):
     g2 = _swin_grads(ve, clips)
     assert g0.keys() == g1.keys() == g2.keys() and len(g0) > 0
     assert any("norm1" in k for k in g0) and any("relative_position_bias_table" in k for k in g0)
-    bad = [k for k in g0 if not torch.equal(g0[k], g1[k])]
+    # biases of split-K weight gradients are summed by float atomics (one add per K slice): f32 rounding
+    bad = [k for k in g0 if not (rel(g1[k], g0[k]) < 1e-5 if k.endswith("bias") else torch.equal(g0[k], g1[k]))]
     assert not bad, bad[:10]
     lin = (".qkv.", ".proj.", ".fc1.", ".fc2.")
     bad = {}
     for k in g0:
         err = rel(g2[k], g0[k])
-        ok = err < 1e-5 if any(t in k for t in lin) else torch.equal(g2[k], g0[k])
+        ok = err < 1e-5 if any(t in k for t in lin) or k.endswith("bias") else torch.equal(g2[k], g0[k])
         if not ok:
             bad[k] = err
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]

@@ -890,6 +890,33 @@ def test_adamw_matches_torch():
     assert rel(p, torch.cat([pref[0].detach(), pref[1].detach()])) < 1e-5
 
 
+def test_adamw_keeps_non_finite_gradient_elements_and_scale_backs_off():
+    """An element whose gradient is inf / NaN (an overflowed fp16 gradient operand) keeps its parameter
+    and moments; the other elements update as usual.  lrce_grad_scale_update halves a scale whose
+    recorded max is not finite (the reference's GradScaler backoff) instead of resetting it."""
+    k = K()
+    n = 2 * 1024
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    g[5], g[1500] = float("inf"), float("nan")
+    m, v = torch.full((n,), 0.1, device=dev), torch.full((n,), 0.2, device=dev)
+    p0, m0, v0 = p.clone(), m.clone(), v.clone()
+    chunk_tensor = torch.tensor([0, 0], dtype=torch.int32, device=dev)
+    lrs = torch.tensor([1e-3], device=dev)
+    k.adamw_step(p, g, m, v, chunk_tensor, lrs, None, None, 2, 0.9, 0.999, 1e-8, 0.01, 1.0, 0.0, 0.1, 0.001)
+    torch.cuda.synchronize()
+    for i in (5, 1500):
+        assert p[i] == p0[i] and m[i] == m0[i] and v[i] == v0[i]
+    ok = torch.ones(n, dtype=torch.bool, device=dev)
+    ok[5] = ok[1500] = False
+    assert bool(torch.isfinite(p).all()) and bool((p[ok] != p0[ok]).all())
+    sc = torch.tensor([[64.0, 1 / 64.0, 0.0, 0.0]], device=dev)
+    sc.view(torch.int32)[0, 2] = 0x7F800000          # +inf recorded as the max
+    k.grad_scale_update(sc)
+    torch.cuda.synchronize()
+    assert sc[0, 0].item() == 32.0 and sc[0, 1].item() == 1 / 32.0 and sc.view(torch.int32)[0, 2].item() == 0
+
+
 def test_rng_offset_changes_masks_and_backward_agrees():
     """The device RNG offset (graph replay) moves every mask; dropout backward uses the same mask as
     its forward at the same offset."""
@@ -1154,6 +1181,7 @@ def test_linear_dw_batched_matches_per_item():
     """lrce_gemm_ptr_batched (a Swin stage's same-shape weight gradients as one launch, one K slice per
     tile) against linear_dw per item (split-K slabs + reduce): dW and the bias gradient to f32 rounding,
     including a K tail (T % 64 != 0) and entries at unrelated addresses."""
+    kk = K()
     torch.manual_seed(0)
     T, O, I, n = 1000, 256, 384, 5
     items, ref = [], []
@@ -1163,10 +1191,10 @@ def test_linear_dw_batched_matches_per_item():
         dw = torch.randn(O, I, device="cuda")
         db = torch.randn(O, device="cuda")
         rw, rb = dw.clone(), db.clone()
-        K.linear_dw(dy, x, rw, bias_grad=rb)
+        kk.linear_dw(dy, x, rw, bias_grad=rb)
         items.append((dy, x, dw, db))
         ref.append((rw, rb))
-    K.linear_dw_batched(items)
+    kk.linear_dw_batched(items)
     torch.cuda.synchronize()
     for (dy, x, dw, db), (rw, rb) in zip(items, ref):
         assert rel(dw, rw) < 1e-5 and rel(db, rb) < 1e-5

@@ -74,12 +74,27 @@ def main():
             main.wait_stream(side)
         return body
 
+    def interleaved():
+        """A's 150 steps and B's 12 issued alternately (A on the side stream): same graph edges as
+        both(), different node creation order"""
+        main = torch.cuda.current_stream()
+        side.wait_stream(main)
+        ya, yb = sx, None
+        for i in range(150):
+            with torch.cuda.stream(side):
+                ya = torch.nn.functional.gelu(ya @ sw)
+            if i % 12 == 0 and i < 144:
+                yb = big_a @ big_b
+        main.wait_stream(side)
+        return ya, yb
+
+    ti = timed(capture(interleaved))
     ta = timed(capture(chain_a))
     tb = timed(capture(chain_b))
     t1 = timed(capture(both(True)))
     t2 = timed(capture(both(False)))
     print(f"A alone {ta:.3f} ms, B alone {tb:.3f} ms, A+B {ta + tb:.3f}, max {max(ta, tb):.3f}")
-    print(f"A || B, side chain captured first: {t1:.3f} ms; captured second: {t2:.3f} ms")
+    print(f"A || B, side chain captured first: {t1:.3f} ms; captured second: {t2:.3f} ms; interleaved: {ti:.3f} ms")
     # two latency-bound chains (neither fills the chip): concurrent branches would take ~max
     sx2 = sx.clone()
 

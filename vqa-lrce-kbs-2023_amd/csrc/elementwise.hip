@@ -212,6 +212,7 @@ __global__ void grad_scale_update_kernel(float* __restrict__ scale, int n) {
   const int e = (int)((bits >> 23) & 0xFF) - 127;
   float s = 1.f;
   if (e < 128 && e > -127) s = ldexpf(1.f, min(100, max(-100, 7 - e)));
+  else if (e >= 128) s = fmaxf(sc[0] * 0.5f, ldexpf(1.f, -100));   // inf / NaN max: back off (GradScaler)
   sc[0] = s;
   sc[1] = 1.f / s;
   words[0] = 0u;

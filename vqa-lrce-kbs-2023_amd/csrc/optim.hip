@@ -106,11 +106,17 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float gr = ga[j] * gscale + rc * pa[j];
-        ma[j] = b1 * ma[j] + (1.0f - b1) * gr;
-        va[j] = b2 * va[j] + (1.0f - b2) * gr * gr;
-        const float np = pa[j] * decay - step * ma[j] / (sqrtf(va[j]) * isb2 + eps);
-        pa[j] = np;
-        ob[j] = f2bf(np);
+        // a non-finite gradient element (an fp16 gradient operand that overflowed) leaves its parameter
+        // and moments as they are, instead of poisoning them for every later step; the reference's
+        // GradScaler skips the whole step in that case (agent_oe.py:40-42)
+        const bool fin = __builtin_isfinite(gr);
+        const float mn = b1 * ma[j] + (1.0f - b1) * gr;
+        const float vn = b2 * va[j] + (1.0f - b2) * gr * gr;
+        const float np = pa[j] * decay - step * mn / (sqrtf(vn) * isb2 + eps);
+        ma[j] = fin ? mn : ma[j];
+        va[j] = fin ? vn : va[j];
+        pa[j] = fin ? np : pa[j];
+        ob[j] = f2bf(pa[j]);
       }
       *reinterpret_cast<float4*>(p + i) = pp[r];
       *reinterpret_cast<float4*>(m + i) = mm[r];

@@ -305,7 +305,8 @@ def _wgrad(flat, lin, dy16, x16, defer=None):
     gw = _g(flat, lin.weight)
     gb = _g(flat, lin.bias) if lin.bias is not None else None
     if gw is not None:
-        if defer is not None and _DEFER_WGRAD and dy16.dtype == torch.bfloat16 and x16.dtype == torch.bfloat16:
+        if (defer is not None and _DEFER_WGRAD and dy16.dtype == torch.bfloat16 and x16.dtype == torch.bfloat16
+                and defer.wants_dw(gw.shape[0], gw.shape[1], x16.shape[0])):
             defer.dw.append((dy16, x16, gw, gb))
         else:
             K.linear_dw(dy16, x16, gw, bias_grad=gb)
@@ -365,7 +366,7 @@ def _stage_deferral(blocks, flat):
         return None
     if not any(p.requires_grad for p in blocks[0].parameters()):
         return None
-    return K.DeferredGrads()
+    return K.DeferredGrads(len(blocks))
 
 
 def _run_blocks(blocks, x, geo, flat, scales, tiles=None):

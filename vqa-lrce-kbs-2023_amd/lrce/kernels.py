@@ -383,8 +383,16 @@ class DeferredGrads:
     (layernorm_bwd(defer=...)) and relative-position bias-table gradients (wattn_dbias(defer=...)).
     Each sum is the one the immediate launch computes, in the same order (bit-identical)."""
 
-    def __init__(self):
+    def __init__(self, n_items=1):
         self.ln, self.db, self.dw = [], [], []
+        self.n_items = n_items   # blocks sharing this object (one weight gradient each per linear)
+
+    def wants_dw(self, out_f, in_f, tokens):
+        """Batch a weight gradient of this shape?  Only when the blocks' 128 x 128 tiles fill the chip
+        (>= 256 workgroups) and each tile's single K loop stays short: one K slice per tile means a
+        stage-1 weight (4 tiles x 2 blocks, 282 240 tokens) would run 8 workgroups for milliseconds."""
+        tiles = -(-out_f // 128) * -(-in_f // 128)
+        return tiles * self.n_items >= 256 and tokens <= 32768
 
     def flush(self, stream_tensor):
         if self.dw:

@@ -330,6 +330,10 @@ _KV_ASYNC = os.environ.get("LRCE_DEC_KV_ASYNC", "1") != "0"
 # it (beside the Swin backward's full-chip GEMMs); LRCE_DEC_WGRAD_EARLY=1.  Measured slower than after the
 # sweep (same-box A/B 284.0 vs 286.4 QA-samples/s, profiles/r5_bench_defer_wgrad_early_ab.txt): the
 # weight-gradient kernels slow the latency-bound sweep they share the CUs with.  Off.
+# the 12 layers' K/V projection weight gradients as one pointer-table launch (LRCE_DEC_KV_WGRAD_BATCHED=1):
+# measured 293.2 / 292.4 vs 294.9 / 294.0 QA-samples/s per layer (profiles/r5_bench_dw_batched_ab.txt) —
+# the per-layer split-K launches interleave better with the Swin backward they run beside.  Off.
+_KV_WGRAD_BATCHED = os.environ.get("LRCE_DEC_KV_WGRAD_BATCHED", "0") == "1"
 _WGRAD_EARLY = os.environ.get("LRCE_DEC_WGRAD_EARLY", "0") == "1"   # measured slower (285.3 vs 286.4): off
 
 
@@ -434,9 +438,9 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         wg = aux_stream(dev, "decoder_wgrad")
         first = [True]
 
-        def layer_wgrads(l, cast_done):
-            """Layer l's query-side weight / LayerNorm gradients over all steps and its K/V projection
-            weight gradients, on the weight-gradient stream (they feed nothing downstream)."""
+        def layer_wgrads(l, cast_done, kv=True):
+            """Layer l's query-side weight / LayerNorm gradients over all steps and (kv) its K/V
+            projection weight gradients, on the weight-gradient stream (they feed nothing downstream)."""
             wg.wait_stream(main)
             if cast_done is not None:
                 wg.wait_event(cast_done)
@@ -444,9 +448,29 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             ca = lay.multihead_attn
             with torch.cuda.stream(wg):
                 _layer_wgrads(lay, flat, acts[l], grads[l], fused=fused_layers[l])
-                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16[l], v16, rows=(E, 3 * E))
+                if kv:
+                    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16[l], v16, rows=(E, 3 * E))
+                    if Lt:
+                        _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[l], t16, rows=(E, 3 * E))
+
+        def kv_wgrads_batched():
+            """Every layer's K/V projection weight gradients (video rows, then question rows) as one
+            pointer-table launch each (K.linear_dw_batched: no split-K slabs / reduce) — False if the
+            layers' gradients are not all trainable (then per layer)."""
+            items_v, items_t = [], []
+            for l, lay in enumerate(layers):
+                ca = lay.multihead_attn
+                gw, gb = _g(flat, ca.in_proj_weight), _g(flat, ca.in_proj_bias)
+                if gw is None or gb is None:
+                    return False
+                items_v.append((dk16[l], v16, gw[E:3 * E], gb[E:3 * E]))
                 if Lt:
-                    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[l], t16, rows=(E, 3 * E))
+                    items_t.append((dt16[l], t16, gw[E:3 * E], gb[E:3 * E]))
+            with torch.cuda.stream(wg):
+                K.linear_dw_batched(items_v)
+                if items_t:
+                    K.linear_dw_batched(items_t)
+            return True
 
         def memory_dx(l):
             """dv (+)= dK/dV_l W_kv,l, dtt likewise: layer l's K/V gradients are complete once step 0's
@@ -497,8 +521,10 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         # while the extractors' backward, which needs only dv / dt, proceeds on this one.  The
         # forward's stream anchor joins that stream back at the end of backward.
         if not _WGRAD_EARLY:
+            wg.wait_stream(main)
+            kv_done = _KV_WGRAD_BATCHED and kv_wgrads_batched()
             for l in range(len(layers)):
-                layer_wgrads(l, None)
+                layer_wgrads(l, None, kv=not kv_done)
         wg.wait_stream(main)
         with torch.cuda.stream(wg):
             gt = _g(flat, ft.summarization_token)
