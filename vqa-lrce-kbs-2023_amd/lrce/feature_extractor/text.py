@@ -471,6 +471,17 @@ class BertModel(nn.Module):
         return list(self.encoder.parameters())
 
     def forward(self, input_ids, attention_mask=None, token_type_ids=None, join_token=None):
+        gen = self.forward_steps(input_ids, attention_mask, token_type_ids, join_token)
+        while True:
+            try:
+                next(gen)
+            except StopIteration as e:
+                return e.value
+
+    def forward_steps(self, input_ids, attention_mask=None, token_type_ids=None, join_token=None):
+        """forward() as a generator that yields after the embeddings and after every layer (its value is
+        the output, returned through StopIteration): a caller can interleave the text branch's launches
+        with another branch's, which decides how the HIP graph executor overlaps them (E2EBase)."""
         flat = ensure(self)
         B, L = input_ids.shape
         dev = input_ids.device
@@ -482,6 +493,7 @@ class BertModel(nn.Module):
         anchor = [t for t in self.embeddings.parameters()]
         x = _EmbedFn.apply(ids, types, self.embeddings, flat, p, seed, join_token, *anchor)
         st = _Stack(self, flat, B * L, dev)
+        yield
         # (LRCE_DEV_BERT_LAYERS=k: a sensitivity experiment only — the step with k of the 12 layers, to
         # measure how much of the text branch is on the step's critical path; never set in the product)
         n_run = int(os.environ.get("LRCE_DEV_BERT_LAYERS", "0")) or len(self.encoder.layer)
@@ -490,6 +502,7 @@ class BertModel(nn.Module):
             if st.flush_at is None and torch.is_grad_enabled() and (x.requires_grad or any(q.requires_grad for q in params)):
                 st.flush_at = i      # the last layer backward to run issues the deferred weight gradients
             x = _LayerFn.apply(x, mask, layer, flat, p, seed + 16 * (i + 1), B, L, st, i, *params)
+            yield
         return x.view(B, L, HIDDEN)
 
 
@@ -550,3 +563,7 @@ class TextExtractor(nn.Module):
 
     def forward(self, input_ids, attention_mask, token_type_ids, join_token=None):
         return self.bert(input_ids, attention_mask, token_type_ids, join_token=join_token)
+
+    def forward_steps(self, input_ids, attention_mask, token_type_ids, join_token=None):
+        """BertModel.forward_steps: the forward as a generator (one step per layer)."""
+        return self.bert.forward_steps(input_ids, attention_mask, token_type_ids, join_token=join_token)

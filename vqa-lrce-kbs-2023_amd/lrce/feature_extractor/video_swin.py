@@ -369,9 +369,10 @@ def _stage_deferral(blocks, flat):
     return K.DeferredGrads(len(blocks))
 
 
-def _run_blocks(blocks, x, geo, flat, scales, tiles=None):
+def _run_blocks(blocks, x, geo, flat, scales, tiles=None, between=None):
     """The blocks of one stage in order; scales [(dp1, dp2)] per block (None entries in eval);
-    tiles: per block the (forward, backward) bias tiles built ahead (_prebuild_bias_tiles) or None."""
+    tiles: per block the (forward, backward) bias tiles built ahead (_prebuild_bias_tiles) or None;
+    between: optional callable run after each block's launches."""
     links = [None] + [_Handoff(scales[j - 1][1]) if _HANDOFF else None for j in range(1, len(blocks))]
     red = _stage_deferral(blocks, flat)
     for j, blk in enumerate(blocks):
@@ -379,6 +380,8 @@ def _run_blocks(blocks, x, geo, flat, scales, tiles=None):
         x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, links[j], links[j + 1] if j + 1 < len(blocks) else None,
                                tiles[j] if tiles is not None else None, (red, j == 0) if red is not None else None,
                                *blk.parameters())
+        if between is not None:
+            between()
     return x
 
 
@@ -619,7 +622,7 @@ class SwinTransformer3D(nn.Module):
         for i, layer in enumerate(self.layers):
             object.__setattr__(layer.blocks[0], "_lrce_group", f"swin{i}" if i > 0 else None)
 
-    def forward_tokens(self, clips, layout="BSTCHW", normalize=True):
+    def forward_tokens(self, clips, layout="BSTCHW", normalize=True, between_blocks=None):
         """clips (B,S,T,3,H,W) f32 in [0,1] (normalised in-kernel) or (B,3,T,H,W) already normalised.
         Returns (features f32 [n_clips*D'*H'*W', C_out], (n_clips, D', H', W'))."""
         flat = ensure(self)
@@ -659,7 +662,7 @@ class SwinTransformer3D(nn.Module):
                 blocks = blocks[:int(os.environ["LRCE_DEV_SWIN_S3"])]
             x = _run_blocks(blocks, x, geo, flat,
                             scales[bi:bi + len(blocks)] if scales is not None else [(None, None)] * len(blocks),
-                            tiles[:len(blocks)] if tiles is not None else None)
+                            tiles[:len(blocks)] if tiles is not None else None, between=between_blocks)
             bi += nb
             if layer.downsample is not None:
                 x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())

@@ -325,6 +325,7 @@ def _layer_wgrads(lay, flat, acts, grads, fused=False):
 # recurrence waits for layer l's K/V only when step 0 reaches layer l, and in the backward each layer's
 # memory-side input-gradient GEMMs start as soon as step 0's sweep has finished that layer.
 _KV_ASYNC = os.environ.get("LRCE_DEC_KV_ASYNC", "1") != "0"
+_KV_AHEAD = os.environ.get("LRCE_DEC_KV_AHEAD", "1") != "0"   # A/B knob: 0 = all 12 layers' K/V up front
 # Each layer's deferred weight gradients are issued on the weight-gradient stream as soon as step 0's
 # backward sweep has passed the layer (beside the rest of the latency-bound sweep) instead of all after
 # it (beside the Swin backward's full-chip GEMMs); LRCE_DEC_WGRAD_EARLY=1.  Measured slower than after the
@@ -357,26 +358,35 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         rows_v = B * S * 150
         v16 = v16.view(rows_v, E)
         t16 = t16.view(Bq * Lt, E) if Lt else None
-        kvv, kvt, kv_ready = [], [], []
+        nL = len(layers)
+        kvv, kvt, kv_ready = [None] * nL, [None] * nL, [None] * nL
         main = torch.cuda.current_stream(dev)
         ks = aux_stream(dev, "decoder_kv") if _KV_ASYNC else main
         if ks is not main:
             ks.wait_stream(main)
-        with torch.cuda.stream(ks):
-            for lay in layers:
-                ca = lay.multihead_attn
-                w = flat.w16(ca.in_proj_weight)[E:]
-                kvv.append(K.linear(v16, w, ca.in_proj_bias[E:]))
-                kvt.append(K.linear(t16, w, ca.in_proj_bias[E:]) if Lt else None)
-                if ks is not main:
-                    kv_ready.append(ks.record_event())
-        if ks is not main:
-            for x in kvv + [x for x in kvt if x is not None]:
-                x.record_stream(main)
             for x in (v16, t16):
                 if x is not None:
                     x.record_stream(ks)
-        nL = len(layers)
+
+        def issue_kv(l):
+            """Layer l's memory K/V projections (video rows, question rows) on the K/V stream.  Issued
+            one layer ahead of the recurrence's step 0 (the graph executor overlaps branches in the
+            order their launches were captured)."""
+            ca = layers[l].multihead_attn
+            w = flat.w16(ca.in_proj_weight)[E:]
+            with torch.cuda.stream(ks):
+                kvv[l] = K.linear(v16, w, ca.in_proj_bias[E:])
+                kvt[l] = K.linear(t16, w, ca.in_proj_bias[E:]) if Lt else None
+                if ks is not main:
+                    kv_ready[l] = ks.record_event()
+            if ks is not main:
+                for x in (kvv[l], kvt[l]):
+                    if x is not None:
+                        x.record_stream(main)
+        issue_kv(0)
+        if not _KV_AHEAD:
+            for l in range(1, nL):
+                issue_kv(l)
         acts = [_LayerActs(S, Bq, dev) for _ in layers]
         s = acts[0].x0[0]
         s.copy_(ft.summarization_token.detach().reshape(1, E).expand(Bq, E))
@@ -386,8 +396,11 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             step_saves = []
             x_in, prev = s, None
             for l, lay in enumerate(layers):
-                if i == 0 and kv_ready:
-                    main.wait_event(kv_ready[l])
+                if i == 0:
+                    if _KV_AHEAD and l + 1 < nL:
+                        issue_kv(l + 1)
+                    if kv_ready[l] is not None:
+                        main.wait_event(kv_ready[l])
                 st = _layer_fwd(lay, prev, x_in, kvv[l].view(-1), kvt[l].view(-1) if Lt else None, i, S, Lt, nmc, p,
                                 seed + 64 * (i * nL + l), acts[l], step_saves[-1] if step_saves else None)
                 step_saves.append(st)
