@@ -194,13 +194,13 @@ def test_decoder_kv_stream_is_bit_identical(task, monkeypatch):
     assert runs[0].keys() == runs[1].keys()
     # MC: the 5 answer choices share each video row, so its dK / dV (and everything fed by it: dv, the
     # memory-side projections' gradients) accumulate by float atomics — reproducible to f32 rounding
-    atomic = ("video_pos_embed.", "dv", "projection_layer.", "multihead_attn.in_proj") if task == "mc" else \
+    atomic = ("video_pos_embed.", "projection_layer.", "multihead_attn.in_proj") if task == "mc" else \
         ("video_pos_embed.",)
     # (MC: the atomically accumulated f32 dK / dV pass through a bf16 cast — a flipped rounding is 2^-8
     # of that element)
     tol = 5e-3 if task == "mc" else 1e-5
     for k in runs[0]:
-        if k.startswith(atomic):
+        if any(a in k for a in atomic) or (task == "mc" and k == "dv"):
             assert rel(runs[1][k], runs[0][k]) < tol, k
         else:
             assert torch.equal(runs[0][k], runs[1][k]), k
