@@ -121,7 +121,8 @@ int lrce_gemm(const LrceGemmDesc* desc, void* stream);
 /* n same-shape weight gradients in one launch (the blocks of a Swin stage): entry i computes
  * c[i][m][n] += sum_k a[i][k][m] b[i][k][n] (bf16 dY_i M-major with desc->lda, bf16 X_i N-major with
  * desc->ldb, f32 dW_i with desc->ldc) and, with LRCE_EPI_BIAS_GRAD, bias[i][m] += sum_k a[i][k][m].
- * desc supplies m / n / k / leading dims / alpha and flags = ACCUM [| BIAS_GRAD]; its pointers, batch,
+ * desc supplies m / n / k / leading dims / alpha and flags = ACCUM (+=) or OUT_F32 (=, for gradients known
+ * to be zero) [| BIAS_GRAD: the bias sum is always added]; its pointers, batch,
  * strides and split_k are ignored (one K slice per tile: no split-K slabs or reduce launch — the n-fold
  * tile count fills the chip).  Pointers 16-B aligned; up to 24 entries per launch (more: several). */
 int lrce_gemm_ptr_batched(const LrceGemmDesc* desc, const void* const* a, const void* const* b, void* const* c,

@@ -99,3 +99,21 @@ def test_padded_window_maps_match_pad_roll_partition(D, H, W):
     ref = torch.stack([m[:, :, 0::2, 0::2], m[:, :, 1::2, 0::2], m[:, :, 0::2, 1::2], m[:, :, 1::2, 1::2]], -1)
     assert torch.equal(g.merge_map.long(), ref.reshape(-1))
     assert g.M_merged == nc * D * ((H + 1) // 2) * ((W + 1) // 2)
+
+
+def test_gradient_freshness_claims():
+    """FlatParams.claim_fresh: a weight gradient may be stored instead of accumulated only when the
+    optimizer cleared the gradients and nothing has claimed that parameter since — a second backward
+    before the next zero_grad accumulates, and gradients cleared any other way are never 'fresh'."""
+    from lrce.flat import FlatParams
+    lin = torch.nn.Linear(8, 8)
+    flat = FlatParams(lin, "cpu")
+    ps = [lin.weight, lin.bias]
+    assert not flat.claim_fresh(ps)          # never cleared by the optimizer
+    flat.grads_zeroed()
+    assert flat.claim_fresh(ps)              # first writer after the clear
+    assert not flat.claim_fresh(ps)          # second backward: accumulate
+    assert not flat.claim_fresh([lin.weight])
+    flat.grads_zeroed()
+    assert flat.claim_fresh([lin.weight])
+    assert not flat.claim_fresh(ps)          # the bias is fresh but the weight was claimed: accumulate

@@ -1335,10 +1335,12 @@ extern "C" int lrce_gemm_ptr_batched(const LrceGemmDesc* d, const void* const* a
   if (!d || n < 0 || (n > 0 && (!a || !b || !c))) return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: null argument");
   if (n == 0) return LRCE_OK;
   const bool bg = d->flags & LRCE_EPI_BIAS_GRAD;
-  if ((d->flags & ~(LRCE_EPI_ACCUM | LRCE_EPI_BIAS_GRAD)) || !(d->flags & LRCE_EPI_ACCUM) || d->a_kmajor || d->b_kmajor ||
+  const int cf = d->flags & (LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32);
+  if ((d->flags & ~(LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32 | LRCE_EPI_BIAS_GRAD)) ||
+      (cf != LRCE_EPI_ACCUM && cf != LRCE_EPI_OUT_F32) || d->a_kmajor || d->b_kmajor ||
       d->a_f32 || d->b_f32 || d->f16 || d->a_map || d->c_map || d->split_k > 1 || d->alpha_dev || d->row_scale ||
       d->a_row_scale || d->scale_cols || d->drop_p > 0.f || (bg && !bias))
-    return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: bf16 weight gradients only (M-major dY, N-major X, ACCUM [| BIAS_GRAD])");
+    return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: bf16 weight gradients only (M-major dY, N-major X, ACCUM or OUT_F32 [| BIAS_GRAD])");
   if (d->m <= 0 || d->n <= 0 || d->k <= 0 || d->m % 8 || d->n % 8 || d->lda % 8 || d->ldb % 8 || d->ldc % 8)
     return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: m=%d n=%d lda=%lld ldb=%lld ldc=%lld", d->m, d->n, (long long)d->lda,
                      (long long)d->ldb, (long long)d->ldc);

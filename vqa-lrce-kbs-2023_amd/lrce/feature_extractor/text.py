@@ -424,8 +424,11 @@ def _flush_wgrads(st):
             if None not in (s_w, s_b, s_a, s_x, s_al) and s_w > 0 and s_b > 0:
                 _, lin, dy, x, _ = seq[0]
                 Nn, Kk = lin.weight.shape
+                # gradients known to be zero (FlatParams.claim_fresh) are stored, not read-modify-written
+                fresh = flat.claim_fresh([q for e in seq for q in (e[1].weight, e[1].bias)]) and _STORE_FRESH
                 K.gemm(dy, x, gw[0], Nn, Kk, st.rows, a_kmajor=False, b_kmajor=False, lda=dy.stride(0),
-                       ldb=x.stride(0), ldc=Kk, flags=N.EPI_ACCUM | N.EPI_BIAS_GRAD, bias=gb[0], batch=len(seq),
+                       ldb=x.stride(0), ldc=Kk, flags=(N.EPI_OUT_F32 if fresh else N.EPI_ACCUM) | N.EPI_BIAS_GRAD,
+                       bias=gb[0], batch=len(seq),
                        stride_a=s_a, stride_b=s_x, stride_c=s_w, stride_bias=s_b, f16=True, alpha_dev=slots[0],
                        stride_alpha=s_al)
                 continue
@@ -435,6 +438,7 @@ def _flush_wgrads(st):
 
 _WGRAD_BATCHED = os.environ.get("LRCE_BERT_WGRAD_BATCHED", "1") != "0"   # A/B knob
 _LN_DEFER = os.environ.get("LRCE_BERT_LN_DEFER", "1") != "0"             # A/B knob
+_STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"      # A/B knob (see FlatParams.claim_fresh)
 _DELAYED_SCALE = os.environ.get("LRCE_BERT_DELAYED_SCALE", "1") != "0"   # A/B knob
 
 

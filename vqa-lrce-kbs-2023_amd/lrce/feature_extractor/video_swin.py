@@ -307,7 +307,8 @@ def _wgrad(flat, lin, dy16, x16, defer=None):
     if gw is not None:
         if (defer is not None and _DEFER_WGRAD and dy16.dtype == torch.bfloat16 and x16.dtype == torch.bfloat16
                 and defer.wants_dw(gw.shape[0], gw.shape[1], x16.shape[0])):
-            defer.dw.append((dy16, x16, gw, gb))
+            ps = [lin.weight] + ([lin.bias] if gb is not None else [])
+            defer.dw.append((dy16, x16, gw, gb, flat.claim_fresh(ps) and _STORE_FRESH))
         else:
             K.linear_dw(dy16, x16, gw, bias_grad=gb)
     elif gb is not None:
@@ -354,6 +355,8 @@ class _Handoff:
 _DEFER_REDUCTIONS = os.environ.get("LRCE_SWIN_DEFER_RED", "1") != "0"   # A/B knob
 # with the reductions deferred, the blocks' weight gradients too: one launch per linear for the stage
 _DEFER_WGRAD = os.environ.get("LRCE_SWIN_DEFER_WGRAD", "1") != "0"      # A/B knob
+# a deferred weight gradient known to start from zero is stored, not added (FlatParams.claim_fresh)
+_STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"     # A/B knob
 
 
 def _stage_deferral(blocks, flat):

@@ -54,6 +54,10 @@ class FlatParams:
         self.tensor_chunk_off = off.to(self.device)
         self._bf16_version = -1
         self._epoch = 0            # bumped by writes the version counters cannot see (collectives)
+        # gradient freshness (claim_fresh): generation of the last optimizer zero_grad, and per
+        # parameter the generation its gradient was last claimed in
+        self._zero_gen = 0
+        self._claimed = {}
         self.f16 = None            # optional IEEE fp16 shadow of [f16_lo, f16_hi) (enable_f16)
         self.f16_lo = self.f16_hi = 0
         self.attach_grads(zero=True)
@@ -88,6 +92,22 @@ class FlatParams:
         if self.f16 is None or off < 0 or off + p.numel() > self.f16.numel():
             raise RuntimeError(f"no fp16 shadow for {self.names.get(id(p), '?')}: call enable_f16 first")
         return self.f16[off:off + p.numel()].view(p.shape)
+
+    def grads_zeroed(self):
+        """The optimizer has just cleared every gradient (FusedAdamW.zero_grad)."""
+        self._zero_gen += 1
+
+    def claim_fresh(self, params):
+        """True iff no gradient of `params` has been claimed since the last optimizer zero_grad — a
+        weight-gradient GEMM may then STORE its product instead of adding it to the (zero) gradient
+        (half the epilogue's memory traffic, no read round trip).  Claims them either way, so a second
+        backward before the next zero_grad accumulates.  False whenever the gradients were cleared
+        some other way (attach_grads, set_to_none): the accumulating path is always correct."""
+        g = self._zero_gen
+        fresh = g > 0 and all(self._claimed.get(id(p), 0) != g for p in params)
+        for p in params:
+            self._claimed[id(p)] = g
+        return fresh
 
     def notify(self, params):
         """Called by native autograd Functions when their parameters' gradients are final."""

@@ -304,9 +304,10 @@ def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_
          a_rows_per_scale=a_rows_per_scale, workspace=ws, f16=f16, alpha_dev=alpha_dev)
 
 
-def linear_dw_batched(items):
+def linear_dw_batched(items, store=False):
     """dW_i += dY_i^T X_i (+ db_i += colsum(dY_i)) for items [(dy16, x16, dw, db|None)] of one shape
-    (bf16 [T, out] / [T, in], f32 [out, in]) as ONE launch (lrce_gemm_ptr_batched: no split-K)."""
+    (bf16 [T, out] / [T, in], f32 [out, in]) as ONE launch (lrce_gemm_ptr_batched: no split-K).
+    store: dW_i = dY_i^T X_i (the gradients are known zero: FlatParams.claim_fresh); db_i still added."""
     dy0, x0, dw0, db0 = items[0]
     T, O, I = x0.shape[0], dw0.shape[0], dw0.shape[1]
     bias = db0 is not None
@@ -319,7 +320,7 @@ def linear_dw_batched(items):
     d.m, d.n, d.k, d.batch = O, I, T, 1
     d.lda, d.ldb, d.ldc = _ld(dy0), _ld(x0), I
     d.a_kmajor, d.b_kmajor = 0, 0
-    d.flags = N.EPI_ACCUM | (N.EPI_BIAS_GRAD if bias else 0)
+    d.flags = (N.EPI_OUT_F32 if store else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if bias else 0)
     d.alpha, d.scale_val, d.rows_per_scale, d.a_rows_per_scale = 1.0, 1.0, 1, 1
     n = len(items)
     arr = lambda vals: ctypes.cast((ctypes.c_void_p * n)(*vals), ctypes.c_void_p)  # noqa: E731
@@ -399,9 +400,9 @@ class DeferredGrads:
             # same-shape weight gradients (one per block and linear) as one launch per shape
             groups = {}
             for it in self.dw:
-                groups.setdefault((tuple(it[0].shape), tuple(it[1].shape), it[3] is not None), []).append(it)
-            for items in groups.values():
-                linear_dw_batched(items)
+                groups.setdefault((tuple(it[0].shape), tuple(it[1].shape), it[3] is not None, it[4]), []).append(it[:4])
+            for key, items in groups.items():
+                linear_dw_batched(items, store=key[3])
         if self.ln:
             n = len(self.ln)
             arr = lambda vals, t: (t * n)(*vals)  # noqa: E731

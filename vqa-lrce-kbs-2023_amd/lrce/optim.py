@@ -173,6 +173,7 @@ class FusedAdamW(torch.optim.Optimizer):
         """flat.grad = 0 (the backward kernels accumulate into it).  overlap=True: the 1.25 GB clear runs
         on an aux stream beside the forward (which never touches gradients); grad_ready() must then
         be called before the backward (it makes the current stream wait for the clear)."""
+        self.flat.grads_zeroed()
         if not overlap or not self.flat.grad.is_cuda:
             self.flat.grad.zero_()
             return
