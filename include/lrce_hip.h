@@ -49,8 +49,11 @@ enum {
   LRCE_EPI_ACCUM = 64,    /* C(f32) += y, non-atomic */
   LRCE_EPI_AUX_OUT = 128, /* store pre-activation (bf16) into aux_out */
   LRCE_EPI_OUT_BOTH = 256, /* also write a bf16 copy of y into aux_out (f32 C + bf16 shadow) */
-  LRCE_EPI_BIAS_GRAD = 512 /* weight-gradient GEMMs (A M-major = dY^T): also bias[m] += sum_k A(m,k)
+  LRCE_EPI_BIAS_GRAD = 512, /* weight-gradient GEMMs (A M-major = dY^T): also bias[m] += sum_k A(m,k)
                               (the nn.Linear bias gradient, with A's row map / row scale applied) */
+  LRCE_EPI_SLABS = 1024    /* split_k > 1 with a workspace: write the split slices' f32 slabs
+                              ws[s][m][n] (alpha applied) and launch NO reduce — a consumer such as
+                              lrce_splitk_reduce_ln sums them (C is not written) */
 };
 
 typedef struct LrceGemmDesc {
@@ -196,6 +199,15 @@ int lrce_layernorm_bwd(const void* dy, int dy_f32, const int32_t* dy_map,
  * partials, then a reduce whose last-arriving block per column adds the chunk sums in order) instead
  * of same-address atomics from every block (a NULL or smaller workspace falls back to the atomics). */
 int64_t lrce_layernorm_bwd_workspace(int rows, int cols);
+/* The output projection + residual + post-norm LayerNorm of a BERT sub-layer (HF BertSelfOutput /
+ * BertOutput: LN(resid + dropout(x W^T + b))) from a split-K GEMM's slabs (LRCE_EPI_SLABS): per row
+ * s = sum_k ws[k][r] + bias, dropout (the mask of lrce_dropout over [rows][cols]), + resid; s is stored
+ * in pre (f32, the LayerNorm backward's input; optional), then y = LN(s) gamma + beta (f32), y16 its
+ * 16-bit copy (fp16 when y16_f16, else bf16; optional), mean / rstd.  One wave per row, cols <= 1024,
+ * cols % 256 == 0.  Replaces splitk reduce + lrce_layernorm_fwd (two launches and a round trip). */
+int lrce_splitk_reduce_ln(const float* ws, int split, int rows, int cols, const float* bias, const float* resid,
+                          int64_t ld_res, float p, uint64_t seed, float* pre, const float* gamma, const float* beta,
+                          float eps, float* y, uint16_t* y16, int y16_f16, float* mean, float* rstd, void* stream);
 /* lrce_layernorm_bwd without its gamma / beta reduction launch: *nb_out = the number of per-block partial
  * rows left in workspace (0: none were needed — a one-block problem, no dw / db, or no workspace — and
  * dw / db are already final).  With nb_out > 0 the caller keeps the workspace and later passes

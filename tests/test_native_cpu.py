@@ -110,3 +110,16 @@ def test_torch_library_ops_registered_with_fake_shapes():
         torch.empty(768, device="meta"), torch.empty(2535, 8, device="meta"),
         torch.empty(392, 392, device="meta", dtype=torch.int64), 2, 8)
     assert out.shape == (294, 256) and qkv.shape == (294, 768) and lse.shape == (2, 8, 160)
+
+
+def test_stale_library_is_refused_whole(monkeypatch):
+    """A shared library missing one declared entry point (a stale build) is refused on EVERY call:
+    never handed out half-declared (undeclared ctypes entries would pass 64-bit pointers as ints)."""
+    import ctypes
+    from lrce import _native as N
+    monkeypatch.setattr(N, "_lib", None)
+    monkeypatch.setitem(N._SIGS, "lrce_no_such_entry_point", [])
+    for _ in range(2):
+        with pytest.raises(N.NativeError, match="stale build"):
+            N.lib()
+    assert N._lib is None

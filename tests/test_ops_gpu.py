@@ -1199,3 +1199,29 @@ def test_linear_dw_batched_matches_per_item():
     torch.cuda.synchronize()
     for (dy, x, dw, db), (rw, rb) in zip(items, ref):
         assert rel(dw, rw) < 1e-5 and rel(db, rb) < 1e-5
+
+
+@pytest.mark.parametrize("Kd,split,drop", [(768, 3, 0.1), (3072, 4, 0.1), (3072, 4, 0.0)])
+def test_linear_resid_ln_matches_unfused(Kd, split, drop):
+    """lrce_splitk_reduce_ln after an LRCE_EPI_SLABS split-K GEMM (BERT's output projections: K = 768
+    in 3 slices, K = 3072 in 4) against the unfused launches — one GEMM with the bias / dropout / residual
+    epilogue, then lrce_layernorm_fwd: same dropout mask, f32 rounding of a different K summation order."""
+    kk = K()
+    torch.manual_seed(0)
+    rows, n = 320, 768
+    x = (torch.randn(rows, Kd, device=dev) * 0.5).half()
+    w = (torch.randn(n, Kd, device=dev) / Kd ** 0.5).half()
+    b = torch.randn(n, device=dev) * 0.1
+    resid = torch.randn(rows, n, device=dev)
+    gam, bet = 1 + 0.1 * torch.randn(n, device=dev), 0.1 * torch.randn(n, device=dev)
+    d = (drop, 12345, 1) if drop > 0 else None
+    out16 = torch.empty(rows, n, dtype=torch.float16, device=dev)
+    pre, y, mean, rstd = kk.linear_resid_ln(x, w, b, resid, d, gam, bet, 1e-12, split, out16=out16)
+    ref_pre = kk.linear(x, w, b, out_f32=True, resid=resid, drop=d)
+    ref16 = torch.empty(rows, n, dtype=torch.float16, device=dev)
+    ref_y, ref_m, ref_r = kk.layernorm(ref_pre, gam, bet, 1e-12, out_f32=True, bf16_copy=ref16)
+    torch.cuda.synchronize()
+    assert torch.equal(pre == resid, ref_pre == resid)   # the same dropout mask (a dropped element is resid + 0)
+    assert rel(pre, ref_pre) < 1e-5 and rel(y, ref_y) < 1e-4
+    assert rel(mean, ref_m) < 1e-4 and rel(rstd, ref_r) < 1e-4
+    assert rel(out16.float(), ref16.float()) < 2e-3

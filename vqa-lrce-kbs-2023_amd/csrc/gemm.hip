@@ -1149,8 +1149,8 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
                          d->batch == 1 && !d->c_map && !d->row_scale && d->scale_cols == 0 && d->n % 4 == 0 &&
                          d->ldc % 4 == 0 && (!d->aux || d->ld_aux % 4 == 0) && d->drop_group <= 1 &&
                          d->workspace_elems >= (int64_t)split * d->m * d->n;
-  if (split > 1 && !(d->flags & LRCE_EPI_ATOMIC) && !epi_split)
-    return lrce_fail(LRCE_E_ARG, "gemm: split_k needs ATOMIC, or a workspace and only BIAS / RESID / OUT_F32 epilogues");
+  if (split > 1 && !(d->flags & (LRCE_EPI_ATOMIC | LRCE_EPI_SLABS)) && !epi_split)
+    return lrce_fail(LRCE_E_ARG, "gemm: split_k needs ATOMIC, SLABS, or a workspace and only BIAS / RESID / OUT_F32 epilogues");
   if ((d->flags & (LRCE_EPI_GELU | LRCE_EPI_AUX_OUT)) == LRCE_EPI_AUX_OUT) return lrce_fail(LRCE_E_ARG, "gemm: AUX_OUT needs GELU");
   if ((d->flags & (LRCE_EPI_DGELU | LRCE_EPI_RESID)) && !d->aux) return lrce_fail(LRCE_E_ARG, "gemm: aux missing");
   if ((d->flags & (LRCE_EPI_AUX_OUT | LRCE_EPI_OUT_BOTH)) && !d->aux_out) return lrce_fail(LRCE_E_ARG, "gemm: aux_out missing");
@@ -1193,7 +1193,12 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   p.rng_off = p.drop_p > 0.f ? lrce_rng_offset() : nullptr;
   if (p.f16 && !glds_ok(d))
     return lrce_fail(LRCE_E_ARG, "gemm: f16 needs 16-B aligned bf16-layout operands (LDS-DMA path)");
-  const bool use_ws = (epi_split || (d->workspace && split > 1 && (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)) == 0 &&
+  // slabs only (LRCE_EPI_SLABS): the split slices' partials for a consumer kernel, no reduce launch
+  const bool slabs_only = (d->flags & LRCE_EPI_SLABS) != 0;
+  if (slabs_only && (split < 2 || !d->workspace || d->workspace_elems < (int64_t)split * d->m * d->n || d->batch != 1 ||
+                     (d->flags & ~LRCE_EPI_SLABS) || d->c_map || d->row_scale || d->n % 4 || !glds_ok(d)))
+    return lrce_fail(LRCE_E_ARG, "gemm: LRCE_EPI_SLABS needs split_k > 1, a workspace of split*m*n, the LDS-DMA path and no other epilogue");
+  const bool use_ws = slabs_only || (epi_split || (d->workspace && split > 1 && (d->flags & ~(LRCE_EPI_ATOMIC | LRCE_EPI_BIAS_GRAD)) == 0 &&
                                      (d->flags & LRCE_EPI_ATOMIC) && d->batch == 1 && !d->c_map && !d->row_scale &&
                                      d->scale_cols == 0 && d->n % 4 == 0 && d->ldc % 4 == 0 &&
                                      d->workspace_elems >= (int64_t)split * d->m * d->n)) &&
@@ -1296,7 +1301,9 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     } else if (int rc = launch(std::integral_constant<int, 2>{})) {
       return rc;
     }
-    if (p.ws && epi_split) {
+    if (slabs_only) {
+      // the consumer reduces
+    } else if (p.ws && epi_split) {
       const long long q4 = (long long)d->m * d->n / 4;
       splitk_reduce_epi_kernel<<<(unsigned)((q4 + 255) / 256), 256, 0, s>>>(
           p.ws, split, d->m, d->n, (d->flags & LRCE_EPI_BIAS) ? d->bias : nullptr,

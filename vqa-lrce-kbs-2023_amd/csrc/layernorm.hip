@@ -334,6 +334,78 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
     reinterpret_cast<unsigned*>(part + ((long long)gridDim.x + (gridDim.x + LN_RED_ROWS - 1) / LN_RED_ROWS) * 2 * cols)[threadIdx.x] = 0u;
 }
 
+// split-K reduce + bias + dropout + residual + LayerNorm forward, one wave per row (lrce_splitk_reduce_ln);
+// the same per-element math as splitk_reduce_epi_kernel (gemm.hip) and ln_fwd above
+template <int CH>
+__global__ void __launch_bounds__(256) splitk_reduce_ln_kernel(const float* __restrict__ ws, int split, int rows, int cols,
+                                                               const float* __restrict__ bias, const float* __restrict__ resid,
+                                                               long long ld_res, float p, uint64_t seed,
+                                                               const uint64_t* __restrict__ off, float* __restrict__ pre,
+                                                               const float* __restrict__ w, const float* __restrict__ b,
+                                                               float eps, float* __restrict__ y, bf16* __restrict__ y16,
+                                                               int y16_f16, float* __restrict__ mean_o,
+                                                               float* __restrict__ rstd_o) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const long long mn = (long long)rows * cols;
+  float4 v[CH], ww[CH], bb[CH];
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const int col = 4 * (lane + 64 * t);
+    const long long e = (long long)r * cols + col;
+    float4 s4 = *reinterpret_cast<const float4*>(ws + e);
+    for (int k = 1; k < split; ++k) {
+      const float4 q = *reinterpret_cast<const float4*>(ws + k * mn + e);
+      s4.x += q.x; s4.y += q.y; s4.z += q.z; s4.w += q.w;
+    }
+    ww[t] = *reinterpret_cast<const float4*>(w + col);
+    bb[t] = *reinterpret_cast<const float4*>(b + col);
+    if (bias) {
+      const float4 q = *reinterpret_cast<const float4*>(bias + col);
+      s4.x += q.x; s4.y += q.y; s4.z += q.z; s4.w += q.w;
+    }
+    if (p > 0.f) {
+      const float4 u = lrce_uniform4(lrce_seed(seed, off), (unsigned long long)e >> 2);
+      const float kd = 1.0f - p;
+      s4.x = u.x >= p ? s4.x / kd : 0.f; s4.y = u.y >= p ? s4.y / kd : 0.f;
+      s4.z = u.z >= p ? s4.z / kd : 0.f; s4.w = u.w >= p ? s4.w / kd : 0.f;
+    }
+    if (resid) {
+      const float4 q = *reinterpret_cast<const float4*>(resid + r * ld_res + col);
+      s4.x += q.x; s4.y += q.y; s4.z += q.z; s4.w += q.w;
+    }
+    v[t] = s4;
+    if (pre) *reinterpret_cast<float4*>(pre + e) = s4;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < CH; ++t) s += v[t].x + v[t].y + v[t].z + v[t].w;
+  const float mean = row_sum<64>(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const float a = v[t].x - mean, b2 = v[t].y - mean, c2 = v[t].z - mean, d = v[t].w - mean;
+    q += a * a + b2 * b2 + c2 * c2 + d * d;
+  }
+  const float rstd = rsqrtf(row_sum<64>(q) / cols + eps);
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const int col = 4 * (lane + 64 * t);
+    float4 o;
+    o.x = (v[t].x - mean) * rstd * ww[t].x + bb[t].x;
+    o.y = (v[t].y - mean) * rstd * ww[t].y + bb[t].y;
+    o.z = (v[t].z - mean) * rstd * ww[t].z + bb[t].z;
+    o.w = (v[t].w - mean) * rstd * ww[t].w + bb[t].w;
+    *reinterpret_cast<float4*>(y + (long long)r * cols + col) = o;
+    if (y16) st4_16(y16 + (long long)r * cols + col, o, y16_f16 != 0);
+  }
+  if (lane == 0) {
+    if (mean_o) mean_o[r] = mean;
+    if (rstd_o) rstd_o[r] = rstd;
+  }
+}
+
 // dw[e] += sum_b part[b][e], db[e] += sum_b part[b][cols + e], deterministically: block (x, y) sums
 // LN_RED_ROWS partial rows of 64 columns (32 per wave, 8 loads in flight) into chunk row y; the last
 // of the column block's ny (<= 16) blocks to arrive (agent-scope stores / counter, as the skinny
@@ -611,4 +683,28 @@ extern "C" int64_t lrce_layernorm_bwd_workspace(int rows, int cols) {
   if (rows <= 0 || cols <= 0) return 0;
   const int nb = ln_bwd_blocks(rows, ln_bwd_lpr(cols), true, cols);
   return nb > 1 ? (int64_t)(nb + (nb + LN_RED_ROWS - 1) / LN_RED_ROWS) * 2 * cols + LN_RED_CTRS : 0;
+}
+
+extern "C" int lrce_splitk_reduce_ln(const float* ws, int split, int rows, int cols, const float* bias, const float* resid,
+                                     int64_t ld_res, float p, uint64_t seed, float* pre, const float* gamma,
+                                     const float* beta, float eps, float* y, uint16_t* y16, int y16_f16, float* mean,
+                                     float* rstd, void* stream) {
+  if (!ws || !gamma || !beta || !y) return lrce_fail(LRCE_E_ARG, "splitk_reduce_ln: null pointer");
+  if (split < 1 || rows < 0 || cols % 256 || cols < 256 || cols > 1024 || (resid && ld_res % 4))
+    return lrce_fail(LRCE_E_ARG, "splitk_reduce_ln: split=%d cols=%d ld_res=%lld", split, cols, (long long)ld_res);
+  if (rows == 0) return LRCE_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint64_t* off = p > 0.f ? lrce_rng_offset() : nullptr;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  bf16* o16 = reinterpret_cast<bf16*>(y16);
+#define LRCE_SRL(CH) splitk_reduce_ln_kernel<CH><<<grid, 256, 0, s>>>(ws, split, rows, cols, bias, resid, ld_res, p, seed, off, \
+                                                                      pre, gamma, beta, eps, y, o16, y16_f16, mean, rstd)
+  switch (cols / 256) {
+    case 1: LRCE_SRL(1); break;
+    case 2: LRCE_SRL(2); break;
+    case 3: LRCE_SRL(3); break;
+    default: LRCE_SRL(4); break;
+  }
+#undef LRCE_SRL
+  return lrce_check_launch("splitk_reduce_ln");
 }

@@ -24,8 +24,12 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise NativeError(f"liblrce_hip.so not built ({LIB_PATH}); run `python __graft_entry__.py` / make -C csrc")
-        _lib = ctypes.CDLL(LIB_PATH)
-        _declare(_lib)
+        L = ctypes.CDLL(LIB_PATH)
+        # every entry point declared before the library is handed out: a stale .so missing one raises
+        # here on every call, instead of leaving later entries undeclared (ctypes would then pass
+        # 64-bit pointers as 32-bit ints into the kernels)
+        _declare(L)
+        _lib = L
     return _lib
 
 
@@ -135,6 +139,7 @@ class DecSaBwd(ctypes.Structure):
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = 1, 2, 4, 8
 EPI_OUT_F32, EPI_ATOMIC, EPI_ACCUM, EPI_AUX_OUT, EPI_OUT_BOTH = 16, 32, 64, 128, 256
 EPI_BIAS_GRAD = 512
+EPI_SLABS = 1024
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -146,6 +151,7 @@ _SIGS = {
     "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
     "lrce_gemm_ln": [ctypes.POINTER(GemmDesc), ctypes.POINTER(LnPrologue), _P],
     "lrce_gemm_ptr_batched": [ctypes.POINTER(GemmDesc), _P, _P, _P, _P, _I, _P],
+    "lrce_splitk_reduce_ln": [_P, _I, _I, _I, _P, _P, _I64, _F, _U64, _P, _P, _P, _F, _P, _P, _I, _P, _P, _P],
     "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _I64,
                            _P],
@@ -206,6 +212,10 @@ _SIGS["lrce_layernorm_bwd_workspace"] = [_I, _I]
 
 
 def _declare(L):
+    missing = [name for name in _SIGS if not hasattr(L, name)]
+    if missing:
+        raise NativeError(f"{LIB_PATH} lacks {missing[:5]} ({len(missing)} entry points): a stale build — "
+                          "rebuild with `python __graft_entry__.py`")
     for name, args in _SIGS.items():
         f = getattr(L, name)
         f.argtypes = args

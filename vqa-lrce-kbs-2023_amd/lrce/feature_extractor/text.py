@@ -193,13 +193,22 @@ class _LayerFn(torch.autograd.Function):
                           lse=lse, B=B, H=HEADS, scale=0.125, drop_p=p, seed=seed)
         K.mha_fwd(desc, ctxt)
         drop1 = (p, seed + 1, 1) if p > 0 else None
-        a2 = K.linear(ctxt, w(ao.dense.weight), ao.dense.bias, out_f32=True, resid=x, drop=drop1)   # x + drop(a)
-        h1, m1, r1 = K.layernorm(a2, ao.LayerNorm.weight, ao.LayerNorm.bias, EPS, out_f32=True, bf16_copy=h1b)
-        K.linear(h1b, w(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre, out=g)
         drop2 = (p, seed + 2, 1) if p > 0 else None
-        o2 = _proj_resid(g, w(oo.dense.weight), oo.dense.bias, h1, drop2)                # h1 + drop(g W2^T + b2)
         nxt = st.fviews(i + 1)[0] if i + 1 < st.n else None   # the next layer's fp16 input
-        out, m2, r2 = K.layernorm(o2, oo.LayerNorm.weight, oo.LayerNorm.bias, EPS, out_f32=True, bf16_copy=nxt)
+        if _REDUCE_LN:
+            # each output projection as split-K slabs + ONE reduce launch that also adds bias, dropout
+            # and residual and runs the post-norm LayerNorm (HF BertSelfOutput / BertOutput)
+            a2, h1, m1, r1 = K.linear_resid_ln(ctxt, w(ao.dense.weight), ao.dense.bias, x, drop1, ao.LayerNorm.weight,
+                                              ao.LayerNorm.bias, EPS, 3, out16=h1b)
+            K.linear(h1b, w(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre, out=g)
+            o2, out, m2, r2 = K.linear_resid_ln(g, w(oo.dense.weight), oo.dense.bias, h1, drop2, oo.LayerNorm.weight,
+                                               oo.LayerNorm.bias, EPS, 4, out16=nxt)
+        else:
+            a2 = K.linear(ctxt, w(ao.dense.weight), ao.dense.bias, out_f32=True, resid=x, drop=drop1)   # x + drop(a)
+            h1, m1, r1 = K.layernorm(a2, ao.LayerNorm.weight, ao.LayerNorm.bias, EPS, out_f32=True, bf16_copy=h1b)
+            K.linear(h1b, w(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre, out=g)
+            o2 = _proj_resid(g, w(oo.dense.weight), oo.dense.bias, h1, drop2)                # h1 + drop(g W2^T + b2)
+            out, m2, r2 = K.layernorm(o2, oo.LayerNorm.weight, oo.LayerNorm.bias, EPS, out_f32=True, bf16_copy=nxt)
         ctx.save = (mask, lse, a2, m1, r1, o2, m2, r2)
         ctx.desc = desc
         ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L, ctx.st, ctx.i = layer, flat, p, seed, B, L, st, i
@@ -438,6 +447,7 @@ def _flush_wgrads(st):
 
 _WGRAD_BATCHED = os.environ.get("LRCE_BERT_WGRAD_BATCHED", "1") != "0"   # A/B knob
 _LN_DEFER = os.environ.get("LRCE_BERT_LN_DEFER", "1") != "0"             # A/B knob
+_REDUCE_LN = os.environ.get("LRCE_BERT_REDUCE_LN", "1") != "0"           # A/B knob (linear_resid_ln)
 _STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"      # A/B knob (see FlatParams.claim_fresh)
 _DELAYED_SCALE = os.environ.get("LRCE_BERT_DELAYED_SCALE", "1") != "0"   # A/B knob
 

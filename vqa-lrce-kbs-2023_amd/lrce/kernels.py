@@ -304,6 +304,26 @@ def linear_dw(dy, x, dw, *, a_map=None, rows=None, a_row_scale=None, a_rows_per_
          a_rows_per_scale=a_rows_per_scale, workspace=ws, f16=f16, alpha_dev=alpha_dev)
 
 
+def linear_resid_ln(x, w, bias, resid, drop, gamma, beta, eps, split, *, out16=None, f16=True):
+    """LN(resid + dropout(x W^T + bias)) for a deep-enough K: the GEMM's split-K slices as f32 slabs
+    (LRCE_EPI_SLABS) and ONE lrce_splitk_reduce_ln launch (sum + bias + dropout + residual + LayerNorm).
+    Returns (pre, y, mean, rstd): pre = the LayerNorm input (its backward reads it), y f32, and out16
+    (optional) the fp16 (f16) / bf16 copy of y."""
+    rows, Kd = x.shape
+    n = w.shape[0]
+    ws = torch.empty(split * rows * n, dtype=F32, device=x.device)
+    gemm(x, w, ws, rows, n, Kd, flags=N.EPI_SLABS, split_k=split, workspace=ws, f16=f16)
+    pre = torch.empty(rows, n, dtype=F32, device=x.device)
+    y = torch.empty(rows, n, dtype=F32, device=x.device)
+    mean = torch.empty(rows, dtype=F32, device=x.device)
+    rstd = torch.empty(rows, dtype=F32, device=x.device)
+    p, seed = (float(drop[0]), drop[1] & (2 ** 64 - 1)) if drop is not None and drop[0] > 0 else (0.0, 0)
+    call("lrce_splitk_reduce_ln", ptr(ws), split, rows, n, ptr(bias), ptr(resid),
+         resid.stride(0) if resid is not None else 0, p, seed, ptr(pre), ptr(gamma), ptr(beta), float(eps), ptr(y),
+         ptr(out16), int(out16 is not None and out16.dtype == F16), ptr(mean), ptr(rstd), stream_of(y))
+    return pre, y, mean, rstd
+
+
 def linear_dw_batched(items, store=False):
     """dW_i += dY_i^T X_i (+ db_i += colsum(dY_i)) for items [(dy16, x16, dw, db|None)] of one shape
     (bf16 [T, out] / [T, in], f32 [out, in]) as ONE launch (lrce_gemm_ptr_batched: no split-K).
