@@ -121,13 +121,27 @@ typedef struct LrceGemmDesc {
 } LrceGemmDesc;
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);
-/* n same-shape weight gradients in one launch (the blocks of a Swin stage): entry i computes
- * c[i][m][n] += sum_k a[i][k][m] b[i][k][n] (bf16 dY_i M-major with desc->lda, bf16 X_i N-major with
- * desc->ldb, f32 dW_i with desc->ldc) and, with LRCE_EPI_BIAS_GRAD, bias[i][m] += sum_k a[i][k][m].
- * desc supplies m / n / k / leading dims / alpha and flags = ACCUM (+=) or OUT_F32 (=, for gradients known
- * to be zero) [| BIAS_GRAD: the bias sum is always added]; its pointers, batch,
- * strides and split_k are ignored (one K slice per tile: no split-K slabs or reduce launch — the n-fold
- * tile count fills the chip).  Pointers 16-B aligned; up to 24 entries per launch (more: several). */
+/* One weight gradient of lrce_gemm_grouped: c[m][n] (=|+=) sum_k a[k][m] b[k][n] (bf16 dY M-major with
+ * lda >= m, bf16 X N-major with ldb >= n, f32 dW with ldc >= n) and, with LRCE_EPI_BIAS_GRAD,
+ * bias[m] += sum_k a[k][m].  flags = ACCUM (+=) or OUT_F32 (=, a gradient known to be zero)
+ * [| BIAS_GRAD: the bias sum is always added].  m, n and the leading dims multiples of 8. */
+typedef struct LrceGemmItem {
+  const void* a;
+  const void* b;
+  float* c;
+  float* bias;
+  int32_t m, n, lda, ldb, ldc, flags;
+} LrceGemmItem;
+/* Weight gradients of n linears of any shapes sharing K (the token count) and alpha, as grouped
+ * launches (the four linears x blocks of a Swin stage at once, Swin backward, video_swin_ori.py:46-57,
+ * 150, 187): each entry's 128 x 128 tiles run one K slice (no split-K slabs or reduce launch), the
+ * entries' tiles form one grid.  Up to 80 entries and 8 distinct shapes per launch, and the C / bias
+ * pointers of one launch within 8 GB of each other (more: several launches).  Pointers 16-B aligned. */
+int lrce_gemm_grouped(const LrceGemmItem* items, int n, int k, float alpha, void* stream);
+/* n same-shape weight gradients (the blocks of a Swin stage): lrce_gemm_grouped with items
+ * {a[i], b[i], c[i], bias[i], desc->m, desc->n, desc->lda, desc->ldb, desc->ldc, desc->flags}; desc
+ * supplies the shape / leading dims / alpha / flags (ACCUM or OUT_F32 [| BIAS_GRAD]); its pointers,
+ * batch, strides and split_k are ignored. */
 int lrce_gemm_ptr_batched(const LrceGemmDesc* desc, const void* const* a, const void* const* b, void* const* c,
                           const float* const* bias, int n, void* stream);
 

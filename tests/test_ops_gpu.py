@@ -1201,6 +1201,39 @@ def test_linear_dw_batched_matches_per_item():
         assert rel(dw, rw) < 1e-5 and rel(db, rb) < 1e-5
 
 
+@pytest.mark.parametrize("n_rep,T", [(3, 1000), (23, 200)])
+def test_linear_dw_grouped_mixed_shapes(n_rep, T):
+    """lrce_gemm_grouped (a Swin stage's linears x blocks as one grid: entries of different shapes, some
+    stored (fresh gradients), some accumulated, with and without a bias gradient, C carved from one flat
+    buffer like the training layout plus a few separate tensors) against linear_dw per item: dW and db
+    to f32 rounding, a K tail (T % 64 != 0), and 92 entries (more than one launch's table) at n_rep 23."""
+    kk = K()
+    torch.manual_seed(0)
+    shapes = [(256, 384), (128, 256), (384, 128), (512, 512)]
+    flat = torch.randn(sum(o * i + o for o, i in shapes) * n_rep + 64, device="cuda")
+    off, items, ref = 0, [], []
+    for r in range(n_rep):
+        for j, (O, I) in enumerate(shapes):
+            dy = torch.randn(T, O, device="cuda").to(torch.bfloat16)
+            x = torch.randn(T, I, device="cuda").to(torch.bfloat16)
+            if (r + j) % 5 == 4:
+                dw, db = torch.randn(O, I, device="cuda"), torch.randn(O, device="cuda")
+            else:
+                dw = flat[off:off + O * I].view(O, I); off += O * I
+                db = flat[off:off + O]; off += O
+            store, bias = (r + j) % 3 == 0, (r + 2 * j) % 4 != 1
+            rw, rb = (torch.zeros_like(dw) if store else dw.clone()), db.clone()
+            kk.linear_dw(dy, x, rw, bias_grad=rb if bias else None)
+            items.append((dy, x, dw, db if bias else None, store))
+            ref.append((rw, rb))
+    kk.linear_dw_grouped(items)
+    torch.cuda.synchronize()
+    for (dy, x, dw, db, store), (rw, rb) in zip(items, ref):
+        assert rel(dw, rw) < 1e-5
+        if db is not None:
+            assert rel(db, rb) < 1e-5
+
+
 @pytest.mark.parametrize("Kd,split,drop", [(768, 3, 0.1), (3072, 4, 0.1), (3072, 4, 0.0)])
 def test_linear_resid_ln_matches_unfused(Kd, split, drop):
     """lrce_splitk_reduce_ln after an LRCE_EPI_SLABS split-K GEMM (BERT's output projections: K = 768

@@ -2,7 +2,8 @@
 """Weight gradients of a Swin stage's blocks (dev tool, GPU): n_blocks separate split-K launches
 (linear_dw: f32 slabs + reduce, what the block backward issues) against ONE batched launch over the
 blocks (batch = n_blocks, one K slice per tile, ACCUM + BIAS_GRAD with per-batch strides), on the
-stage-3 shapes.  HIP events over back-to-back repetitions.
+stage-3 shapes; then a stage's flush as one launch per shape against ONE grouped launch over every
+linear and block (stage 3: 18 blocks, stage 4: 2 blocks).  HIP events over back-to-back repetitions.
 
     python tools/dw_batch_bench.py [--blocks 18] [--iters 5]
 """
@@ -70,6 +71,38 @@ def main():
         print(f"{name:5s} {O:5d}x{I:5d}x{T}: {nb} split-K launches {ts:8.1f} us ({fl / ts / 1e6:6.1f} TF/s)   "
               f"batched {tb:8.1f} us ({fl / tb / 1e6:6.1f} TF/s)   rel diff w {err:.1e} b {errb:.1e}", flush=True)
     print(f"stage total: separate {total_sep:.1f} us, batched {total_bat:.1f} us")
+    grouped_vs_per_shape(nb, T, SHAPES, a.iters)
+    C4 = [("qkv", 3072, 1024), ("proj", 1024, 1024), ("fc1", 4096, 1024), ("fc2", 1024, 4096)]
+    grouped_vs_per_shape(2, T // 4, C4, a.iters)
+
+
+def grouped_vs_per_shape(nb, T, shapes, iters):
+    """A stage's flush: the blocks' weight gradients as one same-shape launch per linear
+    (linear_dw_batched) against ONE grouped launch over every linear and block (linear_dw_grouped)."""
+    bf = torch.bfloat16
+    items = []
+    for j in range(nb):
+        for name, O, I in shapes:
+            items.append((torch.rand(T, O, device="cuda").sub_(0.5).to(bf), torch.rand(T, I, device="cuda").sub_(0.5).to(bf),
+                          torch.zeros(O, I, device="cuda"), torch.zeros(O, device="cuda"), False))
+
+    def per_shape():
+        for k in range(len(shapes)):
+            K.linear_dw_batched([it[:4] for it in items[k::len(shapes)]])
+
+    def grouped():
+        K.linear_dw_grouped(items)
+
+    per_shape(); torch.cuda.synchronize()
+    ref = [(it[2].clone(), it[3].clone()) for it in items]
+    for it in items:
+        it[2].zero_(); it[3].zero_()
+    grouped(); torch.cuda.synchronize()
+    err = max(((it[2] - r[0]).abs().max() / r[0].abs().max()).item() for it, r in zip(items, ref))
+    tp, tg = timed(per_shape, iters), timed(grouped, iters)
+    fl = sum(2.0 * T * O * I for _, O, I in shapes) * nb
+    print(f"{nb} blocks x {[s[0] for s in shapes]} T={T}: per-shape launches {tp:8.1f} us ({fl / tp / 1e6:6.1f} TF/s)   "
+          f"grouped {tg:8.1f} us ({fl / tg / 1e6:6.1f} TF/s)   first-pass rel diff {err:.1e}", flush=True)
 
 
 if __name__ == "__main__":

@@ -17,6 +17,7 @@
 // and are zeroed by a select), which keeps the global loads of a K-tile batched.
 #include <cstdlib>
 #include <type_traits>
+#include <vector>
 
 #include "common.h"
 #include "lrce_capi.h"
@@ -62,15 +63,25 @@ struct GemmP {
   const uint64_t* rng_off;
 };
 
-// Pointer-table batch (lrce_gemm_ptr_batched): batch entry z reads A / B / C / bias from its own
-// pointers instead of base + z * stride — a Swin stage's per-block weight gradients as one launch
-// without copying the blocks' operands into uniformly strided buffers.
-constexpr int GPT = 24;
+// Grouped weight-gradient launch (lrce_gemm_grouped; lrce_gemm_ptr_batched is its one-shape case):
+// entry e reads A / B from its own pointers, writes C / the bias gradient at f32 element offsets from
+// p.c / p.bias, has its own shape (one of GSH per launch) and epilogue flags, and owns workgroups
+// [start[e], start[e+1]) of a 1-D grid.  A Swin stage's four linears x blocks then run as ONE launch:
+// no tail round per shape, and with the grid XCD-remapped as a whole each XCD walks whole entries in
+// order, so its L2 reads an entry's dY / X panels once instead of every XCD reading a share of each.
+constexpr int GPT = 80, GSH = 8;
+struct GemmShape {
+  int m, n, lda, ldb, ldc, tiles_m, tiles_n;
+};
 struct GemmPT : GemmP {
+  int ng;                 // entries
+  GemmShape sh[GSH];
+  int start[GPT + 1];     // first workgroup of each entry; start[ng] = the grid
+  int meta[GPT];          // shape index | epilogue flags << 8
+  int coff[GPT];          // C offset from p.c (f32 elements)
+  int boff[GPT];          // bias-gradient offset from p.bias (f32 elements), -1: none
   const void* ta[GPT];
   const bf16* tb[GPT];
-  void* tc[GPT];
-  const float* tbias[GPT];
 };
 template <bool PT>
 using GemmArg = typename std::conditional<PT, GemmPT, GemmP>::type;
@@ -601,20 +612,47 @@ constexpr int pf_rs_slots(int im) { return im <= 4 ? im : 1; }
 // DROP: the fused-dropout epilogue (a separate instantiation: the branch in every kernel measured
 // 14-17 % slower tall-tile GEMMs through changed code generation)
 template <int TBM, int TBN, bool A_KM, bool B_KM, bool F16 = false, int NS = 2, bool DROP = false, bool PT = false>
-__global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmArg<PT> p) {
+__global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(const GemmArg<PT> pa) {
+  // the shared fields as a local copy (registers); the grouped tables are read from the unmodified
+  // argument (a dynamically indexed copy of the whole struct would live in scratch)
+  GemmP p = pa;
   constexpr int WM = TBM / 2, WN = TBN / 2;      // per-wave tile
   constexpr int IM = WM / 16, JN = WN / 16;      // 16x16 accumulator blocks per wave
   constexpr int A_EL = TBM * BK, B_EL = TBN * BK;
   __shared__ __attribute__((aligned(16))) bf16 lds[NS * (A_EL + B_EL)];  // [stage][A | B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tiles = p.tiles_m * p.tiles_n;
   const int z = blockIdx.y;
   const int bz = z / p.split_k, sk = z % p.split_k;
-  if constexpr (PT) p.bias = p.tbias[bz];
-  else p.bias += (long long)bz * p.sbias;
-  if (p.alpha_dev) p.alpha_dev += (long long)bz * p.salpha;
-  const int lin = xcd_remap(blockIdx.x, tiles);
+  int lin;
+  const bf16* abase;
+  const bf16* bbase;
+  if constexpr (PT) {
+    // grouped: the entry owning this workgroup (binary search of the start table), its shape / flags
+    const int g = xcd_remap(blockIdx.x, pa.start[pa.ng]);
+    int lo = 0, hi = pa.ng - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pa.start[mid] <= g) lo = mid;
+      else hi = mid - 1;
+    }
+    const int meta = pa.meta[lo];
+    const GemmShape sh = pa.sh[meta & (GSH - 1)];
+    p.m = sh.m; p.n = sh.n; p.lda = sh.lda; p.ldb = sh.ldb; p.ldc = sh.ldc;
+    p.tiles_m = sh.tiles_m; p.tiles_n = sh.tiles_n;
+    p.flags = meta >> 8;
+    p.bias = pa.boff[lo] >= 0 ? p.bias + pa.boff[lo] : nullptr;
+    p.c = static_cast<float*>(p.c) + pa.coff[lo];
+    abase = static_cast<const bf16*>(pa.ta[lo]);
+    bbase = pa.tb[lo];
+    lin = g - pa.start[lo];
+  } else {
+    p.bias += (long long)bz * p.sbias;
+    if (p.alpha_dev) p.alpha_dev += (long long)bz * p.salpha;
+    lin = xcd_remap(blockIdx.x, p.tiles_m * p.tiles_n);
+    abase = static_cast<const bf16*>(p.a) + (long long)bz * p.sa;
+    bbase = p.b + (long long)bz * p.sb;
+  }
   int tm, tn;
   tile_of(p, lin, tm, tn);
   const int m0 = tm * TBM, n0 = tn * TBN;
@@ -625,15 +663,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmArg<PT> p) {
     p.trace[(long long)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
   }
 #endif
-  const bf16* abase;
-  const bf16* bbase;
-  if constexpr (PT) {
-    abase = static_cast<const bf16*>(p.ta[bz]);
-    bbase = p.tb[bz];
-  } else {
-    abase = static_cast<const bf16*>(p.a) + (long long)bz * p.sa;
-    bbase = p.b + (long long)bz * p.sb;
-  }
   const int kb = sk * p.k_chunk;
   const int ke = min(p.k, kb + p.k_chunk);
   const int nfull = ke > kb ? (ke - kb) / BK : 0;
@@ -810,10 +839,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(GemmArg<PT> p) {
       if (m < p.m) __hip_atomic_fetch_add(db + m, alpha_of(p) * accb[i][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  char* cbase;
-  if constexpr (PT) cbase = static_cast<char*>(p.tc[bz]);
-  else cbase = static_cast<char*>(p.c) +
-               (long long)bz * p.sc * ((p.flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
+  char* const cbase = static_cast<char*>(p.c) +   // (grouped: already the entry's C, bz = 0)
+                      (long long)bz * p.sc * ((p.flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) ? 4 : 2);
   if ((p.flags & LRCE_EPI_ATOMIC) && !p.ws) {
     // split-K partials: stage 32-row slabs through LDS (free now) so each atomic instruction covers
     // consecutive columns of a row.  acc[i][j][r] = C[m = i*16 + (lane&15)][n = j*16 + 4*(lane>>4) + r]
@@ -1332,55 +1359,102 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   return lrce_check_launch("gemm");
 }
 
-// Weight gradients of n same-shape linears in one launch: dW_z[m][n] += sum_k dY_z[k][m] X_z[k][n]
-// (A M-major = dY_z with lda, B N-major = X_z with ldb, C_z f32 with ldc), bias_z[m] += sum_k dY_z[k][m]
-// when d->flags has BIAS_GRAD.  One K slice per tile (no split-K slabs, no reduce launch): the
-// n-fold tile count fills the chip.  d gives the shape / leading dims / flags (ACCUM [| BIAS_GRAD]);
-// its a / b / c / bias / batch / strides are ignored.  Chunks of GPT entries per launch.
+// Weight gradients of n linears in grouped launches: dW_e (=|+=) sum_k dY_e[k][m] X_e[k][n] (A M-major =
+// dY_e, B N-major = X_e, C_e f32), db_e[m] += sum_k dY_e[k][m] for entries with BIAS_GRAD.  One K slice
+// per tile (no split-K slabs, no reduce launch): the entries' summed tile count fills the chip.  All
+// entries share K (the token count) and alpha; up to GPT entries / GSH distinct shapes per launch.
+extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alpha, void* stream) {
+  if (n < 0 || (n > 0 && !it) || k <= 0) return lrce_fail(LRCE_E_ARG, "gemm_grouped: n=%d k=%d", n, k);
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  for (int i = 0; i < n; ++i) {
+    const LrceGemmItem& e = it[i];
+    const int cf = e.flags & (LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32);
+    const bool bg = e.flags & LRCE_EPI_BIAS_GRAD;
+    if ((e.flags & ~(LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32 | LRCE_EPI_BIAS_GRAD)) ||
+        (cf != LRCE_EPI_ACCUM && cf != LRCE_EPI_OUT_F32) || (bg && !e.bias))
+      return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d flags %d (ACCUM or OUT_F32 [| BIAS_GRAD with a bias])", i, e.flags);
+    if (e.m <= 0 || e.n <= 0 || e.m % 8 || e.n % 8 || e.lda < e.m || e.ldb < e.n || e.ldc < e.n || e.lda % 8 ||
+        e.ldb % 8 || e.ldc % 8)
+      return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d m=%d n=%d lda=%d ldb=%d ldc=%d", i, e.m, e.n, e.lda, e.ldb, e.ldc);
+    if (((long long)k * e.lda + e.m) * 2 >= (1LL << 31) || ((long long)k * e.ldb + e.n) * 2 >= (1LL << 31))
+      return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d operand extent over 2 GB", i);
+    if (!e.a || !e.b || !e.c || !al16(e.a) || !al16(e.b) || !al16(e.c) || (bg && !al16(e.bias)))
+      return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d null or not 16-B aligned", i);
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  constexpr long long SPAN = (1LL << 31) - 1;   // f32 elements an offset from the chunk's base may reach
+  int i = 0;
+  while (i < n) {
+    // one launch: entries i .. j-1, as many as fit the tables and keep C / bias within an int offset
+    GemmPT p{};
+    p.k = k; p.split_k = 1; p.batch = 1;
+    p.k_chunk = (k + BK - 1) / BK * BK;
+    p.alpha = alpha; p.scale_val = 1.f; p.rows_per_scale = 1; p.a_rows_per_scale = 1;
+    p.group_m = 4;
+    p.vec = 1;
+    p.trace = g_gemm_trace;
+    uintptr_t clo = ~(uintptr_t)0, chi = 0, blo = ~(uintptr_t)0, bhi = 0;
+    int nsh = 0, j = i, tiles = 0;
+    for (; j < n && j - i < GPT; ++j) {
+      const LrceGemmItem& e = it[j];
+      int si = 0;
+      while (si < nsh && !(p.sh[si].m == e.m && p.sh[si].n == e.n && p.sh[si].lda == e.lda && p.sh[si].ldb == e.ldb &&
+                           p.sh[si].ldc == e.ldc))
+        ++si;
+      if (si == nsh && nsh == GSH) break;
+      const uintptr_t c0 = reinterpret_cast<uintptr_t>(e.c);
+      const uintptr_t c1 = c0 + ((uintptr_t)(e.m - 1) * e.ldc + e.n) * 4;
+      const uintptr_t nclo = c0 < clo ? c0 : clo, nchi = c1 > chi ? c1 : chi;
+      if ((long long)((nchi - nclo) / 4) > SPAN) break;
+      uintptr_t nblo = blo, nbhi = bhi;
+      if (e.flags & LRCE_EPI_BIAS_GRAD) {
+        const uintptr_t b0 = reinterpret_cast<uintptr_t>(e.bias), b1 = b0 + (uintptr_t)e.m * 4;
+        nblo = b0 < blo ? b0 : blo; nbhi = b1 > bhi ? b1 : bhi;
+        if ((long long)((nbhi - nblo) / 4) > SPAN) break;
+      }
+      const int tm = (e.m + BM - 1) / BM, tn = (e.n + BN - 1) / BN;
+      if ((long long)tiles + (long long)tm * tn >= (1LL << 31)) break;
+      if (si == nsh) p.sh[nsh++] = GemmShape{e.m, e.n, e.lda, e.ldb, e.ldc, tm, tn};
+      clo = nclo; chi = nchi; blo = nblo; bhi = nbhi;
+      p.start[j - i] = tiles;
+      tiles += tm * tn;
+      p.meta[j - i] = si | (e.flags << 8);
+      p.ta[j - i] = e.a;
+      p.tb[j - i] = static_cast<const bf16*>(e.b);
+    }
+    p.ng = j - i;
+    p.start[p.ng] = tiles;
+    p.c = reinterpret_cast<void*>(clo);
+    p.bias = bhi ? reinterpret_cast<const float*>(blo) : nullptr;
+    for (int q = 0; q < p.ng; ++q) {
+      const LrceGemmItem& e = it[i + q];
+      p.coff[q] = (int)((reinterpret_cast<uintptr_t>(e.c) - clo) / 4);
+      p.boff[q] = (e.flags & LRCE_EPI_BIAS_GRAD) ? (int)((reinterpret_cast<uintptr_t>(e.bias) - blo) / 4) : -1;
+    }
+    p.a = p.ta[0]; p.b = p.tb[0];
+    p.m = p.sh[0].m; p.n = p.sh[0].n; p.tiles_m = p.sh[0].tiles_m; p.tiles_n = p.sh[0].tiles_n;
+    gemm_glds_kernel<128, 128, false, false, false, 2, false, true><<<dim3(tiles, 1), NT, 0, s>>>(p);
+    i = j;
+  }
+  return lrce_check_launch("gemm_grouped");
+}
+
+// n same-shape weight gradients (d: shape / leading dims / flags ACCUM or OUT_F32 [| BIAS_GRAD]; its
+// a / b / c / bias / batch / strides are ignored): lrce_gemm_grouped with one shape.
 extern "C" int lrce_gemm_ptr_batched(const LrceGemmDesc* d, const void* const* a, const void* const* b, void* const* c,
                                      const float* const* bias, int n, void* stream) {
   if (!d || n < 0 || (n > 0 && (!a || !b || !c))) return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: null argument");
   if (n == 0) return LRCE_OK;
   const bool bg = d->flags & LRCE_EPI_BIAS_GRAD;
-  const int cf = d->flags & (LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32);
-  if ((d->flags & ~(LRCE_EPI_ACCUM | LRCE_EPI_OUT_F32 | LRCE_EPI_BIAS_GRAD)) ||
-      (cf != LRCE_EPI_ACCUM && cf != LRCE_EPI_OUT_F32) || d->a_kmajor || d->b_kmajor ||
-      d->a_f32 || d->b_f32 || d->f16 || d->a_map || d->c_map || d->split_k > 1 || d->alpha_dev || d->row_scale ||
-      d->a_row_scale || d->scale_cols || d->drop_p > 0.f || (bg && !bias))
+  if (d->a_kmajor || d->b_kmajor || d->a_f32 || d->b_f32 || d->f16 || d->a_map || d->c_map || d->split_k > 1 ||
+      d->alpha_dev || d->row_scale || d->a_row_scale || d->scale_cols || d->drop_p > 0.f || (bg && !bias) ||
+      d->lda > INT32_MAX || d->ldb > INT32_MAX || d->ldc > INT32_MAX)
     return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: bf16 weight gradients only (M-major dY, N-major X, ACCUM or OUT_F32 [| BIAS_GRAD])");
-  if (d->m <= 0 || d->n <= 0 || d->k <= 0 || d->m % 8 || d->n % 8 || d->lda % 8 || d->ldb % 8 || d->ldc % 8)
-    return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: m=%d n=%d lda=%lld ldb=%lld ldc=%lld", d->m, d->n, (long long)d->lda,
-                     (long long)d->ldb, (long long)d->ldc);
-  if (((long long)d->k * d->lda + d->m) * 2 >= (1LL << 31) || ((long long)d->k * d->ldb + d->n) * 2 >= (1LL << 31))
-    return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: operand extent over 2 GB");
-  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  std::vector<LrceGemmItem> items(n);
   for (int i = 0; i < n; ++i)
-    if (!a[i] || !b[i] || !c[i] || !al16(a[i]) || !al16(b[i]) || !al16(c[i]) || (bg && (!bias[i] || !al16(bias[i]))))
-      return lrce_fail(LRCE_E_ARG, "gemm_ptr_batched: entry %d null or not 16-B aligned", i);
-  GemmPT p{};
-  p.lda = d->lda; p.ldb = d->ldb; p.ldc = d->ldc;
-  p.m = d->m; p.n = d->n; p.k = d->k; p.split_k = 1;
-  p.k_chunk = (d->k + BK - 1) / BK * BK;
-  p.flags = d->flags;
-  p.alpha = d->alpha; p.scale_val = 1.f; p.rows_per_scale = 1; p.a_rows_per_scale = 1;
-  p.tiles_m = (d->m + BM - 1) / BM; p.tiles_n = (d->n + BN - 1) / BN;
-  p.group_m = 4;
-  p.vec = 1;
-  p.trace = g_gemm_trace;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  for (int i0 = 0; i0 < n; i0 += GPT) {
-    const int cnt = n - i0 < GPT ? n - i0 : GPT;
-    for (int j = 0; j < cnt; ++j) {
-      p.ta[j] = a[i0 + j];
-      p.tb[j] = static_cast<const bf16*>(b[i0 + j]);
-      p.tc[j] = c[i0 + j];
-      p.tbias[j] = bg ? bias[i0 + j] : nullptr;
-    }
-    p.batch = cnt;
-    p.a = p.ta[0]; p.b = p.tb[0]; p.c = p.tc[0]; p.bias = p.tbias[0];
-    gemm_glds_kernel<128, 128, false, false, false, 2, false, true><<<dim3(p.tiles_m * p.tiles_n, cnt), NT, 0, s>>>(p);
-  }
-  return lrce_check_launch("gemm_ptr_batched");
+    items[i] = LrceGemmItem{a[i], b[i], static_cast<float*>(c[i]), bg ? const_cast<float*>(bias[i]) : nullptr,
+                            d->m, d->n, (int32_t)d->lda, (int32_t)d->ldb, (int32_t)d->ldc, d->flags};
+  return lrce_gemm_grouped(items.data(), n, d->k, d->alpha, stream);
 }
 
 // debug: phase timestamps of gemm_glds_kernel into buf (device, >= 8 per workgroup), NULL = off; the

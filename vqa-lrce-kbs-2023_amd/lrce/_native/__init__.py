@@ -136,6 +136,14 @@ class DecSaBwd(ctypes.Structure):
     ] + _WS
 
 
+class GemmItem(ctypes.Structure):
+    _fields_ = [
+        ("a", ctypes.c_void_p), ("b", ctypes.c_void_p), ("c", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("m", ctypes.c_int32), ("n", ctypes.c_int32), ("lda", ctypes.c_int32), ("ldb", ctypes.c_int32),
+        ("ldc", ctypes.c_int32), ("flags", ctypes.c_int32),
+    ]
+
+
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = 1, 2, 4, 8
 EPI_OUT_F32, EPI_ATOMIC, EPI_ACCUM, EPI_AUX_OUT, EPI_OUT_BOTH = 16, 32, 64, 128, 256
 EPI_BIAS_GRAD = 512
@@ -151,6 +159,7 @@ _SIGS = {
     "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
     "lrce_gemm_ln": [ctypes.POINTER(GemmDesc), ctypes.POINTER(LnPrologue), _P],
     "lrce_gemm_ptr_batched": [ctypes.POINTER(GemmDesc), _P, _P, _P, _P, _I, _P],
+    "lrce_gemm_grouped": [ctypes.POINTER(GemmItem), _I, _I, _F, _P],
     "lrce_splitk_reduce_ln": [_P, _I, _I, _I, _P, _P, _I64, _F, _U64, _P, _P, _P, _F, _P, _P, _I, _P, _P, _P],
     "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _I64,

@@ -326,28 +326,37 @@ def linear_resid_ln(x, w, bias, resid, drop, gamma, beta, eps, split, *, out16=N
 
 def linear_dw_batched(items, store=False):
     """dW_i += dY_i^T X_i (+ db_i += colsum(dY_i)) for items [(dy16, x16, dw, db|None)] of one shape
-    (bf16 [T, out] / [T, in], f32 [out, in]) as ONE launch (lrce_gemm_ptr_batched: no split-K).
-    store: dW_i = dY_i^T X_i (the gradients are known zero: FlatParams.claim_fresh); db_i still added."""
+    (bf16 [T, out] / [T, in], f32 [out, in]).  store: dW_i = dY_i^T X_i (the gradients are known zero:
+    FlatParams.claim_fresh); db_i still added.  (linear_dw_grouped with one shape.)"""
     dy0, x0, dw0, db0 = items[0]
-    T, O, I = x0.shape[0], dw0.shape[0], dw0.shape[1]
-    bias = db0 is not None
+    shape = (tuple(dy0.shape), tuple(x0.shape), db0 is not None)
     for dy, x, dw, db in items:
+        if (tuple(dy.shape), tuple(x.shape), db is not None) != shape:
+            raise N.NativeError("linear_dw_batched: items differ in shape")
+    linear_dw_grouped([(dy, x, dw, db, store) for dy, x, dw, db in items])
+
+
+def linear_dw_grouped(items):
+    """Weight gradients of linears of any shapes over the same tokens, items [(dy16, x16, dw, db|None,
+    store)] (bf16 [T, out] / [T, in], f32 [out, in]): dW = (store) or += (not store) dY^T X, db +=
+    colsum(dY), as grouped launches (lrce_gemm_grouped: every entry's tiles in one grid, one K slice
+    per tile)."""
+    T = items[0][1].shape[0]
+    arr = (N.GemmItem * len(items))()
+    flops = 0.0
+    for e, (dy, x, dw, db, store) in zip(arr, items):
+        O, I = dw.shape
         if (dy.dtype != BF16 or x.dtype != BF16 or dw.dtype != F32 or dy.shape != (T, O) or x.shape != (T, I)
-                or dw.shape != (O, I) or (db is not None) != bias or not dw.is_contiguous()
-                or dy.stride(1) != 1 or x.stride(1) != 1):
-            raise N.NativeError("linear_dw_batched: items differ in shape / dtype / layout")
-    d = N.GemmDesc()
-    d.m, d.n, d.k, d.batch = O, I, T, 1
-    d.lda, d.ldb, d.ldc = _ld(dy0), _ld(x0), I
-    d.a_kmajor, d.b_kmajor = 0, 0
-    d.flags = (N.EPI_OUT_F32 if store else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if bias else 0)
-    d.alpha, d.scale_val, d.rows_per_scale, d.a_rows_per_scale = 1.0, 1.0, 1, 1
-    n = len(items)
-    arr = lambda vals: ctypes.cast((ctypes.c_void_p * n)(*vals), ctypes.c_void_p)  # noqa: E731
-    _timed("gemm", dw0, lambda: call("lrce_gemm_ptr_batched", ctypes.byref(d), arr([ptr(i[0]) for i in items]),
-                                     arr([ptr(i[1]) for i in items]), arr([ptr(i[2]) for i in items]),
-                                     arr([ptr(i[3]) for i in items]), n, stream_of(dw0)),
-           flops=2.0 * O * I * T * n, key=(O, I, T, n, "AM", "BN", "a16", 1, d.flags))
+                or not dw.is_contiguous() or dy.stride(1) != 1 or x.stride(1) != 1
+                or (db is not None and (db.dtype != F32 or db.shape != (O,)))):
+            raise N.NativeError("linear_dw_grouped: an item's dtype / shape / layout")
+        e.a, e.b, e.c, e.bias = ptr(dy), ptr(x), ptr(dw), ptr(db)
+        e.m, e.n, e.lda, e.ldb, e.ldc = O, I, _ld(dy), _ld(x), I
+        e.flags = (N.EPI_OUT_F32 if store else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if db is not None else 0)
+        flops += 2.0 * O * I * T
+    dw0 = items[0][2]
+    _timed("gemm", dw0, lambda: call("lrce_gemm_grouped", arr, len(items), T, 1.0, stream_of(dw0)),
+           flops=flops, key=("grouped", T, len(items)))
 
 
 def colsum(x, out, *, row_map=None, rows=None, row_scale=None, rows_per_scale=1):
@@ -398,6 +407,9 @@ def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1,
     return out
 
 
+_GROUPED_DW = os.environ.get("LRCE_GROUPED_DW", "1") != "0"   # A/B knob: one grouped launch vs one per shape
+
+
 class DeferredGrads:
     """Parameter-gradient reductions that nothing downstream reads before the optimizer, collected over
     several blocks and issued as batched launches by flush(): LayerNorm gamma / beta sums
@@ -409,20 +421,24 @@ class DeferredGrads:
         self.n_items = n_items   # blocks sharing this object (one weight gradient each per linear)
 
     def wants_dw(self, out_f, in_f, tokens):
-        """Batch a weight gradient of this shape?  Only when the blocks' 128 x 128 tiles fill the chip
-        (>= 256 workgroups) and each tile's single K loop stays short: one K slice per tile means a
-        stage-1 weight (4 tiles x 2 blocks, 282 240 tokens) would run 8 workgroups for milliseconds."""
+        """Batch a weight gradient of this shape?  Only when each tile's single K loop stays short (one
+        K slice per tile: a stage-1 weight, 282 240 tokens, would run its few workgroups for
+        milliseconds) and the blocks' 128 x 128 tiles of this linear are a fair share of a chip-filling
+        grouped launch (stage 4's 1024 x 1024 projection: 2 x 64)."""
         tiles = -(-out_f // 128) * -(-in_f // 128)
-        return tiles * self.n_items >= 256 and tokens <= 32768
+        return tiles * self.n_items >= (64 if _GROUPED_DW else 256) and tokens <= 32768
 
     def flush(self, stream_tensor):
         if self.dw:
-            # same-shape weight gradients (one per block and linear) as one launch per shape
-            groups = {}
-            for it in self.dw:
-                groups.setdefault((tuple(it[0].shape), tuple(it[1].shape), it[3] is not None, it[4]), []).append(it[:4])
-            for key, items in groups.items():
-                linear_dw_batched(items, store=key[3])
+            # every deferred weight gradient (the stage's linears x blocks, same tokens) in one grouped grid
+            if _GROUPED_DW:
+                linear_dw_grouped(self.dw)
+            else:
+                groups = {}
+                for it in self.dw:
+                    groups.setdefault((tuple(it[0].shape), tuple(it[1].shape), it[3] is not None, it[4]), []).append(it[:4])
+                for key, items in groups.items():
+                    linear_dw_batched(items, store=key[3])
         if self.ln:
             n = len(self.ln)
             arr = lambda vals, t: (t * n)(*vals)  # noqa: E731
