@@ -121,22 +121,26 @@ typedef struct LrceGemmDesc {
 } LrceGemmDesc;
 
 int lrce_gemm(const LrceGemmDesc* desc, void* stream);
-/* One weight gradient of lrce_gemm_grouped: c[m][n] (=|+=) sum_k a[k][m] b[k][n] (bf16 dY M-major with
- * lda >= m, bf16 X N-major with ldb >= n, f32 dW with ldc >= n) and, with LRCE_EPI_BIAS_GRAD,
- * bias[m] += sum_k a[k][m].  flags = ACCUM (+=) or OUT_F32 (=, a gradient known to be zero)
- * [| BIAS_GRAD: the bias sum is always added].  m, n and the leading dims multiples of 8. */
+/* One weight gradient of lrce_gemm_grouped: c[m][n] (=|+=) alpha sum_k a[k][m] b[k][n] (16-bit dY M-major
+ * with lda >= m, 16-bit X N-major with ldb >= n, f32 dW with ldc >= n) and, with LRCE_EPI_BIAS_GRAD,
+ * bias[m] += alpha sum_k a[k][m].  flags = ACCUM (+=) or OUT_F32 (=, a gradient known to be zero)
+ * [| BIAS_GRAD: the bias sum is always added].  alpha_dev: alpha read from device memory (a gradient
+ * scale computed on the GPU; NULL: the call's alpha).  f16: the 16-bit operands are IEEE fp16 (else
+ * bf16).  m, n and the leading dims multiples of 8. */
 typedef struct LrceGemmItem {
   const void* a;
   const void* b;
   float* c;
   float* bias;
-  int32_t m, n, lda, ldb, ldc, flags;
+  const float* alpha_dev;
+  int32_t m, n, lda, ldb, ldc, flags, f16;
 } LrceGemmItem;
 /* Weight gradients of n linears of any shapes sharing K (the token count) and alpha, as grouped
  * launches (the four linears x blocks of a Swin stage at once, Swin backward, video_swin_ori.py:46-57,
  * 150, 187): each entry's 128 x 128 tiles run one K slice (no split-K slabs or reduce launch), the
- * entries' tiles form one grid.  Up to 80 entries and 8 distinct shapes per launch, and the C / bias
- * pointers of one launch within 8 GB of each other (more: several launches).  Pointers 16-B aligned. */
+ * entries' tiles form one grid.  Up to 80 entries and 8 distinct shapes per launch, one operand
+ * format (f16) per launch, and the C / bias / alpha pointers of one launch within 8 GB of each other
+ * (more: several launches).  Pointers 16-B aligned (alpha_dev 4-B). */
 int lrce_gemm_grouped(const LrceGemmItem* items, int n, int k, float alpha, void* stream);
 /* n same-shape weight gradients (the blocks of a Swin stage): lrce_gemm_grouped with items
  * {a[i], b[i], c[i], bias[i], desc->m, desc->n, desc->lda, desc->ldb, desc->ldc, desc->flags}; desc

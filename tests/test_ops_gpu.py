@@ -1201,12 +1201,13 @@ def test_linear_dw_batched_matches_per_item():
         assert rel(dw, rw) < 1e-5 and rel(db, rb) < 1e-5
 
 
-@pytest.mark.parametrize("n_rep,T", [(3, 1000), (23, 200)])
-def test_linear_dw_grouped_mixed_shapes(n_rep, T):
+@pytest.mark.parametrize("n_rep,T,f16", [(3, 1000, False), (23, 200, False), (4, 320, True)])
+def test_linear_dw_grouped_mixed_shapes(n_rep, T, f16):
     """lrce_gemm_grouped (a Swin stage's linears x blocks as one grid: entries of different shapes, some
     stored (fresh gradients), some accumulated, with and without a bias gradient, C carved from one flat
     buffer like the training layout plus a few separate tensors) against linear_dw per item: dW and db
-    to f32 rounding, a K tail (T % 64 != 0), and 92 entries (more than one launch's table) at n_rep 23."""
+    to f32 rounding, a K tail (T % 64 != 0), and 92 entries (more than one launch's table) at n_rep 23;
+    f16: fp16 operands with a per-entry device alpha (BERT's flush: inverse gradient scales)."""
     kk = K()
     torch.manual_seed(0)
     shapes = [(256, 384), (128, 256), (384, 128), (512, 512)]
@@ -1214,8 +1215,10 @@ def test_linear_dw_grouped_mixed_shapes(n_rep, T):
     off, items, ref = 0, [], []
     for r in range(n_rep):
         for j, (O, I) in enumerate(shapes):
-            dy = torch.randn(T, O, device="cuda").to(torch.bfloat16)
-            x = torch.randn(T, I, device="cuda").to(torch.bfloat16)
+            dt = torch.float16 if f16 else torch.bfloat16
+            dy = torch.randn(T, O, device="cuda").to(dt)
+            x = torch.randn(T, I, device="cuda").to(dt)
+            al = torch.tensor([2.0 ** -(r + j)], device="cuda") if f16 and (r + j) % 3 != 2 else None
             if (r + j) % 5 == 4:
                 dw, db = torch.randn(O, I, device="cuda"), torch.randn(O, device="cuda")
             else:
@@ -1223,8 +1226,8 @@ def test_linear_dw_grouped_mixed_shapes(n_rep, T):
                 db = flat[off:off + O]; off += O
             store, bias = (r + j) % 3 == 0, (r + 2 * j) % 4 != 1
             rw, rb = (torch.zeros_like(dw) if store else dw.clone()), db.clone()
-            kk.linear_dw(dy, x, rw, bias_grad=rb if bias else None)
-            items.append((dy, x, dw, db if bias else None, store))
+            kk.linear_dw(dy, x, rw, bias_grad=rb if bias else None, alpha_dev=al)
+            items.append((dy, x, dw, db if bias else None, store, al))
             ref.append((rw, rb))
     kk.linear_dw_grouped(items)
     torch.cuda.synchronize()

@@ -80,9 +80,11 @@ struct GemmPT : GemmP {
   int meta[GPT];          // shape index | epilogue flags << 8
   int coff[GPT];          // C offset from p.c (f32 elements)
   int boff[GPT];          // bias-gradient offset from p.bias (f32 elements), -1: none
+  int aoff[GPT];          // device alpha offset from p.alpha_dev (floats), -1: the launch's alpha
   const void* ta[GPT];
   const bf16* tb[GPT];
 };
+static_assert(sizeof(GemmPT) <= 3840, "grouped GEMM tables must fit the kernel-argument block");
 template <bool PT>
 using GemmArg = typename std::conditional<PT, GemmPT, GemmP>::type;
 
@@ -642,6 +644,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(const GemmArg<PT> pa) 
     p.tiles_m = sh.tiles_m; p.tiles_n = sh.tiles_n;
     p.flags = meta >> 8;
     p.bias = pa.boff[lo] >= 0 ? p.bias + pa.boff[lo] : nullptr;
+    p.alpha_dev = pa.aoff[lo] >= 0 ? p.alpha_dev + pa.aoff[lo] : nullptr;
     p.c = static_cast<float*>(p.c) + pa.coff[lo];
     abase = static_cast<const bf16*>(pa.ta[lo]);
     bbase = pa.tb[lo];
@@ -1378,8 +1381,9 @@ extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alp
       return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d m=%d n=%d lda=%d ldb=%d ldc=%d", i, e.m, e.n, e.lda, e.ldb, e.ldc);
     if (((long long)k * e.lda + e.m) * 2 >= (1LL << 31) || ((long long)k * e.ldb + e.n) * 2 >= (1LL << 31))
       return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d operand extent over 2 GB", i);
-    if (!e.a || !e.b || !e.c || !al16(e.a) || !al16(e.b) || !al16(e.c) || (bg && !al16(e.bias)))
-      return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d null or not 16-B aligned", i);
+    if (!e.a || !e.b || !e.c || !al16(e.a) || !al16(e.b) || !al16(e.c) || (bg && !al16(e.bias)) ||
+        (reinterpret_cast<uintptr_t>(e.alpha_dev) & 3) || (e.f16 != 0 && e.f16 != 1))
+      return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d null, misaligned or f16=%d", i, e.f16);
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   constexpr long long SPAN = (1LL << 31) - 1;   // f32 elements an offset from the chunk's base may reach
@@ -1393,10 +1397,12 @@ extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alp
     p.group_m = 4;
     p.vec = 1;
     p.trace = g_gemm_trace;
-    uintptr_t clo = ~(uintptr_t)0, chi = 0, blo = ~(uintptr_t)0, bhi = 0;
+    uintptr_t clo = ~(uintptr_t)0, chi = 0, blo = ~(uintptr_t)0, bhi = 0, alo = ~(uintptr_t)0, ahi = 0;
     int nsh = 0, j = i, tiles = 0;
+    const int f16 = it[i].f16;
     for (; j < n && j - i < GPT; ++j) {
       const LrceGemmItem& e = it[j];
+      if (e.f16 != f16) break;   // one operand format per launch
       int si = 0;
       while (si < nsh && !(p.sh[si].m == e.m && p.sh[si].n == e.n && p.sh[si].lda == e.lda && p.sh[si].ldb == e.ldb &&
                            p.sh[si].ldc == e.ldc))
@@ -1412,10 +1418,16 @@ extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alp
         nblo = b0 < blo ? b0 : blo; nbhi = b1 > bhi ? b1 : bhi;
         if ((long long)((nbhi - nblo) / 4) > SPAN) break;
       }
+      uintptr_t nalo = alo, nahi = ahi;
+      if (e.alpha_dev) {
+        const uintptr_t a0 = reinterpret_cast<uintptr_t>(e.alpha_dev), a1 = a0 + 4;
+        nalo = a0 < alo ? a0 : alo; nahi = a1 > ahi ? a1 : ahi;
+        if ((long long)((nahi - nalo) / 4) > SPAN) break;
+      }
       const int tm = (e.m + BM - 1) / BM, tn = (e.n + BN - 1) / BN;
       if ((long long)tiles + (long long)tm * tn >= (1LL << 31)) break;
       if (si == nsh) p.sh[nsh++] = GemmShape{e.m, e.n, e.lda, e.ldb, e.ldc, tm, tn};
-      clo = nclo; chi = nchi; blo = nblo; bhi = nbhi;
+      clo = nclo; chi = nchi; blo = nblo; bhi = nbhi; alo = nalo; ahi = nahi;
       p.start[j - i] = tiles;
       tiles += tm * tn;
       p.meta[j - i] = si | (e.flags << 8);
@@ -1426,14 +1438,18 @@ extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alp
     p.start[p.ng] = tiles;
     p.c = reinterpret_cast<void*>(clo);
     p.bias = bhi ? reinterpret_cast<const float*>(blo) : nullptr;
+    p.alpha_dev = ahi ? reinterpret_cast<const float*>(alo) : nullptr;
+    p.f16 = f16;
     for (int q = 0; q < p.ng; ++q) {
       const LrceGemmItem& e = it[i + q];
       p.coff[q] = (int)((reinterpret_cast<uintptr_t>(e.c) - clo) / 4);
       p.boff[q] = (e.flags & LRCE_EPI_BIAS_GRAD) ? (int)((reinterpret_cast<uintptr_t>(e.bias) - blo) / 4) : -1;
+      p.aoff[q] = e.alpha_dev ? (int)((reinterpret_cast<uintptr_t>(e.alpha_dev) - alo) / 4) : -1;
     }
     p.a = p.ta[0]; p.b = p.tb[0];
     p.m = p.sh[0].m; p.n = p.sh[0].n; p.tiles_m = p.sh[0].tiles_m; p.tiles_n = p.sh[0].tiles_n;
-    gemm_glds_kernel<128, 128, false, false, false, 2, false, true><<<dim3(tiles, 1), NT, 0, s>>>(p);
+    if (f16) gemm_glds_kernel<128, 128, false, false, true, 2, false, true><<<dim3(tiles, 1), NT, 0, s>>>(p);
+    else gemm_glds_kernel<128, 128, false, false, false, 2, false, true><<<dim3(tiles, 1), NT, 0, s>>>(p);
     i = j;
   }
   return lrce_check_launch("gemm_grouped");
@@ -1453,7 +1469,7 @@ extern "C" int lrce_gemm_ptr_batched(const LrceGemmDesc* d, const void* const* a
   std::vector<LrceGemmItem> items(n);
   for (int i = 0; i < n; ++i)
     items[i] = LrceGemmItem{a[i], b[i], static_cast<float*>(c[i]), bg ? const_cast<float*>(bias[i]) : nullptr,
-                            d->m, d->n, (int32_t)d->lda, (int32_t)d->ldb, (int32_t)d->ldc, d->flags};
+                            nullptr, d->m, d->n, (int32_t)d->lda, (int32_t)d->ldb, (int32_t)d->ldc, d->flags, 0};
   return lrce_gemm_grouped(items.data(), n, d->k, d->alpha, stream);
 }
 

@@ -139,8 +139,9 @@ class DecSaBwd(ctypes.Structure):
 class GemmItem(ctypes.Structure):
     _fields_ = [
         ("a", ctypes.c_void_p), ("b", ctypes.c_void_p), ("c", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("alpha_dev", ctypes.c_void_p),
         ("m", ctypes.c_int32), ("n", ctypes.c_int32), ("lda", ctypes.c_int32), ("ldb", ctypes.c_int32),
-        ("ldc", ctypes.c_int32), ("flags", ctypes.c_int32),
+        ("ldc", ctypes.c_int32), ("flags", ctypes.c_int32), ("f16", ctypes.c_int32),
     ]
 
 

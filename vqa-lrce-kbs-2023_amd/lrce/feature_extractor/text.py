@@ -417,6 +417,20 @@ def _flush_wgrads(st):
     flat = st.flat
     layers = sorted(st.done)
     items = {i: _wgrad_items(st, i) for i in layers}
+    if _WGRAD_GROUPED:
+        # every layer's six products as ONE grouped launch (per-entry shape, scale slot and freshness)
+        todo = []
+        for i in layers:
+            for lin, dy, x, slot in items[i]:
+                gw, gb = _g(flat, lin.weight), _g(flat, lin.bias)
+                if gw is None or gb is None:
+                    _wgrad(flat, lin, dy, x, st.scales[i, slot, 1:2])
+                    continue
+                fresh = flat.claim_fresh([lin.weight, lin.bias]) and _STORE_FRESH
+                todo.append((dy, x, gw, gb, fresh, st.scales[i, slot, 1:2]))
+        if todo:
+            K.linear_dw_grouped(todo)
+        return
     for j in range(6):
         per = [(i,) + items[i][j] for i in layers]          # (layer, lin, dy, x, slot)
         gws = [_g(flat, lin.weight) for _, lin, _, _, _ in per]
@@ -446,6 +460,7 @@ def _flush_wgrads(st):
 
 
 _WGRAD_BATCHED = os.environ.get("LRCE_BERT_WGRAD_BATCHED", "1") != "0"   # A/B knob
+_WGRAD_GROUPED = os.environ.get("LRCE_BERT_WGRAD_GROUPED", "1") != "0"   # A/B knob (one grouped launch)
 _LN_DEFER = os.environ.get("LRCE_BERT_LN_DEFER", "1") != "0"             # A/B knob
 _REDUCE_LN = os.environ.get("LRCE_BERT_REDUCE_LN", "1") != "0"           # A/B knob (linear_resid_ln)
 _STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"      # A/B knob (see FlatParams.claim_fresh)

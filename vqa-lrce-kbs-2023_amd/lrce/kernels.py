@@ -338,21 +338,26 @@ def linear_dw_batched(items, store=False):
 
 def linear_dw_grouped(items):
     """Weight gradients of linears of any shapes over the same tokens, items [(dy16, x16, dw, db|None,
-    store)] (bf16 [T, out] / [T, in], f32 [out, in]): dW = (store) or += (not store) dY^T X, db +=
-    colsum(dY), as grouped launches (lrce_gemm_grouped: every entry's tiles in one grid, one K slice
-    per tile)."""
+    store[, alpha_dev])] (bf16 or fp16 [T, out] / [T, in], f32 [out, in]): dW = (store) or += (not
+    store) a dY^T X, db += a colsum(dY), a = alpha_dev[0] (a device f32, e.g. an inverse gradient scale)
+    or 1, as grouped launches (lrce_gemm_grouped: every entry's tiles in one grid, one K slice per tile;
+    fp16 and bf16 entries in separate launches)."""
     T = items[0][1].shape[0]
     arr = (N.GemmItem * len(items))()
     flops = 0.0
-    for e, (dy, x, dw, db, store) in zip(arr, items):
+    for e, item in zip(arr, items):
+        dy, x, dw, db, store = item[:5]
+        al = item[5] if len(item) > 5 else None
         O, I = dw.shape
-        if (dy.dtype != BF16 or x.dtype != BF16 or dw.dtype != F32 or dy.shape != (T, O) or x.shape != (T, I)
-                or not dw.is_contiguous() or dy.stride(1) != 1 or x.stride(1) != 1
-                or (db is not None and (db.dtype != F32 or db.shape != (O,)))):
+        if (dy.dtype not in (BF16, F16) or x.dtype != dy.dtype or dw.dtype != F32 or dy.shape != (T, O)
+                or x.shape != (T, I) or not dw.is_contiguous() or dy.stride(1) != 1 or x.stride(1) != 1
+                or (db is not None and (db.dtype != F32 or db.shape != (O,)))
+                or (al is not None and (al.dtype != F32 or al.device != dw.device))):
             raise N.NativeError("linear_dw_grouped: an item's dtype / shape / layout")
-        e.a, e.b, e.c, e.bias = ptr(dy), ptr(x), ptr(dw), ptr(db)
+        e.a, e.b, e.c, e.bias, e.alpha_dev = ptr(dy), ptr(x), ptr(dw), ptr(db), ptr(al)
         e.m, e.n, e.lda, e.ldb, e.ldc = O, I, _ld(dy), _ld(x), I
         e.flags = (N.EPI_OUT_F32 if store else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if db is not None else 0)
+        e.f16 = int(dy.dtype == F16)
         flops += 2.0 * O * I * T
     dw0 = items[0][2]
     _timed("gemm", dw0, lambda: call("lrce_gemm_grouped", arr, len(items), T, 1.0, stream_of(dw0)),
