@@ -1231,7 +1231,7 @@ def test_linear_dw_grouped_mixed_shapes(n_rep, T, f16):
             ref.append((rw, rb))
     kk.linear_dw_grouped(items)
     torch.cuda.synchronize()
-    for (dy, x, dw, db, store), (rw, rb) in zip(items, ref):
+    for (dy, x, dw, db, store, _al), (rw, rb) in zip(items, ref):
         assert rel(dw, rw) < 1e-5
         if db is not None:
             assert rel(db, rb) < 1e-5
