@@ -460,7 +460,7 @@ def _flush_wgrads(st):
 
 
 _WGRAD_BATCHED = os.environ.get("LRCE_BERT_WGRAD_BATCHED", "1") != "0"   # A/B knob
-_WGRAD_GROUPED = os.environ.get("LRCE_BERT_WGRAD_GROUPED", "1") != "0"   # A/B knob (one grouped launch)
+_WGRAD_GROUPED = os.environ.get("LRCE_BERT_WGRAD_GROUPED", "0") == "1"   # A/B knob (one grouped launch): within noise, off
 _LN_DEFER = os.environ.get("LRCE_BERT_LN_DEFER", "1") != "0"             # A/B knob
 _REDUCE_LN = os.environ.get("LRCE_BERT_REDUCE_LN", "1") != "0"           # A/B knob (linear_resid_ln)
 _STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"      # A/B knob (see FlatParams.claim_fresh)
