@@ -134,6 +134,10 @@ typedef struct LrceGemmItem {
   float* bias;
   const float* alpha_dev;
   int32_t m, n, lda, ldb, ldc, flags, f16;
+  /* split > 1: K in `split` slices of k_chunk (a multiple of 64) tokens; slice s stores its partial
+   * into c + s * m * ldc and adds its bias partial into bias + s * m (zeroed by the caller): flags
+   * must be OUT_F32 [| BIAS_GRAD]; lrce_slab_sum_grouped then sums the slabs in slice order. */
+  int32_t split, k_chunk;
 } LrceGemmItem;
 /* Weight gradients of n linears of any shapes sharing K (the token count) and alpha, as grouped
  * launches (the four linears x blocks of a Swin stage at once, Swin backward, video_swin_ori.py:46-57,
@@ -142,6 +146,15 @@ typedef struct LrceGemmItem {
  * format (f16) per launch, and the C / bias / alpha pointers of one launch within 8 GB of each other
  * (more: several launches).  Pointers 16-B aligned (alpha_dev 4-B). */
 int lrce_gemm_grouped(const LrceGemmItem* items, int n, int k, float alpha, void* stream);
+/* dst (=|+=) sum_s slabs[s * n + i] over s = 0 .. split-1 in that order (deterministic), for a batch of
+ * items (a grouped split-K launch's weight / bias slabs).  n % 4 == 0, pointers 16-B aligned. */
+typedef struct LrceSlabSum {
+  const float* slabs;
+  float* dst;
+  int64_t n;
+  int32_t split, accumulate;
+} LrceSlabSum;
+int lrce_slab_sum_grouped(const LrceSlabSum* items, int n, void* stream);
 /* n same-shape weight gradients (the blocks of a Swin stage): lrce_gemm_grouped with items
  * {a[i], b[i], c[i], bias[i], desc->m, desc->n, desc->lda, desc->ldb, desc->ldc, desc->flags}; desc
  * supplies the shape / leading dims / alpha / flags (ACCUM or OUT_F32 [| BIAS_GRAD]); its pointers,

@@ -1201,13 +1201,15 @@ def test_linear_dw_batched_matches_per_item():
         assert rel(dw, rw) < 1e-5 and rel(db, rb) < 1e-5
 
 
-@pytest.mark.parametrize("n_rep,T,f16", [(3, 1000, False), (23, 200, False), (4, 320, True)])
-def test_linear_dw_grouped_mixed_shapes(n_rep, T, f16):
+@pytest.mark.parametrize("n_rep,T,f16,split", [(3, 1000, False, 1), (23, 200, False, 1), (4, 320, True, 1),
+                                               (3, 5000, False, 4), (2, 4000, True, 3)])
+def test_linear_dw_grouped_mixed_shapes(n_rep, T, f16, split):
     """lrce_gemm_grouped (a Swin stage's linears x blocks as one grid: entries of different shapes, some
     stored (fresh gradients), some accumulated, with and without a bias gradient, C carved from one flat
     buffer like the training layout plus a few separate tensors) against linear_dw per item: dW and db
     to f32 rounding, a K tail (T % 64 != 0), and 92 entries (more than one launch's table) at n_rep 23;
-    f16: fp16 operands with a per-entry device alpha (BERT's flush: inverse gradient scales)."""
+    f16: fp16 operands with a per-entry device alpha (BERT's flush: inverse gradient scales); split: K in
+    slices with f32 slabs summed by lrce_slab_sum_grouped (Swin stages 1-2, a K tail in the last slice)."""
     kk = K()
     torch.manual_seed(0)
     shapes = [(256, 384), (128, 256), (384, 128), (512, 512)]
@@ -1229,7 +1231,7 @@ def test_linear_dw_grouped_mixed_shapes(n_rep, T, f16):
             kk.linear_dw(dy, x, rw, bias_grad=rb if bias else None, alpha_dev=al)
             items.append((dy, x, dw, db if bias else None, store, al))
             ref.append((rw, rb))
-    kk.linear_dw_grouped(items)
+    kk.linear_dw_grouped(items, split=split)
     torch.cuda.synchronize()
     for (dy, x, dw, db, store, _al), (rw, rb) in zip(items, ref):
         assert rel(dw, rw) < 1e-5

@@ -74,6 +74,41 @@ def main():
     grouped_vs_per_shape(nb, T, SHAPES, a.iters)
     C4 = [("qkv", 3072, 1024), ("proj", 1024, 1024), ("fc1", 4096, 1024), ("fc2", 1024, 4096)]
     grouped_vs_per_shape(2, T // 4, C4, a.iters)
+    for C, TT in ((256, T * 4), (128, T * 16)):   # stages 2 and 1: few tiles over a long K
+        split_vs_per_item(2, TT, [("qkv", 3 * C, C), ("proj", C, C), ("fc1", 4 * C, C), ("fc2", C, 4 * C)], a.iters)
+
+
+def split_vs_per_item(nb, T, shapes, iters):
+    """A long-K stage's weight gradients: one split-K launch + reduce per linear (linear_dw, the
+    immediate path) against ONE grouped launch with per-entry K slices + one slab-sum launch."""
+    bf = torch.bfloat16
+    items = []
+    for j in range(nb):
+        for name, O, I in shapes:
+            items.append((torch.rand(T, O, device="cuda").sub_(0.5).to(bf), torch.rand(T, I, device="cuda").sub_(0.5).to(bf),
+                          torch.zeros(O, I, device="cuda"), torch.zeros(O, device="cuda"), False))
+    tiles = sum(-(-O // 128) * -(-I // 128) for _, O, I in shapes) * nb
+    split = max(2, min(64, round(512 / tiles)))
+
+    def per_item():
+        for dy, x, dw, db, _ in items:
+            K.linear_dw(dy, x, dw, bias_grad=db)
+
+    def grouped():
+        K.linear_dw_grouped(items, split=split)
+
+    per_item(); torch.cuda.synchronize()
+    ref = [(it[2].clone(), it[3].clone()) for it in items]
+    for it in items:
+        it[2].zero_(); it[3].zero_()
+    grouped(); torch.cuda.synchronize()
+    err = max(((it[2] - r[0]).abs().max() / r[0].abs().max()).item() for it, r in zip(items, ref))
+    errb = max(((it[3] - r[1]).abs().max() / r[1].abs().max()).item() for it, r in zip(items, ref))
+    tp, tg = timed(per_item, iters), timed(grouped, iters)
+    fl = sum(2.0 * T * O * I for _, O, I in shapes) * nb
+    print(f"{nb} blocks x C={shapes[1][1]} T={T} ({tiles} tiles, split {split}): per-item split-K {tp:8.1f} us "
+          f"({fl / tp / 1e6:6.1f} TF/s)   grouped split {tg:8.1f} us ({fl / tg / 1e6:6.1f} TF/s)   "
+          f"rel diff w {err:.1e} b {errb:.1e}", flush=True)
 
 
 def grouped_vs_per_shape(nb, T, shapes, iters):

@@ -72,6 +72,7 @@ struct GemmP {
 constexpr int GPT = 80, GSH = 8;
 struct GemmShape {
   int m, n, lda, ldb, ldc, tiles_m, tiles_n;
+  int split, k_chunk;   // K slices of each entry of this shape (slice s: its own C / bias slab)
 };
 struct GemmPT : GemmP {
   int ng;                 // entries
@@ -627,6 +628,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(const GemmArg<PT> pa) 
   const int z = blockIdx.y;
   const int bz = z / p.split_k, sk = z % p.split_k;
   int lin;
+  int kslice = sk;   // this workgroup's K slice
   const bf16* abase;
   const bf16* bbase;
   if constexpr (PT) {
@@ -649,6 +651,14 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(const GemmArg<PT> pa) 
     abase = static_cast<const bf16*>(pa.ta[lo]);
     bbase = pa.tb[lo];
     lin = g - pa.start[lo];
+    if (sh.split > 1) {   // slice-major: slice s stores its partial into slab s of C and of the bias
+      const int tiles = sh.tiles_m * sh.tiles_n;
+      kslice = lin / tiles;
+      lin -= kslice * tiles;
+      p.k_chunk = sh.k_chunk;
+      p.c = static_cast<float*>(p.c) + (long long)kslice * sh.m * sh.ldc;
+      if (p.bias) p.bias += (long long)kslice * sh.m;
+    }
   } else {
     p.bias += (long long)bz * p.sbias;
     if (p.alpha_dev) p.alpha_dev += (long long)bz * p.salpha;
@@ -666,7 +676,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(const GemmArg<PT> pa) 
     p.trace[(long long)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
   }
 #endif
-  const int kb = sk * p.k_chunk;
+  const int kb = kslice * p.k_chunk;
   const int ke = min(p.k, kb + p.k_chunk);
   const int nfull = ke > kb ? (ke - kb) / BK : 0;
   const bool tail = ke > kb + nfull * BK;
@@ -1379,6 +1389,11 @@ extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alp
     if (e.m <= 0 || e.n <= 0 || e.m % 8 || e.n % 8 || e.lda < e.m || e.ldb < e.n || e.ldc < e.n || e.lda % 8 ||
         e.ldb % 8 || e.ldc % 8)
       return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d m=%d n=%d lda=%d ldb=%d ldc=%d", i, e.m, e.n, e.lda, e.ldb, e.ldc);
+    if (e.split > 1 && (cf != LRCE_EPI_OUT_F32 || e.k_chunk <= 0 || e.k_chunk % BK || (long long)(e.split - 1) * e.k_chunk >= k ||
+                        (long long)e.split * e.k_chunk < k))
+      return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d split %d x k_chunk %d over k=%d (slabs are stored: OUT_F32)", i,
+                       e.split, e.k_chunk, k);
+    if (e.split < 0 || e.split > 4096) return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d split %d", i, e.split);
     if (((long long)k * e.lda + e.m) * 2 >= (1LL << 31) || ((long long)k * e.ldb + e.n) * 2 >= (1LL << 31))
       return lrce_fail(LRCE_E_ARG, "gemm_grouped: entry %d operand extent over 2 GB", i);
     if (!e.a || !e.b || !e.c || !al16(e.a) || !al16(e.b) || !al16(e.c) || (bg && !al16(e.bias)) ||
@@ -1404,17 +1419,18 @@ extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alp
       const LrceGemmItem& e = it[j];
       if (e.f16 != f16) break;   // one operand format per launch
       int si = 0;
+      const int sp = e.split > 1 ? e.split : 1, kc = e.split > 1 ? e.k_chunk : 0;
       while (si < nsh && !(p.sh[si].m == e.m && p.sh[si].n == e.n && p.sh[si].lda == e.lda && p.sh[si].ldb == e.ldb &&
-                           p.sh[si].ldc == e.ldc))
+                           p.sh[si].ldc == e.ldc && p.sh[si].split == sp && p.sh[si].k_chunk == kc))
         ++si;
       if (si == nsh && nsh == GSH) break;
       const uintptr_t c0 = reinterpret_cast<uintptr_t>(e.c);
-      const uintptr_t c1 = c0 + ((uintptr_t)(e.m - 1) * e.ldc + e.n) * 4;
+      const uintptr_t c1 = c0 + ((uintptr_t)(sp - 1) * e.m * e.ldc + (uintptr_t)(e.m - 1) * e.ldc + e.n) * 4;
       const uintptr_t nclo = c0 < clo ? c0 : clo, nchi = c1 > chi ? c1 : chi;
       if ((long long)((nchi - nclo) / 4) > SPAN) break;
       uintptr_t nblo = blo, nbhi = bhi;
       if (e.flags & LRCE_EPI_BIAS_GRAD) {
-        const uintptr_t b0 = reinterpret_cast<uintptr_t>(e.bias), b1 = b0 + (uintptr_t)e.m * 4;
+        const uintptr_t b0 = reinterpret_cast<uintptr_t>(e.bias), b1 = b0 + (uintptr_t)sp * e.m * 4;
         nblo = b0 < blo ? b0 : blo; nbhi = b1 > bhi ? b1 : bhi;
         if ((long long)((nbhi - nblo) / 4) > SPAN) break;
       }
@@ -1425,11 +1441,11 @@ extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alp
         if ((long long)((nahi - nalo) / 4) > SPAN) break;
       }
       const int tm = (e.m + BM - 1) / BM, tn = (e.n + BN - 1) / BN;
-      if ((long long)tiles + (long long)tm * tn >= (1LL << 31)) break;
-      if (si == nsh) p.sh[nsh++] = GemmShape{e.m, e.n, e.lda, e.ldb, e.ldc, tm, tn};
+      if ((long long)tiles + (long long)tm * tn * sp >= (1LL << 31)) break;
+      if (si == nsh) p.sh[nsh++] = GemmShape{e.m, e.n, e.lda, e.ldb, e.ldc, tm, tn, sp, kc};
       clo = nclo; chi = nchi; blo = nblo; bhi = nbhi; alo = nalo; ahi = nahi;
       p.start[j - i] = tiles;
-      tiles += tm * tn;
+      tiles += tm * tn * sp;
       p.meta[j - i] = si | (e.flags << 8);
       p.ta[j - i] = e.a;
       p.tb[j - i] = static_cast<const bf16*>(e.b);
@@ -1469,8 +1485,68 @@ extern "C" int lrce_gemm_ptr_batched(const LrceGemmDesc* d, const void* const* a
   std::vector<LrceGemmItem> items(n);
   for (int i = 0; i < n; ++i)
     items[i] = LrceGemmItem{a[i], b[i], static_cast<float*>(c[i]), bg ? const_cast<float*>(bias[i]) : nullptr,
-                            nullptr, d->m, d->n, (int32_t)d->lda, (int32_t)d->ldb, (int32_t)d->ldc, d->flags, 0};
+                            nullptr, d->m, d->n, (int32_t)d->lda, (int32_t)d->ldb, (int32_t)d->ldc, d->flags, 0, 1, 0};
   return lrce_gemm_grouped(items.data(), n, d->k, d->alpha, stream);
+}
+
+// dst_i (=|+=) sum_s slabs_i[s][0..n_i) in slice order (the grouped launch's split-K weight gradients):
+// one grid over every item's float4s, the item found by a scan of the start table.
+constexpr int SLAB_ITEMS = 32;
+struct SlabSumArgs {
+  int items;
+  long long start[SLAB_ITEMS + 1];   // first float4 of each item
+  const float* src[SLAB_ITEMS];
+  float* dst[SLAB_ITEMS];
+  long long n[SLAB_ITEMS];
+  int split[SLAB_ITEMS];
+  int accum[SLAB_ITEMS];
+};
+__global__ void __launch_bounds__(256) slab_sum_kernel(const SlabSumArgs a) {
+  const long long total = a.start[a.items];
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < total; q += (long long)gridDim.x * 256) {
+    int it = 0;
+    while (it + 1 < a.items && a.start[it + 1] <= q) ++it;
+    const long long i = (q - a.start[it]) * 4;
+    const float* src = a.src[it] + i;
+    const long long n = a.n[it];
+    float4 acc = *reinterpret_cast<const float4*>(src);
+    for (int sl = 1; sl < a.split[it]; ++sl) {
+      const float4 v = *reinterpret_cast<const float4*>(src + sl * n);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    float4* d = reinterpret_cast<float4*>(a.dst[it] + i);
+    if (a.accum[it]) {
+      const float4 o = *d;
+      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+    }
+    *d = acc;
+  }
+}
+
+extern "C" int lrce_slab_sum_grouped(const LrceSlabSum* items, int n, void* stream) {
+  if (n < 0 || (n > 0 && !items)) return lrce_fail(LRCE_E_ARG, "slab_sum_grouped: n=%d", n);
+  for (int i = 0; i < n; ++i) {
+    const LrceSlabSum& e = items[i];
+    if (!e.slabs || !e.dst || e.n <= 0 || e.n % 4 || e.split < 1 || (reinterpret_cast<uintptr_t>(e.slabs) & 15) ||
+        (reinterpret_cast<uintptr_t>(e.dst) & 15))
+      return lrce_fail(LRCE_E_ARG, "slab_sum_grouped: item %d (n %% 4 == 0, 16-B aligned, split >= 1)", i);
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += SLAB_ITEMS) {
+    SlabSumArgs a{};
+    a.items = n - i0 < SLAB_ITEMS ? n - i0 : SLAB_ITEMS;
+    long long tot = 0;
+    for (int j = 0; j < a.items; ++j) {
+      const LrceSlabSum& e = items[i0 + j];
+      a.start[j] = tot;
+      tot += e.n / 4;
+      a.src[j] = e.slabs; a.dst[j] = e.dst; a.n[j] = e.n; a.split[j] = e.split; a.accum[j] = e.accumulate != 0;
+    }
+    a.start[a.items] = tot;
+    const long long blocks = (tot + 255) / 256;
+    slab_sum_kernel<<<(int)(blocks < 2048 ? blocks : 2048), 256, 0, s>>>(a);
+  }
+  return lrce_check_launch("slab_sum_grouped");
 }
 
 // debug: phase timestamps of gemm_glds_kernel into buf (device, >= 8 per workgroup), NULL = off; the

@@ -142,7 +142,13 @@ class GemmItem(ctypes.Structure):
         ("alpha_dev", ctypes.c_void_p),
         ("m", ctypes.c_int32), ("n", ctypes.c_int32), ("lda", ctypes.c_int32), ("ldb", ctypes.c_int32),
         ("ldc", ctypes.c_int32), ("flags", ctypes.c_int32), ("f16", ctypes.c_int32),
+        ("split", ctypes.c_int32), ("k_chunk", ctypes.c_int32),
     ]
+
+
+class SlabSum(ctypes.Structure):
+    _fields_ = [("slabs", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("n", ctypes.c_int64),
+                ("split", ctypes.c_int32), ("accumulate", ctypes.c_int32)]
 
 
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = 1, 2, 4, 8
@@ -161,6 +167,7 @@ _SIGS = {
     "lrce_gemm_ln": [ctypes.POINTER(GemmDesc), ctypes.POINTER(LnPrologue), _P],
     "lrce_gemm_ptr_batched": [ctypes.POINTER(GemmDesc), _P, _P, _P, _P, _I, _P],
     "lrce_gemm_grouped": [ctypes.POINTER(GemmItem), _I, _I, _F, _P],
+    "lrce_slab_sum_grouped": [ctypes.POINTER(SlabSum), _I, _P],
     "lrce_splitk_reduce_ln": [_P, _I, _I, _I, _P, _P, _I64, _F, _U64, _P, _P, _P, _F, _P, _P, _I, _P, _P, _P],
     "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_layernorm_bwd": [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _I64,

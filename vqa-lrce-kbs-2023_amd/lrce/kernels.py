@@ -336,13 +336,28 @@ def linear_dw_batched(items, store=False):
     linear_dw_grouped([(dy, x, dw, db, store) for dy, x, dw, db in items])
 
 
-def linear_dw_grouped(items):
+def linear_dw_grouped(items, split=1):
     """Weight gradients of linears of any shapes over the same tokens, items [(dy16, x16, dw, db|None,
     store[, alpha_dev])] (bf16 or fp16 [T, out] / [T, in], f32 [out, in]): dW = (store) or += (not
     store) a dY^T X, db += a colsum(dY), a = alpha_dev[0] (a device f32, e.g. an inverse gradient scale)
-    or 1, as grouped launches (lrce_gemm_grouped: every entry's tiles in one grid, one K slice per tile;
-    fp16 and bf16 entries in separate launches)."""
+    or 1, as grouped launches (lrce_gemm_grouped: every entry's tiles in one grid; fp16 and bf16
+    entries in separate launches).  split > 1: each entry's K in `split` slices of a multiple of 64
+    tokens, every slice storing f32 slabs (weight and bias), then ONE lrce_slab_sum_grouped launch sums
+    them in slice order into dW / db (deterministic; the long-K stages whose few tiles would otherwise
+    run one K loop each for milliseconds)."""
     T = items[0][1].shape[0]
+    kc = 0
+    if split > 1:
+        kc = -(-(-(-T // split)) // 64) * 64
+        split = -(-T // kc)
+    dev = items[0][2].device
+    if split > 1:
+        wn = sum(it[2].numel() for it in items) * split
+        bn = sum(it[2].shape[0] for it in items if it[3] is not None) * split
+        wslab = torch.empty(wn, dtype=F32, device=dev)
+        bslab = torch.zeros(max(bn, 4), dtype=F32, device=dev)
+        sums = (N.SlabSum * (2 * len(items)))()
+        nsum = wo = bo = 0
     arr = (N.GemmItem * len(items))()
     flops = 0.0
     for e, item in zip(arr, items):
@@ -351,17 +366,38 @@ def linear_dw_grouped(items):
         O, I = dw.shape
         if (dy.dtype not in (BF16, F16) or x.dtype != dy.dtype or dw.dtype != F32 or dy.shape != (T, O)
                 or x.shape != (T, I) or not dw.is_contiguous() or dy.stride(1) != 1 or x.stride(1) != 1
-                or (db is not None and (db.dtype != F32 or db.shape != (O,)))
+                or (db is not None and (db.dtype != F32 or db.shape != (O,) or not db.is_contiguous()))
                 or (al is not None and (al.dtype != F32 or al.device != dw.device))):
             raise N.NativeError("linear_dw_grouped: an item's dtype / shape / layout")
-        e.a, e.b, e.c, e.bias, e.alpha_dev = ptr(dy), ptr(x), ptr(dw), ptr(db), ptr(al)
+        e.a, e.b, e.alpha_dev = ptr(dy), ptr(x), ptr(al)
         e.m, e.n, e.lda, e.ldb, e.ldc = O, I, _ld(dy), _ld(x), I
-        e.flags = (N.EPI_OUT_F32 if store else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if db is not None else 0)
         e.f16 = int(dy.dtype == F16)
+        e.split, e.k_chunk = max(split, 1), kc
+        if split > 1:
+            e.c = wslab.data_ptr() + 4 * wo
+            sums[nsum].slabs, sums[nsum].dst, sums[nsum].n = e.c, ptr(dw), O * I
+            sums[nsum].split, sums[nsum].accumulate = split, int(not store)
+            nsum += 1
+            wo += O * I * split
+            e.bias = None
+            if db is not None:
+                e.bias = bslab.data_ptr() + 4 * bo
+                sums[nsum].slabs, sums[nsum].dst, sums[nsum].n = e.bias, ptr(db), O
+                sums[nsum].split, sums[nsum].accumulate = split, 1
+                nsum += 1
+                bo += O * split
+            e.flags = N.EPI_OUT_F32 | (N.EPI_BIAS_GRAD if db is not None else 0)
+        else:
+            e.c, e.bias = ptr(dw), ptr(db)
+            e.flags = (N.EPI_OUT_F32 if store else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if db is not None else 0)
         flops += 2.0 * O * I * T
     dw0 = items[0][2]
-    _timed("gemm", dw0, lambda: call("lrce_gemm_grouped", arr, len(items), T, 1.0, stream_of(dw0)),
-           flops=flops, key=("grouped", T, len(items)))
+
+    def run():
+        call("lrce_gemm_grouped", arr, len(items), T, 1.0, stream_of(dw0))
+        if split > 1:
+            call("lrce_slab_sum_grouped", sums, nsum, stream_of(dw0))
+    _timed("gemm", dw0, run, flops=flops, key=("grouped", T, len(items), split))
 
 
 def colsum(x, out, *, row_map=None, rows=None, row_scale=None, rows_per_scale=1):
@@ -413,6 +449,7 @@ def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1,
 
 
 _GROUPED_DW = os.environ.get("LRCE_GROUPED_DW", "1") != "0"   # A/B knob: one grouped launch vs one per shape
+_SPLIT_DW = os.environ.get("LRCE_SPLIT_DW", "1") != "0"       # A/B knob: long-K stages deferred as split slabs
 
 
 class DeferredGrads:
@@ -431,13 +468,20 @@ class DeferredGrads:
         milliseconds) and the blocks' 128 x 128 tiles of this linear are a fair share of a chip-filling
         grouped launch (stage 4's 1024 x 1024 projection: 2 x 64)."""
         tiles = -(-out_f // 128) * -(-in_f // 128)
-        return tiles * self.n_items >= (64 if _GROUPED_DW else 256) and tokens <= 32768
+        if tokens > 32768:
+            return _GROUPED_DW and _SPLIT_DW   # split-K slabs in the grouped launch (stages 1 and 2)
+        return tiles * self.n_items >= (64 if _GROUPED_DW else 256)
 
     def flush(self, stream_tensor):
         if self.dw:
             # every deferred weight gradient (the stage's linears x blocks, same tokens) in one grouped grid
             if _GROUPED_DW:
-                linear_dw_grouped(self.dw)
+                T = self.dw[0][1].shape[0]
+                split = 1
+                if T > 32768:   # a few tiles over a long K: slices so the grid fills ~one round of the chip
+                    tiles = sum(-(-it[2].shape[0] // 128) * -(-it[2].shape[1] // 128) for it in self.dw)
+                    split = max(2, min(64, round(512 / tiles)))
+                linear_dw_grouped(self.dw, split=split)
             else:
                 groups = {}
                 for it in self.dw:
