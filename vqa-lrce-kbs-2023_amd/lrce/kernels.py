@@ -476,12 +476,15 @@ class DeferredGrads:
         if self.dw:
             # every deferred weight gradient (the stage's linears x blocks, same tokens) in one grouped grid
             if _GROUPED_DW:
-                T = self.dw[0][1].shape[0]
-                split = 1
-                if T > 32768:   # a few tiles over a long K: slices so the grid fills ~one round of the chip
-                    tiles = sum(-(-it[2].shape[0] // 128) * -(-it[2].shape[1] // 128) for it in self.dw)
-                    split = max(2, min(64, round(512 / tiles)))
-                linear_dw_grouped(self.dw, split=split)
+                by_t = {}   # (blocks of a padded stage may differ in token count: one grid per count)
+                for it in self.dw:
+                    by_t.setdefault((it[1].shape[0], it[0].dtype), []).append(it)
+                for (T, _), items in by_t.items():
+                    split = 1
+                    if T > 32768:   # a few tiles over a long K: slices so the grid fills ~one round of the chip
+                        tiles = sum(-(-it[2].shape[0] // 128) * -(-it[2].shape[1] // 128) for it in items)
+                        split = max(2, min(64, round(512 / tiles)))
+                    linear_dw_grouped(items, split=split)
             else:
                 groups = {}
                 for it in self.dw:
