@@ -361,15 +361,19 @@ _STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"     # A/B kn
 
 def _stage_deferral(blocks, flat):
     """A DeferredGrads the stage's blocks share, or None: the LayerNorm gamma / beta and bias-table
-    gradient reductions of every block then run as batched launches when the backward reaches the
-    stage's first block (always the last of them, and present in the graph whenever its parameters
-    train).  Not with a gradient reducer: it launches a bucket's exchange as soon as a block reports its
-    parameters final."""
-    if not _DEFER_REDUCTIONS or getattr(flat, "reducer", None) is not None or not torch.is_grad_enabled():
+    gradient reductions and the weight gradients of every block then run as batched launches when the
+    backward reaches the stage's first block (always the last of them, and present in the graph whenever
+    its parameters train).  With a gradient reducer the stage's blocks report their parameters final
+    together, at that flush (a bucket's exchange starts then, instead of block by block)."""
+    if not _DEFER_REDUCTIONS or not torch.is_grad_enabled():
+        return None
+    if getattr(flat, "reducer", None) is not None and not _DEFER_WITH_REDUCER:
         return None
     if not any(p.requires_grad for p in blocks[0].parameters()):
         return None
-    return K.DeferredGrads(len(blocks))
+    d = K.DeferredGrads(len(blocks))
+    d.blocks = list(blocks)
+    return d
 
 
 def _run_blocks(blocks, x, geo, flat, scales, tiles=None, between=None):
@@ -405,6 +409,7 @@ def _bias_tiles(blk, geo):
 
 
 _PREBUILD_BIAS = os.environ.get("LRCE_SWIN_BIAS_PREBUILD", "1") != "0"   # A/B knob
+_DEFER_WITH_REDUCER = os.environ.get("LRCE_DEFER_WITH_REDUCER", "1") != "0"   # A/B knob (data parallel)
 
 
 def _prebuild_bias_tiles(stages, dev):
@@ -533,7 +538,11 @@ class _SwinBlockFn(torch.autograd.Function):
         if flush:
             red.flush(dx)   # the stage's deferred LayerNorm / bias-table gradient sums
         ctx.save = ctx.up = ctx.down = ctx.red = None
-        flat.notify(blk.parameters())
+        if red is None:
+            flat.notify(blk.parameters())
+        elif flush:   # every block of the stage is final only now (their gradients were deferred)
+            for b in red.blocks:
+                flat.notify(b.parameters())
         group = getattr(blk, "_lrce_group", None)
         if group is not None and flat.early_update is not None:
             # this stage's gradients are final: its optimizer update runs on the decoder's weight-
