@@ -152,8 +152,8 @@ class _Stack:
         self.delayed = _DELAYED_SCALE and getattr(bert, "_lrce_scales_ready", False)
         self.done = []          # layer indices whose backward has run (their dY in dbuf)
         # the layers' LayerNorm gamma / beta reductions, one batched launch at the flush (LRCE_BERT_LN_DEFER=0:
-        # one launch per LayerNorm); not with a gradient reducer (it would see the layers final too early)
-        self.red = K.DeferredGrads() if _LN_DEFER and getattr(flat, "reducer", None) is None else None
+        # one launch per LayerNorm); a gradient reducer hears of the layers only after that flush
+        self.red = K.DeferredGrads() if _LN_DEFER else None
 
     def fviews(self, i):
         return _views(self.fbuf[i], self.rows, (HIDDEN,) * 6 + (INTER,) * 2)
