@@ -387,6 +387,9 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         if not _KV_AHEAD:
             for l in range(1, nL):
                 issue_kv(l)
+        clear = getattr(flat, "pending_clear", None)
+        if clear is not None:
+            clear()   # the step's gradient clear (FusedAdamW.zero_grad) beside the latency-bound recurrence
         acts = [_LayerActs(S, Bq, dev) for _ in layers]
         s = acts[0].x0[0]
         s.copy_(ft.summarization_token.detach().reshape(1, E).expand(Bq, E))

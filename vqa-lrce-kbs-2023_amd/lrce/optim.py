@@ -9,6 +9,7 @@ is two launches for all 312 M parameters, and it also refreshes the bf16 shadow 
 Semantics = torch.optim.AdamW (decoupled weight decay 0.01 default, bias-corrected moments).
 """
 import math
+import os
 
 import torch
 
@@ -172,11 +173,21 @@ class FusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none=False, overlap=False):
         """flat.grad = 0 (the backward kernels accumulate into it).  overlap=True: the 1.25 GB clear runs
         on an aux stream beside the forward (which never touches gradients); grad_ready() must then
-        be called before the backward (it makes the current stream wait for the clear)."""
+        be called before the backward (it makes the current stream wait for the clear).  The clear is
+        issued when the forward reaches the recurrent decoder (flat.pending_clear), whose latency-bound
+        launches leave most CUs idle — issued at the step's start it delayed the BERT forward, the
+        step's first critical-path chain, by ~0.2 ms; grad_ready() issues it if nothing did."""
         self.flat.grads_zeroed()
         if not overlap or not self.flat.grad.is_cuda:
             self.flat.grad.zero_()
             return
+        if _CLEAR_AT_DECODER:
+            self.flat.pending_clear = self._issue_clear
+        else:
+            self._issue_clear()
+
+    def _issue_clear(self):
+        self.flat.pending_clear = None
         dev = self.flat.device
         s = aux_stream(dev, "grad_zero")
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -186,6 +197,8 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def grad_ready(self):
         """Join an overlapped zero_grad (no-op otherwise): call between the forward and the backward."""
+        if getattr(self.flat, "pending_clear", None) is not None:
+            self._issue_clear()
         s = getattr(self, "_zero_stream", None)
         if s is not None:
             torch.cuda.current_stream(self.flat.device).wait_stream(s)
@@ -228,3 +241,6 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def _device_step(self):
         return float(self.step_t.item())
+
+
+_CLEAR_AT_DECODER = os.environ.get("LRCE_CLEAR_AT_DECODER", "1") != "0"   # A/B knob (see zero_grad)
