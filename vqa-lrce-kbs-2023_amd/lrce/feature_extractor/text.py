@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from .. import _native as N
 from .. import kernels as K
-from ..runtime import ensure
+from ..runtime import aux_stream, ensure
 
 HIDDEN, HEADS, INTER, VOCAB, MAXPOS, TYPES, EPS = 768, 12, 3072, 30522, 512, 2, 1e-12
 
@@ -154,6 +154,9 @@ class _Stack:
         # the layers' LayerNorm gamma / beta reductions, one batched launch at the flush (LRCE_BERT_LN_DEFER=0:
         # one launch per LayerNorm); a gradient reducer hears of the layers only after that flush
         self.red = K.DeferredGrads() if _LN_DEFER else None
+        # the upper half of the stack (layers >= mid) is flushed when the backward reaches layer mid, and
+        # its optimizer update ("text_hi", E2EBase.optimizer_groups) runs beside the lower half's backward
+        self.mid = n // 2 if _SPLIT_FLUSH else None
 
     def fviews(self, i):
         return _views(self.fbuf[i], self.rows, (HIDDEN,) * 6 + (INTER,) * 2)
@@ -266,6 +269,22 @@ class _LayerFn(torch.autograd.Function):
         dx = _qkv_dx(dqkv, sa, w, da2, inv_a, rows, (cq, ck, cv))
         ctx.save = ctx.desc = None
         st.done.append(i)
+        if (i == st.mid and st.flush_at is not None and st.flush_at < i and flat.early_update is not None
+                and getattr(flat, "reducer", None) is None):
+            # upper half final: its weight gradients / LayerNorm sums now, and its AdamW on the decoder's
+            # weight-gradient stream (joined at the end of backward) while layers < mid run here
+            _flush_wgrads(st)
+            if st.red is not None:
+                st.red.flush(dx)
+                st.red = K.DeferredGrads()
+            for j in st.done:
+                flat.notify(st.bert.encoder.layer[j].parameters())
+            st.done = []
+            main = torch.cuda.current_stream(dx.device)
+            s = aux_stream(dx.device, "decoder_wgrad")
+            s.wait_stream(main)
+            with torch.cuda.stream(s):
+                flat.group_done("text_hi")
         if i == st.flush_at:
             _flush_wgrads(st)
             if st.red is not None:
@@ -465,6 +484,7 @@ _LN_DEFER = os.environ.get("LRCE_BERT_LN_DEFER", "1") != "0"             # A/B k
 _REDUCE_LN = os.environ.get("LRCE_BERT_REDUCE_LN", "1") != "0"           # A/B knob (linear_resid_ln)
 _STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"      # A/B knob (see FlatParams.claim_fresh)
 _DELAYED_SCALE = os.environ.get("LRCE_BERT_DELAYED_SCALE", "1") != "0"   # A/B knob
+_SPLIT_FLUSH = os.environ.get("LRCE_BERT_SPLIT_FLUSH", "1") != "0"       # A/B knob (upper half updated early)
 
 
 def _uniform_stride(ts, es):

@@ -89,8 +89,15 @@ class E2EBase(nn.Module):
         2 (the backward runs stage 4 -> 1; stage 4's group carries the final LayerNorm)."""
         pool = {id(p) for p in self.text_extractor.bert.pooler.parameters()}
         swin = self.video_extractor.swin
-        groups = {"decoder": list(self.fusion_model.fusion_transformer.parameters()),
-                  "text": [p for p in self.text_extractor.parameters() if id(p) not in pool]}
+        text = [p for p in self.text_extractor.parameters() if id(p) not in pool]
+        groups = {"decoder": list(self.fusion_model.fusion_transformer.parameters()), "text": text}
+        bert = self.text_extractor.bert
+        if _text_split_flush():
+            # BERT's upper half is final when the backward reaches its middle layer (text._SPLIT_FLUSH)
+            mid = len(bert.encoder.layer) // 2
+            hi = {id(p) for layer in bert.encoder.layer[mid:] for p in layer.parameters()}
+            groups["text_hi"] = [p for p in text if id(p) in hi]
+            groups["text"] = [p for p in text if id(p) not in hi]
         for i in range(len(swin.layers) - 1, 0, -1):
             ps = list(swin.layers[i].parameters())
             if i == len(swin.layers) - 1:
@@ -215,3 +222,8 @@ class E2ECount(E2EBase):
                  temporal_scale: List[int] = [1, 2, 3], text_seq_len: int = 30, **pretrained) -> None:
         super().__init__(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim,
                          frame_sample_size, temporal_scale, text_seq_len, **pretrained)
+
+
+def _text_split_flush():
+    from ..feature_extractor import text as T
+    return T._SPLIT_FLUSH
