@@ -173,10 +173,11 @@ class FusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none=False, overlap=False):
         """flat.grad = 0 (the backward kernels accumulate into it).  overlap=True: the 1.25 GB clear runs
         on an aux stream beside the forward (which never touches gradients); grad_ready() must then
-        be called before the backward (it makes the current stream wait for the clear).  The clear is
-        issued when the forward reaches the recurrent decoder (flat.pending_clear), whose latency-bound
-        launches leave most CUs idle — issued at the step's start it delayed the BERT forward, the
-        step's first critical-path chain, by ~0.2 ms; grad_ready() issues it if nothing did."""
+        be called before the backward (it makes the current stream wait for the clear).  It is issued at
+        the step's start, beside the BERT forward (LRCE_CLEAR_AT_DECODER=1 defers it to the recurrent
+        decoder's start instead, flat.pending_clear: 303.2 vs 309.5 QA-samples/s — the decoder's
+        latency chain suffers more from the 1.25 GB stream than BERT's); grad_ready() issues a deferred
+        clear if nothing did."""
         self.flat.grads_zeroed()
         if not overlap or not self.flat.grad.is_cuda:
             self.flat.grad.zero_()
@@ -243,4 +244,4 @@ class FusedAdamW(torch.optim.Optimizer):
         return float(self.step_t.item())
 
 
-_CLEAR_AT_DECODER = os.environ.get("LRCE_CLEAR_AT_DECODER", "1") != "0"   # A/B knob (see zero_grad)
+_CLEAR_AT_DECODER = os.environ.get("LRCE_CLEAR_AT_DECODER", "0") == "1"   # A/B knob (see zero_grad): slower, off
