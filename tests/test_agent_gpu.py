@@ -148,7 +148,7 @@ def test_early_group_updates_match_one_update():
     opt.enable_early_updates(model.optimizer_groups())
     opt.zero_grad()
     F.cross_entropy(model(*b[:4]).float(), b[4]).backward()
-    assert opt.early_updates == 5                 # decoder, text, swin3, swin2, swin1 inside the backward
+    assert opt.early_updates == len(model.optimizer_groups())   # decoder, text(_hi), swin3, swin2, swin1 inside the backward
     opt.step()
     torch.cuda.synchronize()
     early = flat.f32.clone()
@@ -226,7 +226,7 @@ def test_early_updates_do_not_race_the_backward():
     g_plain, w_plain, n_plain = run({})
     g_plain2, w_plain2, _ = run({})
     g_early, w_early, n_early = run(model.optimizer_groups())
-    assert n_early == 5 and n_plain == 0
+    assert n_early == len(model.optimizer_groups()) and n_plain == 0
     noise = worst(g_plain2, g_plain, g_plain)
     err = worst(g_early, g_plain, g_plain)
     assert noise[0] < 1e-4, f"plain runs differ: {noise}"
