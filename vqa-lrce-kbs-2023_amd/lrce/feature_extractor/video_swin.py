@@ -663,6 +663,8 @@ class SwinTransformer3D(nn.Module):
                 x = x_leaf
             geo = geos[li]
             nb = len(layer.blocks)
+            if li == 2 and getattr(flat, "pending_clear_at", None) == "swin3":
+                flat.pending_clear()   # the step's gradient clear beside stage 3's MFMA-bound GEMMs (optim.zero_grad)
             tiles = None
             if pre is not None:
                 tiles, ev = pre[li]

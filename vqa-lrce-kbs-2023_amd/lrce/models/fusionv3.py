@@ -388,7 +388,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             for l in range(1, nL):
                 issue_kv(l)
         clear = getattr(flat, "pending_clear", None)
-        if clear is not None:
+        if clear is not None and getattr(flat, "pending_clear_at", None) == "decoder":
             clear()   # the step's gradient clear (FusedAdamW.zero_grad) beside the latency-bound recurrence
         acts = [_LayerActs(S, Bq, dev) for _ in layers]
         s = acts[0].x0[0]

@@ -184,11 +184,13 @@ class FusedAdamW(torch.optim.Optimizer):
             return
         if _CLEAR_AT_DECODER:
             self.flat.pending_clear = self._issue_clear
+            self.flat.pending_clear_at = _CLEAR_AT
         else:
             self._issue_clear()
 
     def _issue_clear(self):
         self.flat.pending_clear = None
+        self.flat.pending_clear_at = None
         dev = self.flat.device
         s = aux_stream(dev, "grad_zero")
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -244,4 +246,7 @@ class FusedAdamW(torch.optim.Optimizer):
         return float(self.step_t.item())
 
 
-_CLEAR_AT_DECODER = os.environ.get("LRCE_CLEAR_AT_DECODER", "0") == "1"   # A/B knob (see zero_grad): slower, off
+# A/B knob (see zero_grad): where the overlapped gradient clear is issued — "start" (the step's start,
+# beside the BERT forward), "decoder" (the recurrent decoder's start: slower), "swin3" (Swin stage 3's start)
+_CLEAR_AT = os.environ.get("LRCE_CLEAR_AT", "start")
+_CLEAR_AT_DECODER = _CLEAR_AT != "start"
