@@ -484,7 +484,7 @@ _LN_DEFER = os.environ.get("LRCE_BERT_LN_DEFER", "1") != "0"             # A/B k
 _REDUCE_LN = os.environ.get("LRCE_BERT_REDUCE_LN", "1") != "0"           # A/B knob (linear_resid_ln)
 _STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"      # A/B knob (see FlatParams.claim_fresh)
 _DELAYED_SCALE = os.environ.get("LRCE_BERT_DELAYED_SCALE", "1") != "0"   # A/B knob
-_SPLIT_FLUSH = os.environ.get("LRCE_BERT_SPLIT_FLUSH", "1") != "0"       # A/B knob (upper half updated early)
+_SPLIT_FLUSH = os.environ.get("LRCE_BERT_SPLIT_FLUSH", "0") == "1"       # A/B knob (upper half updated early): not faster, off
 
 
 def _uniform_stride(ts, es):
