@@ -33,6 +33,9 @@ def main(d, kname, out, note=""):
            "correction": "FETCH_SIZE x2 (gfx950: 128-B requests counted as 64 B), KB -> B",
            "note": note}
     res["traffic_bytes_per_launch"] = res["fetch_bytes_per_launch"] + res["write_bytes_per_launch"]
+    # per dispatch (capture order within each pass), for launches of different sizes
+    res["per_dispatch_fetch_bytes"] = [round(2.0 * 1024.0 * v) for v in fetch]
+    res["per_dispatch_write_bytes"] = [round(1024.0 * v) for v in write]
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
