@@ -135,9 +135,11 @@ def grouped_vs_per_shape(nb, T, shapes, iters):
     grouped(); torch.cuda.synchronize()
     err = max(((it[2] - r[0]).abs().max() / r[0].abs().max()).item() for it, r in zip(items, ref))
     tp, tg = timed(per_shape, iters), timed(grouped, iters)
+    t2 = timed(lambda: K.linear_dw_grouped(items, split=2), iters)
     fl = sum(2.0 * T * O * I for _, O, I in shapes) * nb
     print(f"{nb} blocks x {[s[0] for s in shapes]} T={T}: per-shape launches {tp:8.1f} us ({fl / tp / 1e6:6.1f} TF/s)   "
-          f"grouped {tg:8.1f} us ({fl / tg / 1e6:6.1f} TF/s)   first-pass rel diff {err:.1e}", flush=True)
+          f"grouped {tg:8.1f} us ({fl / tg / 1e6:6.1f} TF/s)   grouped 2 K slices {t2:8.1f} us   "
+          f"first-pass rel diff {err:.1e}", flush=True)
 
 
 if __name__ == "__main__":

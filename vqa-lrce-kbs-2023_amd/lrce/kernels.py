@@ -450,6 +450,7 @@ def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1,
 
 _GROUPED_DW = os.environ.get("LRCE_GROUPED_DW", "1") != "0"   # A/B knob: one grouped launch vs one per shape
 _SPLIT_DW = os.environ.get("LRCE_SPLIT_DW", "1") != "0"       # A/B knob: long-K stages deferred as split slabs
+_SHORT_SPLIT = int(os.environ.get("LRCE_DW_SHORT_SPLIT", "1"))   # A/B knob: K slices of the short-K stages (3-4)
 
 
 class DeferredGrads:
@@ -480,7 +481,7 @@ class DeferredGrads:
                 for it in self.dw:
                     by_t.setdefault((it[1].shape[0], it[0].dtype), []).append(it)
                 for (T, _), items in by_t.items():
-                    split = 1
+                    split = _SHORT_SPLIT
                     if T > 32768:   # a few tiles over a long K: slices so the grid fills ~one round of the chip
                         tiles = sum(-(-it[2].shape[0] // 128) * -(-it[2].shape[1] // 128) for it in items)
                         split = max(2, min(64, round(512 / tiles)))
