@@ -123,3 +123,89 @@ def test_stale_library_is_refused_whole(monkeypatch):
         with pytest.raises(N.NativeError, match="stale build"):
             N.lib()
     assert N._lib is None
+
+
+def _gitem(N, **kw):
+    e = N.GemmItem()
+    e.a = e.b = e.c = 0x7F0000000000
+    e.m, e.n, e.lda, e.ldb, e.ldc = 256, 128, 256, 128, 128
+    e.flags, e.f16, e.split, e.k_chunk = N.EPI_ACCUM, 0, 1, 0
+    for k, v in kw.items():
+        setattr(e, k, v)
+    return e
+
+
+@pytest.mark.parametrize("kw,msg", [(dict(m=100), b"m=100"), (dict(flags=64 | 512), b"flags"),
+                                    (dict(split=3, k_chunk=320, flags=16), b"k_chunk 320"),
+                                    (dict(split=3, k_chunk=384), b"OUT_F32"), (dict(lda=128), b"lda=128"),
+                                    (dict(f16=2), b"f16=2"), (dict(a=0x7F0000000008), b"aligned")])
+def test_grouped_gemm_rejects_bad_items_without_launching(kw, msg):
+    """lrce_gemm_grouped validates every entry before any launch: shape multiples, epilogue flags (a
+    bias gradient needs a bias), K slices (split x k_chunk must cover K exactly, slabs are stored),
+    leading dims, operand format and alignment."""
+    from lrce import _native as N
+    items = (N.GemmItem * 2)(_gitem(N), _gitem(N, **kw))
+    assert N.lib().lrce_gemm_grouped(items, 2, 1000, 1.0, None) == 1
+    assert msg in N.lib().lrce_last_error(), N.lib().lrce_last_error()
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="would launch on the GPU with fake pointers")
+def test_grouped_gemm_host_path_returns_without_a_device():
+    """100 valid entries of 9 shapes (more than one launch's 80-entry / 8-shape tables, bf16 and fp16,
+    split and unsplit): the host side packs every launch and returns the HIP error as a status code."""
+    from lrce import _native as N
+    its = []
+    for i in range(100):
+        m = 128 * (1 + i % 9)
+        its.append(_gitem(N, m=m, lda=m, f16=i % 2, split=1 + (i % 3 == 0) * 2, k_chunk=384 if i % 3 == 0 else 0,
+                          flags=N.EPI_OUT_F32 if i % 3 == 0 else N.EPI_ACCUM, c=0x7F0000000000 + 0x100000 * i))
+    items = (N.GemmItem * 100)(*its)
+    assert N.lib().lrce_gemm_grouped(items, 100, 1000, 1.0, None) != 0
+    s = (N.SlabSum * 1)()
+    s[0].slabs, s[0].dst, s[0].n, s[0].split, s[0].accumulate = 0x7F0000000000, 0x7F0000100000, 6, 2, 1
+    assert N.lib().lrce_slab_sum_grouped(s, 1, None) == 1 and b"n % 4" in N.lib().lrce_last_error()
+
+
+def test_grouped_weight_gradient_packing(monkeypatch):
+    """kernels.linear_dw_grouped's host packing (CPU tensors, the launch intercepted): per-entry shape /
+    leading dims / flags / device alpha, and with K slices every weight and bias slab carved from one
+    workspace, k_chunk a multiple of 64 covering T, the slab sums storing fresh weights and adding biases."""
+    from lrce import kernels as K, _native as N
+    calls = {}
+
+    def fake_call(name, *args):
+        calls[name] = args
+    monkeypatch.setattr(K, "call", fake_call)
+    monkeypatch.setattr(K, "stream_of", lambda t: None)
+    T = 1000
+    shapes = [(256, 384), (128, 256), (384, 128)]
+    items = []
+    for j, (O, I) in enumerate(shapes):
+        dy = torch.zeros(T, O, dtype=torch.bfloat16)
+        x = torch.zeros(T, 2 * I, dtype=torch.bfloat16)[:, :I]          # a column block: ldb = 2I
+        dw, db = torch.zeros(O, I), (torch.zeros(O) if j != 1 else None)
+        items.append((dy, x, dw, db, j == 0))
+    K.linear_dw_grouped(items)
+    arr = calls["lrce_gemm_grouped"][0]
+    assert calls["lrce_gemm_grouped"][1:4] == (3, T, 1.0) and "lrce_slab_sum_grouped" not in calls
+    for e, (dy, x, dw, db, store) in zip(arr, items):
+        assert (e.m, e.n, e.lda, e.ldb, e.ldc, e.split) == (dw.shape[0], dw.shape[1], dw.shape[0], 2 * dw.shape[1],
+                                                          dw.shape[1], 1)
+        assert e.c == dw.data_ptr() and (e.bias or 0) == (db.data_ptr() if db is not None else 0)
+        assert e.flags == ((N.EPI_OUT_F32 if store else N.EPI_ACCUM) | (N.EPI_BIAS_GRAD if db is not None else 0))
+    calls.clear()
+    K.linear_dw_grouped(items, split=3)
+    arr = calls["lrce_gemm_grouped"][0]
+    sums, nsum = calls["lrce_slab_sum_grouped"][0], calls["lrce_slab_sum_grouped"][1]
+    kc = arr[0].k_chunk
+    assert kc % 64 == 0 and (arr[0].split - 1) * kc < T <= arr[0].split * kc
+    assert nsum == 5   # three weights + two biases
+    k = 0
+    for e, (dy, x, dw, db, store) in zip(arr, items):
+        assert e.flags & N.EPI_OUT_F32 and e.split == arr[0].split
+        assert sums[k].slabs == e.c and sums[k].dst == dw.data_ptr() and sums[k].n == dw.numel()
+        assert sums[k].accumulate == int(not store)
+        k += 1
+        if db is not None:
+            assert sums[k].slabs == e.bias and sums[k].dst == db.data_ptr() and sums[k].accumulate == 1
+            k += 1
