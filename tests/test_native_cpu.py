@@ -145,7 +145,7 @@ def test_grouped_gemm_rejects_bad_items_without_launching(kw, msg):
     leading dims, operand format and alignment."""
     from lrce import _native as N
     items = (N.GemmItem * 2)(_gitem(N), _gitem(N, **kw))
-    assert N.lib().lrce_gemm_grouped(items, 2, 1000, 1.0, None) == 1
+    assert N.lib().lrce_gemm_grouped(items, 2, 1000, 1.0, None, None) == 1
     assert msg in N.lib().lrce_last_error(), N.lib().lrce_last_error()
 
 
@@ -160,7 +160,7 @@ def test_grouped_gemm_host_path_returns_without_a_device():
         its.append(_gitem(N, m=m, lda=m, f16=i % 2, split=1 + (i % 3 == 0) * 2, k_chunk=384 if i % 3 == 0 else 0,
                           flags=N.EPI_OUT_F32 if i % 3 == 0 else N.EPI_ACCUM, c=0x7F0000000000 + 0x100000 * i))
     items = (N.GemmItem * 100)(*its)
-    assert N.lib().lrce_gemm_grouped(items, 100, 1000, 1.0, None) != 0
+    assert N.lib().lrce_gemm_grouped(items, 100, 1000, 1.0, None, None) != 0
     s = (N.SlabSum * 1)()
     s[0].slabs, s[0].dst, s[0].n, s[0].split, s[0].accumulate = 0x7F0000000000, 0x7F0000100000, 6, 2, 1
     assert N.lib().lrce_slab_sum_grouped(s, 1, None) == 1 and b"n % 4" in N.lib().lrce_last_error()
@@ -187,7 +187,7 @@ def test_grouped_weight_gradient_packing(monkeypatch):
         items.append((dy, x, dw, db, j == 0))
     K.linear_dw_grouped(items)
     arr = calls["lrce_gemm_grouped"][0]
-    assert calls["lrce_gemm_grouped"][1:4] == (3, T, 1.0) and "lrce_slab_sum_grouped" not in calls
+    assert calls["lrce_gemm_grouped"][1:5] == (3, T, 1.0, None) and "lrce_slab_sum_grouped" not in calls
     for e, (dy, x, dw, db, store) in zip(arr, items):
         assert (e.m, e.n, e.lda, e.ldb, e.ldc, e.split) == (dw.shape[0], dw.shape[1], dw.shape[0], 2 * dw.shape[1],
                                                           dw.shape[1], 1)

@@ -84,6 +84,12 @@ struct GemmPT : GemmP {
   int aoff[GPT];          // device alpha offset from p.alpha_dev (floats), -1: the launch's alpha
   const void* ta[GPT];
   const bf16* tb[GPT];
+  // lockstep throttle (or null): prog[wg] = the K phase (prog_ph K tiles) workgroup wg has reached; a
+  // workgroup more than one phase ahead of the one dispatched before it on its XCD (blockIdx.x - 8,
+  // always resident or done) sleeps, boundedly, so co-resident tiles reading the same panels stay
+  // within the L2's window of them
+  unsigned* prog;
+  int prog_ph;
 };
 static_assert(sizeof(GemmPT) <= 3840, "grouped GEMM tables must fit the kernel-argument block");
 template <bool PT>
@@ -819,6 +825,19 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(const GemmArg<PT> pa) 
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (kt == 0) GT_MARK(1);
+      if constexpr (PT) {
+        if (pa.prog && kt > 0 && threadIdx.x == 0 && kt % pa.prog_ph == 0) {
+          const unsigned ph = (unsigned)(kt / pa.prog_ph);
+          __hip_atomic_store(pa.prog + blockIdx.x, ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (blockIdx.x >= 8) {
+            const unsigned* prev = pa.prog + blockIdx.x - 8;
+            for (int it = 0; it < 128; ++it) {   // bounded: a throttle, never a dependency
+              if (__hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u >= ph) break;
+              __builtin_amdgcn_s_sleep(4);
+            }
+          }
+        }
+      }
       if (kt + NS - 1 < nfull) {
         const int nxt = cur == 0 ? NS - 1 : cur - 1;   // (kt + NS - 1) % NS
         ga.advance(); gb.advance();
@@ -832,6 +851,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(const GemmArg<PT> pa) 
     }
     __builtin_amdgcn_s_barrier();   // every wave is done with every stage (tail / LDS epilogue reuse)
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PT) {
+      if (pa.prog && threadIdx.x == 0)   // done: never holds a successor back
+        __hip_atomic_store(pa.prog + blockIdx.x, 0x7FFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (tail) {
     const int k0 = kb + nfull * BK;
@@ -1376,7 +1399,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
 // dY_e, B N-major = X_e, C_e f32), db_e[m] += sum_k dY_e[k][m] for entries with BIAS_GRAD.  One K slice
 // per tile (no split-K slabs, no reduce launch): the entries' summed tile count fills the chip.  All
 // entries share K (the token count) and alpha; up to GPT entries / GSH distinct shapes per launch.
-extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alpha, void* stream) {
+extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alpha, uint32_t* progress, void* stream) {
   if (n < 0 || (n > 0 && !it) || k <= 0) return lrce_fail(LRCE_E_ARG, "gemm_grouped: n=%d k=%d", n, k);
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   for (int i = 0; i < n; ++i) {
@@ -1464,6 +1487,9 @@ extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alp
     }
     p.a = p.ta[0]; p.b = p.tb[0];
     p.m = p.sh[0].m; p.n = p.sh[0].n; p.tiles_m = p.sh[0].tiles_m; p.tiles_n = p.sh[0].tiles_n;
+    p.prog = progress;
+    p.prog_ph = 8;
+    if (progress) progress += tiles;   // the next launch's workgroups
     if (f16) gemm_glds_kernel<128, 128, false, false, true, 2, false, true><<<dim3(tiles, 1), NT, 0, s>>>(p);
     else gemm_glds_kernel<128, 128, false, false, false, 2, false, true><<<dim3(tiles, 1), NT, 0, s>>>(p);
     i = j;
@@ -1486,7 +1512,7 @@ extern "C" int lrce_gemm_ptr_batched(const LrceGemmDesc* d, const void* const* a
   for (int i = 0; i < n; ++i)
     items[i] = LrceGemmItem{a[i], b[i], static_cast<float*>(c[i]), bg ? const_cast<float*>(bias[i]) : nullptr,
                             nullptr, d->m, d->n, (int32_t)d->lda, (int32_t)d->ldb, (int32_t)d->ldc, d->flags, 0, 1, 0};
-  return lrce_gemm_grouped(items.data(), n, d->k, d->alpha, stream);
+  return lrce_gemm_grouped(items.data(), n, d->k, d->alpha, nullptr, stream);
 }
 
 // dst_i (=|+=) sum_s slabs_i[s][0..n_i) in slice order (the grouped launch's split-K weight gradients):

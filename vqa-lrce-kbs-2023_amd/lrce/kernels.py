@@ -393,8 +393,13 @@ def linear_dw_grouped(items, split=1):
         flops += 2.0 * O * I * T
     dw0 = items[0][2]
 
+    prog = None
+    if _DW_LOCKSTEP:
+        wgs = sum(-(-it[2].shape[0] // 128) * -(-it[2].shape[1] // 128) for it in items) * max(split, 1)
+        prog = torch.zeros(wgs, dtype=torch.int32, device=dev)
+
     def run():
-        call("lrce_gemm_grouped", arr, len(items), T, 1.0, stream_of(dw0))
+        call("lrce_gemm_grouped", arr, len(items), T, 1.0, ptr(prog), stream_of(dw0))
         if split > 1:
             call("lrce_slab_sum_grouped", sums, nsum, stream_of(dw0))
     _timed("gemm", dw0, run, flops=flops, key=("grouped", T, len(items), split))
@@ -451,6 +456,7 @@ def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1,
 _GROUPED_DW = os.environ.get("LRCE_GROUPED_DW", "1") != "0"   # A/B knob: one grouped launch vs one per shape
 _SPLIT_DW = os.environ.get("LRCE_SPLIT_DW", "1") != "0"       # A/B knob: long-K stages deferred as split slabs
 _SHORT_SPLIT = int(os.environ.get("LRCE_DW_SHORT_SPLIT", "1"))   # A/B knob: K slices of the short-K stages (3-4)
+_DW_LOCKSTEP = os.environ.get("LRCE_DW_LOCKSTEP", "0") == "1"   # A/B knob: lrce_gemm_grouped progress throttle
 
 
 class DeferredGrads:
