@@ -5,6 +5,8 @@
 // that every tensor starts at a multiple of 1024 elements; chunk c (1024 elements) belongs to one
 // tensor (chunk_tensor[c]).  One pass reads p, g, m, v and writes p, m, v and the bf16 shadow
 // copy the forward kernels consume: 4+4+4+4 + 4+4+4+2 = 30 B per parameter, HBM-bound.
+#include <cstdlib>
+
 #include "common.h"
 #include "lrce_capi.h"
 
@@ -58,6 +60,24 @@ __global__ void __launch_bounds__(256) segsum_kernel(const float* __restrict__ c
 // (exp2 of t * log2(beta)), so the launch replays unchanged from a HIP graph.
 constexpr int ADAMW_CPW = 2;
 
+// NT: non-temporal loads / stores (every operand is touched once per step); CPW: chunks per wave
+typedef float f32x4n __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 ld_s(const float* q) {
+  if constexpr (NT) {
+    const f32x4n t = __builtin_nontemporal_load(reinterpret_cast<const f32x4n*>(q));
+    return make_float4(t.x, t.y, t.z, t.w);
+  } else {
+    return *reinterpret_cast<const float4*>(q);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st_s(float* q, float4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(f32x4n{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4n*>(q));
+  else *reinterpret_cast<float4*>(q) = v;
+}
+
+template <bool NT, int CPW>
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, const int* __restrict__ chunk_tensor,
                                                     const float* __restrict__ tensor_lr, const float* __restrict__ sumsq,
@@ -74,8 +94,8 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
     bc2 = 1.0f - exp2f(t * __log2f(b2));
   }
   const float isb2 = rsqrtf(bc2);
-  for (int k = 0; k < ADAMW_CPW; ++k) {
-    const int c = wave_id * ADAMW_CPW + k;
+  for (int k = 0; k < CPW; ++k) {
+    const int c = wave_id * CPW + k;
     if (c >= n_chunks) break;
     const int t = chunk_tensor[c];
     const float lr = tensor_lr[t];
@@ -87,15 +107,15 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const long long i = base + r * 256;
-      pp[r] = *reinterpret_cast<const float4*>(p + i);
+      pp[r] = ld_s<NT>(p + i);
       if (g16) {   // bf16 gradient (the all-reduced bf16 buckets of lrce/distributed.py)
         const bf16x4 h = *reinterpret_cast<const bf16x4*>(g16 + i);
         gg[r] = make_float4(bf2f(h[0]), bf2f(h[1]), bf2f(h[2]), bf2f(h[3]));
       } else {
-        gg[r] = *reinterpret_cast<const float4*>(g + i);
+        gg[r] = ld_s<NT>(g + i);
       }
-      mm[r] = *reinterpret_cast<const float4*>(m + i);
-      vv[r] = *reinterpret_cast<const float4*>(v + i);
+      mm[r] = ld_s<NT>(m + i);
+      vv[r] = ld_s<NT>(v + i);
     }
     float q = 0.f;
 #pragma unroll
@@ -118,9 +138,9 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
         pa[j] = fin ? np : pa[j];
         ob[j] = f2bf(pa[j]);
       }
-      *reinterpret_cast<float4*>(p + i) = pp[r];
-      *reinterpret_cast<float4*>(m + i) = mm[r];
-      *reinterpret_cast<float4*>(v + i) = vv[r];
+      st_s<NT>(p + i, pp[r]);
+      st_s<NT>(m + i, mm[r]);
+      st_s<NT>(v + i, vv[r]);
       if (pb) *reinterpret_cast<bf16x4*>(pb + i) = ob;
       if (ph && i >= h_lo && i < h_hi) {   // fp16 shadow of the BERT range (chunk-uniform branch)
         bf16x4 oh;
@@ -162,13 +182,26 @@ extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, con
   // the f16 range is relative to p (it may start before this call's first chunk: a sub-range update)
   if (p_f16 && (f16_lo % 1024 || f16_hi % 1024 || f16_hi < f16_lo))
     return lrce_fail(LRCE_E_ARG, "adamw_step: f16 shadow range [%lld, %lld) not chunk aligned", (long long)f16_lo, (long long)f16_hi);
-  if (n_chunks > 0)
-    adamw_kernel<<<(n_chunks + 4 * ADAMW_CPW - 1) / (4 * ADAMW_CPW), 256, 0, static_cast<hipStream_t>(stream)>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq,
-                                                                         reinterpret_cast<bf16*>(p_bf16), n_chunks, beta1, beta2, eps,
-                                                                         weight_decay, grad_scale, reg, bc1, bc2, step, sumsq_next,
-                                                                         reinterpret_cast<bf16*>(p_f16), f16_lo, f16_hi,
-                                                                         reinterpret_cast<const bf16*>(g_bf16),
-                                                                         sumsq_next ? chunk_sq : nullptr);
+  if (n_chunks > 0) {
+    // A/B variants (LRCE_ADAMW_VARIANT): 0 plain loads / stores, 2 chunks per wave; 1 non-temporal;
+    // 2 one chunk per wave; 3 both
+    static const int var = getenv("LRCE_ADAMW_VARIANT") ? atoi(getenv("LRCE_ADAMW_VARIANT")) : 0;
+    const int cpw = (var & 2) ? 1 : ADAMW_CPW;
+    const dim3 grid((n_chunks + 4 * cpw - 1) / (4 * cpw));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto launch = [&](auto kern) {
+      kern<<<grid, 256, 0, s>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq, reinterpret_cast<bf16*>(p_bf16), n_chunks, beta1,
+                                beta2, eps, weight_decay, grad_scale, reg, bc1, bc2, step, sumsq_next,
+                                reinterpret_cast<bf16*>(p_f16), f16_lo, f16_hi, reinterpret_cast<const bf16*>(g_bf16),
+                                sumsq_next ? chunk_sq : nullptr);
+    };
+    switch (var & 3) {
+      case 1: launch(adamw_kernel<true, ADAMW_CPW>); break;
+      case 2: launch(adamw_kernel<false, 1>); break;
+      case 3: launch(adamw_kernel<true, 1>); break;
+      default: launch(adamw_kernel<false, ADAMW_CPW>); break;
+    }
+  }
   if (sumsq_next && chunk_sq && tensor_chunk_off && n_tensors > 0)
     segsum_kernel<<<n_tensors, 256, 0, static_cast<hipStream_t>(stream)>>>(chunk_sq, tensor_chunk_off, n_tensors, sumsq_next);
   return lrce_check_launch("adamw_step");
