@@ -43,8 +43,8 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
-    print(f"variant {os.environ.get('LRCE_ADAMW_VARIANT', '0')}: {n / 1e6:.0f} M params  {us:8.1f} us  "
-          f"{30.0 * n / us / 1e3:6.2f} TB/s (30 B/param)", flush=True)
+    print(f"variant {os.environ.get('LRCE_ADAMW_VARIANT', 'default')}: {n / 1e6:.0f} M params  {us:8.1f} us  "
+          f"{30.0 * n / us / 1e6:6.2f} TB/s (30 B/param)", flush=True)
 
 
 if __name__ == "__main__":
