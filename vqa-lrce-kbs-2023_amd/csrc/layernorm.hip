@@ -8,6 +8,9 @@
 // which pads BEFORE its norm, :328-331) the segment reads as zeros; a whole missing row of a
 // one-segment gather is a window position past the volume (the block pads AFTER norm1, :253-258):
 // its output row is zero and it takes no part in the backward.
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 #include "lrce_capi.h"
 #include <cstdlib>
@@ -152,7 +155,25 @@ struct F16Scaled {
   const uint64_t* off;
 };
 
-template <typename TD, typename TX, int CH, int LPR, bool F16S = false>
+// NT: non-temporal loads of x / dres and stores of dx (each touched once here; dx is next read by a
+// LayerNorm backward a whole block later)
+typedef float lnf4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 ld4f(const float* p) {
+  if constexpr (NT) {
+    const lnf4 t = __builtin_nontemporal_load(reinterpret_cast<const lnf4*>(p));
+    return make_float4(t.x, t.y, t.z, t.w);
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
+}
+template <bool NT, typename TX>
+__device__ __forceinline__ float4 ld4x(const TX* p) {
+  if constexpr (NT && std::is_same<TX, float>::value) return ld4f<true>(reinterpret_cast<const float*>(p));
+  else return ld4<TX>(p);
+}
+
+template <typename TD, typename TX, int CH, int LPR, bool F16S = false, bool NT = false>
 __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, const TX* x, const int* in_map, int nseg,
                                               const float* mean_i, const float* rstd_i, const float* w, float* dx,
                                               const float* dres, float* dw, float* db, int rows, int cols, bf16* dx16,
@@ -187,8 +208,8 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
         int ok;
         const long long o = src_off(in_map, nseg, seg, r, c, ok);
         if (ok) {
-          xv[t] = ld4<TX>(x + o);
-          if (dres) rv[t] = *reinterpret_cast<const float4*>(dres + o);
+          xv[t] = ld4x<NT, TX>(x + o);
+          if (dres) rv[t] = ld4f<NT>(dres + o);
         } else if (nseg == 1) {
           pad = true;
         }
@@ -255,7 +276,10 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
           const float4 rr = rcur[t];
           out.x += rr.x; out.y += rr.y; out.z += rr.z; out.w += rr.w;
         }
-        if (dx) *reinterpret_cast<float4*>(dx + o) = out;
+        if (dx) {
+          if constexpr (NT) __builtin_nontemporal_store(lnf4{out.x, out.y, out.z, out.w}, reinterpret_cast<lnf4*>(dx + o));
+          else *reinterpret_cast<float4*>(dx + o) = out;
+        }
         if constexpr (F16S) {   // (identity maps on this path: the host checks)
           const float a4[4] = {out.x, out.y, out.z, out.w};
 #pragma unroll
@@ -559,11 +583,11 @@ static int layernorm_bwd_impl(const void* dy, int dy_f32, const int32_t* dy_map,
   float* part = want && nb_ws > 1 && workspace && workspace_elems >= (int64_t)(nb_ws + ny) * 2 * cols + LN_RED_CTRS
                     ? workspace : nullptr;
   const int nb = (part || !want) ? nb_ws : ln_bwd_blocks(rows, lpr, false, cols);
+  static const bool nt = getenv("LRCE_LN_NT") && atoi(getenv("LRCE_LN_NT")) != 0;   // A/B knob
 #define LNB3(TD, TX, CH, LPR)                                                                                          \
-  ln_bwd<TD, TX, CH, LPR><<<nb, 256, 0, s>>>(static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, \
-                                                     nseg, mean, rstd, w, dx, dres, dw, db, rows, cols,      \
-                                                     reinterpret_cast<bf16*>(dx_bf16), dx_bf16_map, dx_scale, dx_scale_rps, \
-                                                     part)
+  (nt ? ln_bwd<TD, TX, CH, LPR, false, true> : ln_bwd<TD, TX, CH, LPR>)<<<nb, 256, 0, s>>>(                         \
+      static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, nseg, mean, rstd, w, dx, dres, dw, db, rows, \
+      cols, reinterpret_cast<bf16*>(dx_bf16), dx_bf16_map, dx_scale, dx_scale_rps, part, F16Scaled{})
 #define LNB(TD, TX)                                   \
   if (nch <= 32) LNB3(TD, TX, 1, 32);                 \
   else if (nch <= 64) LNB3(TD, TX, 1, 64);            \
