@@ -583,7 +583,10 @@ static int layernorm_bwd_impl(const void* dy, int dy_f32, const int32_t* dy_map,
   float* part = want && nb_ws > 1 && workspace && workspace_elems >= (int64_t)(nb_ws + ny) * 2 * cols + LN_RED_CTRS
                     ? workspace : nullptr;
   const int nb = (part || !want) ? nb_ws : ln_bwd_blocks(rows, lpr, false, cols);
-  static const bool nt = getenv("LRCE_LN_NT") && atoi(getenv("LRCE_LN_NT")) != 0;   // A/B knob
+  // non-temporal x / dres / dx on the large shapes only (tools/ln_bench.py: 250 880 x 128 and 62 720 x 512
+  // 113 -> 98 / 94 us; at <= 16 M elements the hint costs up to 15 %); LRCE_LN_NT=0 / 1 forces it
+  static const int nt_env = getenv("LRCE_LN_NT") ? atoi(getenv("LRCE_LN_NT")) : -1;
+  const bool nt = nt_env >= 0 ? nt_env != 0 : (long long)rows * cols >= (24LL << 20);
 #define LNB3(TD, TX, CH, LPR)                                                                                          \
   (nt ? ln_bwd<TD, TX, CH, LPR, false, true> : ln_bwd<TD, TX, CH, LPR>)<<<nb, 256, 0, s>>>(                         \
       static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, nseg, mean, rstd, w, dx, dres, dw, db, rows, \
