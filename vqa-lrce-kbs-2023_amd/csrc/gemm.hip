@@ -1111,6 +1111,19 @@ __global__ void splitk_reduce_epi_kernel(const float* __restrict__ ws, int split
 // the one-thread-per-float4 reduce above with a few waves each walking every slab serially; here a
 // block is 64 float4 columns x 4 slice groups, each thread keeps 4 slab loads in flight, and the
 // groups meet in LDS.
+// slab reads: each slab element is read exactly once (NT: streaming hint, LRCE_RED_NT A/B)
+typedef float rf4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 ld_slab(const float* q) {
+  if constexpr (NT) {
+    const rf4 t = __builtin_nontemporal_load(reinterpret_cast<const rf4*>(q));
+    return make_float4(t.x, t.y, t.z, t.w);
+  } else {
+    return *reinterpret_cast<const float4*>(q);
+  }
+}
+
+template <bool NT>
 __global__ void __launch_bounds__(256) splitk_reduce_deep_kernel(const float* __restrict__ ws, int split, int m, int n,
                                                                  float* __restrict__ c, long long ldc) {
   const long long mn = (long long)m * n;
@@ -1121,13 +1134,13 @@ __global__ void __launch_bounds__(256) splitk_reduce_deep_kernel(const float* __
   if (e < mn) {
     int k = g;
     for (; k + 12 < split; k += 16) {
-      const float4 t0 = *reinterpret_cast<const float4*>(ws + k * mn + e);
-      const float4 t1 = *reinterpret_cast<const float4*>(ws + (k + 4) * mn + e);
-      const float4 t2 = *reinterpret_cast<const float4*>(ws + (k + 8) * mn + e);
-      const float4 t3 = *reinterpret_cast<const float4*>(ws + (k + 12) * mn + e);
+      const float4 t0 = ld_slab<NT>(ws + k * mn + e);
+      const float4 t1 = ld_slab<NT>(ws + (k + 4) * mn + e);
+      const float4 t2 = ld_slab<NT>(ws + (k + 8) * mn + e);
+      const float4 t3 = ld_slab<NT>(ws + (k + 12) * mn + e);
       add(t0); add(t1); add(t2); add(t3);
     }
-    for (; k < split; k += 4) add(*reinterpret_cast<const float4*>(ws + k * mn + e));
+    for (; k < split; k += 4) add(ld_slab<NT>(ws + k * mn + e));
   }
   __shared__ float4 red[4][64];
   red[g][lane] = s;
@@ -1153,6 +1166,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream);
 static bool glds_ok(const LrceGemmDesc* d);
 static bool g_force_legacy_gemm = getenv("LRCE_LEGACY_GEMM") != nullptr;   // A/B switch for benchmarking
 static int g_gemm_tile = getenv("LRCE_GEMM_TILE") ? atoi(getenv("LRCE_GEMM_TILE")) : 0;   // 0 auto, 64, 128
+static bool g_red_nt = getenv("LRCE_RED_NT") && atoi(getenv("LRCE_RED_NT")) != 0;            // A/B knob
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
 
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
@@ -1375,7 +1389,8 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     } else if (p.ws) {
       const long long q4 = (long long)d->m * d->n / 4;
       if (split >= 8)
-        splitk_reduce_deep_kernel<<<(unsigned)((q4 + 63) / 64), 256, 0, s>>>(p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
+        (g_red_nt ? splitk_reduce_deep_kernel<true> : splitk_reduce_deep_kernel<false>)<<<(unsigned)((q4 + 63) / 64), 256, 0, s>>>(
+            p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
       else
         splitk_reduce_kernel<<<(unsigned)((q4 + 255) / 256), 256, 0, s>>>(p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
     }
@@ -1527,6 +1542,7 @@ struct SlabSumArgs {
   int split[SLAB_ITEMS];
   int accum[SLAB_ITEMS];
 };
+template <bool NT>
 __global__ void __launch_bounds__(256) slab_sum_kernel(const SlabSumArgs a) {
   const long long total = a.start[a.items];
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < total; q += (long long)gridDim.x * 256) {
@@ -1535,9 +1551,9 @@ __global__ void __launch_bounds__(256) slab_sum_kernel(const SlabSumArgs a) {
     const long long i = (q - a.start[it]) * 4;
     const float* src = a.src[it] + i;
     const long long n = a.n[it];
-    float4 acc = *reinterpret_cast<const float4*>(src);
+    float4 acc = ld_slab<NT>(src);
     for (int sl = 1; sl < a.split[it]; ++sl) {
-      const float4 v = *reinterpret_cast<const float4*>(src + sl * n);
+      const float4 v = ld_slab<NT>(src + sl * n);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     float4* d = reinterpret_cast<float4*>(a.dst[it] + i);
@@ -1570,7 +1586,7 @@ extern "C" int lrce_slab_sum_grouped(const LrceSlabSum* items, int n, void* stre
     }
     a.start[a.items] = tot;
     const long long blocks = (tot + 255) / 256;
-    slab_sum_kernel<<<(int)(blocks < 2048 ? blocks : 2048), 256, 0, s>>>(a);
+    (g_red_nt ? slab_sum_kernel<true> : slab_sum_kernel<false>)<<<(int)(blocks < 2048 ? blocks : 2048), 256, 0, s>>>(a);
   }
   return lrce_check_launch("slab_sum_grouped");
 }
