@@ -70,6 +70,22 @@ def parse():
     return ap.parse_args()
 
 
+def lrce_env():
+    """Every LRCE_* variable set in this process's environment (the product's A/B switches): recorded
+    in the JSON line, so a number measured with a non-default switch says so."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("LRCE_")}
+
+
+def refuse_tampering():
+    """The headline must be the full training step: refuse any LRCE_DEV_* variable (dev-only
+    experiments that skip work; none is read by the product any more, but an old tree or a stray
+    export must never produce a silently inflated number)."""
+    bad = sorted(k for k in os.environ if k.startswith("LRCE_DEV_"))
+    if bad:
+        log(f"refusing to run: dev-only work-skipping variables set: {', '.join(bad)}")
+        sys.exit(2)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -114,7 +130,8 @@ def dry_run(args, world, rank):
                           "unit": "launcher-check steps/s (not a measurement)", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
                           "config": {"parallelism": f"dp{world}", "per_gpu_batch": args.batch_size,
-                                     "grad_reduce": args.grad_reduce_dtype if world > 1 else None}}), flush=True)
+                                     "grad_reduce": args.grad_reduce_dtype if world > 1 else None},
+                          "lrce_env": lrce_env()}), flush=True)
 
 
 def synthetic_batch(batch, seed):
@@ -282,6 +299,7 @@ def cpu_baseline(threads, batch=10):
 
 def main():
     args = parse()
+    refuse_tampering()
     if args.gpus < 1:
         log("--gpus must be >= 1")
         sys.exit(2)
@@ -301,7 +319,8 @@ def main():
             dry_run(args, world, rank)
             dist.destroy_process_group()
         elif rank == 0:
-            print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": 1, "config": {"parallelism": "dp1"}}), flush=True)
+            print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": 1, "config": {"parallelism": "dp1"},
+                              "lrce_env": lrce_env()}), flush=True)
         return
     if world > 1:
         torch.cuda.set_device(local)
@@ -381,6 +400,7 @@ def main():
            "model_tflops": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0, 2),
            "model_mfu": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0 / (MFMA_BF16_PEAK_TFLOPS * world), 4)}
     out["roofline"] = roof
+    out["lrce_env"] = lrce_env()   # non-default product switches (empty for the default step)
     if agent is not None:
         out["agent_path"] = agent
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -42,3 +42,30 @@ def test_world_mismatch_is_an_error():
     rc, lines, err = _run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert rc != 0 and not lines
     assert "--gpus 2" in err
+
+
+def test_dev_only_work_skipping_variables_are_refused():
+    # a stray LRCE_DEV_* export must never yield a (silently inflated) headline
+    rc, lines, err = _run(["--gpus", "1", "--dry-run"], {"LRCE_DEV_SWIN_S3": "9"})
+    assert rc != 0 and not lines
+    assert "LRCE_DEV_SWIN_S3" in err
+
+
+def test_non_default_switches_are_recorded():
+    rc, lines, err = _run(["--gpus", "1", "--dry-run"], {"LRCE_DEC_KV_ASYNC": "0"})
+    assert rc == 0, err[-2000:]
+    assert json.loads(lines[0])["lrce_env"] == {"LRCE_DEC_KV_ASYNC": "0"}
+
+
+def test_product_reads_no_dev_only_variables():
+    # the work-skipping sensitivity knobs are gone from the product sources (their A/Bs are recorded
+    # in DESIGN.md / profiles/r5_bench_sensitivity_ab.txt)
+    pkg = os.path.join(REPO, "vqa-lrce-kbs-2023_amd")
+    hits = []
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                with open(os.path.join(root, f)) as fh:
+                    if "LRCE_DEV_" in fh.read():
+                        hits.append(f)
+    assert not hits, hits

@@ -543,10 +543,7 @@ class BertModel(nn.Module):
         x = _EmbedFn.apply(ids, types, self.embeddings, flat, p, seed, join_token, *anchor)
         st = _Stack(self, flat, B * L, dev)
         yield
-        # (LRCE_DEV_BERT_LAYERS=k: a sensitivity experiment only — the step with k of the 12 layers, to
-        # measure how much of the text branch is on the step's critical path; never set in the product)
-        n_run = int(os.environ.get("LRCE_DEV_BERT_LAYERS", "0")) or len(self.encoder.layer)
-        for i, layer in enumerate(list(self.encoder.layer)[:n_run]):
+        for i, layer in enumerate(self.encoder.layer):
             params = list(layer.parameters())
             if st.flush_at is None and torch.is_grad_enabled() and (x.requires_grad or any(q.requires_grad for q in params)):
                 st.flush_at = i      # the last layer backward to run issues the deferred weight gradients

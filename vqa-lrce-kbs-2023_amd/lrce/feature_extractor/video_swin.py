@@ -670,10 +670,6 @@ class SwinTransformer3D(nn.Module):
                 tiles, ev = pre[li]
                 torch.cuda.current_stream(dev).wait_event(ev)
             blocks = list(layer.blocks)
-            if li == 2 and os.environ.get("LRCE_DEV_SWIN_S3"):
-                # (a critical-path sensitivity experiment only: stage 3 with the first k of its 18 blocks;
-                # never set in the product)
-                blocks = blocks[:int(os.environ["LRCE_DEV_SWIN_S3"])]
             x = _run_blocks(blocks, x, geo, flat,
                             scales[bi:bi + len(blocks)] if scales is not None else [(None, None)] * len(blocks),
                             tiles[:len(blocks)] if tiles is not None else None, between=between_blocks)

@@ -338,13 +338,6 @@ _KV_WGRAD_BATCHED = os.environ.get("LRCE_DEC_KV_WGRAD_BATCHED", "0") == "1"
 _WGRAD_EARLY = os.environ.get("LRCE_DEC_WGRAD_EARLY", "0") == "1"   # measured slower (285.3 vs 286.4): off
 
 
-def _dev_layers(ft):
-    """The decoder layers a step runs: all 12 (LRCE_DEV_DEC_LAYERS=k keeps the first k — a critical-path
-    sensitivity experiment only, never set in the product)."""
-    k = int(os.environ.get("LRCE_DEV_DEC_LAYERS", "0"))
-    return list(ft.transformer.layers)[:k] if k else ft.transformer.layers
-
-
 class _RecurrentDecoderFn(torch.autograd.Function):
     """FusionTransformer.forward (fusionv3.py:27-51) as one autograd node; with t = None the memory
     is the video tokens alone (FusionVideo.forward, fusionv3.py:70-88)."""
@@ -352,7 +345,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, v, v16, t, t16, ft, flat, p, seed, B, S, nmc, anchor, *params):
         dev = v.device
-        layers = _dev_layers(ft)
+        layers = ft.transformer.layers
         Lt = t.shape[1] if t is not None else 0
         Bq = t.shape[0] if t is not None else B * nmc
         rows_v = B * S * 150
@@ -425,7 +418,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         kvv, kvt, saves, fused, v16, t16, acts = ctx.save
         ft, flat, p, seed = ctx.ft, ctx.flat, ctx.p, ctx.seed
         B, S, nmc, Bq, Lt = ctx.dims
-        layers = _dev_layers(ft)
+        layers = ft.transformer.layers
         dev = ds.device
         # video K/V gradients: written once per row by the step's attention backward (OE / Count), or
         # accumulated by the answer choices sharing the row (MC: atomics onto zeros)

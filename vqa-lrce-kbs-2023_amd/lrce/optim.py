@@ -179,10 +179,6 @@ class FusedAdamW(torch.optim.Optimizer):
         latency chain suffers more from the 1.25 GB stream than BERT's); grad_ready() issues a deferred
         clear if nothing did."""
         self.flat.grads_zeroed()
-        if os.environ.get("LRCE_DEV_NO_CLEAR"):
-            # (an upper-bound experiment only: what the clear costs the step; gradients then accumulate
-            # across steps — never set in the product)
-            return
         if not overlap or not self.flat.grad.is_cuda:
             self.flat.grad.zero_()
             return
