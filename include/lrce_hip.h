@@ -51,6 +51,8 @@ enum {
   LRCE_EPI_OUT_BOTH = 256, /* also write a bf16 copy of y into aux_out (f32 C + bf16 shadow) */
   LRCE_EPI_BIAS_GRAD = 512, /* weight-gradient GEMMs (A M-major = dY^T): also bias[m] += sum_k A(m,k)
                               (the nn.Linear bias gradient, with A's row map / row scale applied) */
+  LRCE_EPI_AUX_F32 = 2048, /* exact-f32 paths (b_f32): the AUX_OUT pre-activation and the DGELU aux are f32, not bf16
+                              (the recurrent decoder's linear1: its GELU derivative sees the exact pre-activation) */
   LRCE_EPI_SLABS = 1024    /* split_k > 1 with a workspace: write the split slices' f32 slabs
                               ws[s][m][n] (alpha applied) and launch NO reduce — a consumer such as
                               lrce_splitk_reduce_ln sums them (C is not written) */
@@ -508,6 +510,68 @@ int lrce_dec_sa_bwd(const LrceDecSaBwd* args, void* stream);
  * dgamma[k] / dbeta[k] may be NULL (frozen parameter). */
 int lrce_dec_ln_grads(const float* const* dy, const float* const* x, const float* const* mean, const float* const* rstd,
                       float* const* dgamma, float* const* dbeta, int n_ln, int rows, void* stream);
+/* ---------------------------------------------------------------- persistent recurrent decoder step
+ * FusionTransformer.forward's clip loop body (fusionv3.py:43-49 over the 12 nn.TransformerDecoderLayer of
+ * fusionv3.py:8-17): ONE launch per recurrent step and direction (csrc/decoder_step.hip), replacing the
+ * 4 + 4 launches per layer of the per-block path above.  12 x R workgroups (R = min(B, 10) row groups)
+ * stay resident for all 12 layers and hand rows to each other inside the launch (agent-scope write-through
+ * stores + arrival counters, bounded spins): per layer, (head h, row b) workgroups run the self-attention
+ * block and the cross-attention block (as lrce_dec_sa_fwd / lrce_dec_ca_fwd), and every workgroup takes
+ * 32-unit slices of the FFN hidden layer for ALL rows (linear1 -> GELU -> dropout -> its partial of
+ * linear2), so each FFN weight is read once per layer-step; the partials are summed by the next layer's
+ * (head, row) workgroups, 64 columns each, in slice order (deterministic).  The step tail (norm3 of the
+ * last layer, s + x3, fusion_layer_norm, dropout) runs in the same launch.  The backward mirrors it.
+ * Saved activations go to an arena laid out by lrce_dec_step_field (f32; element (step, row, col) of
+ * field f of layer l at field(f, l) + (step * B + row) * width(f) + col); the layer index n_layers
+ * holds the step tail.  Dropout masks and seeds are those of the per-block path: layer (i, l) uses
+ * seed + 64 (i n_layers + l) (+ 1 .. + 5 as lrce_dec_*), the tail seed + 7 + 64000 (i + 1). */
+#define LRCE_DEC_LAYERS 12
+typedef struct LrceDecLayerW {   /* one layer's parameters: 16-bit weights are the fp16 shadow [out][in] */
+  const uint16_t* wv; const float* bv;     /* self_attn.in_proj rows 2E..3E */
+  const uint16_t* wo; const float* bo;     /* self_attn.out_proj */
+  const float* g1; const float* be1;       /* norm1 */
+  const uint16_t* wq; const float* bq;     /* multihead_attn.in_proj rows 0..E */
+  const uint16_t* woc; const float* boc;   /* multihead_attn.out_proj */
+  const float* g2; const float* be2;       /* norm2 */
+  const uint16_t* w1; const float* b1;     /* linear1 [3072][768] */
+  const uint16_t* w2; const float* b2;     /* linear2 [768][3072] */
+  const float* g3; const float* be3;       /* norm3 */
+} LrceDecLayerW;
+typedef struct LrceDecStep {
+  int32_t B, S, step, nmc, lt, n_layers;   /* query rows, steps, this step, rows per video sample, question keys */
+  float eps, drop_p;
+  uint64_t seed;
+  const float* gf; const float* bf;        /* fusion_layer_norm */
+  const uint16_t* kv_video; int64_t kv_video_lstride;   /* layer l: [B/nmc*S*150][1536] bf16 (K | V) */
+  const uint16_t* kv_text; int64_t kv_text_lstride;     /* layer l: [B*lt][1536] bf16 (NULL when lt == 0) */
+  float* acts;                             /* forward arena (written by the forward, read by the backward) */
+  float* grads;                            /* backward arena */
+  float* s_out;                            /* forward of the last step: the output rows [B][768] */
+  const float* ds_in;                      /* backward: gradient of this step's output [B][768] */
+  float* ds_out;                           /* backward: gradient of this step's input [B][768] */
+  uint16_t* dkv_video16;                   /* backward, nmc == 1: video-row dK|dV stored bf16, layer stride dkv_video_lstride */
+  float* dkv_video32;                      /* backward, nmc > 1: f32 (zeroed by the caller), atomically added */
+  int64_t dkv_video_lstride;
+  float* dkv_text;                         /* backward: [B*lt][1536] f32 per layer, stored at step S-1 then added */
+  int64_t dkv_text_lstride;
+  float* ws;                               /* lrce_dec_step_ws_elems() f32 */
+  uint32_t* counters;                      /* lrce_dec_step_counter_words() uint32, zero (left zero by every launch) */
+  uint32_t* status;                        /* [4] uint32: [0] != 0 after a hand-off timed out (sticky until cleared) */
+  LrceDecLayerW layer[LRCE_DEC_LAYERS];
+} LrceDecStep;
+/* field offsets of the arenas: kind 0 = forward (fields x0 sad x1p x1 q ctx x2p x2 x3p pre gd lse m1 r1 m2 r2 m3
+ * r3; the tail block l = n_layers: x0 = tsum, m1 = mean, r1 = rstd), kind 1 = backward (df dgp dcao dq dsao dsav dln1
+ * dln2 dln3; tail: df = du, dcao = dt); returns -1 for a bad field.  lrce_dec_step_field(kind, -1, 0, B, S, L) = total. */
+int64_t lrce_dec_step_field(int kind, int field, int layer, int B, int S, int n_layers);
+int64_t lrce_dec_step_ws_elems(void);
+int64_t lrce_dec_step_counter_words(void);
+int lrce_dec_step_fwd(const LrceDecStep* args, void* stream);
+int lrce_dec_step_bwd(const LrceDecStep* args, void* stream);
+/* zero the counter block and the status words (after a timeout: status[0] != 0) */
+int lrce_dec_step_reset(uint32_t* counters, uint32_t* status, void* stream);
+/* workgroups of one launch for B rows (12 x min(B, 10)) */
+int lrce_dec_step_grid(int B);
+
 /* Debug: phase timestamps (s_memrealtime, 100 MHz) of the four fused block kernels (k = sa_fwd, ca_fwd,
  * ca_bwd, sa_bwd) into buf[(k * 1024 + workgroup) * 16 + mark] (device memory, 4 * 1024 * 16 uint64);
  * NULL turns it off (the default).  tools/decoder_trace.py reads it. */

@@ -123,21 +123,25 @@ def test_fusion_backward_matches_oracle(task, L, ncls, B):
         assert rel(named[k].grad, sd["fusion_model." + k].grad) < 3e-2, k
 
 
+@pytest.mark.parametrize("mode", ["step", "blocks"])
 @pytest.mark.parametrize("task,L,ncls,B,drop", [("oe", 32, 1000, 3, 0.1), ("oe", 32, 1000, 2, 0.0), ("mc", 40, 1, 2, 0.1),
-                                                 ("mcsim", 40, 1, 2, 0.1)])
-def test_fused_decoder_blocks_match_unfused(task, L, ncls, B, drop, monkeypatch):
-    """The per-head fused attention blocks of the recurrent decoder (csrc/decoder.hip: one launch per
-    block, forward and backward) against the unfused launches (lrce_gemm_ln / lrce_mha / lrce_gemm) on
-    the same inputs, in train mode with dropout on: both draw the same masks, so logits and every
-    parameter / input gradient must agree to f32 rounding (different summation order only)."""
+                                                 ("mcsim", 40, 1, 2, 0.1), ("oe", 32, 1000, 12, 0.1)])
+def test_fused_decoder_blocks_match_unfused(task, L, ncls, B, drop, mode, monkeypatch):
+    """The fused recurrent decoder — "step": one persistent launch per recurrent step and direction
+    (csrc/decoder_step.hip), "blocks": one launch per attention block (csrc/decoder.hip) — against the
+    unfused launches (lrce_gemm_ln / lrce_mha / lrce_gemm) on the same inputs, in train mode with
+    dropout on: all draw the same masks, so logits and every parameter / input gradient must agree to
+    f32 rounding (different summation order only).  B = 12 > 10 rows: the step kernel's workgroups
+    take two rows each."""
     from lrce.models.fusionv3 import LRCEOpenEnded, LRCEMultipleChoice, LRCEMultipleChoiceSim
+    from lrce import kernels as K
     cls = {"oe": LRCEOpenEnded, "mc": LRCEMultipleChoice, "mcsim": LRCEMultipleChoiceSim}[task]
     torch.manual_seed(3)
     m = cls(768, ncls, drop, (7, 7), 1024, 5, [3], L).cuda().train()
     vf = torch.randn(B, 3, 3, 49, 1024, device="cuda")
     tf = torch.randn(B, 5, L, 768, device="cuda") if task != "oe" else torch.randn(B, L, 768, device="cuda")
     runs = []
-    for fused in ("0", "1"):
+    for fused in ("0", mode):
         monkeypatch.setenv("LRCE_DEC_FUSED", fused)
         m.zero_grad(set_to_none=True)
         vg, tg = vf.clone().requires_grad_(True), tf.clone().requires_grad_(True)
@@ -146,13 +150,14 @@ def test_fused_decoder_blocks_match_unfused(task, L, ncls, B, drop, monkeypatch)
         R = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).cuda()
         (y.float() * R).sum().backward()
         torch.cuda.synchronize()
+        assert K.dec_step_status("cuda") == 0
         runs.append((y.detach().float().clone(), vg.grad.clone(), tg.grad.clone(),
                      {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}))
     (y0, v0, t0, g0), (y1, v1, t1, g1) = runs
     assert rel(y1, y0) < 1e-4
     # the memory side (dK / dV -> bf16 -> the K/V projection's dX and dW, the embeddings) and linear1
-    # (its saved pre-activation is bf16, so dGELU sees it rounded) pass through one bf16 rounding: f32
-    # differences in the last bits flip single bf16 roundings (2^-8 relative)
+    # (the unfused path's saved pre-activation is bf16, so dGELU sees it rounded) pass through one bf16
+    # rounding: f32 differences in the last bits flip single bf16 roundings (2^-8 relative)
     assert rel(v1, v0) < 5e-3 and rel(t1, t0) < 5e-3
     assert g0.keys() == g1.keys()
     query_side = ("self_attn.", "multihead_attn.out_proj", "linear2", "norm1", "norm2", "norm3",

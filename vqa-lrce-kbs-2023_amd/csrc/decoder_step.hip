@@ -1,0 +1,1190 @@
+// The recurrent LRCE decoder step as ONE persistent launch per recurrent step and direction
+// (FusionTransformer.forward's clip loop, fusionv3.py:43-49, over the 12 nn.TransformerDecoderLayer of
+// fusionv3.py:8-17: d_model 768, 12 heads x 64, FFN 3072 GELU, post-norm, eps 1e-12) on gfx950.
+//
+// Why: the step is a chain of M = B (10..64) row linears — 36 layer-steps, each four dependent
+// launches of ~10-17 us on the per-block path (decoder.hip + the skinny FFN GEMMs), the chip mostly
+// idle.  Here 12 x R workgroups (R = min(B, 10) row groups, one per CU: the LDS image of a weight
+// slice keeps one per CU) stay resident for the whole step and hand rows to each other inside the
+// launch, so nothing waits for a kernel boundary and every phase issues its weight loads BEFORE it
+// waits for its input rows (the weights do not depend on them).
+//
+// Per layer l (forward):
+//   A  (head h, row b):  [x3p_{l-1} = x2_{l-1} + drop(sum_j P_j + b2) for columns h*64..h*64+63 (the FFN
+//                        partials of the previous layer, summed in slice order)] -> x0 = LN3_{l-1}(x3p)
+//                        -> v_h -> head dropout -> W_o[:, h] v_h partial -> the last of the 12 heads of
+//                        row b sums them: x1p = x0 + drop(. + b_o)              (as dec_sa_fwd)
+//   B  (head h, row b):  x1 = LN1(x1p) -> q_h -> attention over the step's memory keys -> W_oc[:, h] ctx_h
+//                        partial -> last head: x2p = x1 + drop(. + b_oc)         (as dec_ca_fwd)
+//   C  (FFN slice j of 32 hidden units, ALL rows): x2 = LN2(x2p) -> pre = W1[j] x2 + b1 -> gd =
+//                        drop(GELU(pre)) -> P_j = W2[:, j] gd (partial of linear2, written to a slab)
+// then the step tail: x3 = LN3(x3p_11), tsum = x3 + s, s' = drop(LN_f(tsum)).  The backward mirrors it:
+//   tail: du = drop'(ds), dt = LN_f'(du) = d x3 of layer 11;  per layer (11 .. 0):
+//   FB (FFN slice j, all rows): dx3p = LN3'(dx3), df = drop'(dx3p), dgp_j = drop'(W2[:, j]^T df) gelu'(pre),
+//                        Q_j = W1[j]^T dgp_j (partial of dx2)
+//   CB (head h, row b):  dx2 = dx3p + sum_j Q_j (columns h*64..) -> LN2' -> ... (as dec_ca_bwd) -> dx1
+//   SB (head h, row b):  LN1' -> ... (as dec_sa_bwd) -> dx0 = d x3 of layer l-1 (or, l = 0, ds_in of the
+//                        previous step: dx0 + dt).
+//
+// Hand-offs (MI355X_MICROARCH.md "Valid forms", first row of the sc1 hand-off table): every handed-off
+// byte is stored write-through (agent-scope relaxed atomic stores / buffer stores with the sc1 bit),
+// every storing wave drains with s_waitcnt vmcnt(0), a workgroup barrier follows, and ONE lane adds to
+// an arrival counter; consumers poll that counter from one lane with agent-scope relaxed loads
+// (s_sleep between polls, bounded: after 0.5 s the launch records a timeout in status[0], raises a
+// sticky abort word and every workgroup leaves at its next wait — never a hang), then read EVERY
+// handed-off byte with sc1 loads.  Bytes written by earlier launches (weights, K/V, the forward's
+// saved activations) are read with plain loads.  The counters are per layer and phase, zeroed by the
+// last workgroup to finish (graph-replay safe); after a timeout the host resets them
+// (lrce_dec_step_reset).  Every cross-workgroup sum is taken in a fixed order: deterministic.
+//
+// Residency: all 12 R workgroups must be resident at once (they wait for each other).  R <= 10 keeps
+// the grid at <= 120 workgroups of one per CU, so even two such launches (two processes sharing a
+// GPU) fit on the 256 CUs together.
+#include "common.h"
+#include "decoder_util.h"
+#include "lrce_capi.h"
+
+namespace {
+
+constexpr int FF = 3072, FS = 32, NF = FF / FS, RMAX = 10, MAXB = LRCE_DEC_MAX_ROWS, RCH = 16;
+constexpr int XP = 100, XROW = 8 * XP;   // padded LDS row of 768: 8 parts of 96 (+4: conflict-free part reads)
+constexpr int NLMAX = LRCE_DEC_LAYERS;
+// counter block (uint32): per layer CL words; then done / abort
+constexpr int C_SL = 0, C_ROWS = 1, C_X3 = 16, C_SA = 16 + MAXB, C_X1 = 16 + 2 * MAXB, C_CA = 16 + 3 * MAXB;
+constexpr int CL = 16 + 4 * MAXB;
+constexpr int C_DONE = NLMAX * CL, C_ABORT = C_DONE + 1, CTR_WORDS = C_DONE + 16;
+constexpr unsigned long long TIMEOUT_TICKS = 50000000ull;   // 0.5 s of s_memrealtime (100 MHz)
+// workspace (f32): two per-head partial slabs [MAXB][12][768], the FFN slice partials [NF][MAXB][768],
+// the backward's dx3p rows [MAXB][768]
+constexpr long long WS_SLAB = (long long)MAXB * H * E;
+constexpr long long WS_P = (long long)NF * MAXB * E;
+constexpr long long WS_ELEMS = 2 * WS_SLAB + WS_P + (long long)MAXB * E;
+
+// ---- arena layout (shared with the host through lrce_dec_step_field)
+constexpr int NFWD = 18, NBWD = 9;
+__host__ __device__ constexpr int fwd_width(int f) {
+  return f <= 8 ? E : f <= 10 ? FF : f == 11 ? H : 1;   // x0 sad x1p x1 q ctx x2p x2 x3p | pre gd | lse | m1 r1 m2 r2 m3 r3
+}
+__host__ __device__ constexpr int bwd_width(int f) { return f == 1 ? FF : E; }   // df dgp dcao dq dsao dsav dln1 dln2 dln3
+__host__ __device__ inline long long field_off(int kind, int f, int l, int B, int S) {
+  const int nf = kind ? NBWD : NFWD;
+  long long pre = 0, tot = 0;
+  for (int i = 0; i < nf; ++i) {
+    const int w = kind ? bwd_width(i) : fwd_width(i);
+    if (i < f) pre += w;
+    tot += w;
+  }
+  const long long block = ((long long)S * B * tot + 63) / 64 * 64;
+  return (long long)l * block + (long long)S * B * pre;
+}
+enum { F_X0 = 0, F_SAD, F_X1P, F_X1, F_Q, F_CTX, F_X2P, F_X2, F_X3P, F_PRE, F_GD, F_LSE, F_M1, F_R1, F_M2, F_R2, F_M3, F_R3 };
+enum { G_DF = 0, G_DGP, G_DCAO, G_DQ, G_DSAO, G_DSAV, G_DLN1, G_DLN2, G_DLN3 };
+
+struct Ar {   // one arena field at (layer, step): row b at base + b * width
+  float* base;
+  int w;
+  __device__ float* row(int b) const { return base + (long long)b * w; }
+};
+__device__ __forceinline__ Ar fwd_field(const LrceDecStep& p, int f, int l, int step) {
+  return Ar{p.acts + field_off(0, f, l, p.B, p.S) + (long long)step * p.B * fwd_width(f), fwd_width(f)};
+}
+__device__ __forceinline__ Ar bwd_field(const LrceDecStep& p, int f, int l, int step) {
+  return Ar{p.grads + field_off(1, f, l, p.B, p.S) + (long long)step * p.B * bwd_width(f), bwd_width(f)};
+}
+
+// ---- write-through hand-off accesses
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFF0, 0x00020000);
+}
+__device__ __forceinline__ float4 ld4_sc1(const float* p) {   // 16 B, sc1 (L1 bypass): a handed-off row
+  const uint4 u = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(p), 0, 0, 16));
+  return __builtin_bit_cast(float4, u);
+}
+__device__ __forceinline__ void st4_sc1(float* p, float4 v) {   // 16 B, sc1 (write-through)
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                         rsrc_of(p), 0, 0, 16);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// every storing wave drains its write-through stores, the workgroup meets, one lane adds `n`
+__device__ __forceinline__ void wg_arrive(unsigned* ctr, unsigned n = 1) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane polls *w >= target (relaxed agent loads, s_sleep), the workgroup meets (LDS-only barrier:
+// the weight loads in flight are not waited for).  false: the launch is aborting (timeout here or
+// elsewhere) — the caller leaves.
+__device__ bool wg_wait(unsigned* w, unsigned target, const LrceDecStep& p, unsigned code, unsigned* ok_word) {
+  if (threadIdx.x == 0) {
+    unsigned ok = 1;
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      unsigned* abort_w = p.counters + C_ABORT;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > TIMEOUT_TICKS) {
+          __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(p.status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+      }
+    }
+    *ok_word = ok;
+  }
+  lds_barrier();
+  const bool ok = *ok_word != 0;
+  lds_barrier();
+  return ok;
+}
+
+// the last workgroup to finish zeroes the counter block (ready for the next launch / graph replay)
+__device__ void finish(const LrceDecStep& p, unsigned* last_word) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *last_word = __hip_atomic_fetch_add(p.counters + C_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!*last_word) return;
+  for (int i = threadIdx.x; i < CTR_WORDS; i += NT) __hip_atomic_store(p.counters + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned* ctr(const LrceDecStep& p, int l, int k) { return p.counters + l * CL + k; }
+__device__ __forceinline__ uint64_t layer_seed(const LrceDecStep& p, int l) {
+  return p.seed + 64ull * (uint64_t)(p.step * p.n_layers + l);
+}
+__device__ __forceinline__ uint64_t tail_seed(const LrceDecStep& p) { return p.seed + 7ull + 64000ull * (uint64_t)(p.step + 1); }
+
+__device__ __forceinline__ KvP kv_of(const LrceDecStep& p, int l) {
+  KvP k;
+  k.k1 = reinterpret_cast<const bf16*>(p.kv_video) + l * p.kv_video_lstride + (long long)p.step * 150 * 2 * E;
+  k.stride1 = (long long)p.S * 150 * 2 * E;
+  k.ld1 = 2 * E;
+  k.bdiv1 = p.nmc;
+  k.lk1 = 150;
+  k.k2 = p.lt ? reinterpret_cast<const bf16*>(p.kv_text) + l * p.kv_text_lstride : nullptr;
+  k.stride2 = (long long)p.lt * 2 * E;
+  k.ld2 = 2 * E;
+  k.bdiv2 = 1;
+  k.lk2 = p.lt;
+  k.v_off = E;
+  return k;
+}
+
+// ------------------------------------------------------------------------------------ LDS images
+struct SaL {                      // self-attention block (forward and backward)
+  f16 wo[E * D];
+  float x0[E];
+  float pp[4][16 * 64];
+  alignas(16) float v[D];
+  float part[E];
+  float dx1p[E];
+  float dsao[E];
+  float red64[4][D];
+  float acc[4][E];
+  float red2[4];
+  unsigned last;
+};
+struct CaL {                      // cross-attention block: forward and backward images share the tail
+  f16 wo[E * D];
+  bf16 vimg[MAXK * D];
+  union {
+    struct {                      // forward
+      float x1[E];
+      float pp[4][16 * 64];
+      float q[D];
+      float ps[MAXK + 64];
+      float opart[4][D];
+      alignas(16) float ctx[D];
+      float part[E];
+    } f;
+    struct {                      // backward
+      union {
+        bf16 kimg[MAXK * D];
+        float acc[4][E];
+      };
+      float dx2p[E];
+      float dcao[E];
+      float red64[4][D];
+      float dctx[D];
+      float dq[D];
+      float q[D];
+      float ps[MAXK + 64];
+      float dss[MAXK + 64];
+    } b;
+  };
+  float red2[4];
+  unsigned last;
+};
+struct FfL {                      // FFN slices over all rows
+  alignas(16) float x[RCH * XROW];
+  alignas(16) float hb[RCH][FS];
+  f16 w2s[E * FS];                // backward: the W2 column slice [768][32]
+};
+struct RedL {
+  float4 red[16][16];
+};
+union StepLds {
+  SaL sa;
+  CaL ca;
+  FfL ff;
+  RedL rd;
+};
+
+// ---------------------------------------------------------------------------- FFN partial reduce
+// out[b][h*64 + c] for c < 64 = base[b][..] + epi(sum_j P[j][b][..]) over the NF slices in slice
+// order (16 groups of 6, then the groups in order); fwd: base = x2, epi = drop(. + b2, seed5); bwd:
+// base = dx3p, epi = identity.  All of P / base are handed-off rows: sc1 loads; out stored sc1.
+__device__ void slice_reduce(const float* P, int b, int h, const float* bias, float drop_p, uint64_t seed, const float* base_row,
+                             float* out_row, RedL& L) {
+  const int t = threadIdx.x, q = t & 15, g = t >> 4;
+  const int col = h * D + 4 * q;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 v[NF / 16];
+#pragma unroll
+  for (int i = 0; i < NF / 16; ++i) v[i] = ld4_sc1(P + ((long long)(g + 16 * i) * MAXB + b) * E + col);
+#pragma unroll
+  for (int i = 0; i < NF / 16; ++i) { s.x += v[i].x; s.y += v[i].y; s.z += v[i].z; s.w += v[i].w; }
+  L.red[g][q] = s;
+  lds_barrier();
+  if (t < 16) {
+    float4 a = L.red[0][q];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) { const float4 r = L.red[i][q]; a.x += r.x; a.y += r.y; a.z += r.z; a.w += r.w; }
+    if (bias) {
+      const float4 bb = *reinterpret_cast<const float4*>(bias + col);
+      a = make_float4(a.x + bb.x, a.y + bb.y, a.z + bb.z, a.w + bb.w);
+      if (drop_p > 0.f) {
+        const long long e = (long long)b * E + col;
+        const float4 u = lrce_uniform4(seed, (uint64_t)e >> 2);
+        const float k = 1.0f - drop_p;
+        a.x = u.x >= drop_p ? a.x / k : 0.f; a.y = u.y >= drop_p ? a.y / k : 0.f;
+        a.z = u.z >= drop_p ? a.z / k : 0.f; a.w = u.w >= drop_p ? a.w / k : 0.f;
+      }
+    }
+    const float4 r = ld4_sc1(base_row + col);
+    st4_sc1(out_row + col, make_float4(r.x + a.x, r.y + a.y, r.z + a.z, r.w + a.w));
+  }
+  lds_barrier();
+}
+
+// ------------------------------------------------------------------- forward: self-attention row
+// x0 (LDS) is ready; v_h -> head dropout -> partial -> the last head of row b writes x1p (sc1) and
+// raises the row flag.  wr: W_v[h] rows (registers), L.wo: the W_o slice (DMA'd; waited for here)
+__device__ void sa_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint4 (&wr)[NRI], float bvv, SaL& L,
+                           uint64_t seed0, uint64_t seed1, bool wait_dma) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const LrceDecLayerW& W = p.layer[l];
+  rows_gemv(wr, L.x0, L.pp[wave], L.v + wave * WROWS, lane);
+  lds_barrier();
+  if (t < D) {
+    float v = L.v[t] + bvv;
+    if (p.drop_p > 0.f) v = drop1(v, p.drop_p, seed0, ((long long)b * E + h * D + t) / D);
+    L.v[t] = v;
+    fwd_field(p, F_SAD, l, p.step).row(b)[h * D + t] = v;
+  }
+  if (wait_dma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  slice_gemv(L.wo, L.v, L.part, t);
+  lds_barrier();
+  if (!publish_partial(L.part, p.ws, ctr(p, l, C_SA), b, h, t, &L.last)) return;
+  float* x1p = fwd_field(p, F_X1P, l, p.step).row(b);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    float y = gather_partials(p.ws, b, n) + W.bo[n];
+    if (p.drop_p > 0.f) y = drop1(y, p.drop_p, seed1, (long long)b * E + n);
+    st_sc1(x1p + n, L.x0[n] + y);
+  }
+  wg_arrive(ctr(p, l, C_X1) + b);
+}
+
+// ------------------------------------------------------------------ forward: cross-attention row
+__device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint4 (&wr)[NRI], float bqv, CaL& L,
+                           uint64_t seed2, uint64_t seed3, bool first_row) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const LrceDecLayerW& W = p.layer[l];
+  const KvP kv = kv_of(p, l);
+  const int Lk = kv.lk1 + kv.lk2;
+  float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
+  const float* x1p = fwd_field(p, F_X1P, l, p.step).row(b);
+  if (t < E / 4) {
+    xr = ld4_sc1(x1p + 4 * t);
+    gg = *reinterpret_cast<const float4*>(W.g1 + 4 * t);
+    be = *reinterpret_cast<const float4*>(W.be1 + 4 * t);
+  }
+  const float s1l = row_sum_local(xr, t);
+  // key row of thread t (registers), the head's V rows (LDS DMA)
+  const bool live = t < Lk;
+  const KvRows kvr = kv_rows(kv, b, h);
+  uint4 kr[8];
+  {
+    const bf16* kp = kv_row(kvr, live ? t : 0);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) kr[c] = *reinterpret_cast<const uint4*>(kp + 8 * c);
+  }
+  {
+    const uint32_t vb = dec_lds_addr(L.vimg);
+    for (int ins = wave; ins * 8 < Lk; ins += 4) {
+      const int r = ins * 8 + (lane >> 3), j = min(r, Lk - 1);
+      const bf16* vp = kv_row(kvr, j) + kv.v_off + (((lane & 7) ^ (r & 7)) << 3);
+      dec_glds_p(vp, vb + (uint32_t)ins * 1024u);
+    }
+  }
+  float mu, rs;
+  ln_row_fwd(xr, s1l, gg, be, p.eps, L.f.x1, L.red2, t, lane, wave, mu, rs);
+  if (h == 0) {
+    if (t < E / 4) *reinterpret_cast<float4*>(fwd_field(p, F_X1, l, p.step).row(b) + 4 * t) = *reinterpret_cast<const float4*>(L.f.x1 + 4 * t);
+    if (t == 0) {
+      fwd_field(p, F_M1, l, p.step).row(b)[0] = mu;
+      fwd_field(p, F_R1, l, p.step).row(b)[0] = rs;
+    }
+  }
+  lds_barrier();
+  rows_gemv(wr, L.f.x1, L.f.pp[wave], L.f.q + wave * WROWS, lane);
+  lds_barrier();
+  if (t < D) {
+    const float q = L.f.q[t] + bqv;
+    fwd_field(p, F_Q, l, p.step).row(b)[h * D + t] = q;
+    L.f.q[t] = q * 0.125f;
+  }
+  lds_barrier();
+  float sc = 0.f;
+  if (live) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const unsigned w4[4] = {kr[c].x, kr[c].y, kr[c].z, kr[c].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sc += bfbits2f((unsigned short)(w4[e] & 0xFFFFu)) * L.f.q[8 * c + 2 * e];
+        sc += bfbits2f((unsigned short)(w4[e] >> 16)) * L.f.q[8 * c + 2 * e + 1];
+      }
+    }
+  }
+  const float m = block_max4(live ? sc : -1.0e30f, L.red2, lane, wave);
+  const float pe = live ? __expf(sc - m) : 0.f;
+  const float s = block_sum4(pe, L.red2, lane, wave);
+  float pf = pe;
+  if (live && p.drop_p > 0.f) pf = drop1(pe, p.drop_p, seed2, ((long long)b * H + h) * Lk + t);
+  L.f.ps[t] = live ? pf : 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // V rows (and, first row, the W_oc slice) have landed
+  lds_barrier();
+  {
+    const int c = t & 7, kg = t >> 3;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int j = kg; j < Lk; j += 32) {
+      float vf[8];
+      unpack8bf(*reinterpret_cast<const uint4*>(L.vimg + kv_swz(j, c)), vf);
+      const float pj = L.f.ps[j];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = fmaf(pj, vf[e], a[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] += dpp_f<0x128>(a[e]);
+      a[e] += __shfl_xor(a[e], 16, 64);
+      a[e] += __shfl_xor(a[e], 32, 64);
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) L.f.opart[wave][c * 8 + e] = a[e];
+    }
+  }
+  lds_barrier();
+  if (t < D) {
+    const float c = ((L.f.opart[0][t] + L.f.opart[1][t]) + (L.f.opart[2][t] + L.f.opart[3][t])) / s;
+    L.f.ctx[t] = c;
+    fwd_field(p, F_CTX, l, p.step).row(b)[h * D + t] = c;
+    if (t == 0) fwd_field(p, F_LSE, l, p.step).row(b)[h] = m + __logf(s);
+  }
+  lds_barrier();
+  slice_gemv(L.wo, L.f.ctx, L.f.part, t);
+  lds_barrier();
+  if (!publish_partial(L.f.part, p.ws + WS_SLAB, ctr(p, l, C_CA), b, h, t, &L.last)) return;
+  float* x2p = fwd_field(p, F_X2P, l, p.step).row(b);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    float y = gather_partials(p.ws + WS_SLAB, b, n) + W.boc[n];
+    if (p.drop_p > 0.f) y = drop1(y, p.drop_p, seed3, (long long)b * E + n);
+    st_sc1(x2p + n, L.f.x1[n] + y);
+  }
+  wg_arrive(ctr(p, l, C_ROWS));
+}
+
+// ------------------------------------------------------------------------ FFN: rows into LDS
+// rows c0 .. c0+nr-1 of a handed-off [B][768] f32 field (sc1) into the padded image L.x
+__device__ __forceinline__ void rows_to_lds(const float* src, int c0, int nr, FfL& L) {
+  for (int i = threadIdx.x; i < nr * (E / 4); i += NT) {
+    const int rr = i / (E / 4), k = (i % (E / 4)) * 4;
+    const float4 v = ld4_sc1(src + (long long)(c0 + rr) * E + k);
+    *reinterpret_cast<float4*>(L.x + rr * XROW + (k / 96) * XP + (k % 96)) = v;
+  }
+}
+// element k of padded row rr
+__device__ __forceinline__ float* xat(FfL& L, int rr, int k) { return L.x + rr * XROW + (k / 96) * XP + (k % 96); }
+
+// wave-per-row LayerNorm (forward) of the image rows in place; lane owns k = 12 lane .. 12 lane + 11
+__device__ void ln_rows_fwd(FfL& L, int nr, const float* g, const float* be, float eps, float* mean_out, float* rstd_out,
+                            float* y_rows /* sc1-stored copy or NULL */, int c0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int rr = wave; rr < nr; rr += 4) {
+    float* xp = xat(L, rr, 12 * lane);
+    float4 v[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) v[i] = *reinterpret_cast<float4*>(xp + 4 * i);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    const float mu = wave_sum(s) * (1.0f / E);
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float4 d = make_float4(v[i].x - mu, v[i].y - mu, v[i].z - mu, v[i].w - mu);
+      s2 += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+    }
+    const float rs = rsqrtf(wave_sum(s2) * (1.0f / E) + eps);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int k = 12 * lane + 4 * i;
+      const float4 gg = *reinterpret_cast<const float4*>(g + k), bb = *reinterpret_cast<const float4*>(be + k);
+      const float4 y = make_float4((v[i].x - mu) * rs * gg.x + bb.x, (v[i].y - mu) * rs * gg.y + bb.y,
+                                   (v[i].z - mu) * rs * gg.z + bb.z, (v[i].w - mu) * rs * gg.w + bb.w);
+      *reinterpret_cast<float4*>(xp + 4 * i) = y;
+      if (y_rows) st4_sc1(y_rows + (long long)(c0 + rr) * E + k, y);
+    }
+    if (lane == 0 && mean_out) {
+      mean_out[c0 + rr] = mu;
+      rstd_out[c0 + rr] = rs;
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- forward: FFN slice j
+__device__ void ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4) {
+  const int t = threadIdx.x, c = t >> 3, part = t & 7;
+  const LrceDecLayerW& W = p.layer[l];
+  const f16* w1 = reinterpret_cast<const f16*>(W.w1);
+  const f16* w2 = reinterpret_cast<const f16*>(W.w2);
+  // W1 rows j*32 + c, k in [96 part, 96 part + 96) -> 12 x 16 B; W2 rows 4t..4t+3 (t < 192), columns j*32 .. +32
+  uint4 w1r[12], w2r[16];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) w1r[i] = *reinterpret_cast<const uint4*>(w1 + (long long)(j * FS + c) * E + part * 96 + 8 * i);
+  if (t < E / 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w2r[q * 4 + u] = *reinterpret_cast<const uint4*>(w2 + (long long)(4 * t + q) * FF + j * FS + 8 * u);
+  }
+  const float b1v = W.b1[j * FS + c];
+  Ar pre = fwd_field(p, F_PRE, l, p.step), gd = fwd_field(p, F_GD, l, p.step);
+  const float* x2p = fwd_field(p, F_X2P, l, p.step).base;
+  for (int c0 = 0; c0 < p.B; c0 += RCH) {
+    const int nr = min(RCH, p.B - c0);
+    lds_barrier();   // the previous chunk's image is consumed
+    rows_to_lds(x2p, c0, nr, L);
+    lds_barrier();
+    Ar x2 = fwd_field(p, F_X2, l, p.step);
+    const bool owner = j == 0;   // slice 0's workgroup materialises x2 (read back by the next layer's reducers) and its stats
+    ln_rows_fwd(L, nr, W.g2, W.be2, p.eps, owner ? fwd_field(p, F_M2, l, p.step).base : nullptr,
+                owner ? fwd_field(p, F_R2, l, p.step).base : nullptr, owner ? x2.base : nullptr, c0);
+    lds_barrier();
+    // linear1 slice + GELU + dropout
+    for (int rr = 0; rr < nr; ++rr) {
+      float acc = 0.f;
+      const float* xp = L.x + rr * XROW + part * XP;
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        float wf[8];
+        unpack8(w1r[i], wf);
+        acc += dot8(wf, xp + 8 * i);
+      }
+      acc = sum8(acc);
+      if (part == 0) {
+        const int b = c0 + rr, col = j * FS + c;
+        const float hv = acc + b1v;
+        pre.row(b)[col] = hv;
+        float gv = gelu_f(hv);
+        if (p.drop_p > 0.f) gv = drop1(gv, p.drop_p, seed4, (long long)b * FF + col);
+        gd.row(b)[col] = gv;
+        L.hb[rr][c] = gv;
+      }
+    }
+    lds_barrier();
+    // linear2 partial of this slice: P_j[b][4t .. 4t+3]
+    if (t < E / 4) {
+      float* Pj = p.ws + 2 * WS_SLAB + (long long)j * MAXB * E;
+      for (int rr = 0; rr < nr; ++rr) {
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 h0 = *reinterpret_cast<const float4*>(&L.hb[rr][8 * u]);
+          const float4 h1 = *reinterpret_cast<const float4*>(&L.hb[rr][8 * u + 4]);
+          const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float wf[8];
+            unpack8(w2r[q * 4 + u], wf);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[q] = fmaf(wf[e], hv[e], o[q]);
+          }
+        }
+        st4_sc1(Pj + (long long)(c0 + rr) * E + 4 * t, make_float4(o[0], o[1], o[2], o[3]));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- forward kernel
+__global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, const uint64_t* rng_off) {
+  __shared__ __attribute__((aligned(16))) StepLds U;
+  __shared__ unsigned ok_word;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int G = gridDim.x, R = G / H;
+  const int h = blockIdx.x % H, r = blockIdx.x / H;
+  const uint64_t roff = rng_off_now(rng_off);
+  const int L_ = p.n_layers;
+  for (int l = 0; l < L_; ++l) {
+    const LrceDecLayerW& W = p.layer[l];
+    const uint64_t sl = layer_seed(p, l) + roff;
+    // ---- A: self-attention block (after reducing the previous layer's FFN partials)
+    uint4 wr[NRI];
+    rows_load(reinterpret_cast<const f16*>(W.wv), h * D + wave * WROWS, lane, wr);
+    const float bvv = t < D ? W.bv[h * D + t] : 0.f;
+    if (l > 0) {
+      if (!wg_wait(ctr(p, l - 1, C_SL), NF, p, 0x100 + l, &ok_word)) return;
+      const LrceDecLayerW& Wp = p.layer[l - 1];
+      for (int b = r; b < p.B; b += R)
+        slice_reduce(p.ws + 2 * WS_SLAB, b, h, Wp.b2, p.drop_p, layer_seed(p, l - 1) + 5 + roff,
+                     fwd_field(p, F_X2, l - 1, p.step).row(b), fwd_field(p, F_X3P, l - 1, p.step).row(b), U.rd);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0)
+        for (int b = r; b < p.B; b += R) __hip_atomic_fetch_add(ctr(p, l - 1, C_X3) + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    SaL& S = U.sa;
+    lds_barrier();
+    slice_dma(reinterpret_cast<const f16*>(W.wo), h, S.wo, wave, lane);
+    bool first = true;
+    for (int b = r; b < p.B; b += R) {
+      if (l > 0) {
+        if (!wg_wait(ctr(p, l - 1, C_X3) + b, H, p, 0x200 + l, &ok_word)) return;
+        const LrceDecLayerW& Wp = p.layer[l - 1];
+        float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
+        if (t < E / 4) {
+          xr = ld4_sc1(fwd_field(p, F_X3P, l - 1, p.step).row(b) + 4 * t);
+          gg = *reinterpret_cast<const float4*>(Wp.g3 + 4 * t);
+          be = *reinterpret_cast<const float4*>(Wp.be3 + 4 * t);
+        }
+        float mu, rs;
+        ln_row_fwd(xr, row_sum_local(xr, t), gg, be, p.eps, S.x0, S.red2, t, lane, wave, mu, rs);
+        if (h == 0) {
+          if (t < E / 4)
+            *reinterpret_cast<float4*>(fwd_field(p, F_X0, l, p.step).row(b) + 4 * t) = *reinterpret_cast<const float4*>(S.x0 + 4 * t);
+          if (t == 0) {
+            fwd_field(p, F_M3, l - 1, p.step).row(b)[0] = mu;
+            fwd_field(p, F_R3, l - 1, p.step).row(b)[0] = rs;
+          }
+        }
+      } else if (t < E / 4) {
+        *reinterpret_cast<float4*>(S.x0 + 4 * t) = *reinterpret_cast<const float4*>(fwd_field(p, F_X0, 0, p.step).row(b) + 4 * t);
+      }
+      lds_barrier();
+      sa_fwd_row(p, l, b, h, wr, bvv, S, sl, sl + 1, first);
+      first = false;
+      lds_barrier();
+    }
+    // ---- B: cross-attention block
+    CaL& C = U.ca;
+    lds_barrier();
+    rows_load(reinterpret_cast<const f16*>(W.wq), h * D + wave * WROWS, lane, wr);
+    const float bqv = t < D ? W.bq[h * D + t] : 0.f;
+    slice_dma(reinterpret_cast<const f16*>(W.woc), h, C.wo, wave, lane);
+    first = true;
+    for (int b = r; b < p.B; b += R) {
+      if (!wg_wait(ctr(p, l, C_X1) + b, 1, p, 0x300 + l, &ok_word)) return;
+      ca_fwd_row(p, l, b, h, wr, bqv, C, sl + 2, sl + 3, first);
+      first = false;
+      lds_barrier();
+    }
+    // ---- C: FFN slices over all rows
+    bool waited = false;
+    for (int j = blockIdx.x; j < NF; j += G) {
+      if (!waited) {
+        if (!wg_wait(ctr(p, l, C_ROWS), p.B, p, 0x400 + l, &ok_word)) return;
+        waited = true;
+      }
+      ffn_fwd_slice(p, l, j, U.ff, sl + 4);
+      wg_arrive(ctr(p, l, C_SL));
+    }
+  }
+  // ---- step tail: x3p of the last layer, then (head 0) x3 = LN3, tsum = x3 + s, s' = drop(LN_f(tsum))
+  const int Ll = L_ - 1;
+  if (!wg_wait(ctr(p, Ll, C_SL), NF, p, 0x500, &ok_word)) return;
+  for (int b = r; b < p.B; b += R)
+    slice_reduce(p.ws + 2 * WS_SLAB, b, h, p.layer[Ll].b2, p.drop_p, layer_seed(p, Ll) + 5 + roff,
+                 fwd_field(p, F_X2, Ll, p.step).row(b), fwd_field(p, F_X3P, Ll, p.step).row(b), U.rd);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0)
+    for (int b = r; b < p.B; b += R) __hip_atomic_fetch_add(ctr(p, Ll, C_X3) + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (h == 0) {
+    SaL& S = U.sa;
+    const uint64_t st = tail_seed(p) + roff;
+    for (int b = r; b < p.B; b += R) {
+      if (!wg_wait(ctr(p, Ll, C_X3) + b, H, p, 0x600, &ok_word)) return;
+      float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
+      if (t < E / 4) {
+        xr = ld4_sc1(fwd_field(p, F_X3P, Ll, p.step).row(b) + 4 * t);
+        gg = *reinterpret_cast<const float4*>(p.layer[Ll].g3 + 4 * t);
+        be = *reinterpret_cast<const float4*>(p.layer[Ll].be3 + 4 * t);
+      }
+      float mu, rs;
+      ln_row_fwd(xr, row_sum_local(xr, t), gg, be, p.eps, S.x0, S.red2, t, lane, wave, mu, rs);
+      if (t == 0) {
+        fwd_field(p, F_M3, Ll, p.step).row(b)[0] = mu;
+        fwd_field(p, F_R3, Ll, p.step).row(b)[0] = rs;
+      }
+      lds_barrier();
+      float4 ts = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (t < E / 4) {
+        const float4 sv = *reinterpret_cast<const float4*>(fwd_field(p, F_X0, 0, p.step).row(b) + 4 * t);
+        const float4 x3 = *reinterpret_cast<const float4*>(S.x0 + 4 * t);
+        ts = make_float4(x3.x + sv.x, x3.y + sv.y, x3.z + sv.z, x3.w + sv.w);
+        *reinterpret_cast<float4*>(fwd_field(p, F_X0, L_, p.step).row(b) + 4 * t) = ts;   // tsum
+        gg = *reinterpret_cast<const float4*>(p.gf + 4 * t);
+        be = *reinterpret_cast<const float4*>(p.bf + 4 * t);
+      }
+      lds_barrier();
+      ln_row_fwd(ts, row_sum_local(ts, t), gg, be, p.eps, S.part, S.red2, t, lane, wave, mu, rs);
+      if (t == 0) {
+        fwd_field(p, F_M1, L_, p.step).row(b)[0] = mu;
+        fwd_field(p, F_R1, L_, p.step).row(b)[0] = rs;
+      }
+      lds_barrier();
+      float* dst = p.step + 1 < p.S ? fwd_field(p, F_X0, 0, p.step + 1).row(b) : p.s_out + (long long)b * E;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int n = t + 256 * i;
+        float v = S.part[n];
+        if (p.drop_p > 0.f) v = drop1(v, p.drop_p, st, (long long)b * E + n);
+        dst[n] = v;
+      }
+      lds_barrier();
+    }
+  }
+  finish(p, &ok_word);
+}
+
+// =============================================================================== backward
+// ---------------------------------------------------------------- backward: FFN slice j, all rows
+__device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, uint64_t seed5) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, c = t >> 3, part = t & 7;
+  const LrceDecLayerW& W = p.layer[l];
+  const f16* w1 = reinterpret_cast<const f16*>(W.w1);
+  const f16* w2 = reinterpret_cast<const f16*>(W.w2);
+  // W2[:, j*32 .. +32] -> LDS [768][32] (DMA: row n = 4 chunks of 16 B), then thread (c, part) keeps
+  // W2[96 part + e][j*32 + c] (e < 96) as 48 packed halves; W1 rows j*32 + c', columns 4t..4t+3 (t < 192)
+  {
+    const uint32_t base = dec_lds_addr(L.w2s);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const int ins = wave * 12 + i;          // 48 instructions x 1 KB
+      const int n = ins * 16 + (lane >> 2);
+      dec_glds(w2, (uint32_t)(((long long)n * FF + j * FS + (lane & 3) * 8) * 2), base + (uint32_t)ins * 1024u);
+    }
+  }
+  uint2 w1t[FS];
+  if (t < E / 4) {
+#pragma unroll
+    for (int cc = 0; cc < FS; ++cc) w1t[cc] = *reinterpret_cast<const uint2*>(w1 + (long long)(j * FS + cc) * E + 4 * t);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  unsigned w2c[48];
+#pragma unroll
+  for (int e = 0; e < 48; ++e) {
+    const unsigned lo = __builtin_bit_cast(unsigned short, L.w2s[(part * 96 + 2 * e) * FS + c]);
+    const unsigned hi = __builtin_bit_cast(unsigned short, L.w2s[(part * 96 + 2 * e + 1) * FS + c]);
+    w2c[e] = lo | (hi << 16);
+  }
+  const Ar dln3 = bwd_field(p, G_DLN3, l, p.step), df = bwd_field(p, G_DF, l, p.step), dgp = bwd_field(p, G_DGP, l, p.step);
+  const Ar x3p = fwd_field(p, F_X3P, l, p.step), m3 = fwd_field(p, F_M3, l, p.step), r3 = fwd_field(p, F_R3, l, p.step);
+  const Ar pre = fwd_field(p, F_PRE, l, p.step);
+  float* dres = p.ws + 2 * WS_SLAB + WS_P;   // dx3p rows (handed to the reducers)
+  float* Qj = p.ws + 2 * WS_SLAB + (long long)j * MAXB * E;
+  const bool owner = j == 0;
+  for (int c0 = 0; c0 < p.B; c0 += RCH) {
+    const int nr = min(RCH, p.B - c0);
+    lds_barrier();
+    rows_to_lds(dln3.base, c0, nr, L);
+    lds_barrier();
+    // LayerNorm-3 backward per row (wave per row), then the out-dropout backward -> df in the image
+    for (int rr = wave; rr < nr; rr += 4) {
+      const int b = c0 + rr;
+      float* xp = xat(L, rr, 12 * lane);
+      const float mu = m3.row(b)[0], rs = r3.row(b)[0];
+      float4 g[3], xh[3];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int k = 12 * lane + 4 * i;
+        const float4 dy = *reinterpret_cast<const float4*>(xp + 4 * i);
+        const float4 gm = *reinterpret_cast<const float4*>(W.g3 + k);
+        const float4 x = *reinterpret_cast<const float4*>(x3p.row(b) + k);
+        g[i] = make_float4(dy.x * gm.x, dy.y * gm.y, dy.z * gm.z, dy.w * gm.w);
+        xh[i] = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+        s1 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
+        s2 += (g[i].x * xh[i].x + g[i].y * xh[i].y) + (g[i].z * xh[i].z + g[i].w * xh[i].w);
+      }
+      const float mg = wave_sum(s1) * (1.0f / E), mgx = wave_sum(s2) * (1.0f / E);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int k = 12 * lane + 4 * i;
+        float4 d = make_float4(rs * (g[i].x - mg - xh[i].x * mgx), rs * (g[i].y - mg - xh[i].y * mgx),
+                               rs * (g[i].z - mg - xh[i].z * mgx), rs * (g[i].w - mg - xh[i].w * mgx));
+        if (owner) st4_sc1(dres + (long long)b * E + k, d);
+        if (p.drop_p > 0.f) {
+          const float4 u = lrce_uniform4(seed5, ((uint64_t)b * E + k) >> 2);
+          const float kd = 1.0f - p.drop_p;
+          d.x = u.x >= p.drop_p ? d.x / kd : 0.f; d.y = u.y >= p.drop_p ? d.y / kd : 0.f;
+          d.z = u.z >= p.drop_p ? d.z / kd : 0.f; d.w = u.w >= p.drop_p ? d.w / kd : 0.f;
+        }
+        *reinterpret_cast<float4*>(xp + 4 * i) = d;
+        if (owner) *reinterpret_cast<float4*>(df.row(b) + k) = d;
+      }
+    }
+    lds_barrier();
+    // dgp = drop'(W2[:, slice]^T df) gelu'(pre)
+    for (int rr = 0; rr < nr; ++rr) {
+      const float* xp = L.x + rr * XROW + part * XP;
+      float acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 48; ++e) {
+        const float2 x2 = *reinterpret_cast<const float2*>(xp + 2 * e);
+        acc = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(w2c[e] & 0xFFFFu)), x2.x, acc);
+        acc = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(w2c[e] >> 16)), x2.y, acc);
+      }
+      acc = sum8(acc);
+      if (part == 0) {
+        const int b = c0 + rr, col = j * FS + c;
+        float d = acc;
+        if (p.drop_p > 0.f) d = drop1(d, p.drop_p, seed4, (long long)b * FF + col);
+        d *= gelu_grad_f(pre.row(b)[col]);
+        dgp.row(b)[col] = d;
+        L.hb[rr][c] = d;
+      }
+    }
+    lds_barrier();
+    // Q_j = W1[slice]^T dgp: columns 4t .. 4t+3
+    if (t < E / 4) {
+      for (int rr = 0; rr < nr; ++rr) {
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cc = 0; cc < FS; ++cc) {
+          const float dv = L.hb[rr][cc];
+          const uint2 u = w1t[cc];
+          o[0] = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(u.x & 0xFFFFu)), dv, o[0]);
+          o[1] = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(u.x >> 16)), dv, o[1]);
+          o[2] = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(u.y & 0xFFFFu)), dv, o[2]);
+          o[3] = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(u.y >> 16)), dv, o[3]);
+        }
+        st4_sc1(Qj + (long long)(c0 + rr) * E + 4 * t, make_float4(o[0], o[1], o[2], o[3]));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ backward: cross-attention row b
+// dx2 (handed-off row) -> LN2' -> dcao -> dctx -> attention backward (dq, memory dK / dV) -> the last
+// head writes dx1 = dx2p + sum_h W_q[h]^T dq_h and raises the row flag
+__device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, const uint4 (&wr)[NRI], CaL& L, uint64_t seed2,
+                           uint64_t seed3) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const LrceDecLayerW& W = p.layer[l];
+  const KvP kv = kv_of(p, l);
+  const int Lk = kv.lk1 + kv.lk2;
+  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
+  if (t < E / 4) {
+    dy = ld4_sc1(bwd_field(p, G_DLN2, l, p.step).row(b) + 4 * t);
+    xr = *reinterpret_cast<const float4*>(fwd_field(p, F_X2P, l, p.step).row(b) + 4 * t);
+    gm = *reinterpret_cast<const float4*>(W.g2 + 4 * t);
+  }
+  const float mu = fwd_field(p, F_M2, l, p.step).row(b)[0], rs = fwd_field(p, F_R2, l, p.step).row(b)[0];
+  LnBwdLocal lnl = ln_row_bwd_local(dy, xr, gm, mu, rs, t);
+  float qd = 0.f, od = 0.f;
+  if (t < D) {
+    qd = fwd_field(p, F_Q, l, p.step).row(b)[h * D + t];
+    od = fwd_field(p, F_CTX, l, p.step).row(b)[h * D + t];
+  }
+  const float lse = fwd_field(p, F_LSE, l, p.step).row(b)[h];
+  const KvRows kvr = kv_rows(kv, b, h);
+  // text rows' running dK / dV (accumulated over the recurrent steps): read now, added at the end
+  const bool dk2_store = p.step == p.S - 1;
+  float* dk2 = p.lt ? p.dkv_text + l * p.dkv_text_lstride : nullptr;
+  const long long tbase = (long long)b * p.lt * 2 * E + h * D;
+  float4 told[TXI][4];
+#pragma unroll
+  for (int i = 0; i < TXI; ++i) {
+    const int e = t + 256 * i, tj = e >> 3, c = e & 7;
+    told[i][0] = told[i][1] = told[i][2] = told[i][3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tj < kv.lk2 && !dk2_store) {
+      const float* src = dk2 + tbase + (long long)tj * 2 * E + c * 8;
+      told[i][0] = *reinterpret_cast<const float4*>(src);
+      told[i][1] = *reinterpret_cast<const float4*>(src + 4);
+      told[i][2] = *reinterpret_cast<const float4*>(src + E);
+      told[i][3] = *reinterpret_cast<const float4*>(src + E + 4);
+    }
+  }
+  const float4 dx = ln_row_bwd(lnl, rs, L.red2, lane, wave);
+  {
+    const uint32_t kb = dec_lds_addr(L.b.kimg), vb = dec_lds_addr(L.vimg);
+    for (int ins = wave; ins * 8 < Lk; ins += 4) {
+      const int r = ins * 8 + (lane >> 3), j = min(r, Lk - 1);
+      const bf16* kp = kv_row(kvr, j) + (((lane & 7) ^ (r & 7)) << 3);
+      dec_glds_p(kp, kb + (uint32_t)ins * 1024u);
+      dec_glds_p(kp + kv.v_off, vb + (uint32_t)ins * 1024u);
+    }
+  }
+  if (t < E / 4) {
+    *reinterpret_cast<float4*>(L.b.dx2p + 4 * t) = dx;
+    float4 d = dx;
+    if (p.drop_p > 0.f) {
+      const long long e = (long long)b * E + 4 * t;
+      d = make_float4(drop1(dx.x, p.drop_p, seed3, e), drop1(dx.y, p.drop_p, seed3, e + 1), drop1(dx.z, p.drop_p, seed3, e + 2),
+                      drop1(dx.w, p.drop_p, seed3, e + 3));
+    }
+    *reinterpret_cast<float4*>(L.b.dcao + 4 * t) = d;
+    if (h == 0) *reinterpret_cast<float4*>(bwd_field(p, G_DCAO, l, p.step).row(b) + 4 * t) = d;
+  }
+  if (t < D) L.b.q[t] = qd * 0.125f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // K / V rows (and, first row, the W_oc slice) have landed
+  lds_barrier();
+  slice_gemv_t(L.wo, L.b.dcao, &L.b.red64[0][0], wave, lane);
+  lds_barrier();
+  float dod = 0.f;
+  if (t < D) {
+    dod = (L.b.red64[0][t] + L.b.red64[1][t]) + (L.b.red64[2][t] + L.b.red64[3][t]);
+    L.b.dctx[t] = dod;
+  }
+  const float delta = block_sum4(dod * od, L.red2, lane, wave);
+  const bool live = t < Lk;
+  float pf = 0.f, ds = 0.f;
+  if (live) {
+    float sc = 0.f, dp = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint4 ku = *reinterpret_cast<const uint4*>(L.b.kimg + kv_swz(t, c));
+      const uint4 vu = *reinterpret_cast<const uint4*>(L.vimg + kv_swz(t, c));
+      const unsigned k4[4] = {ku.x, ku.y, ku.z, ku.w}, v4[4] = {vu.x, vu.y, vu.z, vu.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sc += bfbits2f((unsigned short)(k4[e] & 0xFFFFu)) * L.b.q[8 * c + 2 * e] +
+              bfbits2f((unsigned short)(k4[e] >> 16)) * L.b.q[8 * c + 2 * e + 1];
+        dp += bfbits2f((unsigned short)(v4[e] & 0xFFFFu)) * L.b.dctx[8 * c + 2 * e] +
+              bfbits2f((unsigned short)(v4[e] >> 16)) * L.b.dctx[8 * c + 2 * e + 1];
+      }
+    }
+    const float pr = __expf(sc - lse);
+    float f = 1.f;
+    if (p.drop_p > 0.f) f = lrce_uniform(seed2, (uint64_t)(((long long)b * H + h) * Lk + t)) >= p.drop_p ? 1.0f / (1.0f - p.drop_p) : 0.f;
+    pf = pr * f;
+    ds = pr * (f * dp - delta);
+  }
+  L.b.ps[t] = pf;
+  L.b.dss[t] = ds;
+  lds_barrier();
+  {
+    float dq0 = 0.f, dq1 = 0.f;
+    int j = wave;
+    for (; j + 4 < Lk; j += 8) {
+      dq0 += L.b.dss[j] * kv_at(L.b.kimg, j, lane);
+      dq1 += L.b.dss[j + 4] * kv_at(L.b.kimg, j + 4, lane);
+    }
+    if (j < Lk) dq0 += L.b.dss[j] * kv_at(L.b.kimg, j, lane);
+    L.b.red64[wave][lane] = dq0 + dq1;
+  }
+  {
+    const long long lvs = l * p.dkv_video_lstride;
+    const long long vbase = (long long)(b / kv.bdiv1) * kv.stride1 + (long long)p.step * 150 * 2 * E + h * D;
+    for (int e = t; e < kv.lk1 * 8; e += 256) {
+      const int j = e >> 3, c = e & 7;
+      const float dsj = L.b.dss[j], pj = L.b.ps[j];
+      float kv8[16];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        kv8[i] = dsj * L.b.q[c * 8 + i];
+        kv8[8 + i] = pj * L.b.dctx[c * 8 + i];
+      }
+      const long long o = lvs + vbase + (long long)j * 2 * E + c * 8;
+      if (p.dkv_video16) {
+        bf16* d16 = reinterpret_cast<bf16*>(p.dkv_video16) + o;
+        bf16x8 k16, v16;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { k16[i] = f2bf(kv8[i]); v16[i] = f2bf(kv8[8 + i]); }
+        *reinterpret_cast<bf16x8*>(d16) = k16;
+        *reinterpret_cast<bf16x8*>(d16 + E) = v16;
+      } else {
+        float* dst = p.dkv_video32 + o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __hip_atomic_fetch_add(dst + i, kv8[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(dst + E + i, kv8[8 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TXI; ++i) {
+      const int e = t + 256 * i, tj = e >> 3, c = e & 7;
+      if (tj < kv.lk2) {
+        const int j = kv.lk1 + tj;
+        const float dsj = L.b.dss[j], pj = L.b.ps[j];
+        const float* qv = L.b.q + c * 8;
+        const float* gv = L.b.dctx + c * 8;
+        float* dst = dk2 + tbase + (long long)tj * 2 * E + c * 8;
+        const float4 a0 = told[i][0], a1 = told[i][1], a2 = told[i][2], a3 = told[i][3];
+        *reinterpret_cast<float4*>(dst) = make_float4(a0.x + dsj * qv[0], a0.y + dsj * qv[1], a0.z + dsj * qv[2], a0.w + dsj * qv[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(a1.x + dsj * qv[4], a1.y + dsj * qv[5], a1.z + dsj * qv[6], a1.w + dsj * qv[7]);
+        *reinterpret_cast<float4*>(dst + E) = make_float4(a2.x + pj * gv[0], a2.y + pj * gv[1], a2.z + pj * gv[2], a2.w + pj * gv[3]);
+        *reinterpret_cast<float4*>(dst + E + 4) = make_float4(a3.x + pj * gv[4], a3.y + pj * gv[5], a3.z + pj * gv[6], a3.w + pj * gv[7]);
+      }
+    }
+  }
+  lds_barrier();
+  if (t < D) {
+    const float dq = ((L.b.red64[0][t] + L.b.red64[1][t]) + (L.b.red64[2][t] + L.b.red64[3][t])) * 0.125f;
+    L.b.dq[t] = dq;
+    bwd_field(p, G_DQ, l, p.step).row(b)[h * D + t] = dq;
+  }
+  lds_barrier();
+  rows_gemv_t(wr, L.b.dq + wave * WROWS, L.b.acc[wave], lane);
+  lds_barrier();
+  float* part = &L.b.acc[0][0];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    part[n] = (L.b.acc[0][n] + L.b.acc[1][n]) + (L.b.acc[2][n] + L.b.acc[3][n]);
+  }
+  lds_barrier();
+  if (!publish_partial(part, p.ws, ctr(p, l, C_SA), b, h, t, &L.last)) return;
+  float* dx1 = bwd_field(p, G_DLN1, l, p.step).row(b);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    st_sc1(dx1 + n, L.b.dx2p[n] + gather_partials(p.ws, b, n));
+  }
+  wg_arrive(ctr(p, l, C_X1) + b);
+}
+
+// ------------------------------------------------------------- backward: self-attention row b
+// dx1 (handed-off row) -> LN1' -> dsao -> dsav_h -> the last head writes dx0 = dx1p + sum_h W_v[h]^T dsav_h:
+// d x3 of layer l-1 (handed off), or (l = 0) the step input's gradient dx0 + dt.
+__device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, const uint4 (&wr)[NRI], SaL& L, uint64_t seed0,
+                           uint64_t seed1) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const LrceDecLayerW& W = p.layer[l];
+  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
+  if (t < E / 4) {
+    dy = ld4_sc1(bwd_field(p, G_DLN1, l, p.step).row(b) + 4 * t);
+    xr = *reinterpret_cast<const float4*>(fwd_field(p, F_X1P, l, p.step).row(b) + 4 * t);
+    gm = *reinterpret_cast<const float4*>(W.g1 + 4 * t);
+  }
+  const float mu = fwd_field(p, F_M1, l, p.step).row(b)[0], rs = fwd_field(p, F_R1, l, p.step).row(b)[0];
+  LnBwdLocal lnl = ln_row_bwd_local(dy, xr, gm, mu, rs, t);
+  const float4 dx = ln_row_bwd(lnl, rs, L.red2, lane, wave);
+  if (t < E / 4) {
+    *reinterpret_cast<float4*>(L.dx1p + 4 * t) = dx;
+    float4 d = dx;
+    if (p.drop_p > 0.f) {
+      const long long e = (long long)b * E + 4 * t;
+      d = make_float4(drop1(dx.x, p.drop_p, seed1, e), drop1(dx.y, p.drop_p, seed1, e + 1), drop1(dx.z, p.drop_p, seed1, e + 2),
+                      drop1(dx.w, p.drop_p, seed1, e + 3));
+    }
+    *reinterpret_cast<float4*>(L.dsao + 4 * t) = d;
+    if (h == 0) *reinterpret_cast<float4*>(bwd_field(p, G_DSAO, l, p.step).row(b) + 4 * t) = d;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  slice_gemv_t(L.wo, L.dsao, &L.red64[0][0], wave, lane);
+  lds_barrier();
+  if (t < D) {
+    float v = (L.red64[0][t] + L.red64[1][t]) + (L.red64[2][t] + L.red64[3][t]);
+    if (p.drop_p > 0.f) v = drop1(v, p.drop_p, seed0, ((long long)b * E + h * D + t) / D);
+    L.v[t] = v;
+    bwd_field(p, G_DSAV, l, p.step).row(b)[h * D + t] = v;
+  }
+  lds_barrier();
+  rows_gemv_t(wr, L.v + wave * WROWS, L.acc[wave], lane);
+  lds_barrier();
+  float* part = &L.acc[0][0];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int n = t + 256 * i;
+    part[n] = (L.acc[0][n] + L.acc[1][n]) + (L.acc[2][n] + L.acc[3][n]);
+  }
+  lds_barrier();
+  if (!publish_partial(part, p.ws + WS_SLAB, ctr(p, l, C_CA), b, h, t, &L.last)) return;
+  if (l > 0) {
+    float* dx3 = bwd_field(p, G_DLN3, l - 1, p.step).row(b);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int n = t + 256 * i;
+      st_sc1(dx3 + n, L.dx1p[n] + gather_partials(p.ws + WS_SLAB, b, n));
+    }
+    wg_arrive(ctr(p, l - 1, C_ROWS));
+  } else {
+    const float* dt = bwd_field(p, G_DCAO, p.n_layers, p.step).row(b);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int n = t + 256 * i;
+      p.ds_out[(long long)b * E + n] = L.dx1p[n] + gather_partials(p.ws + WS_SLAB, b, n) + ld_sc1(dt + n);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, const uint64_t* rng_off) {
+  __shared__ __attribute__((aligned(16))) StepLds U;
+  __shared__ unsigned ok_word;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int G = gridDim.x, R = G / H;
+  const int h = blockIdx.x % H, r = blockIdx.x / H;
+  const uint64_t roff = rng_off_now(rng_off);
+  const int L_ = p.n_layers;
+  // ---- tail: du = drop'(ds), dt = LN_f'(du) -> d x3 of the last layer
+  if (h == 0) {
+    SaL& S = U.sa;
+    const uint64_t st = tail_seed(p) + roff;
+    for (int b = r; b < p.B; b += R) {
+      float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
+      if (t < E / 4) {
+        dy = *reinterpret_cast<const float4*>(p.ds_in + (long long)b * E + 4 * t);
+        if (p.drop_p > 0.f) {
+          const long long e = (long long)b * E + 4 * t;
+          dy = make_float4(drop1(dy.x, p.drop_p, st, e), drop1(dy.y, p.drop_p, st, e + 1), drop1(dy.z, p.drop_p, st, e + 2),
+                           drop1(dy.w, p.drop_p, st, e + 3));
+        }
+        *reinterpret_cast<float4*>(bwd_field(p, G_DF, L_, p.step).row(b) + 4 * t) = dy;   // du (fusion LN's gamma / beta)
+        xr = *reinterpret_cast<const float4*>(fwd_field(p, F_X0, L_, p.step).row(b) + 4 * t);   // tsum
+        gm = *reinterpret_cast<const float4*>(p.gf + 4 * t);
+      }
+      const float mu = fwd_field(p, F_M1, L_, p.step).row(b)[0], rs = fwd_field(p, F_R1, L_, p.step).row(b)[0];
+      LnBwdLocal lnl = ln_row_bwd_local(dy, xr, gm, mu, rs, t);
+      const float4 dx = ln_row_bwd(lnl, rs, S.red2, lane, wave);
+      if (t < E / 4) {
+        st4_sc1(bwd_field(p, G_DCAO, L_, p.step).row(b) + 4 * t, dx);    // dt (read back by the layer-0 tail of this launch)
+        st4_sc1(bwd_field(p, G_DLN3, L_ - 1, p.step).row(b) + 4 * t, dx);
+      }
+      wg_arrive(ctr(p, L_ - 1, C_ROWS));
+    }
+  }
+  for (int l = L_ - 1; l >= 0; --l) {
+    const LrceDecLayerW& W = p.layer[l];
+    const uint64_t sl = layer_seed(p, l) + roff;
+    // ---- FB: FFN slices over all rows
+    bool waited = false;
+    for (int j = blockIdx.x; j < NF; j += G) {
+      if (!waited) {
+        if (!wg_wait(ctr(p, l, C_ROWS), p.B, p, 0x700 + l, &ok_word)) return;
+        waited = true;
+      }
+      ffn_bwd_slice(p, l, j, U.ff, sl + 4, sl + 5);
+      wg_arrive(ctr(p, l, C_SL));
+    }
+    // ---- CB: dx2 slices, then the cross-attention block backward per row
+    uint4 wr[NRI];
+    rows_load(reinterpret_cast<const f16*>(W.wq), h * D + wave * WROWS, lane, wr);
+    if (!wg_wait(ctr(p, l, C_SL), NF, p, 0x800 + l, &ok_word)) return;
+    for (int b = r; b < p.B; b += R)
+      slice_reduce(p.ws + 2 * WS_SLAB, b, h, nullptr, 0.f, 0, p.ws + 2 * WS_SLAB + WS_P + (long long)b * E,
+                   bwd_field(p, G_DLN2, l, p.step).row(b), U.rd);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0)
+      for (int b = r; b < p.B; b += R) __hip_atomic_fetch_add(ctr(p, l, C_X3) + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    CaL& C = U.ca;
+    lds_barrier();
+    slice_dma(reinterpret_cast<const f16*>(W.woc), h, C.wo, wave, lane);
+    for (int b = r; b < p.B; b += R) {
+      if (!wg_wait(ctr(p, l, C_X3) + b, H, p, 0x900 + l, &ok_word)) return;
+      ca_bwd_row(p, l, b, h, wr, C, sl + 2, sl + 3);
+      lds_barrier();
+    }
+    // ---- SB: self-attention block backward per row
+    SaL& S = U.sa;
+    lds_barrier();
+    rows_load(reinterpret_cast<const f16*>(W.wv), h * D + wave * WROWS, lane, wr);
+    slice_dma(reinterpret_cast<const f16*>(W.wo), h, S.wo, wave, lane);
+    for (int b = r; b < p.B; b += R) {
+      if (!wg_wait(ctr(p, l, C_X1) + b, 1, p, 0xA00 + l, &ok_word)) return;
+      sa_bwd_row(p, l, b, h, wr, S, sl, sl + 1);
+      lds_barrier();
+    }
+  }
+  finish(p, &ok_word);
+}
+
+int grid_for(int B) { return H * (B < RMAX ? B : RMAX); }
+
+int check(const LrceDecStep* a, bool bwd) {
+  if (!a || !a->acts || !a->ws || !a->counters || !a->status || !a->kv_video || !a->gf || !a->bf)
+    return lrce_fail(LRCE_E_ARG, "dec_step: null pointer");
+  if (a->B < 1 || a->B > MAXB) return lrce_fail(LRCE_E_ARG, "dec_step: B=%d outside [1, %d]", a->B, MAXB);
+  if (a->n_layers < 1 || a->n_layers > NLMAX || a->S < 1 || a->step < 0 || a->step >= a->S || a->nmc < 1 || a->B % a->nmc)
+    return lrce_fail(LRCE_E_ARG, "dec_step: n_layers=%d S=%d step=%d nmc=%d", a->n_layers, a->S, a->step, a->nmc);
+  if (a->lt < 0 || a->lt > MAXTXT || 150 + a->lt > MAXK || (a->lt > 0 && !a->kv_text))
+    return lrce_fail(LRCE_E_ARG, "dec_step: lt=%d (<= %d question keys)", a->lt, MAXTXT);
+  if (!bwd && a->step == a->S - 1 && !a->s_out) return lrce_fail(LRCE_E_ARG, "dec_step: the last step needs s_out");
+  if (bwd && (!a->grads || !a->ds_in || !a->ds_out || (!a->dkv_video16 && !a->dkv_video32) || (a->lt > 0 && !a->dkv_text)))
+    return lrce_fail(LRCE_E_ARG, "dec_step backward: grads / ds_in / ds_out / dK dV buffers");
+  if (bwd && a->dkv_video16 && a->nmc != 1) return lrce_fail(LRCE_E_ARG, "dec_step backward: bf16 video dK/dV needs nmc == 1");
+  for (int l = 0; l < a->n_layers; ++l) {
+    const LrceDecLayerW& w = a->layer[l];
+    const void* ps[] = {w.wv, w.bv, w.wo, w.bo, w.g1, w.be1, w.wq, w.bq, w.woc, w.boc, w.g2, w.be2, w.w1, w.b1, w.w2, w.b2, w.g3, w.be3};
+    for (const void* q : ps)
+      if (!q || (reinterpret_cast<uintptr_t>(q) & 15)) return lrce_fail(LRCE_E_ARG, "dec_step: layer %d parameter null or not 16-B aligned", l);
+  }
+  if ((reinterpret_cast<uintptr_t>(a->acts) & 15) || (a->grads && (reinterpret_cast<uintptr_t>(a->grads) & 15)) ||
+      (reinterpret_cast<uintptr_t>(a->ws) & 15) || (reinterpret_cast<uintptr_t>(a->kv_video) & 15) ||
+      (a->kv_text && (reinterpret_cast<uintptr_t>(a->kv_text) & 15)))
+    return lrce_fail(LRCE_E_ARG, "dec_step: arenas / K/V need 16-B alignment");
+  return LRCE_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t lrce_dec_step_field(int kind, int field, int layer, int B, int S, int n_layers) {
+  if (kind < 0 || kind > 1 || B < 1 || S < 1 || n_layers < 1 || n_layers > NLMAX) return -1;
+  if (field == -1) return field_off(kind, 0, n_layers + 1, B, S);   // total: n_layers + the tail block
+  if (field < 0 || field >= (kind ? NBWD : NFWD) || layer < 0 || layer > n_layers) return -1;
+  return field_off(kind, field, layer, B, S);
+}
+extern "C" int64_t lrce_dec_step_ws_elems(void) { return WS_ELEMS; }
+extern "C" int64_t lrce_dec_step_counter_words(void) { return CTR_WORDS; }
+extern "C" int lrce_dec_step_grid(int B) { return grid_for(B); }
+
+extern "C" int lrce_dec_step_fwd(const LrceDecStep* a, void* stream) {
+  if (int rc = check(a, false)) return rc;
+  dec_step_fwd_kernel<<<grid_for(a->B), NT, 0, static_cast<hipStream_t>(stream)>>>(*a, lrce_rng_offset());
+  return lrce_check_launch("dec_step_fwd");
+}
+
+extern "C" int lrce_dec_step_bwd(const LrceDecStep* a, void* stream) {
+  if (int rc = check(a, true)) return rc;
+  dec_step_bwd_kernel<<<grid_for(a->B), NT, 0, static_cast<hipStream_t>(stream)>>>(*a, lrce_rng_offset());
+  return lrce_check_launch("dec_step_bwd");
+}
+
+extern "C" int lrce_dec_step_reset(uint32_t* counters, uint32_t* status, void* stream) {
+  if (!counters || !status) return lrce_fail(LRCE_E_ARG, "dec_step_reset: null pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(counters, 0, CTR_WORDS * sizeof(uint32_t), st) != hipSuccess ||
+      hipMemsetAsync(status, 0, 4 * sizeof(uint32_t), st) != hipSuccess)
+    return lrce_fail(LRCE_E_LAUNCH, "dec_step_reset: memset failed");
+  return LRCE_OK;
+}

@@ -1208,6 +1208,8 @@ static bool glds_ok(const LrceGemmDesc* d) {
 
 static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   if (d->m <= 0 || d->n <= 0 || d->k <= 0 || d->batch <= 0) return lrce_fail(LRCE_E_ARG, "gemm: empty shape");
+  if ((d->flags & LRCE_EPI_AUX_F32) && !d->b_f32)
+    return lrce_fail(LRCE_E_ARG, "gemm: AUX_F32 (f32 pre-activation) is an exact-f32 path flag");
   if ((d->flags & (LRCE_EPI_DGELU | LRCE_EPI_RESID)) && !d->aux) return lrce_fail(LRCE_E_ARG, "gemm: aux missing");
   if ((d->flags & (LRCE_EPI_AUX_OUT | LRCE_EPI_OUT_BOTH)) && !d->aux_out) return lrce_fail(LRCE_E_ARG, "gemm: aux_out missing");
   if ((d->flags & LRCE_EPI_BIAS) && !d->bias) return lrce_fail(LRCE_E_ARG, "gemm: bias missing");

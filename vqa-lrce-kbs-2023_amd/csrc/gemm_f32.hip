@@ -118,10 +118,15 @@ __global__ void __launch_bounds__(NT) gemm_f32_kernel(GemmF32P p) {
         if (row < 0) continue;   // c_map -1: padded position, no output row
         float v = acc[i][j][r] * p.alpha + bias;
         if (fl & LRCE_EPI_GELU) {
-          if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + n] = f2bf(v);
+          if (fl & LRCE_EPI_AUX_OUT) {
+            if (fl & LRCE_EPI_AUX_F32) reinterpret_cast<float*>(p.aux_out)[row * p.ld_aux_out + n] = v;
+            else p.aux_out[row * p.ld_aux_out + n] = f2bf(v);
+          }
           v = gelu_f(v);
         }
-        if (fl & LRCE_EPI_DGELU) v *= gelu_grad_f(bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]));
+        if (fl & LRCE_EPI_DGELU)
+          v *= gelu_grad_f((fl & LRCE_EPI_AUX_F32) ? static_cast<const float*>(p.aux)[row * p.ld_aux + n]
+                                                   : bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]));
         if (p.row_scale) v *= p.row_scale[m / p.rows_per_scale];
         if ((fl & LRCE_EPI_RESID) && sk == 0) v += static_cast<const float*>(p.aux)[row * p.ld_aux + n];
         if (fl & LRCE_EPI_ATOMIC) atomicAdd(static_cast<float*>(p.c) + row * p.ldc + n, v);
@@ -206,7 +211,9 @@ __device__ __forceinline__ SkPre sk_prefetch(const SkinnyP& p, int m, int n) {
   const int fl = p.flags;
   const long long row = m;
   if (fl & LRCE_EPI_BIAS) e.bias = p.bias[n];
-  if (fl & LRCE_EPI_DGELU) e.dg = bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]);
+  if (fl & LRCE_EPI_DGELU)
+    e.dg = (fl & LRCE_EPI_AUX_F32) ? static_cast<const float*>(p.aux)[row * p.ld_aux + n]
+                                   : bf2f(static_cast<const bf16*>(p.aux)[row * p.ld_aux + n]);
   if (fl & LRCE_EPI_RESID) e.res = static_cast<const float*>(p.aux)[row * p.ld_aux + n];
   if (fl & (LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM)) e.acc = static_cast<const float*>(p.c)[row * p.ldc + n];
   return e;
@@ -218,7 +225,10 @@ __device__ __forceinline__ void sk_epilogue(const SkinnyP& p, float x, int m, in
   x = x * p.alpha + e.bias;
   x *= (n < p.scale_cols) ? p.scale_val : 1.f;
   if (fl & LRCE_EPI_GELU) {
-    if (fl & LRCE_EPI_AUX_OUT) p.aux_out[row * p.ld_aux_out + n] = f2bf(x);
+    if (fl & LRCE_EPI_AUX_OUT) {
+      if (fl & LRCE_EPI_AUX_F32) reinterpret_cast<float*>(p.aux_out)[row * p.ld_aux_out + n] = x;
+      else p.aux_out[row * p.ld_aux_out + n] = f2bf(x);
+    }
     x = gelu_f(x);
   }
   if (fl & LRCE_EPI_DGELU) x *= gelu_grad_f(e.dg);

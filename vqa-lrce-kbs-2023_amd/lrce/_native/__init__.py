@@ -136,6 +136,30 @@ class DecSaBwd(ctypes.Structure):
     ] + _WS
 
 
+class DecLayerW(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wv", "bv", "wo", "bo", "g1", "be1", "wq", "bq", "woc", "boc", "g2", "be2",
+                                               "w1", "b1", "w2", "b2", "g3", "be3")]
+
+
+DEC_LAYERS = 12
+
+
+class DecStep(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("S", ctypes.c_int32), ("step", ctypes.c_int32), ("nmc", ctypes.c_int32),
+        ("lt", ctypes.c_int32), ("n_layers", ctypes.c_int32), ("eps", ctypes.c_float), ("drop_p", ctypes.c_float),
+        ("seed", ctypes.c_uint64), ("gf", ctypes.c_void_p), ("bf", ctypes.c_void_p),
+        ("kv_video", ctypes.c_void_p), ("kv_video_lstride", ctypes.c_int64),
+        ("kv_text", ctypes.c_void_p), ("kv_text_lstride", ctypes.c_int64),
+        ("acts", ctypes.c_void_p), ("grads", ctypes.c_void_p), ("s_out", ctypes.c_void_p),
+        ("ds_in", ctypes.c_void_p), ("ds_out", ctypes.c_void_p),
+        ("dkv_video16", ctypes.c_void_p), ("dkv_video32", ctypes.c_void_p), ("dkv_video_lstride", ctypes.c_int64),
+        ("dkv_text", ctypes.c_void_p), ("dkv_text_lstride", ctypes.c_int64),
+        ("ws", ctypes.c_void_p), ("counters", ctypes.c_void_p), ("status", ctypes.c_void_p),
+        ("layer", DecLayerW * DEC_LAYERS),
+    ]
+
+
 class GemmItem(ctypes.Structure):
     _fields_ = [
         ("a", ctypes.c_void_p), ("b", ctypes.c_void_p), ("c", ctypes.c_void_p), ("bias", ctypes.c_void_p),
@@ -155,6 +179,7 @@ EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = 1, 2, 4, 8
 EPI_OUT_F32, EPI_ATOMIC, EPI_ACCUM, EPI_AUX_OUT, EPI_OUT_BOTH = 16, 32, 64, 128, 256
 EPI_BIAS_GRAD = 512
 EPI_SLABS = 1024
+EPI_AUX_F32 = 2048
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -191,6 +216,13 @@ _SIGS = {
     "lrce_dec_sa_bwd": [ctypes.POINTER(DecSaBwd), _P],
     "lrce_dec_ln_grads": [_P, _P, _P, _P, _P, _P, _I, _I, _P],
     "lrce_dec_set_trace": [_P],
+    "lrce_dec_step_fwd": [ctypes.POINTER(DecStep), _P],
+    "lrce_dec_step_bwd": [ctypes.POINTER(DecStep), _P],
+    "lrce_dec_step_reset": [_P, _P, _P],
+    "lrce_dec_step_field": [_I, _I, _I, _I, _I, _I],
+    "lrce_dec_step_ws_elems": [],
+    "lrce_dec_step_counter_words": [],
+    "lrce_dec_step_grid": [_I],
     "lrce_wattn_set_trace": [_P],
     "lrce_gemm_set_trace": [_P],
     "lrce_frames_resize": [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P],
@@ -225,6 +257,7 @@ _SIGS["lrce_wattn_bias_elems"] = [_I, _I]
 _SIGS["lrce_dec_slab_elems"] = [_I]
 _RET["lrce_dec_slab_elems"] = _I64
 _SIGS["lrce_wattn_dbias_part_elems"] = [_I, _I, _I]
+_RET.update({"lrce_dec_step_field": _I64, "lrce_dec_step_ws_elems": _I64, "lrce_dec_step_counter_words": _I64})
 _SIGS["lrce_layernorm_bwd_workspace"] = [_I, _I]
 
 

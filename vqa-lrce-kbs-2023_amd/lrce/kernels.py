@@ -234,7 +234,7 @@ def linear(x, w, bias=None, *, out=None, out_f32=False, gelu=False, pre_out=None
     if gelu:
         flags |= N.EPI_GELU
         if pre_out is not None:
-            flags |= N.EPI_AUX_OUT
+            flags |= N.EPI_AUX_OUT | (N.EPI_AUX_F32 if pre_out.dtype == F32 else 0)
     if resid is not None:
         flags |= N.EPI_RESID
     if out is None:
@@ -268,7 +268,7 @@ def linear_dx(dy, w, *, out=None, out_f32=True, dgelu_pre=None, a_map=None, rows
     Nn, K = w.shape
     flags = 0
     if dgelu_pre is not None:
-        flags |= N.EPI_DGELU
+        flags |= N.EPI_DGELU | (N.EPI_AUX_F32 if dgelu_pre.dtype == F32 else 0)
     if resid is not None:
         assert dgelu_pre is None
         flags |= N.EPI_RESID
@@ -687,6 +687,59 @@ def dec_workspace(device):
         ctr = torch.zeros(DEC_MAX_ROWS, dtype=torch.int32, device=key)
         _DEC_WS[key] = ws = (slab, ctr)
     return ws
+
+
+# ---- recurrent decoder: one persistent launch per recurrent step (csrc/decoder_step.hip) ------------
+_STEP_WS = {}
+DEC_STEP_FWD_FIELDS = ("x0", "sad", "x1p", "x1", "q", "ctx", "x2p", "x2", "x3p", "pre", "gd", "lse",
+                       "m1", "r1", "m2", "r2", "m3", "r3")
+DEC_STEP_BWD_FIELDS = ("df", "dgp", "dcao", "dq", "dsao", "dsav", "dln1", "dln2", "dln3")
+
+
+def dec_step_workspace(device):
+    """(ws f32, counters int32, status int32[4]) of the persistent decoder step, one per device (the
+    decoder runs on one stream at a time; the counters are left zero by every launch)."""
+    key = torch.device(device)
+    ws = _STEP_WS.get(key)
+    if ws is None:
+        L = N.lib()
+        ws = (torch.empty(int(L.lrce_dec_step_ws_elems()), dtype=F32, device=key),
+              torch.zeros(int(L.lrce_dec_step_counter_words()), dtype=torch.int32, device=key),
+              torch.zeros(4, dtype=torch.int32, device=key))
+        _STEP_WS[key] = ws
+    return ws
+
+
+def dec_step_field(kind, field, layer, B, S, n_layers):
+    """Element offset of an arena field (include/lrce_hip.h lrce_dec_step_field); field -1: the size."""
+    names = DEC_STEP_BWD_FIELDS if kind else DEC_STEP_FWD_FIELDS
+    f = names.index(field) if isinstance(field, str) else field
+    off = int(N.lib().lrce_dec_step_field(kind, f, layer, B, S, n_layers))
+    if off < 0:
+        raise N.NativeError(f"dec_step_field({kind}, {field}, {layer}, B={B}, S={S}, L={n_layers})")
+    return off
+
+
+def dec_step_fwd(desc, stream_tensor):
+    _timed("decoder", stream_tensor, lambda: call("lrce_dec_step_fwd", ctypes.byref(desc), stream_of(stream_tensor)))
+
+
+def dec_step_bwd(desc, stream_tensor):
+    _timed("decoder", stream_tensor, lambda: call("lrce_dec_step_bwd", ctypes.byref(desc), stream_of(stream_tensor)))
+
+
+def dec_step_status(device, reset=True):
+    """status[0] of the persistent decoder step (synchronises): 0, or the code of a hand-off that timed
+    out (0x100-0xAFF: phase << 8 | layer).  A timed-out launch leaves its counters set: reset=True
+    zeroes them and the status."""
+    ws = _STEP_WS.get(torch.device(device))
+    if ws is None:
+        return 0
+    code = int(ws[2][0].item())
+    if code and reset:
+        call("lrce_dec_step_reset", ptr(ws[1]), ptr(ws[2]), stream_of(ws[2]))
+        torch.cuda.synchronize(device)
+    return code
 
 
 def dec_kv(k1, *, stride1, ld1, bdiv1, lk1, k2=None, stride2=0, ld2=0, bdiv2=1, lk2=0, v_off):

@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 
 from .. import kernels as K
+from .. import _native as N
 from ..runtime import ensure, aux_stream, stream_anchor
 from .embedding import TextPosEmbed, VideoPosEmbed, VideoEmbedFn, TextEmbedFn, init_weight
 
@@ -148,7 +149,7 @@ class _LayerGrads:
 def _fused_ok(lay, Bq, Lt):
     """The per-head fused attention blocks (csrc/decoder.hip) need the fp16 weight shadow, <= 64 query
     rows and <= 150 + 42 memory keys; LRCE_DEC_FUSED=0 selects the unfused launches (A/B, tests)."""
-    if os.environ.get("LRCE_DEC_FUSED", "1") == "0":
+    if os.environ.get("LRCE_DEC_FUSED", "step") == "0":
         return False
     flat = getattr(lay, "_lrce_flat", None)
     return (flat is not None and flat.has_f16(lay.self_attn.in_proj_weight) and flat.has_f16(lay.multihead_attn.in_proj_weight)
@@ -204,7 +205,7 @@ def _layer_fwd(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts, st_pr
     st.m2, st.r2 = torch.empty(Bq, device=dev), torch.empty(Bq, device=dev)
     x2 = acts.x2[step]
     pro = K.ln_fwd_prologue(lay.norm2.weight, lay.norm2.bias, EPS, mean=st.m2, rstd=st.r2, y_out=x2)
-    st.pre = torch.empty(Bq, FF, dtype=torch.bfloat16, device=dev)
+    st.pre = torch.empty(Bq, FF, device=dev)
     gd = K.linear(st.x2p, _wq(lay, lay.linear1.weight), lay.linear1.bias, gelu=True, pre_out=st.pre, out=acts.gd[step],
                   drop=(p, seed + 4, 1), ln=pro)
     st.x3p = K.linear(gd, _wq(lay, lay.linear2.weight), lay.linear2.bias, out_f32=True, resid=x2, drop=(p, seed + 5, 1))
@@ -240,7 +241,7 @@ def _layer_fwd_fused(lay, prev, x_in, kvv, kvt, step, S, Lt, nmc, p, seed, acts,
     st.x2p, st.m2, st.r2 = acts.x2p[step], acts.m2[step], acts.r2[step]
     x2 = acts.x2[step]
     pro = K.ln_fwd_prologue(lay.norm2.weight, lay.norm2.bias, EPS, mean=st.m2, rstd=st.r2, y_out=x2)
-    st.pre = torch.empty(Bq, FF, dtype=torch.bfloat16, device=x_in.device)
+    st.pre = torch.empty(Bq, FF, device=x_in.device)
     gd = K.linear(st.x2p, _wq(lay, lay.linear1.weight), lay.linear1.bias, gelu=True, pre_out=st.pre, out=acts.gd[step],
                   drop=(p, seed + 4, 1), ln=pro)
     st.x3p = K.linear(gd, _wq(lay, lay.linear2.weight), lay.linear2.bias, out_f32=True, resid=x2, drop=(p, seed + 5, 1))
@@ -553,6 +554,209 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             (None,) * len(ctx.needs_input_grad[12:])
 
 
+# ------------------------------------------------------------------- persistent recurrent step
+def _step_mode(ft, Bq, Lt):
+    """Which recurrent-decoder implementation runs: "step" (default: one persistent launch per
+    recurrent step and direction, csrc/decoder_step.hip), "blocks" (LRCE_DEC_FUSED=blocks: the per-block
+    launches of csrc/decoder.hip + the skinny FFN GEMMs) or "unfused" (LRCE_DEC_FUSED=0).  The step and
+    block kernels need the fp16 weight shadow, <= 64 query rows and <= 150 + 42 memory keys."""
+    mode = os.environ.get("LRCE_DEC_FUSED", "step")
+    if mode == "0":
+        return "unfused"
+    lay = ft.transformer.layers[0]
+    if not _fused_ok(lay, Bq, Lt):
+        return "unfused"
+    return "blocks" if mode == "blocks" else "step"
+
+
+class _StepArena:
+    """Views of a persistent-step arena (lrce_dec_step_field): field f of layer l as [S, Bq, width]."""
+
+    def __init__(self, kind, nL, S, Bq, dev):
+        self.kind, self.nL, self.S, self.Bq = kind, nL, S, Bq
+        self.buf = torch.empty(K.dec_step_field(kind, -1, 0, Bq, S, nL), device=dev)
+
+    def f(self, name, l):
+        off = K.dec_step_field(self.kind, name, l, self.Bq, self.S, self.nL)
+        names = K.DEC_STEP_BWD_FIELDS if self.kind else K.DEC_STEP_FWD_FIELDS
+        w = {"pre": FF, "gd": FF, "dgp": FF, "lse": NHEAD}.get(name, 1 if name[0] in "mr" and len(name) == 2 else E)
+        assert name in names
+        return self.buf[off:off + self.S * self.Bq * w].view(self.S, self.Bq, w)
+
+    def rows(self, name, l):
+        t = self.f(name, l)
+        return t.view(self.S * self.Bq, t.shape[-1])
+
+
+def _step_desc(ft, flat, layers, B, S, nmc, Lt, p, seed):
+    """The LrceDecStep of one decoder call (per-step fields are filled by the caller)."""
+    d = N.DecStep()
+    d.B, d.S, d.nmc, d.lt, d.n_layers = B, S, nmc, Lt, len(layers)
+    d.eps, d.drop_p, d.seed = EPS, float(p), seed & (2 ** 64 - 1)
+    d.gf, d.bf = N.ptr(ft.fusion_layer_norm.weight), N.ptr(ft.fusion_layer_norm.bias)
+    for l, lay in enumerate(layers):
+        sa, ca = lay.self_attn, lay.multihead_attn
+        w = d.layer[l]
+        w.wv, w.bv = N.ptr(_wq(lay, sa.in_proj_weight)[2 * E:]), N.ptr(sa.in_proj_bias[2 * E:])
+        w.wo, w.bo = N.ptr(_wq(lay, sa.out_proj.weight)), N.ptr(sa.out_proj.bias)
+        w.g1, w.be1 = N.ptr(lay.norm1.weight), N.ptr(lay.norm1.bias)
+        w.wq, w.bq = N.ptr(_wq(lay, ca.in_proj_weight)[:E]), N.ptr(ca.in_proj_bias[:E])
+        w.woc, w.boc = N.ptr(_wq(lay, ca.out_proj.weight)), N.ptr(ca.out_proj.bias)
+        w.g2, w.be2 = N.ptr(lay.norm2.weight), N.ptr(lay.norm2.bias)
+        w.w1, w.b1 = N.ptr(_wq(lay, lay.linear1.weight)), N.ptr(lay.linear1.bias)
+        w.w2, w.b2 = N.ptr(_wq(lay, lay.linear2.weight)), N.ptr(lay.linear2.bias)
+        w.g3, w.be3 = N.ptr(lay.norm3.weight), N.ptr(lay.norm3.bias)
+    return d
+
+
+class _StepDecoderFn(torch.autograd.Function):
+    """FusionTransformer.forward (fusionv3.py:27-51) with each recurrent step ONE persistent launch
+    (all 12 layers and the step tail; csrc/decoder_step.hip), backward likewise.  The memory K/V of all
+    12 layers are projected first (one bf16 GEMM per layer and segment, on the K/V stream); the
+    query-side weight gradients of all steps are one outer product per weight after the backward."""
+
+    @staticmethod
+    def forward(ctx, v, v16, t, t16, ft, flat, p, seed, B, S, nmc, anchor, *params):
+        dev = v.device
+        layers = ft.transformer.layers
+        nL = len(layers)
+        Lt = t.shape[1] if t is not None else 0
+        Bq = t.shape[0] if t is not None else B * nmc
+        rows_v = B * S * 150
+        v16 = v16.view(rows_v, E)
+        t16 = t16.view(Bq * Lt, E) if Lt else None
+        main = torch.cuda.current_stream(dev)
+        ks = aux_stream(dev, "decoder_kv") if _KV_ASYNC else main
+        kvv = torch.empty(nL, rows_v, 2 * E, dtype=torch.bfloat16, device=dev)
+        kvt = torch.empty(nL, Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None
+        if ks is not main:
+            ks.wait_stream(main)
+            for x in (v16, t16, kvv, kvt):
+                if x is not None:
+                    x.record_stream(ks)
+        with torch.cuda.stream(ks):
+            for l, lay in enumerate(layers):
+                ca = lay.multihead_attn
+                w = flat.w16(ca.in_proj_weight)[E:]
+                K.linear(v16, w, ca.in_proj_bias[E:], out=kvv[l])
+                if Lt:
+                    K.linear(t16, w, ca.in_proj_bias[E:], out=kvt[l])
+        clear = getattr(flat, "pending_clear", None)
+        if clear is not None and getattr(flat, "pending_clear_at", None) == "decoder":
+            clear()
+        A = _StepArena(0, nL, S, Bq, dev)
+        A.f("x0", 0)[0].copy_(ft.summarization_token.detach().reshape(1, E).expand(Bq, E))
+        if ks is not main:
+            main.wait_stream(ks)
+        ws, ctrs, status = K.dec_step_workspace(dev)
+        d = _step_desc(ft, flat, layers, Bq, S, nmc, Lt, p, seed)
+        d.kv_video, d.kv_video_lstride = N.ptr(kvv), rows_v * 2 * E
+        d.kv_text, d.kv_text_lstride = N.ptr(kvt), Bq * Lt * 2 * E
+        d.acts, d.ws, d.counters, d.status = N.ptr(A.buf), N.ptr(ws), N.ptr(ctrs), N.ptr(status)
+        out = torch.empty(Bq, E, device=dev)
+        d.s_out = N.ptr(out)
+        for i in range(S):
+            d.step = i
+            K.dec_step_fwd(d, out)
+        ctx.save = (kvv, kvt, v16, t16, A, d)
+        ctx.ft, ctx.flat, ctx.dims = ft, flat, (B, S, nmc, Bq, Lt)
+        return out
+
+    @staticmethod
+    def backward(ctx, ds):
+        kvv, kvt, v16, t16, A, d = ctx.save
+        ft, flat = ctx.ft, ctx.flat
+        B, S, nmc, Bq, Lt = ctx.dims
+        layers = ft.transformer.layers
+        nL = len(layers)
+        dev = ds.device
+        rows_v = B * S * 150
+        main = torch.cuda.current_stream(dev)
+        G = _StepArena(1, nL, S, Bq, dev)
+        # video-row dK|dV: one writer per row (OE / Count) -> bf16 stored directly; shared by the MC
+        # answer choices -> f32 atomics onto zeros, cast after.  Question rows: f32, stored by the first
+        # backward step, accumulated by the others.
+        dkvv = torch.empty(nL, rows_v, 2 * E, dtype=torch.bfloat16, device=dev) if nmc == 1 else \
+            torch.zeros(nL, rows_v, 2 * E, device=dev)
+        dkvt = torch.empty(nL, Bq * Lt, 2 * E, device=dev) if Lt else None
+        d.grads = N.ptr(G.buf)
+        if nmc == 1:
+            d.dkv_video16, d.dkv_video32 = N.ptr(dkvv), None
+        else:
+            d.dkv_video16, d.dkv_video32 = None, N.ptr(dkvv)
+        d.dkv_video_lstride = rows_v * 2 * E
+        d.dkv_text, d.dkv_text_lstride = N.ptr(dkvt), Bq * Lt * 2 * E
+        cur = ds.contiguous()
+        bufs = [torch.empty(Bq, E, device=dev), torch.empty(Bq, E, device=dev)]
+        for k, i in enumerate(reversed(range(S))):
+            d.step = i
+            d.ds_in, d.ds_out = N.ptr(cur), N.ptr(bufs[k % 2])
+            K.dec_step_bwd(d, bufs[k % 2])
+            cur = bufs[k % 2]
+        ds0 = cur   # gradient of the summary-token rows fed to step 0
+        # memory side: dv = sum_l dK|dV_l W_kv,l (and the question rows likewise), on the K/V stream
+        ks = aux_stream(dev, "decoder_kv") if _KV_ASYNC else main
+        if ks is not main:
+            ks.wait_stream(main)
+        dv = torch.empty(rows_v, E, device=dev)
+        dtt = torch.empty(Bq * Lt, E, device=dev) if Lt else None
+        dk16 = dkvv if nmc == 1 else torch.empty(nL, rows_v, 2 * E, dtype=torch.bfloat16, device=dev)
+        dt16 = torch.empty(nL, Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None
+        with torch.cuda.stream(ks):
+            for l, lay in enumerate(layers):
+                if nmc != 1:
+                    K.cast_bf16(dkvv[l], dk16[l])
+                if Lt:
+                    K.cast_bf16(dkvt[l], dt16[l])
+                w = flat.w16(lay.multihead_attn.in_proj_weight)[E:]
+                K.linear_dx(dk16[l], w, out=dv, accumulate=l > 0)
+                if Lt:
+                    K.linear_dx(dt16[l], w, out=dtt, accumulate=l > 0)
+        if ks is not main:
+            main.wait_stream(ks)
+            for x in (dv, dtt, dk16, dt16, dkvv, dkvt, kvv, kvt):
+                if x is not None:
+                    x.record_stream(ks)
+        # weight gradients (query side over all steps, LayerNorms, memory K/V, summary token) on the
+        # weight-gradient stream: nothing downstream reads them
+        wg = aux_stream(dev, "decoder_wgrad")
+        wg.wait_stream(main)
+        R = S * Bq
+        with torch.cuda.stream(wg):
+            for l, lay in enumerate(layers):
+                sa, ca = lay.self_attn, lay.multihead_attn
+                items = [(G.rows(dy, l), A.rows(x, l), A.rows(m, l), A.rows(r, l), _g(flat, n.weight), _g(flat, n.bias))
+                         for dy, x, m, r, n in (("dln1", "x1p", "m1", "r1", lay.norm1), ("dln2", "x2p", "m2", "r2", lay.norm2),
+                                                ("dln3", "x3p", "m3", "r3", lay.norm3))]
+                items = [it for it in items if it[4] is not None or it[5] is not None]
+                if items:
+                    K.dec_ln_grads(items, R)
+                _wgrad(flat, lay.linear2.weight, lay.linear2.bias, G.rows("df", l), A.rows("gd", l))
+                _wgrad(flat, lay.linear1.weight, lay.linear1.bias, G.rows("dgp", l), A.rows("x2", l))
+                _wgrad(flat, ca.out_proj.weight, ca.out_proj.bias, G.rows("dcao", l), A.rows("ctx", l))
+                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, G.rows("dq", l), A.rows("x1", l), rows=(0, E))
+                _wgrad(flat, sa.out_proj.weight, sa.out_proj.bias, G.rows("dsao", l), A.rows("sad", l))
+                _wgrad(flat, sa.in_proj_weight, sa.in_proj_bias, G.rows("dsav", l), A.rows("x0", l), rows=(2 * E, 3 * E))
+                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16[l], v16, rows=(E, 3 * E))
+                if Lt:
+                    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[l], t16, rows=(E, 3 * E))
+            fl = ft.fusion_layer_norm
+            gw, gb = _g(flat, fl.weight), _g(flat, fl.bias)
+            if gw is not None or gb is not None:
+                K.dec_ln_grads([(G.rows("df", nL), A.rows("x0", nL), A.rows("m1", nL), A.rows("r1", nL), gw, gb)], R)
+            gt = _g(flat, ft.summarization_token)
+            if gt is not None:
+                K.colsum(ds0, gt.view(E))
+            flat.notify(ft.parameters())
+            flat.group_done("decoder")
+        for x in [ds0, v16, dk16, A.buf, G.buf] + ([t16, dt16] if Lt else []):
+            x.record_stream(wg)
+        ctx.save = None
+        danchor = torch.zeros(1, device=dev) if ctx.needs_input_grad[11] else None
+        return (dv.view(B, S, 150, E), None, dtt.view(Bq, Lt, E) if Lt else None) + (None,) * 8 + (danchor,) + \
+            (None,) * len(ctx.needs_input_grad[12:])
+
+
 class _LinearFn(torch.autograd.Function):
     """y = x W^T + b (final_fc, fusionv3.py:160,195) on the exact-f32 MFMA path (M = B rows)."""
 
@@ -597,7 +801,9 @@ class FusionTransformer(nn.Module):
         p = self.drop_out_rate if self.training else 0.0
         seed = int(torch.randint(0, 2 ** 40, (1,)).item())
         anchor = stream_anchor(self, aux_stream(v.device, "decoder_wgrad"))
-        return _RecurrentDecoderFn.apply(v, v16, t, t16, self, flat, p, seed, B, S, nmc, anchor, *self.parameters())
+        Bq = t.shape[0] if t is not None else B * nmc
+        fn = _StepDecoderFn if _step_mode(self, Bq, t.shape[1] if t is not None else 0) == "step" else _RecurrentDecoderFn
+        return fn.apply(v, v16, t, t16, self, flat, p, seed, B, S, nmc, anchor, *self.parameters())
 
 
 class FusionVideo(FusionTransformer):
