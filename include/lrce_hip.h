@@ -569,6 +569,9 @@ int lrce_dec_step_fwd(const LrceDecStep* args, void* stream);
 int lrce_dec_step_bwd(const LrceDecStep* args, void* stream);
 /* zero the counter block and the status words (after a timeout: status[0] != 0) */
 int lrce_dec_step_reset(uint32_t* counters, uint32_t* status, void* stream);
+/* Debug: phase timestamps (s_memrealtime, 100 MHz) of the step kernels into buf[((dir * 128 + workgroup) * 16 + layer) * 8 + mark]
+ * (dir 0 forward, 1 backward; 2 * 128 * 16 * 8 uint64); NULL turns it off (the default).  tools/decoder_step_bench.py --trace. */
+int lrce_dec_step_set_trace(uint64_t* buf);
 /* workgroups of one launch for B rows (12 x min(B, 10)) */
 int lrce_dec_step_grid(int B);
 

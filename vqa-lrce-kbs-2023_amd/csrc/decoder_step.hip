@@ -47,7 +47,7 @@
 namespace {
 
 constexpr int FF = 3072, FS = 32, NF = FF / FS, RMAX = 10, MAXB = LRCE_DEC_MAX_ROWS, RCH = 16;
-constexpr int XP = 100, XROW = 8 * XP;   // padded LDS row of 768: 8 parts of 96 (+4: conflict-free part reads)
+constexpr int XP = 100, XROW = 8 * XP + 4;   // padded LDS row of 768: 8 parts of 96 (+4), rows 804 apart (MFMA row reads)
 constexpr int NLMAX = LRCE_DEC_LAYERS;
 // counter block (uint32): per layer CL words; then done / abort
 constexpr int C_SL = 0, C_ROWS = 1, C_X3 = 16, C_SA = 16 + MAXB, C_X1 = 16 + 2 * MAXB, C_CA = 16 + 3 * MAXB;
@@ -92,20 +92,57 @@ __device__ __forceinline__ Ar bwd_field(const LrceDecStep& p, int f, int l, int 
   return Ar{p.grads + field_off(1, f, l, p.B, p.S) + (long long)step * p.B * bwd_width(f), bwd_width(f)};
 }
 
-// ---- write-through hand-off accesses
+// ---- write-through hand-off accesses: 16-B buffer loads / stores with the sc1 bit.  The buffer
+// descriptor must be wave-uniform (SGPRs): a per-lane pointer would make hipcc loop over the lanes
+// (a waterfall of 64 descriptor builds per access), so every call takes a uniform base (forced with
+// readfirstlane) and a per-lane element offset.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFF0, 0x00020000);
+  const uint64_t a = reinterpret_cast<uintptr_t>(p);
+  const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(u), (short)0, 0x7FFFFFFF, 0x00020000);
 }
-__device__ __forceinline__ float4 ld4_sc1(const float* p) {   // 16 B, sc1 (L1 bypass): a handed-off row
-  const uint4 u = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(p), 0, 0, 16));
-  return __builtin_bit_cast(float4, u);
+__device__ __forceinline__ float4 ld4_sc1(const float* base, long long off) {   // 16 B, sc1 (L1 bypass): a handed-off row
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(base), (int)(off * 4), 0, 16);
+  return __builtin_bit_cast(float4, v);
 }
-__device__ __forceinline__ void st4_sc1(float* p, float4 v) {   // 16 B, sc1 (write-through)
+__device__ __forceinline__ void st4_sc1(float* base, long long off, float4 v) {   // 16 B, sc1 (write-through)
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
-                                         rsrc_of(p), 0, 0, 16);
+                                         rsrc_of(base), (int)(off * 4), 0, 16);
 }
 __device__ __forceinline__ float ld_sc1(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// y / (1 - p) where the element's uniform >= p, else 0: the mask of lrce_dropout over [rows][768] for elements e .. e+3
+__device__ __forceinline__ float4 drop4(float4 y, float p, uint64_t seed, long long e) {
+  if (p <= 0.f) return y;
+  const float4 u = lrce_uniform4(seed, (uint64_t)e >> 2);
+  const float k = 1.0f - p;
+  return make_float4(u.x >= p ? y.x / k : 0.f, u.y >= p ? y.y / k : 0.f, u.z >= p ? y.z / k : 0.f, u.w >= p ? y.w / k : 0.f);
+}
+
+// Publish this head's partial row (LDS part[768], 16-B aligned) to slab[b][h] with 16-B write-through
+// stores and return true in the last of the 12 heads of row b to arrive (the counter's add returns 11);
+// gather4: columns 4t .. 4t+3 of the 12 partials, summed in head order (deterministic).
+__device__ bool publish4(const float* part, float* slab, unsigned* ctr, int b, int h, unsigned* last) {
+  const int t = threadIdx.x;
+  if (t < E / 4) st4_sc1(slab, ((long long)b * H + h) * E + 4 * t, lds4(part + 4 * t));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) *last = __hip_atomic_fetch_add(&ctr[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(H - 1);
+  __syncthreads();
+  return *last != 0;
+}
+__device__ float4 gather4(const float* slab, int b, int t) {
+  float4 v[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) v[j] = ld4_sc1(slab, ((long long)b * H + j) * E + 4 * t);
+  float4 s = v[0];
+#pragma unroll
+  for (int j = 1; j < H; ++j) s = add4(s, v[j]);
+  return s;
+}
 
 // every storing wave drains its write-through stores, the workgroup meets, one lane adds `n`
 __device__ __forceinline__ void wg_arrive(unsigned* ctr, unsigned n = 1) {
@@ -155,6 +192,16 @@ __device__ void finish(const LrceDecStep& p, unsigned* last_word) {
 }
 
 __device__ __forceinline__ unsigned* ctr(const LrceDecStep& p, int l, int k) { return p.counters + l * CL + k; }
+
+// Debug phase timestamps (lrce_dec_step_set_trace; NULL in production): thread 0 of workgroup w stores
+// s_memrealtime (100 MHz) at mark i of layer l into trace[((dir * 128 + w) * 16 + l) * 8 + i].
+unsigned long long* g_step_trace = nullptr;
+#define STEP_MARK_P(DIR, L, I) do { } while (0)
+#define STEP_MARK(DIR, L, I)                                                                              \
+  do {                                                                                                    \
+    if (trace && threadIdx.x == 0)                                                                        \
+      trace[(((DIR) * 128 + blockIdx.x) * 16 + (L)) * 8 + (I)] = __builtin_amdgcn_s_memrealtime();       \
+  } while (0)
 __device__ __forceinline__ uint64_t layer_seed(const LrceDecStep& p, int l) {
   return p.seed + 64ull * (uint64_t)(p.step * p.n_layers + l);
 }
@@ -179,14 +226,14 @@ __device__ __forceinline__ KvP kv_of(const LrceDecStep& p, int l) {
 // ------------------------------------------------------------------------------------ LDS images
 struct SaL {                      // self-attention block (forward and backward)
   f16 wo[E * D];
-  float x0[E];
+  alignas(16) float x0[E];
   float pp[4][16 * 64];
   alignas(16) float v[D];
-  float part[E];
-  float dx1p[E];
+  alignas(16) float part[E];
+  alignas(16) float dx1p[E];
   float dsao[E];
   float red64[4][D];
-  float acc[4][E];
+  alignas(16) float acc[4][E];
   float red2[4];
   unsigned last;
 };
@@ -195,20 +242,20 @@ struct CaL {                      // cross-attention block: forward and backward
   bf16 vimg[MAXK * D];
   union {
     struct {                      // forward
-      float x1[E];
+      alignas(16) float x1[E];
       float pp[4][16 * 64];
       float q[D];
       float ps[MAXK + 64];
       float opart[4][D];
       alignas(16) float ctx[D];
-      float part[E];
+      alignas(16) float part[E];
     } f;
     struct {                      // backward
       union {
         bf16 kimg[MAXK * D];
-        float acc[4][E];
+        alignas(16) float acc[4][E];
       };
-      float dx2p[E];
+      alignas(16) float dx2p[E];
       float dcao[E];
       float red64[4][D];
       float dctx[D];
@@ -221,19 +268,21 @@ struct CaL {                      // cross-attention block: forward and backward
   float red2[4];
   unsigned last;
 };
-struct FfL {                      // FFN slices over all rows
-  alignas(16) float x[RCH * XROW];
-  alignas(16) float hb[RCH][FS];
+struct FfL {                      // FFN slices over all rows (MFMA: the rows are the 16 M lanes)
+  alignas(16) float x[RCH * XROW];   // the chunk's input rows (padded), then the output partial tile
+  alignas(16) float hb[RCH][FS + 4]; // the hidden slice (forward: dropped GELU; backward: dgp)
+  float kacc[2][16][16];          // the second K half of the hidden-slice product
   f16 w2s[E * FS];                // backward: the W2 column slice [768][32]
+  f16 w1s[FS * E];                // backward: the W1 row slice [32][768]
+  float preb[RCH][FS];            // backward: the saved pre-activations of the chunk's rows
 };
-struct RedL {
-  float4 red[16][16];
+struct RedL {                     // the FFN-partial reduce (outside the union: the next phase's weight
+  float4 red[16][16];             // slices stream into the union while it runs)
 };
 union StepLds {
   SaL sa;
   CaL ca;
   FfL ff;
-  RedL rd;
 };
 
 // ---------------------------------------------------------------------------- FFN partial reduce
@@ -247,7 +296,7 @@ __device__ void slice_reduce(const float* P, int b, int h, const float* bias, fl
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 v[NF / 16];
 #pragma unroll
-  for (int i = 0; i < NF / 16; ++i) v[i] = ld4_sc1(P + ((long long)(g + 16 * i) * MAXB + b) * E + col);
+  for (int i = 0; i < NF / 16; ++i) v[i] = ld4_sc1(P, ((long long)(g + 16 * i) * MAXB + b) * E + col);
 #pragma unroll
   for (int i = 0; i < NF / 16; ++i) { s.x += v[i].x; s.y += v[i].y; s.z += v[i].z; s.w += v[i].w; }
   L.red[g][q] = s;
@@ -267,10 +316,41 @@ __device__ void slice_reduce(const float* P, int b, int h, const float* bias, fl
         a.z = u.z >= drop_p ? a.z / k : 0.f; a.w = u.w >= drop_p ? a.w / k : 0.f;
       }
     }
-    const float4 r = ld4_sc1(base_row + col);
-    st4_sc1(out_row + col, make_float4(r.x + a.x, r.y + a.y, r.z + a.z, r.w + a.w));
+    const float4 r = ld4_sc1(base_row, col);
+    st4_sc1(out_row, col, make_float4(r.x + a.x, r.y + a.y, r.z + a.z, r.w + a.w));
   }
   lds_barrier();
+}
+
+// W rows h*64 .. h*64+63 of a row-major [768][768] fp16 matrix -> LDS [64][768] (96 KB contiguous: 24
+// LDS-DMA instructions of 1 KB per wave)
+__device__ __forceinline__ void rows_dma(const f16* w, int h, void* lds, int wave, int lane) {
+  const uint32_t base = dec_lds_addr(lds);
+#pragma unroll 4
+  for (int i = 0; i < 24; ++i) {
+    const int ins = wave * 24 + i;
+    dec_glds(w, (uint32_t)(h * D * E * 2 + ins * 1024 + lane * 16), base + (uint32_t)ins * 1024u);
+  }
+}
+// part[4t .. 4t+3] (t < 192) = sum_r v[r] W[r][4t .. 4t+3] over the 64 LDS rows (the transposed product W^T v of
+// a backward dX partial: each thread sums all 64 rows of its 4 columns, no cross-wave reduction)
+__device__ __forceinline__ void rows_t_lds(const f16* Wl, const float* v, float* part) {
+  const int t = threadIdx.x;
+  if (t >= E / 4) return;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+#pragma unroll 8
+  for (int r = 0; r < D; r += 2) {
+    const uint2 u0 = *reinterpret_cast<const uint2*>(Wl + r * E + 4 * t);
+    const uint2 u1 = *reinterpret_cast<const uint2*>(Wl + (r + 1) * E + 4 * t);
+    const float v0 = v[r], v1 = v[r + 1];
+    const float4 w0 = make_float4((float)__builtin_bit_cast(f16, (unsigned short)(u0.x & 0xFFFFu)), (float)__builtin_bit_cast(f16, (unsigned short)(u0.x >> 16)),
+                                  (float)__builtin_bit_cast(f16, (unsigned short)(u0.y & 0xFFFFu)), (float)__builtin_bit_cast(f16, (unsigned short)(u0.y >> 16)));
+    const float4 w1 = make_float4((float)__builtin_bit_cast(f16, (unsigned short)(u1.x & 0xFFFFu)), (float)__builtin_bit_cast(f16, (unsigned short)(u1.x >> 16)),
+                                  (float)__builtin_bit_cast(f16, (unsigned short)(u1.y & 0xFFFFu)), (float)__builtin_bit_cast(f16, (unsigned short)(u1.y >> 16)));
+    a.x = fmaf(v0, w0.x, a.x); a.y = fmaf(v0, w0.y, a.y); a.z = fmaf(v0, w0.z, a.z); a.w = fmaf(v0, w0.w, a.w);
+    c.x = fmaf(v1, w1.x, c.x); c.y = fmaf(v1, w1.y, c.y); c.z = fmaf(v1, w1.z, c.z); c.w = fmaf(v1, w1.w, c.w);
+  }
+  *reinterpret_cast<float4*>(part + 4 * t) = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w + c.w);
 }
 
 // ------------------------------------------------------------------- forward: self-attention row
@@ -292,21 +372,37 @@ __device__ void sa_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint
   lds_barrier();
   slice_gemv(L.wo, L.v, L.part, t);
   lds_barrier();
-  if (!publish_partial(L.part, p.ws, ctr(p, l, C_SA), b, h, t, &L.last)) return;
-  float* x1p = fwd_field(p, F_X1P, l, p.step).row(b);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int n = t + 256 * i;
-    float y = gather_partials(p.ws, b, n) + W.bo[n];
-    if (p.drop_p > 0.f) y = drop1(y, p.drop_p, seed1, (long long)b * E + n);
-    st_sc1(x1p + n, L.x0[n] + y);
+  if (!publish4(L.part, p.ws, ctr(p, l, C_SA), b, h, &L.last)) return;
+  if (t < E / 4) {
+    const float4 y = drop4(add4(gather4(p.ws, b, t), lds4(W.bo + 4 * t)), p.drop_p, seed1, (long long)b * E + 4 * t);
+    st4_sc1(fwd_field(p, F_X1P, l, p.step).row(b), 4 * t, add4(lds4(L.x0 + 4 * t), y));
   }
   wg_arrive(ctr(p, l, C_X1) + b);
 }
 
 // ------------------------------------------------------------------ forward: cross-attention row
+// what a cross-attention row needs that nothing in this launch writes: the key row of thread t
+// (registers) and the head's V rows (LDS DMA) — issued before the row's wait
+__device__ void ca_fwd_prefetch(const LrceDecStep& p, int l, int b, int h, CaL& L, uint4 (&kr)[8]) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const KvP kv = kv_of(p, l);
+  const int Lk = kv.lk1 + kv.lk2;
+  const KvRows kvr = kv_rows(kv, b, h);
+  {
+    const bf16* kp = kv_row(kvr, t < Lk ? t : 0);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) kr[c] = *reinterpret_cast<const uint4*>(kp + 8 * c);
+  }
+  const uint32_t vb = dec_lds_addr(L.vimg);
+  for (int ins = wave; ins * 8 < Lk; ins += 4) {
+    const int r = ins * 8 + (lane >> 3), j = min(r, Lk - 1);
+    const bf16* vp = kv_row(kvr, j) + kv.v_off + (((lane & 7) ^ (r & 7)) << 3);
+    dec_glds_p(vp, vb + (uint32_t)ins * 1024u);
+  }
+}
+
 __device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint4 (&wr)[NRI], float bqv, CaL& L,
-                           uint64_t seed2, uint64_t seed3, bool first_row) {
+                           uint64_t seed2, uint64_t seed3, const uint4 (&kr)[8]) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
   const KvP kv = kv_of(p, l);
@@ -314,28 +410,12 @@ __device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint
   float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
   const float* x1p = fwd_field(p, F_X1P, l, p.step).row(b);
   if (t < E / 4) {
-    xr = ld4_sc1(x1p + 4 * t);
+    xr = ld4_sc1(x1p, 4 * t);
     gg = *reinterpret_cast<const float4*>(W.g1 + 4 * t);
     be = *reinterpret_cast<const float4*>(W.be1 + 4 * t);
   }
   const float s1l = row_sum_local(xr, t);
-  // key row of thread t (registers), the head's V rows (LDS DMA)
   const bool live = t < Lk;
-  const KvRows kvr = kv_rows(kv, b, h);
-  uint4 kr[8];
-  {
-    const bf16* kp = kv_row(kvr, live ? t : 0);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) kr[c] = *reinterpret_cast<const uint4*>(kp + 8 * c);
-  }
-  {
-    const uint32_t vb = dec_lds_addr(L.vimg);
-    for (int ins = wave; ins * 8 < Lk; ins += 4) {
-      const int r = ins * 8 + (lane >> 3), j = min(r, Lk - 1);
-      const bf16* vp = kv_row(kvr, j) + kv.v_off + (((lane & 7) ^ (r & 7)) << 3);
-      dec_glds_p(vp, vb + (uint32_t)ins * 1024u);
-    }
-  }
   float mu, rs;
   ln_row_fwd(xr, s1l, gg, be, p.eps, L.f.x1, L.red2, t, lane, wave, mu, rs);
   if (h == 0) {
@@ -406,14 +486,10 @@ __device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint
   lds_barrier();
   slice_gemv(L.wo, L.f.ctx, L.f.part, t);
   lds_barrier();
-  if (!publish_partial(L.f.part, p.ws + WS_SLAB, ctr(p, l, C_CA), b, h, t, &L.last)) return;
-  float* x2p = fwd_field(p, F_X2P, l, p.step).row(b);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int n = t + 256 * i;
-    float y = gather_partials(p.ws + WS_SLAB, b, n) + W.boc[n];
-    if (p.drop_p > 0.f) y = drop1(y, p.drop_p, seed3, (long long)b * E + n);
-    st_sc1(x2p + n, L.f.x1[n] + y);
+  if (!publish4(L.f.part, p.ws + WS_SLAB, ctr(p, l, C_CA), b, h, &L.last)) return;
+  if (t < E / 4) {
+    const float4 y = drop4(add4(gather4(p.ws + WS_SLAB, b, t), lds4(W.boc + 4 * t)), p.drop_p, seed3, (long long)b * E + 4 * t);
+    st4_sc1(fwd_field(p, F_X2P, l, p.step).row(b), 4 * t, add4(lds4(L.f.x1 + 4 * t), y));
   }
   wg_arrive(ctr(p, l, C_ROWS));
 }
@@ -421,10 +497,17 @@ __device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint
 // ------------------------------------------------------------------------ FFN: rows into LDS
 // rows c0 .. c0+nr-1 of a handed-off [B][768] f32 field (sc1) into the padded image L.x
 __device__ __forceinline__ void rows_to_lds(const float* src, int c0, int nr, FfL& L) {
-  for (int i = threadIdx.x; i < nr * (E / 4); i += NT) {
-    const int rr = i / (E / 4), k = (i % (E / 4)) * 4;
-    const float4 v = ld4_sc1(src + (long long)(c0 + rr) * E + k);
-    *reinterpret_cast<float4*>(L.x + rr * XROW + (k / 96) * XP + (k % 96)) = v;
+  constexpr int PER = RCH * (E / 4) / NT;   // 12 float4 per thread: all loads in flight at once
+  float4 v[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
+    v[q] = rr < nr ? ld4_sc1(src, (long long)(c0 + rr) * E + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
+    *reinterpret_cast<float4*>(L.x + rr * XROW + (k / 96) * XP + (k % 96)) = v[q];
   }
 }
 // element k of padded row rr
@@ -457,7 +540,7 @@ __device__ void ln_rows_fwd(FfL& L, int nr, const float* g, const float* be, flo
       const float4 y = make_float4((v[i].x - mu) * rs * gg.x + bb.x, (v[i].y - mu) * rs * gg.y + bb.y,
                                    (v[i].z - mu) * rs * gg.z + bb.z, (v[i].w - mu) * rs * gg.w + bb.w);
       *reinterpret_cast<float4*>(xp + 4 * i) = y;
-      if (y_rows) st4_sc1(y_rows + (long long)(c0 + rr) * E + k, y);
+      if (y_rows) st4_sc1(y_rows, (long long)(c0 + rr) * E + k, y);
     }
     if (lane == 0 && mean_out) {
       mean_out[c0 + rr] = mu;
@@ -467,83 +550,125 @@ __device__ void ln_rows_fwd(FfL& L, int nr, const float* g, const float* be, flo
 }
 
 // --------------------------------------------------------------------------- forward: FFN slice j
-__device__ void ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4) {
-  const int t = threadIdx.x, c = t >> 3, part = t & 7;
+#define PIN4(u) asm volatile("" : "+v"((u).x), "+v"((u).y), "+v"((u).z), "+v"((u).w))
+// wait: the row-arrival counter to wait for after the weight loads are issued (NULL: none); false =
+// the launch is aborting
+__device__ __forceinline__ float4 h4f(uint2 u) {   // four fp16 -> f32
+  return make_float4((float)__builtin_bit_cast(f16, (unsigned short)(u.x & 0xFFFFu)), (float)__builtin_bit_cast(f16, (unsigned short)(u.x >> 16)),
+                     (float)__builtin_bit_cast(f16, (unsigned short)(u.y & 0xFFFFu)), (float)__builtin_bit_cast(f16, (unsigned short)(u.y >> 16)));
+}
+#define PIN2(u) asm volatile("" : "+v"((u).x), "+v"((u).y))
+// MFMA f32 16x16x4 on four consecutive k (the skinny GEMMs' form): A(i = lane & 15, k0 + 4 (lane >> 4) + e),
+// B(k0 + 4 (lane >> 4) + e, j = lane & 15), e = 0..3; C row 4 (lane >> 4) + r, column lane & 15
+__device__ __forceinline__ f32x4 mfma4(float4 a, float4 b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+}
+
+// C tiles of one wave (12 column tiles of 16 over the 768 outputs, rows = the chunk's 16 rows) -> the
+// padded image, then the chunk's live rows -> dst (write-through 16-B stores)
+__device__ __forceinline__ void tiles_out(FfL& L, const f32x4 (&acc)[12], float* dst, int c0, int nr) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int tt = 0; tt < 12; ++tt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) *xat(L, 4 * kq + r, (wave * 12 + tt) * 16 + col) = acc[tt][r];
+  lds_barrier();
+  constexpr int PER = RCH * (E / 4) / NT;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
+    if (rr < nr) st4_sc1(dst, (long long)(c0 + rr) * E + k, *reinterpret_cast<const float4*>(xat(L, rr, k)));
+  }
+}
+
+// Forward FFN slice j (32 hidden units) over all rows, 16 rows per chunk as the MFMA M dimension:
+// linear1 (wave = 16 hidden units x half of K, the halves added through LDS) -> + b1 -> pre, GELU,
+// dropout -> gd; linear2 partial (wave = 12 of the 48 output tiles, K = 32) -> P_j.  The weight
+// fragments are loaded before the wait (wait: the row counter, NULL for a second slice).
+__device__ bool ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, unsigned* wait, unsigned* ok_word) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
+  const int ct = wave & 1, kh = wave >> 1;
   const LrceDecLayerW& W = p.layer[l];
   const f16* w1 = reinterpret_cast<const f16*>(W.w1);
   const f16* w2 = reinterpret_cast<const f16*>(W.w2);
-  // W1 rows j*32 + c, k in [96 part, 96 part + 96) -> 12 x 16 B; W2 rows 4t..4t+3 (t < 192), columns j*32 .. +32
-  uint4 w1r[12], w2r[16];
+  uint2 b1f[24], b2f[12][2];
+  {
+    const f16* src = w1 + (long long)(j * FS + ct * 16 + col) * E + kh * 384 + 4 * kq;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) w1r[i] = *reinterpret_cast<const uint4*>(w1 + (long long)(j * FS + c) * E + part * 96 + 8 * i);
-  if (t < E / 4) {
+    for (int s = 0; s < 24; ++s) b1f[s] = *reinterpret_cast<const uint2*>(src + 16 * s);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int tt = 0; tt < 12; ++tt)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) w2r[q * 4 + u] = *reinterpret_cast<const uint4*>(w2 + (long long)(4 * t + q) * FF + j * FS + 8 * u);
+      for (int q = 0; q < 2; ++q)
+        b2f[tt][q] = *reinterpret_cast<const uint2*>(w2 + (long long)((wave * 12 + tt) * 16 + col) * FF + j * FS + 16 * q + 4 * kq);
   }
-  const float b1v = W.b1[j * FS + c];
+  const float b1v = W.b1[j * FS + ct * 16 + col];
+  if (wait && !wg_wait(wait, p.B, p, 0x400 + l, ok_word)) return false;
+  // keep the fragments in registers (hipcc would otherwise re-load them per use to save VGPRs)
+#pragma unroll
+  for (int s = 0; s < 24; ++s) PIN2(b1f[s]);
+#pragma unroll
+  for (int tt = 0; tt < 12; ++tt) { PIN2(b2f[tt][0]); PIN2(b2f[tt][1]); }
   Ar pre = fwd_field(p, F_PRE, l, p.step), gd = fwd_field(p, F_GD, l, p.step);
   const float* x2p = fwd_field(p, F_X2P, l, p.step).base;
+  float* Pj = p.ws + 2 * WS_SLAB + (long long)j * MAXB * E;
+  const bool owner = j == 0;   // slice 0's workgroup materialises x2 (read back by the next layer's reducers) and its stats
   for (int c0 = 0; c0 < p.B; c0 += RCH) {
     const int nr = min(RCH, p.B - c0);
     lds_barrier();   // the previous chunk's image is consumed
     rows_to_lds(x2p, c0, nr, L);
     lds_barrier();
-    Ar x2 = fwd_field(p, F_X2, l, p.step);
-    const bool owner = j == 0;   // slice 0's workgroup materialises x2 (read back by the next layer's reducers) and its stats
     ln_rows_fwd(L, nr, W.g2, W.be2, p.eps, owner ? fwd_field(p, F_M2, l, p.step).base : nullptr,
-                owner ? fwd_field(p, F_R2, l, p.step).base : nullptr, owner ? x2.base : nullptr, c0);
+                owner ? fwd_field(p, F_R2, l, p.step).base : nullptr, owner ? fwd_field(p, F_X2, l, p.step).base : nullptr, c0);
     lds_barrier();
-    // linear1 slice + GELU + dropout
-    for (int rr = 0; rr < nr; ++rr) {
-      float acc = 0.f;
-      const float* xp = L.x + rr * XROW + part * XP;
+    // linear1 slice
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        float wf[8];
-        unpack8(w1r[i], wf);
-        acc += dot8(wf, xp + 8 * i);
-      }
-      acc = sum8(acc);
-      if (part == 0) {
-        const int b = c0 + rr, col = j * FS + c;
-        const float hv = acc + b1v;
-        pre.row(b)[col] = hv;
-        float gv = gelu_f(hv);
-        if (p.drop_p > 0.f) gv = drop1(gv, p.drop_p, seed4, (long long)b * FF + col);
-        gd.row(b)[col] = gv;
-        L.hb[rr][c] = gv;
-      }
+    for (int s = 0; s < 24; ++s)
+      acc = mfma4(*reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq)), h4f(b1f[s]), acc);
+    if (kh) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) L.kacc[ct][4 * kq + r][col] = acc[r];
     }
     lds_barrier();
-    // linear2 partial of this slice: P_j[b][4t .. 4t+3]
-    if (t < E / 4) {
-      float* Pj = p.ws + 2 * WS_SLAB + (long long)j * MAXB * E;
-      for (int rr = 0; rr < nr; ++rr) {
-        float o[4] = {0.f, 0.f, 0.f, 0.f};
+    if (!kh) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float4 h0 = *reinterpret_cast<const float4*>(&L.hb[rr][8 * u]);
-          const float4 h1 = *reinterpret_cast<const float4*>(&L.hb[rr][8 * u + 4]);
-          const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float wf[8];
-            unpack8(w2r[q * 4 + u], wf);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[q] = fmaf(wf[e], hv[e], o[q]);
-          }
+      for (int r = 0; r < 4; ++r) {
+        const int rr = 4 * kq + r, b = c0 + rr, cc = ct * 16 + col, cg = j * FS + cc;
+        float g = 0.f;
+        if (rr < nr) {
+          const float hv = acc[r] + L.kacc[ct][rr][col] + b1v;
+          pre.row(b)[cg] = hv;
+          g = gelu_f(hv);
+          if (p.drop_p > 0.f) g = drop1(g, p.drop_p, seed4, (long long)b * FF + cg);
+          gd.row(b)[cg] = g;
         }
-        st4_sc1(Pj + (long long)(c0 + rr) * E + 4 * t, make_float4(o[0], o[1], o[2], o[3]));
+        L.hb[rr][cc] = g;
       }
     }
+    lds_barrier();
+    // linear2 partial: 12 output tiles per wave, K = the 32 hidden units
+    f32x4 o[12];
+#pragma unroll
+    for (int tt = 0; tt < 12; ++tt) o[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float4 a = *reinterpret_cast<const float4*>(&L.hb[col][16 * q + 4 * kq]);
+#pragma unroll
+      for (int tt = 0; tt < 12; ++tt) o[tt] = mfma4(a, h4f(b2f[tt][q]), o[tt]);
+    }
+    tiles_out(L, o, Pj, c0, nr);
   }
+  return true;
 }
 
 // ------------------------------------------------------------------------------- forward kernel
-__global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, const uint64_t* rng_off) {
+__global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, const uint64_t* rng_off, unsigned long long* trace) {
   __shared__ __attribute__((aligned(16))) StepLds U;
+  __shared__ __attribute__((aligned(16))) RedL RD;
   __shared__ unsigned ok_word;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int G = gridDim.x, R = G / H;
@@ -554,31 +679,34 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
     const LrceDecLayerW& W = p.layer[l];
     const uint64_t sl = layer_seed(p, l) + roff;
     // ---- A: self-attention block (after reducing the previous layer's FFN partials)
+    STEP_MARK(0, l, 0);
     uint4 wr[NRI];
     rows_load(reinterpret_cast<const f16*>(W.wv), h * D + wave * WROWS, lane, wr);
     const float bvv = t < D ? W.bv[h * D + t] : 0.f;
+    SaL& S = U.sa;
+    lds_barrier();
+    slice_dma(reinterpret_cast<const f16*>(W.wo), h, S.wo, wave, lane);
     if (l > 0) {
       if (!wg_wait(ctr(p, l - 1, C_SL), NF, p, 0x100 + l, &ok_word)) return;
+      STEP_MARK(0, l, 1);
       const LrceDecLayerW& Wp = p.layer[l - 1];
       for (int b = r; b < p.B; b += R)
         slice_reduce(p.ws + 2 * WS_SLAB, b, h, Wp.b2, p.drop_p, layer_seed(p, l - 1) + 5 + roff,
-                     fwd_field(p, F_X2, l - 1, p.step).row(b), fwd_field(p, F_X3P, l - 1, p.step).row(b), U.rd);
+                     fwd_field(p, F_X2, l - 1, p.step).row(b), fwd_field(p, F_X3P, l - 1, p.step).row(b), RD);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (t == 0)
         for (int b = r; b < p.B; b += R) __hip_atomic_fetch_add(ctr(p, l - 1, C_X3) + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    SaL& S = U.sa;
-    lds_barrier();
-    slice_dma(reinterpret_cast<const f16*>(W.wo), h, S.wo, wave, lane);
     bool first = true;
     for (int b = r; b < p.B; b += R) {
       if (l > 0) {
         if (!wg_wait(ctr(p, l - 1, C_X3) + b, H, p, 0x200 + l, &ok_word)) return;
+        if (first) STEP_MARK(0, l, 2);
         const LrceDecLayerW& Wp = p.layer[l - 1];
         float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
         if (t < E / 4) {
-          xr = ld4_sc1(fwd_field(p, F_X3P, l - 1, p.step).row(b) + 4 * t);
+          xr = ld4_sc1(fwd_field(p, F_X3P, l - 1, p.step).row(b), 4 * t);
           gg = *reinterpret_cast<const float4*>(Wp.g3 + 4 * t);
           be = *reinterpret_cast<const float4*>(Wp.be3 + 4 * t);
         }
@@ -600,6 +728,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
       first = false;
       lds_barrier();
     }
+    STEP_MARK(0, l, 3);
     // ---- B: cross-attention block
     CaL& C = U.ca;
     lds_barrier();
@@ -608,28 +737,29 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
     slice_dma(reinterpret_cast<const f16*>(W.woc), h, C.wo, wave, lane);
     first = true;
     for (int b = r; b < p.B; b += R) {
+      uint4 kr[8];
+      ca_fwd_prefetch(p, l, b, h, C, kr);
       if (!wg_wait(ctr(p, l, C_X1) + b, 1, p, 0x300 + l, &ok_word)) return;
-      ca_fwd_row(p, l, b, h, wr, bqv, C, sl + 2, sl + 3, first);
+      if (first) STEP_MARK(0, l, 4);
+      ca_fwd_row(p, l, b, h, wr, bqv, C, sl + 2, sl + 3, kr);
       first = false;
       lds_barrier();
     }
+    STEP_MARK(0, l, 5);
     // ---- C: FFN slices over all rows
-    bool waited = false;
     for (int j = blockIdx.x; j < NF; j += G) {
-      if (!waited) {
-        if (!wg_wait(ctr(p, l, C_ROWS), p.B, p, 0x400 + l, &ok_word)) return;
-        waited = true;
-      }
-      ffn_fwd_slice(p, l, j, U.ff, sl + 4);
+      if (!ffn_fwd_slice(p, l, j, U.ff, sl + 4, j == (int)blockIdx.x ? ctr(p, l, C_ROWS) : nullptr, &ok_word)) return;
       wg_arrive(ctr(p, l, C_SL));
     }
+    STEP_MARK(0, l, 7);
   }
   // ---- step tail: x3p of the last layer, then (head 0) x3 = LN3, tsum = x3 + s, s' = drop(LN_f(tsum))
   const int Ll = L_ - 1;
   if (!wg_wait(ctr(p, Ll, C_SL), NF, p, 0x500, &ok_word)) return;
+  STEP_MARK(0, L_, 1);
   for (int b = r; b < p.B; b += R)
     slice_reduce(p.ws + 2 * WS_SLAB, b, h, p.layer[Ll].b2, p.drop_p, layer_seed(p, Ll) + 5 + roff,
-                 fwd_field(p, F_X2, Ll, p.step).row(b), fwd_field(p, F_X3P, Ll, p.step).row(b), U.rd);
+                 fwd_field(p, F_X2, Ll, p.step).row(b), fwd_field(p, F_X3P, Ll, p.step).row(b), RD);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0)
@@ -641,7 +771,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
       if (!wg_wait(ctr(p, Ll, C_X3) + b, H, p, 0x600, &ok_word)) return;
       float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
       if (t < E / 4) {
-        xr = ld4_sc1(fwd_field(p, F_X3P, Ll, p.step).row(b) + 4 * t);
+        xr = ld4_sc1(fwd_field(p, F_X3P, Ll, p.step).row(b), 4 * t);
         gg = *reinterpret_cast<const float4*>(p.layer[Ll].g3 + 4 * t);
         be = *reinterpret_cast<const float4*>(p.layer[Ll].be3 + 4 * t);
       }
@@ -679,18 +809,20 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
       lds_barrier();
     }
   }
+  STEP_MARK(0, L_, 7);
   finish(p, &ok_word);
 }
 
 // =============================================================================== backward
 // ---------------------------------------------------------------- backward: FFN slice j, all rows
-__device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, uint64_t seed5) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, c = t >> 3, part = t & 7;
+__device__ bool ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, uint64_t seed5, unsigned* wait,
+                              unsigned* ok_word) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
+  const int ct = wave & 1, kh = wave >> 1;
   const LrceDecLayerW& W = p.layer[l];
   const f16* w1 = reinterpret_cast<const f16*>(W.w1);
   const f16* w2 = reinterpret_cast<const f16*>(W.w2);
-  // W2[:, j*32 .. +32] -> LDS [768][32] (DMA: row n = 4 chunks of 16 B), then thread (c, part) keeps
-  // W2[96 part + e][j*32 + c] (e < 96) as 48 packed halves; W1 rows j*32 + c', columns 4t..4t+3 (t < 192)
+  // W2[:, j*32 .. +32] -> LDS [768][32] (DMA: row n = 4 chunks of 16 B), W1[j*32 .. +32][:] -> LDS [32][768]
   {
     const uint32_t base = dec_lds_addr(L.w2s);
 #pragma unroll
@@ -700,19 +832,15 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
       dec_glds(w2, (uint32_t)(((long long)n * FF + j * FS + (lane & 3) * 8) * 2), base + (uint32_t)ins * 1024u);
     }
   }
-  uint2 w1t[FS];
-  if (t < E / 4) {
+  {
+    // W1[j*32 .. +32][:] -> LDS [32][768]: row c = 96 chunks of 16 B, 48 instructions x 1 KB
+    const uint32_t base = dec_lds_addr(L.w1s);
 #pragma unroll
-    for (int cc = 0; cc < FS; ++cc) w1t[cc] = *reinterpret_cast<const uint2*>(w1 + (long long)(j * FS + cc) * E + 4 * t);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
-  unsigned w2c[48];
-#pragma unroll
-  for (int e = 0; e < 48; ++e) {
-    const unsigned lo = __builtin_bit_cast(unsigned short, L.w2s[(part * 96 + 2 * e) * FS + c]);
-    const unsigned hi = __builtin_bit_cast(unsigned short, L.w2s[(part * 96 + 2 * e + 1) * FS + c]);
-    w2c[e] = lo | (hi << 16);
+    for (int i = 0; i < 12; ++i) {
+      const int ins = wave * 12 + i;
+      const int chunk = ins * 64 + lane;           // 3072 chunks: row chunk / 96, piece chunk % 96
+      dec_glds(w1, (uint32_t)(((long long)(j * FS + chunk / 96) * E + (chunk % 96) * 8) * 2), base + (uint32_t)ins * 1024u);
+    }
   }
   const Ar dln3 = bwd_field(p, G_DLN3, l, p.step), df = bwd_field(p, G_DF, l, p.step), dgp = bwd_field(p, G_DGP, l, p.step);
   const Ar x3p = fwd_field(p, F_X3P, l, p.step), m3 = fwd_field(p, F_M3, l, p.step), r3 = fwd_field(p, F_R3, l, p.step);
@@ -720,16 +848,46 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
   float* dres = p.ws + 2 * WS_SLAB + WS_P;   // dx3p rows (handed to the reducers)
   float* Qj = p.ws + 2 * WS_SLAB + (long long)j * MAXB * E;
   const bool owner = j == 0;
+  // what a chunk of rows needs that this launch does not write (the forward's x3p / stats / pre-
+  // activations): for the first chunk issued before the wait for the rows' gradients
+  auto prefetch = [&](int c0, int nr) {
+    for (int i = t; i < nr * FS; i += NT) L.preb[i / FS][i % FS] = pre.row(c0 + i / FS)[j * FS + i % FS];
+  };
+  prefetch(0, min(RCH, p.B));
+  if (wait && !wg_wait(wait, p.B, p, 0x700 + l, ok_word)) return false;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slices and prefetches have landed (read after the next barrier)
+  lds_barrier();
+  // B fragments from the LDS slices, once per slice: dgp (wave = 16 hidden units x half of the 768
+  // outputs): W2[n][j*32 + ct*16 + col], n = kh*384 + 16 s + 4 kq + e; Q (wave = 12 of the 48 column
+  // tiles): W1[j*32 + 16 s + 4 kq + e][tile*16 + col]
+  uint2 bdf[24], bqf[12][2];
+  auto pack4 = [](const f16* p0, int stride) {
+    const unsigned a = __builtin_bit_cast(unsigned short, p0[0]), b = __builtin_bit_cast(unsigned short, p0[stride]);
+    const unsigned c = __builtin_bit_cast(unsigned short, p0[2 * stride]), d = __builtin_bit_cast(unsigned short, p0[3 * stride]);
+    return make_uint2(a | (b << 16), c | (d << 16));
+  };
+#pragma unroll
+  for (int s = 0; s < 24; ++s) bdf[s] = pack4(L.w2s + (kh * 384 + 16 * s + 4 * kq) * FS + ct * 16 + col, FS);
+#pragma unroll
+  for (int tt = 0; tt < 12; ++tt)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) bqf[tt][q] = pack4(L.w1s + (16 * q + 4 * kq) * E + (wave * 12 + tt) * 16 + col, E);
   for (int c0 = 0; c0 < p.B; c0 += RCH) {
     const int nr = min(RCH, p.B - c0);
     lds_barrier();
+    if (c0 > 0) prefetch(c0, nr);
     rows_to_lds(dln3.base, c0, nr, L);
     lds_barrier();
     // LayerNorm-3 backward per row (wave per row), then the out-dropout backward -> df in the image
-    for (int rr = wave; rr < nr; rr += 4) {
+    for (int q = 0; q < RCH / 4; ++q) {
+      const int rr = wave + 4 * q;
+      if (rr >= nr) break;
       const int b = c0 + rr;
       float* xp = xat(L, rr, 12 * lane);
       const float mu = m3.row(b)[0], rs = r3.row(b)[0];
+      float4 xv[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) xv[i] = *reinterpret_cast<const float4*>(x3p.row(b) + 12 * lane + 4 * i);
       float4 g[3], xh[3];
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -737,7 +895,7 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
         const int k = 12 * lane + 4 * i;
         const float4 dy = *reinterpret_cast<const float4*>(xp + 4 * i);
         const float4 gm = *reinterpret_cast<const float4*>(W.g3 + k);
-        const float4 x = *reinterpret_cast<const float4*>(x3p.row(b) + k);
+        const float4 x = xv[i];
         g[i] = make_float4(dy.x * gm.x, dy.y * gm.y, dy.z * gm.z, dy.w * gm.w);
         xh[i] = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
         s1 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
@@ -749,109 +907,120 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
         const int k = 12 * lane + 4 * i;
         float4 d = make_float4(rs * (g[i].x - mg - xh[i].x * mgx), rs * (g[i].y - mg - xh[i].y * mgx),
                                rs * (g[i].z - mg - xh[i].z * mgx), rs * (g[i].w - mg - xh[i].w * mgx));
-        if (owner) st4_sc1(dres + (long long)b * E + k, d);
-        if (p.drop_p > 0.f) {
-          const float4 u = lrce_uniform4(seed5, ((uint64_t)b * E + k) >> 2);
-          const float kd = 1.0f - p.drop_p;
-          d.x = u.x >= p.drop_p ? d.x / kd : 0.f; d.y = u.y >= p.drop_p ? d.y / kd : 0.f;
-          d.z = u.z >= p.drop_p ? d.z / kd : 0.f; d.w = u.w >= p.drop_p ? d.w / kd : 0.f;
-        }
+        if (owner) st4_sc1(dres, (long long)b * E + k, d);
+        d = drop4(d, p.drop_p, seed5, (long long)b * E + k);
         *reinterpret_cast<float4*>(xp + 4 * i) = d;
         if (owner) *reinterpret_cast<float4*>(df.row(b) + k) = d;
       }
     }
     lds_barrier();
     // dgp = drop'(W2[:, slice]^T df) gelu'(pre)
-    for (int rr = 0; rr < nr; ++rr) {
-      const float* xp = L.x + rr * XROW + part * XP;
-      float acc = 0.f;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int e = 0; e < 48; ++e) {
-        const float2 x2 = *reinterpret_cast<const float2*>(xp + 2 * e);
-        acc = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(w2c[e] & 0xFFFFu)), x2.x, acc);
-        acc = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(w2c[e] >> 16)), x2.y, acc);
-      }
-      acc = sum8(acc);
-      if (part == 0) {
-        const int b = c0 + rr, col = j * FS + c;
-        float d = acc;
-        if (p.drop_p > 0.f) d = drop1(d, p.drop_p, seed4, (long long)b * FF + col);
-        d *= gelu_grad_f(pre.row(b)[col]);
-        dgp.row(b)[col] = d;
-        L.hb[rr][c] = d;
+    for (int s = 0; s < 24; ++s)
+      acc = mfma4(*reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq)), h4f(bdf[s]), acc);
+    if (kh) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) L.kacc[ct][4 * kq + r][col] = acc[r];
+    }
+    lds_barrier();
+    if (!kh) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = 4 * kq + r, b = c0 + rr, cc = ct * 16 + col, cg = j * FS + cc;
+        float d = 0.f;
+        if (rr < nr) {
+          d = acc[r] + L.kacc[ct][rr][col];
+          if (p.drop_p > 0.f) d = drop1(d, p.drop_p, seed4, (long long)b * FF + cg);
+          d *= gelu_grad_f(L.preb[rr][cc]);
+          dgp.row(b)[cg] = d;
+        }
+        L.hb[rr][cc] = d;
       }
     }
     lds_barrier();
-    // Q_j = W1[slice]^T dgp: columns 4t .. 4t+3
-    if (t < E / 4) {
-      for (int rr = 0; rr < nr; ++rr) {
-        float o[4] = {0.f, 0.f, 0.f, 0.f};
+    // Q_j = W1[slice]^T dgp: 12 column tiles per wave, K = the 32 hidden units
+    f32x4 o[12];
 #pragma unroll
-        for (int cc = 0; cc < FS; ++cc) {
-          const float dv = L.hb[rr][cc];
-          const uint2 u = w1t[cc];
-          o[0] = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(u.x & 0xFFFFu)), dv, o[0]);
-          o[1] = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(u.x >> 16)), dv, o[1]);
-          o[2] = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(u.y & 0xFFFFu)), dv, o[2]);
-          o[3] = fmaf((float)__builtin_bit_cast(f16, (unsigned short)(u.y >> 16)), dv, o[3]);
-        }
-        st4_sc1(Qj + (long long)(c0 + rr) * E + 4 * t, make_float4(o[0], o[1], o[2], o[3]));
-      }
+    for (int tt = 0; tt < 12; ++tt) o[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float4 a = *reinterpret_cast<const float4*>(&L.hb[col][16 * q + 4 * kq]);
+#pragma unroll
+      for (int tt = 0; tt < 12; ++tt) o[tt] = mfma4(a, h4f(bqf[tt][q]), o[tt]);
     }
+    tiles_out(L, o, Qj, c0, nr);
   }
+  return true;
 }
 
 // ------------------------------------------------------------ backward: cross-attention row b
 // dx2 (handed-off row) -> LN2' -> dcao -> dctx -> attention backward (dq, memory dK / dV) -> the last
 // head writes dx1 = dx2p + sum_h W_q[h]^T dq_h and raises the row flag
-__device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, const uint4 (&wr)[NRI], CaL& L, uint64_t seed2,
-                           uint64_t seed3) {
+// what a cross-attention backward row needs that this launch does not write (the forward's rows and
+// statistics, the question rows' running dK / dV, the head's K / V images by DMA): issued before the
+// row's wait
+struct CaBwdPre {
+  float4 xr, gm;
+  float mu, rs, qd, od, lse;
+  float4 told[TXI][4];
+};
+__device__ void ca_bwd_prefetch(const LrceDecStep& p, int l, int b, int h, CaL& L, CaBwdPre& q) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
   const KvP kv = kv_of(p, l);
   const int Lk = kv.lk1 + kv.lk2;
-  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
+  q.xr = q.gm = make_float4(0.f, 0.f, 0.f, 0.f);
   if (t < E / 4) {
-    dy = ld4_sc1(bwd_field(p, G_DLN2, l, p.step).row(b) + 4 * t);
-    xr = *reinterpret_cast<const float4*>(fwd_field(p, F_X2P, l, p.step).row(b) + 4 * t);
-    gm = *reinterpret_cast<const float4*>(W.g2 + 4 * t);
+    q.xr = *reinterpret_cast<const float4*>(fwd_field(p, F_X2P, l, p.step).row(b) + 4 * t);
+    q.gm = *reinterpret_cast<const float4*>(W.g2 + 4 * t);
   }
-  const float mu = fwd_field(p, F_M2, l, p.step).row(b)[0], rs = fwd_field(p, F_R2, l, p.step).row(b)[0];
-  LnBwdLocal lnl = ln_row_bwd_local(dy, xr, gm, mu, rs, t);
-  float qd = 0.f, od = 0.f;
+  q.mu = fwd_field(p, F_M2, l, p.step).row(b)[0];
+  q.rs = fwd_field(p, F_R2, l, p.step).row(b)[0];
+  q.qd = q.od = 0.f;
   if (t < D) {
-    qd = fwd_field(p, F_Q, l, p.step).row(b)[h * D + t];
-    od = fwd_field(p, F_CTX, l, p.step).row(b)[h * D + t];
+    q.qd = fwd_field(p, F_Q, l, p.step).row(b)[h * D + t];
+    q.od = fwd_field(p, F_CTX, l, p.step).row(b)[h * D + t];
   }
-  const float lse = fwd_field(p, F_LSE, l, p.step).row(b)[h];
-  const KvRows kvr = kv_rows(kv, b, h);
-  // text rows' running dK / dV (accumulated over the recurrent steps): read now, added at the end
+  q.lse = fwd_field(p, F_LSE, l, p.step).row(b)[h];
   const bool dk2_store = p.step == p.S - 1;
-  float* dk2 = p.lt ? p.dkv_text + l * p.dkv_text_lstride : nullptr;
+  const float* dk2 = p.lt ? p.dkv_text + l * p.dkv_text_lstride : nullptr;
   const long long tbase = (long long)b * p.lt * 2 * E + h * D;
-  float4 told[TXI][4];
 #pragma unroll
   for (int i = 0; i < TXI; ++i) {
     const int e = t + 256 * i, tj = e >> 3, c = e & 7;
-    told[i][0] = told[i][1] = told[i][2] = told[i][3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    q.told[i][0] = q.told[i][1] = q.told[i][2] = q.told[i][3] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (tj < kv.lk2 && !dk2_store) {
       const float* src = dk2 + tbase + (long long)tj * 2 * E + c * 8;
-      told[i][0] = *reinterpret_cast<const float4*>(src);
-      told[i][1] = *reinterpret_cast<const float4*>(src + 4);
-      told[i][2] = *reinterpret_cast<const float4*>(src + E);
-      told[i][3] = *reinterpret_cast<const float4*>(src + E + 4);
+      q.told[i][0] = *reinterpret_cast<const float4*>(src);
+      q.told[i][1] = *reinterpret_cast<const float4*>(src + 4);
+      q.told[i][2] = *reinterpret_cast<const float4*>(src + E);
+      q.told[i][3] = *reinterpret_cast<const float4*>(src + E + 4);
     }
   }
+  const KvRows kvr = kv_rows(kv, b, h);
+  const uint32_t kb = dec_lds_addr(L.b.kimg), vb = dec_lds_addr(L.vimg);
+  for (int ins = wave; ins * 8 < Lk; ins += 4) {
+    const int r = ins * 8 + (lane >> 3), j = min(r, Lk - 1);
+    const bf16* kp = kv_row(kvr, j) + (((lane & 7) ^ (r & 7)) << 3);
+    dec_glds_p(kp, kb + (uint32_t)ins * 1024u);
+    dec_glds_p(kp + kv.v_off, vb + (uint32_t)ins * 1024u);
+  }
+}
+
+__device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, CaL& L, uint64_t seed2, uint64_t seed3,
+                           const CaBwdPre& q) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const KvP kv = kv_of(p, l);
+  const int Lk = kv.lk1 + kv.lk2;
+  float4 dy = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < E / 4) dy = ld4_sc1(bwd_field(p, G_DLN2, l, p.step).row(b), 4 * t);
+  const float rs = q.rs, qd = q.qd, od = q.od, lse = q.lse;
+  LnBwdLocal lnl = ln_row_bwd_local(dy, q.xr, q.gm, q.mu, rs, t);
+  const float* dk2r = p.lt ? p.dkv_text + l * p.dkv_text_lstride : nullptr;
+  float* dk2 = const_cast<float*>(dk2r);
+  const long long tbase = (long long)b * p.lt * 2 * E + h * D;
   const float4 dx = ln_row_bwd(lnl, rs, L.red2, lane, wave);
-  {
-    const uint32_t kb = dec_lds_addr(L.b.kimg), vb = dec_lds_addr(L.vimg);
-    for (int ins = wave; ins * 8 < Lk; ins += 4) {
-      const int r = ins * 8 + (lane >> 3), j = min(r, Lk - 1);
-      const bf16* kp = kv_row(kvr, j) + (((lane & 7) ^ (r & 7)) << 3);
-      dec_glds_p(kp, kb + (uint32_t)ins * 1024u);
-      dec_glds_p(kp + kv.v_off, vb + (uint32_t)ins * 1024u);
-    }
-  }
   if (t < E / 4) {
     *reinterpret_cast<float4*>(L.b.dx2p + 4 * t) = dx;
     float4 d = dx;
@@ -868,6 +1037,8 @@ __device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, const uint
   lds_barrier();
   slice_gemv_t(L.wo, L.b.dcao, &L.b.red64[0][0], wave, lane);
   lds_barrier();
+  // the W_oc slice is consumed: stream W_q[h] rows into its place for the dX partial at the end
+  rows_dma(reinterpret_cast<const f16*>(p.layer[l].wq), h, L.wo, wave, lane);
   float dod = 0.f;
   if (t < D) {
     dod = (L.b.red64[0][t] + L.b.red64[1][t]) + (L.b.red64[2][t] + L.b.red64[3][t]);
@@ -948,7 +1119,7 @@ __device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, const uint
         const float* qv = L.b.q + c * 8;
         const float* gv = L.b.dctx + c * 8;
         float* dst = dk2 + tbase + (long long)tj * 2 * E + c * 8;
-        const float4 a0 = told[i][0], a1 = told[i][1], a2 = told[i][2], a3 = told[i][3];
+        const float4 a0 = q.told[i][0], a1 = q.told[i][1], a2 = q.told[i][2], a3 = q.told[i][3];
         *reinterpret_cast<float4*>(dst) = make_float4(a0.x + dsj * qv[0], a0.y + dsj * qv[1], a0.z + dsj * qv[2], a0.w + dsj * qv[3]);
         *reinterpret_cast<float4*>(dst + 4) = make_float4(a1.x + dsj * qv[4], a1.y + dsj * qv[5], a1.z + dsj * qv[6], a1.w + dsj * qv[7]);
         *reinterpret_cast<float4*>(dst + E) = make_float4(a2.x + pj * gv[0], a2.y + pj * gv[1], a2.z + pj * gv[2], a2.w + pj * gv[3]);
@@ -963,35 +1134,24 @@ __device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, const uint
     bwd_field(p, G_DQ, l, p.step).row(b)[h * D + t] = dq;
   }
   lds_barrier();
-  rows_gemv_t(wr, L.b.dq + wave * WROWS, L.b.acc[wave], lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the W_q rows have landed
   lds_barrier();
   float* part = &L.b.acc[0][0];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int n = t + 256 * i;
-    part[n] = (L.b.acc[0][n] + L.b.acc[1][n]) + (L.b.acc[2][n] + L.b.acc[3][n]);
-  }
-  lds_barrier();
-  if (!publish_partial(part, p.ws, ctr(p, l, C_SA), b, h, t, &L.last)) return;
-  float* dx1 = bwd_field(p, G_DLN1, l, p.step).row(b);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int n = t + 256 * i;
-    st_sc1(dx1 + n, L.b.dx2p[n] + gather_partials(p.ws, b, n));
-  }
+  rows_t_lds(L.wo, L.b.dq, part);
+  if (!publish4(part, p.ws, ctr(p, l, C_SA), b, h, &L.last)) return;
+  if (t < E / 4) st4_sc1(bwd_field(p, G_DLN1, l, p.step).row(b), 4 * t, add4(lds4(L.b.dx2p + 4 * t), gather4(p.ws, b, t)));
   wg_arrive(ctr(p, l, C_X1) + b);
 }
 
 // ------------------------------------------------------------- backward: self-attention row b
 // dx1 (handed-off row) -> LN1' -> dsao -> dsav_h -> the last head writes dx0 = dx1p + sum_h W_v[h]^T dsav_h:
 // d x3 of layer l-1 (handed off), or (l = 0) the step input's gradient dx0 + dt.
-__device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, const uint4 (&wr)[NRI], SaL& L, uint64_t seed0,
-                           uint64_t seed1) {
+__device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, SaL& L, uint64_t seed0, uint64_t seed1) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
   float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
   if (t < E / 4) {
-    dy = ld4_sc1(bwd_field(p, G_DLN1, l, p.step).row(b) + 4 * t);
+    dy = ld4_sc1(bwd_field(p, G_DLN1, l, p.step).row(b), 4 * t);
     xr = *reinterpret_cast<const float4*>(fwd_field(p, F_X1P, l, p.step).row(b) + 4 * t);
     gm = *reinterpret_cast<const float4*>(W.g1 + 4 * t);
   }
@@ -1013,6 +1173,7 @@ __device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, const uint
   lds_barrier();
   slice_gemv_t(L.wo, L.dsao, &L.red64[0][0], wave, lane);
   lds_barrier();
+  rows_dma(reinterpret_cast<const f16*>(p.layer[l].wv), h, L.wo, wave, lane);   // W_v[h] rows in place of the W_o slice
   if (t < D) {
     float v = (L.red64[0][t] + L.red64[1][t]) + (L.red64[2][t] + L.red64[3][t]);
     if (p.drop_p > 0.f) v = drop1(v, p.drop_p, seed0, ((long long)b * E + h * D + t) / D);
@@ -1020,36 +1181,24 @@ __device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, const uint
     bwd_field(p, G_DSAV, l, p.step).row(b)[h * D + t] = v;
   }
   lds_barrier();
-  rows_gemv_t(wr, L.v + wave * WROWS, L.acc[wave], lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
   float* part = &L.acc[0][0];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int n = t + 256 * i;
-    part[n] = (L.acc[0][n] + L.acc[1][n]) + (L.acc[2][n] + L.acc[3][n]);
-  }
-  lds_barrier();
-  if (!publish_partial(part, p.ws + WS_SLAB, ctr(p, l, C_CA), b, h, t, &L.last)) return;
+  rows_t_lds(L.wo, L.v, part);
+  if (!publish4(part, p.ws + WS_SLAB, ctr(p, l, C_CA), b, h, &L.last)) return;
   if (l > 0) {
-    float* dx3 = bwd_field(p, G_DLN3, l - 1, p.step).row(b);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int n = t + 256 * i;
-      st_sc1(dx3 + n, L.dx1p[n] + gather_partials(p.ws + WS_SLAB, b, n));
-    }
+    if (t < E / 4)
+      st4_sc1(bwd_field(p, G_DLN3, l - 1, p.step).row(b), 4 * t, add4(lds4(L.dx1p + 4 * t), gather4(p.ws + WS_SLAB, b, t)));
     wg_arrive(ctr(p, l - 1, C_ROWS));
-  } else {
-    const float* dt = bwd_field(p, G_DCAO, p.n_layers, p.step).row(b);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int n = t + 256 * i;
-      p.ds_out[(long long)b * E + n] = L.dx1p[n] + gather_partials(p.ws + WS_SLAB, b, n) + ld_sc1(dt + n);
-    }
+  } else if (t < E / 4) {
+    const float4 dt = ld4_sc1(bwd_field(p, G_DCAO, p.n_layers, p.step).row(b), 4 * t);
+    *reinterpret_cast<float4*>(p.ds_out + (long long)b * E + 4 * t) = add4(add4(lds4(L.dx1p + 4 * t), gather4(p.ws + WS_SLAB, b, t)), dt);
   }
 }
 
-__global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, const uint64_t* rng_off) {
+__global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, const uint64_t* rng_off, unsigned long long* trace) {
   __shared__ __attribute__((aligned(16))) StepLds U;
+  __shared__ __attribute__((aligned(16))) RedL RD;
   __shared__ unsigned ok_word;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int G = gridDim.x, R = G / H;
@@ -1057,6 +1206,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
   const uint64_t roff = rng_off_now(rng_off);
   const int L_ = p.n_layers;
   // ---- tail: du = drop'(ds), dt = LN_f'(du) -> d x3 of the last layer
+  STEP_MARK(1, L_, 0);
   if (h == 0) {
     SaL& S = U.sa;
     const uint64_t st = tail_seed(p) + roff;
@@ -1077,8 +1227,8 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
       LnBwdLocal lnl = ln_row_bwd_local(dy, xr, gm, mu, rs, t);
       const float4 dx = ln_row_bwd(lnl, rs, S.red2, lane, wave);
       if (t < E / 4) {
-        st4_sc1(bwd_field(p, G_DCAO, L_, p.step).row(b) + 4 * t, dx);    // dt (read back by the layer-0 tail of this launch)
-        st4_sc1(bwd_field(p, G_DLN3, L_ - 1, p.step).row(b) + 4 * t, dx);
+        st4_sc1(bwd_field(p, G_DCAO, L_, p.step).row(b), 4 * t, dx);    // dt (read back by the layer-0 tail of this launch)
+        st4_sc1(bwd_field(p, G_DLN3, L_ - 1, p.step).row(b), 4 * t, dx);
       }
       wg_arrive(ctr(p, L_ - 1, C_ROWS));
     }
@@ -1087,44 +1237,54 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
     const LrceDecLayerW& W = p.layer[l];
     const uint64_t sl = layer_seed(p, l) + roff;
     // ---- FB: FFN slices over all rows
-    bool waited = false;
+    STEP_MARK(1, l, 0);
     for (int j = blockIdx.x; j < NF; j += G) {
-      if (!waited) {
-        if (!wg_wait(ctr(p, l, C_ROWS), p.B, p, 0x700 + l, &ok_word)) return;
-        waited = true;
-      }
-      ffn_bwd_slice(p, l, j, U.ff, sl + 4, sl + 5);
+      if (!ffn_bwd_slice(p, l, j, U.ff, sl + 4, sl + 5, j == (int)blockIdx.x ? ctr(p, l, C_ROWS) : nullptr, &ok_word)) return;
       wg_arrive(ctr(p, l, C_SL));
     }
-    // ---- CB: dx2 slices, then the cross-attention block backward per row
-    uint4 wr[NRI];
-    rows_load(reinterpret_cast<const f16*>(W.wq), h * D + wave * WROWS, lane, wr);
+    // ---- CB: dx2 slices, then the cross-attention block backward per row; the weight slices and the
+    // first row's saved operands / K / V images are issued before the wait for the FFN slices
+    CaL& C = U.ca;
+    lds_barrier();
+    slice_dma(reinterpret_cast<const f16*>(W.woc), h, C.wo, wave, lane);
+    CaBwdPre pre;
+    ca_bwd_prefetch(p, l, r, h, C, pre);
+    STEP_MARK(1, l, 2);
     if (!wg_wait(ctr(p, l, C_SL), NF, p, 0x800 + l, &ok_word)) return;
+    STEP_MARK(1, l, 3);
     for (int b = r; b < p.B; b += R)
       slice_reduce(p.ws + 2 * WS_SLAB, b, h, nullptr, 0.f, 0, p.ws + 2 * WS_SLAB + WS_P + (long long)b * E,
-                   bwd_field(p, G_DLN2, l, p.step).row(b), U.rd);
+                   bwd_field(p, G_DLN2, l, p.step).row(b), RD);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0)
       for (int b = r; b < p.B; b += R) __hip_atomic_fetch_add(ctr(p, l, C_X3) + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    CaL& C = U.ca;
-    lds_barrier();
-    slice_dma(reinterpret_cast<const f16*>(W.woc), h, C.wo, wave, lane);
+    bool first = true;
     for (int b = r; b < p.B; b += R) {
+      if (!first) {   // the previous row left W_q rows in the slice's place
+        slice_dma(reinterpret_cast<const f16*>(W.woc), h, C.wo, wave, lane);
+        ca_bwd_prefetch(p, l, b, h, C, pre);
+      }
       if (!wg_wait(ctr(p, l, C_X3) + b, H, p, 0x900 + l, &ok_word)) return;
-      ca_bwd_row(p, l, b, h, wr, C, sl + 2, sl + 3);
+      if (first) STEP_MARK(1, l, 4);
+      first = false;
+      ca_bwd_row(p, l, b, h, C, sl + 2, sl + 3, pre);
       lds_barrier();
     }
+    STEP_MARK(1, l, 5);
     // ---- SB: self-attention block backward per row
     SaL& S = U.sa;
-    lds_barrier();
-    rows_load(reinterpret_cast<const f16*>(W.wv), h * D + wave * WROWS, lane, wr);
-    slice_dma(reinterpret_cast<const f16*>(W.wo), h, S.wo, wave, lane);
+    first = true;
     for (int b = r; b < p.B; b += R) {
+      lds_barrier();
+      slice_dma(reinterpret_cast<const f16*>(W.wo), h, S.wo, wave, lane);
       if (!wg_wait(ctr(p, l, C_X1) + b, 1, p, 0xA00 + l, &ok_word)) return;
-      sa_bwd_row(p, l, b, h, wr, S, sl, sl + 1);
+      if (first) STEP_MARK(1, l, 6);
+      first = false;
+      sa_bwd_row(p, l, b, h, S, sl, sl + 1);
       lds_barrier();
     }
+    STEP_MARK(1, l, 7);
   }
   finish(p, &ok_word);
 }
@@ -1170,14 +1330,19 @@ extern "C" int lrce_dec_step_grid(int B) { return grid_for(B); }
 
 extern "C" int lrce_dec_step_fwd(const LrceDecStep* a, void* stream) {
   if (int rc = check(a, false)) return rc;
-  dec_step_fwd_kernel<<<grid_for(a->B), NT, 0, static_cast<hipStream_t>(stream)>>>(*a, lrce_rng_offset());
+  dec_step_fwd_kernel<<<grid_for(a->B), NT, 0, static_cast<hipStream_t>(stream)>>>(*a, lrce_rng_offset(), g_step_trace);
   return lrce_check_launch("dec_step_fwd");
 }
 
 extern "C" int lrce_dec_step_bwd(const LrceDecStep* a, void* stream) {
   if (int rc = check(a, true)) return rc;
-  dec_step_bwd_kernel<<<grid_for(a->B), NT, 0, static_cast<hipStream_t>(stream)>>>(*a, lrce_rng_offset());
+  dec_step_bwd_kernel<<<grid_for(a->B), NT, 0, static_cast<hipStream_t>(stream)>>>(*a, lrce_rng_offset(), g_step_trace);
   return lrce_check_launch("dec_step_bwd");
+}
+
+extern "C" int lrce_dec_step_set_trace(uint64_t* buf) {
+  g_step_trace = reinterpret_cast<unsigned long long*>(buf);
+  return LRCE_OK;
 }
 
 extern "C" int lrce_dec_step_reset(uint32_t* counters, uint32_t* status, void* stream) {

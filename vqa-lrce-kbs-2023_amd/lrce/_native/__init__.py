@@ -223,6 +223,7 @@ _SIGS = {
     "lrce_dec_step_ws_elems": [],
     "lrce_dec_step_counter_words": [],
     "lrce_dec_step_grid": [_I],
+    "lrce_dec_step_set_trace": [_P],
     "lrce_wattn_set_trace": [_P],
     "lrce_gemm_set_trace": [_P],
     "lrce_frames_resize": [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P],
