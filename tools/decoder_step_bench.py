@@ -75,17 +75,17 @@ def trace(B, task):
         valid = x[x > 0]
         t0 = valid.min()
         print(f"== {'forward' if d == 0 else 'backward'} (last launch), us from launch start: median / max over workgroups")
-        layers = range(13) if d == 0 else range(12, -1, -1)
+        layers = list(range(13) if d == 0 else range(12, -1, -1)) + [14]
         prev_end = None
         for l in layers:
             row = []
-            for i, nm in enumerate(names):
+            for i, nm in enumerate(names if l != 14 else [f"s{k}" for k in range(8)]):
                 v = x[:, l, i]
                 v = v[v > 0]
                 if len(v):
                     row.append(f"{nm} {(np.median(v) - t0) / 100:7.1f}/{(v.max() - t0) / 100:7.1f}")
             if row:
-                print(f"L{l:2d}  " + "  ".join(row))
+                print(f"L{l:2d}  " + "  ".join(row) if l != 14 else "FFN sub-phases of layer 1 (marks 0-7): " + "  ".join(row))
 
 
 def main():

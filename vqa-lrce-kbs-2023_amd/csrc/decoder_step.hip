@@ -196,6 +196,12 @@ __device__ __forceinline__ unsigned* ctr(const LrceDecStep& p, int l, int k) { r
 // Debug phase timestamps (lrce_dec_step_set_trace; NULL in production): thread 0 of workgroup w stores
 // s_memrealtime (100 MHz) at mark i of layer l into trace[((dir * 128 + w) * 16 + l) * 8 + i].
 unsigned long long* g_step_trace = nullptr;
+// sub-phase marks inside the FFN slices of layer 1 (slot 14 of the layer index)
+#define SUB_MARK(DIR, I)                                                                                  \
+  do {                                                                                                    \
+    if (trace && l == 1 && threadIdx.x == 0)                                                              \
+      trace[(((DIR) * 128 + blockIdx.x) * 16 + 14) * 8 + (I)] = __builtin_amdgcn_s_memrealtime();         \
+  } while (0)
 #define STEP_MARK_P(DIR, L, I) do { } while (0)
 #define STEP_MARK(DIR, L, I)                                                                              \
   do {                                                                                                    \
@@ -514,31 +520,66 @@ __device__ __forceinline__ void rows_to_lds(const float* src, int c0, int nr, Ff
 __device__ __forceinline__ float* xat(FfL& L, int rr, int k) { return L.x + rr * XROW + (k / 96) * XP + (k % 96); }
 
 // wave-per-row LayerNorm (forward) of the image rows in place; lane owns k = 12 lane .. 12 lane + 11
+// full-wave sum without LDS round trips (a __shfl_xor butterfly is six dependent ds_bpermute): DPP within
+// 16-lane rows, then the four row sums by v_readlane
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror
+  v += dpp_f<0x140>(v);   // row_mirror: every lane holds its 16-lane row's sum
+  // the four row sums through the scalar unit (uniform result, in row order)
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+// the four rows of a wave reduced together (independent chains: their latencies overlap)
+__device__ __forceinline__ void wave_sum_x4(float (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = wave_sum_dpp(v[q]);
+}
+
+// wave-per-row LayerNorm (forward) of the image rows in place, the wave's rows rr = wave + 4 q (q < 4)
+// processed together; lane owns k = 12 lane .. 12 lane + 11
 __device__ void ln_rows_fwd(FfL& L, int nr, const float* g, const float* be, float eps, float* mean_out, float* rstd_out,
                             float* y_rows /* sc1-stored copy or NULL */, int c0) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int rr = wave; rr < nr; rr += 4) {
-    float* xp = xat(L, rr, 12 * lane);
-    float4 v[3];
+  float4 v[4][3];
+  float s1[4], s2[4];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) v[i] = *reinterpret_cast<float4*>(xp + 4 * i);
-    float s = 0.f;
+  for (int q = 0; q < 4; ++q) {
+    const float* xp = xat(L, wave + 4 * q, 12 * lane);   // rows >= nr are zero
 #pragma unroll
-    for (int i = 0; i < 3; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-    const float mu = wave_sum(s) * (1.0f / E);
-    float s2 = 0.f;
+    for (int i = 0; i < 3; ++i) v[q][i] = *reinterpret_cast<const float4*>(xp + 4 * i);
+    s1[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) s1[q] += (v[q][i].x + v[q][i].y) + (v[q][i].z + v[q][i].w);
+  }
+  wave_sum_x4(s1);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float mu = s1[q] * (1.0f / E);
+    s2[q] = 0.f;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const float4 d = make_float4(v[i].x - mu, v[i].y - mu, v[i].z - mu, v[i].w - mu);
-      s2 += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+      const float4 d = make_float4(v[q][i].x - mu, v[q][i].y - mu, v[q][i].z - mu, v[q][i].w - mu);
+      s2[q] += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
     }
-    const float rs = rsqrtf(wave_sum(s2) * (1.0f / E) + eps);
+  }
+  wave_sum_x4(s2);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int rr = wave + 4 * q;
+    if (rr >= nr) break;
+    const float mu = s1[q] * (1.0f / E), rs = rsqrtf(s2[q] * (1.0f / E) + eps);
+    float* xp = xat(L, rr, 12 * lane);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int k = 12 * lane + 4 * i;
       const float4 gg = *reinterpret_cast<const float4*>(g + k), bb = *reinterpret_cast<const float4*>(be + k);
-      const float4 y = make_float4((v[i].x - mu) * rs * gg.x + bb.x, (v[i].y - mu) * rs * gg.y + bb.y,
-                                   (v[i].z - mu) * rs * gg.z + bb.z, (v[i].w - mu) * rs * gg.w + bb.w);
+      const float4 y = make_float4((v[q][i].x - mu) * rs * gg.x + bb.x, (v[q][i].y - mu) * rs * gg.y + bb.y,
+                                   (v[q][i].z - mu) * rs * gg.z + bb.z, (v[q][i].w - mu) * rs * gg.w + bb.w);
       *reinterpret_cast<float4*>(xp + 4 * i) = y;
       if (y_rows) st4_sc1(y_rows, (long long)(c0 + rr) * E + k, y);
     }
@@ -584,34 +625,37 @@ __device__ __forceinline__ void tiles_out(FfL& L, const f32x4 (&acc)[12], float*
   }
 }
 
+// the FFN slice's weights into LDS by DMA: W2[:, j*32 .. +32] -> [768][32] (row n = 4 chunks of 16 B) and
+// W1[j*32 .. +32][:] -> [32][768] (row c = 96 chunks); 12 + 12 instructions of 1 KB per wave.  The MFMA
+// B fragments are read from these images right before each use (nothing held in registers across a wait).
+__device__ __forceinline__ void ffn_slices_dma(const f16* w1, const f16* w2, int j, FfL& L, int wave, int lane) {
+  const uint32_t b2 = dec_lds_addr(L.w2s), b1 = dec_lds_addr(L.w1s);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const int ins = wave * 12 + i;
+    const int n = ins * 16 + (lane >> 2);
+    dec_glds(w2, (uint32_t)(((long long)n * FF + j * FS + (lane & 3) * 8) * 2), b2 + (uint32_t)ins * 1024u);
+    const int chunk = ins * 64 + lane;
+    dec_glds(w1, (uint32_t)(((long long)(j * FS + chunk / 96) * E + (chunk % 96) * 8) * 2), b1 + (uint32_t)ins * 1024u);
+  }
+}
+
 // Forward FFN slice j (32 hidden units) over all rows, 16 rows per chunk as the MFMA M dimension:
 // linear1 (wave = 16 hidden units x half of K, the halves added through LDS) -> + b1 -> pre, GELU,
 // dropout -> gd; linear2 partial (wave = 12 of the 48 output tiles, K = 32) -> P_j.  The weight
 // fragments are loaded before the wait (wait: the row counter, NULL for a second slice).
-__device__ bool ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, unsigned* wait, unsigned* ok_word) {
+__device__ bool ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, unsigned* wait, unsigned* ok_word,
+                              unsigned long long* trace) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
   const int ct = wave & 1, kh = wave >> 1;
   const LrceDecLayerW& W = p.layer[l];
   const f16* w1 = reinterpret_cast<const f16*>(W.w1);
   const f16* w2 = reinterpret_cast<const f16*>(W.w2);
-  uint2 b1f[24], b2f[12][2];
-  {
-    const f16* src = w1 + (long long)(j * FS + ct * 16 + col) * E + kh * 384 + 4 * kq;
-#pragma unroll
-    for (int s = 0; s < 24; ++s) b1f[s] = *reinterpret_cast<const uint2*>(src + 16 * s);
-#pragma unroll
-    for (int tt = 0; tt < 12; ++tt)
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        b2f[tt][q] = *reinterpret_cast<const uint2*>(w2 + (long long)((wave * 12 + tt) * 16 + col) * FF + j * FS + 16 * q + 4 * kq);
-  }
+  ffn_slices_dma(w1, w2, j, L, wave, lane);
   const float b1v = W.b1[j * FS + ct * 16 + col];
+  SUB_MARK(0, 0);
   if (wait && !wg_wait(wait, p.B, p, 0x400 + l, ok_word)) return false;
-  // keep the fragments in registers (hipcc would otherwise re-load them per use to save VGPRs)
-#pragma unroll
-  for (int s = 0; s < 24; ++s) PIN2(b1f[s]);
-#pragma unroll
-  for (int tt = 0; tt < 12; ++tt) { PIN2(b2f[tt][0]); PIN2(b2f[tt][1]); }
+  SUB_MARK(0, 1);
   Ar pre = fwd_field(p, F_PRE, l, p.step), gd = fwd_field(p, F_GD, l, p.step);
   const float* x2p = fwd_field(p, F_X2P, l, p.step).base;
   float* Pj = p.ws + 2 * WS_SLAB + (long long)j * MAXB * E;
@@ -620,15 +664,22 @@ __device__ bool ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     const int nr = min(RCH, p.B - c0);
     lds_barrier();   // the previous chunk's image is consumed
     rows_to_lds(x2p, c0, nr, L);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (first chunk) the weight slices have landed too
     lds_barrier();
+    SUB_MARK(0, 2);
     ln_rows_fwd(L, nr, W.g2, W.be2, p.eps, owner ? fwd_field(p, F_M2, l, p.step).base : nullptr,
                 owner ? fwd_field(p, F_R2, l, p.step).base : nullptr, owner ? fwd_field(p, F_X2, l, p.step).base : nullptr, c0);
     lds_barrier();
+    SUB_MARK(0, 3);
     // linear1 slice
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc4[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int s = 0; s < 24; ++s)
-      acc = mfma4(*reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq)), h4f(b1f[s]), acc);
+    for (int s = 0; s < 24; ++s)   // four independent accumulation chains
+      acc4[s & 3] = mfma4(*reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq)),
+                          h4f(*reinterpret_cast<const uint2*>(L.w1s + (ct * 16 + col) * E + kh * 384 + 16 * s + 4 * kq)), acc4[s & 3]);
+    f32x4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = (acc4[0][r] + acc4[1][r]) + (acc4[2][r] + acc4[3][r]);
     if (kh) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) L.kacc[ct][4 * kq + r][col] = acc[r];
@@ -650,6 +701,7 @@ __device__ bool ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
       }
     }
     lds_barrier();
+    SUB_MARK(0, 4);
     // linear2 partial: 12 output tiles per wave, K = the 32 hidden units
     f32x4 o[12];
 #pragma unroll
@@ -658,9 +710,12 @@ __device__ bool ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     for (int q = 0; q < 2; ++q) {
       const float4 a = *reinterpret_cast<const float4*>(&L.hb[col][16 * q + 4 * kq]);
 #pragma unroll
-      for (int tt = 0; tt < 12; ++tt) o[tt] = mfma4(a, h4f(b2f[tt][q]), o[tt]);
+      for (int tt = 0; tt < 12; ++tt)
+        o[tt] = mfma4(a, h4f(*reinterpret_cast<const uint2*>(L.w2s + ((wave * 12 + tt) * 16 + col) * FS + 16 * q + 4 * kq)), o[tt]);
     }
+    SUB_MARK(0, 5);
     tiles_out(L, o, Pj, c0, nr);
+    SUB_MARK(0, 6);
   }
   return true;
 }
@@ -748,8 +803,9 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
     STEP_MARK(0, l, 5);
     // ---- C: FFN slices over all rows
     for (int j = blockIdx.x; j < NF; j += G) {
-      if (!ffn_fwd_slice(p, l, j, U.ff, sl + 4, j == (int)blockIdx.x ? ctr(p, l, C_ROWS) : nullptr, &ok_word)) return;
+      if (!ffn_fwd_slice(p, l, j, U.ff, sl + 4, j == (int)blockIdx.x ? ctr(p, l, C_ROWS) : nullptr, &ok_word, trace)) return;
       wg_arrive(ctr(p, l, C_SL));
+      SUB_MARK(0, 7);
     }
     STEP_MARK(0, l, 7);
   }
@@ -816,32 +872,13 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
 // =============================================================================== backward
 // ---------------------------------------------------------------- backward: FFN slice j, all rows
 __device__ bool ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, uint64_t seed5, unsigned* wait,
-                              unsigned* ok_word) {
+                              unsigned* ok_word, unsigned long long* trace) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
   const int ct = wave & 1, kh = wave >> 1;
   const LrceDecLayerW& W = p.layer[l];
   const f16* w1 = reinterpret_cast<const f16*>(W.w1);
   const f16* w2 = reinterpret_cast<const f16*>(W.w2);
-  // W2[:, j*32 .. +32] -> LDS [768][32] (DMA: row n = 4 chunks of 16 B), W1[j*32 .. +32][:] -> LDS [32][768]
-  {
-    const uint32_t base = dec_lds_addr(L.w2s);
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      const int ins = wave * 12 + i;          // 48 instructions x 1 KB
-      const int n = ins * 16 + (lane >> 2);
-      dec_glds(w2, (uint32_t)(((long long)n * FF + j * FS + (lane & 3) * 8) * 2), base + (uint32_t)ins * 1024u);
-    }
-  }
-  {
-    // W1[j*32 .. +32][:] -> LDS [32][768]: row c = 96 chunks of 16 B, 48 instructions x 1 KB
-    const uint32_t base = dec_lds_addr(L.w1s);
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      const int ins = wave * 12 + i;
-      const int chunk = ins * 64 + lane;           // 3072 chunks: row chunk / 96, piece chunk % 96
-      dec_glds(w1, (uint32_t)(((long long)(j * FS + chunk / 96) * E + (chunk % 96) * 8) * 2), base + (uint32_t)ins * 1024u);
-    }
-  }
+  ffn_slices_dma(w1, w2, j, L, wave, lane);
   const Ar dln3 = bwd_field(p, G_DLN3, l, p.step), df = bwd_field(p, G_DF, l, p.step), dgp = bwd_field(p, G_DGP, l, p.step);
   const Ar x3p = fwd_field(p, F_X3P, l, p.step), m3 = fwd_field(p, F_M3, l, p.step), r3 = fwd_field(p, F_R3, l, p.step);
   const Ar pre = fwd_field(p, F_PRE, l, p.step);
@@ -854,71 +891,80 @@ __device__ bool ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     for (int i = t; i < nr * FS; i += NT) L.preb[i / FS][i % FS] = pre.row(c0 + i / FS)[j * FS + i % FS];
   };
   prefetch(0, min(RCH, p.B));
+  SUB_MARK(1, 0);
   if (wait && !wg_wait(wait, p.B, p, 0x700 + l, ok_word)) return false;
+  SUB_MARK(1, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slices and prefetches have landed (read after the next barrier)
   lds_barrier();
-  // B fragments from the LDS slices, once per slice: dgp (wave = 16 hidden units x half of the 768
-  // outputs): W2[n][j*32 + ct*16 + col], n = kh*384 + 16 s + 4 kq + e; Q (wave = 12 of the 48 column
-  // tiles): W1[j*32 + 16 s + 4 kq + e][tile*16 + col]
-  uint2 bdf[24], bqf[12][2];
-  auto pack4 = [](const f16* p0, int stride) {
+  auto pack4 = [](const f16* p0, int stride) {   // four fp16 down a column of an LDS image
     const unsigned a = __builtin_bit_cast(unsigned short, p0[0]), b = __builtin_bit_cast(unsigned short, p0[stride]);
     const unsigned c = __builtin_bit_cast(unsigned short, p0[2 * stride]), d = __builtin_bit_cast(unsigned short, p0[3 * stride]);
     return make_uint2(a | (b << 16), c | (d << 16));
   };
-#pragma unroll
-  for (int s = 0; s < 24; ++s) bdf[s] = pack4(L.w2s + (kh * 384 + 16 * s + 4 * kq) * FS + ct * 16 + col, FS);
-#pragma unroll
-  for (int tt = 0; tt < 12; ++tt)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) bqf[tt][q] = pack4(L.w1s + (16 * q + 4 * kq) * E + (wave * 12 + tt) * 16 + col, E);
+  SUB_MARK(1, 2);
   for (int c0 = 0; c0 < p.B; c0 += RCH) {
     const int nr = min(RCH, p.B - c0);
     lds_barrier();
     if (c0 > 0) prefetch(c0, nr);
     rows_to_lds(dln3.base, c0, nr, L);
     lds_barrier();
-    // LayerNorm-3 backward per row (wave per row), then the out-dropout backward -> df in the image
-    for (int q = 0; q < RCH / 4; ++q) {
-      const int rr = wave + 4 * q;
-      if (rr >= nr) break;
-      const int b = c0 + rr;
-      float* xp = xat(L, rr, 12 * lane);
-      const float mu = m3.row(b)[0], rs = r3.row(b)[0];
-      float4 xv[3];
+    SUB_MARK(1, 3);
+    // LayerNorm-3 backward per row (the wave's four rows together), then the out-dropout backward -> df
+    // in the image
+    {
+      float4 g[4][3], xh[4][3];
+      float s1[4], s2[4], rsq[4];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) xv[i] = *reinterpret_cast<const float4*>(x3p.row(b) + 12 * lane + 4 * i);
-      float4 g[3], xh[3];
-      float s1 = 0.f, s2 = 0.f;
+      for (int q = 0; q < 4; ++q) {
+        const int rr = wave + 4 * q, b = c0 + min(rr, nr - 1);
+        const float mu = m3.row(b)[0], rs = r3.row(b)[0];
+        rsq[q] = rs;
+        const float* xp = xat(L, rr, 12 * lane);
+        s1[q] = s2[q] = 0.f;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int k = 12 * lane + 4 * i;
-        const float4 dy = *reinterpret_cast<const float4*>(xp + 4 * i);
-        const float4 gm = *reinterpret_cast<const float4*>(W.g3 + k);
-        const float4 x = xv[i];
-        g[i] = make_float4(dy.x * gm.x, dy.y * gm.y, dy.z * gm.z, dy.w * gm.w);
-        xh[i] = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
-        s1 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
-        s2 += (g[i].x * xh[i].x + g[i].y * xh[i].y) + (g[i].z * xh[i].z + g[i].w * xh[i].w);
+        for (int i = 0; i < 3; ++i) {
+          const int k = 12 * lane + 4 * i;
+          const float4 dy = *reinterpret_cast<const float4*>(xp + 4 * i);   // zero for rows >= nr
+          const float4 gm = *reinterpret_cast<const float4*>(W.g3 + k);
+          const float4 x = *reinterpret_cast<const float4*>(x3p.row(b) + k);
+          g[q][i] = make_float4(dy.x * gm.x, dy.y * gm.y, dy.z * gm.z, dy.w * gm.w);
+          xh[q][i] = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+          s1[q] += (g[q][i].x + g[q][i].y) + (g[q][i].z + g[q][i].w);
+          s2[q] += (g[q][i].x * xh[q][i].x + g[q][i].y * xh[q][i].y) + (g[q][i].z * xh[q][i].z + g[q][i].w * xh[q][i].w);
+        }
       }
-      const float mg = wave_sum(s1) * (1.0f / E), mgx = wave_sum(s2) * (1.0f / E);
+      wave_sum_x4(s1);
+      wave_sum_x4(s2);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int k = 12 * lane + 4 * i;
-        float4 d = make_float4(rs * (g[i].x - mg - xh[i].x * mgx), rs * (g[i].y - mg - xh[i].y * mgx),
-                               rs * (g[i].z - mg - xh[i].z * mgx), rs * (g[i].w - mg - xh[i].w * mgx));
-        if (owner) st4_sc1(dres, (long long)b * E + k, d);
-        d = drop4(d, p.drop_p, seed5, (long long)b * E + k);
-        *reinterpret_cast<float4*>(xp + 4 * i) = d;
-        if (owner) *reinterpret_cast<float4*>(df.row(b) + k) = d;
+      for (int q = 0; q < 4; ++q) {
+        const int rr = wave + 4 * q;
+        if (rr >= nr) break;
+        const int b = c0 + rr;
+        const float rs = rsq[q], mg = s1[q] * (1.0f / E), mgx = s2[q] * (1.0f / E);
+        float* xp = xat(L, rr, 12 * lane);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int k = 12 * lane + 4 * i;
+          float4 d = make_float4(rs * (g[q][i].x - mg - xh[q][i].x * mgx), rs * (g[q][i].y - mg - xh[q][i].y * mgx),
+                                 rs * (g[q][i].z - mg - xh[q][i].z * mgx), rs * (g[q][i].w - mg - xh[q][i].w * mgx));
+          if (owner) st4_sc1(dres, (long long)b * E + k, d);
+          d = drop4(d, p.drop_p, seed5, (long long)b * E + k);
+          *reinterpret_cast<float4*>(xp + 4 * i) = d;
+          if (owner) *reinterpret_cast<float4*>(df.row(b) + k) = d;
+        }
       }
     }
     lds_barrier();
+    SUB_MARK(1, 4);
     // dgp = drop'(W2[:, slice]^T df) gelu'(pre)
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc4[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 24; ++s)
-      acc = mfma4(*reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq)), h4f(bdf[s]), acc);
+      acc4[s & 3] = mfma4(*reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq)),
+                          h4f(pack4(L.w2s + (kh * 384 + 16 * s + 4 * kq) * FS + ct * 16 + col, FS)), acc4[s & 3]);
+    f32x4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = (acc4[0][r] + acc4[1][r]) + (acc4[2][r] + acc4[3][r]);
     if (kh) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) L.kacc[ct][4 * kq + r][col] = acc[r];
@@ -947,9 +993,12 @@ __device__ bool ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     for (int q = 0; q < 2; ++q) {
       const float4 a = *reinterpret_cast<const float4*>(&L.hb[col][16 * q + 4 * kq]);
 #pragma unroll
-      for (int tt = 0; tt < 12; ++tt) o[tt] = mfma4(a, h4f(bqf[tt][q]), o[tt]);
+      for (int tt = 0; tt < 12; ++tt)
+        o[tt] = mfma4(a, h4f(pack4(L.w1s + (16 * q + 4 * kq) * E + (wave * 12 + tt) * 16 + col, E)), o[tt]);
     }
+    SUB_MARK(1, 5);
     tiles_out(L, o, Qj, c0, nr);
+    SUB_MARK(1, 6);
   }
   return true;
 }
@@ -1239,8 +1288,9 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
     // ---- FB: FFN slices over all rows
     STEP_MARK(1, l, 0);
     for (int j = blockIdx.x; j < NF; j += G) {
-      if (!ffn_bwd_slice(p, l, j, U.ff, sl + 4, sl + 5, j == (int)blockIdx.x ? ctr(p, l, C_ROWS) : nullptr, &ok_word)) return;
+      if (!ffn_bwd_slice(p, l, j, U.ff, sl + 4, sl + 5, j == (int)blockIdx.x ? ctr(p, l, C_ROWS) : nullptr, &ok_word, trace)) return;
       wg_arrive(ctr(p, l, C_SL));
+      SUB_MARK(1, 7);
     }
     // ---- CB: dx2 slices, then the cross-attention block backward per row; the weight slices and the
     // first row's saved operands / K / V images are issued before the wait for the FFN slices
