@@ -146,10 +146,8 @@ typedef struct LrceGemmItem {
  * 150, 187): each entry's 128 x 128 tiles run one K slice (no split-K slabs or reduce launch), the
  * entries' tiles form one grid.  Up to 80 entries and 8 distinct shapes per launch, one operand
  * format (f16) per launch, and the C / bias / alpha pointers of one launch within 8 GB of each other
- * (more: several launches).  Pointers 16-B aligned (alpha_dev 4-B).  progress: NULL, or one zeroed
- * uint32 per workgroup of all launches (sum over entries of tiles x split) for a bounded lockstep
- * throttle between workgroups dispatched one after another on an XCD (L2 reuse of shared panels). */
-int lrce_gemm_grouped(const LrceGemmItem* items, int n, int k, float alpha, uint32_t* progress, void* stream);
+ * (more: several launches).  Pointers 16-B aligned (alpha_dev 4-B). */
+int lrce_gemm_grouped(const LrceGemmItem* items, int n, int k, float alpha, void* stream);
 /* dst (=|+=) sum_s slabs[s * n + i] over s = 0 .. split-1 in that order (deterministic), for a batch of
  * items (a grouped split-K launch's weight / bias slabs).  n % 4 == 0, pointers 16-B aligned. */
 typedef struct LrceSlabSum {

@@ -52,9 +52,9 @@ def test_dev_only_work_skipping_variables_are_refused():
 
 
 def test_non_default_switches_are_recorded():
-    rc, lines, err = _run(["--gpus", "1", "--dry-run"], {"LRCE_DEC_KV_ASYNC": "0"})
+    rc, lines, err = _run(["--gpus", "1", "--dry-run"], {"LRCE_DEC_FUSED": "blocks"})
     assert rc == 0, err[-2000:]
-    assert json.loads(lines[0])["lrce_env"] == {"LRCE_DEC_KV_ASYNC": "0"}
+    assert json.loads(lines[0])["lrce_env"] == {"LRCE_DEC_FUSED": "blocks"}
 
 
 def test_product_reads_no_dev_only_variables():

@@ -145,7 +145,7 @@ def test_grouped_gemm_rejects_bad_items_without_launching(kw, msg):
     leading dims, operand format and alignment."""
     from lrce import _native as N
     items = (N.GemmItem * 2)(_gitem(N), _gitem(N, **kw))
-    assert N.lib().lrce_gemm_grouped(items, 2, 1000, 1.0, None, None) == 1
+    assert N.lib().lrce_gemm_grouped(items, 2, 1000, 1.0, None) == 1
     assert msg in N.lib().lrce_last_error(), N.lib().lrce_last_error()
 
 

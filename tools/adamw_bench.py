@@ -1,9 +1,8 @@
 #!/usr/bin/env python
 """AdamW launch over a BERT-sized flat buffer (dev tool, GPU): microseconds per launch and effective
-HBM rate (30 B per parameter: p, g, m, v read, p, m, v and the bf16 shadow written).  The variant is
-LRCE_ADAMW_VARIANT (read once per process by the library): run one process per variant.
+HBM rate (30 B per parameter: p, g, m, v read, p, m, v and the bf16 shadow written).
 
-    LRCE_ADAMW_VARIANT=1 python tools/adamw_bench.py [--params 110000000]
+    python tools/adamw_bench.py [--params 110000000]
 """
 import argparse
 import os
@@ -43,7 +42,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
-    print(f"variant {os.environ.get('LRCE_ADAMW_VARIANT', 'default')}: {n / 1e6:.0f} M params  {us:8.1f} us  "
+    print(f"adamw: {n / 1e6:.0f} M params  {us:8.1f} us  "
           f"{30.0 * n / us / 1e6:6.2f} TB/s (30 B/param)", flush=True)
 
 

@@ -3,7 +3,7 @@
 row x column shapes, isolated (HIP events over back-to-back launches), against torch's native
 layer_norm backward on the same shape.  Bytes are the algorithmic ones of the lrce call.
 
-    python tools/ln_bench.py [--iters 30]      (LRCE_LN_BWD_PERCU=0|k: grid A/B knob of layernorm.hip)
+    python tools/ln_bench.py [--iters 30]
 """
 import argparse
 import os

@@ -84,12 +84,6 @@ struct GemmPT : GemmP {
   int aoff[GPT];          // device alpha offset from p.alpha_dev (floats), -1: the launch's alpha
   const void* ta[GPT];
   const bf16* tb[GPT];
-  // lockstep throttle (or null): prog[wg] = the K phase (prog_ph K tiles) workgroup wg has reached; a
-  // workgroup more than one phase ahead of the one dispatched before it on its XCD (blockIdx.x - 8,
-  // always resident or done) sleeps, boundedly, so co-resident tiles reading the same panels stay
-  // within the L2's window of them
-  unsigned* prog;
-  int prog_ph;
 };
 static_assert(sizeof(GemmPT) <= 3840, "grouped GEMM tables must fit the kernel-argument block");
 template <bool PT>
@@ -825,19 +819,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(const GemmArg<PT> pa) 
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (kt == 0) GT_MARK(1);
-      if constexpr (PT) {
-        if (pa.prog && kt > 0 && threadIdx.x == 0 && kt % pa.prog_ph == 0) {
-          const unsigned ph = (unsigned)(kt / pa.prog_ph);
-          __hip_atomic_store(pa.prog + blockIdx.x, ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (blockIdx.x >= 8) {
-            const unsigned* prev = pa.prog + blockIdx.x - 8;
-            for (int it = 0; it < 128; ++it) {   // bounded: a throttle, never a dependency
-              if (__hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u >= ph) break;
-              __builtin_amdgcn_s_sleep(4);
-            }
-          }
-        }
-      }
       if (kt + NS - 1 < nfull) {
         const int nxt = cur == 0 ? NS - 1 : cur - 1;   // (kt + NS - 1) % NS
         ga.advance(); gb.advance();
@@ -851,10 +832,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_glds_kernel(const GemmArg<PT> pa) 
     }
     __builtin_amdgcn_s_barrier();   // every wave is done with every stage (tail / LDS epilogue reuse)
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PT) {
-      if (pa.prog && threadIdx.x == 0)   // done: never holds a successor back
-        __hip_atomic_store(pa.prog + blockIdx.x, 0x7FFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
   if (tail) {
     const int k0 = kb + nfull * BK;
@@ -1111,19 +1088,9 @@ __global__ void splitk_reduce_epi_kernel(const float* __restrict__ ws, int split
 // the one-thread-per-float4 reduce above with a few waves each walking every slab serially; here a
 // block is 64 float4 columns x 4 slice groups, each thread keeps 4 slab loads in flight, and the
 // groups meet in LDS.
-// slab reads: each slab element is read exactly once (NT: streaming hint, LRCE_RED_NT A/B)
-typedef float rf4 __attribute__((ext_vector_type(4)));
-template <bool NT>
-__device__ __forceinline__ float4 ld_slab(const float* q) {
-  if constexpr (NT) {
-    const rf4 t = __builtin_nontemporal_load(reinterpret_cast<const rf4*>(q));
-    return make_float4(t.x, t.y, t.z, t.w);
-  } else {
-    return *reinterpret_cast<const float4*>(q);
-  }
-}
+// slab reads: each slab element is read exactly once (a non-temporal hint measured no faster)
+__device__ __forceinline__ float4 ld_slab(const float* q) { return *reinterpret_cast<const float4*>(q); }
 
-template <bool NT>
 __global__ void __launch_bounds__(256) splitk_reduce_deep_kernel(const float* __restrict__ ws, int split, int m, int n,
                                                                  float* __restrict__ c, long long ldc) {
   const long long mn = (long long)m * n;
@@ -1134,13 +1101,13 @@ __global__ void __launch_bounds__(256) splitk_reduce_deep_kernel(const float* __
   if (e < mn) {
     int k = g;
     for (; k + 12 < split; k += 16) {
-      const float4 t0 = ld_slab<NT>(ws + k * mn + e);
-      const float4 t1 = ld_slab<NT>(ws + (k + 4) * mn + e);
-      const float4 t2 = ld_slab<NT>(ws + (k + 8) * mn + e);
-      const float4 t3 = ld_slab<NT>(ws + (k + 12) * mn + e);
+      const float4 t0 = ld_slab(ws + k * mn + e);
+      const float4 t1 = ld_slab(ws + (k + 4) * mn + e);
+      const float4 t2 = ld_slab(ws + (k + 8) * mn + e);
+      const float4 t3 = ld_slab(ws + (k + 12) * mn + e);
       add(t0); add(t1); add(t2); add(t3);
     }
-    for (; k < split; k += 4) add(ld_slab<NT>(ws + k * mn + e));
+    for (; k < split; k += 4) add(ld_slab(ws + k * mn + e));
   }
   __shared__ float4 red[4][64];
   red[g][lane] = s;
@@ -1164,9 +1131,6 @@ extern "C" int lrce_colsum(const void* x, int x_f32, const int32_t* row_map, int
 
 static int gemm_dispatch(const LrceGemmDesc* d, void* stream);
 static bool glds_ok(const LrceGemmDesc* d);
-static bool g_force_legacy_gemm = getenv("LRCE_LEGACY_GEMM") != nullptr;   // A/B switch for benchmarking
-static int g_gemm_tile = getenv("LRCE_GEMM_TILE") ? atoi(getenv("LRCE_GEMM_TILE")) : 0;   // 0 auto, 64, 128
-static bool g_red_nt = getenv("LRCE_RED_NT") && atoi(getenv("LRCE_RED_NT")) != 0;            // A/B knob
 bool lrce_gemm_f32_outer_ok(const LrceGemmDesc* d);
 
 extern "C" int lrce_gemm(const LrceGemmDesc* d, void* stream) {
@@ -1202,8 +1166,7 @@ static bool glds_ok(const LrceGemmDesc* d) {
   const long long ext_a = d->a_kmajor ? (long long)d->m * d->lda + d->k : (long long)d->k * d->lda + d->m;
   const long long ext_b = d->b_kmajor ? (long long)d->n * d->ldb + d->k : (long long)d->k * d->ldb + d->n;
   return !d->a_f32 && !d->b_f32 && al16(d->a) && al16(d->b) && (d->stride_a % 8 == 0) && (d->stride_b % 8 == 0) &&
-         (d->lda % 8 == 0) && (d->ldb % 8 == 0) && !d->a_map && ext_a * 2 < (1LL << 31) && ext_b * 2 < (1LL << 31) &&
-         !g_force_legacy_gemm;
+         (d->lda % 8 == 0) && (d->ldb % 8 == 0) && !d->a_map && ext_a * 2 < (1LL << 31) && ext_b * 2 < (1LL << 31);
 }
 
 static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
@@ -1257,8 +1220,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
   p.tiles_m = (d->m + BM - 1) / BM; p.tiles_n = (d->n + BN - 1) / BN;
   // grouped raster for the weight gradients (M-major A: split-K over tokens, 4-16 x 4-16 tiles per split,
   // 512x2048x17640 64.9 -> 58.0 us); the token-major forward / dX shapes measured 1-3 % better row-major
-  static const int g_group_m = getenv("LRCE_GEMM_GROUP_M") ? atoi(getenv("LRCE_GEMM_GROUP_M")) : 0;   // A/B knob
-  p.group_m = g_group_m > 0 ? g_group_m : (d->a_kmajor ? 1 : 4);
+  p.group_m = d->a_kmajor ? 1 : 4;
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   const bool out32 = d->flags & (LRCE_EPI_OUT_F32 | LRCE_EPI_ATOMIC | LRCE_EPI_ACCUM);
   p.vec = (d->n % 8 == 0) && (d->ldc % 8 == 0) && al16(d->c) && (d->stride_c % 8 == 0) && (d->scale_cols % 8 == 0) &&
@@ -1291,13 +1253,13 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     // 128x128 tiles when they give every CU work; 64x64 otherwise (small-M / small-N problems)
     const int t128 = p.tiles_m * p.tiles_n * d->batch * split;
     // (fused dropout: 64x64 tiles only — the one instantiation family that carries that epilogue)
-    const bool small = g_gemm_tile == 64 || (g_gemm_tile == 0 && t128 < 256) || p.drop_p > 0.f;
+    const bool small = t128 < 256 || p.drop_p > 0.f;
     // Taller tiles (K-major A only): 160 or 192 rows x 128 do 1.25x / 1.5x the work of a 128x128
     // tile, so they win when the 128-row tile count overshoots a round of the 2-blocks-per-CU grid.
     // Pick the height minimising rounds x rows (e.g. M 17 640, N 512: 552 -> 444 tiles in ONE round
     // at 160 rows; N 2048: 3 rounds of 192-row tiles beat 4 of 160 and 5 of 128).
     int tall_m = 0;
-    if (!small && d->a_kmajor && g_gemm_tile != 128) {
+    if (!small && d->a_kmajor) {
       const int slots = 2 * 256;
       const bool atomic_rows = (d->flags & LRCE_EPI_ATOMIC) && !p.ws;   // its LDS-slab epilogue wants an even row-block count
       long long best = (long long)((t128 + slots - 1) / slots) * 128;
@@ -1305,8 +1267,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
         if (h == 160 && atomic_rows) continue;
         const long long th = (long long)((d->m + h - 1) / h) * p.tiles_n * d->batch * split;
         const long long cost = (th + slots - 1) / slots * h;
-        if (g_gemm_tile == h || (g_gemm_tile == 0 && cost < best)) { best = cost; tall_m = h; }
-        if (g_gemm_tile == h) break;
+        if (cost < best) { best = cost; tall_m = h; }
       }
     }
     if (small) {
@@ -1352,7 +1313,6 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     // 64x64 tiles (small problems: few workgroups, each latency-bound on its operand stream) take a
     // 4-stage ring in the same 64 KB of LDS as two 128x128 stages, so three K tiles are in flight
     // per workgroup instead of one
-    static const int g_small_ns = getenv("LRCE_GEMM_SMALL_NS") ? atoi(getenv("LRCE_GEMM_SMALL_NS")) : 4;   // A/B knob
     auto launch_small = [&](auto nsc) {
       constexpr int S = decltype(nsc)::value;
       if (p.drop_p > 0.f) {
@@ -1375,7 +1335,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
       }
       return (int)LRCE_OK;
     };
-    if (small && (g_small_ns == 4 || p.drop_p > 0.f)) {
+    if (small) {
       if (int rc = launch_small(std::integral_constant<int, 4>{})) return rc;
     } else if (int rc = launch(std::integral_constant<int, 2>{})) {
       return rc;
@@ -1391,7 +1351,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
     } else if (p.ws) {
       const long long q4 = (long long)d->m * d->n / 4;
       if (split >= 8)
-        (g_red_nt ? splitk_reduce_deep_kernel<true> : splitk_reduce_deep_kernel<false>)<<<(unsigned)((q4 + 63) / 64), 256, 0, s>>>(
+        splitk_reduce_deep_kernel<<<(unsigned)((q4 + 63) / 64), 256, 0, s>>>(
             p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
       else
         splitk_reduce_kernel<<<(unsigned)((q4 + 255) / 256), 256, 0, s>>>(p.ws, split, d->m, d->n, static_cast<float*>(d->c), d->ldc);
@@ -1416,7 +1376,7 @@ static int gemm_dispatch(const LrceGemmDesc* d, void* stream) {
 // dY_e, B N-major = X_e, C_e f32), db_e[m] += sum_k dY_e[k][m] for entries with BIAS_GRAD.  One K slice
 // per tile (no split-K slabs, no reduce launch): the entries' summed tile count fills the chip.  All
 // entries share K (the token count) and alpha; up to GPT entries / GSH distinct shapes per launch.
-extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alpha, uint32_t* progress, void* stream) {
+extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alpha, void* stream) {
   if (n < 0 || (n > 0 && !it) || k <= 0) return lrce_fail(LRCE_E_ARG, "gemm_grouped: n=%d k=%d", n, k);
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   for (int i = 0; i < n; ++i) {
@@ -1504,9 +1464,6 @@ extern "C" int lrce_gemm_grouped(const LrceGemmItem* it, int n, int k, float alp
     }
     p.a = p.ta[0]; p.b = p.tb[0];
     p.m = p.sh[0].m; p.n = p.sh[0].n; p.tiles_m = p.sh[0].tiles_m; p.tiles_n = p.sh[0].tiles_n;
-    p.prog = progress;
-    p.prog_ph = 8;
-    if (progress) progress += tiles;   // the next launch's workgroups
     if (f16) gemm_glds_kernel<128, 128, false, false, true, 2, false, true><<<dim3(tiles, 1), NT, 0, s>>>(p);
     else gemm_glds_kernel<128, 128, false, false, false, 2, false, true><<<dim3(tiles, 1), NT, 0, s>>>(p);
     i = j;
@@ -1529,7 +1486,7 @@ extern "C" int lrce_gemm_ptr_batched(const LrceGemmDesc* d, const void* const* a
   for (int i = 0; i < n; ++i)
     items[i] = LrceGemmItem{a[i], b[i], static_cast<float*>(c[i]), bg ? const_cast<float*>(bias[i]) : nullptr,
                             nullptr, d->m, d->n, (int32_t)d->lda, (int32_t)d->ldb, (int32_t)d->ldc, d->flags, 0, 1, 0};
-  return lrce_gemm_grouped(items.data(), n, d->k, d->alpha, nullptr, stream);
+  return lrce_gemm_grouped(items.data(), n, d->k, d->alpha, stream);
 }
 
 // dst_i (=|+=) sum_s slabs_i[s][0..n_i) in slice order (the grouped launch's split-K weight gradients):
@@ -1544,7 +1501,6 @@ struct SlabSumArgs {
   int split[SLAB_ITEMS];
   int accum[SLAB_ITEMS];
 };
-template <bool NT>
 __global__ void __launch_bounds__(256) slab_sum_kernel(const SlabSumArgs a) {
   const long long total = a.start[a.items];
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < total; q += (long long)gridDim.x * 256) {
@@ -1553,9 +1509,9 @@ __global__ void __launch_bounds__(256) slab_sum_kernel(const SlabSumArgs a) {
     const long long i = (q - a.start[it]) * 4;
     const float* src = a.src[it] + i;
     const long long n = a.n[it];
-    float4 acc = ld_slab<NT>(src);
+    float4 acc = ld_slab(src);
     for (int sl = 1; sl < a.split[it]; ++sl) {
-      const float4 v = ld_slab<NT>(src + sl * n);
+      const float4 v = ld_slab(src + sl * n);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     float4* d = reinterpret_cast<float4*>(a.dst[it] + i);
@@ -1588,7 +1544,7 @@ extern "C" int lrce_slab_sum_grouped(const LrceSlabSum* items, int n, void* stre
     }
     a.start[a.items] = tot;
     const long long blocks = (tot + 255) / 256;
-    (g_red_nt ? slab_sum_kernel<true> : slab_sum_kernel<false>)<<<(int)(blocks < 2048 ? blocks : 2048), 256, 0, s>>>(a);
+    slab_sum_kernel<<<(int)(blocks < 2048 ? blocks : 2048), 256, 0, s>>>(a);
   }
   return lrce_check_launch("slab_sum_grouped");
 }

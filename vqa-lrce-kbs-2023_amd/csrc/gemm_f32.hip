@@ -765,11 +765,6 @@ __global__ void __launch_bounds__(LN_W * 64) skinny_ln_kernel(SkinnyP p, LnP q) 
 }  // namespace
 
 namespace {
-bool getenv_flag(const char* name) {
-  const char* v = getenv(name);
-  return v && *v && *v != '0';
-}
-
 // Per-device split-K scratch of the skinny kernel: partial tiles + zero-initialised arrival
 // counters (self-resetting).  Allocated once, outside stream capture; one stream per device uses it
 // at a time (kernels on one stream serialise), so reuse across launches is race-free.
@@ -860,8 +855,7 @@ int lrce_gemm_f32(const LrceGemmDesc* d, void* stream) {
       // ~192 workgroups (A/B on the full step: splitting the K = 768 linears too cost 0.4 %, K >= 2048 gained 1.4 %)
       int ks = 1;
       SkinnySplitWs* ws = nullptr;
-      static const int min_k = getenv("LRCE_SKINNY_MINK") ? atoi(getenv("LRCE_SKINNY_MINK")) : 2048;
-      if (tiles < 192 && d->k >= min_k && !getenv_flag("LRCE_SKINNY_NOSPLIT")) {
+      if (tiles < 192 && d->k >= 2048) {
         ks = std::min(std::min(4, d->k / 256), std::max(1, 192 / tiles));
         if (ks > 1 && !(ws = skinny_split_ws(st, tiles, ks, mt))) ks = 1;
       }

@@ -504,21 +504,15 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce_batched(LnRedBatch b) {
 // as many waves as rows); larger ones 4-8 with the next row prefetched.  (A chip-capacity grid —
 // one row per wave up to 2-8 resident blocks per CU — measured 5-25 % slower on the 15 680 x 512 and
 // 3 920 x 1024 shapes, 4 % faster on 62 720 rows: more blocks mean more dw / db partials to reduce;
-// tools/ln_bench.py, LRCE_LN_BWD_PERCU=k selects it for A/B.)  Without a partials workspace every
+// tools/ln_bench.py.)  Without a partials workspace every
 // block adds its dw/db into the SAME 2 x cols addresses, so blocks are capped.
 int ln_bwd_blocks(int rows, int lpr, bool ws, int cols) {
   const int rpb = 4 * (64 / lpr);                 // rows per block per pass
-  static const int knob = getenv("LRCE_LN_BWD_PERCU") ? atoi(getenv("LRCE_LN_BWD_PERCU")) : 0;   // A/B knob
-  if (ws && knob > 0) {
-    const int nb1 = (rows + rpb - 1) / rpb;
-    const int cap = 256 * knob > 2048 ? 2048 : 256 * knob;   // ln_bwd_reduce: <= LN_RED_MAXY * LN_RED_ROWS partial rows
-    return nb1 < 1 ? 1 : (nb1 > cap ? cap : nb1);
-  }
   // measured per row width (tools/ln_bench.py sweep, round 4): rows of <= 512 columns stream best
   // on a capped chip-wide grid — 1024 blocks at <= 256 columns, 768 at 512 (250 880 x 128: 116.5 ->
   // 112.6 us, 62 720 x 512: 123 -> 108 us) — wider rows with 4-8 rows per wave
   const int nch = cols / 4;
-  if (ws && rows > 8192 && nch <= 128 && knob == 0) {   // (knob -1: 4-8 rows per wave everywhere, for A/B)
+  if (ws && rows > 8192 && nch <= 128) {
     const int nb1 = (rows + rpb - 1) / rpb, cap = nch <= 64 ? 1024 : 768;
     return nb1 > cap ? cap : nb1;
   }
@@ -584,9 +578,8 @@ static int layernorm_bwd_impl(const void* dy, int dy_f32, const int32_t* dy_map,
                     ? workspace : nullptr;
   const int nb = (part || !want) ? nb_ws : ln_bwd_blocks(rows, lpr, false, cols);
   // non-temporal x / dres / dx on the large shapes only (tools/ln_bench.py: 250 880 x 128 and 62 720 x 512
-  // 113 -> 98 / 94 us; at <= 16 M elements the hint costs up to 15 %); LRCE_LN_NT=0 / 1 forces it
-  static const int nt_env = getenv("LRCE_LN_NT") ? atoi(getenv("LRCE_LN_NT")) : -1;
-  const bool nt = nt_env >= 0 ? nt_env != 0 : (long long)rows * cols >= (24LL << 20);
+  // 113 -> 98 / 94 us; at <= 16 M elements the hint costs up to 15 %)
+  const bool nt = (long long)rows * cols >= (24LL << 20);
 #define LNB3(TD, TX, CH, LPR)                                                                                          \
   (nt ? ln_bwd<TD, TX, CH, LPR, false, true> : ln_bwd<TD, TX, CH, LPR>)<<<nb, 256, 0, s>>>(                         \
       static_cast<const TD*>(dy), dy_map, static_cast<const TX*>(x), in_map, nseg, mean, rstd, w, dx, dres, dw, db, rows, \

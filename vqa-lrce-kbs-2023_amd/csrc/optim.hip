@@ -183,12 +183,11 @@ extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, con
   if (p_f16 && (f16_lo % 1024 || f16_hi % 1024 || f16_hi < f16_lo))
     return lrce_fail(LRCE_E_ARG, "adamw_step: f16 shadow range [%lld, %lld) not chunk aligned", (long long)f16_lo, (long long)f16_hi);
   if (n_chunks > 0) {
-    // variants (LRCE_ADAMW_VARIANT, A/B): 0 plain loads / stores, 2 chunks per wave; 1 non-temporal;
-    // 2 one chunk per wave; 3 both — the default: every operand is touched once per step, so the
-    // streaming hint keeps them from evicting L2 lines for nothing, and one chunk per wave doubles the
-    // waves in flight (tools/adamw_bench.py, 110 M parameters: 630 -> 515 us, 5.2 -> 6.4 TB/s)
-    static const int var = getenv("LRCE_ADAMW_VARIANT") ? atoi(getenv("LRCE_ADAMW_VARIANT")) : 3;
-    const int cpw = (var & 2) ? 1 : ADAMW_CPW;
+    // one chunk per wave with non-temporal loads / stores: every operand is touched once per step, so
+    // the streaming hint keeps them from evicting L2 lines for nothing, and one chunk per wave doubles
+    // the waves in flight (110 M parameters: 630 -> 515 us, 5.2 -> 6.4 TB/s against two chunks per
+    // wave with plain accesses)
+    const int cpw = 1;
     const dim3 grid((n_chunks + 4 * cpw - 1) / (4 * cpw));
     hipStream_t s = static_cast<hipStream_t>(stream);
     auto launch = [&](auto kern) {
@@ -197,12 +196,7 @@ extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, con
                                 reinterpret_cast<bf16*>(p_f16), f16_lo, f16_hi, reinterpret_cast<const bf16*>(g_bf16),
                                 sumsq_next ? chunk_sq : nullptr);
     };
-    switch (var & 3) {
-      case 1: launch(adamw_kernel<true, ADAMW_CPW>); break;
-      case 2: launch(adamw_kernel<false, 1>); break;
-      case 3: launch(adamw_kernel<true, 1>); break;
-      default: launch(adamw_kernel<false, ADAMW_CPW>); break;
-    }
+    launch(adamw_kernel<true, 1>);
   }
   if (sumsq_next && chunk_sq && tensor_chunk_off && n_tensors > 0)
     segsum_kernel<<<n_tensors, 256, 0, static_cast<hipStream_t>(stream)>>>(chunk_sq, tensor_chunk_off, n_tensors, sumsq_next);

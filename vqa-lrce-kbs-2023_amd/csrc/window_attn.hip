@@ -732,8 +732,7 @@ extern "C" int lrce_wattn_bwd(const uint16_t* qkv, const uint16_t* out, const ui
   while ((ba - wh * ww) % 32) ++ba;
   const int boff = (wd - 1) * ba + (wh - 1) * bb + (ww - 1);
   if (2 * boff + 1 > NBL) return lrce_fail(LRCE_E_ARG, "wattn_bwd: %d bank-spread bins > %d", 2 * boff + 1, NBL);
-  static const bool one_head = getenv("LRCE_WATTN_HPW1") != nullptr;   // A/B: one head per workgroup
-  const int hpw = (nH & 1) || one_head ? 1 : 2;
+  const int hpw = (nH & 1) ? 1 : 2;   // two heads per workgroup (one head each measured slower)
   const auto kern = bias_f16 ? (hpw == 2 ? wattn_bwd_kernel<true, 2> : wattn_bwd_kernel<true, 1>)
                              : (hpw == 2 ? wattn_bwd_kernel<false, 2> : wattn_bwd_kernel<false, 1>);
   kern<<<(unsigned)(n_win * nH / hpw), BW * 64 * hpw, 0, static_cast<hipStream_t>(stream)>>>(

@@ -191,7 +191,7 @@ _SIGS = {
     "lrce_gemm": [ctypes.POINTER(GemmDesc), _P],
     "lrce_gemm_ln": [ctypes.POINTER(GemmDesc), ctypes.POINTER(LnPrologue), _P],
     "lrce_gemm_ptr_batched": [ctypes.POINTER(GemmDesc), _P, _P, _P, _P, _I, _P],
-    "lrce_gemm_grouped": [ctypes.POINTER(GemmItem), _I, _I, _F, _P, _P],
+    "lrce_gemm_grouped": [ctypes.POINTER(GemmItem), _I, _I, _F, _P],
     "lrce_slab_sum_grouped": [ctypes.POINTER(SlabSum), _I, _P],
     "lrce_splitk_reduce_ln": [_P, _I, _I, _I, _P, _P, _I64, _F, _U64, _P, _P, _P, _F, _P, _P, _I, _P, _P, _P],
     "lrce_layernorm_fwd": [_P, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P, _P, _I, _I, _I, _P],

@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from .. import _native as N
 from .. import kernels as K
-from ..runtime import aux_stream, ensure
+from ..runtime import ensure
 
 HIDDEN, HEADS, INTER, VOCAB, MAXPOS, TYPES, EPS = 768, 12, 3072, 30522, 512, 2, 1e-12
 
@@ -148,15 +148,12 @@ class _Stack:
         self.flush_at = None
         # delayed gradient scales (lrce_layernorm_bwd_f16s): once a backward has computed every layer's
         # scales from its own maxima, each later step uses the previous step's (the reference's
-        # GradScaler likewise keeps one scale across steps); LRCE_BERT_DELAYED_SCALE=0: per-step scales
+        # GradScaler likewise keeps one scale across steps); _DELAYED_SCALE = False: per-step scales
         self.delayed = _DELAYED_SCALE and getattr(bert, "_lrce_scales_ready", False)
         self.done = []          # layer indices whose backward has run (their dY in dbuf)
-        # the layers' LayerNorm gamma / beta reductions, one batched launch at the flush (LRCE_BERT_LN_DEFER=0:
-        # one launch per LayerNorm); a gradient reducer hears of the layers only after that flush
-        self.red = K.DeferredGrads() if _LN_DEFER else None
-        # the upper half of the stack (layers >= mid) is flushed when the backward reaches layer mid, and
-        # its optimizer update ("text_hi", E2EBase.optimizer_groups) runs beside the lower half's backward
-        self.mid = n // 2 if _SPLIT_FLUSH else None
+        # the layers' LayerNorm gamma / beta reductions, one batched launch at the flush; a gradient
+        # reducer hears of the layers only after that flush
+        self.red = K.DeferredGrads()
 
     def fviews(self, i):
         return _views(self.fbuf[i], self.rows, (HIDDEN,) * 6 + (INTER,) * 2)
@@ -198,20 +195,13 @@ class _LayerFn(torch.autograd.Function):
         drop1 = (p, seed + 1, 1) if p > 0 else None
         drop2 = (p, seed + 2, 1) if p > 0 else None
         nxt = st.fviews(i + 1)[0] if i + 1 < st.n else None   # the next layer's fp16 input
-        if _REDUCE_LN:
-            # each output projection as split-K slabs + ONE reduce launch that also adds bias, dropout
-            # and residual and runs the post-norm LayerNorm (HF BertSelfOutput / BertOutput)
-            a2, h1, m1, r1 = K.linear_resid_ln(ctxt, w(ao.dense.weight), ao.dense.bias, x, drop1, ao.LayerNorm.weight,
-                                              ao.LayerNorm.bias, EPS, 3, out16=h1b)
-            K.linear(h1b, w(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre, out=g)
-            o2, out, m2, r2 = K.linear_resid_ln(g, w(oo.dense.weight), oo.dense.bias, h1, drop2, oo.LayerNorm.weight,
-                                               oo.LayerNorm.bias, EPS, 4, out16=nxt)
-        else:
-            a2 = K.linear(ctxt, w(ao.dense.weight), ao.dense.bias, out_f32=True, resid=x, drop=drop1)   # x + drop(a)
-            h1, m1, r1 = K.layernorm(a2, ao.LayerNorm.weight, ao.LayerNorm.bias, EPS, out_f32=True, bf16_copy=h1b)
-            K.linear(h1b, w(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre, out=g)
-            o2 = _proj_resid(g, w(oo.dense.weight), oo.dense.bias, h1, drop2)                # h1 + drop(g W2^T + b2)
-            out, m2, r2 = K.layernorm(o2, oo.LayerNorm.weight, oo.LayerNorm.bias, EPS, out_f32=True, bf16_copy=nxt)
+        # each output projection as split-K slabs + ONE reduce launch that also adds bias, dropout and
+        # residual and runs the post-norm LayerNorm (HF BertSelfOutput / BertOutput)
+        a2, h1, m1, r1 = K.linear_resid_ln(ctxt, w(ao.dense.weight), ao.dense.bias, x, drop1, ao.LayerNorm.weight,
+                                          ao.LayerNorm.bias, EPS, 3, out16=h1b)
+        K.linear(h1b, w(it.dense.weight), it.dense.bias, gelu=True, pre_out=pre, out=g)
+        o2, out, m2, r2 = K.linear_resid_ln(g, w(oo.dense.weight), oo.dense.bias, h1, drop2, oo.LayerNorm.weight,
+                                           oo.LayerNorm.bias, EPS, 4, out16=nxt)
         ctx.save = (mask, lse, a2, m1, r1, o2, m2, r2)
         ctx.desc = desc
         ctx.layer, ctx.flat, ctx.p, ctx.seed, ctx.B, ctx.L, ctx.st, ctx.i = layer, flat, p, seed, B, L, st, i
@@ -269,26 +259,9 @@ class _LayerFn(torch.autograd.Function):
         dx = _qkv_dx(dqkv, sa, w, da2, inv_a, rows, (cq, ck, cv))
         ctx.save = ctx.desc = None
         st.done.append(i)
-        if (i == st.mid and st.flush_at is not None and st.flush_at < i and flat.early_update is not None
-                and getattr(flat, "reducer", None) is None):
-            # upper half final: its weight gradients / LayerNorm sums now, and its AdamW on the decoder's
-            # weight-gradient stream (joined at the end of backward) while layers < mid run here
-            _flush_wgrads(st)
-            if st.red is not None:
-                st.red.flush(dx)
-                st.red = K.DeferredGrads()
-            for j in st.done:
-                flat.notify(st.bert.encoder.layer[j].parameters())
-            st.done = []
-            main = torch.cuda.current_stream(dx.device)
-            s = aux_stream(dx.device, "decoder_wgrad")
-            s.wait_stream(main)
-            with torch.cuda.stream(s):
-                flat.group_done("text_hi")
         if i == st.flush_at:
             _flush_wgrads(st)
-            if st.red is not None:
-                st.red.flush(dx)
+            st.red.flush(dx)
             for j in st.done:
                 flat.notify(st.bert.encoder.layer[j].parameters())
             # a full backward has set every scale: later steps may use delayed scales
@@ -312,7 +285,7 @@ def _qkv_dx(dqkv, sa, w, resid, inv_scale, rows, cols):
     weights when the three sit back to back in the fp16 shadow, else three accumulating GEMMs."""
     ws = [w(l.weight) for l in (sa.query, sa.key, sa.value)]
     lo = min(ws, key=lambda t: t.data_ptr())
-    if _QKV_DX_FUSED and sorted(t.data_ptr() - lo.data_ptr() for t in ws) == [0, 2 * HIDDEN * HIDDEN, 4 * HIDDEN * HIDDEN]:
+    if sorted(t.data_ptr() - lo.data_ptr() for t in ws) == [0, 2 * HIDDEN * HIDDEN, 4 * HIDDEN * HIDDEN]:
         wstack = torch.as_strided(lo, (3 * HIDDEN, HIDDEN), (HIDDEN, 1))
         return _dx_resid(dqkv, wstack, resid, inv_scale)
     dx = None
@@ -325,26 +298,6 @@ def _qkv_dx(dqkv, sa, w, resid, inv_scale, rows, cols):
     return dx
 
 
-_QKV_DX_FUSED = os.environ.get("LRCE_BERT_QKV_DX_FUSED", "1") != "0"   # A/B knob
-
-
-def _proj_resid(x, w, bias, resid, drop):
-    """resid + drop(x W^T + bias), f32, for the K = 3072 output projection of the 320-row text branch:
-    split-K slices of 768 into f32 slabs, then ONE reduce launch that adds the bias, draws the dropout
-    mask of lrce_dropout and adds the residual (a 60-workgroup grid with the whole K per workgroup is
-    bound by each workgroup's serial operand intake)."""
-    Kd = x.shape[1]
-    split = Kd // 768 if (_SPLIT_DX and Kd % 768 == 0 and Kd >= 1536) else 1
-    if split == 1:
-        return K.linear(x, w, bias, out_f32=True, resid=resid, drop=drop)
-    rows, n = x.shape[0], w.shape[0]
-    out = torch.empty(rows, n, dtype=torch.float32, device=x.device)
-    ws = torch.empty(split * rows * n, dtype=torch.float32, device=x.device)
-    K.gemm(x, w, out, rows, n, Kd, flags=N.EPI_BIAS | N.EPI_RESID | N.EPI_OUT_F32, bias=bias, aux=resid, ld_aux=n,
-           split_k=split, workspace=ws, drop=drop, f16=True)
-    return out
-
-
 def _dx_resid(dy, w, resid, inv_scale):
     """resid + inv_scale * (dY W) for a deep-K input gradient of the 320-row text branch (K = 2304 /
     3072): split-K slices of 768 (12 K tiles each) write f32 slabs and ONE reduce launch adds them INTO
@@ -352,7 +305,7 @@ def _dx_resid(dy, w, resid, inv_scale):
     the whole K per workgroup is bound by each workgroup's serial operand intake (36-48 K tiles); the
     slices put 180-240 workgroups on the chip."""
     Kd = w.shape[0]
-    split = Kd // 768 if (_SPLIT_DX and Kd % 768 == 0 and Kd >= 1536) else 1
+    split = Kd // 768 if (Kd % 768 == 0 and Kd >= 1536) else 1
     if split == 1:
         return K.linear_dx(dy, w, resid=resid, alpha_dev=inv_scale)
     rows, n = dy.shape[0], w.shape[1]
@@ -360,9 +313,6 @@ def _dx_resid(dy, w, resid, inv_scale):
     K.gemm(dy, w, resid, rows, n, Kd, a_kmajor=True, b_kmajor=False, lda=dy.stride(0), ldb=n, ldc=n,
            flags=N.EPI_ATOMIC, split_k=split, workspace=ws, f16=True, alpha_dev=inv_scale)
     return resid
-
-
-_SPLIT_DX = os.environ.get("LRCE_BERT_SPLIT_DX", "1") != "0"   # A/B knob
 
 
 def _qkv(xb, sa, w, q, k, v, rows):
@@ -375,7 +325,7 @@ def _qkv(xb, sa, w, q, k, v, rows):
     sw = [(ws[i + 1].data_ptr() - ws[i].data_ptr()) // es for i in range(2)]
     sb = [(lins[i + 1].bias.data_ptr() - lins[i].bias.data_ptr()) // 4 for i in range(2)]
     sc = [(o2.data_ptr() - o1.data_ptr()) // es for o1, o2 in ((q, k), (k, v))]
-    if _QKV_BATCHED and sw[0] == sw[1] == sb[0] == sb[1] and sc[0] == sc[1] == rows * HIDDEN and sw[0] != 0:
+    if sw[0] == sw[1] == sb[0] == sb[1] and sc[0] == sc[1] == rows * HIDDEN and sw[0] != 0:
         if sw[0] > 0:
             K.gemm(xb, ws[0], q, rows, HIDDEN, HIDDEN, flags=N.EPI_BIAS, bias=lins[0].bias, batch=3, stride_b=sw[0],
                    stride_c=sc[0], stride_bias=sb[0], f16=True)
@@ -385,9 +335,6 @@ def _qkv(xb, sa, w, q, k, v, rows):
         return
     for lin, wt, o in zip(lins, ws, (q, k, v)):
         K.linear(xb, wt, lin.bias, out=o)
-
-
-_QKV_BATCHED = os.environ.get("LRCE_BERT_QKV_BATCHED", "1") != "0"   # A/B knob
 
 
 def _views(buf, rows, widths):
@@ -436,25 +383,11 @@ def _flush_wgrads(st):
     flat = st.flat
     layers = sorted(st.done)
     items = {i: _wgrad_items(st, i) for i in layers}
-    if _WGRAD_GROUPED:
-        # every layer's six products as ONE grouped launch (per-entry shape, scale slot and freshness)
-        todo = []
-        for i in layers:
-            for lin, dy, x, slot in items[i]:
-                gw, gb = _g(flat, lin.weight), _g(flat, lin.bias)
-                if gw is None or gb is None:
-                    _wgrad(flat, lin, dy, x, st.scales[i, slot, 1:2])
-                    continue
-                fresh = flat.claim_fresh([lin.weight, lin.bias]) and _STORE_FRESH
-                todo.append((dy, x, gw, gb, fresh, st.scales[i, slot, 1:2]))
-        if todo:
-            K.linear_dw_grouped(todo)
-        return
     for j in range(6):
         per = [(i,) + items[i][j] for i in layers]          # (layer, lin, dy, x, slot)
         gws = [_g(flat, lin.weight) for _, lin, _, _, _ in per]
         gbs = [_g(flat, lin.bias) for _, lin, _, _, _ in per]
-        if _WGRAD_BATCHED and len(per) > 1 and all(t is not None for t in gws + gbs):
+        if len(per) > 1 and all(t is not None for t in gws + gbs):
             order = sorted(range(len(per)), key=lambda t: gws[t].data_ptr())
             seq = [per[t] for t in order]
             gw, gb = [gws[t] for t in order], [gbs[t] for t in order]
@@ -478,13 +411,10 @@ def _flush_wgrads(st):
             _wgrad(flat, lin, dy, x, st.scales[i, slot, 1:2])
 
 
-_WGRAD_BATCHED = os.environ.get("LRCE_BERT_WGRAD_BATCHED", "1") != "0"   # A/B knob
-_WGRAD_GROUPED = os.environ.get("LRCE_BERT_WGRAD_GROUPED", "0") == "1"   # A/B knob (one grouped launch): within noise, off
-_LN_DEFER = os.environ.get("LRCE_BERT_LN_DEFER", "1") != "0"             # A/B knob
-_REDUCE_LN = os.environ.get("LRCE_BERT_REDUCE_LN", "1") != "0"           # A/B knob (linear_resid_ln)
-_STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"      # A/B knob (see FlatParams.claim_fresh)
-_DELAYED_SCALE = os.environ.get("LRCE_BERT_DELAYED_SCALE", "1") != "0"   # A/B knob
-_SPLIT_FLUSH = os.environ.get("LRCE_BERT_SPLIT_FLUSH", "0") == "1"       # A/B knob (upper half updated early): not faster, off
+# module switches (tests compare both settings): a batched weight gradient known to start from zero is
+# stored, not added (FlatParams.claim_fresh); delayed gradient scales (_Stack.delayed)
+_STORE_FRESH = True
+_DELAYED_SCALE = True
 
 
 def _uniform_stride(ts, es):
@@ -520,17 +450,6 @@ class BertModel(nn.Module):
         return list(self.encoder.parameters())
 
     def forward(self, input_ids, attention_mask=None, token_type_ids=None, join_token=None):
-        gen = self.forward_steps(input_ids, attention_mask, token_type_ids, join_token)
-        while True:
-            try:
-                next(gen)
-            except StopIteration as e:
-                return e.value
-
-    def forward_steps(self, input_ids, attention_mask=None, token_type_ids=None, join_token=None):
-        """forward() as a generator that yields after the embeddings and after every layer (its value is
-        the output, returned through StopIteration): a caller can interleave the text branch's launches
-        with another branch's, which decides how the HIP graph executor overlaps them (E2EBase)."""
         flat = ensure(self)
         B, L = input_ids.shape
         dev = input_ids.device
@@ -542,13 +461,11 @@ class BertModel(nn.Module):
         anchor = [t for t in self.embeddings.parameters()]
         x = _EmbedFn.apply(ids, types, self.embeddings, flat, p, seed, join_token, *anchor)
         st = _Stack(self, flat, B * L, dev)
-        yield
         for i, layer in enumerate(self.encoder.layer):
             params = list(layer.parameters())
             if st.flush_at is None and torch.is_grad_enabled() and (x.requires_grad or any(q.requires_grad for q in params)):
                 st.flush_at = i      # the last layer backward to run issues the deferred weight gradients
             x = _LayerFn.apply(x, mask, layer, flat, p, seed + 16 * (i + 1), B, L, st, i, *params)
-            yield
         return x.view(B, L, HIDDEN)
 
 
@@ -609,7 +526,3 @@ class TextExtractor(nn.Module):
 
     def forward(self, input_ids, attention_mask, token_type_ids, join_token=None):
         return self.bert(input_ids, attention_mask, token_type_ids, join_token=join_token)
-
-    def forward_steps(self, input_ids, attention_mask, token_type_ids, join_token=None):
-        """BertModel.forward_steps: the forward as a generator (one step per layer)."""
-        return self.bert.forward_steps(input_ids, attention_mask, token_type_ids, join_token=join_token)

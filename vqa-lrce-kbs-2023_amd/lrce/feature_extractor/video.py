@@ -39,9 +39,8 @@ class VideoExtractor(nn.Module):
             warnings.warn(f"Swin checkpoint {ckpt_path} not found: the video backbone keeps its random "
                           "initialisation", stacklevel=2)
 
-    def forward(self, clips, between_blocks=None):
-        """clips (B, S, T, 3, H, W) f32 in [0,1] -> (B, S, (T+1)//2, (H//32)*(W//32), 1024).
-        between_blocks: optional callable run after each Swin block's launches (launch interleaving)."""
+    def forward(self, clips):
+        """clips (B, S, T, 3, H, W) f32 in [0,1] -> (B, S, (T+1)//2, (H//32)*(W//32), 1024)."""
         B, S = clips.shape[:2]
-        feats, (nc, D, h, w) = self.swin.forward_tokens(clips.contiguous(), between_blocks=between_blocks)
+        feats, (nc, D, h, w) = self.swin.forward_tokens(clips.contiguous())
         return feats.view(B, S, D, h * w, feats.shape[-1])

@@ -15,9 +15,6 @@ execution:
 * one autograd Function per block (forward 6 launches, backward 15) with gradients accumulated
   straight into the flat parameter store (lrce/flat.py).
 """
-import math
-import os
-from functools import lru_cache
 
 import torch
 import torch.nn as nn
@@ -268,8 +265,8 @@ class _PatchEmbedFn(torch.autograd.Function):
 
 
 # LayerNorm-backward input gradients of rows this wide or wider stay f32 (the LN backward's bf16 loads
-# measured slower there, tools/ln_bench.py); LRCE_LN_F32_WIDE overrides (A/B)
-_LN_F32_WIDE = int(os.environ.get("LRCE_LN_F32_WIDE", "1024"))
+# measured slower there, tools/ln_bench.py)
+_LN_F32_WIDE = 1024
 
 
 def _drop_path_scale(rate, nc, device, training):
@@ -352,11 +349,12 @@ class _Handoff:
         return dx16
 
 
-_DEFER_REDUCTIONS = os.environ.get("LRCE_SWIN_DEFER_RED", "1") != "0"   # A/B knob
-# with the reductions deferred, the blocks' weight gradients too: one launch per linear for the stage
-_DEFER_WGRAD = os.environ.get("LRCE_SWIN_DEFER_WGRAD", "1") != "0"      # A/B knob
+# (module switches the tests turn off to compare against the per-block launches)
+_DEFER_REDUCTIONS = True
+# with the reductions deferred, the blocks' weight gradients too: one grouped launch for the stage
+_DEFER_WGRAD = True
 # a deferred weight gradient known to start from zero is stored, not added (FlatParams.claim_fresh)
-_STORE_FRESH = os.environ.get("LRCE_STORE_FRESH_GRADS", "1") != "0"     # A/B knob
+_STORE_FRESH = True
 
 
 def _stage_deferral(blocks, flat):
@@ -367,8 +365,6 @@ def _stage_deferral(blocks, flat):
     together, at that flush (a bucket's exchange starts then, instead of block by block)."""
     if not _DEFER_REDUCTIONS or not torch.is_grad_enabled():
         return None
-    if getattr(flat, "reducer", None) is not None and not _DEFER_WITH_REDUCER:
-        return None
     if not any(p.requires_grad for p in blocks[0].parameters()):
         return None
     d = K.DeferredGrads(len(blocks))
@@ -376,10 +372,9 @@ def _stage_deferral(blocks, flat):
     return d
 
 
-def _run_blocks(blocks, x, geo, flat, scales, tiles=None, between=None):
+def _run_blocks(blocks, x, geo, flat, scales, tiles=None):
     """The blocks of one stage in order; scales [(dp1, dp2)] per block (None entries in eval);
-    tiles: per block the (forward, backward) bias tiles built ahead (_prebuild_bias_tiles) or None;
-    between: optional callable run after each block's launches."""
+    tiles: per block the (forward, backward) bias tiles built ahead (_prebuild_bias_tiles) or None."""
     links = [None] + [_Handoff(scales[j - 1][1]) if _HANDOFF else None for j in range(1, len(blocks))]
     red = _stage_deferral(blocks, flat)
     for j, blk in enumerate(blocks):
@@ -387,8 +382,6 @@ def _run_blocks(blocks, x, geo, flat, scales, tiles=None, between=None):
         x = _SwinBlockFn.apply(x, blk, geo, flat, dp1, dp2, links[j], links[j + 1] if j + 1 < len(blocks) else None,
                                tiles[j] if tiles is not None else None, (red, j == 0) if red is not None else None,
                                *blk.parameters())
-        if between is not None:
-            between()
     return x
 
 
@@ -406,10 +399,6 @@ def _bias_tiles(blk, geo):
     K.wattn_bias_build(blk.attn.relative_position_bias_table, blk.attn.relative_position_index, geo.n, nH, region,
                        n_pat, bias_f, bias_b)
     return bias_f, bias_b
-
-
-_PREBUILD_BIAS = os.environ.get("LRCE_SWIN_BIAS_PREBUILD", "1") != "0"   # A/B knob
-_DEFER_WITH_REDUCER = os.environ.get("LRCE_DEFER_WITH_REDUCER", "1") != "0"   # A/B knob (data parallel)
 
 
 def _prebuild_bias_tiles(stages, dev):
@@ -634,7 +623,7 @@ class SwinTransformer3D(nn.Module):
         for i, layer in enumerate(self.layers):
             object.__setattr__(layer.blocks[0], "_lrce_group", f"swin{i}" if i > 0 else None)
 
-    def forward_tokens(self, clips, layout="BSTCHW", normalize=True, between_blocks=None):
+    def forward_tokens(self, clips, layout="BSTCHW", normalize=True):
         """clips (B,S,T,3,H,W) f32 in [0,1] (normalised in-kernel) or (B,3,T,H,W) already normalised.
         Returns (features f32 [n_clips*D'*H'*W', C_out], (n_clips, D', H', W'))."""
         flat = ensure(self)
@@ -654,7 +643,7 @@ class SwinTransformer3D(nn.Module):
             if layer.downsample is not None:
                 h, w = (h + 1) // 2, (w + 1) // 2
         pre = (_prebuild_bias_tiles([(list(layer.blocks), g) for layer, g in zip(self.layers, geos)], dev)
-               if _PREBUILD_BIAS and dev.type == "cuda" else None)
+               if dev.type == "cuda" else None)
         bi = 0
         for li, layer in enumerate(self.layers):
             if li == self.split_at and torch.is_grad_enabled() and x.requires_grad:
@@ -663,8 +652,6 @@ class SwinTransformer3D(nn.Module):
                 x = x_leaf
             geo = geos[li]
             nb = len(layer.blocks)
-            if li == 2 and getattr(flat, "pending_clear_at", None) == "swin3":
-                flat.pending_clear()   # the step's gradient clear beside stage 3's MFMA-bound GEMMs (optim.zero_grad)
             tiles = None
             if pre is not None:
                 tiles, ev = pre[li]
@@ -672,7 +659,7 @@ class SwinTransformer3D(nn.Module):
             blocks = list(layer.blocks)
             x = _run_blocks(blocks, x, geo, flat,
                             scales[bi:bi + len(blocks)] if scales is not None else [(None, None)] * len(blocks),
-                            tiles[:len(blocks)] if tiles is not None else None, between=between_blocks)
+                            tiles[:len(blocks)] if tiles is not None else None)
             bi += nb
             if layer.downsample is not None:
                 x = _PatchMergeFn.apply(x, layer.downsample, geo, flat, *layer.downsample.parameters())

@@ -25,8 +25,6 @@ class FlatParams:
             self.params = list(order)
         self.reducer = None          # notify target during a backward (lrce/distributed.py)
         self.early_update = None     # optimizer hook: a parameter group's gradients are final (optim.py)
-        self.pending_clear = None    # a deferred gradient clear (FusedAdamW.zero_grad) and where it is issued
-        self.pending_clear_at = None
         self.step_begin_hook = None  # optimizer hook: a training forward starts (optim.py)
         self.grad_reducer = None     # its GradReducer, whose reduced gradient the optimizer reads
         self.names = {id(p): n for n, p in module.named_parameters()}

@@ -6,7 +6,6 @@ Conventions: activations are 2-D row-major [rows, features]; weights are nn.Line
 """
 import ctypes
 import math
-import os
 
 import torch
 
@@ -17,8 +16,8 @@ BF16 = torch.bfloat16
 F16 = torch.float16
 F32 = torch.float32
 NUM_CU = 256
-_SPLIT_PER_CU = float(os.environ.get("LRCE_SPLITK_PER_CU", "2"))   # A/B knob: split-K blocks per CU
-_SPLIT_MIN_DEPTH = int(os.environ.get("LRCE_SPLITK_MIN_DEPTH", "1024"))   # A/B knob: shallowest K slice
+_SPLIT_PER_CU = 2            # split-K blocks per CU
+_SPLIT_MIN_DEPTH = 1024       # shallowest K slice
 
 
 class KernelTimer:
@@ -393,13 +392,8 @@ def linear_dw_grouped(items, split=1):
         flops += 2.0 * O * I * T
     dw0 = items[0][2]
 
-    prog = None
-    if _DW_LOCKSTEP:
-        wgs = sum(-(-it[2].shape[0] // 128) * -(-it[2].shape[1] // 128) for it in items) * max(split, 1)
-        prog = torch.zeros(wgs, dtype=torch.int32, device=dev)
-
     def run():
-        call("lrce_gemm_grouped", arr, len(items), T, 1.0, ptr(prog), stream_of(dw0))
+        call("lrce_gemm_grouped", arr, len(items), T, 1.0, stream_of(dw0))
         if split > 1:
             call("lrce_slab_sum_grouped", sums, nsum, stream_of(dw0))
     _timed("gemm", dw0, run, flops=flops, key=("grouped", T, len(items), split))
@@ -453,12 +447,6 @@ def layernorm_bwd(dy, x, mean, rstd, w, dx, *, dy_map=None, in_map=None, nseg=1,
     return out
 
 
-_GROUPED_DW = os.environ.get("LRCE_GROUPED_DW", "1") != "0"   # A/B knob: one grouped launch vs one per shape
-_SPLIT_DW = os.environ.get("LRCE_SPLIT_DW", "1") != "0"       # A/B knob: long-K stages deferred as split slabs
-_SHORT_SPLIT = int(os.environ.get("LRCE_DW_SHORT_SPLIT", "1"))   # A/B knob: K slices of the short-K stages (3-4)
-_DW_LOCKSTEP = os.environ.get("LRCE_DW_LOCKSTEP", "0") == "1"   # A/B knob: lrce_gemm_grouped progress throttle
-
-
 class DeferredGrads:
     """Parameter-gradient reductions that nothing downstream reads before the optimizer, collected over
     several blocks and issued as batched launches by flush(): LayerNorm gamma / beta sums
@@ -476,28 +464,21 @@ class DeferredGrads:
         grouped launch (stage 4's 1024 x 1024 projection: 2 x 64)."""
         tiles = -(-out_f // 128) * -(-in_f // 128)
         if tokens > 32768:
-            return _GROUPED_DW and _SPLIT_DW   # split-K slabs in the grouped launch (stages 1 and 2)
-        return tiles * self.n_items >= (64 if _GROUPED_DW else 256)
+            return True   # split-K slabs in the grouped launch (stages 1 and 2)
+        return tiles * self.n_items >= 64
 
     def flush(self, stream_tensor):
         if self.dw:
             # every deferred weight gradient (the stage's linears x blocks, same tokens) in one grouped grid
-            if _GROUPED_DW:
-                by_t = {}   # (blocks of a padded stage may differ in token count: one grid per count)
-                for it in self.dw:
-                    by_t.setdefault((it[1].shape[0], it[0].dtype), []).append(it)
-                for (T, _), items in by_t.items():
-                    split = _SHORT_SPLIT
-                    if T > 32768:   # a few tiles over a long K: slices so the grid fills ~one round of the chip
-                        tiles = sum(-(-it[2].shape[0] // 128) * -(-it[2].shape[1] // 128) for it in items)
-                        split = max(2, min(64, round(512 / tiles)))
-                    linear_dw_grouped(items, split=split)
-            else:
-                groups = {}
-                for it in self.dw:
-                    groups.setdefault((tuple(it[0].shape), tuple(it[1].shape), it[3] is not None, it[4]), []).append(it[:4])
-                for key, items in groups.items():
-                    linear_dw_batched(items, store=key[3])
+            by_t = {}   # (blocks of a padded stage may differ in token count: one grid per count)
+            for it in self.dw:
+                by_t.setdefault((it[1].shape[0], it[0].dtype), []).append(it)
+            for (T, _), items in by_t.items():
+                split = 1
+                if T > 32768:   # a few tiles over a long K: slices so the grid fills ~one round of the chip
+                    tiles = sum(-(-it[2].shape[0] // 128) * -(-it[2].shape[1] // 128) for it in items)
+                    split = max(2, min(64, round(512 / tiles)))
+                linear_dw_grouped(items, split=split)
         if self.ln:
             n = len(self.ln)
             arr = lambda vals, t: (t * n)(*vals)  # noqa: E731

@@ -10,7 +10,6 @@ arguments swin_ckpt / bert_dir; None = random initialisation on purpose), warns 
 touches the network, and exposes `pretrained_loaded` so the training CLI can refuse a real run that
 would start from random backbones.
 """
-import os
 from typing import Iterable, List
 
 import torch
@@ -21,12 +20,6 @@ from ..feature_extractor.video import VideoExtractor, SWIN_B_CKPT
 from .. import kernels as K
 from ..runtime import prepare, side_stream
 from .fusionv3 import LRCEOpenEnded, LRCEMultipleChoice, LRCECount
-
-
-# Interleave the text branch's launches with the video branch's (one BERT layer after each Swin block)
-# instead of issuing all of BERT first: the HIP graph executor overlaps captured branches by the order
-# their nodes were created (A/B knob LRCE_TEXT_INTERLEAVE=1).
-_TEXT_INTERLEAVE = os.environ.get("LRCE_TEXT_INTERLEAVE", "0") == "1"
 
 
 def _head_args(feature_dim, num_classes, drop_out_rate, video_feature_res, video_feature_dim, frame_sample_size,
@@ -61,12 +54,6 @@ class E2EBase(nn.Module):
     def extract_text_features(self, texts, attention_mask, texts_type_ids, join_token=None):
         return self.text_extractor(texts, attention_mask, texts_type_ids, join_token=join_token)
 
-    def text_feature_steps(self, texts, attention_mask, texts_type_ids, join_token=None):
-        """extract_text_features as a generator (one step per BERT layer; the features are its return
-        value)."""
-        return (yield from self.text_extractor.forward_steps(texts, attention_mask, texts_type_ids,
-                                                             join_token=join_token))
-
     @property
     def pretrained_loaded(self):
         """Both backbones came from checkpoints (Swin Kinetics-600 + BERT)."""
@@ -91,13 +78,6 @@ class E2EBase(nn.Module):
         swin = self.video_extractor.swin
         text = [p for p in self.text_extractor.parameters() if id(p) not in pool]
         groups = {"decoder": list(self.fusion_model.fusion_transformer.parameters()), "text": text}
-        bert = self.text_extractor.bert
-        if _text_split_flush():
-            # BERT's upper half is final when the backward reaches its middle layer (text._SPLIT_FLUSH)
-            mid = len(bert.encoder.layer) // 2
-            hi = {id(p) for layer in bert.encoder.layer[mid:] for p in layer.parameters()}
-            groups["text_hi"] = [p for p in text if id(p) in hi]
-            groups["text"] = [p for p in text if id(p) not in hi]
         for i in range(len(swin.layers) - 1, 0, -1):
             ps = list(swin.layers[i].parameters())
             if i == len(swin.layers) - 1:
@@ -129,27 +109,9 @@ class E2EBase(nn.Module):
         side.wait_stream(main)
         swin = self.video_extractor.swin
         swin.split_at = self.split_swin_stage if self.split_backward else None
-        if _TEXT_INTERLEAVE:
-            gen = self.text_feature_steps(texts, texts_attention_mask, texts_type_ids, join_token=tok)
-            box = {}
-
-            def tick():
-                if "t" in box:
-                    return
-                with torch.cuda.stream(side):
-                    try:
-                        next(gen)
-                    except StopIteration as e:
-                        box["t"] = e.value
-            tick()
-            v = self.video_extractor(video_clips, between_blocks=tick)
-            while "t" not in box:
-                tick()
-            t = box["t"]
-        else:
-            with torch.cuda.stream(side):
-                t = self.extract_text_features(texts, texts_attention_mask, texts_type_ids, join_token=tok)
-            v = self.extract_video_features(video_clips)
+        with torch.cuda.stream(side):
+            t = self.extract_text_features(texts, texts_attention_mask, texts_type_ids, join_token=tok)
+        v = self.extract_video_features(video_clips)
         main.wait_stream(side)
         t.record_stream(main)
         if self.split_backward and torch.is_grad_enabled():
@@ -207,12 +169,6 @@ class E2EMultipleChoice(E2EBase):
                                     join_token=join_token)
         return feats.view(b, n_choice, seq, -1)
 
-    def text_feature_steps(self, texts, attention_mask, texts_type_ids, join_token=None):
-        b, n_choice, seq = texts.shape
-        feats = yield from self.text_extractor.forward_steps(texts.flatten(0, 1), attention_mask.flatten(0, 1),
-                                                             texts_type_ids.flatten(0, 1), join_token=join_token)
-        return feats.view(b, n_choice, seq, -1)
-
 
 class E2ECount(E2EBase):
     HEAD = LRCECount
@@ -224,6 +180,4 @@ class E2ECount(E2EBase):
                          frame_sample_size, temporal_scale, text_seq_len, **pretrained)
 
 
-def _text_split_flush():
-    from ..feature_extractor import text as T
-    return T._SPLIT_FLUSH
+

@@ -322,21 +322,15 @@ def _layer_wgrads(lay, flat, acts, grads, fused=False):
     _wgrad(flat, sa.in_proj_weight, sa.in_proj_bias, v(grads.dsav), v(acts.x0), rows=(2 * E, 3 * E))
 
 
-# Memory-side K/V projections on their own stream (A/B knob LRCE_DEC_KV_ASYNC=0: in line): the
+# Memory-side K/V projections on their own stream (_KV_ASYNC = False: in line, for tests): the
 # recurrence waits for layer l's K/V only when step 0 reaches layer l, and in the backward each layer's
 # memory-side input-gradient GEMMs start as soon as step 0's sweep has finished that layer.
-_KV_ASYNC = os.environ.get("LRCE_DEC_KV_ASYNC", "1") != "0"
-_KV_AHEAD = os.environ.get("LRCE_DEC_KV_AHEAD", "1") != "0"   # A/B knob: 0 = all 12 layers' K/V up front
-# Each layer's deferred weight gradients are issued on the weight-gradient stream as soon as step 0's
-# backward sweep has passed the layer (beside the rest of the latency-bound sweep) instead of all after
-# it (beside the Swin backward's full-chip GEMMs); LRCE_DEC_WGRAD_EARLY=1.  Measured slower than after the
-# sweep (same-box A/B 284.0 vs 286.4 QA-samples/s, profiles/r5_bench_defer_wgrad_early_ab.txt): the
-# weight-gradient kernels slow the latency-bound sweep they share the CUs with.  Off.
-# the 12 layers' K/V projection weight gradients as one pointer-table launch (LRCE_DEC_KV_WGRAD_BATCHED=1):
-# measured 293.2 / 292.4 vs 294.9 / 294.0 QA-samples/s per layer (profiles/r5_bench_dw_batched_ab.txt) —
-# the per-layer split-K launches interleave better with the Swin backward they run beside.  Off.
-_KV_WGRAD_BATCHED = os.environ.get("LRCE_DEC_KV_WGRAD_BATCHED", "0") == "1"
-_WGRAD_EARLY = os.environ.get("LRCE_DEC_WGRAD_EARLY", "0") == "1"   # measured slower (285.3 vs 286.4): off
+_KV_ASYNC = True
+# The decoder's weight gradients run on their own stream after the backward sweep: issued per layer as
+# soon as step 0's sweep has passed it they measured slower (284.0 vs 286.4 QA-samples/s,
+# profiles/r5_bench_defer_wgrad_early_ab.txt: they slow the latency-bound sweep they share the CUs
+# with), and the 12 layers' K/V projection weight gradients as one pointer-table launch measured 293.2 /
+# 292.4 vs 294.9 / 294.0 (profiles/r5_bench_dw_batched_ab.txt).
 
 
 class _RecurrentDecoderFn(torch.autograd.Function):
@@ -378,12 +372,6 @@ class _RecurrentDecoderFn(torch.autograd.Function):
                     if x is not None:
                         x.record_stream(main)
         issue_kv(0)
-        if not _KV_AHEAD:
-            for l in range(1, nL):
-                issue_kv(l)
-        clear = getattr(flat, "pending_clear", None)
-        if clear is not None and getattr(flat, "pending_clear_at", None) == "decoder":
-            clear()   # the step's gradient clear (FusedAdamW.zero_grad) beside the latency-bound recurrence
         acts = [_LayerActs(S, Bq, dev) for _ in layers]
         s = acts[0].x0[0]
         s.copy_(ft.summarization_token.detach().reshape(1, E).expand(Bq, E))
@@ -394,7 +382,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
             x_in, prev = s, None
             for l, lay in enumerate(layers):
                 if i == 0:
-                    if _KV_AHEAD and l + 1 < nL:
+                    if l + 1 < nL:
                         issue_kv(l + 1)
                     if kv_ready[l] is not None:
                         main.wait_event(kv_ready[l])
@@ -463,25 +451,6 @@ class _RecurrentDecoderFn(torch.autograd.Function):
                     if Lt:
                         _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[l], t16, rows=(E, 3 * E))
 
-        def kv_wgrads_batched():
-            """Every layer's K/V projection weight gradients (video rows, then question rows) as one
-            pointer-table launch each (K.linear_dw_batched: no split-K slabs / reduce) — False if the
-            layers' gradients are not all trainable (then per layer)."""
-            items_v, items_t = [], []
-            for l, lay in enumerate(layers):
-                ca = lay.multihead_attn
-                gw, gb = _g(flat, ca.in_proj_weight), _g(flat, ca.in_proj_bias)
-                if gw is None or gb is None:
-                    return False
-                items_v.append((dk16[l], v16, gw[E:3 * E], gb[E:3 * E]))
-                if Lt:
-                    items_t.append((dt16[l], t16, gw[E:3 * E], gb[E:3 * E]))
-            with torch.cuda.stream(wg):
-                K.linear_dw_batched(items_v)
-                if items_t:
-                    K.linear_dw_batched(items_t)
-            return True
-
         def memory_dx(l):
             """dv (+)= dK/dV_l W_kv,l, dtt likewise: layer l's K/V gradients are complete once step 0's
             sweep has passed it (the first layer issued writes, the rest add).  Returns the event of
@@ -515,9 +484,7 @@ class _RecurrentDecoderFn(torch.autograd.Function):
                                 dkvt[l].view(-1) if Lt else None, S, Lt, p, seed + 64 * (i * len(layers) + l),
                                 grads[l], i)
                 if i == 0:
-                    cast_done = memory_dx(l)
-                    if _WGRAD_EARLY:
-                        layer_wgrads(l, cast_done)
+                    memory_dx(l)
             ds = K.dropout(dx, 0.0, 0, res=dt)   # s fed both the residual and the decoder
             saves[i] = None
         if ks is not main:
@@ -530,11 +497,9 @@ class _RecurrentDecoderFn(torch.autograd.Function):
         # decoder's optimizer update, which rewrites the weights dv / dt were just computed with —
         # while the extractors' backward, which needs only dv / dt, proceeds on this one.  The
         # forward's stream anchor joins that stream back at the end of backward.
-        if not _WGRAD_EARLY:
-            wg.wait_stream(main)
-            kv_done = _KV_WGRAD_BATCHED and kv_wgrads_batched()
-            for l in range(len(layers)):
-                layer_wgrads(l, None, kv=not kv_done)
+        wg.wait_stream(main)
+        for l in range(len(layers)):
+            layer_wgrads(l, None)
         wg.wait_stream(main)
         with torch.cuda.stream(wg):
             gt = _g(flat, ft.summarization_token)
@@ -641,9 +606,6 @@ class _StepDecoderFn(torch.autograd.Function):
                 K.linear(v16, w, ca.in_proj_bias[E:], out=kvv[l])
                 if Lt:
                     K.linear(t16, w, ca.in_proj_bias[E:], out=kvt[l])
-        clear = getattr(flat, "pending_clear", None)
-        if clear is not None and getattr(flat, "pending_clear_at", None) == "decoder":
-            clear()
         A = _StepArena(0, nL, S, Bq, dev)
         A.f("x0", 0)[0].copy_(ft.summarization_token.detach().reshape(1, E).expand(Bq, E))
         if ks is not main:

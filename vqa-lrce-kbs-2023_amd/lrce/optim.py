@@ -8,8 +8,6 @@ added inside the update kernel (csrc/optim.hip) from one multi-tensor norm pass:
 is two launches for all 312 M parameters, and it also refreshes the bf16 shadow the forward reads.
 Semantics = torch.optim.AdamW (decoupled weight decay 0.01 default, bias-corrected moments).
 """
-import math
-import os
 
 import torch
 
@@ -174,23 +172,13 @@ class FusedAdamW(torch.optim.Optimizer):
         """flat.grad = 0 (the backward kernels accumulate into it).  overlap=True: the 1.25 GB clear runs
         on an aux stream beside the forward (which never touches gradients); grad_ready() must then
         be called before the backward (it makes the current stream wait for the clear).  It is issued at
-        the step's start, beside the BERT forward (LRCE_CLEAR_AT_DECODER=1 defers it to the recurrent
-        decoder's start instead, flat.pending_clear: 303.2 vs 309.5 QA-samples/s — the decoder's
-        latency chain suffers more from the 1.25 GB stream than BERT's); grad_ready() issues a deferred
-        clear if nothing did."""
+        the step's start, beside the BERT forward (at the recurrent decoder's start instead it measured
+        303.2 vs 309.5 QA-samples/s: the decoder's latency chain suffers more from the 1.25 GB stream
+        than BERT's)."""
         self.flat.grads_zeroed()
         if not overlap or not self.flat.grad.is_cuda:
             self.flat.grad.zero_()
             return
-        if _CLEAR_AT_DECODER:
-            self.flat.pending_clear = self._issue_clear
-            self.flat.pending_clear_at = _CLEAR_AT
-        else:
-            self._issue_clear()
-
-    def _issue_clear(self):
-        self.flat.pending_clear = None
-        self.flat.pending_clear_at = None
         dev = self.flat.device
         s = aux_stream(dev, "grad_zero")
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -200,8 +188,6 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def grad_ready(self):
         """Join an overlapped zero_grad (no-op otherwise): call between the forward and the backward."""
-        if getattr(self.flat, "pending_clear", None) is not None:
-            self._issue_clear()
         s = getattr(self, "_zero_stream", None)
         if s is not None:
             torch.cuda.current_stream(self.flat.device).wait_stream(s)
@@ -245,8 +231,3 @@ class FusedAdamW(torch.optim.Optimizer):
     def _device_step(self):
         return float(self.step_t.item())
 
-
-# A/B knob (see zero_grad): where the overlapped gradient clear is issued — "start" (the step's start,
-# beside the BERT forward), "decoder" (the recurrent decoder's start: slower), "swin3" (Swin stage 3's start)
-_CLEAR_AT = os.environ.get("LRCE_CLEAR_AT", "start")
-_CLEAR_AT_DECODER = _CLEAR_AT != "start"

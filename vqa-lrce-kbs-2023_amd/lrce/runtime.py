@@ -5,7 +5,6 @@ submodule (attribute `_lrce_flat`).  Native forward paths call `prepare(module)`
 first use / device change, refreshes the bf16 shadow when masters changed and, when a backward will
 follow, makes sure every p.grad is the flat view the kernels accumulate into.
 """
-import os
 
 import torch
 
@@ -78,7 +77,6 @@ def needs_grad(*tensors):
 
 
 _SIDE_STREAMS = {}
-_SINGLE_STREAM = os.environ.get("LRCE_SINGLE_STREAM", "0") == "1"   # A/B knob
 
 
 def aux_stream(device, name="text"):
@@ -86,10 +84,6 @@ def aux_stream(device, name="text"):
     video branch (Swin) runs on the current stream — the extractors are independent until the fusion
     head, and BERT's small latency-bound launches fill the gaps of Swin's large ones.
     "decoder_wgrad": the recurrent decoder's weight gradients, which feed nothing downstream."""
-    if _SINGLE_STREAM:
-        # every branch on the caller's stream, in issue order (the HIP graph executor of this runtime
-        # runs a captured graph's stream branches one after another anyway: tools/graph_overlap_probe.py)
-        return torch.cuda.current_stream(device)
     key = (torch.device(device).index, name)
     s = _SIDE_STREAMS.get(key)
     if s is None:
