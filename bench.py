@@ -20,6 +20,9 @@ first launches the N ranks itself, as children through torch.distributed.run, be
 the GPU, and exits with their status.  A joined world that differs from --gpus is an error.
 --dry-run: the same launcher and rank/world checks over gloo on the CPU (no model, no GPU) — the
 launcher's test.
+--shared-device (test-only rehearsal, never a measurement): the N ranks all run on cuda:0 and exchange
+over gloo instead of RCCL, so the N-GPU model path (split backward at SPLIT_SWIN_STAGE, bf16 gradient
+buckets, the early-update graphs) runs end to end on a one-GPU box; the JSON line says so.
 """
 import argparse
 import json
@@ -67,6 +70,8 @@ def parse():
                     help="write the per-shape roofline table of the bf16 GEMMs of the roofline steps (markdown) here")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check: N gloo ranks on the CPU time an all-reduce 'step'; no GPU, no model")
+    ap.add_argument("--shared-device", action="store_true",
+                    help="test-only rehearsal of N > 1: every rank on cuda:0, gloo instead of RCCL (not a measurement)")
     return ap.parse_args()
 
 
@@ -98,7 +103,7 @@ def launch_ranks(args):
     """--gpus N > 1 from a plain start: N rank processes through torch.distributed.run, as CHILDREN of
     this process, which has not touched the GPU (torch.cuda.device_count() does not initialise HIP on
     this image; nothing else here runs before this point).  Returns their exit status."""
-    if not args.dry_run:
+    if not args.dry_run and not args.shared_device:
         ndev = torch.cuda.device_count()
         if ndev < args.gpus:
             log(f"--gpus {args.gpus}: only {ndev} device(s) visible")
@@ -132,6 +137,17 @@ def dry_run(args, world, rank):
                           "config": {"parallelism": f"dp{world}", "per_gpu_batch": args.batch_size,
                                      "grad_reduce": args.grad_reduce_dtype if world > 1 else None},
                           "lrce_env": lrce_env()}), flush=True)
+
+
+def replica_digest(model):
+    """Two integer sums over the bits of the rank's f32 master weights (plain and position-weighted,
+    wrapping int64): equal on every rank iff the replicas are (practically) bit-identical."""
+    from lrce.runtime import flat_of
+    v = flat_of(model).f32.view(torch.int32).long()
+    w = torch.arange(v.numel(), device=v.device) % 65521 + 1
+    d = torch.stack([v.sum(), (v * w).sum()])
+    del v, w
+    return d
 
 
 def synthetic_batch(batch, seed):
@@ -322,14 +338,20 @@ def main():
             print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": 1, "config": {"parallelism": "dp1"},
                               "lrce_env": lrce_env()}), flush=True)
         return
+    shared = args.shared_device and world > 1
+    dev_index = 0 if shared else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev_index)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = dist.get_world_size()
     if world != args.gpus:
         log(f"rank {rank}: joined a world of {world} ranks but --gpus {args.gpus}")
         sys.exit(3)
-    device = torch.device("cuda", local)
+    device = torch.device("cuda", dev_index)
+    coll = torch.device("cpu") if shared else device   # small collectives: gloo on host tensors
     from lrce import kernels as K
     from lrce import _native
     _native.lib()
@@ -337,6 +359,7 @@ def main():
     log(f"rank {rank}/{world}: building model (bs={args.batch_size})")
     model, opt, reducer, batch = build(args.batch_size, device, gdt)
     step = make_step(model, opt, reducer, batch, args.mode, world)
+    split_stage = getattr(model, "split_swin_stage", None) if world > 1 else None
     for i in range(args.warmup):
         step()
         torch.cuda.synchronize()
@@ -351,10 +374,15 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    replicas = None
     if world > 1:
-        t = torch.tensor([elapsed], device=device)
+        t = torch.tensor([elapsed], device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        d = replica_digest(model).to(coll)
+        ds = [torch.empty_like(d) for _ in range(world)]
+        dist.all_gather(ds, d)
+        replicas = all(torch.equal(ds[0], x) for x in ds)
     loss_v = float(loss.item())
     samples = world * args.batch_size * args.steps
     value = samples / elapsed
@@ -393,6 +421,7 @@ def main():
                       "global_batch": samples // args.steps, "per_gpu_batch": args.batch_size, "frames": 16,
                       "resolution": 224, "question_tokens": 20, "text_seq_len": 32,
                       "parallelism": f"dp{world}", "launch": args.mode,
+                      "split_swin_stage": split_stage,
                       "grad_reduce": args.grad_reduce_dtype if world > 1 else None,
                       "precision": "bf16 MFMA (Swin, decoder memory, backward), fp16 MFMA BERT forward, "
                                    "exact-f32 decoder query side, f32 masters"},
@@ -400,6 +429,10 @@ def main():
            "model_tflops": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0, 2),
            "model_mfu": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0 / (MFMA_BF16_PEAK_TFLOPS * world), 4)}
     out["roofline"] = roof
+    if world > 1:
+        out["replicas_identical"] = replicas   # the ranks' master weights after the timed steps
+    if shared:
+        out["rehearsal"] = "shared-device: every rank on cuda:0 over gloo — a path test, not a measurement"
     out["lrce_env"] = lrce_env()   # non-default product switches (empty for the default step)
     if agent is not None:
         out["agent_path"] = agent

@@ -229,3 +229,22 @@ def test_graph_capture_refuses_the_crashing_hip_debug_queue_knob(monkeypatch):
         graph._check_runtime_env()
     monkeypatch.setenv("DEBUG_HIP_FORCE_GRAPH_QUEUES", "0")
     graph._check_runtime_env()
+
+
+def test_graph_capture_refuses_unregistered_or_in_capture_streams(monkeypatch):
+    """The round-5 capture-time SIGSEGV ("r5ab2": half of BERT's weight-gradient flush on a new sixth
+    stream) and the round-4 one share one trait: one more stream branch in the captured step.  The
+    runtime refuses a branch name outside the captured-and-replayed set, and creating a stream while a
+    graph is being captured; graph.py joins every branch forked into a capture (join_capture_branches)."""
+    from lrce import runtime as R
+    with pytest.raises(ValueError, match="AUX_STREAM_NAMES"):
+        R.aux_stream(torch.device("cuda", 0), "text_flush2")
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+    monkeypatch.setattr(R, "_SIDE_STREAMS", {})
+    with pytest.raises(RuntimeError, match="inside a HIP graph capture"):
+        R.aux_stream(torch.device("cuda", 0), "decoder_wgrad")
+    for name in ("text", "grad_zero", "decoder_kv", "decoder_wgrad", "swin_bias"):
+        assert name in R.AUX_STREAM_NAMES
+    from lrce import graph
+    assert graph.join_capture_branches is R.join_capture_branches

@@ -235,3 +235,27 @@ def test_early_updates_do_not_race_the_backward():
     werr = worst(w_early, w_plain, upd)
     wnoise = worst(w_plain2, w_plain, upd)
     assert werr[0] < max(1e-3, 4 * wnoise[0]), f"updates with early updates: {werr} (noise {wnoise})"
+
+
+def test_capture_joins_a_forked_branch():
+    """graph.py's capture guard (the r5ab2 analysis): a branch forked into the capture and
+    never joined by the captured code is joined by the capture itself (runtime.join_capture_branches),
+    so the capture ends cleanly and the replay runs the branch's work before the graph completes."""
+    from lrce import runtime as R
+    from lrce.graph import CapturedStep
+    dev = torch.device("cuda", 0)
+    x = torch.ones(1 << 20, device=dev)
+    out = torch.zeros_like(x)
+    s = R.aux_stream(dev, "grad_zero")
+
+    def fn():
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            torch.mul(x, 2.0, out=out)      # forked, not joined here
+        return out
+    step = CapturedStep(fn, warmup=1)
+    x.fill_(3.0)
+    out.zero_()
+    step.replay()
+    torch.cuda.synchronize()
+    assert torch.all(out == 6.0)

@@ -13,10 +13,19 @@ import os
 
 import torch
 
+from .runtime import join_capture_branches
+
 # HIP runtime debug variable that hands a graph's parallel branches to N extra queues.  With it set to
 # 8 the ROCm 7 runtime crashed in the first captured training step of this model (round-4 A/B variant
 # "fq8": core dump at the capture; reproduced once in round 5: segmentation fault), so the capture
-# refuses it with an explanation instead of reaching that crash.
+# refuses it with an explanation instead of reaching that crash.  The round-5 crash (A/B "r5ab2", a
+# SIGSEGV in the first captured step after half of BERT's weight-gradient flush moved to a new sixth
+# stream) shares the trait of one more stream branch in the graph; its diff was reverted before a
+# commit, so the exact fault is not reconstructible.  The capture therefore refuses the patterns that
+# trait can take (runtime.aux_stream): a branch name outside the captured-and-replayed set, and a
+# stream created while capturing; and it joins every branch forked into a capture back into the
+# capturing stream before the capture ends (runtime.join_capture_branches), so an unjoined fork can
+# never reach the runtime's end-of-capture path.
 _FORCE_GRAPH_QUEUES = "DEBUG_HIP_FORCE_GRAPH_QUEUES"
 
 
@@ -41,6 +50,7 @@ class CapturedStep:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=pool):
             self.out = fn()
+            join_capture_branches(torch.cuda.current_stream().device)
         torch.cuda.synchronize()
 
     def replay(self):
@@ -156,6 +166,7 @@ class TrainStepGraph:
             with torch.cuda.graph(st.g_step, pool=pool):
                 st.out = self.body(*st.static)
                 self.optim.step(grad_scale=1.0)
+                join_capture_branches(self.optim.flat.device)
         else:
             self.reducer.capture_begin()
             try:
@@ -163,6 +174,7 @@ class TrainStepGraph:
                     with torch.cuda.graph(st.g_step, pool=pool):
                         st.out = self.body(*st.static)
                         self.reducer.finish()            # captures the remaining buckets' bf16 casts
+                        join_capture_branches(self.optim.flat.device)
                     st.order = list(self.reducer.captured)
                 else:
                     with torch.cuda.graph(st.g_step, pool=pool):
@@ -172,6 +184,7 @@ class TrainStepGraph:
                             # pass if the masters changed outside the optimizer) on the main stream,
                             # ahead of every exchange: the early-update graphs then hold only updates
                             self.optim._begin()
+                        join_capture_branches(self.optim.flat.device)
                     marks = [self.reducer.capture_mark()]
                     st.g_tail = []
                     for i, seg in enumerate(self.tail):
@@ -180,6 +193,7 @@ class TrainStepGraph:
                             seg()
                             if i == len(self.tail) - 1:
                                 self.reducer.finish()
+                            join_capture_branches(self.optim.flat.device)
                         st.g_tail.append(g)
                         marks.append(self.reducer.capture_mark())
                     st.order = list(self.reducer.captured[:marks[0]])
@@ -195,10 +209,12 @@ class TrainStepGraph:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=epool):
                         self.optim.update_chunks(self.reducer.chunk_ranges(order), grad_scale=1.0 / self.world)
+                        join_capture_branches(self.optim.flat.device)
                     st.g_early.append(g)
             st.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(st.g_opt, pool=pool):
                 self.optim.step(grad_scale=1.0 / self.world)
+                join_capture_branches(self.optim.flat.device)
         self.optim.step_count = steps
         self.optim.flat.mark_bf16_fresh()
         torch.cuda.synchronize()

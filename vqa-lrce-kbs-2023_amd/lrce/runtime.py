@@ -77,18 +77,56 @@ def needs_grad(*tensors):
 
 
 _SIDE_STREAMS = {}
+# The stream branches a captured training step may fork into: the set every GPU run of the product has
+# captured and replayed.  Two A/B variants that each added one more branch to the captured step crashed
+# the HIP runtime in the first captured step (round 4 "fq8", DEBUG_HIP_FORCE_GRAPH_QUEUES=8: graph
+# branches on extra queues; round 5 "r5ab2": half of BERT's weight-gradient flush on a sixth stream,
+# a new stream whose fork / join pattern nothing else in the step has) — see graph.py and DESIGN §8.
+# A new branch is a deliberate change: add its name here after a GPU capture test of it.
+AUX_STREAM_NAMES = frozenset({"text", "grad_zero", "decoder_kv", "decoder_wgrad", "swin_bias"})
+
+
+def _capturing():
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
 
 def aux_stream(device, name="text"):
     """A named extra HIP stream of `device`.  "text": the text branch (BERT) runs on it while the
     video branch (Swin) runs on the current stream — the extractors are independent until the fusion
     head, and BERT's small latency-bound launches fill the gaps of Swin's large ones.
-    "decoder_wgrad": the recurrent decoder's weight gradients, which feed nothing downstream."""
+    "decoder_wgrad": the recurrent decoder's weight gradients, which feed nothing downstream.
+    Refused: a name outside AUX_STREAM_NAMES, and creating a stream while a HIP graph is being captured
+    (every stream must exist before the capture: the eager first step creates them)."""
+    if name not in AUX_STREAM_NAMES:
+        raise ValueError(f"aux stream {name!r} is not one of the captured step's branches "
+                         f"{sorted(AUX_STREAM_NAMES)} (runtime.AUX_STREAM_NAMES)")
     key = (torch.device(device).index, name)
     s = _SIDE_STREAMS.get(key)
     if s is None:
+        if _capturing():
+            raise RuntimeError(f"aux stream {name!r} would be created inside a HIP graph capture: streams "
+                               "must exist before the capture (run the step eagerly once first)")
         s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
     return s
+
+
+def join_capture_branches(device):
+    """Make the current (capturing) stream wait for every aux stream that is part of the running
+    capture: a branch forked into a capture must be joined back before it ends, and a missing join is
+    exactly the kind of pattern the runtime answered with a crash instead of an error.  Joining an
+    already-joined branch adds an edge and no work.  Returns the number of branches joined."""
+    cur = torch.cuda.current_stream(device)
+    idx = torch.device(device).index
+    n = 0
+    for (i, _), st in list(_SIDE_STREAMS.items()):
+        if i != idx or st == cur:
+            continue
+        with torch.cuda.stream(st):
+            part = torch.cuda.is_current_stream_capturing()
+        if part:
+            cur.wait_stream(st)
+            n += 1
+    return n
 
 
 def side_stream(device):
