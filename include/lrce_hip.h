@@ -512,8 +512,8 @@ int lrce_dec_ln_grads(const float* const* dy, const float* const* x, const float
  * FusionTransformer.forward's clip loop body (fusionv3.py:43-49 over the 12 nn.TransformerDecoderLayer of
  * fusionv3.py:8-17): ONE launch per recurrent step and direction (csrc/decoder_step.hip), replacing the
  * 4 + 4 launches per layer of the per-block path above.  12 x R workgroups (R = min(B, 10) row groups)
- * stay resident for all 12 layers and hand rows to each other inside the launch (agent-scope write-through
- * stores + arrival counters, bounded spins): per layer, (head h, row b) workgroups run the self-attention
+ * stay resident for all 12 layers and hand rows to each other inside the launch (16-B write-through
+ * stores into sentinel-armed buffers, polled with bounded spins: the payload is the flag): per layer, (head h, row b) workgroups run the self-attention
  * block and the cross-attention block (as lrce_dec_sa_fwd / lrce_dec_ca_fwd), and every workgroup takes
  * 32-unit slices of the FFN hidden layer for ALL rows (linear1 -> GELU -> dropout -> its partial of
  * linear2), so each FFN weight is read once per layer-step; the partials are summed by the next layer's
@@ -552,8 +552,9 @@ typedef struct LrceDecStep {
   int64_t dkv_video_lstride;
   float* dkv_text;                         /* backward: [B*lt][1536] f32 per layer, stored at step S-1 then added */
   int64_t dkv_text_lstride;
-  float* ws;                               /* lrce_dec_step_ws_elems() f32 */
-  uint32_t* counters;                      /* lrce_dec_step_counter_words() uint32, zero (left zero by every launch) */
+  float* ws;                               /* lrce_dec_step_ws_elems() f32, every byte 0xFF before the first launch
+                                              (the launches keep it so; lrce_dec_step_reset restores it) */
+  uint32_t* counters;                      /* lrce_dec_step_counter_words() uint32, zero before the first launch */
   uint32_t* status;                        /* [4] uint32: [0] != 0 after a hand-off timed out (sticky until cleared) */
   LrceDecLayerW layer[LRCE_DEC_LAYERS];
 } LrceDecStep;
@@ -565,8 +566,9 @@ int64_t lrce_dec_step_ws_elems(void);
 int64_t lrce_dec_step_counter_words(void);
 int lrce_dec_step_fwd(const LrceDecStep* args, void* stream);
 int lrce_dec_step_bwd(const LrceDecStep* args, void* stream);
-/* zero the counter block and the status words (after a timeout: status[0] != 0) */
-int lrce_dec_step_reset(uint32_t* counters, uint32_t* status, void* stream);
+/* re-arm the workspace (every byte 0xFF), zero the counter block and the status words (after a timeout:
+ * status[0] != 0) */
+int lrce_dec_step_reset(float* ws, uint32_t* counters, uint32_t* status, void* stream);
 /* Debug: phase timestamps (s_memrealtime, 100 MHz) of the step kernels into buf[((dir * 128 + workgroup) * 16 + layer) * 8 + mark]
  * (dir 0 forward, 1 backward; 2 * 128 * 16 * 8 uint64); NULL turns it off (the default).  tools/decoder_step_bench.py --trace. */
 int lrce_dec_step_set_trace(uint64_t* buf);

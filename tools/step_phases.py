@@ -11,8 +11,8 @@ import sys
 from rocprof_summary import short_name
 
 MARK = {"bert fwd": ("mhaL_fwd", "bert_embed_kernel"), "bert bwd": ("mhaL_bwd", "bert_embed_bwd"),
-        "swin fwd": ("wattn_qkv_fwd", "im2col"), "swin bwd": ("wattn_bwd",), "decoder fwd": ("dec_ca_fwd",),
-        "decoder bwd": ("dec_ca_bwd",), "adamw": ("adamw",)}
+        "swin fwd": ("wattn_qkv_fwd", "im2col"), "swin bwd": ("wattn_bwd",), "decoder fwd": ("dec_ca_fwd", "dec_step_fwd"),
+        "decoder bwd": ("dec_ca_bwd", "dec_step_bwd"), "adamw": ("adamw",)}
 
 
 def main():

@@ -26,16 +26,26 @@
 //   SB (head h, row b):  LN1' -> ... (as dec_sa_bwd) -> dx0 = d x3 of layer l-1 (or, l = 0, ds_in of the
 //                        previous step: dx0 + dt).
 //
-// Hand-offs (MI355X_MICROARCH.md "Valid forms", first row of the sc1 hand-off table): every handed-off
-// byte is stored write-through (agent-scope relaxed atomic stores / buffer stores with the sc1 bit),
-// every storing wave drains with s_waitcnt vmcnt(0), a workgroup barrier follows, and ONE lane adds to
-// an arrival counter; consumers poll that counter from one lane with agent-scope relaxed loads
-// (s_sleep between polls, bounded: after 0.5 s the launch records a timeout in status[0], raises a
-// sticky abort word and every workgroup leaves at its next wait — never a hang), then read EVERY
-// handed-off byte with sc1 loads.  Bytes written by earlier launches (weights, K/V, the forward's
-// saved activations) are read with plain loads.  The counters are per layer and phase, zeroed by the
-// last workgroup to finish (graph-replay safe); after a timeout the host resets them
-// (lrce_dec_step_reset).  Every cross-workgroup sum is taken in a fixed order: deterministic.
+// Hand-offs: the payload is the flag.  Every hand-off buffer holds a sentinel bit pattern (0xFFFFFFFF,
+// a NaN no arithmetic here produces: converted fp16 / bf16 NaNs and the hardware's canonical NaN all
+// differ) until its producer stores the value with a 16-B write-through (sc1) store; a consumer reads
+// the 16-B piece with an sc1 load and re-reads it (s_sleep between polls) while any of its four dwords
+// is still the sentinel — dword stores are single-copy atomic, so no torn value is ever accepted.  No
+// arrival counter, no drain before a signal: one store and one load per hand-off instead of store,
+// drain, atomic, poll and load (tools/hop_probe.hip on the box: 0.93 us per 12-producer exchange
+// against 4.35 us for the counter protocol, whose 120 atomics on one word alone serialise to 1.96 us).
+// Buffers are re-armed in two ways:
+//  * the head partial slabs and the FFN slice partials have ONE reader per piece, which stores the
+//    sentinel back after reading it (and drains those stores before its next hand-off: the next write
+//    of the piece is causally after that);
+//  * the row mailboxes (many readers) are per layer, in two sets used by alternate launches: a launch
+//    uses set (epoch & 1) and re-arms the other set, which the previous launch used; the epoch word
+//    advances when the last workgroup finishes.
+// Polls are bounded: after 0.5 s a wait records its code in status[0] and raises a sticky abort word,
+// and every later wait gives up at once (the launch ends with garbage and the host raises; never a
+// hang); lrce_dec_step_reset then re-arms the workspace.  Bytes written by earlier launches (weights,
+// K/V, the forward's saved activations) are read with plain loads.  Every cross-workgroup sum is taken
+// in a fixed order: deterministic.
 //
 // Residency: all 12 R workgroups must be resident at once (they wait for each other).  R <= 10 keeps
 // the grid at <= 120 workgroups of one per CU, so even two such launches (two processes sharing a
@@ -49,16 +59,21 @@ namespace {
 constexpr int FF = 3072, FS = 32, NF = FF / FS, RMAX = 10, MAXB = LRCE_DEC_MAX_ROWS, RCH = 16;
 constexpr int XP = 100, XROW = 8 * XP + 4;   // padded LDS row of 768: 8 parts of 96 (+4), rows 804 apart (MFMA row reads)
 constexpr int NLMAX = LRCE_DEC_LAYERS;
-// counter block (uint32): per layer CL words; then done / abort
-constexpr int C_SL = 0, C_ROWS = 1, C_X3 = 16, C_SA = 16 + MAXB, C_X1 = 16 + 2 * MAXB, C_CA = 16 + 3 * MAXB;
-constexpr int CL = 16 + 4 * MAXB;
-constexpr int C_DONE = NLMAX * CL, C_ABORT = C_DONE + 1, CTR_WORDS = C_DONE + 16;
-constexpr unsigned long long TIMEOUT_TICKS = 50000000ull;   // 0.5 s of s_memrealtime (100 MHz)
-// workspace (f32): two per-head partial slabs [MAXB][12][768], the FFN slice partials [NF][MAXB][768],
-// the backward's dx3p rows [MAXB][768]
+// counter block (uint32): the finishing count, the sticky abort word, the launch epoch
+constexpr int C_DONE = 0, C_ABORT = 1, C_EPOCH = 2, CTR_WORDS = 16;
+// workspace (f32, all sentinel between launches): two per-head partial slabs [MAXB][12][768], the FFN
+// slice partials [NF][MAXB][768], then the row mailboxes: 2 sets x NKIND kinds x NLMAX layers x
+// [MAXB][768].  Kinds, forward: x3p, x1p, x2p, x2 (LN2 output); backward: d x3 (the FFN block's
+// input gradient), dx3p, dx2 (LN2 input gradient), dx1, dt (layer 0 only)
 constexpr long long WS_SLAB = (long long)MAXB * H * E;
 constexpr long long WS_P = (long long)NF * MAXB * E;
-constexpr long long WS_ELEMS = 2 * WS_SLAB + WS_P + (long long)MAXB * E;
+constexpr int NKIND = 5;
+enum { K_X3P = 0, K_X1P = 1, K_X2P = 2, K_X2 = 3 };
+enum { K_DLN3 = 0, K_DRES = 1, K_DLN2 = 2, K_DLN1 = 3, K_DT = 4 };
+constexpr long long MB_KIND = (long long)NLMAX * MAXB * E;
+constexpr long long WS_MB = 2LL * NKIND * MB_KIND;
+constexpr long long WS_ELEMS = 2 * WS_SLAB + WS_P + WS_MB;
+constexpr unsigned SENT = 0xFFFFFFFFu;
 
 // ---- arena layout (shared with the host through lrce_dec_step_field)
 constexpr int NFWD = 18, NBWD = 9;
@@ -122,76 +137,105 @@ __device__ __forceinline__ float4 drop4(float4 y, float p, uint64_t seed, long l
   return make_float4(u.x >= p ? y.x / k : 0.f, u.y >= p ? y.y / k : 0.f, u.z >= p ? y.z / k : 0.f, u.w >= p ? y.w / k : 0.f);
 }
 
-// Publish this head's partial row (LDS part[768], 16-B aligned) to slab[b][h] with 16-B write-through
-// stores and return true in the last of the 12 heads of row b to arrive (the counter's add returns 11);
-// gather4: columns 4t .. 4t+3 of the 12 partials, summed in head order (deterministic).
-__device__ bool publish4(const float* part, float* slab, unsigned* ctr, int b, int h, unsigned* last) {
+__device__ __forceinline__ bool unset4(float4 v) {
+  return __float_as_uint(v.x) == SENT || __float_as_uint(v.y) == SENT || __float_as_uint(v.z) == SENT ||
+         __float_as_uint(v.w) == SENT;
+}
+__device__ __forceinline__ float4 sent4() {
+  const float f = __uint_as_float(SENT);
+  return make_float4(f, f, f, f);
+}
+// A handed-off 16-B piece: re-read (s_sleep between polls) while any dword is still the sentinel.
+// Bounded: every 64 polls the sticky abort word is checked; after SPIN_MAX polls (~0.5 s: each poll is
+// a memory round trip) the wait gives up through wait_fail (raises the abort word, records the code).
+constexpr unsigned SPIN_MAX = 1u << 20;
+__device__ __attribute__((noinline)) void wait_fail(unsigned* ctrs, unsigned* status, unsigned code) {
+  __hip_atomic_store(ctrs + C_ABORT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned zero = 0;
+  __hip_atomic_compare_exchange_strong(status, &zero, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float4 ld4_wait(const float* base, long long off, const LrceDecStep& p, unsigned code) {
+  float4 v = ld4_sc1(base, off);
+  unsigned it = 0;
+  while (unset4(v)) {
+    __builtin_amdgcn_s_sleep(1);
+    v = ld4_sc1(base, off);
+    if ((++it & 63u) == 0 &&
+        (it >= SPIN_MAX || __hip_atomic_load(p.counters + C_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      if (it >= SPIN_MAX) wait_fail(p.counters, p.status, code);
+      break;
+    }
+  }
+  return v;
+}
+
+// this head's partial row (LDS part[768], 16-B aligned) -> slab[b][h] (write-through)
+__device__ __forceinline__ void publish(const float* part, float* slab, int b, int h) {
   const int t = threadIdx.x;
   if (t < E / 4) st4_sc1(slab, ((long long)b * H + h) * E + 4 * t, lds4(part + 4 * t));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) *last = __hip_atomic_fetch_add(&ctr[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(H - 1);
-  __syncthreads();
-  return *last != 0;
 }
-__device__ float4 gather4(const float* slab, int b, int t) {
-  float4 v[H];
+// columns h*64 .. h*64+63 of row b summed over the 12 heads' partials in head order (thread q < 16
+// returns columns 4q .. 4q+3): thread (j, q) waits for its piece of head j, stores the sentinel back
+// (this workgroup is the piece's only reader) and the sum runs through red.  The re-arming stores are
+// drained before the caller's next hand-off (s_waitcnt vmcnt(0) in the caller's path).
+__device__ float4 gather_cols(float* slab, int b, int h, float4 (&red)[16][16], const LrceDecStep& p, unsigned code) {
+  const int t = threadIdx.x;
+  if (t < H * 16) {
+    const int j = t >> 4, q = t & 15;
+    const long long off = ((long long)b * H + j) * E + h * D + 4 * q;
+    red[j][q] = ld4_wait(slab, off, p, code);
+    st4_sc1(slab, off, sent4());
+  }
+  lds_barrier();
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < 16) {
+    s = red[0][t];
 #pragma unroll
-  for (int j = 0; j < H; ++j) v[j] = ld4_sc1(slab, ((long long)b * H + j) * E + 4 * t);
-  float4 s = v[0];
-#pragma unroll
-  for (int j = 1; j < H; ++j) s = add4(s, v[j]);
+    for (int j = 1; j < H; ++j) s = add4(s, red[j][t]);
+  }
+  lds_barrier();
   return s;
 }
 
-// every storing wave drains its write-through stores, the workgroup meets, one lane adds `n`
-__device__ __forceinline__ void wg_arrive(unsigned* ctr, unsigned n = 1) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// threadIdx.x through an empty asm: lane-derived values computed from it inside a loop body stay in
+// that body (the compiler cannot hoist them out of the layer loop and keep them live, or spill them,
+// across every phase)
+__device__ __forceinline__ int opaque_tid() {
+  int v = threadIdx.x;
+  asm volatile("" : "+v"(v));
+  return v;
 }
 
-// One lane polls *w >= target (relaxed agent loads, s_sleep), the workgroup meets (LDS-only barrier:
-// the weight loads in flight are not waited for).  false: the launch is aborting (timeout here or
-// elsewhere) — the caller leaves.
-__device__ bool wg_wait(unsigned* w, unsigned target, const LrceDecStep& p, unsigned code, unsigned* ok_word) {
-  if (threadIdx.x == 0) {
-    unsigned ok = 1;
-    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      unsigned* abort_w = p.counters + C_ABORT;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (;;) {
-        __builtin_amdgcn_s_sleep(1);
-        if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-        if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > TIMEOUT_TICKS) {
-          __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(p.status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = 0;
-          break;
-        }
-      }
-    }
-    *ok_word = ok;
+// the row mailboxes of one set: kind k, layer l, row b at mb(...) + b * E
+__device__ __forceinline__ float* mb_of(const LrceDecStep& p, unsigned set, int kind, int l) {
+  return p.ws + 2 * WS_SLAB + WS_P + ((long long)(set * NKIND + kind) * NLMAX + l) * MAXB * E;
+}
+// the launch's epoch (read by every workgroup before any finishes) and the re-arming of the other set
+// (used by the previous launch, which has ended): rows < B of every kind and layer, sentinel stores
+__device__ unsigned launch_begin(const LrceDecStep& p) {
+  const unsigned ep = __hip_atomic_load(p.counters + C_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned other = (ep + 1) & 1u;
+  const long long per = (long long)p.B * (E / 4);   // float4 pieces of one (kind, layer)
+  const long long tot = (long long)NKIND * p.n_layers * per;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < tot; i += (long long)gridDim.x * NT) {
+    const long long kl = i / per, e = i % per;
+    st4_sc1(mb_of(p, other, (int)(kl / p.n_layers), (int)(kl % p.n_layers)), 4 * e, sent4());
   }
-  lds_barrier();
-  const bool ok = *ok_word != 0;
-  lds_barrier();
-  return ok;
+  return ep & 1u;
 }
 
-// the last workgroup to finish zeroes the counter block (ready for the next launch / graph replay)
+// the last workgroup to finish zeroes the finishing count and advances the epoch (the next launch
+// then uses the other mailbox set)
 __device__ void finish(const LrceDecStep& p, unsigned* last_word) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
     *last_word = __hip_atomic_fetch_add(p.counters + C_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
-  if (!*last_word) return;
-  for (int i = threadIdx.x; i < CTR_WORDS; i += NT) __hip_atomic_store(p.counters + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!*last_word || threadIdx.x != 0) return;
+  __hip_atomic_store(p.counters + C_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(p.counters + C_EPOCH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
-__device__ __forceinline__ unsigned* ctr(const LrceDecStep& p, int l, int k) { return p.counters + l * CL + k; }
 
 // Debug phase timestamps (lrce_dec_step_set_trace; NULL in production): thread 0 of workgroup w stores
 // s_memrealtime (100 MHz) at mark i of layer l into trace[((dir * 128 + w) * 16 + l) * 8 + i].
@@ -292,17 +336,25 @@ union StepLds {
 };
 
 // ---------------------------------------------------------------------------- FFN partial reduce
-// out[b][h*64 + c] for c < 64 = base[b][..] + epi(sum_j P[j][b][..]) over the NF slices in slice
-// order (16 groups of 6, then the groups in order); fwd: base = x2, epi = drop(. + b2, seed5); bwd:
-// base = dx3p, epi = identity.  All of P / base are handed-off rows: sc1 loads; out stored sc1.
-__device__ void slice_reduce(const float* P, int b, int h, const float* bias, float drop_p, uint64_t seed, const float* base_row,
-                             float* out_row, RedL& L) {
+// columns h*64 .. h*64+63 of row b: out = base + epi(sum_j P[j][b][..]) over the NF slices in slice order
+// (16 groups of 6, then the groups in order); fwd: base = x2, epi = drop(. + b2, seed); bwd: base =
+// dx3p, epi = identity.  P pieces are waited for and re-armed (this workgroup is their only reader),
+// base is a mailbox row (waited for); out goes to the mailbox row (sc1) and to the arena row `keep`.
+// Ends with the re-arming stores drained (before this workgroup's next hand-off).
+__device__ void slice_reduce(float* P, int b, int h, const float* bias, float drop_p, uint64_t seed, const float* base_row,
+                             float* out_row, float* keep, RedL& L, const LrceDecStep& p, unsigned code) {
   const int t = threadIdx.x, q = t & 15, g = t >> 4;
   const int col = h * D + 4 * q;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 v[NF / 16];
 #pragma unroll
   for (int i = 0; i < NF / 16; ++i) v[i] = ld4_sc1(P, ((long long)(g + 16 * i) * MAXB + b) * E + col);
+#pragma unroll
+  for (int i = 0; i < NF / 16; ++i) {
+    const long long off = ((long long)(g + 16 * i) * MAXB + b) * E + col;
+    if (unset4(v[i])) v[i] = ld4_wait(P, off, p, code);
+    st4_sc1(P, off, sent4());
+  }
 #pragma unroll
   for (int i = 0; i < NF / 16; ++i) { s.x += v[i].x; s.y += v[i].y; s.z += v[i].z; s.w += v[i].w; }
   L.red[g][q] = s;
@@ -322,9 +374,12 @@ __device__ void slice_reduce(const float* P, int b, int h, const float* bias, fl
         a.z = u.z >= drop_p ? a.z / k : 0.f; a.w = u.w >= drop_p ? a.w / k : 0.f;
       }
     }
-    const float4 r = ld4_sc1(base_row, col);
-    st4_sc1(out_row, col, make_float4(r.x + a.x, r.y + a.y, r.z + a.z, r.w + a.w));
+    const float4 r = ld4_wait(base_row, col, p, code + 0x1000);
+    const float4 o = make_float4(r.x + a.x, r.y + a.y, r.z + a.z, r.w + a.w);
+    st4_sc1(out_row, col, o);
+    *reinterpret_cast<float4*>(keep + col) = o;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
 }
 
@@ -360,13 +415,18 @@ __device__ __forceinline__ void rows_t_lds(const f16* Wl, const float* v, float*
 }
 
 // ------------------------------------------------------------------- forward: self-attention row
-// x0 (LDS) is ready; v_h -> head dropout -> partial -> the last head of row b writes x1p (sc1) and
-// raises the row flag.  wr: W_v[h] rows (registers), L.wo: the W_o slice (DMA'd; waited for here)
-__device__ void sa_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint4 (&wr)[NRI], float bvv, SaL& L,
-                           uint64_t seed0, uint64_t seed1, bool wait_dma) {
+// x0 (LDS) is ready; v_h -> head dropout -> partial (published) -> this workgroup's 64 columns of row b:
+// x1p = x0 + drop(sum of the 12 partials + b_o), into the x1p mailbox (and the arena).  wr: W_v[h] rows
+// (registers), L.wo: the W_o slice (DMA'd; waited for here)
+__device__ void sa_fwd_row(const LrceDecStep& p, int l, int b, int h, const f16* wv, float bvv, SaL& L,
+                           uint64_t seed0, uint64_t seed1, bool wait_dma, RedL& RD, float* mbx1) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
-  rows_gemv(wr, L.x0, L.pp[wave], L.v + wave * WROWS, lane);
+  {
+    uint4 wr[NRI];
+    rows_load(wv, h * D + wave * WROWS, lane, wr);
+    rows_gemv(wr, L.x0, L.pp[wave], L.v + wave * WROWS, lane);
+  }
   lds_barrier();
   if (t < D) {
     float v = L.v[t] + bvv;
@@ -378,12 +438,16 @@ __device__ void sa_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint
   lds_barrier();
   slice_gemv(L.wo, L.v, L.part, t);
   lds_barrier();
-  if (!publish4(L.part, p.ws, ctr(p, l, C_SA), b, h, &L.last)) return;
-  if (t < E / 4) {
-    const float4 y = drop4(add4(gather4(p.ws, b, t), lds4(W.bo + 4 * t)), p.drop_p, seed1, (long long)b * E + 4 * t);
-    st4_sc1(fwd_field(p, F_X1P, l, p.step).row(b), 4 * t, add4(lds4(L.x0 + 4 * t), y));
+  publish(L.part, p.ws, b, h);
+  const float4 sm = gather_cols(p.ws, b, h, RD.red, p, 0x200 + l);
+  if (t < 16) {
+    const int c = h * D + 4 * t;
+    const float4 y = drop4(add4(sm, lds4(W.bo + c)), p.drop_p, seed1, (long long)b * E + c);
+    const float4 o = add4(lds4(L.x0 + c), y);
+    st4_sc1(mbx1 + (long long)b * E, c, o);
+    *reinterpret_cast<float4*>(fwd_field(p, F_X1P, l, p.step).row(b) + c) = o;
   }
-  wg_arrive(ctr(p, l, C_X1) + b);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-arming stores, before the next hand-off
 }
 
 // ------------------------------------------------------------------ forward: cross-attention row
@@ -407,16 +471,15 @@ __device__ void ca_fwd_prefetch(const LrceDecStep& p, int l, int b, int h, CaL& 
   }
 }
 
-__device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint4 (&wr)[NRI], float bqv, CaL& L,
-                           uint64_t seed2, uint64_t seed3, const uint4 (&kr)[8]) {
+__device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const f16* wq, float bqv, CaL& L,
+                           uint64_t seed2, uint64_t seed3, const uint4 (&kr)[8], RedL& RD, const float* mbx1, float* mbx2) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
   const KvP kv = kv_of(p, l);
   const int Lk = kv.lk1 + kv.lk2;
   float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
-  const float* x1p = fwd_field(p, F_X1P, l, p.step).row(b);
   if (t < E / 4) {
-    xr = ld4_sc1(x1p, 4 * t);
+    xr = ld4_wait(mbx1 + (long long)b * E, 4 * t, p, 0x300 + l);
     gg = *reinterpret_cast<const float4*>(W.g1 + 4 * t);
     be = *reinterpret_cast<const float4*>(W.be1 + 4 * t);
   }
@@ -432,7 +495,11 @@ __device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint
     }
   }
   lds_barrier();
-  rows_gemv(wr, L.f.x1, L.f.pp[wave], L.f.q + wave * WROWS, lane);
+  {
+    uint4 wr[NRI];
+    rows_load(wq, h * D + wave * WROWS, lane, wr);
+    rows_gemv(wr, L.f.x1, L.f.pp[wave], L.f.q + wave * WROWS, lane);
+  }
   lds_barrier();
   if (t < D) {
     const float q = L.f.q[t] + bqv;
@@ -492,18 +559,23 @@ __device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const uint
   lds_barrier();
   slice_gemv(L.wo, L.f.ctx, L.f.part, t);
   lds_barrier();
-  if (!publish4(L.f.part, p.ws + WS_SLAB, ctr(p, l, C_CA), b, h, &L.last)) return;
-  if (t < E / 4) {
-    const float4 y = drop4(add4(gather4(p.ws + WS_SLAB, b, t), lds4(W.boc + 4 * t)), p.drop_p, seed3, (long long)b * E + 4 * t);
-    st4_sc1(fwd_field(p, F_X2P, l, p.step).row(b), 4 * t, add4(lds4(L.f.x1 + 4 * t), y));
+  publish(L.f.part, p.ws + WS_SLAB, b, h);
+  const float4 sm = gather_cols(p.ws + WS_SLAB, b, h, RD.red, p, 0x400 + l);
+  if (t < 16) {
+    const int c = h * D + 4 * t;
+    const float4 y = drop4(add4(sm, lds4(W.boc + c)), p.drop_p, seed3, (long long)b * E + c);
+    const float4 o = add4(lds4(L.f.x1 + c), y);
+    st4_sc1(mbx2 + (long long)b * E, c, o);
+    *reinterpret_cast<float4*>(fwd_field(p, F_X2P, l, p.step).row(b) + c) = o;
   }
-  wg_arrive(ctr(p, l, C_ROWS));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-arming stores, before the next hand-off
 }
 
 // ------------------------------------------------------------------------ FFN: rows into LDS
-// rows c0 .. c0+nr-1 of a handed-off [B][768] f32 field (sc1) into the padded image L.x
-__device__ __forceinline__ void rows_to_lds(const float* src, int c0, int nr, FfL& L) {
-  constexpr int PER = RCH * (E / 4) / NT;   // 12 float4 per thread: all loads in flight at once
+// rows c0 .. c0+nr-1 of a [B][768] row mailbox into the padded image L.x: all 12 loads per thread in
+// flight at once, then the pieces not yet written are waited for
+__device__ __forceinline__ void rows_to_lds(const float* src, int c0, int nr, FfL& L, const LrceDecStep& p, unsigned code) {
+  constexpr int PER = RCH * (E / 4) / NT;
   float4 v[PER];
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -513,6 +585,7 @@ __device__ __forceinline__ void rows_to_lds(const float* src, int c0, int nr, Ff
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int i = threadIdx.x + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
+    if (rr < nr && unset4(v[q])) v[q] = ld4_wait(src, (long long)(c0 + rr) * E + k, p, code);
     *reinterpret_cast<float4*>(L.x + rr * XROW + (k / 96) * XP + (k % 96)) = v[q];
   }
 }
@@ -543,7 +616,7 @@ __device__ __forceinline__ void wave_sum_x4(float (&v)[4]) {
 // wave-per-row LayerNorm (forward) of the image rows in place, the wave's rows rr = wave + 4 q (q < 4)
 // processed together; lane owns k = 12 lane .. 12 lane + 11
 __device__ void ln_rows_fwd(FfL& L, int nr, const float* g, const float* be, float eps, float* mean_out, float* rstd_out,
-                            float* y_rows /* sc1-stored copy or NULL */, int c0) {
+                            float* y_rows /* sc1-stored mailbox copy or NULL */, float* y_keep /* arena copy */, int c0) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float4 v[4][3];
   float s1[4], s2[4];
@@ -581,7 +654,10 @@ __device__ void ln_rows_fwd(FfL& L, int nr, const float* g, const float* be, flo
       const float4 y = make_float4((v[q][i].x - mu) * rs * gg.x + bb.x, (v[q][i].y - mu) * rs * gg.y + bb.y,
                                    (v[q][i].z - mu) * rs * gg.z + bb.z, (v[q][i].w - mu) * rs * gg.w + bb.w);
       *reinterpret_cast<float4*>(xp + 4 * i) = y;
-      if (y_rows) st4_sc1(y_rows, (long long)(c0 + rr) * E + k, y);
+      if (y_rows) {
+        st4_sc1(y_rows, (long long)(c0 + rr) * E + k, y);
+        *reinterpret_cast<float4*>(y_keep + (long long)(c0 + rr) * E + k) = y;
+      }
     }
     if (lane == 0 && mean_out) {
       mean_out[c0 + rr] = mu;
@@ -642,9 +718,9 @@ __device__ __forceinline__ void ffn_slices_dma(const f16* w1, const f16* w2, int
 
 // Forward FFN slice j (32 hidden units) over all rows, 16 rows per chunk as the MFMA M dimension:
 // linear1 (wave = 16 hidden units x half of K, the halves added through LDS) -> + b1 -> pre, GELU,
-// dropout -> gd; linear2 partial (wave = 12 of the 48 output tiles, K = 32) -> P_j.  The weight
-// fragments are loaded before the wait (wait: the row counter, NULL for a second slice).
-__device__ bool ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, unsigned* wait, unsigned* ok_word,
+// dropout -> gd; linear2 partial (wave = 12 of the 48 output tiles, K = 32) -> P_j.  The weight slices
+// are issued before the rows are waited for (mbx2: the layer's x2p mailbox, mbxn: its x2 mailbox).
+__device__ void ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, const float* mbx2, float* mbxn,
                               unsigned long long* trace) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
   const int ct = wave & 1, kh = wave >> 1;
@@ -654,21 +730,19 @@ __device__ bool ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
   ffn_slices_dma(w1, w2, j, L, wave, lane);
   const float b1v = W.b1[j * FS + ct * 16 + col];
   SUB_MARK(0, 0);
-  if (wait && !wg_wait(wait, p.B, p, 0x400 + l, ok_word)) return false;
   SUB_MARK(0, 1);
   Ar pre = fwd_field(p, F_PRE, l, p.step), gd = fwd_field(p, F_GD, l, p.step);
-  const float* x2p = fwd_field(p, F_X2P, l, p.step).base;
   float* Pj = p.ws + 2 * WS_SLAB + (long long)j * MAXB * E;
   const bool owner = j == 0;   // slice 0's workgroup materialises x2 (read back by the next layer's reducers) and its stats
   for (int c0 = 0; c0 < p.B; c0 += RCH) {
     const int nr = min(RCH, p.B - c0);
     lds_barrier();   // the previous chunk's image is consumed
-    rows_to_lds(x2p, c0, nr, L);
+    rows_to_lds(mbx2, c0, nr, L, p, 0x500 + l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (first chunk) the weight slices have landed too
     lds_barrier();
     SUB_MARK(0, 2);
     ln_rows_fwd(L, nr, W.g2, W.be2, p.eps, owner ? fwd_field(p, F_M2, l, p.step).base : nullptr,
-                owner ? fwd_field(p, F_R2, l, p.step).base : nullptr, owner ? fwd_field(p, F_X2, l, p.step).base : nullptr, c0);
+                owner ? fwd_field(p, F_R2, l, p.step).base : nullptr, owner ? mbxn : nullptr, fwd_field(p, F_X2, l, p.step).base, c0);
     lds_barrier();
     SUB_MARK(0, 3);
     // linear1 slice
@@ -717,7 +791,6 @@ __device__ bool ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     tiles_out(L, o, Pj, c0, nr);
     SUB_MARK(0, 6);
   }
-  return true;
 }
 
 // ------------------------------------------------------------------------------- forward kernel
@@ -730,41 +803,36 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
   const int h = blockIdx.x % H, r = blockIdx.x / H;
   const uint64_t roff = rng_off_now(rng_off);
   const int L_ = p.n_layers;
+  const unsigned set = launch_begin(p);
   for (int l = 0; l < L_; ++l) {
     const LrceDecLayerW& W = p.layer[l];
     const uint64_t sl = layer_seed(p, l) + roff;
     // ---- A: self-attention block (after reducing the previous layer's FFN partials)
     STEP_MARK(0, l, 0);
-    uint4 wr[NRI];
-    rows_load(reinterpret_cast<const f16*>(W.wv), h * D + wave * WROWS, lane, wr);
-    const float bvv = t < D ? W.bv[h * D + t] : 0.f;
     SaL& S = U.sa;
     lds_barrier();
     slice_dma(reinterpret_cast<const f16*>(W.wo), h, S.wo, wave, lane);
     if (l > 0) {
-      if (!wg_wait(ctr(p, l - 1, C_SL), NF, p, 0x100 + l, &ok_word)) return;
       STEP_MARK(0, l, 1);
       const LrceDecLayerW& Wp = p.layer[l - 1];
       for (int b = r; b < p.B; b += R)
         slice_reduce(p.ws + 2 * WS_SLAB, b, h, Wp.b2, p.drop_p, layer_seed(p, l - 1) + 5 + roff,
-                     fwd_field(p, F_X2, l - 1, p.step).row(b), fwd_field(p, F_X3P, l - 1, p.step).row(b), RD);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t == 0)
-        for (int b = r; b < p.B; b += R) __hip_atomic_fetch_add(ctr(p, l - 1, C_X3) + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                     mb_of(p, set, K_X2, l - 1) + (long long)b * E, mb_of(p, set, K_X3P, l - 1) + (long long)b * E,
+                     fwd_field(p, F_X3P, l - 1, p.step).row(b), RD, p, 0x100 + l);
     }
+    // W_v rows into registers after the reduce (held across it they cost spills)
+    const float bvv = t < D ? W.bv[h * D + t] : 0.f;
     bool first = true;
     for (int b = r; b < p.B; b += R) {
       if (l > 0) {
-        if (!wg_wait(ctr(p, l - 1, C_X3) + b, H, p, 0x200 + l, &ok_word)) return;
-        if (first) STEP_MARK(0, l, 2);
         const LrceDecLayerW& Wp = p.layer[l - 1];
         float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
         if (t < E / 4) {
-          xr = ld4_sc1(fwd_field(p, F_X3P, l - 1, p.step).row(b), 4 * t);
+          xr = ld4_wait(mb_of(p, set, K_X3P, l - 1) + (long long)b * E, 4 * t, p, 0x600 + l);
           gg = *reinterpret_cast<const float4*>(Wp.g3 + 4 * t);
           be = *reinterpret_cast<const float4*>(Wp.be3 + 4 * t);
         }
+        if (first) STEP_MARK(0, l, 2);
         float mu, rs;
         ln_row_fwd(xr, row_sum_local(xr, t), gg, be, p.eps, S.x0, S.red2, t, lane, wave, mu, rs);
         if (h == 0) {
@@ -779,7 +847,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
         *reinterpret_cast<float4*>(S.x0 + 4 * t) = *reinterpret_cast<const float4*>(fwd_field(p, F_X0, 0, p.step).row(b) + 4 * t);
       }
       lds_barrier();
-      sa_fwd_row(p, l, b, h, wr, bvv, S, sl, sl + 1, first);
+      sa_fwd_row(p, l, b, h, reinterpret_cast<const f16*>(W.wv), bvv, S, sl, sl + 1, first, RD, mb_of(p, set, K_X1P, l));
       first = false;
       lds_barrier();
     }
@@ -787,47 +855,39 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
     // ---- B: cross-attention block
     CaL& C = U.ca;
     lds_barrier();
-    rows_load(reinterpret_cast<const f16*>(W.wq), h * D + wave * WROWS, lane, wr);
     const float bqv = t < D ? W.bq[h * D + t] : 0.f;
     slice_dma(reinterpret_cast<const f16*>(W.woc), h, C.wo, wave, lane);
     first = true;
     for (int b = r; b < p.B; b += R) {
       uint4 kr[8];
       ca_fwd_prefetch(p, l, b, h, C, kr);
-      if (!wg_wait(ctr(p, l, C_X1) + b, 1, p, 0x300 + l, &ok_word)) return;
       if (first) STEP_MARK(0, l, 4);
-      ca_fwd_row(p, l, b, h, wr, bqv, C, sl + 2, sl + 3, kr);
+      ca_fwd_row(p, l, b, h, reinterpret_cast<const f16*>(W.wq), bqv, C, sl + 2, sl + 3, kr, RD, mb_of(p, set, K_X1P, l), mb_of(p, set, K_X2P, l));
       first = false;
       lds_barrier();
     }
     STEP_MARK(0, l, 5);
     // ---- C: FFN slices over all rows
     for (int j = blockIdx.x; j < NF; j += G) {
-      if (!ffn_fwd_slice(p, l, j, U.ff, sl + 4, j == (int)blockIdx.x ? ctr(p, l, C_ROWS) : nullptr, &ok_word, trace)) return;
-      wg_arrive(ctr(p, l, C_SL));
+      ffn_fwd_slice(p, l, j, U.ff, sl + 4, mb_of(p, set, K_X2P, l), mb_of(p, set, K_X2, l), trace);
       SUB_MARK(0, 7);
     }
     STEP_MARK(0, l, 7);
   }
   // ---- step tail: x3p of the last layer, then (head 0) x3 = LN3, tsum = x3 + s, s' = drop(LN_f(tsum))
   const int Ll = L_ - 1;
-  if (!wg_wait(ctr(p, Ll, C_SL), NF, p, 0x500, &ok_word)) return;
   STEP_MARK(0, L_, 1);
   for (int b = r; b < p.B; b += R)
     slice_reduce(p.ws + 2 * WS_SLAB, b, h, p.layer[Ll].b2, p.drop_p, layer_seed(p, Ll) + 5 + roff,
-                 fwd_field(p, F_X2, Ll, p.step).row(b), fwd_field(p, F_X3P, Ll, p.step).row(b), RD);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0)
-    for (int b = r; b < p.B; b += R) __hip_atomic_fetch_add(ctr(p, Ll, C_X3) + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                 mb_of(p, set, K_X2, Ll) + (long long)b * E, mb_of(p, set, K_X3P, Ll) + (long long)b * E,
+                 fwd_field(p, F_X3P, Ll, p.step).row(b), RD, p, 0x700);
   if (h == 0) {
     SaL& S = U.sa;
     const uint64_t st = tail_seed(p) + roff;
     for (int b = r; b < p.B; b += R) {
-      if (!wg_wait(ctr(p, Ll, C_X3) + b, H, p, 0x600, &ok_word)) return;
       float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
       if (t < E / 4) {
-        xr = ld4_sc1(fwd_field(p, F_X3P, Ll, p.step).row(b), 4 * t);
+        xr = ld4_wait(mb_of(p, set, K_X3P, Ll) + (long long)b * E, 4 * t, p, 0x800);
         gg = *reinterpret_cast<const float4*>(p.layer[Ll].g3 + 4 * t);
         be = *reinterpret_cast<const float4*>(p.layer[Ll].be3 + 4 * t);
       }
@@ -871,8 +931,8 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
 
 // =============================================================================== backward
 // ---------------------------------------------------------------- backward: FFN slice j, all rows
-__device__ bool ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, uint64_t seed5, unsigned* wait,
-                              unsigned* ok_word, unsigned long long* trace) {
+__device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, uint64_t seed5, const float* mbd3,
+                              float* dres, unsigned long long* trace) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
   const int ct = wave & 1, kh = wave >> 1;
   const LrceDecLayerW& W = p.layer[l];
@@ -882,7 +942,6 @@ __device__ bool ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
   const Ar dln3 = bwd_field(p, G_DLN3, l, p.step), df = bwd_field(p, G_DF, l, p.step), dgp = bwd_field(p, G_DGP, l, p.step);
   const Ar x3p = fwd_field(p, F_X3P, l, p.step), m3 = fwd_field(p, F_M3, l, p.step), r3 = fwd_field(p, F_R3, l, p.step);
   const Ar pre = fwd_field(p, F_PRE, l, p.step);
-  float* dres = p.ws + 2 * WS_SLAB + WS_P;   // dx3p rows (handed to the reducers)
   float* Qj = p.ws + 2 * WS_SLAB + (long long)j * MAXB * E;
   const bool owner = j == 0;
   // what a chunk of rows needs that this launch does not write (the forward's x3p / stats / pre-
@@ -892,7 +951,6 @@ __device__ bool ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
   };
   prefetch(0, min(RCH, p.B));
   SUB_MARK(1, 0);
-  if (wait && !wg_wait(wait, p.B, p, 0x700 + l, ok_word)) return false;
   SUB_MARK(1, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slices and prefetches have landed (read after the next barrier)
   lds_barrier();
@@ -906,7 +964,7 @@ __device__ bool ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     const int nr = min(RCH, p.B - c0);
     lds_barrier();
     if (c0 > 0) prefetch(c0, nr);
-    rows_to_lds(dln3.base, c0, nr, L);
+    rows_to_lds(mbd3, c0, nr, L, p, 0x900 + l);
     lds_barrier();
     SUB_MARK(1, 3);
     // LayerNorm-3 backward per row (the wave's four rows together), then the out-dropout backward -> df
@@ -1000,7 +1058,6 @@ __device__ bool ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     tiles_out(L, o, Qj, c0, nr);
     SUB_MARK(1, 6);
   }
-  return true;
 }
 
 // ------------------------------------------------------------ backward: cross-attention row b
@@ -1058,12 +1115,12 @@ __device__ void ca_bwd_prefetch(const LrceDecStep& p, int l, int b, int h, CaL& 
 }
 
 __device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, CaL& L, uint64_t seed2, uint64_t seed3,
-                           const CaBwdPre& q) {
+                           const CaBwdPre& q, RedL& RD, const float* mbd2, float* mbd1) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const KvP kv = kv_of(p, l);
   const int Lk = kv.lk1 + kv.lk2;
   float4 dy = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (t < E / 4) dy = ld4_sc1(bwd_field(p, G_DLN2, l, p.step).row(b), 4 * t);
+  if (t < E / 4) dy = ld4_wait(mbd2 + (long long)b * E, 4 * t, p, 0xB00 + l);
   const float rs = q.rs, qd = q.qd, od = q.od, lse = q.lse;
   LnBwdLocal lnl = ln_row_bwd_local(dy, q.xr, q.gm, q.mu, rs, t);
   const float* dk2r = p.lt ? p.dkv_text + l * p.dkv_text_lstride : nullptr;
@@ -1187,20 +1244,27 @@ __device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, CaL& L, ui
   lds_barrier();
   float* part = &L.b.acc[0][0];
   rows_t_lds(L.wo, L.b.dq, part);
-  if (!publish4(part, p.ws, ctr(p, l, C_SA), b, h, &L.last)) return;
-  if (t < E / 4) st4_sc1(bwd_field(p, G_DLN1, l, p.step).row(b), 4 * t, add4(lds4(L.b.dx2p + 4 * t), gather4(p.ws, b, t)));
-  wg_arrive(ctr(p, l, C_X1) + b);
+  publish(part, p.ws, b, h);
+  const float4 sm = gather_cols(p.ws, b, h, RD.red, p, 0xC00 + l);
+  if (t < 16) {
+    const int c = h * D + 4 * t;
+    const float4 o = add4(lds4(L.b.dx2p + c), sm);
+    st4_sc1(mbd1 + (long long)b * E, c, o);
+    *reinterpret_cast<float4*>(bwd_field(p, G_DLN1, l, p.step).row(b) + c) = o;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-arming stores, before the next hand-off
 }
 
 // ------------------------------------------------------------- backward: self-attention row b
 // dx1 (handed-off row) -> LN1' -> dsao -> dsav_h -> the last head writes dx0 = dx1p + sum_h W_v[h]^T dsav_h:
 // d x3 of layer l-1 (handed off), or (l = 0) the step input's gradient dx0 + dt.
-__device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, SaL& L, uint64_t seed0, uint64_t seed1) {
+__device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, SaL& L, uint64_t seed0, uint64_t seed1, RedL& RD,
+                           const float* mbd1, float* mbd3, const float* mbdt) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
   float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
   if (t < E / 4) {
-    dy = ld4_sc1(bwd_field(p, G_DLN1, l, p.step).row(b), 4 * t);
+    dy = ld4_wait(mbd1 + (long long)b * E, 4 * t, p, 0xD00 + l);
     xr = *reinterpret_cast<const float4*>(fwd_field(p, F_X1P, l, p.step).row(b) + 4 * t);
     gm = *reinterpret_cast<const float4*>(W.g1 + 4 * t);
   }
@@ -1234,15 +1298,20 @@ __device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, SaL& L, ui
   lds_barrier();
   float* part = &L.acc[0][0];
   rows_t_lds(L.wo, L.v, part);
-  if (!publish4(part, p.ws + WS_SLAB, ctr(p, l, C_CA), b, h, &L.last)) return;
-  if (l > 0) {
-    if (t < E / 4)
-      st4_sc1(bwd_field(p, G_DLN3, l - 1, p.step).row(b), 4 * t, add4(lds4(L.dx1p + 4 * t), gather4(p.ws + WS_SLAB, b, t)));
-    wg_arrive(ctr(p, l - 1, C_ROWS));
-  } else if (t < E / 4) {
-    const float4 dt = ld4_sc1(bwd_field(p, G_DCAO, p.n_layers, p.step).row(b), 4 * t);
-    *reinterpret_cast<float4*>(p.ds_out + (long long)b * E + 4 * t) = add4(add4(lds4(L.dx1p + 4 * t), gather4(p.ws + WS_SLAB, b, t)), dt);
+  publish(part, p.ws + WS_SLAB, b, h);
+  const float4 sm = gather_cols(p.ws + WS_SLAB, b, h, RD.red, p, 0xE00 + l);
+  if (t < 16) {
+    const int c = h * D + 4 * t;
+    if (l > 0) {
+      const float4 o = add4(lds4(L.dx1p + c), sm);
+      st4_sc1(mbd3 + (long long)b * E, c, o);
+      *reinterpret_cast<float4*>(bwd_field(p, G_DLN3, l - 1, p.step).row(b) + c) = o;
+    } else {
+      const float4 dt = ld4_wait(mbdt + (long long)b * E, c, p, 0xF00);
+      *reinterpret_cast<float4*>(p.ds_out + (long long)b * E + c) = add4(add4(lds4(L.dx1p + c), sm), dt);
+    }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-arming stores, before the next hand-off
 }
 
 __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, const uint64_t* rng_off, unsigned long long* trace) {
@@ -1254,6 +1323,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
   const int h = blockIdx.x % H, r = blockIdx.x / H;
   const uint64_t roff = rng_off_now(rng_off);
   const int L_ = p.n_layers;
+  const unsigned set = launch_begin(p);
   // ---- tail: du = drop'(ds), dt = LN_f'(du) -> d x3 of the last layer
   STEP_MARK(1, L_, 0);
   if (h == 0) {
@@ -1276,10 +1346,11 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
       LnBwdLocal lnl = ln_row_bwd_local(dy, xr, gm, mu, rs, t);
       const float4 dx = ln_row_bwd(lnl, rs, S.red2, lane, wave);
       if (t < E / 4) {
-        st4_sc1(bwd_field(p, G_DCAO, L_, p.step).row(b), 4 * t, dx);    // dt (read back by the layer-0 tail of this launch)
-        st4_sc1(bwd_field(p, G_DLN3, L_ - 1, p.step).row(b), 4 * t, dx);
+        *reinterpret_cast<float4*>(bwd_field(p, G_DCAO, L_, p.step).row(b) + 4 * t) = dx;   // dt
+        *reinterpret_cast<float4*>(bwd_field(p, G_DLN3, L_ - 1, p.step).row(b) + 4 * t) = dx;
+        st4_sc1(mb_of(p, set, K_DT, 0) + (long long)b * E, 4 * t, dx);         // read by layer 0's last step
+        st4_sc1(mb_of(p, set, K_DLN3, L_ - 1) + (long long)b * E, 4 * t, dx);
       }
-      wg_arrive(ctr(p, L_ - 1, C_ROWS));
     }
   }
   for (int l = L_ - 1; l >= 0; --l) {
@@ -1288,37 +1359,29 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
     // ---- FB: FFN slices over all rows
     STEP_MARK(1, l, 0);
     for (int j = blockIdx.x; j < NF; j += G) {
-      if (!ffn_bwd_slice(p, l, j, U.ff, sl + 4, sl + 5, j == (int)blockIdx.x ? ctr(p, l, C_ROWS) : nullptr, &ok_word, trace)) return;
-      wg_arrive(ctr(p, l, C_SL));
+      ffn_bwd_slice(p, l, j, U.ff, sl + 4, sl + 5, mb_of(p, set, K_DLN3, l), mb_of(p, set, K_DRES, l), trace);
       SUB_MARK(1, 7);
     }
     // ---- CB: dx2 slices, then the cross-attention block backward per row; the weight slices and the
-    // first row's saved operands / K / V images are issued before the wait for the FFN slices
+    // first row's saved operands / K / V images are issued before the FFN slices are waited for
     CaL& C = U.ca;
     lds_barrier();
     slice_dma(reinterpret_cast<const f16*>(W.woc), h, C.wo, wave, lane);
-    CaBwdPre pre;
-    ca_bwd_prefetch(p, l, r, h, C, pre);
     STEP_MARK(1, l, 2);
-    if (!wg_wait(ctr(p, l, C_SL), NF, p, 0x800 + l, &ok_word)) return;
     STEP_MARK(1, l, 3);
     for (int b = r; b < p.B; b += R)
-      slice_reduce(p.ws + 2 * WS_SLAB, b, h, nullptr, 0.f, 0, p.ws + 2 * WS_SLAB + WS_P + (long long)b * E,
-                   bwd_field(p, G_DLN2, l, p.step).row(b), RD);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0)
-      for (int b = r; b < p.B; b += R) __hip_atomic_fetch_add(ctr(p, l, C_X3) + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      slice_reduce(p.ws + 2 * WS_SLAB, b, h, nullptr, 0.f, 0, mb_of(p, set, K_DRES, l) + (long long)b * E,
+                   mb_of(p, set, K_DLN2, l) + (long long)b * E, bwd_field(p, G_DLN2, l, p.step).row(b), RD, p, 0xA00 + l);
+    // the row's saved operands and K / V images after the reduce (held across it they cost spills)
+    CaBwdPre pre;
     bool first = true;
     for (int b = r; b < p.B; b += R) {
-      if (!first) {   // the previous row left W_q rows in the slice's place
+      if (!first)   // the previous row left W_q rows in the slice's place
         slice_dma(reinterpret_cast<const f16*>(W.woc), h, C.wo, wave, lane);
-        ca_bwd_prefetch(p, l, b, h, C, pre);
-      }
-      if (!wg_wait(ctr(p, l, C_X3) + b, H, p, 0x900 + l, &ok_word)) return;
+      ca_bwd_prefetch(p, l, b, h, C, pre);
       if (first) STEP_MARK(1, l, 4);
       first = false;
-      ca_bwd_row(p, l, b, h, C, sl + 2, sl + 3, pre);
+      ca_bwd_row(p, l, b, h, C, sl + 2, sl + 3, pre, RD, mb_of(p, set, K_DLN2, l), mb_of(p, set, K_DLN1, l));
       lds_barrier();
     }
     STEP_MARK(1, l, 5);
@@ -1328,10 +1391,10 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
     for (int b = r; b < p.B; b += R) {
       lds_barrier();
       slice_dma(reinterpret_cast<const f16*>(W.wo), h, S.wo, wave, lane);
-      if (!wg_wait(ctr(p, l, C_X1) + b, 1, p, 0xA00 + l, &ok_word)) return;
       if (first) STEP_MARK(1, l, 6);
       first = false;
-      sa_bwd_row(p, l, b, h, S, sl, sl + 1);
+      sa_bwd_row(p, l, b, h, S, sl, sl + 1, RD, mb_of(p, set, K_DLN1, l), l > 0 ? mb_of(p, set, K_DLN3, l - 1) : nullptr,
+                 mb_of(p, set, K_DT, 0));
       lds_barrier();
     }
     STEP_MARK(1, l, 7);
@@ -1395,10 +1458,11 @@ extern "C" int lrce_dec_step_set_trace(uint64_t* buf) {
   return LRCE_OK;
 }
 
-extern "C" int lrce_dec_step_reset(uint32_t* counters, uint32_t* status, void* stream) {
-  if (!counters || !status) return lrce_fail(LRCE_E_ARG, "dec_step_reset: null pointer");
+extern "C" int lrce_dec_step_reset(float* ws, uint32_t* counters, uint32_t* status, void* stream) {
+  if (!ws || !counters || !status) return lrce_fail(LRCE_E_ARG, "dec_step_reset: null pointer");
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(counters, 0, CTR_WORDS * sizeof(uint32_t), st) != hipSuccess ||
+  if (hipMemsetAsync(ws, 0xFF, WS_ELEMS * sizeof(float), st) != hipSuccess ||
+      hipMemsetAsync(counters, 0, CTR_WORDS * sizeof(uint32_t), st) != hipSuccess ||
       hipMemsetAsync(status, 0, 4 * sizeof(uint32_t), st) != hipSuccess)
     return lrce_fail(LRCE_E_LAUNCH, "dec_step_reset: memset failed");
   return LRCE_OK;

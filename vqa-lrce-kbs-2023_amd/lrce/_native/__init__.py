@@ -218,7 +218,7 @@ _SIGS = {
     "lrce_dec_set_trace": [_P],
     "lrce_dec_step_fwd": [ctypes.POINTER(DecStep), _P],
     "lrce_dec_step_bwd": [ctypes.POINTER(DecStep), _P],
-    "lrce_dec_step_reset": [_P, _P, _P],
+    "lrce_dec_step_reset": [_P, _P, _P, _P],
     "lrce_dec_step_field": [_I, _I, _I, _I, _I, _I],
     "lrce_dec_step_ws_elems": [],
     "lrce_dec_step_counter_words": [],

@@ -679,12 +679,13 @@ DEC_STEP_BWD_FIELDS = ("df", "dgp", "dcao", "dq", "dsao", "dsav", "dln1", "dln2"
 
 def dec_step_workspace(device):
     """(ws f32, counters int32, status int32[4]) of the persistent decoder step, one per device (the
-    decoder runs on one stream at a time; the counters are left zero by every launch)."""
+    decoder runs on one stream at a time).  The workspace starts with every byte 0xFF: the hand-off
+    buffers' sentinel, which every launch leaves in place (lrce_dec_step_reset restores it)."""
     key = torch.device(device)
     ws = _STEP_WS.get(key)
     if ws is None:
         L = N.lib()
-        ws = (torch.empty(int(L.lrce_dec_step_ws_elems()), dtype=F32, device=key),
+        ws = (torch.full((int(L.lrce_dec_step_ws_elems()),), -1, dtype=torch.int32, device=key).view(F32),
               torch.zeros(int(L.lrce_dec_step_counter_words()), dtype=torch.int32, device=key),
               torch.zeros(4, dtype=torch.int32, device=key))
         _STEP_WS[key] = ws
@@ -711,14 +712,14 @@ def dec_step_bwd(desc, stream_tensor):
 
 def dec_step_status(device, reset=True):
     """status[0] of the persistent decoder step (synchronises): 0, or the code of a hand-off that timed
-    out (0x100-0xAFF: phase << 8 | layer).  A timed-out launch leaves its counters set: reset=True
-    zeroes them and the status."""
+    out (0x100-0x1FFF: phase << 8 | layer).  A timed-out launch leaves the hand-off buffers half used:
+    reset=True re-arms them and zeroes the counters and the status."""
     ws = _STEP_WS.get(torch.device(device))
     if ws is None:
         return 0
     code = int(ws[2][0].item())
     if code and reset:
-        call("lrce_dec_step_reset", ptr(ws[1]), ptr(ws[2]), stream_of(ws[2]))
+        call("lrce_dec_step_reset", ptr(ws[0]), ptr(ws[1]), ptr(ws[2]), stream_of(ws[2]))
         torch.cuda.synchronize(device)
     return code
 
