@@ -358,6 +358,7 @@ def main():
     gdt = torch.bfloat16 if args.grad_reduce_dtype == "bf16" else torch.float32
     log(f"rank {rank}/{world}: building model (bs={args.batch_size})")
     model, opt, reducer, batch = build(args.batch_size, device, gdt)
+    torch.cuda.reset_peak_memory_stats(device)
     step = make_step(model, opt, reducer, batch, args.mode, world)
     split_stage = getattr(model, "split_swin_stage", None) if world > 1 else None
     for i in range(args.warmup):
@@ -384,6 +385,7 @@ def main():
         dist.all_gather(ds, d)
         replicas = all(torch.equal(ds[0], x) for x in ds)
     loss_v = float(loss.item())
+    peak_gib = torch.cuda.max_memory_allocated(device) / 2 ** 30   # warmup (eager step + capture) and replays
     samples = world * args.batch_size * args.steps
     value = samples / elapsed
     ms = 1000.0 * elapsed / args.steps
@@ -428,6 +430,7 @@ def main():
            "loss": round(loss_v, 4),
            "model_tflops": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0, 2),
            "model_mfu": round(STEP_GFLOP_PER_SAMPLE * value / 1000.0 / (MFMA_BF16_PEAK_TFLOPS * world), 4)}
+    out["peak_memory_gib"] = round(peak_gib, 2)   # torch allocator peak of the measured step (graph pool included)
     out["roofline"] = roof
     if world > 1:
         out["replicas_identical"] = replicas   # the ranks' master weights after the timed steps

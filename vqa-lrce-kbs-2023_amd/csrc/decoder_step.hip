@@ -684,6 +684,20 @@ __device__ __forceinline__ f32x4 mfma4(float4 a, float4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
 }
 
+// The same 16 k as an f32 x fp16 product on the f16 MFMA: a split into hi = f16(a) and lo = f16(a - hi)
+// (a = hi + lo to ~22 bits: the products of fp16 weights with either part are exact in f32), two
+// v_mfma_f32_16x16x16_f16 (K = 16, 8 passes each) in place of four f32 16x16x4 (32 passes each) and
+// the weight conversions.  b: four fp16 of B(k0 + 4 (lane >> 4) + e, j).  For operands of order one
+// (LayerNorm outputs, GELU activations): no scaling needed for the f16 range.
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4v;
+__device__ __forceinline__ f32x4 mfma_sp(float4 a, uint2 b, f32x4 c) {
+  const f16x4v hi = {(f16)a.x, (f16)a.y, (f16)a.z, (f16)a.w};
+  const f16x4v lo = {(f16)(a.x - (float)hi[0]), (f16)(a.y - (float)hi[1]), (f16)(a.z - (float)hi[2]), (f16)(a.w - (float)hi[3])};
+  const f16x4v bb = __builtin_bit_cast(f16x4v, b);
+  c = __builtin_amdgcn_mfma_f32_16x16x16f16(hi, bb, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x16f16(lo, bb, c, 0, 0, 0);
+}
+
 // C tiles of one wave (12 column tiles of 16 over the 768 outputs, rows = the chunk's 16 rows) -> the
 // padded image, then the chunk's live rows -> dst (write-through 16-B stores)
 __device__ __forceinline__ void tiles_out(FfL& L, const f32x4 (&acc)[12], float* dst, int c0, int nr) {
@@ -749,8 +763,8 @@ __device__ void ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     f32x4 acc4[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 24; ++s)   // four independent accumulation chains
-      acc4[s & 3] = mfma4(*reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq)),
-                          h4f(*reinterpret_cast<const uint2*>(L.w1s + (ct * 16 + col) * E + kh * 384 + 16 * s + 4 * kq)), acc4[s & 3]);
+      acc4[s & 3] = mfma_sp(*reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq)),
+                            *reinterpret_cast<const uint2*>(L.w1s + (ct * 16 + col) * E + kh * 384 + 16 * s + 4 * kq), acc4[s & 3]);
     f32x4 acc;
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[r] = (acc4[0][r] + acc4[1][r]) + (acc4[2][r] + acc4[3][r]);
@@ -785,7 +799,7 @@ __device__ void ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
       const float4 a = *reinterpret_cast<const float4*>(&L.hb[col][16 * q + 4 * kq]);
 #pragma unroll
       for (int tt = 0; tt < 12; ++tt)
-        o[tt] = mfma4(a, h4f(*reinterpret_cast<const uint2*>(L.w2s + ((wave * 12 + tt) * 16 + col) * FS + 16 * q + 4 * kq)), o[tt]);
+        o[tt] = mfma_sp(a, *reinterpret_cast<const uint2*>(L.w2s + ((wave * 12 + tt) * 16 + col) * FS + 16 * q + 4 * kq), o[tt]);
     }
     SUB_MARK(0, 5);
     tiles_out(L, o, Pj, c0, nr);
