@@ -325,6 +325,7 @@ struct FfL {                      // FFN slices over all rows (MFMA: the rows ar
   f16 w2s[E * FS];                // backward: the W2 column slice [768][32]
   f16 w1s[FS * E];                // backward: the W1 row slice [32][768]
   float preb[RCH][FS];            // backward: the saved pre-activations of the chunk's rows
+  float rsc[RCH], rinv[RCH];      // backward: per-row power-of-two scale of the f16-split MFMA operands
 };
 struct RedL {                     // the FFN-partial reduce (outside the union: the next phase's weight
   float4 red[16][16];             // slices stream into the union while it runs)
@@ -606,6 +607,17 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
   const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
   return (r0 + r1) + (r2 + r3);
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {   // v >= 0
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 // the four rows of a wave reduced together (independent chains: their latencies overlap)
 __device__ __forceinline__ void wave_sum_x4(float (&v)[4]) {
@@ -1023,6 +1035,31 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
           d = drop4(d, p.drop_p, seed5, (long long)b * E + k);
           *reinterpret_cast<float4*>(xp + 4 * i) = d;
           if (owner) *reinterpret_cast<float4*>(df.row(b) + k) = d;
+          g[q][i] = d;   // (for the row maximum below)
+        }
+      }
+      // per-row power-of-two scale 2^(7 - e), e = exponent of the row's max |df|: the f16-split operands
+      // of this chunk (df, then dgp) sit in [2^7, 2^8) at most, far from the f16 range's ends (exact:
+      // the products and the later unscaling are by powers of two)
+      float mx[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        mx[q] = 0.f;
+        if (wave + 4 * q < nr) {
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+            mx[q] = fmaxf(mx[q], fmaxf(fmaxf(fabsf(g[q][i].x), fabsf(g[q][i].y)), fmaxf(fabsf(g[q][i].z), fabsf(g[q][i].w))));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mx[q] = wave_max_dpp(mx[q]);
+      if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rr = wave + 4 * q;
+          const int e = mx[q] > 0.f ? ilogbf(mx[q]) : 0;
+          L.rsc[rr] = ldexpf(1.0f, 7 - e);
+          L.rinv[rr] = ldexpf(1.0f, e - 7);
         }
       }
     }
@@ -1031,9 +1068,12 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     // dgp = drop'(W2[:, slice]^T df) gelu'(pre)
     f32x4 acc4[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int s = 0; s < 24; ++s)
-      acc4[s & 3] = mfma4(*reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq)),
-                          h4f(pack4(L.w2s + (kh * 384 + 16 * s + 4 * kq) * FS + ct * 16 + col, FS)), acc4[s & 3]);
+    for (int s = 0; s < 24; ++s) {
+      const float sa = L.rsc[col];
+      float4 a = *reinterpret_cast<const float4*>(xat(L, col, kh * 384 + 16 * s + 4 * kq));
+      a = make_float4(a.x * sa, a.y * sa, a.z * sa, a.w * sa);
+      acc4[s & 3] = mfma_sp(a, pack4(L.w2s + (kh * 384 + 16 * s + 4 * kq) * FS + ct * 16 + col, FS), acc4[s & 3]);
+    }
     f32x4 acc;
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[r] = (acc4[0][r] + acc4[1][r]) + (acc4[2][r] + acc4[3][r]);
@@ -1048,12 +1088,12 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
         const int rr = 4 * kq + r, b = c0 + rr, cc = ct * 16 + col, cg = j * FS + cc;
         float d = 0.f;
         if (rr < nr) {
-          d = acc[r] + L.kacc[ct][rr][col];
+          d = acc[r] + L.kacc[ct][rr][col];   // scaled by rsc[rr]
           if (p.drop_p > 0.f) d = drop1(d, p.drop_p, seed4, (long long)b * FF + cg);
           d *= gelu_grad_f(L.preb[rr][cc]);
-          dgp.row(b)[cg] = d;
+          dgp.row(b)[cg] = d * L.rinv[rr];
         }
-        L.hb[rr][cc] = d;
+        L.hb[rr][cc] = d;   // kept scaled for Q_j
       }
     }
     lds_barrier();
@@ -1066,7 +1106,13 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
       const float4 a = *reinterpret_cast<const float4*>(&L.hb[col][16 * q + 4 * kq]);
 #pragma unroll
       for (int tt = 0; tt < 12; ++tt)
-        o[tt] = mfma4(a, h4f(pack4(L.w1s + (16 * q + 4 * kq) * E + (wave * 12 + tt) * 16 + col, E)), o[tt]);
+        o[tt] = mfma_sp(a, pack4(L.w1s + (16 * q + 4 * kq) * E + (wave * 12 + tt) * 16 + col, E), o[tt]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {   // unscale row 4 kq + r
+      const float u = L.rinv[4 * kq + r];
+#pragma unroll
+      for (int tt = 0; tt < 12; ++tt) o[tt][r] *= u;
     }
     SUB_MARK(1, 5);
     tiles_out(L, o, Qj, c0, nr);
@@ -1083,7 +1129,6 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
 struct CaBwdPre {
   float4 xr, gm;
   float mu, rs, qd, od, lse;
-  float4 told[TXI][4];
 };
 __device__ void ca_bwd_prefetch(const LrceDecStep& p, int l, int b, int h, CaL& L, CaBwdPre& q) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -1103,21 +1148,6 @@ __device__ void ca_bwd_prefetch(const LrceDecStep& p, int l, int b, int h, CaL& 
     q.od = fwd_field(p, F_CTX, l, p.step).row(b)[h * D + t];
   }
   q.lse = fwd_field(p, F_LSE, l, p.step).row(b)[h];
-  const bool dk2_store = p.step == p.S - 1;
-  const float* dk2 = p.lt ? p.dkv_text + l * p.dkv_text_lstride : nullptr;
-  const long long tbase = (long long)b * p.lt * 2 * E + h * D;
-#pragma unroll
-  for (int i = 0; i < TXI; ++i) {
-    const int e = t + 256 * i, tj = e >> 3, c = e & 7;
-    q.told[i][0] = q.told[i][1] = q.told[i][2] = q.told[i][3] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tj < kv.lk2 && !dk2_store) {
-      const float* src = dk2 + tbase + (long long)tj * 2 * E + c * 8;
-      q.told[i][0] = *reinterpret_cast<const float4*>(src);
-      q.told[i][1] = *reinterpret_cast<const float4*>(src + 4);
-      q.told[i][2] = *reinterpret_cast<const float4*>(src + E);
-      q.told[i][3] = *reinterpret_cast<const float4*>(src + E + 4);
-    }
-  }
   const KvRows kvr = kv_rows(kv, b, h);
   const uint32_t kb = dec_lds_addr(L.b.kimg), vb = dec_lds_addr(L.vimg);
   for (int ins = wave; ins * 8 < Lk; ins += 4) {
@@ -1201,6 +1231,24 @@ __device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, CaL& L, ui
     if (j < Lk) dq0 += L.b.dss[j] * kv_at(L.b.kimg, j, lane);
     L.b.red64[wave][lane] = dq0 + dq1;
   }
+  // the question rows' running dK / dV (stored by the first backward step, S - 1, added to after it):
+  // loaded here, ahead of the video rows' loop that hides their latency
+  float4 told[TXI][4];
+  {
+    const bool dk2_store = p.step == p.S - 1;
+#pragma unroll
+    for (int i = 0; i < TXI; ++i) {
+      const int e = t + 256 * i, tj = e >> 3, c = e & 7;
+      told[i][0] = told[i][1] = told[i][2] = told[i][3] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (tj < kv.lk2 && !dk2_store) {
+        const float* src = dk2 + tbase + (long long)tj * 2 * E + c * 8;
+        told[i][0] = *reinterpret_cast<const float4*>(src);
+        told[i][1] = *reinterpret_cast<const float4*>(src + 4);
+        told[i][2] = *reinterpret_cast<const float4*>(src + E);
+        told[i][3] = *reinterpret_cast<const float4*>(src + E + 4);
+      }
+    }
+  }
   {
     const long long lvs = l * p.dkv_video_lstride;
     const long long vbase = (long long)(b / kv.bdiv1) * kv.stride1 + (long long)p.step * 150 * 2 * E + h * D;
@@ -1239,7 +1287,7 @@ __device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, CaL& L, ui
         const float* qv = L.b.q + c * 8;
         const float* gv = L.b.dctx + c * 8;
         float* dst = dk2 + tbase + (long long)tj * 2 * E + c * 8;
-        const float4 a0 = q.told[i][0], a1 = q.told[i][1], a2 = q.told[i][2], a3 = q.told[i][3];
+        const float4 a0 = told[i][0], a1 = told[i][1], a2 = told[i][2], a3 = told[i][3];
         *reinterpret_cast<float4*>(dst) = make_float4(a0.x + dsj * qv[0], a0.y + dsj * qv[1], a0.z + dsj * qv[2], a0.w + dsj * qv[3]);
         *reinterpret_cast<float4*>(dst + 4) = make_float4(a1.x + dsj * qv[4], a1.y + dsj * qv[5], a1.z + dsj * qv[6], a1.w + dsj * qv[7]);
         *reinterpret_cast<float4*>(dst + E) = make_float4(a2.x + pj * gv[0], a2.y + pj * gv[1], a2.z + pj * gv[2], a2.w + pj * gv[3]);
