@@ -205,6 +205,11 @@ __device__ __forceinline__ int opaque_tid() {
   asm volatile("" : "+v"(v));
   return v;
 }
+// the thread index a shared helper uses: opaque in the backward kernel (O = true: its per-lane
+// offsets are recomputed in each phase instead of hoisted and spilled), plain in the forward (which
+// does not spill and measured faster with the hoisted form)
+template <bool O>
+__device__ __forceinline__ int tid_() { return O ? opaque_tid() : (int)threadIdx.x; }
 
 // the row mailboxes of one set: kind k, layer l, row b at mb(...) + b * E
 __device__ __forceinline__ float* mb_of(const LrceDecStep& p, unsigned set, int kind, int l) {
@@ -217,7 +222,7 @@ __device__ unsigned launch_begin(const LrceDecStep& p) {
   const unsigned other = (ep + 1) & 1u;
   const long long per = (long long)p.B * (E / 4);   // float4 pieces of one (kind, layer)
   const long long tot = (long long)NKIND * p.n_layers * per;
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < tot; i += (long long)gridDim.x * NT) {
+  for (long long i = (long long)blockIdx.x * NT + opaque_tid(); i < tot; i += (long long)gridDim.x * NT) {
     const long long kl = i / per, e = i % per;
     st4_sc1(mb_of(p, other, (int)(kl / p.n_layers), (int)(kl % p.n_layers)), 4 * e, sent4());
   }
@@ -229,10 +234,10 @@ __device__ unsigned launch_begin(const LrceDecStep& p) {
 __device__ void finish(const LrceDecStep& p, unsigned* last_word) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
+  if (opaque_tid() == 0)
     *last_word = __hip_atomic_fetch_add(p.counters + C_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
-  if (!*last_word || threadIdx.x != 0) return;
+  if (!*last_word || opaque_tid() != 0) return;
   __hip_atomic_store(p.counters + C_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_add(p.counters + C_EPOCH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -243,13 +248,13 @@ unsigned long long* g_step_trace = nullptr;
 // sub-phase marks inside the FFN slices of layer 1 (slot 14 of the layer index)
 #define SUB_MARK(DIR, I)                                                                                  \
   do {                                                                                                    \
-    if (trace && l == 1 && threadIdx.x == 0)                                                              \
+    if (trace && l == 1 && opaque_tid() == 0)                                                              \
       trace[(((DIR) * 128 + blockIdx.x) * 16 + 14) * 8 + (I)] = __builtin_amdgcn_s_memrealtime();         \
   } while (0)
 #define STEP_MARK_P(DIR, L, I) do { } while (0)
 #define STEP_MARK(DIR, L, I)                                                                              \
   do {                                                                                                    \
-    if (trace && threadIdx.x == 0)                                                                        \
+    if (trace && opaque_tid() == 0)                                                                        \
       trace[(((DIR) * 128 + blockIdx.x) * 16 + (L)) * 8 + (I)] = __builtin_amdgcn_s_memrealtime();       \
   } while (0)
 __device__ __forceinline__ uint64_t layer_seed(const LrceDecStep& p, int l) {
@@ -342,9 +347,10 @@ union StepLds {
 // dx3p, epi = identity.  P pieces are waited for and re-armed (this workgroup is their only reader),
 // base is a mailbox row (waited for); out goes to the mailbox row (sc1) and to the arena row `keep`.
 // Ends with the re-arming stores drained (before this workgroup's next hand-off).
+template <bool O>
 __device__ void slice_reduce(float* P, int b, int h, const float* bias, float drop_p, uint64_t seed, const float* base_row,
                              float* out_row, float* keep, RedL& L, const LrceDecStep& p, unsigned code) {
-  const int t = threadIdx.x, q = t & 15, g = t >> 4;
+  const int t = tid_<O>(), q = t & 15, g = t >> 4;
   const int col = h * D + 4 * q;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 v[NF / 16];
@@ -397,7 +403,7 @@ __device__ __forceinline__ void rows_dma(const f16* w, int h, void* lds, int wav
 // part[4t .. 4t+3] (t < 192) = sum_r v[r] W[r][4t .. 4t+3] over the 64 LDS rows (the transposed product W^T v of
 // a backward dX partial: each thread sums all 64 rows of its 4 columns, no cross-wave reduction)
 __device__ __forceinline__ void rows_t_lds(const f16* Wl, const float* v, float* part) {
-  const int t = threadIdx.x;
+  const int t = opaque_tid();
   if (t >= E / 4) return;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
 #pragma unroll 8
@@ -575,17 +581,18 @@ __device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const f16*
 // ------------------------------------------------------------------------ FFN: rows into LDS
 // rows c0 .. c0+nr-1 of a [B][768] row mailbox into the padded image L.x: all 12 loads per thread in
 // flight at once, then the pieces not yet written are waited for
+template <bool O>
 __device__ __forceinline__ void rows_to_lds(const float* src, int c0, int nr, FfL& L, const LrceDecStep& p, unsigned code) {
   constexpr int PER = RCH * (E / 4) / NT;
   float4 v[PER];
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int i = threadIdx.x + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
+    const int i = tid_<O>() + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
     v[q] = rr < nr ? ld4_sc1(src, (long long)(c0 + rr) * E + k) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int i = threadIdx.x + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
+    const int i = tid_<O>() + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
     if (rr < nr && unset4(v[q])) v[q] = ld4_wait(src, (long long)(c0 + rr) * E + k, p, code);
     *reinterpret_cast<float4*>(L.x + rr * XROW + (k / 96) * XP + (k % 96)) = v[q];
   }
@@ -712,8 +719,9 @@ __device__ __forceinline__ f32x4 mfma_sp(float4 a, uint2 b, f32x4 c) {
 
 // C tiles of one wave (12 column tiles of 16 over the 768 outputs, rows = the chunk's 16 rows) -> the
 // padded image, then the chunk's live rows -> dst (write-through 16-B stores)
+template <bool O>
 __device__ __forceinline__ void tiles_out(FfL& L, const f32x4 (&acc)[12], float* dst, int c0, int nr) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, kq = lane >> 4;
+  const int lane = tid_<O>() & 63, wave = tid_<O>() >> 6, col = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int tt = 0; tt < 12; ++tt)
 #pragma unroll
@@ -722,7 +730,7 @@ __device__ __forceinline__ void tiles_out(FfL& L, const f32x4 (&acc)[12], float*
   constexpr int PER = RCH * (E / 4) / NT;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int i = threadIdx.x + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
+    const int i = tid_<O>() + q * NT, rr = i / (E / 4), k = (i % (E / 4)) * 4;
     if (rr < nr) st4_sc1(dst, (long long)(c0 + rr) * E + k, *reinterpret_cast<const float4*>(xat(L, rr, k)));
   }
 }
@@ -763,7 +771,7 @@ __device__ void ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
   for (int c0 = 0; c0 < p.B; c0 += RCH) {
     const int nr = min(RCH, p.B - c0);
     lds_barrier();   // the previous chunk's image is consumed
-    rows_to_lds(mbx2, c0, nr, L, p, 0x500 + l);
+    rows_to_lds<false>(mbx2, c0, nr, L, p, 0x500 + l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (first chunk) the weight slices have landed too
     lds_barrier();
     SUB_MARK(0, 2);
@@ -814,7 +822,7 @@ __device__ void ffn_fwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
         o[tt] = mfma_sp(a, *reinterpret_cast<const uint2*>(L.w2s + ((wave * 12 + tt) * 16 + col) * FS + 16 * q + 4 * kq), o[tt]);
     }
     SUB_MARK(0, 5);
-    tiles_out(L, o, Pj, c0, nr);
+    tiles_out<false>(L, o, Pj, c0, nr);
     SUB_MARK(0, 6);
   }
 }
@@ -842,7 +850,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
       STEP_MARK(0, l, 1);
       const LrceDecLayerW& Wp = p.layer[l - 1];
       for (int b = r; b < p.B; b += R)
-        slice_reduce(p.ws + 2 * WS_SLAB, b, h, Wp.b2, p.drop_p, layer_seed(p, l - 1) + 5 + roff,
+        slice_reduce<false>(p.ws + 2 * WS_SLAB, b, h, Wp.b2, p.drop_p, layer_seed(p, l - 1) + 5 + roff,
                      mb_of(p, set, K_X2, l - 1) + (long long)b * E, mb_of(p, set, K_X3P, l - 1) + (long long)b * E,
                      fwd_field(p, F_X3P, l - 1, p.step).row(b), RD, p, 0x100 + l);
     }
@@ -904,7 +912,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
   const int Ll = L_ - 1;
   STEP_MARK(0, L_, 1);
   for (int b = r; b < p.B; b += R)
-    slice_reduce(p.ws + 2 * WS_SLAB, b, h, p.layer[Ll].b2, p.drop_p, layer_seed(p, Ll) + 5 + roff,
+    slice_reduce<false>(p.ws + 2 * WS_SLAB, b, h, p.layer[Ll].b2, p.drop_p, layer_seed(p, Ll) + 5 + roff,
                  mb_of(p, set, K_X2, Ll) + (long long)b * E, mb_of(p, set, K_X3P, Ll) + (long long)b * E,
                  fwd_field(p, F_X3P, Ll, p.step).row(b), RD, p, 0x700);
   if (h == 0) {
@@ -959,7 +967,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
 // ---------------------------------------------------------------- backward: FFN slice j, all rows
 __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64_t seed4, uint64_t seed5, const float* mbd3,
                               float* dres, unsigned long long* trace) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
+  const int t = opaque_tid(), lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
   const int ct = wave & 1, kh = wave >> 1;
   const LrceDecLayerW& W = p.layer[l];
   const f16* w1 = reinterpret_cast<const f16*>(W.w1);
@@ -990,7 +998,7 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
     const int nr = min(RCH, p.B - c0);
     lds_barrier();
     if (c0 > 0) prefetch(c0, nr);
-    rows_to_lds(mbd3, c0, nr, L, p, 0x900 + l);
+    rows_to_lds<true>(mbd3, c0, nr, L, p, 0x900 + l);
     lds_barrier();
     SUB_MARK(1, 3);
     // LayerNorm-3 backward per row (the wave's four rows together), then the out-dropout backward -> df
@@ -1115,7 +1123,7 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
       for (int tt = 0; tt < 12; ++tt) o[tt][r] *= u;
     }
     SUB_MARK(1, 5);
-    tiles_out(L, o, Qj, c0, nr);
+    tiles_out<true>(L, o, Qj, c0, nr);
     SUB_MARK(1, 6);
   }
 }
@@ -1131,7 +1139,7 @@ struct CaBwdPre {
   float mu, rs, qd, od, lse;
 };
 __device__ void ca_bwd_prefetch(const LrceDecStep& p, int l, int b, int h, CaL& L, CaBwdPre& q) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = opaque_tid(), lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
   const KvP kv = kv_of(p, l);
   const int Lk = kv.lk1 + kv.lk2;
@@ -1160,7 +1168,7 @@ __device__ void ca_bwd_prefetch(const LrceDecStep& p, int l, int b, int h, CaL& 
 
 __device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, CaL& L, uint64_t seed2, uint64_t seed3,
                            const CaBwdPre& q, RedL& RD, const float* mbd2, float* mbd1) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = opaque_tid(), lane = t & 63, wave = t >> 6;
   const KvP kv = kv_of(p, l);
   const int Lk = kv.lk1 + kv.lk2;
   float4 dy = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1322,7 +1330,7 @@ __device__ void ca_bwd_row(const LrceDecStep& p, int l, int b, int h, CaL& L, ui
 // d x3 of layer l-1 (handed off), or (l = 0) the step input's gradient dx0 + dt.
 __device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, SaL& L, uint64_t seed0, uint64_t seed1, RedL& RD,
                            const float* mbd1, float* mbd3, const float* mbdt) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = opaque_tid(), lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
   float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
   if (t < E / 4) {
@@ -1380,7 +1388,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
   __shared__ __attribute__((aligned(16))) StepLds U;
   __shared__ __attribute__((aligned(16))) RedL RD;
   __shared__ unsigned ok_word;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = opaque_tid(), lane = t & 63, wave = t >> 6;
   const int G = gridDim.x, R = G / H;
   const int h = blockIdx.x % H, r = blockIdx.x / H;
   const uint64_t roff = rng_off_now(rng_off);
@@ -1432,7 +1440,7 @@ __global__ void __launch_bounds__(NT, 1) dec_step_bwd_kernel(LrceDecStep p, cons
     STEP_MARK(1, l, 2);
     STEP_MARK(1, l, 3);
     for (int b = r; b < p.B; b += R)
-      slice_reduce(p.ws + 2 * WS_SLAB, b, h, nullptr, 0.f, 0, mb_of(p, set, K_DRES, l) + (long long)b * E,
+      slice_reduce<true>(p.ws + 2 * WS_SLAB, b, h, nullptr, 0.f, 0, mb_of(p, set, K_DRES, l) + (long long)b * E,
                    mb_of(p, set, K_DLN2, l) + (long long)b * E, bwd_field(p, G_DLN2, l, p.step).row(b), RD, p, 0xA00 + l);
     // the row's saved operands and K / V images after the reduce (held across it they cost spills)
     CaBwdPre pre;
