@@ -972,18 +972,49 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
   const LrceDecLayerW& W = p.layer[l];
   const f16* w1 = reinterpret_cast<const f16*>(W.w1);
   const f16* w2 = reinterpret_cast<const f16*>(W.w2);
-  ffn_slices_dma(w1, w2, j, L, wave, lane);
-  const Ar dln3 = bwd_field(p, G_DLN3, l, p.step), df = bwd_field(p, G_DF, l, p.step), dgp = bwd_field(p, G_DGP, l, p.step);
+  const Ar df = bwd_field(p, G_DF, l, p.step), dgp = bwd_field(p, G_DGP, l, p.step);
   const Ar x3p = fwd_field(p, F_X3P, l, p.step), m3 = fwd_field(p, F_M3, l, p.step), r3 = fwd_field(p, F_R3, l, p.step);
   const Ar pre = fwd_field(p, F_PRE, l, p.step);
   float* Qj = p.ws + 2 * WS_SLAB + (long long)j * MAXB * E;
   const bool owner = j == 0;
-  // what a chunk of rows needs that this launch does not write (the forward's x3p / stats / pre-
-  // activations): for the first chunk issued before the wait for the rows' gradients
-  auto prefetch = [&](int c0, int nr) {
-    for (int i = t; i < nr * FS; i += NT) L.preb[i / FS][i % FS] = pre.row(c0 + i / FS)[j * FS + i % FS];
+  // the saved pre-activations of a chunk's rows (written by the forward launch): loaded into registers
+  // BEFORE the weight-slice DMA (vmcnt is in order: a load issued after the DMA could only be consumed
+  // once the whole 96 KB had landed), parked in LDS once the chunk's rows arrived
+  constexpr int PPT = RCH * FS / NT;   // 2 per thread
+  float pv[PPT];
+  auto pre_load = [&](int c0, int nr) {
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const int i = t + q * NT;
+      pv[q] = i < nr * FS ? pre.row(c0 + i / FS)[j * FS + i % FS] : 0.f;
+    }
   };
-  prefetch(0, min(RCH, p.B));
+  auto pre_park = [&]() {
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const int i = t + q * NT;
+      L.preb[i / FS][i % FS] = pv[q];
+    }
+  };
+  // likewise the LayerNorm-3 operands of the wave's four rows (x3p, mean, rstd, gamma)
+  float4 xq[4][3], gq[3];
+  float muq[4], rsq[4];
+  auto ln_load = [&](int c0, int nr) {
+    const int lane_ = t & 63;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) gq[i] = *reinterpret_cast<const float4*>(W.g3 + 12 * lane_ + 4 * i);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int b = c0 + min(wave + 4 * q, nr - 1);
+      muq[q] = m3.row(b)[0];
+      rsq[q] = r3.row(b)[0];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) xq[q][i] = *reinterpret_cast<const float4*>(x3p.row(b) + 12 * lane_ + 4 * i);
+    }
+  };
+  pre_load(0, min(RCH, p.B));
+  ln_load(0, min(RCH, p.B));
+  ffn_slices_dma(w1, w2, j, L, wave, lane);
   SUB_MARK(1, 0);
   SUB_MARK(1, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slices and prefetches have landed (read after the next barrier)
@@ -997,28 +1028,30 @@ __device__ void ffn_bwd_slice(const LrceDecStep& p, int l, int j, FfL& L, uint64
   for (int c0 = 0; c0 < p.B; c0 += RCH) {
     const int nr = min(RCH, p.B - c0);
     lds_barrier();
-    if (c0 > 0) prefetch(c0, nr);
+    if (c0 > 0) {
+      pre_load(c0, nr);
+      ln_load(c0, nr);
+    }
     rows_to_lds<true>(mbd3, c0, nr, L, p, 0x900 + l);
+    pre_park();
     lds_barrier();
     SUB_MARK(1, 3);
     // LayerNorm-3 backward per row (the wave's four rows together), then the out-dropout backward -> df
     // in the image
     {
       float4 g[4][3], xh[4][3];
-      float s1[4], s2[4], rsq[4];
+      float s1[4], s2[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int rr = wave + 4 * q, b = c0 + min(rr, nr - 1);
-        const float mu = m3.row(b)[0], rs = r3.row(b)[0];
-        rsq[q] = rs;
+        const int rr = wave + 4 * q;
+        const float mu = muq[q], rs = rsq[q];
         const float* xp = xat(L, rr, 12 * lane);
         s1[q] = s2[q] = 0.f;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-          const int k = 12 * lane + 4 * i;
           const float4 dy = *reinterpret_cast<const float4*>(xp + 4 * i);   // zero for rows >= nr
-          const float4 gm = *reinterpret_cast<const float4*>(W.g3 + k);
-          const float4 x = *reinterpret_cast<const float4*>(x3p.row(b) + k);
+          const float4 gm = gq[i];
+          const float4 x = xq[q][i];
           g[q][i] = make_float4(dy.x * gm.x, dy.y * gm.y, dy.z * gm.z, dy.w * gm.w);
           xh[q][i] = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
           s1[q] += (g[q][i].x + g[q][i].y) + (g[q][i].z + g[q][i].w);
