@@ -430,7 +430,7 @@ __device__ void sa_fwd_row(const LrceDecStep& p, int l, int b, int h, const f16*
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
   {
-    uint4 wr[NRI];
+    uint4 wr[NRI];   // W_v[h] rows, loaded at use: held across the row's waits they cost spills
     rows_load(wv, h * D + wave * WROWS, lane, wr);
     rows_gemv(wr, L.x0, L.pp[wave], L.v + wave * WROWS, lane);
   }
@@ -486,9 +486,9 @@ __device__ void ca_fwd_row(const LrceDecStep& p, int l, int b, int h, const f16*
   const int Lk = kv.lk1 + kv.lk2;
   float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
   if (t < E / 4) {
-    xr = ld4_wait(mbx1 + (long long)b * E, 4 * t, p, 0x300 + l);
     gg = *reinterpret_cast<const float4*>(W.g1 + 4 * t);
     be = *reinterpret_cast<const float4*>(W.be1 + 4 * t);
+    xr = ld4_wait(mbx1 + (long long)b * E, 4 * t, p, 0x300 + l);
   }
   const float s1l = row_sum_local(xr, t);
   const bool live = t < Lk;
@@ -862,9 +862,9 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
         const LrceDecLayerW& Wp = p.layer[l - 1];
         float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
         if (t < E / 4) {
-          xr = ld4_wait(mb_of(p, set, K_X3P, l - 1) + (long long)b * E, 4 * t, p, 0x600 + l);
           gg = *reinterpret_cast<const float4*>(Wp.g3 + 4 * t);
           be = *reinterpret_cast<const float4*>(Wp.be3 + 4 * t);
+          xr = ld4_wait(mb_of(p, set, K_X3P, l - 1) + (long long)b * E, 4 * t, p, 0x600 + l);
         }
         if (first) STEP_MARK(0, l, 2);
         float mu, rs;
@@ -921,9 +921,9 @@ __global__ void __launch_bounds__(NT, 1) dec_step_fwd_kernel(LrceDecStep p, cons
     for (int b = r; b < p.B; b += R) {
       float4 xr = make_float4(0.f, 0.f, 0.f, 0.f), gg = xr, be = xr;
       if (t < E / 4) {
-        xr = ld4_wait(mb_of(p, set, K_X3P, Ll) + (long long)b * E, 4 * t, p, 0x800);
         gg = *reinterpret_cast<const float4*>(p.layer[Ll].g3 + 4 * t);
         be = *reinterpret_cast<const float4*>(p.layer[Ll].be3 + 4 * t);
+        xr = ld4_wait(mb_of(p, set, K_X3P, Ll) + (long long)b * E, 4 * t, p, 0x800);
       }
       float mu, rs;
       ln_row_fwd(xr, row_sum_local(xr, t), gg, be, p.eps, S.x0, S.red2, t, lane, wave, mu, rs);
@@ -1366,12 +1366,12 @@ __device__ void sa_bwd_row(const LrceDecStep& p, int l, int b, int h, SaL& L, ui
   const int t = opaque_tid(), lane = t & 63, wave = t >> 6;
   const LrceDecLayerW& W = p.layer[l];
   float4 dy = make_float4(0.f, 0.f, 0.f, 0.f), xr = dy, gm = dy;
+  const float mu = fwd_field(p, F_M1, l, p.step).row(b)[0], rs = fwd_field(p, F_R1, l, p.step).row(b)[0];
   if (t < E / 4) {
-    dy = ld4_wait(mbd1 + (long long)b * E, 4 * t, p, 0xD00 + l);
     xr = *reinterpret_cast<const float4*>(fwd_field(p, F_X1P, l, p.step).row(b) + 4 * t);
     gm = *reinterpret_cast<const float4*>(W.g1 + 4 * t);
+    dy = ld4_wait(mbd1 + (long long)b * E, 4 * t, p, 0xD00 + l);
   }
-  const float mu = fwd_field(p, F_M1, l, p.step).row(b)[0], rs = fwd_field(p, F_R1, l, p.step).row(b)[0];
   LnBwdLocal lnl = ln_row_bwd_local(dy, xr, gm, mu, rs, t);
   const float4 dx = ln_row_bwd(lnl, rs, L.red2, lane, wave);
   if (t < E / 4) {
