@@ -117,3 +117,34 @@ def test_gradient_freshness_claims():
     flat.grads_zeroed()
     assert flat.claim_fresh([lin.weight])
     assert not flat.claim_fresh(ps)          # the bias is fresh but the weight was claimed: accumulate
+
+
+def test_decoder_kv_layer_slots():
+    """The persistent decoder projects all 12 layers' memory K/V with ONE batched GEMM when the layers'
+    W_kv (and biases) sit at one stride (fusionv3._layer_slots): ascending -> slot l, descending (the
+    flat store's reverse forward order) -> slot n-1-l with the lowest-address layer first; anything
+    else -> per-layer launches.  Checked on the real flat layout of the model and on synthetic cases."""
+    from lrce.models import fusionv3 as F
+    from lrce.flat import FlatParams
+    from lrce.models.e2e import E2EOpenEnded
+
+    class T:
+        def __init__(self, p):
+            self.p = p
+
+        def data_ptr(self):
+            return self.p
+    assert F._layer_slots([T(1000 + 64 * i) for i in range(4)], 2) == ([0, 1, 2, 3], 0, 1, 32)
+    assert F._layer_slots([T(1000 - 64 * i) for i in range(4)], 2) == ([3, 2, 1, 0], 3, -1, 32)
+    assert F._layer_slots([T(0), T(64), T(192)], 2) is None
+    assert F._layer_slots([T(0)], 2) is None
+    torch.manual_seed(0)
+    m = E2EOpenEnded(768, 10, 0.0, (7, 7), 1024, 5, [3], 32, swin_ckpt=None, bert_dir=None)
+    flat = FlatParams(m, "cpu", order=m.lrce_param_order())   # the layout prepare() builds on the GPU
+    layers = m.fusion_model.fusion_transformer.transformer.layers
+    w = [flat.w16(l.multihead_attn.in_proj_weight)[768:] for l in layers]
+    b = [l.multihead_attn.in_proj_bias[768:] for l in layers]
+    sw, sb = F._layer_slots(w, 2), F._layer_slots(b, 4)
+    assert sw is not None and sb is not None and sw[:3] == sb[:3]
+    slot, first = sw[0], sw[1]
+    assert sorted(slot) == list(range(12)) and slot[first] == 0

@@ -843,6 +843,17 @@ def patch_im2col(clips, patches, *, layout="BSTCHW", normalize=True):
          stream_of(patches))
 
 
+def slab_sum(items):
+    """dst (=|+=) the sum of `split` consecutive slabs of n f32 each, in slab order, for every item
+    (slabs, dst, n, split, accumulate) — one launch (lrce_slab_sum_grouped)."""
+    if not items:
+        return
+    arr = (N.SlabSum * len(items))()
+    for e, (slabs, dst, n, split, acc) in zip(arr, items):
+        e.slabs, e.dst, e.n, e.split, e.accumulate = ptr(slabs), ptr(dst), int(n), int(split), int(acc)
+    call("lrce_slab_sum_grouped", arr, len(items), stream_of(items[0][1]))
+
+
 def cast_bf16(x, y):
     call("lrce_cast_bf16", ptr(x), ptr(y), x.numel(), stream_of(y))
 

@@ -553,6 +553,24 @@ class _StepArena:
         return t.view(self.S * self.Bq, t.shape[-1])
 
 
+def _layer_slots(ts, esize):
+    """Buffer slot of each layer for the per-layer memory-side operands and a uniform weight stride:
+    (slot[l], first, step, stride) where the layers' tensors ts[l] sit at one element stride in memory
+    (ascending or descending with the layer index — the flat store lays every layer out alike, in
+    reverse forward order) so ONE batched GEMM covers all layers: batch i = the layer at the i-th lowest
+    address, written to slot i.  None when they do not (then one launch per layer)."""
+    n = len(ts)
+    if n < 2:
+        return None
+    ptrs = [t.data_ptr() for t in ts]
+    d = ptrs[1] - ptrs[0]
+    if d == 0 or d % esize or any(ptrs[i + 1] - ptrs[i] != d for i in range(n - 1)):
+        return None
+    if d > 0:
+        return list(range(n)), 0, 1, d // esize
+    return list(range(n - 1, -1, -1)), n - 1, -1, -d // esize
+
+
 def _step_desc(ft, flat, layers, B, S, nmc, Lt, p, seed):
     """The LrceDecStep of one decoder call (per-step fields are filled by the caller)."""
     d = N.DecStep()
@@ -592,6 +610,13 @@ class _StepDecoderFn(torch.autograd.Function):
         t16 = t16.view(Bq * Lt, E) if Lt else None
         main = torch.cuda.current_stream(dev)
         ks = aux_stream(dev, "decoder_kv") if _KV_ASYNC else main
+        # K|V of layer l in slot slot[l] (address order of the layers' weights), so that one batched GEMM
+        # per segment projects all 12 layers (24 launches of 8-22 us on the critical path -> 2)
+        wkv = [flat.w16(lay.multihead_attn.in_proj_weight)[E:] for lay in layers]
+        bkv = [lay.multihead_attn.in_proj_bias[E:] for lay in layers]
+        lw, lb = _layer_slots(wkv, 2), _layer_slots(bkv, 4)
+        batched = lw is not None and lb is not None and lw[:3] == lb[:3]
+        slot = lw[0] if batched else list(range(nL))
         kvv = torch.empty(nL, rows_v, 2 * E, dtype=torch.bfloat16, device=dev)
         kvt = torch.empty(nL, Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None
         if ks is not main:
@@ -600,20 +625,26 @@ class _StepDecoderFn(torch.autograd.Function):
                 if x is not None:
                     x.record_stream(ks)
         with torch.cuda.stream(ks):
-            for l, lay in enumerate(layers):
-                ca = lay.multihead_attn
-                w = flat.w16(ca.in_proj_weight)[E:]
-                K.linear(v16, w, ca.in_proj_bias[E:], out=kvv[l])
-                if Lt:
-                    K.linear(t16, w, ca.in_proj_bias[E:], out=kvt[l])
+            if batched:
+                f0 = lw[1]   # the layer at the lowest address (slot 0)
+                for x, out, rows in ((v16, kvv, rows_v), (t16, kvt, Bq * Lt)):
+                    if x is not None and rows:
+                        K.gemm(x, wkv[f0], out, rows, 2 * E, E, flags=N.EPI_BIAS, bias=bkv[f0], batch=nL,
+                               stride_b=lw[3], stride_c=rows * 2 * E, stride_bias=lb[3])
+            else:
+                for l in range(nL):
+                    K.linear(v16, wkv[l], bkv[l], out=kvv[l])
+                    if Lt:
+                        K.linear(t16, wkv[l], bkv[l], out=kvt[l])
         A = _StepArena(0, nL, S, Bq, dev)
         A.f("x0", 0)[0].copy_(ft.summarization_token.detach().reshape(1, E).expand(Bq, E))
         if ks is not main:
             main.wait_stream(ks)
         ws, ctrs, status = K.dec_step_workspace(dev)
         d = _step_desc(ft, flat, layers, Bq, S, nmc, Lt, p, seed)
-        d.kv_video, d.kv_video_lstride = N.ptr(kvv), rows_v * 2 * E
-        d.kv_text, d.kv_text_lstride = N.ptr(kvt), Bq * Lt * 2 * E
+        sgn = (slot[1] - slot[0]) if nL > 1 else 1
+        d.kv_video, d.kv_video_lstride = N.ptr(kvv[slot[0]]), sgn * rows_v * 2 * E
+        d.kv_text, d.kv_text_lstride = (N.ptr(kvt[slot[0]]) if Lt else None), sgn * Bq * Lt * 2 * E
         d.acts, d.ws, d.counters, d.status = N.ptr(A.buf), N.ptr(ws), N.ptr(ctrs), N.ptr(status)
         out = torch.empty(Bq, E, device=dev)
         d.s_out = N.ptr(out)
@@ -621,12 +652,14 @@ class _StepDecoderFn(torch.autograd.Function):
             d.step = i
             K.dec_step_fwd(d, out)
         ctx.save = (kvv, kvt, v16, t16, A, d)
+        ctx.kv_batch = (slot, wkv, lw if batched else None)
         ctx.ft, ctx.flat, ctx.dims = ft, flat, (B, S, nmc, Bq, Lt)
         return out
 
     @staticmethod
     def backward(ctx, ds):
         kvv, kvt, v16, t16, A, d = ctx.save
+        slot, wkv, lw = ctx.kv_batch
         ft, flat = ctx.ft, ctx.flat
         B, S, nmc, Bq, Lt = ctx.dims
         layers = ft.transformer.layers
@@ -642,12 +675,13 @@ class _StepDecoderFn(torch.autograd.Function):
             torch.zeros(nL, rows_v, 2 * E, device=dev)
         dkvt = torch.empty(nL, Bq * Lt, 2 * E, device=dev) if Lt else None
         d.grads = N.ptr(G.buf)
+        sgn = (slot[1] - slot[0]) if nL > 1 else 1   # the slots of the forward's K|V (address order)
         if nmc == 1:
-            d.dkv_video16, d.dkv_video32 = N.ptr(dkvv), None
+            d.dkv_video16, d.dkv_video32 = N.ptr(dkvv[slot[0]]), None
         else:
-            d.dkv_video16, d.dkv_video32 = None, N.ptr(dkvv)
-        d.dkv_video_lstride = rows_v * 2 * E
-        d.dkv_text, d.dkv_text_lstride = N.ptr(dkvt), Bq * Lt * 2 * E
+            d.dkv_video16, d.dkv_video32 = None, N.ptr(dkvv[slot[0]])
+        d.dkv_video_lstride = sgn * rows_v * 2 * E
+        d.dkv_text, d.dkv_text_lstride = (N.ptr(dkvt[slot[0]]) if Lt else None), sgn * Bq * Lt * 2 * E
         cur = ds.contiguous()
         bufs = [torch.empty(Bq, E, device=dev), torch.empty(Bq, E, device=dev)]
         for k, i in enumerate(reversed(range(S))):
@@ -665,15 +699,28 @@ class _StepDecoderFn(torch.autograd.Function):
         dk16 = dkvv if nmc == 1 else torch.empty(nL, rows_v, 2 * E, dtype=torch.bfloat16, device=dev)
         dt16 = torch.empty(nL, Bq * Lt, 2 * E, dtype=torch.bfloat16, device=dev) if Lt else None
         with torch.cuda.stream(ks):
-            for l, lay in enumerate(layers):
-                if nmc != 1:
-                    K.cast_bf16(dkvv[l], dk16[l])
-                if Lt:
-                    K.cast_bf16(dkvt[l], dt16[l])
-                w = flat.w16(lay.multihead_attn.in_proj_weight)[E:]
-                K.linear_dx(dk16[l], w, out=dv, accumulate=l > 0)
-                if Lt:
-                    K.linear_dx(dt16[l], w, out=dtt, accumulate=l > 0)
+            if nmc != 1:
+                K.cast_bf16(dkvv, dk16)
+            if Lt:
+                K.cast_bf16(dkvt, dt16)
+            if lw is not None:
+                # every layer's dK|dV W_kv as one batched GEMM into per-slot f32 slabs, summed in slot
+                # order by one launch (24 launches -> 3)
+                f0 = lw[1]
+                sums = []
+                for g16, out, rows in ((dk16, dv, rows_v), (dt16, dtt, Bq * Lt)):
+                    if g16 is None or not rows:
+                        continue
+                    slabs = torch.empty(nL, rows, E, device=dev)
+                    K.gemm(g16, wkv[f0], slabs, rows, E, 2 * E, a_kmajor=True, b_kmajor=False, lda=2 * E, ldb=E,
+                           flags=N.EPI_OUT_F32, batch=nL, stride_a=rows * 2 * E, stride_b=lw[3], stride_c=rows * E)
+                    sums.append((slabs, out, rows * E, nL, 0))
+                K.slab_sum(sums)
+            else:
+                for l in range(nL):
+                    K.linear_dx(dk16[slot[l]], wkv[l], out=dv, accumulate=l > 0)
+                    if Lt:
+                        K.linear_dx(dt16[slot[l]], wkv[l], out=dtt, accumulate=l > 0)
         if ks is not main:
             main.wait_stream(ks)
             for x in (dv, dtt, dk16, dt16, dkvv, dkvt, kvv, kvt):
@@ -699,9 +746,9 @@ class _StepDecoderFn(torch.autograd.Function):
                 _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, G.rows("dq", l), A.rows("x1", l), rows=(0, E))
                 _wgrad(flat, sa.out_proj.weight, sa.out_proj.bias, G.rows("dsao", l), A.rows("sad", l))
                 _wgrad(flat, sa.in_proj_weight, sa.in_proj_bias, G.rows("dsav", l), A.rows("x0", l), rows=(2 * E, 3 * E))
-                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16[l], v16, rows=(E, 3 * E))
+                _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dk16[slot[l]], v16, rows=(E, 3 * E))
                 if Lt:
-                    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[l], t16, rows=(E, 3 * E))
+                    _wgrad(flat, ca.in_proj_weight, ca.in_proj_bias, dt16[slot[l]], t16, rows=(E, 3 * E))
             fl = ft.fusion_layer_norm
             gw, gb = _g(flat, fl.weight), _g(flat, fl.bias)
             if gw is not None or gb is not None:
