@@ -170,6 +170,30 @@ def test_fused_decoder_blocks_match_unfused(task, L, ncls, B, drop, mode, monkey
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]
 
 
+def test_step_decoder_across_row_counts(monkeypatch):
+    """The persistent decoder's hand-off workspace is shared by every call on the device and re-armed
+    launch by launch (the row mailboxes: the rows the previous launch wrote).  Calls with different row
+    counts in sequence — 12, 5 (MC, one video), 45 (MC, nine videos: several rows per workgroup), 12 —
+    must each match the unfused launches (eval mode)."""
+    from lrce.models.fusionv3 import LRCEOpenEnded, LRCEMultipleChoice
+    from lrce import kernels as K
+    torch.manual_seed(4)
+    oe = LRCEOpenEnded(768, 1000, 0.0, (7, 7), 1024, 5, [3], 32).cuda().eval()
+    mc = LRCEMultipleChoice(768, 1, 0.0, (7, 7), 1024, 5, [3], 40).cuda().eval()
+    cases = [(oe, 12), (mc, 1), (mc, 9), (oe, 12), (mc, 1)]
+    for m, B in cases:
+        vf = torch.randn(B, 3, 3, 49, 1024, device="cuda")
+        tf = torch.randn(B, 5, 40, 768, device="cuda") if m is mc else torch.randn(B, 32, 768, device="cuda")
+        ys = []
+        for fused in ("0", "step"):
+            monkeypatch.setenv("LRCE_DEC_FUSED", fused)
+            with torch.no_grad():
+                ys.append(m(vf, tf, None).float())
+            torch.cuda.synchronize()
+            assert K.dec_step_status("cuda") == 0
+        assert rel(ys[1], ys[0]) < 1e-4, (B, rel(ys[1], ys[0]))
+
+
 @pytest.mark.parametrize("task", ["oe", "mc"])
 def test_decoder_kv_stream_is_bit_identical(task, monkeypatch):
     """The memory-side K/V projections and their input-gradient GEMMs on the "decoder_kv" stream

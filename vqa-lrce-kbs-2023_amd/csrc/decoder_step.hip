@@ -59,8 +59,9 @@ namespace {
 constexpr int FF = 3072, FS = 32, NF = FF / FS, RMAX = 10, MAXB = LRCE_DEC_MAX_ROWS, RCH = 16;
 constexpr int XP = 100, XROW = 8 * XP + 4;   // padded LDS row of 768: 8 parts of 96 (+4), rows 804 apart (MFMA row reads)
 constexpr int NLMAX = LRCE_DEC_LAYERS;
-// counter block (uint32): the finishing count, the sticky abort word, the launch epoch
-constexpr int C_DONE = 0, C_ABORT = 1, C_EPOCH = 2, CTR_WORDS = 16;
+// counter block (uint32): the finishing count, the sticky abort word, the launch epoch, the row count of
+// the last launch (the rows of the mailbox set it used)
+constexpr int C_DONE = 0, C_ABORT = 1, C_EPOCH = 2, C_LASTB = 3, CTR_WORDS = 16;
 // workspace (f32, all sentinel between launches): two per-head partial slabs [MAXB][12][768], the FFN
 // slice partials [NF][MAXB][768], then the row mailboxes: 2 sets x NKIND kinds x NLMAX layers x
 // [MAXB][768].  Kinds, forward: x3p, x1p, x2p, x2 (LN2 output); backward: d x3 (the FFN block's
@@ -215,16 +216,18 @@ __device__ __forceinline__ int tid_() { return O ? opaque_tid() : (int)threadIdx
 __device__ __forceinline__ float* mb_of(const LrceDecStep& p, unsigned set, int kind, int l) {
   return p.ws + 2 * WS_SLAB + WS_P + ((long long)(set * NKIND + kind) * NLMAX + l) * MAXB * E;
 }
-// the launch's epoch (read by every workgroup before any finishes) and the re-arming of the other set
-// (used by the previous launch, which has ended): rows < B of every kind and layer, sentinel stores
+// the launch's epoch (read by every workgroup before any finishes) and the re-arming of the other set,
+// which the previous launch used (it has ended): the rows it wrote — its row count, which may differ
+// from this launch's — of every kind and layer, sentinel stores
 __device__ unsigned launch_begin(const LrceDecStep& p) {
   const unsigned ep = __hip_atomic_load(p.counters + C_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned pb = __hip_atomic_load(p.counters + C_LASTB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned other = (ep + 1) & 1u;
-  const long long per = (long long)p.B * (E / 4);   // float4 pieces of one (kind, layer)
-  const long long tot = (long long)NKIND * p.n_layers * per;
+  const long long per = (long long)(pb < (unsigned)MAXB ? pb : (unsigned)MAXB) * (E / 4);   // float4 pieces of one (kind, layer)
+  const long long tot = (long long)NKIND * NLMAX * per;
   for (long long i = (long long)blockIdx.x * NT + opaque_tid(); i < tot; i += (long long)gridDim.x * NT) {
     const long long kl = i / per, e = i % per;
-    st4_sc1(mb_of(p, other, (int)(kl / p.n_layers), (int)(kl % p.n_layers)), 4 * e, sent4());
+    st4_sc1(mb_of(p, other, (int)(kl / NLMAX), (int)(kl % NLMAX)), 4 * e, sent4());
   }
   return ep & 1u;
 }
@@ -239,6 +242,7 @@ __device__ void finish(const LrceDecStep& p, unsigned* last_word) {
   __syncthreads();
   if (!*last_word || opaque_tid() != 0) return;
   __hip_atomic_store(p.counters + C_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p.counters + C_LASTB, (unsigned)p.B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_add(p.counters + C_EPOCH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
