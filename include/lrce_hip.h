@@ -675,16 +675,23 @@ int lrce_set_rng_offset(const uint64_t* offset);
  * (decoupled weight decay, bias corrections bc1 = 1-beta1^t, bc2 = 1-beta2^t) on the gradient
  * grad_scale * g + reg * p / ||p|| (the L2-regulariser term), tensor_lr[t] per tensor; also writes
  * the bf16 shadow copy of p (p_bf16, optional) used by the next forward.  An element whose gradient
- * term is not finite keeps its parameter and moments (the reference's GradScaler skips the whole
- * step on an overflow; per element here, so early per-group updates need no global flag). */
+ * term is not finite keeps its parameter and moments; a whole chunk range keeps them when a found-inf
+ * flag of skip_slots is set (the reference's GradScaler skips the step on an overflow; here the group
+ * whose gradients come from the overflowed fp16 operands, so early per-group updates of the other
+ * groups need not wait for BERT's backward). */
 int lrce_l2norm_multi(const float* p, const int32_t* chunk_tensor, int n_chunks, float* sumsq, int n_tensors,
                       const int32_t* tensor_chunk_off, float* chunk_sq, void* stream);
 int lrce_adamw_step(float* p, const float* g, float* m, float* v, const int32_t* chunk_tensor, const float* tensor_lr,
                     const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
                     float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
                     float* sumsq_next, uint16_t* p_f16, int64_t f16_lo, int64_t f16_hi, const uint16_t* g_bf16,
-                    const int32_t* tensor_chunk_off, float* chunk_sq, int n_tensors, void* stream);
-/* step: optional device step count t (bc1/bc2 then computed from it: graph-safe).  sumsq_next:
+                    const int32_t* tensor_chunk_off, float* chunk_sq, int n_tensors, const float* skip_slots,
+                    int n_skip_slots, int64_t skip_c0, int64_t skip_c1, void* stream);
+/* skip_slots (optional): n_skip_slots (<= 64) gradient-scale slots [S, 1/S, amax, found-inf] of the
+ * delayed fp16 backward (lrce_layernorm_bwd_f16s); when any found-inf word is set, chunks [skip_c0,
+ * skip_c1) of this call (relative to p) keep their parameters and moments — the step GradScaler would
+ * skip, for the parameter group whose gradients those fp16 operands produce (their norms are still
+ * written).  step: optional device step count t (bc1/bc2 then computed from it: graph-safe).  sumsq_next:
  * optional zeroed buffer that receives ||p_t||^2 of the UPDATED parameters, i.e. the next step's
  * sumsq without a separate norm pass over the 1.25 GB master copy.  p_f16 (optional): an IEEE fp16
  * shadow of elements [f16_lo, f16_hi) (multiples of 1024; element i at p_f16[i - f16_lo]) — the

@@ -163,6 +163,52 @@ def test_early_group_updates_match_one_update():
     assert torch.equal(early, flat.f32)
 
 
+def test_fp16_overflow_skips_the_text_group_update():
+    """The delayed fp16 scales of BERT's backward (text.py) can overflow when a gradient grows by more
+    than 2^8 between steps; the fused LN backward then raises its slot's found-inf flag and FusedAdamW's
+    guard (model.overflow_guard) keeps the text group's parameters and moments for that step, as the
+    reference's GradScaler skips an overflowing step (agent_oe.py:40-42), while the decoder and Swin
+    groups update.  The overflow is forced by recording a tiny max in the slot of the first fp16 operand
+    the backward writes (the top layer's FFN output gradient), so its next scale is 2^100; the slots
+    below it see the non-finite gradient as a non-finite max and back off.  The step after it rescales
+    and updates the text group again."""
+    from lrce.optim import FusedAdamW
+    b = [t.cuda() for t in _batch("oe", 32)]
+    model = _model("oe", 50, 32).cuda().train()
+    opt = FusedAdamW(model, [model.parameters()], lr=1e-4, reg_strength=0.001)
+    opt.enable_early_updates(model.optimizer_groups())
+    flat = opt.flat
+    (c0, c1), slots = opt._guard
+    text = slice(c0 * 1024, c1 * 1024)
+
+    def step():
+        opt.zero_grad()
+        loss = F.cross_entropy(model(*b[:4]).float(), b[4])
+        loss.backward()
+        opt.step()
+        torch.cuda.synchronize()
+        return loss.item()
+
+    step()
+    step()                                                   # a delayed-scale step
+    assert float(slots[..., 3].abs().sum()) == 0.0
+    slots.view(torch.int32)[-1, 0, 2] = 0x01800000           # recorded max 2^-124: S = 2^(7+124) -> 2^100 cap
+    before = [t.clone() for t in (flat.f32, opt.exp_avg, opt.exp_avg_sq)]
+    loss = step()
+    assert loss == loss
+    assert float(slots[..., 3].abs().sum()) != 0.0          # the top layer's operands overflowed
+    for now, was in zip((flat.f32, opt.exp_avg, opt.exp_avg_sq), before):
+        assert torch.equal(now[text], was[text])
+    rest = torch.ones(flat.f32.numel(), dtype=torch.bool, device=flat.f32.device)
+    rest[text] = False
+    assert bool(torch.isfinite(flat.f32).all())
+    assert (flat.f32[rest] != before[0][rest]).float().mean().item() > 0.5
+    w = flat.f32[text].clone()
+    step()
+    assert float(slots[..., 3].abs().sum()) == 0.0
+    assert bool(torch.isfinite(flat.f32).all()) and (flat.f32[text] != w).float().mean().item() > 0.5
+
+
 def test_early_updates_do_not_race_the_backward():
     """The same training step run from identical weights and optimizer state — once with the
     in-backward group updates, once with one update after the backward — with every stochastic element

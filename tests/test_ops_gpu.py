@@ -250,6 +250,54 @@ def test_layernorm_bwd_f16s_matches_unfused(p):
     k.grad_scale_update(sc)                      # no recorded max: the scale stays
     torch.cuda.synchronize()
     assert float(sc[0]) == S2
+    assert float(sc[3]) == 0.0                   # nothing overflowed: no found-inf flag
+
+
+def test_found_inf_flag_skips_the_guarded_chunks():
+    """An fp16 operand that overflows under its delayed scale (lrce_layernorm_bwd_f16s with S far above
+    2^7 / max|dx|) raises the slot's found-inf word; lrce_adamw_step then leaves the guarded chunk range
+    (parameters, moments) as it was and updates the rest, still writing every chunk's norm;
+    lrce_grad_scale_update clears the flag and the next update runs in full (GradScaler's skipped step,
+    agent_oe.py:40-42, for the group those operands feed)."""
+    k = K()
+    R, C = 320, 768
+    x = torch.randn(R, C, device=dev)
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    _, mean, rstd = k.layernorm(x, g, b, 1e-12, out_f32=True)
+    dy = torch.randn(R, C, device=dev)
+    slots = torch.tensor([[2.0 ** 4, 2.0 ** -4, 0.0, 0.0], [2.0 ** 20, 2.0 ** -20, 0.0, 0.0]], device=dev)
+    out16 = torch.empty(R, C, device=dev, dtype=torch.float16)
+    dx = torch.empty(R, C, device=dev)
+    k.layernorm_bwd_f16s(dy, x, mean, rstd, g, dx, out16, slots[0], 0.0, 3)
+    torch.cuda.synchronize()
+    assert float(slots[0, 3]) == 0.0 and bool(torch.isfinite(out16).all())
+    k.layernorm_bwd_f16s(dy, x, mean, rstd, g, dx, out16, slots[1], 0.0, 3)   # |dx| 2^20 > 65504
+    torch.cuda.synchronize()
+    assert float(slots[1, 3]) != 0.0 and not bool(torch.isfinite(out16).all())
+    n = 4 * 1024
+    p = torch.randn(n, device=dev)
+    gr = torch.randn(n, device=dev)
+    m, v = torch.full((n,), 0.1, device=dev), torch.full((n,), 0.2, device=dev)
+    p0, m0, v0 = p.clone(), m.clone(), v.clone()
+    ct = torch.zeros(4, dtype=torch.int32, device=dev)
+    lrs, chunk_sq = torch.tensor([1e-3], device=dev), torch.zeros(4, device=dev)
+    sumsq_next = torch.zeros(1, device=dev)
+    k.adamw_step(p, gr, m, v, ct, lrs, None, None, 4, 0.9, 0.999, 1e-8, 0.01, 1.0, 0.0, 0.1, 0.001,
+                 sumsq_next=sumsq_next, chunk_sq=chunk_sq, n_tensors=0, skip=(slots, 1, 3))
+    torch.cuda.synchronize()
+    kept = slice(1024, 3 * 1024)
+    assert torch.equal(p[kept], p0[kept]) and torch.equal(m[kept], m0[kept]) and torch.equal(v[kept], v0[kept])
+    for c in (0, 3):
+        sl = slice(c * 1024, (c + 1) * 1024)
+        assert (p[sl] != p0[sl]).float().mean().item() > 0.99
+    assert torch.allclose(chunk_sq, (p.view(4, 1024) ** 2).sum(1), rtol=1e-5)
+    k.grad_scale_update(slots)
+    torch.cuda.synchronize()
+    assert float(slots[0, 3]) == 0.0 and float(slots[1, 3]) == 0.0
+    p1 = p.clone()
+    k.adamw_step(p, gr, m, v, ct, lrs, None, None, 4, 0.9, 0.999, 1e-8, 0.01, 1.0, 0.0, 0.1, 0.001, skip=(slots, 1, 3))
+    torch.cuda.synchronize()
+    assert (p[kept] != p1[kept]).float().mean().item() > 0.99
 
 
 @pytest.mark.parametrize("M,N,Kd", [(320, 768, 768), (320, 3072, 768), (2000, 768, 3072)])

@@ -201,13 +201,15 @@ __global__ void __launch_bounds__(256) grad_scale_kernel(const float* __restrict
 
 // Delayed per-tensor scales (lrce_layernorm_bwd_f16s): slot i's max |x| of the last step (word 2,
 // accumulated by the fused LN backward) becomes its scale S = 2^(7 - floor(log2 max)) and 1/S, and the
-// word is cleared for this step; a slot with no recorded max keeps its scale.  One thread per slot.
+// word is cleared for this step, as is the found-inf flag (word 3, read by the last step's optimizer
+// update); a slot with no recorded max keeps its scale.  One thread per slot.
 __global__ void grad_scale_update_kernel(float* __restrict__ scale, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float* sc = scale + 4 * i;
   unsigned* words = reinterpret_cast<unsigned*>(sc + 2);
   const unsigned bits = words[0];
+  words[1] = 0u;
   if (bits == 0u) return;
   const int e = (int)((bits >> 23) & 0xFF) - 127;
   float s = 1.f;

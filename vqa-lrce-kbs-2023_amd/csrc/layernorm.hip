@@ -147,9 +147,11 @@ __global__ void __launch_bounds__(256) ln_fwd(const TX* x, const int* in_map, in
 // Scaled fp16 copy of the LN input gradient (F16S: the BERT backward, text.py): dx16[r][c] =
 // fp16(keep ? dx * S / (1 - p) : 0) with S = f16s->scale[0] (a delayed per-tensor gradient scale,
 // lrce_grad_scale_update), the mask of lrce_dropout over the contiguous [rows][cols] tensor, and
-// max|dx| folded into f16s->scale word 2 for the next step's scale.
+// max|dx| folded into f16s->scale word 2 for the next step's scale.  A kept element whose scaled value
+// rounds past the fp16 range (|dx S / (1 - p)| >= 65520: an infinite operand for the GEMMs that follow)
+// sets word 3, the slot's found-inf flag (lrce_adamw_step's skip slots; lrce_grad_scale_update clears it).
 struct F16Scaled {
-  float* scale;          // [S, 1/S, amax bits (next step), -]
+  float* scale;          // [S, 1/S, amax bits (next step), found-inf]
   float p;
   uint64_t seed;
   const uint64_t* off;
@@ -228,6 +230,7 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
   float mcur = 0.f, scur = 0.f;
   bool pcur = false;
   float amax = 0.f;                                    // F16S: max |dx| of this wave's rows
+  bool ovf = false;                                    // F16S: a kept element overflowed fp16
   const float s16 = F16S ? fs.scale[0] / (fs.p > 0.f ? 1.0f - fs.p : 1.0f) : 0.f;
   const uint64_t dseed = F16S && fs.p > 0.f ? lrce_seed(fs.seed, fs.off) : 0ull;
   if (r0 < rows) fetch(r0, xcur, dcur, rcur, mcur, scur, pcur);
@@ -291,8 +294,13 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
           if (fs.p > 0.f) u = lrce_uniform4(dseed, ((unsigned long long)r * cols + 4 * c) >> 2);
           typedef __attribute__((ext_vector_type(4))) _Float16 h4;
           h4 hv;
-          hv[0] = (f16)(u.x >= fs.p ? out.x * s16 : 0.f); hv[1] = (f16)(u.y >= fs.p ? out.y * s16 : 0.f);
-          hv[2] = (f16)(u.z >= fs.p ? out.z * s16 : 0.f); hv[3] = (f16)(u.w >= fs.p ? out.w * s16 : 0.f);
+          const float o4[4] = {u.x >= fs.p ? out.x * s16 : 0.f, u.y >= fs.p ? out.y * s16 : 0.f,
+                               u.z >= fs.p ? out.z * s16 : 0.f, u.w >= fs.p ? out.w * s16 : 0.f};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            hv[e] = (f16)o4[e];
+            ovf |= !(fabsf(o4[e]) < 65520.f);   // rounds to fp16 inf (or is NaN)
+          }
           *reinterpret_cast<h4*>(dx16 + (long long)r * cols + 4 * c) = hv;
         } else if (dx16) {   // bf16 copy (optionally row-scaled / row-permuted) for the next GEMMs' A operand
           const float f = dsc ? dsc[r / dsc_rps] : 1.f;
@@ -318,6 +326,8 @@ __global__ void __launch_bounds__(256) ln_bwd(const TD* dy, const int* dy_map, c
     if (lane == 0 && amax != 0.f)
       __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(fs.scale + 2), __float_as_uint(amax), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+    if (__ballot(ovf) != 0ull && lane == 0)
+      __hip_atomic_store(reinterpret_cast<unsigned*>(fs.scale + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (!dw && !db) return;
   if (LPR == 32) {  // fold the two half-wave row slots onto lanes 0..31

@@ -85,9 +85,16 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
                                                     float gscale, float reg, float bc1, float bc2, const float* __restrict__ step_dev,
                                                     float* __restrict__ sumsq_next, bf16* __restrict__ ph, long long h_lo,
                                                     long long h_hi, const bf16* __restrict__ g16,
-                                                    float* __restrict__ chunk_sq) {
+                                                    float* __restrict__ chunk_sq, const float* __restrict__ skip_slots,
+                                                    int n_skip, long long skip_c0, long long skip_c1) {
   const int lane = threadIdx.x & 63;
   const int wave_id = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // found-inf: chunks [skip_c0, skip_c1) keep their parameters and moments when any of the n_skip
+  // gradient-scale slots [S, 1/S, amax, flag] raised its flag (an fp16 gradient operand overflowed,
+  // lrce_layernorm_bwd_f16s) — GradScaler's skipped step for the group those operands feed
+  bool found_inf = false;
+  if (skip_slots && wave_id * CPW < skip_c1 && (wave_id + 1) * CPW > skip_c0)
+    found_inf = __ballot(lane < n_skip && skip_slots[4 * lane + 3] != 0.f) != 0ull;
   if (step_dev) {
     const float t = *step_dev;
     bc1 = 1.0f - exp2f(t * __log2f(b1));
@@ -103,6 +110,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
     const float rc = (reg != 0.f && ss > 0.f) ? reg * rsqrtf(ss) : 0.f;
     const float step = lr / bc1, decay = 1.0f - lr * wd;
     const long long base = (long long)c * 1024 + lane * 4;
+    const bool skip = found_inf && c >= skip_c0 && c < skip_c1;
     float4 pp[4], gg[4], mm[4], vv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -129,7 +137,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
         // a non-finite gradient element (an fp16 gradient operand that overflowed) leaves its parameter
         // and moments as they are, instead of poisoning them for every later step; the reference's
         // GradScaler skips the whole step in that case (agent_oe.py:40-42)
-        const bool fin = __builtin_isfinite(gr);
+        const bool fin = __builtin_isfinite(gr) && !skip;
         const float mn = b1 * ma[j] + (1.0f - b1) * gr;
         const float vn = b2 * va[j] + (1.0f - b2) * gr * gr;
         const float np = pa[j] * decay - step * mn / (sqrtf(vn) * isb2 + eps);
@@ -176,8 +184,12 @@ extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, con
                                const float* sumsq, uint16_t* p_bf16, int n_chunks, float beta1, float beta2, float eps,
                                float weight_decay, float grad_scale, float reg, float bc1, float bc2, const float* step,
                                float* sumsq_next, uint16_t* p_f16, int64_t f16_lo, int64_t f16_hi, const uint16_t* g_bf16,
-                               const int32_t* tensor_chunk_off, float* chunk_sq, int n_tensors, void* stream) {
+                               const int32_t* tensor_chunk_off, float* chunk_sq, int n_tensors, const float* skip_slots,
+                               int n_skip_slots, int64_t skip_c0, int64_t skip_c1, void* stream) {
   if (tensor_chunk_off && !chunk_sq) return lrce_fail(LRCE_E_ARG, "adamw_step: tensor_chunk_off needs chunk_sq");
+  if (skip_slots && (n_skip_slots < 1 || n_skip_slots > 64 || skip_c0 < 0 || skip_c1 < skip_c0))
+    return lrce_fail(LRCE_E_ARG, "adamw_step: skip slots n=%d range [%lld, %lld)", n_skip_slots, (long long)skip_c0,
+                     (long long)skip_c1);
   if (!p || (!g && !g_bf16) || !m || !v || !chunk_tensor || !tensor_lr) return lrce_fail(LRCE_E_ARG, "adamw_step: null pointer");
   // the f16 range is relative to p (it may start before this call's first chunk: a sub-range update)
   if (p_f16 && (f16_lo % 1024 || f16_hi % 1024 || f16_hi < f16_lo))
@@ -194,7 +206,7 @@ extern "C" int lrce_adamw_step(float* p, const float* g, float* m, float* v, con
       kern<<<grid, 256, 0, s>>>(p, g, m, v, chunk_tensor, tensor_lr, sumsq, reinterpret_cast<bf16*>(p_bf16), n_chunks, beta1,
                                 beta2, eps, weight_decay, grad_scale, reg, bc1, bc2, step, sumsq_next,
                                 reinterpret_cast<bf16*>(p_f16), f16_lo, f16_hi, reinterpret_cast<const bf16*>(g_bf16),
-                                sumsq_next ? chunk_sq : nullptr);
+                                sumsq_next ? chunk_sq : nullptr, skip_slots, n_skip_slots, skip_c0, skip_c1);
     };
     launch(adamw_kernel<true, 1>);
   }

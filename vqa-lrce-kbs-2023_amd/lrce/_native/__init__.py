@@ -247,7 +247,7 @@ _SIGS = {
     "lrce_text_posembed_bwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "lrce_l2norm_multi": [_P, _P, _I, _P, _I, _P, _P, _P],
     "lrce_adamw_step": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _F, _F, _F, _P, _P, _P, _I64, _I64,
-                        _P, _P, _P, _I, _P],
+                        _P, _P, _P, _I, _P, _I, _I64, _I64, _P],
     "lrce_set_rng_offset": [_P],
     "lrce_version": [],
     "lrce_last_error": [],

@@ -438,7 +438,11 @@ class BertModel(nn.Module):
 
     def _grad_scales(self, dev):
         """The layers' gradient-scale slots [n_layers, 2, 4] f32 (S, 1/S, two arrival words zeroed once:
-        the lrce_grad_scale contract), allocated on first use and kept (graph replays reuse them)."""
+        the lrce_grad_scale contract; under delayed scales the last step's max and the found-inf flag),
+        allocated on first use and kept (graph replays and the optimizer's overflow guard reuse them)."""
+        dev = torch.device(dev)
+        if dev.type == "cuda" and dev.index is None:   # "cuda" and "cuda:0" name the same slots
+            dev = torch.device("cuda", torch.cuda.current_device())
         sc = getattr(self, "_lrce_grad_scales", None)
         if sc is None or sc.device != dev:
             sc = torch.zeros(len(self.encoder.layer), 2, 4, device=dev)

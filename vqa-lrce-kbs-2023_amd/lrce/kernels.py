@@ -977,14 +977,19 @@ def l2norm_multi(p, chunk_tensor, n_chunks, sumsq, n_tensors, tensor_chunk_off=N
 
 def adamw_step(p, g, m, v, chunk_tensor, tensor_lr, sumsq, p_bf16, n_chunks, beta1, beta2, eps, wd, grad_scale, reg,
                bc1, bc2, step=None, sumsq_next=None, p_f16=None, f16_range=(0, 0), g_bf16=None, tensor_chunk_off=None,
-               chunk_sq=None, n_tensors=None):
+               chunk_sq=None, n_tensors=None, skip=None):
     """step: optional f32 device scalar holding t (bias corrections computed on device: graph-safe).
     sumsq_next: optional [n_tensors] buffer receiving ||p_t||^2 of the updated parameters (zeroed first
-    only without chunk_sq / tensor_chunk_off: the per-chunk path stores every entry)."""
+    only without chunk_sq / tensor_chunk_off: the per-chunk path stores every entry).
+    skip: optional (slots, c0, c1) — f32 gradient-scale slots [..., 4] whose found-inf words, when any is
+    set, leave chunks [c0, c1) of this call unchanged (lrce_adamw_step)."""
+    if skip is not None:
+        _chk(skip[0], F32, "skip slots")
     call("lrce_adamw_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(chunk_tensor), ptr(tensor_lr), ptr(sumsq), ptr(p_bf16),
          n_chunks, beta1, beta2, eps, wd, grad_scale, reg, bc1, bc2, ptr(step), ptr(sumsq_next), ptr(p_f16),
          int(f16_range[0]), int(f16_range[1]), ptr(g_bf16), ptr(tensor_chunk_off), ptr(chunk_sq),
          (0 if tensor_chunk_off is None else tensor_chunk_off.numel() - 1) if n_tensors is None else n_tensors,
+         *((None, 0, 0, 0) if skip is None else (ptr(skip[0]), skip[0].numel() // 4, int(skip[1]), int(skip[2]))),
          stream_of(p))
 
 

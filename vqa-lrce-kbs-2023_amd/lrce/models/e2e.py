@@ -85,6 +85,15 @@ class E2EBase(nn.Module):
             groups[swin.layers[i].blocks[0]._lrce_group] = ps
         return groups
 
+    def overflow_guard(self, device):
+        """(parameters, scale slots) for FusedAdamW's found-inf guard: BERT's backward runs on fp16
+        operands with delayed per-tensor scales (text.py), and an operand that overflowed raises its
+        slot's flag; the text group (the parameters those operands' gradients reach) then keeps its
+        values for the step, as the reference's GradScaler skips an overflowing step (agent_oe.py:40-42)."""
+        pool = {id(p) for p in self.text_extractor.bert.pooler.parameters()}
+        text = [p for p in self.text_extractor.parameters() if id(p) not in pool]
+        return text, self.text_extractor.bert._grad_scales(torch.device(device))
+
     def extract_video_features(self, video_clips):
         return self.video_extractor(video_clips)
 

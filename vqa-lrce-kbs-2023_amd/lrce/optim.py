@@ -46,6 +46,13 @@ class FusedAdamW(torch.optim.Optimizer):
         self._begun = False     # this step's counters / norms are set up (_begin)
         self._done = []         # chunk ranges already updated this step
         self.early_updates = 0  # group updates issued from inside a backward (statistics)
+        # found-inf guard: the chunk range whose gradients come from delayed-scale fp16 operands and those
+        # operands' scale slots (model.overflow_guard(): BERT's); an overflow skips that range's update
+        guard = getattr(model, "overflow_guard", None)
+        self._guard = None
+        if guard is not None:
+            params, slots = guard(dev)
+            self._guard = (flat.chunk_range(params), slots)
 
     def enable_early_updates(self, groups):
         """groups: {name: parameters}.  When the backward reports a group final (flat.group_done,
@@ -84,12 +91,18 @@ class FusedAdamW(torch.optim.Optimizer):
         e0, e1 = c0 * 1024, c1 * 1024
         hyper = (b1, b2, self.defaults["eps"], self.defaults["weight_decay"], float(grad_scale), self.reg_strength,
                  1.0 - b1 ** t, 1.0 - b2 ** t)
+        skip = None
+        if self._guard is not None:
+            (s0, s1), slots = self._guard
+            if max(s0, c0) < min(s1, c1):
+                skip = (slots, max(s0, c0) - c0, min(s1, c1) - c0)
         if c1 > c0:
             K.adamw_step(flat.f32[e0:e1], flat.grad[e0:e1] if g16 is None else None, self.exp_avg[e0:e1],
                          self.exp_avg_sq[e0:e1], flat.chunk_tensor[c0:c1], self.tensor_lr, self.sumsq, flat.bf16[e0:e1],
                          c1 - c0, *hyper, step=self.step_t, sumsq_next=self.sumsq_next, p_f16=flat.f16,
                          f16_range=(flat.f16_lo - e0, flat.f16_hi - e0) if flat.f16 is not None else (0, 0),
-                         g_bf16=None if g16 is None else g16[e0:e1], chunk_sq=self.chunk_sq[c0:c1], n_tensors=0)
+                         g_bf16=None if g16 is None else g16[e0:e1], chunk_sq=self.chunk_sq[c0:c1], n_tensors=0,
+                         skip=skip)
         if last:   # no update: the fixed-order per-tensor sums over the whole chunk_sq
             K.adamw_step(flat.f32, flat.grad, self.exp_avg, self.exp_avg_sq, flat.chunk_tensor, self.tensor_lr,
                          self.sumsq, None, 0, *hyper, step=self.step_t, sumsq_next=self.sumsq_next,
