@@ -148,3 +148,31 @@ def test_decoder_kv_layer_slots():
     assert sw is not None and sb is not None and sw[:3] == sb[:3]
     slot, first = sw[0], sw[1]
     assert sorted(slot) == list(range(12)) and slot[first] == 0
+
+
+def test_overflow_guard_range_and_skip_argument():
+    """FusedAdamW's found-inf guard (model.overflow_guard): BERT's encoder + embedding parameters form
+    one contiguous chunk range of the flat layout, its 24 scale slots are the ones the BERT backward
+    writes (one per layer and gradient, [S, 1/S, amax, found-inf]), and guard_skip clips that range to
+    each update's chunk range (relative to its first chunk) or drops it."""
+    from lrce.flat import FlatParams
+    from lrce.models.e2e import E2EOpenEnded
+    from lrce.optim import guard_skip
+
+    slots = torch.zeros(2, 4)
+    assert guard_skip(None, 0, 10) is None
+    assert guard_skip(((5, 9), slots), 0, 20)[1:] == (5, 9)
+    assert guard_skip(((5, 9), slots), 7, 20)[1:] == (0, 2)
+    assert guard_skip(((5, 9), slots), 0, 6)[1:] == (5, 6)
+    assert guard_skip(((5, 9), slots), 9, 20) is None and guard_skip(((5, 9), slots), 0, 5) is None
+    torch.manual_seed(0)
+    m = E2EOpenEnded(768, 10, 0.0, (7, 7), 1024, 5, [3], 32, swin_ckpt=None, bert_dir=None)
+    flat = FlatParams(m, "cpu", order=m.lrce_param_order())
+    params, sc = m.overflow_guard("cpu")
+    assert sc.shape == (12, 2, 4) and sc is m.text_extractor.bert._grad_scales(torch.device("cpu"))
+    c0, c1 = flat.chunk_range(params)                 # contiguous, or chunk_range raises
+    bert = m.text_extractor.bert
+    ids = {id(p) for p in params}
+    assert all(id(p) in ids for p in list(bert.encoder.parameters()) + list(bert.embeddings.parameters()))
+    assert not any(id(p) in ids for p in bert.pooler.parameters())
+    assert c1 - c0 == sum(-(-p.numel() // 1024) for p in params)

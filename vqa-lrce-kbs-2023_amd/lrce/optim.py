@@ -15,6 +15,17 @@ from . import kernels as K
 from .runtime import aux_stream, flat_of, ensure
 
 
+def guard_skip(guard, c0, c1):
+    """The found-inf skip argument of an update over chunks [c0, c1): guard = ((s0, s1), slots) — the
+    guarded chunk range and its scale slots — or None.  Returns (slots, first, end) relative to c0 for
+    the part of [s0, s1) inside [c0, c1), or None when they do not meet."""
+    if guard is None:
+        return None
+    (s0, s1), slots = guard
+    lo, hi = max(s0, c0), min(s1, c1)
+    return (slots, lo - c0, hi - c0) if lo < hi else None
+
+
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, model, groups, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, reg_strength=0.0):
         """groups: list of iterables of parameters (e.g. [fusion.parameters(), text..., video...]) or of
@@ -91,11 +102,7 @@ class FusedAdamW(torch.optim.Optimizer):
         e0, e1 = c0 * 1024, c1 * 1024
         hyper = (b1, b2, self.defaults["eps"], self.defaults["weight_decay"], float(grad_scale), self.reg_strength,
                  1.0 - b1 ** t, 1.0 - b2 ** t)
-        skip = None
-        if self._guard is not None:
-            (s0, s1), slots = self._guard
-            if max(s0, c0) < min(s1, c1):
-                skip = (slots, max(s0, c0) - c0, min(s1, c1) - c0)
+        skip = guard_skip(self._guard, c0, c1)
         if c1 > c0:
             K.adamw_step(flat.f32[e0:e1], flat.grad[e0:e1] if g16 is None else None, self.exp_avg[e0:e1],
                          self.exp_avg_sq[e0:e1], flat.chunk_tensor[c0:c1], self.tensor_lr, self.sumsq, flat.bf16[e0:e1],
