@@ -690,27 +690,11 @@ __device__ void ln_rows_fwd(FfL& L, int nr, const float* g, const float* be, flo
 }
 
 // --------------------------------------------------------------------------- forward: FFN slice j
-#define PIN4(u) asm volatile("" : "+v"((u).x), "+v"((u).y), "+v"((u).z), "+v"((u).w))
-// wait: the row-arrival counter to wait for after the weight loads are issued (NULL: none); false =
-// the launch is aborting
-__device__ __forceinline__ float4 h4f(uint2 u) {   // four fp16 -> f32
-  return make_float4((float)__builtin_bit_cast(f16, (unsigned short)(u.x & 0xFFFFu)), (float)__builtin_bit_cast(f16, (unsigned short)(u.x >> 16)),
-                     (float)__builtin_bit_cast(f16, (unsigned short)(u.y & 0xFFFFu)), (float)__builtin_bit_cast(f16, (unsigned short)(u.y >> 16)));
-}
-#define PIN2(u) asm volatile("" : "+v"((u).x), "+v"((u).y))
-// MFMA f32 16x16x4 on four consecutive k (the skinny GEMMs' form): A(i = lane & 15, k0 + 4 (lane >> 4) + e),
-// B(k0 + 4 (lane >> 4) + e, j = lane & 15), e = 0..3; C row 4 (lane >> 4) + r, column lane & 15
-__device__ __forceinline__ f32x4 mfma4(float4 a, float4 b, f32x4 c) {
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
-}
-
-// The same 16 k as an f32 x fp16 product on the f16 MFMA: a split into hi = f16(a) and lo = f16(a - hi)
+// 16 k of an f32 x fp16 product on the f16 MFMA: a split into hi = f16(a) and lo = f16(a - hi)
 // (a = hi + lo to ~22 bits: the products of fp16 weights with either part are exact in f32), two
 // v_mfma_f32_16x16x16_f16 (K = 16, 8 passes each) in place of four f32 16x16x4 (32 passes each) and
-// the weight conversions.  b: four fp16 of B(k0 + 4 (lane >> 4) + e, j).  For operands of order one
+// the weight conversions.  A(i = lane & 15, k0 + 4 (lane >> 4) + e), C row 4 (lane >> 4) + r, column
+// lane & 15.  b: four fp16 of B(k0 + 4 (lane >> 4) + e, j).  For operands of order one
 // (LayerNorm outputs, GELU activations): no scaling needed for the f16 range.
 typedef __attribute__((ext_vector_type(4))) _Float16 f16x4v;
 __device__ __forceinline__ f32x4 mfma_sp(float4 a, uint2 b, f32x4 c) {
