@@ -463,7 +463,7 @@ def main():
 
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 RIDGE = MFMA_BF16_PEAK_TFLOPS * 1000.0 / HBM_PEAK_GBS   # 312.5 flop/B
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r5_pmc_wattn_qkv_fwd.json")   # tools/pmc_traffic.py output
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r6_pmc_wattn_qkv_fwd.json")   # tools/pmc_traffic.py output
 
 
 def _pmc_traffic():
