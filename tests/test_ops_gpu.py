@@ -904,6 +904,16 @@ def test_patch_im2col_matches_conv():
     p2 = torch.empty_like(patches)
     k.patch_im2col(O.normalize_clip(clips.cpu()).to(dev).flatten(0, 1).transpose(1, 2).contiguous(), p2, layout='BCTHW', normalize=False)
     assert rel(p2, patches) < 1e-2
+    # exact: the same f32 normalisation ((x - mean) * (1 / std), f32 constants) rounded to bf16, zero
+    # padded frame, column c*32 + kt*16 + kh*4 + kw of token (clip, d, h, w)
+    one = torch.tensor(1.0, device=dev)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=dev).view(1, 3, 1, 1, 1)
+    istd = (one / torch.tensor([0.229, 0.224, 0.225], device=dev)).view(1, 3, 1, 1, 1)
+    x = ((clips.flatten(0, 1).transpose(1, 2) - mean) * istd).to(torch.bfloat16)          # (n, 3, T, H, W)
+    x = F.pad(x, (0, 0, 0, 0, 0, T % 2))
+    n = B * S
+    ref = x.view(n, 3, Dp, 2, H // 4, 4, W // 4, 4).permute(0, 2, 4, 6, 1, 3, 5, 7).reshape(-1, 96)
+    assert torch.equal(patches, ref)
     wconv = torch.randn(128, 3, 2, 4, 4, device=dev)
     x = O.normalize_clip(clips.cpu()).to(dev).flatten(0, 1).transpose(1, 2)
     x = F.pad(x, (0, 0, 0, 0, 0, T % 2))
