@@ -1,6 +1,8 @@
 #!/usr/bin/env python
-"""Patch im2col microbenchmark (dev tool, GPU): lrce_patch_im2col at the bs-10 step's shape (30 clips of
-5 frames, 224^2, normalised), HIP-event timed; bytes = the f32 clips read + the bf16 patches written."""
+"""Elementwise microbenchmarks (dev tool, GPU), HIP-event timed: lrce_patch_im2col at the bs-10 step's
+shape (30 clips of 5 frames, 224^2, normalised; bytes = the f32 clips read + the bf16 patches written)
+and lrce_scale_cast_bf16 at the Swin stage shapes with per-clip row scales (the DropPath-scaled bf16
+copy of a block's output gradient)."""
 import os
 import sys
 
@@ -30,6 +32,21 @@ def main():
     ms = e0.elapsed_time(e1) / it
     gb = (clips.numel() * 4 + patches.numel() * 2) / 1e9
     print(f"patch_im2col {ntok} tokens: {ms * 1e3:.1f} us  {gb / ms:.2f} TB/s")
+    for rows, cols in ((282240, 128), (70560, 256), (15680, 512), (3920, 1024)):
+        x = torch.randn(rows, cols, device=dev)
+        sc = torch.rand(30, device=dev)
+        y = torch.empty(rows, cols, device=dev, dtype=torch.bfloat16)
+        f = lambda: K.scale_cast_bf16(x, sc, rows // 30, out=y)   # noqa: E731
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(it):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / it
+        print(f"scale_cast_bf16 {rows}x{cols}: {ms * 1e3:.1f} us  {rows * cols * 6 / 1e9 / ms:.2f} TB/s")
 
 
 if __name__ == "__main__":
